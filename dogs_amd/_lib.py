@@ -1,0 +1,140 @@
+"""ctypes binding of libdogs_hip.so (include/dogs_hip.h).
+
+This is the only way the Python layer reaches the GPU kernels.  There is no CPU fallback: if the
+library is missing or a tensor is not on a HIP device, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libdogs_hip.so")
+
+_f32p = C.POINTER(C.c_float)
+
+
+class DgRasterArgs(C.Structure):
+    _fields_ = [
+        ("P", C.c_int), ("D", C.c_int), ("M", C.c_int), ("W", C.c_int), ("H", C.c_int),
+        ("prefiltered", C.c_int), ("antialiasing", C.c_int), ("debug", C.c_int),
+        ("scale_modifier", C.c_float), ("tanfovx", C.c_float), ("tanfovy", C.c_float),
+        ("bg", C.c_void_p), ("means3D", C.c_void_p), ("colors", C.c_void_p), ("opacities", C.c_void_p),
+        ("scales", C.c_void_p), ("rotations", C.c_void_p), ("cov3D_precomp", C.c_void_p),
+        ("viewmatrix", C.c_void_p), ("projmatrix", C.c_void_p), ("dc", C.c_void_p), ("sh", C.c_void_p),
+        ("campos", C.c_void_p),
+    ]
+
+
+ALLOC_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int, C.c_uint64)
+DG_BUF_GEOM, DG_BUF_BINNING, DG_BUF_IMAGE, DG_BUF_BACKWARD, DG_BUF_TEMP = range(5)
+
+EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_mark_visible", "dg_rasterize_filter",
+           "dg_adam_update", "dg_fused_ssim_forward", "dg_fused_ssim_backward", "dg_dist_cuda2",
+           "dg_geom_bytes", "dg_image_bytes", "dg_binning_bytes", "dg_debug_sorted_instances",
+           "dg_debug_geometry", "dg_debug_image_state", "dg_sort_pairs_u32", "dg_exclusive_scan_u32",
+           "dg_last_error", "dg_version")
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str | None = None):
+    """Load (once) and type the library.  Raises ImportError when it is not built."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise ImportError(f"libdogs_hip.so not found at {p}: build it with "
+                              "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+        L = C.CDLL(p)
+        vp, i64p = C.c_void_p, C.POINTER(C.c_int64)
+        L.dg_rasterize_forward.restype = C.c_int
+        L.dg_rasterize_forward.argtypes = [C.POINTER(DgRasterArgs), vp, vp, vp, ALLOC_FN, vp,
+                                           C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), i64p, i64p, vp]
+        L.dg_rasterize_backward.restype = C.c_int
+        L.dg_rasterize_backward.argtypes = [C.POINTER(DgRasterArgs), vp, vp, vp, vp, C.c_int64, C.c_int64, vp, vp,
+                                            vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, ALLOC_FN, vp, vp]
+        L.dg_mark_visible.restype = C.c_int
+        L.dg_mark_visible.argtypes = [C.c_int, vp, vp, vp, vp, vp]
+        L.dg_rasterize_filter.restype = C.c_int
+        L.dg_rasterize_filter.argtypes = [C.POINTER(DgRasterArgs), vp, vp]
+        L.dg_adam_update.restype = C.c_int
+        L.dg_adam_update.argtypes = [vp, vp, vp, vp, vp, C.c_float, C.c_float, C.c_float, C.c_float,
+                                     C.c_uint32, C.c_uint32, vp]
+        L.dg_fused_ssim_forward.restype = C.c_int
+        L.dg_fused_ssim_forward.argtypes = [C.c_int] * 4 + [C.c_float, C.c_float] + [vp] * 6 + [vp]
+        L.dg_fused_ssim_backward.restype = C.c_int
+        L.dg_fused_ssim_backward.argtypes = [C.c_int] * 4 + [C.c_float, C.c_float] + [vp] * 7 + [vp]
+        L.dg_dist_cuda2.restype = C.c_int
+        L.dg_dist_cuda2.argtypes = [C.c_int, vp, vp, ALLOC_FN, vp, vp]
+        L.dg_geom_bytes.restype = C.c_uint64
+        L.dg_geom_bytes.argtypes = [C.c_int]
+        L.dg_image_bytes.restype = C.c_uint64
+        L.dg_image_bytes.argtypes = [C.c_int, C.c_int]
+        L.dg_binning_bytes.restype = C.c_uint64
+        L.dg_binning_bytes.argtypes = [C.c_int64, C.c_int, C.c_int]
+        L.dg_debug_sorted_instances.restype = C.c_int
+        L.dg_debug_sorted_instances.argtypes = [vp, C.c_int64, C.c_int, C.c_int, vp, vp, vp]
+        L.dg_debug_geometry.restype = C.c_int
+        L.dg_debug_geometry.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp]
+        L.dg_debug_image_state.restype = C.c_int
+        L.dg_debug_image_state.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]
+        L.dg_sort_pairs_u32.restype = C.c_int
+        L.dg_sort_pairs_u32.argtypes = [vp, vp, C.c_uint32, C.c_int, C.c_int, ALLOC_FN, vp, vp]
+        L.dg_exclusive_scan_u32.restype = C.c_int
+        L.dg_exclusive_scan_u32.argtypes = [vp, vp, C.c_uint32, vp, ALLOC_FN, vp, vp]
+        L.dg_last_error.restype = C.c_char_p
+        L.dg_last_error.argtypes = []
+        L.dg_version.restype = C.c_int
+        if path is None:
+            _lib = L
+        return L
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = load().dg_last_error()
+        raise RuntimeError(msg.decode() if msg else "libdogs_hip call failed")
+
+
+def ptr(t: torch.Tensor | None):
+    """Device pointer of a tensor; None/empty -> NULL (the reference's 'empty tensor = absent')."""
+    if t is None or t.numel() == 0:
+        return None
+    return t.data_ptr()
+
+
+def require_device(t: torch.Tensor, name: str) -> None:
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be a HIP (cuda) tensor: libdogs_hip has no CPU path")
+
+
+def stream_of(device: torch.device):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class TensorArena:
+    """dg_alloc_fn backed by the torch caching allocator; keeps the uint8 tensors per buffer kind."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.buffers: dict[int, torch.Tensor] = {}
+
+        def _alloc(user, which, nbytes):  # noqa: ARG001
+            try:
+                t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self.device)
+            except Exception:  # noqa: BLE001 - reported to C as NULL, surfaces as RuntimeError
+                return None
+            self.buffers[int(which)] = t
+            return t.data_ptr()
+
+        self.fn = ALLOC_FN(_alloc)
+
+    def get(self, which: int) -> torch.Tensor:
+        return self.buffers.get(which, torch.empty(0, dtype=torch.uint8, device=self.device))

@@ -1,0 +1,16 @@
+// aux_kernels.h -- launchers of fused SSIM, sparse Adam and simple-knn (aux_kernels.hip)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace gs {
+void launch_ssim_fwd(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2, float* map,
+                     float* dmu1, float* ds1, float* ds12, hipStream_t s);
+void launch_ssim_bwd(int B, int CH, int H, int W, const float* img1, const float* img2, const float* dL,
+                     const float* dmu1, const float* ds1, const float* ds12, float* dimg1, hipStream_t s);
+void launch_adam(float* param, const float* grad, float* m, float* v, const bool* visible, float lr, float b1, float b2,
+                 float eps, uint32_t N, uint32_t M, hipStream_t s);
+size_t knn_temp_bytes(int P);
+void launch_knn(int P, const float* pts, float* out, void* temp, hipStream_t s);
+}  // namespace gs

@@ -1,0 +1,337 @@
+// aux_kernels.hip -- the satellite kernels that ship in the same extension as the rasterizer:
+//   fused SSIM forward/backward  (fused-ssim/ssim.cu:187-366 semantics)
+//   sparse Adam                  (cuda_rasterizer/adam.cu:10-38)
+//   simple-knn distCUDA2         (simple-knn/simple_knn.cu:45-221)
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <stdint.h>
+#include "aux_kernels.h"
+#include "sortscan.h"
+
+namespace gs {
+
+// ------------------------------------------------------------------------------------------------
+// fused SSIM.  One 256-thread workgroup per 32x32 tile of one (batch, channel) plane.  The reference
+// runs five separable convolutions back to back through one scratch buffer (15 barriers per channel);
+// here the x-pass of all five moments is done in one sweep over the 42x42 halo tile and the y-pass
+// reads them from LDS.  Accumulation order per moment is the reference's (tap 0..10, x then y).
+// ------------------------------------------------------------------------------------------------
+__constant__ float c_gw[11] = {0.001028380123898387f, 0.0075987582094967365f, 0.036000773310661316f,
+                               0.10936068743467331f, 0.21300552785396576f, 0.26601171493530273f,
+                               0.21300552785396576f, 0.10936068743467331f, 0.036000773310661316f,
+                               0.0075987582094967365f, 0.001028380123898387f};
+constexpr int SB = 32, SH = SB + 10;
+
+__device__ __forceinline__ float pix_at(const float* img, int y, int x, int H, int W) {
+    return (x >= W || y >= H || x < 0 || y < 0) ? 0.0f : img[(size_t)y * W + x];
+}
+
+template <bool TRAIN>
+__global__ void __launch_bounds__(256) k_ssim_fwd(int H, int W, float C1, float C2, const float* __restrict__ img1,
+                                                  const float* __restrict__ img2, float* __restrict__ map,
+                                                  float* __restrict__ dmu1, float* __restrict__ ds1,
+                                                  float* __restrict__ ds12) {
+    __shared__ float s1[SH][SH + 1];
+    __shared__ float s2[SH][SH + 1];
+    __shared__ float hx[5][SH][SB + 1];
+    const size_t plane = (size_t)blockIdx.z * H * W;
+    const float* a = img1 + plane;
+    const float* b = img2 + plane;
+    const int y0 = blockIdx.y * SB - 5, x0 = blockIdx.x * SB - 5;
+    for (int i = threadIdx.x; i < SH * SH; i += 256) {
+        const int ly = i / SH, lx = i % SH;
+        s1[ly][lx] = pix_at(a, y0 + ly, x0 + lx, H, W);
+        s2[ly][lx] = pix_at(b, y0 + ly, x0 + lx, H, W);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < SH * SB; i += 256) {
+        const int ly = i / SB, lx = i % SB;
+        float m1 = 0, m2 = 0, q1 = 0, q2 = 0, q12 = 0;
+#pragma unroll
+        for (int k = 0; k < 11; k++) {
+            const float g = c_gw[k];
+            const float u = s1[ly][lx + k], v = s2[ly][lx + k];
+            m1 = fmaf(g, u, m1);
+            q1 = fmaf(g, u * u, q1);
+            m2 = fmaf(g, v, m2);
+            q2 = fmaf(g, v * v, q2);
+            q12 = fmaf(g, u * v, q12);
+        }
+        hx[0][ly][lx] = m1; hx[1][ly][lx] = q1; hx[2][ly][lx] = m2; hx[3][ly][lx] = q2; hx[4][ly][lx] = q12;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < SB * SB; i += 256) {
+        const int ly = i / SB, lx = i % SB;
+        const int y = blockIdx.y * SB + ly, x = blockIdx.x * SB + lx;
+        float v[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 11; k++) {
+            const float g = c_gw[k];
+#pragma unroll
+            for (int q = 0; q < 5; q++) v[q] = fmaf(g, hx[q][ly + k][lx], v[q]);
+        }
+        const float mu1 = v[0], mu2 = v[2];
+        const float sigma1_sq = fmaf(-mu1, mu1, v[1]);
+        const float sigma2_sq = fmaf(-mu2, mu2, v[3]);
+        const float sigma12 = fmaf(-mu1, mu2, v[4]);
+        const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu1_mu2 = mu1 * mu2;
+        const float Cc = fmaf(2.0f, mu1_mu2, C1);
+        const float D = fmaf(2.0f, sigma12, C2);
+        const float A = (mu1_sq + mu2_sq) + C1;
+        const float B = (sigma1_sq + sigma2_sq) + C2;
+        if (x < W && y < H) {
+            const size_t gi = plane + (size_t)y * W + x;
+            map[gi] = (Cc * D) / (A * B);
+            if (TRAIN) {
+                dmu1[gi] = ((mu2 * 2.0f * D) / (A * B) - (mu2 * 2.0f * Cc) / (A * B) - (mu1 * 2.0f * Cc * D) / (A * A * B) +
+                            (mu1 * 2.0f * Cc * D) / (A * B * B));
+                ds1[gi] = ((-Cc * D) / (A * B * B));
+                ds12[gi] = ((2 * Cc) / (A * B));
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ssim_bwd(int H, int W, const float* __restrict__ img1,
+                                                  const float* __restrict__ img2, const float* __restrict__ dL,
+                                                  const float* __restrict__ dmu1, const float* __restrict__ ds1,
+                                                  const float* __restrict__ ds12, float* __restrict__ dimg1) {
+    __shared__ float s[3][SH][SH + 1];
+    __shared__ float hx[3][SH][SB + 1];
+    const size_t plane = (size_t)blockIdx.z * H * W;
+    const int y0 = blockIdx.y * SB - 5, x0 = blockIdx.x * SB - 5;
+    for (int i = threadIdx.x; i < SH * SH; i += 256) {
+        const int ly = i / SH, lx = i % SH;
+        const int y = y0 + ly, x = x0 + lx;
+        const float l = pix_at(dL + plane, y, x, H, W);
+        s[0][ly][lx] = pix_at(dmu1 + plane, y, x, H, W) * l;
+        s[1][ly][lx] = pix_at(ds1 + plane, y, x, H, W) * l;
+        s[2][ly][lx] = pix_at(ds12 + plane, y, x, H, W) * l;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < SH * SB; i += 256) {
+        const int ly = i / SB, lx = i % SB;
+        float h0 = 0, h1 = 0, h2 = 0;
+#pragma unroll
+        for (int k = 0; k < 11; k++) {
+            const float g = c_gw[k];
+            h0 = fmaf(g, s[0][ly][lx + k], h0);
+            h1 = fmaf(g, s[1][ly][lx + k], h1);
+            h2 = fmaf(g, s[2][ly][lx + k], h2);
+        }
+        hx[0][ly][lx] = h0; hx[1][ly][lx] = h1; hx[2][ly][lx] = h2;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < SB * SB; i += 256) {
+        const int ly = i / SB, lx = i % SB;
+        const int y = blockIdx.y * SB + ly, x = blockIdx.x * SB + lx;
+        if (x >= W || y >= H) continue;
+        float v0 = 0, v1 = 0, v2 = 0;
+#pragma unroll
+        for (int k = 0; k < 11; k++) {
+            const float g = c_gw[k];
+            v0 = fmaf(g, hx[0][ly + k][lx], v0);
+            v1 = fmaf(g, hx[1][ly + k][lx], v1);
+            v2 = fmaf(g, hx[2][ly + k][lx], v2);
+        }
+        const size_t gi = plane + (size_t)y * W + x;
+        float d = v0;
+        d += (img1[gi] * 2.0f) * v1;
+        d += img2[gi] * v2;
+        dimg1[gi] = d;
+    }
+}
+
+void launch_ssim_fwd(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2, float* map,
+                     float* dmu1, float* ds1, float* ds12, hipStream_t s) {
+    if ((size_t)B * CH * H * W == 0) return;
+    dim3 grid((W + SB - 1) / SB, (H + SB - 1) / SB, B * CH);
+    if (dmu1)
+        k_ssim_fwd<true><<<grid, 256, 0, s>>>(H, W, C1, C2, img1, img2, map, dmu1, ds1, ds12);
+    else
+        k_ssim_fwd<false><<<grid, 256, 0, s>>>(H, W, C1, C2, img1, img2, map, nullptr, nullptr, nullptr);
+}
+void launch_ssim_bwd(int B, int CH, int H, int W, const float* img1, const float* img2, const float* dL,
+                     const float* dmu1, const float* ds1, const float* ds12, float* dimg1, hipStream_t s) {
+    if ((size_t)B * CH * H * W == 0) return;
+    dim3 grid((W + SB - 1) / SB, (H + SB - 1) / SB, B * CH);
+    k_ssim_bwd<<<grid, 256, 0, s>>>(H, W, img1, img2, dL, dmu1, ds1, ds12, dimg1);
+}
+
+// ------------------------------------------------------------------------------------------------
+// sparse Adam (adam.cu:10-38): visible Gaussians only, no bias correction.  Grid-stride, one element
+// per lane per step; N*M is up to 45*5e6 so 64-bit indices.
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_adam(float* __restrict__ param, const float* __restrict__ grad,
+                                              float* __restrict__ m, float* __restrict__ v,
+                                              const bool* __restrict__ visible, float lr, float b1, float b2,
+                                              float eps, uint64_t total, uint32_t M) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (!visible[i / M]) continue;
+        const float gr = grad[i];
+        const float em = fmaf(b1, m[i], (1.0f - b1) * gr);
+        const float ev = fmaf(b2, v[i], ((1.0f - b2) * gr) * gr);
+        const float step = -lr * em / (sqrtf(ev) + eps);
+        param[i] += step;
+        m[i] = em;
+        v[i] = ev;
+    }
+}
+
+void launch_adam(float* param, const float* grad, float* m, float* v, const bool* visible, float lr, float b1, float b2,
+                 float eps, uint32_t N, uint32_t M, hipStream_t s) {
+    const uint64_t total = (uint64_t)N * M;
+    if (total == 0 || M == 0) return;
+    uint64_t blocks = (total + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    k_adam<<<(unsigned)blocks, 256, 0, s>>>(param, grad, m, v, visible, lr, b1, b2, eps, total, M);
+}
+
+// ------------------------------------------------------------------------------------------------
+// simple-knn
+// ------------------------------------------------------------------------------------------------
+constexpr int KNN_BOX = 1024;
+
+// bbox with the reference's {0,0,0} reduction init (simple_knn.cu:191)
+__global__ void __launch_bounds__(1024) k_knn_bbox(int P, const float* __restrict__ pts, float* __restrict__ bb) {
+    __shared__ float s[6][16];
+    float mn[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
+    for (int i = threadIdx.x; i < P; i += 1024)
+        for (int k = 0; k < 3; k++) {
+            const float v = pts[3 * i + k];
+            mn[k] = fminf(mn[k], v);
+            mx[k] = fmaxf(mx[k], v);
+        }
+    for (int o = 32; o > 0; o >>= 1)
+        for (int k = 0; k < 3; k++) {
+            mn[k] = fminf(mn[k], __shfl_xor(mn[k], o));
+            mx[k] = fmaxf(mx[k], __shfl_xor(mx[k], o));
+        }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 3; k++) { s[k][w] = mn[k]; s[3 + k][w] = mx[k]; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const int k = threadIdx.x;
+        float a = s[k][0], b = s[3 + k][0];
+        for (int j = 1; j < 16; j++) { a = fminf(a, s[k][j]); b = fmaxf(b, s[3 + k][j]); }
+        bb[k] = a;
+        bb[3 + k] = b;
+    }
+}
+
+__device__ __forceinline__ uint32_t prep_morton(uint32_t x) {
+    x = (x | (x << 16)) & 0x030000FF;
+    x = (x | (x << 8)) & 0x0300F00F;
+    x = (x | (x << 4)) & 0x030C30C3;
+    x = (x | (x << 2)) & 0x09249249;
+    return x;
+}
+__device__ __forceinline__ uint32_t sat_f2u(float f) {
+    if (!(f > 0.0f)) return 0u;
+    if (f >= 4294967296.0f) return 0xffffffffu;
+    return (uint32_t)f;
+}
+
+__global__ void __launch_bounds__(256) k_knn_morton(int P, const float* __restrict__ pts, const float* __restrict__ bb,
+                                                    uint32_t* __restrict__ codes) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    uint32_t c[3];
+    for (int k = 0; k < 3; k++) c[k] = prep_morton(sat_f2u(((pts[3 * i + k] - bb[k]) / (bb[3 + k] - bb[k])) * 1023.0f));
+    codes[i] = c[0] | (c[1] << 1) | (c[2] << 2);
+}
+
+__global__ void __launch_bounds__(256) k_knn_boxes(int P, const float* __restrict__ pts, const uint32_t* __restrict__ order,
+                                                   float* __restrict__ boxes) {
+    __shared__ float s[6][4];
+    const int b = blockIdx.x;
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (int i = b * KNN_BOX + threadIdx.x; i < P && i < (b + 1) * KNN_BOX; i += 256) {
+        const uint32_t g = order[i];
+        for (int k = 0; k < 3; k++) {
+            const float v = pts[3 * g + k];
+            mn[k] = fminf(mn[k], v);
+            mx[k] = fmaxf(mx[k], v);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1)
+        for (int k = 0; k < 3; k++) {
+            mn[k] = fminf(mn[k], __shfl_xor(mn[k], o));
+            mx[k] = fmaxf(mx[k], __shfl_xor(mx[k], o));
+        }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 3; k++) { s[k][w] = mn[k]; s[3 + k][w] = mx[k]; }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int k = threadIdx.x;
+        float r = s[k][0];
+        for (int j = 1; j < 4; j++) r = k < 3 ? fminf(r, s[k][j]) : fmaxf(r, s[k][j]);
+        boxes[6 * b + k] = r;
+    }
+}
+
+__device__ __forceinline__ void upd3(float rx, float ry, float rz, const float* pt, float* best) {
+    const float dx = pt[0] - rx, dy = pt[1] - ry, dz = pt[2] - rz;
+    float dist = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+        if (best[j] > dist) { const float t = best[j]; best[j] = dist; dist = t; }
+}
+
+__global__ void __launch_bounds__(256) k_knn_dist(int P, const float* __restrict__ pts, const uint32_t* __restrict__ order,
+                                                  const float* __restrict__ boxes, float* __restrict__ out) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    const uint32_t me = order[idx];
+    const float px = pts[3 * me], py = pts[3 * me + 1], pz = pts[3 * me + 2];
+    float best[3] = {FLT_MAX, FLT_MAX, FLT_MAX};
+    const int lo = idx - 3 > 0 ? idx - 3 : 0, hi = idx + 3 < P - 1 ? idx + 3 : P - 1;
+    for (int i = lo; i <= hi; i++)
+        if (i != idx) upd3(px, py, pz, pts + 3 * order[i], best);
+    const float reject = best[2];
+    best[0] = best[1] = best[2] = FLT_MAX;
+    const int nb = (P + KNN_BOX - 1) / KNN_BOX;
+    for (int b = 0; b < nb; b++) {
+        const float* bx = boxes + 6 * b;
+        float d[3] = {0, 0, 0};
+        const float p3[3] = {px, py, pz};
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+            if (p3[k] < bx[k] || p3[k] > bx[3 + k]) d[k] = fminf(fabsf(p3[k] - bx[k]), fabsf(p3[k] - bx[3 + k]));
+        const float dist = fmaf(d[2], d[2], fmaf(d[1], d[1], d[0] * d[0]));
+        if (dist > reject || dist > best[2]) continue;
+        const int e = (b + 1) * KNN_BOX < P ? (b + 1) * KNN_BOX : P;
+        for (int i = b * KNN_BOX; i < e; i++)
+            if (i != idx) upd3(px, py, pz, pts + 3 * order[i], best);
+    }
+    out[me] = (best[0] + best[1] + best[2]) / 3.0f;
+}
+
+size_t knn_temp_bytes(int P) {
+    const size_t n = (size_t)(P > 0 ? P : 1);
+    const size_t nb = (n + KNN_BOX - 1) / KNN_BOX;
+    return 256 + 4 * n * 4 + nb * 6 * 4 + radix_sort_temp_bytes((uint32_t)n) + 1024;
+}
+
+void launch_knn(int P, const float* pts, float* out, void* temp, hipStream_t s) {
+    if (P <= 0) return;
+    char* t = (char*)temp;
+    float* bb = (float*)t; t += 256;
+    uint32_t* k0 = (uint32_t*)t; t += 4 * (size_t)P;
+    uint32_t* v0 = (uint32_t*)t; t += 4 * (size_t)P;
+    uint32_t* k1 = (uint32_t*)t; t += 4 * (size_t)P;
+    uint32_t* v1 = (uint32_t*)t; t += 4 * (size_t)P;
+    const int nb = (P + KNN_BOX - 1) / KNN_BOX;
+    float* boxes = (float*)t; t += (size_t)nb * 6 * 4;
+    t = (char*)(((uintptr_t)t + 255) & ~(uintptr_t)255);
+    k_knn_bbox<<<1, 1024, 0, s>>>(P, pts, bb);
+    k_knn_morton<<<(P + 255) / 256, 256, 0, s>>>(P, pts, bb, k0);
+    const int which = radix_sort_pairs(k0, v0, k1, v1, nullptr, (uint32_t)P, 0, 32, t, s);
+    const uint32_t* order = which ? v1 : v0;
+    k_knn_boxes<<<nb, 256, 0, s>>>(P, pts, order, boxes);
+    k_knn_dist<<<(P + 255) / 256, 256, 0, s>>>(P, pts, order, boxes, out);
+}
+
+}  // namespace gs

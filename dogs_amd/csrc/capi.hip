@@ -1,0 +1,461 @@
+// capi.hip -- extern "C" entry points of libdogs_hip.so (declared in include/dogs_hip.h).
+//
+// Owns the host-side orchestration of Rasterizer::forward/backward (rasterizer_impl.cu:334-676):
+// carving of the private state blocks, the single host sync (instance count), launch order.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <string>
+
+#include "../../include/dogs_hip.h"
+#include "aux_kernels.h"
+#include "raster.h"
+#include "sortscan.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const char* fmt, const char* a = "", int b = 0) {
+    char buf[512];
+    snprintf(buf, sizeof(buf), fmt, a, b);
+    g_err = buf;
+    return 1;
+}
+
+#define HIP_OK(x)                                                                \
+    do {                                                                         \
+        hipError_t _e = (x);                                                     \
+        if (_e != hipSuccess) return fail("HIP error: %s (line %d)", hipGetErrorString(_e), __LINE__); \
+    } while (0)
+
+#define DBG_SYNC(dbg, s)                                                         \
+    do {                                                                         \
+        if (dbg) {                                                               \
+            HIP_OK(hipStreamSynchronize(s));                                     \
+            HIP_OK(hipGetLastError());                                           \
+        }                                                                        \
+    } while (0)
+
+constexpr size_t ALIGN = 256;
+inline size_t al(size_t x) { return (x + ALIGN - 1) & ~(ALIGN - 1); }
+
+struct Carver {
+    char* base;
+    size_t off = 0;
+    explicit Carver(void* b) : base((char*)b) {}
+    template <typename T>
+    T* take(size_t count) {
+        T* p = base ? (T*)(base + off) : nullptr;
+        off += al(count * sizeof(T) + (count == 0 ? 1 : 0));
+        return p;
+    }
+};
+
+inline int tiles_x_of(int W) { return (W + 15) / 16; }
+inline int tiles_y_of(int H) { return (H + 15) / 16; }
+inline int bits_for(uint32_t n) {  // bits needed for ids in [0, n)
+    int b = 1;
+    while ((1u << b) < n && b < 32) b++;
+    return b;
+}
+
+struct Geom {
+    uint32_t* counters;  // [0] K total, [1] err, [2..3] u64 rect sum
+    float2* xy;
+    float4* co;
+    float4* rgbi;
+    uint32_t *k0, *v0, *k1, *v1, *cnt, *first_e, *off;
+    void* sort_tmp;
+    void* scan_tmp;
+    size_t bytes;
+};
+Geom carve_geom(void* base, int P) {
+    Carver c(base);
+    Geom g;
+    const size_t n = (size_t)(P > 0 ? P : 1);
+    g.counters = c.take<uint32_t>(16);
+    g.xy = c.take<float2>(n);
+    g.co = c.take<float4>(n);
+    g.rgbi = c.take<float4>(n);
+    g.k0 = c.take<uint32_t>(n);
+    g.v0 = c.take<uint32_t>(n);
+    g.k1 = c.take<uint32_t>(n);
+    g.v1 = c.take<uint32_t>(n);
+    g.cnt = c.take<uint32_t>(n);
+    g.first_e = c.take<uint32_t>(n);
+    g.off = c.take<uint32_t>(n);
+    g.sort_tmp = c.take<char>(gs::radix_sort_temp_bytes((uint32_t)n));
+    g.scan_tmp = c.take<char>(gs::scan_temp_bytes((uint32_t)n));
+    g.bytes = c.off;
+    return g;
+}
+
+struct Image {
+    float *final_T, *img_color, *img_invd;
+    uint32_t *n_contrib, *max_contrib;
+    uint2* ranges;
+    size_t bytes;
+};
+Image carve_image(void* base, int W, int H) {
+    Carver c(base);
+    Image im;
+    const size_t HW = (size_t)W * H > 0 ? (size_t)W * H : 1;
+    const size_t T = (size_t)tiles_x_of(W) * tiles_y_of(H) > 0 ? (size_t)tiles_x_of(W) * tiles_y_of(H) : 1;
+    im.final_T = c.take<float>(HW);
+    im.n_contrib = c.take<uint32_t>(HW);
+    im.img_color = c.take<float>(3 * HW);
+    im.img_invd = c.take<float>(HW);
+    im.ranges = c.take<uint2>(T);
+    im.max_contrib = c.take<uint32_t>(T);
+    im.bytes = c.off;
+    return im;
+}
+
+struct Binning {
+    uint32_t *tk0, *se0, *tk1, *se1, *eg;
+    void* sort_tmp;
+    size_t bytes;
+};
+Binning carve_binning(void* base, int64_t K) {
+    Carver c(base);
+    Binning b;
+    const size_t n = (size_t)(K > 0 ? K : 1);
+    b.tk0 = c.take<uint32_t>(n);
+    b.se0 = c.take<uint32_t>(n);
+    b.tk1 = c.take<uint32_t>(n);
+    b.se1 = c.take<uint32_t>(n);
+    b.eg = c.take<uint32_t>(n);
+    b.sort_tmp = c.take<char>(gs::radix_sort_temp_bytes((uint32_t)n));
+    b.bytes = c.off;
+    return b;
+}
+
+struct BwdScratch {
+    uint8_t* flag;
+    float* rec;
+    size_t bytes;
+};
+BwdScratch carve_bwd(void* base, int64_t K) {
+    Carver c(base);
+    BwdScratch s;
+    const size_t n = (size_t)(K > 0 ? K : 1);
+    s.flag = c.take<uint8_t>(n);
+    s.rec = c.take<float>(12 * n);
+    s.bytes = c.off;
+    return s;
+}
+
+void fill_pre(gs::PreArgs& p, const dg_raster_args* a) {
+    memset(&p, 0, sizeof(p));
+    p.P = a->P; p.D = a->D; p.M = a->M; p.W = a->W; p.H = a->H;
+    p.tiles_x = tiles_x_of(a->W); p.tiles_y = tiles_y_of(a->H);
+    p.antialiasing = a->antialiasing; p.prefiltered = a->prefiltered;
+    p.tanfovx = a->tanfovx; p.tanfovy = a->tanfovy;
+    p.focal_y = a->H / (2.0f * a->tanfovy);
+    p.focal_x = a->W / (2.0f * a->tanfovx);
+    p.scale_mod = a->scale_modifier;
+    p.means3D = a->means3D; p.scales = a->scales; p.rotations = a->rotations; p.opacities = a->opacities;
+    p.dc = a->dc; p.sh = a->sh; p.colors = a->colors; p.cov3D_precomp = a->cov3D_precomp;
+    p.view = a->viewmatrix; p.proj = a->projmatrix; p.campos = a->campos;
+    if (p.sh == nullptr || p.M == 0) { p.sh = nullptr; p.D = 0; }
+}
+
+int check_args(const dg_raster_args* a) {
+    if (!a) return fail("null args%s%d");
+    if (a->P < 0 || a->W <= 0 || a->H <= 0) return fail("bad sizes P/W/H%s (P=%d)", "", a->P);
+    if (a->P > 0 && (!a->means3D || !a->opacities || !a->viewmatrix || !a->projmatrix || !a->bg))
+        return fail("missing required tensor%s%d");
+    if (a->P > 0 && !a->colors && (!a->dc || !a->campos))
+        return fail("SH path needs dc and campos (or provide colors_precomp)%s%d");
+    if (a->P > 0 && !a->cov3D_precomp && (!a->scales || !a->rotations))
+        return fail("need scales+rotations or cov3D_precomp%s%d");
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* dg_last_error(void) { return g_err.c_str(); }
+
+int dg_sort_pairs_u32(uint32_t* keys, uint32_t* vals, uint32_t n, int begin_bit, int end_bit, dg_alloc_fn alloc,
+                      void* user, dg_stream_t stream) {
+    if (n == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    Carver c(nullptr);
+    c.take<uint32_t>(n); c.take<uint32_t>(n);
+    c.take<char>(gs::radix_sort_temp_bytes(n));
+    void* base = alloc(user, DG_BUF_TEMP, c.off);
+    if (!base) return fail("sort scratch allocation failed%s%d");
+    Carver d(base);
+    uint32_t* k1 = d.take<uint32_t>(n);
+    uint32_t* v1 = d.take<uint32_t>(n);
+    void* tmp = d.take<char>(gs::radix_sort_temp_bytes(n));
+    const int which = gs::radix_sort_pairs(keys, vals, k1, v1, vals, n, begin_bit, end_bit, tmp, s);
+    if (which) {
+        HIP_OK(hipMemcpyAsync(keys, k1, 4 * (size_t)n, hipMemcpyDeviceToDevice, s));
+        HIP_OK(hipMemcpyAsync(vals, v1, 4 * (size_t)n, hipMemcpyDeviceToDevice, s));
+    }
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* total, dg_alloc_fn alloc,
+                          void* user, dg_stream_t stream) {
+    void* tmp = alloc(user, DG_BUF_TEMP, gs::scan_temp_bytes(n));
+    if (!tmp) return fail("scan scratch allocation failed%s%d");
+    gs::exclusive_scan(in, nullptr, n, out, total, tmp, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+int dg_version(void) { return 1; }
+
+uint64_t dg_geom_bytes(int P) { return carve_geom(nullptr, P).bytes; }
+uint64_t dg_image_bytes(int W, int H) { return carve_image(nullptr, W, H).bytes; }
+uint64_t dg_binning_bytes(int64_t K, int W, int H) { (void)W; (void)H; return carve_binning(nullptr, K).bytes; }
+
+int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_invdepth, int* radii,
+                         dg_alloc_fn alloc, void* user, void** geom_out, void** binning_out, void** image_out,
+                         int64_t* num_rendered, int64_t* num_instances, dg_stream_t stream_) {
+    if (check_args(a)) return 1;
+    hipStream_t s = (hipStream_t)stream_;
+    const int P = a->P, W = a->W, H = a->H;
+    const int tx = tiles_x_of(W), ty = tiles_y_of(H), T = tx * ty;
+    *num_rendered = 0;
+    *num_instances = 0;
+
+    const size_t gbytes = carve_geom(nullptr, P).bytes;
+    void* gbase = alloc(user, DG_BUF_GEOM, gbytes);
+    if (!gbase) return fail("geometry allocation failed%s%d");
+    Geom g = carve_geom(gbase, P);
+    const size_t ibytes = carve_image(nullptr, W, H).bytes;
+    void* ibase = alloc(user, DG_BUF_IMAGE, ibytes);
+    if (!ibase) return fail("image allocation failed%s%d");
+    Image im = carve_image(ibase, W, H);
+    *geom_out = gbase;
+    *image_out = ibase;
+    *binning_out = nullptr;
+
+    HIP_OK(hipMemsetAsync(g.counters, 0, 64, s));
+    gs::PreArgs pre;
+    fill_pre(pre, a);
+    pre.radii = radii; pre.xy = g.xy; pre.co = g.co; pre.rgbi = g.rgbi; pre.depthkey = g.k0; pre.cnt = g.cnt;
+    pre.rect_sum = (unsigned long long*)(g.counters + 2); pre.err = g.counters + 1;
+    gs::launch_preprocess(pre, s);
+    DBG_SYNC(a->debug, s);
+
+    // stable depth sort of (depth bits, index): 4 passes -> result back in k0/v0
+    const uint32_t* order = g.v0;
+    if (P > 0) {
+        const int which = gs::radix_sort_pairs(g.k0, g.v0, g.k1, g.v1, nullptr, (uint32_t)P, 0, 32, g.sort_tmp, s);
+        order = which ? g.v1 : g.v0;
+        DBG_SYNC(a->debug, s);
+        gs::exclusive_scan(g.cnt, order, (uint32_t)P, g.off, g.counters, g.scan_tmp, s);
+        DBG_SYNC(a->debug, s);
+    }
+    uint32_t hc[4] = {0, 0, 0, 0};
+    HIP_OK(hipMemcpyAsync(hc, g.counters, 16, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (hc[1]) return fail("a Gaussian was filtered although prefiltered is set%s%d");
+    const int64_t K = hc[0];
+    *num_rendered = (int64_t)((uint64_t)hc[2] | ((uint64_t)hc[3] << 32));
+    *num_instances = K;
+
+    const size_t bbytes = carve_binning(nullptr, K).bytes;
+    void* bbase = alloc(user, DG_BUF_BINNING, bbytes);
+    if (!bbase) return fail("binning allocation failed%s%d");
+    *binning_out = bbase;
+    Binning b = carve_binning(bbase, K);
+
+    const uint32_t* s_e = b.se0;
+    const uint32_t* s_keys = b.tk0;
+    if (K > 0) {
+        gs::launch_emit(P, order, g.cnt, g.off, g.xy, g.co, radii, tx, ty, g.first_e, b.tk0, b.eg, s);
+        DBG_SYNC(a->debug, s);
+        const int which = gs::radix_sort_pairs(b.tk0, b.se0, b.tk1, b.se1, nullptr, (uint32_t)K, 0, bits_for((uint32_t)T),
+                                               b.sort_tmp, s);
+        s_e = which ? b.se1 : b.se0;
+        s_keys = which ? b.tk1 : b.tk0;
+        DBG_SYNC(a->debug, s);
+    }
+    HIP_OK(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * (size_t)T, s));
+    gs::launch_ranges((uint32_t)K, s_keys, im.ranges, (uint32_t)T, s);
+    DBG_SYNC(a->debug, s);
+
+    gs::RenderArgs r;
+    r.W = W; r.H = H; r.tiles_x = tx; r.num_tiles = T;
+    r.K = (uint32_t)(K > 0 ? K : 1); r.P = (uint32_t)(P > 0 ? P : 1);
+    r.ranges = im.ranges; r.s_e = s_e; r.eg = b.eg; r.xy = g.xy; r.co = g.co; r.rgbi = g.rgbi; r.bg = a->bg;
+    r.out_color = out_color; r.out_invd = out_invdepth; r.final_T = im.final_T; r.img_color = im.img_color;
+    r.img_invd = im.img_invd; r.n_contrib = im.n_contrib; r.max_contrib = im.max_contrib;
+    gs::launch_render_fwd(r, s);
+    DBG_SYNC(a->debug, s);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void* geom, const void* binning,
+                          const void* image, int64_t num_rendered, int64_t K, const float* dL_dout_color,
+                          const float* dL_dout_invdepth, float* dmeans2D, float* dcolors, float* dopacity,
+                          float* dmeans3D, float* dcov3D, float* ddc, float* dsh, float* dscales, float* drot,
+                          float* depth, dg_alloc_fn alloc, void* user, dg_stream_t stream_) {
+    (void)num_rendered;
+    if (check_args(a)) return 1;
+    hipStream_t s = (hipStream_t)stream_;
+    const int P = a->P, W = a->W, H = a->H;
+    const int tx = tiles_x_of(W), ty = tiles_y_of(H), T = tx * ty;
+    if (P == 0) return 0;
+    Geom g = carve_geom((void*)geom, P);
+    Image im = carve_image((void*)image, W, H);
+    Binning b = carve_binning((void*)binning, K);
+    const int passes = (bits_for((uint32_t)T) + 7) / 8;
+    const uint32_t* s_e = (passes & 1) ? b.se1 : b.se0;
+
+    const size_t sbytes = carve_bwd(nullptr, K).bytes;
+    void* sbase = alloc(user, DG_BUF_BACKWARD, sbytes);
+    if (!sbase) return fail("backward scratch allocation failed%s%d");
+    BwdScratch sc = carve_bwd(sbase, K);
+    if (K > 0) {
+        HIP_OK(hipMemsetAsync(sc.flag, 0, (size_t)K, s));
+        gs::RenderBwdArgs r;
+        r.W = W; r.H = H; r.tiles_x = tx; r.num_tiles = T;
+        r.K = (uint32_t)K; r.P = (uint32_t)P;
+        r.ranges = im.ranges; r.max_contrib = im.max_contrib; r.s_e = s_e; r.eg = b.eg;
+        r.xy = g.xy; r.co = g.co; r.rgbi = g.rgbi; r.bg = a->bg;
+        r.final_T = im.final_T; r.img_color = im.img_color; r.img_invd = im.img_invd; r.n_contrib = im.n_contrib;
+        r.dL_dpix = dL_dout_color; r.dL_dinvd = dL_dout_invdepth; r.rec = sc.rec; r.flag = sc.flag;
+        gs::launch_render_bwd(r, s);
+        DBG_SYNC(a->debug, s);
+    }
+    gs::GaussBwdArgs q;
+    memset(&q, 0, sizeof(q));
+    q.P = P; q.D = a->D; q.M = a->M; q.W = W; q.H = H; q.antialiasing = a->antialiasing;
+    q.K = (uint32_t)K;
+    q.tanfovx = a->tanfovx; q.tanfovy = a->tanfovy;
+    q.focal_y = H / (2.0f * a->tanfovy);
+    q.focal_x = W / (2.0f * a->tanfovx);
+    q.scale_mod = a->scale_modifier;
+    q.means3D = a->means3D; q.scales = a->scales; q.rotations = a->rotations; q.opacities = a->opacities;
+    q.dc = a->dc; q.sh = (a->M > 0) ? a->sh : nullptr; q.cov3D_precomp = a->cov3D_precomp;
+    q.view = a->viewmatrix; q.proj = a->projmatrix; q.campos = a->campos;
+    q.radii = radii; q.cnt = g.cnt; q.first_e = g.first_e; q.rec = sc.rec; q.flag = sc.flag;
+    q.dmeans2D = dmeans2D; q.dcolors = dcolors; q.dopacity = dopacity; q.dmeans3D = dmeans3D; q.dcov3D = dcov3D;
+    q.ddc = ddc; q.dsh = dsh; q.dscales = dscales; q.drot = drot; q.depth = depth;
+    if (q.M > 0 && !dsh) return fail("dsh output required when M > 0%s%d");
+    gs::launch_gauss_bwd(q, s);
+    DBG_SYNC(a->debug, s);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,
+                    dg_stream_t stream) {
+    (void)projmatrix;
+    gs::launch_mark_visible(P, means3D, viewmatrix, (bool*)present, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_rasterize_filter(const dg_raster_args* a, int* radii, dg_stream_t stream) {
+    if (!a || a->P < 0) return fail("bad args%s%d");
+    if (a->P == 0) return 0;
+    gs::PreArgs p;
+    fill_pre(p, a);
+    p.radii = radii;
+    uint32_t* err = nullptr;
+    HIP_OK(hipMallocAsync((void**)&err, 4, (hipStream_t)stream));
+    HIP_OK(hipMemsetAsync(err, 0, 4, (hipStream_t)stream));
+    p.err = err;
+    gs::launch_filter(p, (hipStream_t)stream);
+    uint32_t h = 0;
+    HIP_OK(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIP_OK(hipFreeAsync(err, (hipStream_t)stream));
+    HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+    if (h) return fail("a Gaussian was filtered although prefiltered is set%s%d");
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_adam_update(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const uint8_t* visible,
+                   float lr, float b1, float b2, float eps, uint32_t N, uint32_t M, dg_stream_t stream) {
+    gs::launch_adam(param, grad, exp_avg, exp_avg_sq, (const bool*)visible, lr, b1, b2, eps, N, M, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_fused_ssim_forward(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,
+                          float* ssim_map, float* dm_dmu1, float* dm_dsigma1_sq, float* dm_dsigma12,
+                          dg_stream_t stream) {
+    if (dm_dmu1 && (!dm_dsigma1_sq || !dm_dsigma12)) return fail("train=True needs all three partial maps%s%d");
+    gs::launch_ssim_fwd(B, CH, H, W, C1, C2, img1, img2, ssim_map, dm_dmu1, dm_dsigma1_sq, dm_dsigma12,
+                        (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_fused_ssim_backward(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,
+                           const float* dL_dmap, const float* dm_dmu1, const float* dm_dsigma1_sq,
+                           const float* dm_dsigma12, float* dL_dimg1, dg_stream_t stream) {
+    (void)C1; (void)C2;
+    gs::launch_ssim_bwd(B, CH, H, W, img1, img2, dL_dmap, dm_dmu1, dm_dsigma1_sq, dm_dsigma12, dL_dimg1,
+                        (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_dist_cuda2(int P, const float* points, float* out, dg_alloc_fn alloc, void* user, dg_stream_t stream) {
+    if (P <= 0) return 0;
+    void* t = alloc(user, DG_BUF_TEMP, gs::knn_temp_bytes(P));
+    if (!t) return fail("knn scratch allocation failed%s%d");
+    gs::launch_knn(P, points, out, t, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+namespace {
+__global__ void k_gather_g(uint32_t K, const uint32_t* s_e, const uint32_t* eg, uint32_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < K) out[i] = eg[s_e[i]];
+}
+}  // namespace
+
+int dg_debug_sorted_instances(const void* binning, int64_t K, int W, int H, uint32_t* tiles_out, uint32_t* gauss_out,
+                              dg_stream_t stream) {
+    if (K <= 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    Binning b = carve_binning((void*)binning, K);
+    const int passes = (bits_for((uint32_t)(tiles_x_of(W) * tiles_y_of(H))) + 7) / 8;
+    const uint32_t* s_e = (passes & 1) ? b.se1 : b.se0;
+    const uint32_t* keys = (passes & 1) ? b.tk1 : b.tk0;
+    HIP_OK(hipMemcpyAsync(tiles_out, keys, 4 * (size_t)K, hipMemcpyDeviceToDevice, s));
+    k_gather_g<<<(unsigned)((K + 255) / 256), 256, 0, s>>>((uint32_t)K, s_e, b.eg, gauss_out);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_debug_geometry(const void* geom, int P, float* means2D, float* conic_opacity, float* rgb_invdepth,
+                      uint32_t* tile_count, dg_stream_t stream) {
+    if (P <= 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    Geom g = carve_geom((void*)geom, P);
+    if (means2D) HIP_OK(hipMemcpyAsync(means2D, g.xy, 8 * (size_t)P, hipMemcpyDeviceToDevice, s));
+    if (conic_opacity) HIP_OK(hipMemcpyAsync(conic_opacity, g.co, 16 * (size_t)P, hipMemcpyDeviceToDevice, s));
+    if (rgb_invdepth) HIP_OK(hipMemcpyAsync(rgb_invdepth, g.rgbi, 16 * (size_t)P, hipMemcpyDeviceToDevice, s));
+    if (tile_count) HIP_OK(hipMemcpyAsync(tile_count, g.cnt, 4 * (size_t)P, hipMemcpyDeviceToDevice, s));
+    return 0;
+}
+
+int dg_debug_image_state(const void* image, int W, int H, float* final_T, uint32_t* n_contrib, uint32_t* max_contrib,
+                         uint32_t* ranges, dg_stream_t stream) {
+    hipStream_t s = (hipStream_t)stream;
+    Image im = carve_image((void*)image, W, H);
+    const size_t HW = (size_t)W * H, T = (size_t)tiles_x_of(W) * tiles_y_of(H);
+    if (final_T) HIP_OK(hipMemcpyAsync(final_T, im.final_T, 4 * HW, hipMemcpyDeviceToDevice, s));
+    if (n_contrib) HIP_OK(hipMemcpyAsync(n_contrib, im.n_contrib, 4 * HW, hipMemcpyDeviceToDevice, s));
+    if (max_contrib) HIP_OK(hipMemcpyAsync(max_contrib, im.max_contrib, 4 * T, hipMemcpyDeviceToDevice, s));
+    if (ranges) HIP_OK(hipMemcpyAsync(ranges, im.ranges, 8 * T, hipMemcpyDeviceToDevice, s));
+    return 0;
+}
+
+}  // extern "C"

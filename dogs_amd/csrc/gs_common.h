@@ -1,0 +1,188 @@
+// gs_common.h -- device helpers shared by the gfx950 rasterizer kernels.
+//
+// Arithmetic contract (see DESIGN.md "Bit-exact keys"): the library is compiled with
+// -ffp-contract=off and -fhip-fp32-correctly-rounded-divide-sqrt; every fused multiply-add is an
+// explicit fmaf() placed exactly where the CPU oracle (oracle/gs_oracle.c) places it, so the
+// per-Gaussian preprocess (depth, means2D, conic, radius, precise tile cull) -- everything that
+// decides the (tile, depth, index) keys -- is bit-identical to the oracle.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GS_TILE_X 16
+#define GS_TILE_Y 16
+#define GS_TILE_PIX 256
+#define GS_WAVE 64
+
+namespace gs {
+
+// auxiliary.h:21-38
+constexpr float SH_C0 = 0.28209479177387814f;
+constexpr float SH_C1 = 0.4886025119029199f;
+__device__ constexpr float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                                       -1.0925484305920792f, 0.5462742152960396f};
+__device__ constexpr float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                                       0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
+                                       -0.5900435899266435f};
+
+struct f3 { float x, y, z; };
+struct f4 { float x, y, z, w; };
+// glm::mat3 layout: m[col][row]
+struct m3 { float m[3][3]; };
+
+__device__ __forceinline__ m3 m3_cols(float a0, float a1, float a2, float a3, float a4, float a5, float a6,
+                                      float a7, float a8) {
+    m3 r;
+    r.m[0][0] = a0; r.m[0][1] = a1; r.m[0][2] = a2;
+    r.m[1][0] = a3; r.m[1][1] = a4; r.m[1][2] = a5;
+    r.m[2][0] = a6; r.m[2][1] = a7; r.m[2][2] = a8;
+    return r;
+}
+// glm operator*(mat3, mat3), product order of type_mat3x3.inl with nvcc-style contraction
+__device__ __forceinline__ m3 m3_mul(const m3& A, const m3& B) {
+    m3 R;
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+            R.m[j][i] = fmaf(A.m[2][i], B.m[j][2], fmaf(A.m[1][i], B.m[j][1], A.m[0][i] * B.m[j][0]));
+    return R;
+}
+__device__ __forceinline__ m3 m3_T(const m3& A) {
+    m3 R;
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+#pragma unroll
+        for (int i = 0; i < 3; i++) R.m[j][i] = A.m[i][j];
+    return R;
+}
+
+// auxiliary.h:69-108 (row-vector convention: x' = m0 x + m4 y + m8 z + m12)
+__device__ __forceinline__ f3 tp4x3(f3 p, const float* m) {
+    return {fmaf(m[8], p.z, fmaf(m[4], p.y, m[0] * p.x)) + m[12],
+            fmaf(m[9], p.z, fmaf(m[5], p.y, m[1] * p.x)) + m[13],
+            fmaf(m[10], p.z, fmaf(m[6], p.y, m[2] * p.x)) + m[14]};
+}
+__device__ __forceinline__ f4 tp4x4(f3 p, const float* m) {
+    return {fmaf(m[8], p.z, fmaf(m[4], p.y, m[0] * p.x)) + m[12],
+            fmaf(m[9], p.z, fmaf(m[5], p.y, m[1] * p.x)) + m[13],
+            fmaf(m[10], p.z, fmaf(m[6], p.y, m[2] * p.x)) + m[14],
+            fmaf(m[11], p.z, fmaf(m[7], p.y, m[3] * p.x)) + m[15]};
+}
+__device__ __forceinline__ f3 tv4x3T(f3 p, const float* m) {
+    return {fmaf(m[2], p.z, fmaf(m[1], p.y, m[0] * p.x)),
+            fmaf(m[6], p.z, fmaf(m[5], p.y, m[4] * p.x)),
+            fmaf(m[10], p.z, fmaf(m[9], p.y, m[8] * p.x))};
+}
+// auxiliary.h:40-43: the reference's double literals make this a double-precision expression
+__device__ __forceinline__ float ndc2pix(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
+
+// v_cvt_i32_f32 saturates and maps NaN to 0 -- the semantics the oracle restates
+__device__ __forceinline__ int f2i(float f) { return (int)f; }
+
+// Deterministic log shared with the oracle (gs_logf in oracle/gs_oracle.c): same operations, same order.
+__device__ __forceinline__ float gs_logf(float a) {
+    if (!(a > 0.0f)) return (a == 0.0f) ? -__builtin_inff() : __builtin_nanf("");
+    if (a == __builtin_inff()) return __builtin_inff();
+    uint32_t u = __float_as_uint(a);
+    int e = 0;
+    if (u < 0x00800000u) { u = __float_as_uint(a * 8388608.0f); e = -23; }
+    e += (int)((u >> 23) & 0xff) - 127;
+    float m = __uint_as_float((u & 0x007fffffu) | 0x3f800000u);
+    if (m > 1.41421356f) { m = m * 0.5f; e += 1; }
+    const float s = (m - 1.0f) / (m + 1.0f);
+    const float s2 = s * s;
+    float p = fmaf(s2, 0.22222222f, 0.28571429f);
+    p = fmaf(s2, p, 0.4f);
+    p = fmaf(s2, p, 0.66666669f);
+    p = fmaf(s2, p, 2.0f);
+    return fmaf((float)e, 0.693147182f, s * p);
+}
+
+// getRect (auxiliary.h:45-55) with the int radius overload
+__device__ __forceinline__ void get_rect(float px, float py, int r, int gx, int gy, int& x0, int& y0, int& x1,
+                                         int& y1) {
+    int a;
+    a = f2i((px - (float)r) / (float)GS_TILE_X); a = a > 0 ? a : 0; x0 = a < gx ? a : gx;
+    a = f2i((py - (float)r) / (float)GS_TILE_Y); a = a > 0 ? a : 0; y0 = a < gy ? a : gy;
+    a = f2i((((px + (float)r) + (float)GS_TILE_X) - 1.0f) / (float)GS_TILE_X); a = a > 0 ? a : 0; x1 = a < gx ? a : gx;
+    a = f2i((((py + (float)r) + (float)GS_TILE_Y) - 1.0f) / (float)GS_TILE_Y); a = a > 0 ? a : 0; y1 = a < gy ? a : gy;
+}
+
+// max_contrib_power_rect_gaussian_float<15,15> (rasterizer_impl.cu:52-100)
+__device__ __forceinline__ float max_contrib_power(f4 co, float mx, float my, float rminx, float rminy, float rmaxx,
+                                                   float rmaxy) {
+    const float x_min_diff = rminx - mx;
+    const float x_left = x_min_diff > 0.0f ? 1.0f : 0.0f;
+    const float not_in_x = x_left + (mx > rmaxx ? 1.0f : 0.0f);
+    const float y_min_diff = rminy - my;
+    const float y_above = y_min_diff > 0.0f ? 1.0f : 0.0f;
+    const float not_in_y = y_above + (my > rmaxy ? 1.0f : 0.0f);
+    float power = 0.0f;
+    if ((not_in_y + not_in_x) > 0.0f) {
+        const float px = x_left > 0.0f ? rminx : rmaxx;
+        const float py = y_above > 0.0f ? rminy : rmaxy;
+        const float dx = copysignf(15.0f, x_min_diff);
+        const float dy = copysignf(15.0f, y_min_diff);
+        const float diffx = mx - px, diffy = my - py;
+        const float rcx = 1.0f / (225.0f * co.x);
+        const float rcz = 1.0f / (225.0f * co.z);
+        float ax = fmaf(dx * co.y, diffy, (dx * co.x) * diffx) * rcx;
+        float ay = fmaf(dy * co.z, diffy, (dy * co.y) * diffx) * rcz;
+        ax = (ax != ax) ? 0.0f : fminf(fmaxf(ax, 0.0f), 1.0f);
+        ay = (ay != ay) ? 0.0f : fminf(fmaxf(ay, 0.0f), 1.0f);
+        const float tx = not_in_y * ax, ty = not_in_x * ay;
+        const float qx = fmaf(tx, dx, px), qy = fmaf(ty, dy, py);
+        const float ddx = mx - qx, ddy = my - qy;
+        power = fmaf(co.y * ddx, ddy, 0.5f * fmaf(co.z * ddy, ddy, (co.x * ddx) * ddx));
+    }
+    return power;
+}
+
+// forward.cu:119-153 (quaternion not normalised in-kernel, :128)
+__device__ __forceinline__ m3 quat_to_R(float r, float x, float y, float z) {
+    return m3_cols(fmaf(-2.f, fmaf(y, y, z * z), 1.f), 2.f * fmaf(x, y, -(r * z)), 2.f * fmaf(x, z, r * y),
+                   2.f * fmaf(x, y, r * z), fmaf(-2.f, fmaf(x, x, z * z), 1.f), 2.f * fmaf(y, z, -(r * x)),
+                   2.f * fmaf(x, z, -(r * y)), 2.f * fmaf(y, z, r * x), fmaf(-2.f, fmaf(x, x, y * y), 1.f));
+}
+__device__ __forceinline__ void cov3d_fwd(f3 s, float mod, f4 q, float* cov) {
+    m3 S = m3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+    S.m[0][0] = mod * s.x; S.m[1][1] = mod * s.y; S.m[2][2] = mod * s.z;
+    m3 R = quat_to_R(q.x, q.y, q.z, q.w);
+    m3 M = m3_mul(S, R);
+    m3 Mt = m3_T(M);
+    m3 Sig = m3_mul(Mt, M);
+    cov[0] = Sig.m[0][0]; cov[1] = Sig.m[0][1]; cov[2] = Sig.m[0][2];
+    cov[3] = Sig.m[1][1]; cov[4] = Sig.m[1][2]; cov[5] = Sig.m[2][2];
+}
+
+// computeCov2D (forward.cu:79-114); optionally returns the intermediates the backward needs
+struct Cov2DState { m3 T, W, V; f3 t; float xgm, ygm; };
+__device__ __forceinline__ f3 cov2d_fwd(f3 mean, float fx, float fy, float tfx, float tfy, const float* cov3D,
+                                        const float* vm, Cov2DState* st) {
+    f3 t = tp4x3(mean, vm);
+    const float limx = 1.3f * tfx, limy = 1.3f * tfy;
+    const float txtz = t.x / t.z, tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const float tz2 = t.z * t.z;
+    m3 J = m3_cols(fx / t.z, 0.0f, -(fx * t.x) / tz2, 0.0f, fy / t.z, -(fy * t.y) / tz2, 0, 0, 0);
+    m3 W = m3_cols(vm[0], vm[4], vm[8], vm[1], vm[5], vm[9], vm[2], vm[6], vm[10]);
+    m3 T = m3_mul(W, J);
+    m3 V = m3_cols(cov3D[0], cov3D[1], cov3D[2], cov3D[1], cov3D[3], cov3D[4], cov3D[2], cov3D[4], cov3D[5]);
+    m3 A = m3_mul(m3_T(T), m3_T(V));
+    m3 cov = m3_mul(A, T);
+    if (st) {
+        st->T = T; st->W = W; st->V = V; st->t = t;
+        st->xgm = (txtz < -limx || txtz > limx) ? 0.f : 1.f;
+        st->ygm = (tytz < -limy || tytz > limy) ? 0.f : 1.f;
+    }
+    return {cov.m[0][0], cov.m[0][1], cov.m[1][1]};
+}
+
+// compositing exponent, identical expression in forward and backward (forward.cu:451, backward.cu:596)
+__device__ __forceinline__ float splat_power(float cx, float cy, float cz, float dx, float dy) {
+    return fmaf(-0.5f, fmaf(cz * dy, dy, (cx * dx) * dx), -((cy * dx) * dy));
+}
+
+}  // namespace gs

@@ -1,0 +1,82 @@
+// raster.h -- kernel argument blocks and launchers of the gfx950 rasterizer (raster_fwd.hip, raster_bwd.hip)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gs {
+
+struct PreArgs {
+    int P, D, M, W, H, tiles_x, tiles_y;
+    int antialiasing, prefiltered;
+    float tanfovx, tanfovy, focal_x, focal_y, scale_mod;
+    const float *means3D, *scales, *rotations, *opacities, *dc, *sh, *colors, *cov3D_precomp;
+    const float *view, *proj, *campos;
+    int* radii;
+    float2* xy;         // means2D
+    float4* co;         // conic (a, b, c), opacity * AA scale
+    float4* rgbi;       // rgb, 1 / view z
+    uint32_t* depthkey; // float bits of view z, 0xffffffff when no tile survives the precise cull
+    uint32_t* cnt;      // precise tile count
+    unsigned long long* rect_sum;  // num_rendered of the reference (sum of rect areas)
+    uint32_t* err;
+};
+
+struct RenderArgs {
+    int W, H, tiles_x, num_tiles;
+    uint32_t K, P;          // bounds of s_e/eg and of the geometry arrays
+    const uint2* ranges;
+    const uint32_t* s_e;   // sorted instance -> emission index
+    const uint32_t* eg;    // emission index -> Gaussian
+    const float2* xy;
+    const float4* co;
+    const float4* rgbi;
+    const float* bg;
+    float *out_color, *out_invd, *final_T, *img_color, *img_invd;
+    uint32_t *n_contrib, *max_contrib;
+};
+
+struct RenderBwdArgs {
+    int W, H, tiles_x, num_tiles;
+    uint32_t K, P;
+    const uint2* ranges;
+    const uint32_t* max_contrib;
+    const uint32_t* s_e;
+    const uint32_t* eg;
+    const float2* xy;
+    const float4* co;
+    const float4* rgbi;
+    const float* bg;
+    const float *final_T, *img_color, *img_invd;
+    const uint32_t* n_contrib;
+    const float* dL_dpix;
+    const float* dL_dinvd;   // may be null
+    float* rec;              // [K][12] per-instance gradient record
+    uint8_t* flag;           // [K] record written
+};
+
+struct GaussBwdArgs {
+    int P, D, M, W, H, antialiasing;
+    uint32_t K;
+    float tanfovx, tanfovy, focal_x, focal_y, scale_mod;
+    const float *means3D, *scales, *rotations, *opacities, *dc, *sh, *cov3D_precomp;
+    const float *view, *proj, *campos;
+    const int* radii;
+    const uint32_t* cnt;
+    const uint32_t* first_e;
+    const float* rec;
+    const uint8_t* flag;
+    float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *ddc, *dsh, *dscales, *drot, *depth;
+};
+
+void launch_preprocess(const PreArgs& a, hipStream_t s);
+void launch_emit(int P, const uint32_t* order, const uint32_t* cnt, const uint32_t* off, const float2* xy,
+                 const float4* co, const int* radii, int tiles_x, int tiles_y, uint32_t* first_e, uint32_t* tilekey,
+                 uint32_t* eg, hipStream_t s);
+void launch_ranges(uint32_t K, const uint32_t* keys, uint2* ranges, uint32_t num_tiles, hipStream_t s);
+void launch_render_fwd(const RenderArgs& a, hipStream_t s);
+void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);
+void launch_filter(const PreArgs& a, hipStream_t s);
+void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);
+void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s);
+
+}  // namespace gs

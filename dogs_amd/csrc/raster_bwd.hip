@@ -1,0 +1,436 @@
+// raster_bwd.hip -- backward of the tile rasterizer for gfx950.
+//
+// k_render_bwd   one wave64 per tile, 4 pixels per lane, front-to-back replay from T = 1 up to the tile's
+//                max contributor. The reference (backward.cu:455-658) replays 32-splat buckets from
+//                ~2 GB of sampled forward state; here the state is recomputed on the fly, which is the
+//                same arithmetic (T *= 1 - alpha, ar += w c) without the sampled-state traffic.
+//                Per splat, the 10 gradient partials are summed over the wave with a transpose
+//                reduce-scatter (13 cross-lane exchanges instead of 60) and stored once as a 48-B record
+//                at the instance's emission slot -- no float atomics (the chip-wide atomic rate and the
+//                scattered-row penalty make per-instance atomicAdd the wrong tool on MI355X).
+// k_gauss_bwd    one thread per Gaussian: sums its records in emission order (deterministic), then
+//                computeCov2DCUDA + preprocessCUDA backward (backward.cu:149-451) fused in one pass.
+#include <hip/hip_runtime.h>
+#include "gs_common.h"
+#include "raster.h"
+
+namespace gs {
+
+__device__ __forceinline__ float bcastf(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// Sum 10 per-lane values over the wave. Returns the total of slot `slot` (valid when slot >= 0).
+__device__ __forceinline__ float wave_reduce10(const float (&p)[10], int lane, int& slot) {
+    const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8, b2 = lane & 4;
+    float q[6];
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        const float send = b5 ? p[i] : p[5 + i];
+        const float keep = b5 ? p[5 + i] : p[i];
+        q[i] = keep + __shfl_xor(send, 32);
+    }
+    q[5] = 0.0f;
+    float r[4];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const float send = b4 ? q[i] : q[3 + i];
+        const float keep = b4 ? q[3 + i] : q[i];
+        r[i] = keep + __shfl_xor(send, 16);
+    }
+    r[3] = 0.0f;
+    float s[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const float send = b3 ? r[i] : r[2 + i];
+        const float keep = b3 ? r[2 + i] : r[i];
+        s[i] = keep + __shfl_xor(send, 8);
+    }
+    float u;
+    {
+        const float send = b2 ? s[0] : s[1];
+        const float keep = b2 ? s[1] : s[0];
+        u = keep + __shfl_xor(send, 4);
+    }
+    u += __shfl_xor(u, 2);
+    u += __shfl_xor(u, 1);
+    const int ri = (b3 ? 2 : 0) + (b2 ? 1 : 0);
+    const bool valid = (ri <= 2) && (!b4 || ri <= 1) && ((lane & 3) == 0);
+    slot = valid ? ((b5 ? 5 : 0) + (b4 ? 3 : 0) + ri) : -1;
+    return u;
+}
+
+__global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= a.num_tiles) return;
+    const uint2 rg = a.ranges[tile];
+    const int nall = (int)(rg.y - rg.x);
+    const int mc = (int)a.max_contrib[tile];
+    const int n = nall < mc ? nall : mc;
+    if (n <= 0) return;
+    const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
+    const int px = tx * GS_TILE_X + (lane & 15);
+    const int py0 = ty * GS_TILE_Y + (lane >> 4);
+    const float pxf = (float)px;
+    const size_t HW = (size_t)a.W * a.H;
+    const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
+    const float hw = 0.5f * a.W, hh = 0.5f * a.H;
+    float T[4], ar0[4], ar1[4], ar2[4], ard[4], Tf[4], d0[4], d1[4], d2[4], dd[4], bgdot[4];
+    int last[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int py = py0 + 4 * k;
+        T[k] = 1.0f;
+        if (px < a.W && py < a.H) {
+            const size_t pid = (size_t)py * a.W + px;
+            last[k] = (int)a.n_contrib[pid];
+            ar0[k] = -a.img_color[pid]; ar1[k] = -a.img_color[HW + pid]; ar2[k] = -a.img_color[2 * HW + pid];
+            ard[k] = -a.img_invd[pid];
+            Tf[k] = a.final_T[pid];
+            d0[k] = a.dL_dpix[pid]; d1[k] = a.dL_dpix[HW + pid]; d2[k] = a.dL_dpix[2 * HW + pid];
+            dd[k] = a.dL_dinvd ? a.dL_dinvd[pid] : 0.0f;
+        } else {
+            last[k] = 0;
+            ar0[k] = ar1[k] = ar2[k] = ard[k] = Tf[k] = d0[k] = d1[k] = d2[k] = dd[k] = 0.0f;
+        }
+        bgdot[k] = fmaf(bg2, d2[k], fmaf(bg1, d1[k], bg0 * d0[k]));
+    }
+    for (int base = 0; base < n; base += 64) {
+        const int j = base + lane;
+        float gx = 0, gy = 0, ca = 0, cb = 0, cc = 0, op = 0, cr = 0, cg = 0, cbl = 0, ci = 0;
+        uint32_t ee = 0;
+        if (j < n) {
+            ee = min(a.s_e[rg.x + j], a.K - 1);
+            const uint32_t g = min(a.eg[ee], a.P - 1);
+            const float2 m = a.xy[g];
+            const float4 c4 = a.co[g];
+            const float4 q = a.rgbi[g];
+            gx = m.x; gy = m.y; ca = c4.x; cb = c4.y; cc = c4.z; op = c4.w;
+            cr = q.x; cg = q.y; cbl = q.z; ci = q.w;
+        }
+        const int cntb = (n - base) < 64 ? (n - base) : 64;
+        for (int jj = 0; jj < cntb; jj++) {
+            const float sx = bcastf(gx, jj), sy = bcastf(gy, jj);
+            const float sa = bcastf(ca, jj), sb = bcastf(cb, jj), sc = bcastf(cc, jj), so = bcastf(op, jj);
+            const float sr = bcastf(cr, jj), sg = bcastf(cg, jj), sbl = bcastf(cbl, jj), si = bcastf(ci, jj);
+            const int sidx = base + jj;
+            const float dx = sx - pxf;
+            float p[10];
+#pragma unroll
+            for (int v = 0; v < 10; v++) p[v] = 0.0f;
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float dy = sy - (float)(py0 + 4 * k);
+                const float power = splat_power(sa, sb, sc, dx, dy);
+                const float G = __expf(power);
+                const float alpha = fminf(0.99f, so * G);
+                const bool act = (sidx < last[k]) && !(power > 0.0f) && !(alpha < (1.0f / 255.0f));
+                if (act) {
+                    any = true;
+                    const float weight = alpha * T[k];
+                    const float oma = 1.0f - alpha;
+                    const float inv = __builtin_amdgcn_rcpf(oma);
+                    ar0[k] = fmaf(weight, sr, ar0[k]);
+                    ar1[k] = fmaf(weight, sg, ar1[k]);
+                    ar2[k] = fmaf(weight, sbl, ar2[k]);
+                    p[6] = fmaf(weight, d0[k], p[6]);
+                    p[7] = fmaf(weight, d1[k], p[7]);
+                    p[8] = fmaf(weight, d2[k], p[8]);
+                    float dLda = fmaf(fmaf(sr, T[k], inv * ar0[k]), d0[k], 0.0f);
+                    dLda = fmaf(fmaf(sg, T[k], inv * ar1[k]), d1[k], dLda);
+                    dLda = fmaf(fmaf(sbl, T[k], inv * ar2[k]), d2[k], dLda);
+                    ard[k] = fmaf(weight, si, ard[k]);
+                    p[9] = fmaf(weight, dd[k], p[9]);
+                    dLda = fmaf(fmaf(si, T[k], inv * ard[k]), dd[k], dLda);
+                    dLda = fmaf(-Tf[k] * inv, bgdot[k], dLda);
+                    T[k] = T[k] * oma;
+                    const float dL_dG = so * dLda;
+                    const float gdx = G * dx, gdy = G * dy;
+                    const float dG_ddelx = fmaf(-gdx, sa, -(gdy * sb));
+                    const float dG_ddely = fmaf(-gdy, sc, -(gdx * sb));
+                    p[0] = fmaf(dL_dG * dG_ddelx, hw, p[0]);
+                    p[1] = fmaf(dL_dG * dG_ddely, hh, p[1]);
+                    p[2] = fmaf(-0.5f * gdx * dx, dL_dG, p[2]);
+                    p[3] = fmaf(-0.5f * gdx * dy, dL_dG, p[3]);
+                    p[4] = fmaf(-0.5f * gdy * dy, dL_dG, p[4]);
+                    p[5] = fmaf(G, dLda, p[5]);
+                }
+            }
+            if (__any(any)) {
+                int slot;
+                const float tot = wave_reduce10(p, lane, slot);
+                const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)ee, jj);
+                if (slot >= 0) a.rec[(size_t)e * 12 + slot] = tot;
+                if (lane == 0) a.flag[e] = 1;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// per-Gaussian backward: record sum + computeCov2DCUDA + preprocessCUDA (backward.cu:23-451)
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float sq(float x) { return x * x; }
+
+__global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    const int M = a.M;
+    float* dsh = a.dsh ? a.dsh + (size_t)idx * M * 3 : nullptr;
+    if (!(a.radii[idx] > 0)) {
+        for (int v = 0; v < 3; v++) {
+            a.dmeans2D[3 * idx + v] = 0.f; a.dcolors[3 * idx + v] = 0.f; a.dmeans3D[3 * idx + v] = 0.f;
+            a.ddc[3 * idx + v] = 0.f; a.dscales[3 * idx + v] = 0.f;
+        }
+        for (int v = 0; v < 6; v++) a.dcov3D[6 * idx + v] = 0.f;
+        for (int v = 0; v < 4; v++) a.drot[4 * idx + v] = 0.f;
+        a.dopacity[idx] = 0.f;
+        a.depth[idx] = 0.f;
+        if (dsh) for (int v = 0; v < 3 * M; v++) dsh[v] = 0.f;
+        return;
+    }
+    // ---- records -> dL/d(mean2D, conic, opacity, color, invdepth)
+    float acc[10];
+#pragma unroll
+    for (int v = 0; v < 10; v++) acc[v] = 0.f;
+    {
+        uint32_t c = a.cnt[idx];
+        const uint32_t e0 = c ? a.first_e[idx] : 0u;
+        if (e0 >= a.K || c > a.K - e0) c = 0;  // defensive: never read outside the record block
+        for (uint32_t e = e0; e < e0 + c; e++) {
+            if (!a.flag[e]) continue;
+            const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
+            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+            acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
+            acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
+            acc[8] += r2.x; acc[9] += r2.y;
+        }
+    }
+    a.dmeans2D[3 * idx + 0] = acc[0];
+    a.dmeans2D[3 * idx + 1] = acc[1];
+    a.dmeans2D[3 * idx + 2] = 0.f;
+    a.dcolors[3 * idx + 0] = acc[6];
+    a.dcolors[3 * idx + 1] = acc[7];
+    a.dcolors[3 * idx + 2] = acc[8];
+    float dLo = acc[5];
+    const float dL_dinvd = acc[9];
+
+    // ---- computeCov2DCUDA (backward.cu:149-326)
+    const f3 mean = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+    float cbuf[6];
+    const float* cov3D;
+    if (a.cov3D_precomp) {
+        cov3D = a.cov3D_precomp + 6 * idx;
+    } else {
+        const f3 s = {a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
+        const f4 q = {a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]};
+        cov3d_fwd(s, a.scale_mod, q, cbuf);
+        cov3D = cbuf;
+    }
+    const float h_x = a.focal_x, h_y = a.focal_y;
+    Cov2DState st;
+    const f3 cv = cov2d_fwd(mean, h_x, h_y, a.tanfovx, a.tanfovy, cov3D, a.view, &st);
+    a.depth[idx] = tp4x3(mean, a.view).z;
+    float c_xx = cv.x, c_xy = cv.y, c_yy = cv.z;
+    const float h_var = 0.3f;
+    float d_inside_root = 0.f;
+    if (a.antialiasing) {
+        const float det_cov = fmaf(c_xx, c_yy, -(c_xy * c_xy));
+        c_xx += h_var; c_yy += h_var;
+        const float det_plus = fmaf(c_xx, c_yy, -(c_xy * c_xy));
+        const float hs = sqrtf(fmaxf(0.000025f, det_cov / det_plus));
+        const float dhs = dLo * a.opacities[idx];
+        dLo = dLo * hs;
+        d_inside_root = (det_cov / det_plus) <= 0.000025f ? 0.f : dhs / (2 * hs);
+    } else {
+        c_xx += h_var; c_yy += h_var;
+    }
+    a.dopacity[idx] = dLo;
+    float dcxx = 0.f, dcxy = 0.f, dcyy = 0.f;
+    if (a.antialiasing) {
+        const float x = c_xx, y = c_yy, z = c_xy, w = h_var;
+        const float denom_f = d_inside_root / sq(w * w + w * (x + y) + x * y - z * z);
+        dcxx = w * (w * y + y * y + z * z) * denom_f;
+        dcyy = w * (w * x + x * x + z * z) * denom_f;
+        dcxy = -2.f * w * z * (w + x + y) * denom_f;
+    }
+    const float gcx = acc[2], gcy = acc[3], gcz = acc[4];  // dL/dconic (x, y, w)
+    const float denom = c_xx * c_yy - c_xy * c_xy;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    const m3& T = st.T;
+    const float T00 = T.m[0][0], T01 = T.m[0][1], T02 = T.m[0][2], T10 = T.m[1][0], T11 = T.m[1][1], T12 = T.m[1][2];
+    float dcov[6];
+    if (denom2inv != 0) {
+        dcxx += denom2inv * (-c_yy * c_yy * gcx + 2 * c_xy * c_yy * gcy + (denom - c_xx * c_yy) * gcz);
+        dcyy += denom2inv * (-c_xx * c_xx * gcz + 2 * c_xx * c_xy * gcy + (denom - c_xx * c_yy) * gcx);
+        dcxy += denom2inv * 2 * (c_xy * c_yy * gcx - (denom + 2 * c_xy * c_xy) * gcy + c_xx * c_xy * gcz);
+        dcov[0] = (T00 * T00 * dcxx + T00 * T10 * dcxy + T10 * T10 * dcyy);
+        dcov[3] = (T01 * T01 * dcxx + T01 * T11 * dcxy + T11 * T11 * dcyy);
+        dcov[5] = (T02 * T02 * dcxx + T02 * T12 * dcxy + T12 * T12 * dcyy);
+        dcov[1] = 2 * T00 * T01 * dcxx + (T00 * T11 + T01 * T10) * dcxy + 2 * T10 * T11 * dcyy;
+        dcov[2] = 2 * T00 * T02 * dcxx + (T00 * T12 + T02 * T10) * dcxy + 2 * T10 * T12 * dcyy;
+        dcov[4] = 2 * T02 * T01 * dcxx + (T01 * T12 + T02 * T11) * dcxy + 2 * T11 * T12 * dcyy;
+    } else {
+        for (int i = 0; i < 6; i++) dcov[i] = 0.f;
+    }
+    for (int i = 0; i < 6; i++) a.dcov3D[6 * idx + i] = dcov[i];
+    const m3& V = st.V;
+    const float dT00 = 2 * (T00 * V.m[0][0] + T01 * V.m[0][1] + T02 * V.m[0][2]) * dcxx + (T10 * V.m[0][0] + T11 * V.m[0][1] + T12 * V.m[0][2]) * dcxy;
+    const float dT01 = 2 * (T00 * V.m[1][0] + T01 * V.m[1][1] + T02 * V.m[1][2]) * dcxx + (T10 * V.m[1][0] + T11 * V.m[1][1] + T12 * V.m[1][2]) * dcxy;
+    const float dT02 = 2 * (T00 * V.m[2][0] + T01 * V.m[2][1] + T02 * V.m[2][2]) * dcxx + (T10 * V.m[2][0] + T11 * V.m[2][1] + T12 * V.m[2][2]) * dcxy;
+    const float dT10 = 2 * (T10 * V.m[0][0] + T11 * V.m[0][1] + T12 * V.m[0][2]) * dcyy + (T00 * V.m[0][0] + T01 * V.m[0][1] + T02 * V.m[0][2]) * dcxy;
+    const float dT11 = 2 * (T10 * V.m[1][0] + T11 * V.m[1][1] + T12 * V.m[1][2]) * dcyy + (T00 * V.m[1][0] + T01 * V.m[1][1] + T02 * V.m[1][2]) * dcxy;
+    const float dT12 = 2 * (T10 * V.m[2][0] + T11 * V.m[2][1] + T12 * V.m[2][2]) * dcyy + (T00 * V.m[2][0] + T01 * V.m[2][1] + T02 * V.m[2][2]) * dcxy;
+    const m3& W = st.W;
+    const float dJ00 = W.m[0][0] * dT00 + W.m[0][1] * dT01 + W.m[0][2] * dT02;
+    const float dJ02 = W.m[2][0] * dT00 + W.m[2][1] * dT01 + W.m[2][2] * dT02;
+    const float dJ11 = W.m[1][0] * dT10 + W.m[1][1] * dT11 + W.m[1][2] * dT12;
+    const float dJ12 = W.m[2][0] * dT10 + W.m[2][1] * dT11 + W.m[2][2] * dT12;
+    const f3 t = st.t;
+    const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dtx = st.xgm * -h_x * tz2 * dJ02;
+    const float dty = st.ygm * -h_y * tz2 * dJ12;
+    const float dtz = -h_x * tz2 * dJ00 - h_y * tz2 * dJ11 + (2 * h_x * t.x) * tz3 * dJ02 + (2 * h_y * t.y) * tz3 * dJ12 -
+                      dL_dinvd * tz2;
+    f3 dmean = tv4x3T({dtx, dty, dtz}, a.view);
+
+    // ---- preprocessCUDA backward: mean2D projection (backward.cu:425-442)
+    {
+        const float* proj = a.proj;
+        const f4 mh = tp4x4(mean, proj);
+        const float m_w = 1.0f / (mh.w + 0.0000001f);
+        const float mul1 = (proj[0] * mean.x + proj[4] * mean.y + proj[8] * mean.z + proj[12]) * m_w * m_w;
+        const float mul2 = (proj[1] * mean.x + proj[5] * mean.y + proj[9] * mean.z + proj[13]) * m_w * m_w;
+        const float gx = acc[0], gy = acc[1];
+        dmean.x += (proj[0] * m_w - proj[3] * mul1) * gx + (proj[1] * m_w - proj[3] * mul2) * gy;
+        dmean.y += (proj[4] * m_w - proj[7] * mul1) * gx + (proj[5] * m_w - proj[7] * mul2) * gy;
+        dmean.z += (proj[8] * m_w - proj[11] * mul1) * gx + (proj[9] * m_w - proj[11] * mul2) * gy;
+    }
+
+    // ---- computeColorFromSH backward (backward.cu:23-144); clamped flags recomputed from the forward rgb
+    if (a.sh) {
+        const float* sh = a.sh + (size_t)idx * M * 3;
+        const float* d0p = a.dc + 3 * idx;
+        const int deg = a.D;
+        const f3 dir_orig = {mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]};
+        const float len = sqrtf(fmaf(dir_orig.z, dir_orig.z, fmaf(dir_orig.y, dir_orig.y, dir_orig.x * dir_orig.x)));
+        const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+        // forward colour (same expression as raster_fwd.hip sh_to_rgb) for the clamp mask
+        float basis[15];
+        int nb = 0;
+        float xx = 0, yy = 0, zz = 0, xy = 0, yz = 0, xz = 0;
+        if (deg > 0) {
+            basis[0] = -SH_C1 * y; basis[1] = SH_C1 * z; basis[2] = -SH_C1 * x; nb = 3;
+            if (deg > 1) {
+                xx = x * x; yy = y * y; zz = z * z; xy = x * y; yz = y * z; xz = x * z;
+                basis[3] = SH_C2[0] * xy;
+                basis[4] = SH_C2[1] * yz;
+                basis[5] = SH_C2[2] * (2.0f * zz - xx - yy);
+                basis[6] = SH_C2[3] * xz;
+                basis[7] = SH_C2[4] * (xx - yy);
+                nb = 8;
+                if (deg > 2) {
+                    basis[8] = SH_C3[0] * y * (3.0f * xx - yy);
+                    basis[9] = SH_C3[1] * xy * z;
+                    basis[10] = SH_C3[2] * y * (4.0f * zz - xx - yy);
+                    basis[11] = SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
+                    basis[12] = SH_C3[4] * x * (4.0f * zz - xx - yy);
+                    basis[13] = SH_C3[5] * z * (xx - yy);
+                    basis[14] = SH_C3[6] * x * (xx - 3.0f * yy);
+                    nb = 15;
+                }
+            }
+        }
+        float dRGB[3];
+        for (int ch = 0; ch < 3; ch++) {
+            float r = SH_C0 * d0p[ch];
+            for (int k = 0; k < nb; k++) r = fmaf(basis[k], sh[3 * k + ch], r);
+            r += 0.5f;
+            dRGB[ch] = (r < 0) ? 0.0f : acc[6 + ch];
+        }
+        for (int ch = 0; ch < 3; ch++) a.ddc[3 * idx + ch] = SH_C0 * dRGB[ch];
+        for (int k = 0; k < M; k++)
+            for (int ch = 0; ch < 3; ch++) dsh[3 * k + ch] = k < nb ? basis[k] * dRGB[ch] : 0.0f;
+        float dx[3] = {0, 0, 0}, dy[3] = {0, 0, 0}, dz[3] = {0, 0, 0};
+#define SHV(k, ch) sh[3 * (k) + (ch)]
+        if (deg > 0) {
+            for (int ch = 0; ch < 3; ch++) {
+                dx[ch] = -SH_C1 * SHV(2, ch); dy[ch] = -SH_C1 * SHV(0, ch); dz[ch] = SH_C1 * SHV(1, ch);
+            }
+            if (deg > 1) {
+                for (int ch = 0; ch < 3; ch++) {
+                    dx[ch] += SH_C2[0] * y * SHV(3, ch) + SH_C2[2] * 2.f * -x * SHV(5, ch) + SH_C2[3] * z * SHV(6, ch) + SH_C2[4] * 2.f * x * SHV(7, ch);
+                    dy[ch] += SH_C2[0] * x * SHV(3, ch) + SH_C2[1] * z * SHV(4, ch) + SH_C2[2] * 2.f * -y * SHV(5, ch) + SH_C2[4] * 2.f * -y * SHV(7, ch);
+                    dz[ch] += SH_C2[1] * y * SHV(4, ch) + SH_C2[2] * 2.f * 2.f * z * SHV(5, ch) + SH_C2[3] * x * SHV(6, ch);
+                }
+                if (deg > 2) {
+                    for (int ch = 0; ch < 3; ch++) {
+                        dx[ch] += (SH_C3[0] * SHV(8, ch) * 3.f * 2.f * xy + SH_C3[1] * SHV(9, ch) * yz + SH_C3[2] * SHV(10, ch) * -2.f * xy +
+                                   SH_C3[3] * SHV(11, ch) * -3.f * 2.f * xz + SH_C3[4] * SHV(12, ch) * (-3.f * xx + 4.f * zz - yy) +
+                                   SH_C3[5] * SHV(13, ch) * 2.f * xz + SH_C3[6] * SHV(14, ch) * 3.f * (xx - yy));
+                        dy[ch] += (SH_C3[0] * SHV(8, ch) * 3.f * (xx - yy) + SH_C3[1] * SHV(9, ch) * xz +
+                                   SH_C3[2] * SHV(10, ch) * (-3.f * yy + 4.f * zz - xx) + SH_C3[3] * SHV(11, ch) * -3.f * 2.f * yz +
+                                   SH_C3[4] * SHV(12, ch) * -2.f * xy + SH_C3[5] * SHV(13, ch) * -2.f * yz + SH_C3[6] * SHV(14, ch) * -3.f * 2.f * xy);
+                        dz[ch] += (SH_C3[1] * SHV(9, ch) * xy + SH_C3[2] * SHV(10, ch) * 4.f * 2.f * yz +
+                                   SH_C3[3] * SHV(11, ch) * 3.f * (2.f * zz - xx - yy) + SH_C3[4] * SHV(12, ch) * 4.f * 2.f * xz +
+                                   SH_C3[5] * SHV(13, ch) * (xx - yy));
+                    }
+                }
+            }
+        }
+#undef SHV
+        const f3 ddir = {dx[0] * dRGB[0] + dx[1] * dRGB[1] + dx[2] * dRGB[2], dy[0] * dRGB[0] + dy[1] * dRGB[1] + dy[2] * dRGB[2],
+                         dz[0] * dRGB[0] + dz[1] * dRGB[1] + dz[2] * dRGB[2]};
+        // dnormvdv (auxiliary.h:118-128)
+        const f3 v = dir_orig;
+        const float sum2 = fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
+        const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+        dmean.x += ((sum2 - v.x * v.x) * ddir.x - v.y * v.x * ddir.y - v.z * v.x * ddir.z) * invsum32;
+        dmean.y += (-v.x * v.y * ddir.x + (sum2 - v.y * v.y) * ddir.y - v.z * v.y * ddir.z) * invsum32;
+        dmean.z += (-v.x * v.z * ddir.x - v.y * v.z * ddir.y + (sum2 - v.z * v.z) * ddir.z) * invsum32;
+    } else {
+        for (int ch = 0; ch < 3; ch++) a.ddc[3 * idx + ch] = 0.f;
+    }
+    a.dmeans3D[3 * idx + 0] = dmean.x;
+    a.dmeans3D[3 * idx + 1] = dmean.y;
+    a.dmeans3D[3 * idx + 2] = dmean.z;
+
+    // ---- computeCov3D backward (backward.cu:330-393)
+    if (a.scales) {
+        const float* q = a.rotations + 4 * idx;
+        const float r = q[0], x = q[1], y = q[2], z = q[3];
+        const m3 R = quat_to_R(r, x, y, z);
+        const f3 s = {a.scale_mod * a.scales[3 * idx], a.scale_mod * a.scales[3 * idx + 1], a.scale_mod * a.scales[3 * idx + 2]};
+        m3 S = m3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+        S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
+        const m3 Mm = m3_mul(S, R);
+        const m3 dSig = m3_cols(dcov[0], 0.5f * dcov[1], 0.5f * dcov[2], 0.5f * dcov[1], dcov[3], 0.5f * dcov[4],
+                                0.5f * dcov[2], 0.5f * dcov[4], dcov[5]);
+        m3 dM = m3_mul(Mm, dSig);
+        for (int i = 0; i < 3; i++) for (int jx = 0; jx < 3; jx++) dM.m[i][jx] *= 2.0f;
+        const m3 Rt = m3_T(R);
+        m3 D = m3_T(dM);
+        for (int k = 0; k < 3; k++)
+            a.dscales[3 * idx + k] = fmaf(Rt.m[k][2], D.m[k][2], fmaf(Rt.m[k][1], D.m[k][1], Rt.m[k][0] * D.m[k][0]));
+        for (int jx = 0; jx < 3; jx++) { D.m[0][jx] *= s.x; D.m[1][jx] *= s.y; D.m[2][jx] *= s.z; }
+        float* dq = a.drot + 4 * idx;
+        dq[0] = 2 * z * (D.m[0][1] - D.m[1][0]) + 2 * y * (D.m[2][0] - D.m[0][2]) + 2 * x * (D.m[1][2] - D.m[2][1]);
+        dq[1] = 2 * y * (D.m[1][0] + D.m[0][1]) + 2 * z * (D.m[2][0] + D.m[0][2]) + 2 * r * (D.m[1][2] - D.m[2][1]) - 4 * x * (D.m[2][2] + D.m[1][1]);
+        dq[2] = 2 * x * (D.m[1][0] + D.m[0][1]) + 2 * r * (D.m[2][0] - D.m[0][2]) + 2 * z * (D.m[1][2] + D.m[2][1]) - 4 * y * (D.m[2][2] + D.m[0][0]);
+        dq[3] = 2 * r * (D.m[0][1] - D.m[1][0]) + 2 * x * (D.m[2][0] + D.m[0][2]) + 2 * y * (D.m[1][2] + D.m[2][1]) - 4 * z * (D.m[1][1] + D.m[0][0]);
+    } else {
+        for (int k = 0; k < 3; k++) a.dscales[3 * idx + k] = 0.f;
+        for (int k = 0; k < 4; k++) a.drot[4 * idx + k] = 0.f;
+    }
+}
+
+void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
+    if (a.num_tiles > 0) k_render_bwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
+}
+void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s) {
+    if (a.P > 0) k_gauss_bwd<<<(a.P + 255) / 256, 256, 0, s>>>(a);
+}
+
+}  // namespace gs

@@ -1,0 +1,331 @@
+// sortscan.hip -- device-wide exclusive scan and stable LSD radix sort for gfx950 (wave64).
+//
+// Radix sort: 8-bit digits, reduce-then-scan per pass:
+//   rs_upsweep   one workgroup per 4096-key tile, per-digit counts -> counts[digit][tile]
+//   rs_scan      one workgroup per digit, exclusive scan over tiles, digit totals
+//   rs_downsweep stable rank inside the tile (wave-level peer masks from 8 ballots, each wave owns a
+//                contiguous 1024-key sub-tile so ranking needs no barrier), LDS reorder, coalesced
+//                scatter of contiguous digit runs.
+// Stability is what makes the (tile, depth, index) order of the reference's cub::SortPairs fall out
+// of two cheap sorts (DESIGN.md "Binning").
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "sortscan.h"
+
+namespace gs {
+
+constexpr int RS_THREADS = 256;
+constexpr int RS_WAVES = RS_THREADS / 64;
+constexpr int RS_ITEMS = 16;                       // keys per thread
+constexpr int RS_TILE = RS_THREADS * RS_ITEMS;     // 4096
+constexpr int RS_WAVE_TILE = 64 * RS_ITEMS;        // 1024 contiguous keys per wave
+constexpr int RS_RADIX = 256;
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const int lane = __lane_id();
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// lanes of this wave (among active ones) whose 8-bit digit equals mine
+__device__ __forceinline__ uint64_t peer_mask(uint32_t digit, bool active) {
+    uint64_t m = __ballot(active);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+        const bool bit = (digit >> b) & 1u;
+        const uint64_t bal = __ballot(bit && active);
+        m &= bit ? bal : ~bal;
+    }
+    return active ? m : 0ull;
+}
+
+__global__ void __launch_bounds__(RS_THREADS) rs_upsweep(const uint32_t* __restrict__ keys, uint32_t n, int shift,
+                                                         uint32_t* __restrict__ counts, uint32_t ntiles) {
+    __shared__ uint32_t hist[RS_RADIX];
+    const int t = threadIdx.x;
+    hist[t] = 0;
+    __syncthreads();
+    const uint32_t tile = blockIdx.x;
+    const uint32_t base = tile * RS_TILE;
+    const int lane = __lane_id();
+#pragma unroll 4
+    for (int r = 0; r < RS_ITEMS; r++) {
+        const uint32_t i = base + r * RS_THREADS + t;
+        const bool act = i < n;
+        const uint32_t d = act ? (keys[i] >> shift) & 0xffu : 0u;
+        const uint64_t m = peer_mask(d, act);
+        if (act && (__ffsll((unsigned long long)m) - 1) == lane) atomicAdd(&hist[d], (uint32_t)__popcll(m));
+    }
+    __syncthreads();
+    counts[(size_t)t * ntiles + tile] = hist[t];
+}
+
+// one block per digit: exclusive scan over tiles in place, total -> digit_total[d]
+__global__ void __launch_bounds__(1024) rs_scan(uint32_t* __restrict__ counts, uint32_t ntiles,
+                                                uint32_t* __restrict__ digit_total) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t* row = counts + (size_t)blockIdx.x * ntiles;
+    if (t == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t b = 0; b < ntiles; b += 1024) {
+        const uint32_t i = b + t;
+        const uint32_t v = i < ntiles ? row[i] : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        if (w == 0) {
+            uint32_t s = lane < 16 ? wsum[lane] : 0u;
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                const uint32_t y = __shfl_up(s, o);
+                if (lane >= o) s += y;
+            }
+            if (lane < 16) wsum[lane] = s;
+        }
+        __syncthreads();
+        const uint32_t excl = carry + (w ? wsum[w - 1] : 0u) + x - v;
+        if (i < ntiles) row[i] = excl;
+        __syncthreads();
+        if (t == 1023) carry = excl + v;
+        __syncthreads();
+    }
+    if (t == 0) digit_total[blockIdx.x] = carry;
+}
+
+__global__ void __launch_bounds__(RS_THREADS) rs_downsweep(const uint32_t* __restrict__ keys_in,
+                                                           const uint32_t* __restrict__ vals_in,
+                                                           uint32_t* __restrict__ keys_out,
+                                                           uint32_t* __restrict__ vals_out, uint32_t n, int shift,
+                                                           const uint32_t* __restrict__ counts, uint32_t ntiles,
+                                                           const uint32_t* __restrict__ digit_total) {
+    __shared__ uint32_t s_keys[RS_TILE];
+    __shared__ uint32_t s_vals[RS_TILE];
+    __shared__ uint32_t whist[RS_WAVES][RS_RADIX];
+    __shared__ uint32_t s_tile_start[RS_RADIX];  // tile-local start of each digit run
+    __shared__ uint32_t s_gbase[RS_RADIX];       // global start of this tile's run of each digit
+    __shared__ uint32_t s_wtmp[RS_WAVES];
+
+    const int t = threadIdx.x, lane = __lane_id(), w = t >> 6;
+    const uint32_t tile = blockIdx.x;
+    const uint32_t base = tile * RS_TILE;
+#pragma unroll
+    for (int k = 0; k < RS_WAVES; k++) whist[k][t] = 0;
+    // exclusive scan of digit totals (256) -> global digit base
+    {
+        const uint32_t v = digit_total[t];
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_wtmp[w] = x;
+        __syncthreads();
+        uint32_t off = 0;
+        for (int k = 0; k < w; k++) off += s_wtmp[k];
+        s_gbase[t] = off + x - v + counts[(size_t)t * ntiles + tile];
+    }
+    // per-wave stable ranking over its contiguous 1024-key sub-tile
+    uint32_t my_key[RS_ITEMS], my_val[RS_ITEMS], my_rank[RS_ITEMS];
+    const uint32_t wbase = base + w * RS_WAVE_TILE;
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; r++) {
+        const uint32_t i = wbase + r * 64 + lane;
+        const bool act = i < n;
+        my_key[r] = act ? keys_in[i] : 0xffffffffu;
+        my_val[r] = act ? (vals_in ? vals_in[i] : i) : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; r++) {
+        const uint32_t i = wbase + r * 64 + lane;
+        const bool act = i < n;
+        const uint32_t d = (my_key[r] >> shift) & 0xffu;
+        const uint64_t m = peer_mask(d, act);
+        const uint32_t before = (uint32_t)__popcll(m & lanemask_lt());
+        const uint32_t cur = act ? whist[w][d] : 0u;
+        my_rank[r] = cur + before;
+        // the group's leader publishes the new count; LDS ops of one wave complete in order
+        if (act && before == 0) whist[w][d] = cur + (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    // per digit: offsets of each wave's run, and the tile-local start of the digit run
+    {
+        uint32_t run = 0;
+        uint32_t woff[RS_WAVES];
+#pragma unroll
+        for (int k = 0; k < RS_WAVES; k++) { woff[k] = run; run += whist[k][t]; }
+        // tile-local exclusive scan over digits of `run`
+        uint32_t x = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        __syncthreads();
+        if (lane == 63) s_wtmp[w] = x;
+        __syncthreads();
+        uint32_t off = 0;
+        for (int k = 0; k < w; k++) off += s_wtmp[k];
+        const uint32_t start = off + x - run;
+        s_tile_start[t] = start;
+#pragma unroll
+        for (int k = 0; k < RS_WAVES; k++) whist[k][t] = start + woff[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; r++) {
+        const uint32_t i = wbase + r * 64 + lane;
+        if (i < n) {
+            const uint32_t d = (my_key[r] >> shift) & 0xffu;
+            const uint32_t lp = whist[w][d] + my_rank[r];
+            s_keys[lp] = my_key[r];
+            s_vals[lp] = my_val[r];
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt = (n - base) < (uint32_t)RS_TILE ? (n - base) : (uint32_t)RS_TILE;
+#pragma unroll 4
+    for (int r = 0; r < RS_ITEMS; r++) {
+        const uint32_t j = r * RS_THREADS + t;
+        if (j < cnt) {
+            const uint32_t k = s_keys[j];
+            const uint32_t d = (k >> shift) & 0xffu;
+            const uint32_t o = s_gbase[d] + (j - s_tile_start[d]);
+            keys_out[o] = k;
+            vals_out[o] = s_vals[j];
+        }
+    }
+}
+
+size_t radix_sort_temp_bytes(uint32_t n) {
+    const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
+    return ((size_t)RS_RADIX * (ntiles ? ntiles : 1) + RS_RADIX) * sizeof(uint32_t);
+}
+
+int radix_sort_pairs(uint32_t* keys0, uint32_t* vals0, uint32_t* keys1, uint32_t* vals1, const uint32_t* vals_first,
+                     uint32_t n, int begin_bit, int end_bit, void* temp, hipStream_t stream) {
+    if (n == 0) return 0;
+    const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
+    uint32_t* counts = (uint32_t*)temp;
+    uint32_t* totals = counts + (size_t)RS_RADIX * ntiles;
+    uint32_t *kin = keys0, *vin = vals0, *kout = keys1, *vout = vals1;
+    int pass = 0;
+    for (int b = begin_bit; b < end_bit; b += 8, pass++) {
+        rs_upsweep<<<ntiles, RS_THREADS, 0, stream>>>(kin, n, b, counts, ntiles);
+        rs_scan<<<RS_RADIX, 1024, 0, stream>>>(counts, ntiles, totals);
+        rs_downsweep<<<ntiles, RS_THREADS, 0, stream>>>(kin, pass == 0 ? vals_first : vin, kout, vout, n, b, counts,
+                                                        ntiles, totals);
+        uint32_t* tk = kin; kin = kout; kout = tk;
+        uint32_t* tv = vin; vin = vout; vout = tv;
+    }
+    return pass & 1;  // 1 -> result in keys1/vals1, 0 -> in keys0/vals0
+}
+
+// ---------------- exclusive scan (u32) ----------------
+constexpr int SC_THREADS = 256;
+constexpr int SC_ITEMS = 8;
+constexpr int SC_TILE = SC_THREADS * SC_ITEMS;
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t& total) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < SC_THREADS / 64; k++) { if (k < w) off += s_w[k]; tot += s_w[k]; }
+    __syncthreads();
+    total = tot;
+    return off + x - v;
+}
+
+__global__ void __launch_bounds__(SC_THREADS) sc_reduce(const uint32_t* __restrict__ in,
+                                                        const uint32_t* __restrict__ gather, uint32_t n,
+                                                        uint32_t* __restrict__ block_sums) {
+    __shared__ uint32_t s_w[SC_THREADS / 64];
+    const uint32_t base = blockIdx.x * SC_TILE + threadIdx.x * SC_ITEMS;
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < SC_ITEMS; k++) {
+        const uint32_t i = base + k;
+        if (i < n) s += in[gather ? gather[i] : i];
+    }
+    uint32_t tot;
+    block_excl_scan(s, s_w, tot);
+    if (threadIdx.x == 0) block_sums[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(SC_THREADS) sc_scan_sums(uint32_t* __restrict__ sums, uint32_t nb,
+                                                           uint32_t* __restrict__ total_out) {
+    __shared__ uint32_t s_w[SC_THREADS / 64];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t b = 0; b < nb; b += SC_THREADS) {
+        const uint32_t i = b + threadIdx.x;
+        const uint32_t v = i < nb ? sums[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan(v, s_w, tot);
+        const uint32_t c = carry;
+        if (i < nb) sums[i] = c + ex;
+        __syncthreads();
+        if (threadIdx.x == 0) carry = c + tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && total_out) *total_out = carry;
+}
+
+__global__ void __launch_bounds__(SC_THREADS) sc_downsweep(const uint32_t* __restrict__ in,
+                                                           const uint32_t* __restrict__ gather, uint32_t n,
+                                                           const uint32_t* __restrict__ block_sums,
+                                                           uint32_t* __restrict__ out) {
+    __shared__ uint32_t s_w[SC_THREADS / 64];
+    const uint32_t base = blockIdx.x * SC_TILE + threadIdx.x * SC_ITEMS;
+    uint32_t v[SC_ITEMS];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < SC_ITEMS; k++) {
+        const uint32_t i = base + k;
+        v[k] = i < n ? in[gather ? gather[i] : i] : 0u;
+        s += v[k];
+    }
+    uint32_t tot;
+    uint32_t run = block_sums[blockIdx.x] + block_excl_scan(s, s_w, tot);
+#pragma unroll
+    for (int k = 0; k < SC_ITEMS; k++) {
+        const uint32_t i = base + k;
+        if (i < n) out[i] = run;
+        run += v[k];
+    }
+}
+
+size_t scan_temp_bytes(uint32_t n) {
+    const uint32_t nb = (n + SC_TILE - 1) / SC_TILE;
+    return (size_t)(nb ? nb : 1) * sizeof(uint32_t);
+}
+
+void exclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t n, uint32_t* out, uint32_t* total,
+                    void* temp, hipStream_t stream) {
+    const uint32_t nb = (n + SC_TILE - 1) / SC_TILE;
+    uint32_t* sums = (uint32_t*)temp;
+    if (n == 0) {
+        (void)hipMemsetAsync(total, 0, sizeof(uint32_t), stream);
+        return;
+    }
+    sc_reduce<<<nb, SC_THREADS, 0, stream>>>(in, gather, n, sums);
+    sc_scan_sums<<<1, SC_THREADS, 0, stream>>>(sums, nb, total);
+    sc_downsweep<<<nb, SC_THREADS, 0, stream>>>(in, gather, n, sums, out);
+}
+
+}  // namespace gs

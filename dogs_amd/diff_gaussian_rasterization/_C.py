@@ -1,0 +1,175 @@
+"""The `_C` function table of diff_gaussian_rasterization (reference ext.cpp:15-23), implemented over the
+C ABI of libdogs_hip.so.  Same names, argument order, return tuples and error behaviour as the
+pybind11 functions in rasterize_points.cu; tensors are torch tensors on a HIP device."""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from .. import _lib
+
+_EMPTY_U8 = None
+
+
+def _f32(t: torch.Tensor | None) -> torch.Tensor | None:
+    if t is None or t.numel() == 0:
+        return None
+    return t.contiguous() if t.dtype == torch.float32 else t.float().contiguous()
+
+
+def _args(P, D, M, W, H, bg, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+          viewmatrix, projmatrix, tan_fovx, tan_fovy, dc, sh, campos, prefiltered, antialiasing, debug):
+    a = _lib.DgRasterArgs()
+    a.P, a.D, a.M, a.W, a.H = int(P), int(D), int(M), int(W), int(H)
+    a.prefiltered, a.antialiasing, a.debug = int(bool(prefiltered)), int(bool(antialiasing)), int(bool(debug))
+    a.scale_modifier, a.tanfovx, a.tanfovy = float(scale_modifier), float(tan_fovx), float(tan_fovy)
+    keep = dict(bg=_f32(bg), means3D=_f32(means3D), colors=_f32(colors), opacities=_f32(opacity),
+                scales=_f32(scales), rotations=_f32(rotations), cov3D_precomp=_f32(cov3D_precomp),
+                viewmatrix=_f32(viewmatrix), projmatrix=_f32(projmatrix), dc=_f32(dc), sh=_f32(sh),
+                campos=_f32(campos))
+    for k, v in keep.items():
+        setattr(a, k, _lib.ptr(v))
+    return a, keep
+
+
+def _sh_m(sh: torch.Tensor) -> int:
+    return int(sh.size(1)) if sh is not None and sh.dim() >= 2 and sh.size(0) != 0 else 0
+
+
+def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                        viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, dc, sh, degree,
+                        campos, prefiltered, antialiasing, debug):
+    """RasterizeGaussiansCUDA (rasterize_points.cu:55-154)."""
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    _lib.require_device(means3D, "means3D")
+    dev = means3D.device
+    P, H, W = int(means3D.size(0)), int(image_height), int(image_width)
+    fopt = dict(dtype=torch.float32, device=dev)
+    u8 = dict(dtype=torch.uint8, device=dev)
+    if P == 0:
+        return (0, 0, torch.zeros((3, H, W), **fopt), torch.zeros((1, H, W), **fopt),
+                torch.zeros((0,), dtype=torch.int32, device=dev), torch.empty(0, **u8), torch.empty(0, **u8),
+                torch.empty(0, **u8), torch.empty(0, **u8))
+    M = _sh_m(sh)
+    with torch.cuda.device(dev):
+        out_color = torch.empty((3, H, W), **fopt)
+        out_invdepth = torch.empty((1, H, W), **fopt)
+        radii = torch.empty((P,), dtype=torch.int32, device=dev)
+        a, keep = _args(P, degree, M, W, H, background, means3D, colors, opacity, scales, rotations, scale_modifier,
+                        cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dc, sh, campos, prefiltered,
+                        antialiasing, debug)
+        arena = _lib.TensorArena(dev)
+        gp, bp, ip = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        nr, nk = C.c_int64(0), C.c_int64(0)
+        _lib.check(_lib.load().dg_rasterize_forward(
+            C.byref(a), out_color.data_ptr(), out_invdepth.data_ptr(), radii.data_ptr(), arena.fn, None,
+            C.byref(gp), C.byref(bp), C.byref(ip), C.byref(nr), C.byref(nk), _lib.stream_of(dev)))
+        del keep
+    return (int(nr.value), int(nk.value), out_color, out_invdepth, radii, arena.get(_lib.DG_BUF_GEOM),
+            arena.get(_lib.DG_BUF_BINNING), arena.get(_lib.DG_BUF_IMAGE), torch.empty(0, **u8))
+
+
+def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, scales, rotations, scale_modifier,
+                                 cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, dc, sh,
+                                 dL_dout_invdepth, degree, campos, geomBuffer, R, binningBuffer, imageBuffer, B,
+                                 sampleBuffer, antialiasing, debug):
+    """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:157-252).  B is the instance count the forward
+    returned in the num_buckets slot."""
+    _lib.require_device(means3D, "means3D")
+    dev = means3D.device
+    P = int(means3D.size(0))
+    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    M = _sh_m(sh)
+    fopt = dict(dtype=torch.float32, device=dev)
+    if P == 0:
+        z = lambda *s: torch.zeros(s, **fopt)  # noqa: E731
+        return (z(0, 3), z(0, 3), z(0, 1), z(0, 3), z(0, 6), z(0, 1, 3), z(0, M, 3), z(0, 3), z(0, 4), z(0, 1))
+    with torch.cuda.device(dev):
+        dmeans2D = torch.empty((P, 3), **fopt)
+        dcolors = torch.empty((P, 3), **fopt)
+        dopacity = torch.empty((P, 1), **fopt)
+        dmeans3D = torch.empty((P, 3), **fopt)
+        dcov3D = torch.empty((P, 6), **fopt)
+        ddc = torch.empty((P, 1, 3), **fopt)
+        dsh = torch.empty((P, M, 3), **fopt)
+        dscales = torch.empty((P, 3), **fopt)
+        drot = torch.empty((P, 4), **fopt)
+        depth = torch.empty((P, 1), **fopt)
+        a, keep = _args(P, degree, M, W, H, background, means3D, colors, opacities, scales, rotations, scale_modifier,
+                        cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dc, sh, campos, False,
+                        antialiasing, debug)
+        gc = _f32(dL_dout_color)
+        gi = _f32(dL_dout_invdepth) if dL_dout_invdepth is not None else None
+        radii_c = radii.contiguous()
+        arena = _lib.TensorArena(dev)
+        _lib.check(_lib.load().dg_rasterize_backward(
+            C.byref(a), radii_c.data_ptr(), geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
+            int(R), int(B), gc.data_ptr(), _lib.ptr(gi), dmeans2D.data_ptr(), dcolors.data_ptr(),
+            dopacity.data_ptr(), dmeans3D.data_ptr(), dcov3D.data_ptr(), ddc.data_ptr(), _lib.ptr(dsh),
+            dscales.data_ptr(), drot.data_ptr(), depth.data_ptr(), arena.fn, None, _lib.stream_of(dev)))
+        del keep
+    return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, ddc, dsh, dscales, drot, depth
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    """markVisible (rasterize_points.cu:254-273)."""
+    _lib.require_device(means3D, "means3D")
+    P = int(means3D.size(0))
+    present = torch.zeros((P,), dtype=torch.bool, device=means3D.device)
+    if P:
+        m, v, p = _f32(means3D), _f32(viewmatrix), _f32(projmatrix)
+        with torch.cuda.device(means3D.device):
+            _lib.check(_lib.load().dg_mark_visible(P, m.data_ptr(), v.data_ptr(), p.data_ptr(), present.data_ptr(),
+                                                   _lib.stream_of(means3D.device)))
+    return present
+
+
+def rasterize_gaussians_filter(means3D, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
+                               tan_fovx, tan_fovy, image_height, image_width, prefiltered, debug):
+    """RasterizeGaussiansFilterCUDA (rasterize_points.cu:276-334)."""
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    _lib.require_device(means3D, "means3D")
+    dev = means3D.device
+    P = int(means3D.size(0))
+    radii = torch.zeros((P,), dtype=torch.int32, device=dev)
+    if P:
+        a, keep = _args(P, 0, 0, image_width, image_height, None, means3D, None, None, scales, rotations,
+                        scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, None, None, None,
+                        prefiltered, False, debug)
+        with torch.cuda.device(dev):
+            _lib.check(_lib.load().dg_rasterize_filter(C.byref(a), radii.data_ptr(), _lib.stream_of(dev)))
+        del keep
+    return radii
+
+
+def adamUpdate(param, param_grad, exp_avg, exp_avg_sq, visible, lr, b1, b2, eps, N, M):  # noqa: N802
+    """adamUpdate (rasterize_points.cu:336-361): in place on param / exp_avg / exp_avg_sq."""
+    for t, n in ((param, "param"), (param_grad, "param_grad"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
+        _lib.require_device(t, n)
+        if not t.is_contiguous() or t.dtype != torch.float32:
+            raise RuntimeError(f"{n} must be a contiguous float32 tensor (updated in place)")
+    vis = visible.contiguous()
+    if vis.dtype != torch.bool:
+        vis = vis.bool()
+    with torch.cuda.device(param.device):
+        _lib.check(_lib.load().dg_adam_update(param.data_ptr(), param_grad.data_ptr(), exp_avg.data_ptr(),
+                                              exp_avg_sq.data_ptr(), vis.data_ptr(), float(lr), float(b1), float(b2),
+                                              float(eps), int(N), int(M), _lib.stream_of(param.device)))
+
+
+def fusedssim(C1, C2, img1, img2):
+    """conv.cu fusedssim (exported by the reference _C, unused by conerf): img [3,H,W] -> SSIM map."""
+    from ..fused_ssim import _cuda
+    m = _cuda.fusedssim(C1, C2, img1.unsqueeze(0), img2.unsqueeze(0), False)[0]
+    return m[0]
+
+
+def fusedssim_backward(C1, C2, img1, img2, dL_dmap):
+    """conv.cu fusedssim_backward: recomputes the partial maps, then the fused backward."""
+    from ..fused_ssim import _cuda
+    a, b = img1.unsqueeze(0), img2.unsqueeze(0)
+    _, d1, d2, d3 = _cuda.fusedssim(C1, C2, a, b, True)
+    return _cuda.fusedssim_backward(C1, C2, a, b, dL_dmap.unsqueeze(0), d1, d2, d3)[0]

@@ -1,0 +1,174 @@
+"""Drop-in `diff_gaussian_rasterization` for MI355X.
+
+Mirrors the Python surface of the reference binding
+(submodules/diff-gaussian-rasterization/diff_gaussian_rasterization/__init__.py):
+  GaussianRasterizationSettings (:203-217), GaussianRasterizer (:220-300) with markVisible /
+  visible_filter, rasterize_gaussians / _RasterizeGaussians (:25-200, incl. the depth_threshold
+  scaling of grad_means2D at :171-185) and SparseGaussianAdam (:303-332).
+The numerical work runs in libdogs_hip.so (gfx950 HIP kernels) through the `_C` table.
+"""
+from __future__ import annotations
+
+from typing import NamedTuple
+
+import torch
+import torch.nn as nn
+
+from . import _C
+
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "SparseGaussianAdam", "rasterize_gaussians", "_C"]
+
+
+def cpu_deep_copy_tuple(input_tuple):
+    return tuple(item.cpu().clone() if isinstance(item, torch.Tensor) else item for item in input_tuple)
+
+
+def rasterize_gaussians(means3D, means2D, dc, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                        raster_settings):
+    return _RasterizeGaussians.apply(means3D, means2D, dc, sh, colors_precomp, opacities, scales, rotations,
+                                     cov3Ds_precomp, raster_settings)
+
+
+class _RasterizeGaussians(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, dc, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                raster_settings):
+        rs = raster_settings
+        args = (rs.bg, means3D, colors_precomp, opacities, scales, rotations, rs.scale_modifier, cov3Ds_precomp,
+                rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, dc, sh,
+                rs.sh_degree, rs.campos, rs.prefiltered, rs.antialiasing, rs.debug)
+        if rs.debug:
+            cpu_args = cpu_deep_copy_tuple(args)
+            try:
+                out = _C.rasterize_gaussians(*args)
+            except Exception as ex:
+                torch.save(cpu_args, "snapshot_fw.dump")
+                print("\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.")
+                raise ex
+        else:
+            out = _C.rasterize_gaussians(*args)
+        num_rendered, num_buckets, color, invdepths, radii, geomBuffer, binningBuffer, imgBuffer, sampleBuffer = out
+        ctx.raster_settings = rs
+        ctx.num_rendered = num_rendered
+        ctx.num_buckets = num_buckets
+        ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, dc, sh, opacities,
+                              geomBuffer, binningBuffer, imgBuffer, sampleBuffer)
+        ctx.mark_non_differentiable(radii)
+        return color, radii, invdepths
+
+    @staticmethod
+    def backward(ctx, grad_out_color, _, grad_out_depth):
+        rs = ctx.raster_settings
+        (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, dc, sh, opacities, geomBuffer,
+         binningBuffer, imgBuffer, sampleBuffer) = ctx.saved_tensors
+        args = (rs.bg, means3D, radii, colors_precomp, opacities, scales, rotations, rs.scale_modifier,
+                cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, dc, sh,
+                grad_out_depth, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer,
+                ctx.num_buckets, sampleBuffer, rs.antialiasing, rs.debug)
+        if rs.debug:
+            cpu_args = cpu_deep_copy_tuple(args)
+            try:
+                g = _C.rasterize_gaussians_backward(*args)
+            except Exception as ex:
+                torch.save(cpu_args, "snapshot_bw.dump")
+                print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
+                raise ex
+        else:
+            g = _C.rasterize_gaussians_backward(*args)
+        (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_dc, grad_sh,
+         grad_scales, grad_rotations, depth) = g
+
+        depth_threshold = getattr(rs, "depth_threshold", 0.0) or 0.0
+        if depth_threshold > 0:
+            scaling = torch.minimum(torch.ones_like(depth), (depth / depth_threshold) ** 2)
+            grad_means2D = grad_means2D * scaling.expand_as(grad_means2D)
+
+        return (grad_means3D, grad_means2D, grad_dc, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
+                grad_rotations, grad_cov3Ds_precomp, None)
+
+
+class GaussianRasterizationSettings(NamedTuple):
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: torch.Tensor
+    scale_modifier: float
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    sh_degree: int
+    campos: torch.Tensor
+    prefiltered: bool
+    debug: bool
+    antialiasing: bool
+    depth_threshold: float
+
+
+def _empty_like_device(ref: torch.Tensor) -> torch.Tensor:
+    return torch.empty(0, dtype=torch.float32, device=ref.device)
+
+
+class GaussianRasterizer(nn.Module):
+    def __init__(self, raster_settings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisible(self, positions):  # noqa: N802
+        with torch.no_grad():
+            rs = self.raster_settings
+            return _C.mark_visible(positions, rs.viewmatrix, rs.projmatrix)
+
+    def forward(self, means3D, means2D, opacities, dc=None, shs=None, colors_precomp=None, scales=None,
+                rotations=None, cov3D_precomp=None):
+        rs = self.raster_settings
+        if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
+            raise Exception("Please provide excatly one of either SHs or precomputed colors!")
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or (
+                (scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!")
+        # extension: full SH features [N,(D+1)^2,3] without a separate dc (the reference requires dc)
+        if shs is not None and (dc is None or dc.numel() == 0) and shs.dim() == 3 and shs.size(1) >= 1:
+            dc, shs = shs[:, :1, :], shs[:, 1:, :]
+        e = _empty_like_device(means3D)
+        dc = e if dc is None else dc
+        shs = e if shs is None else shs
+        colors_precomp = e if colors_precomp is None else colors_precomp
+        scales = e if scales is None else scales
+        rotations = e if rotations is None else rotations
+        cov3D_precomp = e if cov3D_precomp is None else cov3D_precomp
+        return rasterize_gaussians(means3D, means2D, dc, shs, colors_precomp, opacities, scales, rotations,
+                                   cov3D_precomp, rs)
+
+    def visible_filter(self, means3D, scales=None, rotations=None, cov3D_precomp=None):
+        rs = self.raster_settings
+        e = _empty_like_device(means3D)
+        with torch.no_grad():
+            return _C.rasterize_gaussians_filter(
+                means3D, e if scales is None else scales, e if rotations is None else rotations, rs.scale_modifier,
+                e if cov3D_precomp is None else cov3D_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy,
+                rs.image_height, rs.image_width, rs.prefiltered, rs.debug)
+
+
+class SparseGaussianAdam(torch.optim.Adam):
+    """Adam restricted to visible Gaussians (adam.cu): b1/b2 fixed at 0.9/0.999, no bias correction."""
+
+    def __init__(self, params, lr, eps):
+        super().__init__(params=params, lr=lr, eps=eps)
+
+    @torch.no_grad()
+    def step(self, visibility, N):
+        for group in self.param_groups:
+            lr = group["lr"]
+            eps = group["eps"]
+            assert len(group["params"]) == 1, "more than one tensor in group"
+            param = group["params"][0]
+            if param.grad is None:
+                continue
+            state = self.state[param]
+            if len(state) == 0:
+                state["step"] = torch.tensor(0.0, dtype=torch.float32)
+                state["exp_avg"] = torch.zeros_like(param, memory_format=torch.preserve_format)
+                state["exp_avg_sq"] = torch.zeros_like(param, memory_format=torch.preserve_format)
+            M = param.numel() // N
+            grad = param.grad if param.grad.is_contiguous() else param.grad.contiguous()
+            _C.adamUpdate(param, grad, state["exp_avg"], state["exp_avg_sq"], visibility, lr, 0.9, 0.999, eps, N, M)

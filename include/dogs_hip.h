@@ -1,0 +1,130 @@
+/*
+ * dogs_hip.h -- C ABI of libdogs_hip.so, the MI355X (gfx950) implementation of the DOGS hot path:
+ * the Taming-3DGS differentiable tile rasterizer, fused SSIM, sparse Adam and simple-knn.
+ *
+ * Every entry point replaces one function of the reference's pybind11 tables; the binding stub a
+ * maintainer adds on the reference side is in INTEGRATION.md.  Conventions:
+ *   - all pointers are device pointers (HBM) unless noted, fp32 row-major exactly as the torch tensors
+ *     the reference passes (rasterize_points.cu:127-147), NULL = "empty tensor" (absent);
+ *   - `stream` is a hipStream_t (the caller's current stream); nothing runs on the null stream;
+ *   - return 0 on success, non-zero on error; dg_last_error() gives the message (thread-local);
+ *   - scratch memory comes from the caller through dg_alloc_fn, like the reference's
+ *     std::function<char*(size_t)> resize callbacks (rasterize_points.cu:30-52).  The forward's
+ *     geometry/binning/image blocks are private state the caller hands back to the backward.
+ */
+#ifndef DOGS_HIP_H
+#define DOGS_HIP_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* dg_stream_t; /* hipStream_t */
+
+/* which: DG_BUF_* below.  Must return a device pointer aligned to >= 256 bytes, or NULL. */
+typedef void* (*dg_alloc_fn)(void* user, int which, uint64_t nbytes);
+enum { DG_BUF_GEOM = 0, DG_BUF_BINNING = 1, DG_BUF_IMAGE = 2, DG_BUF_BACKWARD = 3, DG_BUF_TEMP = 4 };
+
+/* The scalar + tensor arguments of _C.rasterize_gaussians (rasterize_points.h:18-40). */
+typedef struct {
+    int P;              /* means3D.size(0) */
+    int D;              /* sh degree (raster_settings.sh_degree) */
+    int M;              /* sh.size(1) (0 when sh is absent) */
+    int W, H;           /* image_width, image_height */
+    int prefiltered, antialiasing, debug;
+    float scale_modifier, tanfovx, tanfovy;
+    const float* bg;            /* [3] */
+    const float* means3D;       /* [P,3] */
+    const float* colors;        /* [P,3] or NULL (colors_precomp) */
+    const float* opacities;     /* [P,1] */
+    const float* scales;        /* [P,3] or NULL */
+    const float* rotations;     /* [P,4] or NULL */
+    const float* cov3D_precomp; /* [P,6] or NULL */
+    const float* viewmatrix;    /* [4,4] = world_to_camera^T */
+    const float* projmatrix;    /* [4,4] = world_to_camera^T @ P^T */
+    const float* dc;            /* [P,1,3] */
+    const float* sh;            /* [P,M,3] or NULL */
+    const float* campos;        /* [3] */
+} dg_raster_args;
+
+/* Replaces RasterizeGaussiansCUDA (rasterize_points.cu:55-154) / _C.rasterize_gaussians.
+ * Outputs out_color [3,H,W], out_invdepth [1,H,W], radii [P] (int32).
+ * *num_rendered = the reference's num_rendered (sum of tile-rect areas);
+ * *num_instances = precise-culled (tile, Gaussian) instances (returned where the reference returns
+ * num_buckets; both are opaque tokens handed back to the backward).
+ * Allocates DG_BUF_GEOM, DG_BUF_IMAGE, DG_BUF_BINNING through `alloc`; the caller keeps the three
+ * pointers (in the order requested) and passes them to dg_rasterize_backward.  One host sync. */
+int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_invdepth, int* radii,
+                         dg_alloc_fn alloc, void* user, void** geom, void** binning, void** image,
+                         int64_t* num_rendered, int64_t* num_instances, dg_stream_t stream);
+
+/* Replaces RasterizeGaussiansBackwardCUDA (rasterize_points.cu:157-252).  Every output is fully
+ * written (no zero-fill needed): dmeans2D [P,3], dcolors [P,3], dopacity [P,1], dmeans3D [P,3],
+ * dcov3D [P,6], ddc [P,1,3], dsh [P,M,3] (may be NULL when M == 0), dscales [P,3], drot [P,4],
+ * depth [P,1].  dL_dout_invdepth may be NULL (treated as zeros).  Allocates DG_BUF_BACKWARD. */
+int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void* geom, const void* binning,
+                          const void* image, int64_t num_rendered, int64_t num_instances,
+                          const float* dL_dout_color, const float* dL_dout_invdepth, float* dmeans2D,
+                          float* dcolors, float* dopacity, float* dmeans3D, float* dcov3D, float* ddc,
+                          float* dsh, float* dscales, float* drot, float* depth, dg_alloc_fn alloc, void* user,
+                          dg_stream_t stream);
+
+/* Replaces markVisible (rasterize_points.cu:254-273) / _C.mark_visible: present [P] bool. */
+int dg_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                    uint8_t* present, dg_stream_t stream);
+
+/* Replaces RasterizeGaussiansFilterCUDA (rasterize_points.cu:276-334) / _C.rasterize_gaussians_filter:
+ * radii [P] only (no low-pass filter), uses P, W, H, tanfov*, scale_modifier, means3D, scales,
+ * rotations, cov3D_precomp, viewmatrix, projmatrix, prefiltered of `a`. */
+int dg_rasterize_filter(const dg_raster_args* a, int* radii, dg_stream_t stream);
+
+/* Replaces adamUpdate (rasterize_points.cu:336-361, adam.cu:10-38) / _C.adamUpdate, in place. */
+int dg_adam_update(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const uint8_t* visible,
+                   float lr, float b1, float b2, float eps, uint32_t N, uint32_t M, dg_stream_t stream);
+
+/* Replaces fusedssim (fused-ssim/ssim.cu:368-404) / fused_ssim_cuda.fusedssim: img [B,CH,H,W];
+ * dm_dmu1/dm_dsigma1_sq/dm_dsigma12 NULL <=> train == false. */
+int dg_fused_ssim_forward(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,
+                          float* ssim_map, float* dm_dmu1, float* dm_dsigma1_sq, float* dm_dsigma12,
+                          dg_stream_t stream);
+
+/* Replaces fusedssim_backward (fused-ssim/ssim.cu:406-444). */
+int dg_fused_ssim_backward(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,
+                           const float* dL_dmap, const float* dm_dmu1, const float* dm_dsigma1_sq,
+                           const float* dm_dsigma12, float* dL_dimg1, dg_stream_t stream);
+
+/* Replaces distCUDA2 (simple-knn/spatial.cu:18-35): mean squared distance to the 3 nearest
+ * neighbours (approximate, Morton boxes).  out [P].  Allocates DG_BUF_TEMP. */
+int dg_dist_cuda2(int P, const float* points, float* out, dg_alloc_fn alloc, void* user, dg_stream_t stream);
+
+/* Bytes of each private state block for P Gaussians / W x H image / K instances (introspection). */
+uint64_t dg_geom_bytes(int P);
+uint64_t dg_image_bytes(int W, int H);
+uint64_t dg_binning_bytes(int64_t K, int W, int H);
+
+/* Introspection of the private forward state, for parity tests (device output pointers, async on stream):
+ * the sorted (tile, Gaussian) instance list, per-Gaussian geometry, per-pixel/per-tile image state. */
+int dg_debug_sorted_instances(const void* binning, int64_t K, int W, int H, uint32_t* tiles_out,
+                              uint32_t* gauss_out, dg_stream_t stream);
+int dg_debug_geometry(const void* geom, int P, float* means2D, float* conic_opacity, float* rgb_invdepth,
+                      uint32_t* tile_count, dg_stream_t stream);
+int dg_debug_image_state(const void* image, int W, int H, float* final_T, uint32_t* n_contrib,
+                         uint32_t* max_contrib, uint32_t* ranges, dg_stream_t stream);
+
+/* Device primitives used by the rasterizer, exported for tests: stable LSD radix sort of (key, value)
+ * pairs over bits [begin_bit, end_bit) in place, and an exclusive scan (total -> *total, device). */
+int dg_sort_pairs_u32(uint32_t* keys, uint32_t* vals, uint32_t n, int begin_bit, int end_bit, dg_alloc_fn alloc,
+                      void* user, dg_stream_t stream);
+int dg_exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* total, dg_alloc_fn alloc,
+                          void* user, dg_stream_t stream);
+
+const char* dg_last_error(void);
+int dg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DOGS_HIP_H */
