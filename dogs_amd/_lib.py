@@ -36,6 +36,7 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_mark_visible", "
            "dg_adam_update", "dg_fused_ssim_forward", "dg_fused_ssim_backward", "dg_dist_cuda2",
            "dg_geom_bytes", "dg_image_bytes", "dg_binning_bytes", "dg_debug_sorted_instances",
            "dg_debug_geometry", "dg_debug_image_state", "dg_sort_pairs_u32", "dg_exclusive_scan_u32",
+           "dg_profile_enable", "dg_profile_collect",
            "dg_last_error", "dg_version")
 
 _lib = None
@@ -89,6 +90,10 @@ def load(path: str | None = None):
         L.dg_sort_pairs_u32.argtypes = [vp, vp, C.c_uint32, C.c_int, C.c_int, ALLOC_FN, vp, vp]
         L.dg_exclusive_scan_u32.restype = C.c_int
         L.dg_exclusive_scan_u32.argtypes = [vp, vp, C.c_uint32, vp, ALLOC_FN, vp, vp]
+        L.dg_profile_enable.restype = None
+        L.dg_profile_enable.argtypes = [C.c_int]
+        L.dg_profile_collect.restype = C.c_int
+        L.dg_profile_collect.argtypes = [C.c_char_p, C.c_int]
         L.dg_last_error.restype = C.c_char_p
         L.dg_last_error.argtypes = []
         L.dg_version.restype = C.c_int
@@ -138,3 +143,21 @@ class TensorArena:
 
     def get(self, which: int) -> torch.Tensor:
         return self.buffers.get(which, torch.empty(0, dtype=torch.uint8, device=self.device))
+
+
+def profile_enable(on: bool = True) -> None:
+    load().dg_profile_enable(1 if on else 0)
+
+
+def profile_collect() -> dict[str, tuple[float, int]]:
+    """{phase: (total_ms, launches)} recorded since the last collect (synchronises the recorded events)."""
+    L = load()
+    buf = C.create_string_buffer(8192)
+    L.dg_profile_collect(buf, 8192)
+    out = {}
+    for item in buf.value.decode().split(";"):
+        if "=" in item:
+            k, v = item.split("=")
+            ms, cnt = v.split("/")
+            out[k] = (float(ms), int(cnt))
+    return out

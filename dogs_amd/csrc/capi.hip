@@ -6,6 +6,8 @@
 #include <stdio.h>
 #include <string.h>
 #include <string>
+#include <vector>
+#include <map>
 
 #include "../../include/dogs_hip.h"
 #include "aux_kernels.h"
@@ -36,6 +38,31 @@ int fail(const char* fmt, const char* a = "", int b = 0) {
             HIP_OK(hipGetLastError());                                           \
         }                                                                        \
     } while (0)
+
+// ---- optional per-kernel event profiling (dg_profile_*): brackets each launch with hipEvents on the
+// caller's stream; used by bench.py for the live roofline figure.  Off by default (no events recorded).
+struct ProfRec { const char* name; hipEvent_t a, b; };
+bool g_prof = false;
+std::vector<ProfRec> g_prof_recs;
+std::vector<hipEvent_t> g_ev_pool;
+hipEvent_t prof_event() {
+    if (!g_ev_pool.empty()) { hipEvent_t e = g_ev_pool.back(); g_ev_pool.pop_back(); return e; }
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+}
+struct ProfScope {
+    ProfRec r;
+    hipStream_t s;
+    bool on;
+    ProfScope(const char* name, hipStream_t st) : s(st), on(g_prof) {
+        if (on) { r.name = name; r.a = prof_event(); r.b = prof_event(); (void)hipEventRecord(r.a, s); }
+    }
+    ~ProfScope() {
+        if (on) { (void)hipEventRecord(r.b, s); g_prof_recs.push_back(r); }
+    }
+};
+#define PROF(name) ProfScope _prof_scope_##__LINE__(name, s)
 
 constexpr size_t ALIGN = 256;
 inline size_t al(size_t x) { return (x + ALIGN - 1) & ~(ALIGN - 1); }
@@ -134,6 +161,7 @@ Binning carve_binning(void* base, int64_t K) {
 struct BwdScratch {
     uint8_t* flag;
     float* rec;
+    uint32_t* invd_flag;
     size_t bytes;
 };
 BwdScratch carve_bwd(void* base, int64_t K) {
@@ -142,6 +170,7 @@ BwdScratch carve_bwd(void* base, int64_t K) {
     const size_t n = (size_t)(K > 0 ? K : 1);
     s.flag = c.take<uint8_t>(n);
     s.rec = c.take<float>(12 * n);
+    s.invd_flag = c.take<uint32_t>(4);
     s.bytes = c.off;
     return s;
 }
@@ -178,6 +207,35 @@ int check_args(const dg_raster_args* a) {
 extern "C" {
 
 const char* dg_last_error(void) { return g_err.c_str(); }
+
+void dg_profile_enable(int on) { g_prof = on != 0; }
+
+int dg_profile_collect(char* buf, int buflen) {
+    // sums per name over everything recorded since the last collect; "name=ms;name=ms;..." (synchronises)
+    std::map<std::string, std::pair<double, int>> acc;
+    for (auto& r : g_prof_recs) {
+        HIP_OK(hipEventSynchronize(r.b));
+        float ms = 0.f;
+        HIP_OK(hipEventElapsedTime(&ms, r.a, r.b));
+        auto& e = acc[r.name];
+        e.first += ms;
+        e.second += 1;
+        g_ev_pool.push_back(r.a);
+        g_ev_pool.push_back(r.b);
+    }
+    g_prof_recs.clear();
+    std::string out;
+    char tmp[128];
+    for (auto& kv : acc) {
+        snprintf(tmp, sizeof(tmp), "%s=%.6f/%d;", kv.first.c_str(), kv.second.first, kv.second.second);
+        out += tmp;
+    }
+    if (buf && buflen > 0) {
+        strncpy(buf, out.c_str(), (size_t)buflen - 1);
+        buf[buflen - 1] = 0;
+    }
+    return (int)out.size();
+}
 
 int dg_sort_pairs_u32(uint32_t* keys, uint32_t* vals, uint32_t n, int begin_bit, int end_bit, dg_alloc_fn alloc,
                       void* user, dg_stream_t stream) {
@@ -242,16 +300,17 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     fill_pre(pre, a);
     pre.radii = radii; pre.xy = g.xy; pre.co = g.co; pre.rgbi = g.rgbi; pre.depthkey = g.k0; pre.cnt = g.cnt;
     pre.rect_sum = (unsigned long long*)(g.counters + 2); pre.err = g.counters + 1;
-    gs::launch_preprocess(pre, s);
+    { PROF("preprocess"); gs::launch_preprocess(pre, s); }
     DBG_SYNC(a->debug, s);
 
     // stable depth sort of (depth bits, index): 4 passes -> result back in k0/v0
     const uint32_t* order = g.v0;
     if (P > 0) {
-        const int which = gs::radix_sort_pairs(g.k0, g.v0, g.k1, g.v1, nullptr, (uint32_t)P, 0, 32, g.sort_tmp, s);
+        int which;
+        { PROF("depth_sort"); which = gs::radix_sort_pairs(g.k0, g.v0, g.k1, g.v1, nullptr, (uint32_t)P, 0, 32, g.sort_tmp, s); }
         order = which ? g.v1 : g.v0;
         DBG_SYNC(a->debug, s);
-        gs::exclusive_scan(g.cnt, order, (uint32_t)P, g.off, g.counters, g.scan_tmp, s);
+        { PROF("count_scan"); gs::exclusive_scan(g.cnt, order, (uint32_t)P, g.off, g.counters, g.scan_tmp, s); }
         DBG_SYNC(a->debug, s);
     }
     uint32_t hc[4] = {0, 0, 0, 0};
@@ -271,16 +330,20 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     const uint32_t* s_e = b.se0;
     const uint32_t* s_keys = b.tk0;
     if (K > 0) {
-        gs::launch_emit(P, order, g.cnt, g.off, g.xy, g.co, radii, tx, ty, g.first_e, b.tk0, b.eg, s);
+        { PROF("emit"); gs::launch_emit(P, order, g.cnt, g.off, g.xy, g.co, radii, tx, ty, g.first_e, b.tk0, b.eg, s); }
         DBG_SYNC(a->debug, s);
-        const int which = gs::radix_sort_pairs(b.tk0, b.se0, b.tk1, b.se1, nullptr, (uint32_t)K, 0, bits_for((uint32_t)T),
-                                               b.sort_tmp, s);
+        int which;
+        { PROF("tile_sort"); which = gs::radix_sort_pairs(b.tk0, b.se0, b.tk1, b.se1, nullptr, (uint32_t)K, 0,
+                                                          bits_for((uint32_t)T), b.sort_tmp, s); }
         s_e = which ? b.se1 : b.se0;
         s_keys = which ? b.tk1 : b.tk0;
         DBG_SYNC(a->debug, s);
     }
-    HIP_OK(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * (size_t)T, s));
-    gs::launch_ranges((uint32_t)K, s_keys, im.ranges, (uint32_t)T, s);
+    {
+        PROF("ranges");
+        HIP_OK(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * (size_t)T, s));
+        gs::launch_ranges((uint32_t)K, s_keys, im.ranges, (uint32_t)T, s);
+    }
     DBG_SYNC(a->debug, s);
 
     gs::RenderArgs r;
@@ -289,7 +352,7 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     r.ranges = im.ranges; r.s_e = s_e; r.eg = b.eg; r.xy = g.xy; r.co = g.co; r.rgbi = g.rgbi; r.bg = a->bg;
     r.out_color = out_color; r.out_invd = out_invdepth; r.final_T = im.final_T; r.img_color = im.img_color;
     r.img_invd = im.img_invd; r.n_contrib = im.n_contrib; r.max_contrib = im.max_contrib;
-    gs::launch_render_fwd(r, s);
+    { PROF("render_fwd"); gs::launch_render_fwd(r, s); }
     DBG_SYNC(a->debug, s);
     HIP_OK(hipGetLastError());
     return 0;
@@ -317,7 +380,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     if (!sbase) return fail("backward scratch allocation failed%s%d");
     BwdScratch sc = carve_bwd(sbase, K);
     if (K > 0) {
-        HIP_OK(hipMemsetAsync(sc.flag, 0, (size_t)K, s));
+        { PROF("flag_clear"); HIP_OK(hipMemsetAsync(sc.flag, 0, (size_t)K, s)); }
         gs::RenderBwdArgs r;
         r.W = W; r.H = H; r.tiles_x = tx; r.num_tiles = T;
         r.K = (uint32_t)K; r.P = (uint32_t)P;
@@ -325,7 +388,8 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
         r.xy = g.xy; r.co = g.co; r.rgbi = g.rgbi; r.bg = a->bg;
         r.final_T = im.final_T; r.img_color = im.img_color; r.img_invd = im.img_invd; r.n_contrib = im.n_contrib;
         r.dL_dpix = dL_dout_color; r.dL_dinvd = dL_dout_invdepth; r.rec = sc.rec; r.flag = sc.flag;
-        gs::launch_render_bwd(r, s);
+        r.invd_nonzero = nullptr;
+        { PROF("render_bwd"); gs::launch_render_bwd(r, sc.invd_flag, s); }
         DBG_SYNC(a->debug, s);
     }
     gs::GaussBwdArgs q;
@@ -343,7 +407,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     q.dmeans2D = dmeans2D; q.dcolors = dcolors; q.dopacity = dopacity; q.dmeans3D = dmeans3D; q.dcov3D = dcov3D;
     q.ddc = ddc; q.dsh = dsh; q.dscales = dscales; q.drot = drot; q.depth = depth;
     if (q.M > 0 && !dsh) return fail("dsh output required when M > 0%s%d");
-    gs::launch_gauss_bwd(q, s);
+    { PROF("gauss_bwd"); gs::launch_gauss_bwd(q, s); }
     DBG_SYNC(a->debug, s);
     HIP_OK(hipGetLastError());
     return 0;

@@ -109,7 +109,8 @@ __device__ __forceinline__ void get_rect(float px, float py, int r, int gx, int 
     a = f2i((((py + (float)r) + (float)GS_TILE_Y) - 1.0f) / (float)GS_TILE_Y); a = a > 0 ? a : 0; y1 = a < gy ? a : gy;
 }
 
-// max_contrib_power_rect_gaussian_float<15,15> (rasterizer_impl.cu:52-100)
+// max_contrib_power_rect_gaussian_float<PATCH,PATCH> (rasterizer_impl.cu:52-100); PATCH = rect size - 1
+template <int PATCH = 15>
 __device__ __forceinline__ float max_contrib_power(f4 co, float mx, float my, float rminx, float rminy, float rmaxx,
                                                    float rmaxy) {
     const float x_min_diff = rminx - mx;
@@ -122,11 +123,11 @@ __device__ __forceinline__ float max_contrib_power(f4 co, float mx, float my, fl
     if ((not_in_y + not_in_x) > 0.0f) {
         const float px = x_left > 0.0f ? rminx : rmaxx;
         const float py = y_above > 0.0f ? rminy : rmaxy;
-        const float dx = copysignf(15.0f, x_min_diff);
-        const float dy = copysignf(15.0f, y_min_diff);
+        const float dx = copysignf((float)PATCH, x_min_diff);
+        const float dy = copysignf((float)PATCH, y_min_diff);
         const float diffx = mx - px, diffy = my - py;
-        const float rcx = 1.0f / (225.0f * co.x);
-        const float rcz = 1.0f / (225.0f * co.z);
+        const float rcx = 1.0f / ((float)(PATCH * PATCH) * co.x);
+        const float rcz = 1.0f / ((float)(PATCH * PATCH) * co.z);
         float ax = fmaf(dx * co.y, diffy, (dx * co.x) * diffx) * rcx;
         float ay = fmaf(dy * co.z, diffy, (dy * co.y) * diffx) * rcz;
         ax = (ax != ax) ? 0.0f : fminf(fmaxf(ax, 0.0f), 1.0f);
@@ -178,6 +179,22 @@ __device__ __forceinline__ f3 cov2d_fwd(f3 mean, float fx, float fy, float tfx, 
         st->ygm = (tytz < -limy || tytz > limy) ? 0.f : 1.f;
     }
     return {cov.m[0][0], cov.m[0][1], cov.m[1][1]};
+}
+
+constexpr float LOG2E = 1.4426950408889634f;
+// Quadrant refinement of the precise tile cull: an 8x8 quadrant whose best point is below the opacity
+// threshold holds no pixel with alpha >= 1/255.  The margin (in log units) keeps the skip conservative
+// against rounding of both the rect test and the per-pixel exponent.
+constexpr float QUAD_MARGIN = 0.01f;
+__device__ __forceinline__ uint32_t quad_mask(f4 co, float mx, float my, float thr, int tx0, int ty0) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const float x0 = (float)(tx0 + (q & 1) * 8), y0 = (float)(ty0 + (q >> 1) * 8);
+        const float p = max_contrib_power<7>(co, mx, my, x0, y0, x0 + 7.0f, y0 + 7.0f);
+        m |= (p <= thr + QUAD_MARGIN) ? (1u << q) : 0u;
+    }
+    return m;
 }
 
 // compositing exponent, identical expression in forward and backward (forward.cu:451, backward.cu:596)

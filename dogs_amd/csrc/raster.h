@@ -52,6 +52,7 @@ struct RenderBwdArgs {
     const float* dL_dinvd;   // may be null
     float* rec;              // [K][12] per-instance gradient record
     uint8_t* flag;           // [K] record written
+    const uint32_t* invd_nonzero;  // device flag: any(dL_dinvd != 0)
 };
 
 struct GaussBwdArgs {
@@ -76,7 +77,7 @@ void launch_ranges(uint32_t K, const uint32_t* keys, uint2* ranges, uint32_t num
 void launch_render_fwd(const RenderArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);
 void launch_filter(const PreArgs& a, hipStream_t s);
-void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);
+void launch_render_bwd(const RenderBwdArgs& a, uint32_t* invd_flag, hipStream_t s);
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s);
 
 }  // namespace gs

@@ -20,153 +20,204 @@ __device__ __forceinline__ float bcastf(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
-// Sum 10 per-lane values over the wave. Returns the total of slot `slot` (valid when slot >= 0).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float pl32_sum(float a, float b) {  // lane<32: a[l]+a[l+32]; lane>=32: b[l-32]+b[l]
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float pl16_sum(float a, float b) {  // even rows: a[l]+a[l+16]; odd rows: b[l-16]+b[l]
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// Sum 10 per-lane values over the wave64 as a reduce-scatter: lane-half swap (v_permlane32_swap),
+// row swap (v_permlane16_swap), row_mirror / row_half_mirror / quad_perm DPP adds -- 26 VALU ops, no LDS.
+// Returns the total of slot `slot` (valid when slot >= 0; one lane per slot writes).
 __device__ __forceinline__ float wave_reduce10(const float (&p)[10], int lane, int& slot) {
-    const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8, b2 = lane & 4;
-    float q[6];
+    const bool b4 = lane & 16, b3 = lane & 8, b2 = lane & 4;
+    float q[5];
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
-        const float send = b5 ? p[i] : p[5 + i];
-        const float keep = b5 ? p[5 + i] : p[i];
-        q[i] = keep + __shfl_xor(send, 32);
-    }
-    q[5] = 0.0f;
-    float r[4];
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-        const float send = b4 ? q[i] : q[3 + i];
-        const float keep = b4 ? q[3 + i] : q[i];
-        r[i] = keep + __shfl_xor(send, 16);
-    }
-    r[3] = 0.0f;
-    float s[2];
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-        const float send = b3 ? r[i] : r[2 + i];
-        const float keep = b3 ? r[2 + i] : r[i];
-        s[i] = keep + __shfl_xor(send, 8);
-    }
-    float u;
-    {
-        const float send = b2 ? s[0] : s[1];
-        const float keep = b2 ? s[1] : s[0];
-        u = keep + __shfl_xor(send, 4);
-    }
-    u += __shfl_xor(u, 2);
-    u += __shfl_xor(u, 1);
+    for (int i = 0; i < 5; i++) q[i] = pl32_sum(p[i], p[5 + i]);         // slot (b5 ? 5 : 0) + i
+    float r[3];
+    r[0] = pl16_sum(q[0], q[3]);                                         // q-index (b4 ? 3 : 0) + i
+    r[1] = pl16_sum(q[1], q[4]);
+    r[2] = pl16_sum(q[2], 0.0f);
+    const float x0 = r[0] + dpp<0x140>(r[0]);                            // row_mirror: partner l ^ 15
+    const float x1 = r[1] + dpp<0x140>(r[1]);
+    const float x2 = r[2] + dpp<0x140>(r[2]);
+    const float s0 = b3 ? x2 : x0;                                       // r-index (b3 ? 2 : 0) + i
+    const float s1 = b3 ? 0.0f : x1;
+    const float y0 = s0 + dpp<0x141>(s0);                                // row_half_mirror: partner l ^ 7
+    const float y1 = s1 + dpp<0x141>(s1);
+    float u = b2 ? y1 : y0;
+    u += dpp<0xB1>(u);                                                   // quad_perm [1,0,3,2]
+    u += dpp<0x4E>(u);                                                   // quad_perm [2,3,0,1]
     const int ri = (b3 ? 2 : 0) + (b2 ? 1 : 0);
     const bool valid = (ri <= 2) && (!b4 || ri <= 1) && ((lane & 3) == 0);
-    slot = valid ? ((b5 ? 5 : 0) + (b4 ? 3 : 0) + ri) : -1;
+    slot = valid ? (((lane & 32) ? 5 : 0) + (b4 ? 3 : 0) + ri) : -1;
     return u;
 }
 
-__global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (tile >= a.num_tiles) return;
+// Front-to-back replay.  Lane l owns pixel (l&7, l>>3) of each 8x8 quadrant k of the tile.  Per
+// 64-splat batch each lane stages its splat in wave-private LDS together with a 4-bit mask of the
+// quadrants it can touch (quad_mask) that still have pixels before their last contributor; the wave
+// walks only splats with a non-empty mask and branches per quadrant on the (uniform) mask bits.
+// Inactive (pixel, splat) pairs inside a processed quadrant get alpha = 0 and dL/dalpha = 0, so the
+// body is branch-free.  HAS_INVD / HAS_BG drop the inverse-depth and background terms when zero.
+template <bool HAS_INVD, bool HAS_BG>
+__device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile, int lane, float4* sb) {
     const uint2 rg = a.ranges[tile];
     const int nall = (int)(rg.y - rg.x);
     const int mc = (int)a.max_contrib[tile];
     const int n = nall < mc ? nall : mc;
     if (n <= 0) return;
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
-    const int px = tx * GS_TILE_X + (lane & 15);
-    const int py0 = ty * GS_TILE_Y + (lane >> 4);
-    const float pxf = (float)px;
+    const int tx0 = tx * GS_TILE_X, ty0 = ty * GS_TILE_Y;
     const size_t HW = (size_t)a.W * a.H;
     const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
     const float hw = 0.5f * a.W, hh = 0.5f * a.H;
-    float T[4], ar0[4], ar1[4], ar2[4], ard[4], Tf[4], d0[4], d1[4], d2[4], dd[4], bgdot[4];
-    int last[4];
+    float T[4], ar0[4], ar1[4], ar2[4], ard[4], Tf[4], d0[4], d1[4], d2[4], dd[4], bgdot[4], pxf[4], pyf[4];
+    int last[4], qlast[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const int py = py0 + 4 * k;
+        const int px = tx0 + (k & 1) * 8 + (lane & 7), py = ty0 + (k >> 1) * 8 + (lane >> 3);
+        pxf[k] = (float)px;
+        pyf[k] = (float)py;
         T[k] = 1.0f;
         if (px < a.W && py < a.H) {
             const size_t pid = (size_t)py * a.W + px;
             last[k] = (int)a.n_contrib[pid];
             ar0[k] = -a.img_color[pid]; ar1[k] = -a.img_color[HW + pid]; ar2[k] = -a.img_color[2 * HW + pid];
-            ard[k] = -a.img_invd[pid];
+            ard[k] = HAS_INVD ? -a.img_invd[pid] : 0.0f;
             Tf[k] = a.final_T[pid];
             d0[k] = a.dL_dpix[pid]; d1[k] = a.dL_dpix[HW + pid]; d2[k] = a.dL_dpix[2 * HW + pid];
-            dd[k] = a.dL_dinvd ? a.dL_dinvd[pid] : 0.0f;
+            dd[k] = HAS_INVD ? a.dL_dinvd[pid] : 0.0f;
         } else {
             last[k] = 0;
             ar0[k] = ar1[k] = ar2[k] = ard[k] = Tf[k] = d0[k] = d1[k] = d2[k] = dd[k] = 0.0f;
         }
-        bgdot[k] = fmaf(bg2, d2[k], fmaf(bg1, d1[k], bg0 * d0[k]));
+        bgdot[k] = HAS_BG ? fmaf(bg2, d2[k], fmaf(bg1, d1[k], bg0 * d0[k])) : 0.0f;
+        int m = last[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const int y = __shfl_xor(m, o);
+            m = y > m ? y : m;
+        }
+        qlast[k] = __builtin_amdgcn_readfirstlane(m);
     }
     for (int base = 0; base < n; base += 64) {
         const int j = base + lane;
-        float gx = 0, gy = 0, ca = 0, cb = 0, cc = 0, op = 0, cr = 0, cg = 0, cbl = 0, ci = 0;
-        uint32_t ee = 0;
+        uint32_t qm = 0;
         if (j < n) {
-            ee = min(a.s_e[rg.x + j], a.K - 1);
+            const uint32_t ee = min(a.s_e[rg.x + j], a.K - 1);
             const uint32_t g = min(a.eg[ee], a.P - 1);
             const float2 m = a.xy[g];
             const float4 c4 = a.co[g];
             const float4 q = a.rgbi[g];
-            gx = m.x; gy = m.y; ca = c4.x; cb = c4.y; cc = c4.z; op = c4.w;
-            cr = q.x; cg = q.y; cbl = q.z; ci = q.w;
+            const float thr = gs_logf(c4.w / (1.0f / 255.0f));
+            qm = quad_mask({c4.x, c4.y, c4.z, c4.w}, m.x, m.y, thr, tx0, ty0);
+#pragma unroll
+            for (int k = 0; k < 4; k++) qm &= (j < qlast[k]) ? 0xfu : ~(1u << k);
+            sb[lane * 4 + 0] = make_float4(m.x, m.y, c4.x * LOG2E, c4.y * LOG2E);
+            sb[lane * 4 + 1] = make_float4(c4.z * LOG2E, c4.w, q.x, q.y);
+            sb[lane * 4 + 2] = make_float4(q.z, q.w, c4.x, c4.y);
+            sb[lane * 4 + 3] = make_float4(c4.z, __uint_as_float(ee), __uint_as_float(qm), 0.0f);
         }
-        const int cntb = (n - base) < 64 ? (n - base) : 64;
-        for (int jj = 0; jj < cntb; jj++) {
-            const float sx = bcastf(gx, jj), sy = bcastf(gy, jj);
-            const float sa = bcastf(ca, jj), sb = bcastf(cb, jj), sc = bcastf(cc, jj), so = bcastf(op, jj);
-            const float sr = bcastf(cr, jj), sg = bcastf(cg, jj), sbl = bcastf(cbl, jj), si = bcastf(ci, jj);
+        __builtin_amdgcn_wave_barrier();
+        uint64_t smask = __ballot(qm != 0u);
+        while (smask) {
+            const int jj = __ffsll((unsigned long long)smask) - 1;
+            smask &= smask - 1;
+            const float4 A = sb[jj * 4 + 0], B = sb[jj * 4 + 1], Cc = sb[jj * 4 + 2], Dv = sb[jj * 4 + 3];
+            const uint32_t m = __builtin_amdgcn_readfirstlane(__float_as_uint(Dv.z));
+            const float sx = A.x, sy = A.y, a2 = A.z, b2 = A.w, c2 = B.x, so = B.y, sr = B.z, sg = B.w;
+            const float sbl = Cc.x, si = HAS_INVD ? Cc.y : 0.0f, sa = Cc.z, sbb = Cc.w, sc = Dv.x;
             const int sidx = base + jj;
-            const float dx = sx - pxf;
             float p[10];
 #pragma unroll
             for (int v = 0; v < 10; v++) p[v] = 0.0f;
-            bool any = false;
+            float anyf = 0.0f;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const float dy = sy - (float)(py0 + 4 * k);
-                const float power = splat_power(sa, sb, sc, dx, dy);
-                const float G = __expf(power);
-                const float alpha = fminf(0.99f, so * G);
-                const bool act = (sidx < last[k]) && !(power > 0.0f) && !(alpha < (1.0f / 255.0f));
-                if (act) {
-                    any = true;
-                    const float weight = alpha * T[k];
-                    const float oma = 1.0f - alpha;
-                    const float inv = __builtin_amdgcn_rcpf(oma);
-                    ar0[k] = fmaf(weight, sr, ar0[k]);
-                    ar1[k] = fmaf(weight, sg, ar1[k]);
-                    ar2[k] = fmaf(weight, sbl, ar2[k]);
-                    p[6] = fmaf(weight, d0[k], p[6]);
-                    p[7] = fmaf(weight, d1[k], p[7]);
-                    p[8] = fmaf(weight, d2[k], p[8]);
-                    float dLda = fmaf(fmaf(sr, T[k], inv * ar0[k]), d0[k], 0.0f);
-                    dLda = fmaf(fmaf(sg, T[k], inv * ar1[k]), d1[k], dLda);
-                    dLda = fmaf(fmaf(sbl, T[k], inv * ar2[k]), d2[k], dLda);
+                if (!((m >> k) & 1u)) continue;  // wave-uniform
+                const float dx = sx - pxf[k], dy = sy - pyf[k];
+                const float p2 = splat_power(a2, b2, c2, dx, dy);
+                const float G = __builtin_amdgcn_exp2f(p2);
+                float alpha = fminf(0.99f, so * G);
+                const bool act = (sidx < last[k]) && !(p2 > 0.0f) && !(alpha < (1.0f / 255.0f));
+                const float actf = act ? 1.0f : 0.0f;
+                alpha = alpha * actf;
+                anyf += actf;
+                const float weight = alpha * T[k];
+                const float oma = 1.0f - alpha;
+                const float inv = __builtin_amdgcn_rcpf(oma);
+                ar0[k] = fmaf(weight, sr, ar0[k]);
+                ar1[k] = fmaf(weight, sg, ar1[k]);
+                ar2[k] = fmaf(weight, sbl, ar2[k]);
+                p[6] = fmaf(weight, d0[k], p[6]);
+                p[7] = fmaf(weight, d1[k], p[7]);
+                p[8] = fmaf(weight, d2[k], p[8]);
+                float dLda = fmaf(sr, T[k], inv * ar0[k]) * d0[k];
+                dLda = fmaf(fmaf(sg, T[k], inv * ar1[k]), d1[k], dLda);
+                dLda = fmaf(fmaf(sbl, T[k], inv * ar2[k]), d2[k], dLda);
+                if (HAS_INVD) {
                     ard[k] = fmaf(weight, si, ard[k]);
                     p[9] = fmaf(weight, dd[k], p[9]);
                     dLda = fmaf(fmaf(si, T[k], inv * ard[k]), dd[k], dLda);
-                    dLda = fmaf(-Tf[k] * inv, bgdot[k], dLda);
-                    T[k] = T[k] * oma;
-                    const float dL_dG = so * dLda;
-                    const float gdx = G * dx, gdy = G * dy;
-                    const float dG_ddelx = fmaf(-gdx, sa, -(gdy * sb));
-                    const float dG_ddely = fmaf(-gdy, sc, -(gdx * sb));
-                    p[0] = fmaf(dL_dG * dG_ddelx, hw, p[0]);
-                    p[1] = fmaf(dL_dG * dG_ddely, hh, p[1]);
-                    p[2] = fmaf(-0.5f * gdx * dx, dL_dG, p[2]);
-                    p[3] = fmaf(-0.5f * gdx * dy, dL_dG, p[3]);
-                    p[4] = fmaf(-0.5f * gdy * dy, dL_dG, p[4]);
-                    p[5] = fmaf(G, dLda, p[5]);
                 }
+                if (HAS_BG) dLda = fmaf(-Tf[k] * inv, bgdot[k], dLda);
+                dLda = dLda * actf;
+                T[k] = T[k] * oma;
+                const float dL_dG = so * dLda;
+                const float gdx = G * dx, gdy = G * dy;
+                const float dG_ddelx = fmaf(-gdx, sa, -(gdy * sbb));
+                const float dG_ddely = fmaf(-gdy, sc, -(gdx * sbb));
+                p[0] = fmaf(dL_dG * dG_ddelx, hw, p[0]);
+                p[1] = fmaf(dL_dG * dG_ddely, hh, p[1]);
+                const float h = -0.5f * dL_dG;
+                p[2] = fmaf(gdx * dx, h, p[2]);
+                p[3] = fmaf(gdx * dy, h, p[3]);
+                p[4] = fmaf(gdy * dy, h, p[4]);
+                p[5] = fmaf(G, dLda, p[5]);
             }
-            if (__any(any)) {
+            if (__any(anyf > 0.0f)) {
                 int slot;
                 const float tot = wave_reduce10(p, lane, slot);
-                const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)ee, jj);
+                const uint32_t e = __builtin_amdgcn_readfirstlane(__float_as_uint(Dv.y));
                 if (slot >= 0) a.rec[(size_t)e * 12 + slot] = tot;
                 if (lane == 0) a.flag[e] = 1;
             }
         }
+        __builtin_amdgcn_wave_barrier();
     }
+}
+
+__global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
+    __shared__ float4 s_b[4][64][4];
+    const int lane = threadIdx.x & 63;
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= a.num_tiles) return;
+    float4* sb = &s_b[threadIdx.x >> 6][0][0];
+    const bool has_bg = a.bg[0] != 0.0f || a.bg[1] != 0.0f || a.bg[2] != 0.0f;
+    const bool has_invd = a.dL_dinvd != nullptr && *a.invd_nonzero != 0u;
+    if (has_invd) {
+        if (has_bg) render_bwd_tile<true, true>(a, tile, lane, sb);
+        else render_bwd_tile<true, false>(a, tile, lane, sb);
+    } else {
+        if (has_bg) render_bwd_tile<false, true>(a, tile, lane, sb);
+        else render_bwd_tile<false, false>(a, tile, lane, sb);
+    }
+}
+
+// flag = any(dL/dinvdepth != 0): lets the replay drop the inverse-depth terms when the loss ignores depth
+__global__ void __launch_bounds__(256) k_any_nonzero(const float* __restrict__ x, uint32_t n, uint32_t* __restrict__ flag) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool nz = false;
+    for (; i < n; i += gridDim.x * blockDim.x) nz |= (x[i] != 0.0f);
+    if (__any(nz) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -174,11 +225,42 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
 // ---------------------------------------------------------------------------------------------------
 __device__ __forceinline__ float sq(float x) { return x * x; }
 
+__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, float* lsh);
+
+// Block of 256 Gaussians; the [256][M][3] SH slab is staged through LDS so both the coefficient loads
+// and the dL/dsh stores are coalesced (a per-thread 180-B stride touches 64 lines per wave instruction).
 __global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.P) return;
+    extern __shared__ __attribute__((aligned(16))) float s_sh[];
+    const int t = threadIdx.x;
+    const int base = blockIdx.x * 256;
+    const int idx = base + t;
+    const int nloc = (a.P - base) < 256 ? (a.P - base) : 256;
     const int M = a.M;
-    float* dsh = a.dsh ? a.dsh + (size_t)idx * M * 3 : nullptr;
+    const int slab = nloc * M * 3;  // floats
+    if (a.sh && M > 0) {
+        const float* src = a.sh + (size_t)base * M * 3;
+        const int n4 = slab >> 2;  // base*M*3*4 bytes is a multiple of 16 (256*M*12)
+        const float4* src4 = reinterpret_cast<const float4*>(src);
+        float4* dst4 = reinterpret_cast<float4*>(s_sh);
+        for (int i = t; i < n4; i += 256) dst4[i] = src4[i];
+        for (int i = (n4 << 2) + t; i < slab; i += 256) s_sh[i] = src[i];
+    }
+    __syncthreads();
+    if (idx < a.P) gauss_bwd_one(a, idx, s_sh + t * M * 3);
+    __syncthreads();
+    if (a.dsh && M > 0) {
+        float* dst = a.dsh + (size_t)base * M * 3;
+        const int n4 = slab >> 2;
+        float4* dst4 = reinterpret_cast<float4*>(dst);
+        const float4* src4 = reinterpret_cast<const float4*>(s_sh);
+        for (int i = t; i < n4; i += 256) dst4[i] = src4[i];
+        for (int i = (n4 << 2) + t; i < slab; i += 256) dst[i] = s_sh[i];
+    }
+}
+
+// One Gaussian; `lsh` is its [M][3] SH row in LDS, overwritten in place with dL/dsh.
+__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, float* lsh) {
+    const int M = a.M;
     if (!(a.radii[idx] > 0)) {
         for (int v = 0; v < 3; v++) {
             a.dmeans2D[3 * idx + v] = 0.f; a.dcolors[3 * idx + v] = 0.f; a.dmeans3D[3 * idx + v] = 0.f;
@@ -188,10 +270,10 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
         for (int v = 0; v < 4; v++) a.drot[4 * idx + v] = 0.f;
         a.dopacity[idx] = 0.f;
         a.depth[idx] = 0.f;
-        if (dsh) for (int v = 0; v < 3 * M; v++) dsh[v] = 0.f;
+        for (int v = 0; v < 3 * M; v++) lsh[v] = 0.f;
         return;
     }
-    // ---- records -> dL/d(mean2D, conic, opacity, color, invdepth)
+    // ---- records -> dL/d(mean2D, conic, opacity, color, invdepth); flags read 4 at a time
     float acc[10];
 #pragma unroll
     for (int v = 0; v < 10; v++) acc[v] = 0.f;
@@ -199,13 +281,21 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
         uint32_t c = a.cnt[idx];
         const uint32_t e0 = c ? a.first_e[idx] : 0u;
         if (e0 >= a.K || c > a.K - e0) c = 0;  // defensive: never read outside the record block
-        for (uint32_t e = e0; e < e0 + c; e++) {
-            if (!a.flag[e]) continue;
-            const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
-            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
-            acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
-            acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
-            acc[8] += r2.x; acc[9] += r2.y;
+        const uint32_t e1 = e0 + c;
+        for (uint32_t w = e0 & ~3u; w < e1; w += 4) {
+            uint32_t f4 = *reinterpret_cast<const uint32_t*>(a.flag + w);
+            if (w < e0) f4 &= 0xffffffffu << (8 * (e0 - w));
+            if (e1 - w < 4) f4 &= 0xffffffffu >> (8 * (4 - (e1 - w)));
+            while (f4) {
+                const int b = (__ffs(f4) - 1) >> 3;
+                f4 &= ~(0xffu << (8 * b));
+                const uint32_t e = w + b;
+                const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
+                const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+                acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
+                acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
+                acc[8] += r2.x; acc[9] += r2.y;
+            }
         }
     }
     a.dmeans2D[3 * idx + 0] = acc[0];
@@ -311,7 +401,7 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
 
     // ---- computeColorFromSH backward (backward.cu:23-144); clamped flags recomputed from the forward rgb
     if (a.sh) {
-        const float* sh = a.sh + (size_t)idx * M * 3;
+        const float* sh = lsh;
         const float* d0p = a.dc + 3 * idx;
         const int deg = a.D;
         const f3 dir_orig = {mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]};
@@ -351,8 +441,6 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
             dRGB[ch] = (r < 0) ? 0.0f : acc[6 + ch];
         }
         for (int ch = 0; ch < 3; ch++) a.ddc[3 * idx + ch] = SH_C0 * dRGB[ch];
-        for (int k = 0; k < M; k++)
-            for (int ch = 0; ch < 3; ch++) dsh[3 * k + ch] = k < nb ? basis[k] * dRGB[ch] : 0.0f;
         float dx[3] = {0, 0, 0}, dy[3] = {0, 0, 0}, dz[3] = {0, 0, 0};
 #define SHV(k, ch) sh[3 * (k) + (ch)]
         if (deg > 0) {
@@ -381,6 +469,9 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
             }
         }
 #undef SHV
+        // dL/dsh overwrites the staged coefficients in place (all reads of them are above)
+        for (int k = 0; k < M; k++)
+            for (int ch = 0; ch < 3; ch++) lsh[3 * k + ch] = k < nb ? basis[k] * dRGB[ch] : 0.0f;
         const f3 ddir = {dx[0] * dRGB[0] + dx[1] * dRGB[1] + dx[2] * dRGB[2], dy[0] * dRGB[0] + dy[1] * dRGB[1] + dy[2] * dRGB[2],
                          dz[0] * dRGB[0] + dz[1] * dRGB[1] + dz[2] * dRGB[2]};
         // dnormvdv (auxiliary.h:118-128)
@@ -392,6 +483,7 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
         dmean.z += (-v.x * v.z * ddir.x - v.y * v.z * ddir.y + (sum2 - v.z * v.z) * ddir.z) * invsum32;
     } else {
         for (int ch = 0; ch < 3; ch++) a.ddc[3 * idx + ch] = 0.f;
+        for (int v = 0; v < 3 * M; v++) lsh[v] = 0.f;
     }
     a.dmeans3D[3 * idx + 0] = dmean.x;
     a.dmeans3D[3 * idx + 1] = dmean.y;
@@ -426,11 +518,19 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
     }
 }
 
-void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
-    if (a.num_tiles > 0) k_render_bwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
+void launch_render_bwd(const RenderBwdArgs& a, uint32_t* invd_flag, hipStream_t s) {
+    if (a.dL_dinvd) {
+        (void)hipMemsetAsync(invd_flag, 0, sizeof(uint32_t), s);
+        const uint32_t n = (uint32_t)a.W * a.H;
+        k_any_nonzero<<<512, 256, 0, s>>>(a.dL_dinvd, n, invd_flag);
+    }
+    RenderBwdArgs b = a;
+    b.invd_nonzero = invd_flag;
+    if (a.num_tiles > 0) k_render_bwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(b);
 }
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s) {
-    if (a.P > 0) k_gauss_bwd<<<(a.P + 255) / 256, 256, 0, s>>>(a);
+    const size_t lds = (size_t)256 * (a.M > 0 ? a.M : 0) * 3 * sizeof(float);
+    if (a.P > 0) k_gauss_bwd<<<(a.P + 255) / 256, 256, lds, s>>>(a);
 }
 
 }  // namespace gs

@@ -76,10 +76,69 @@ __device__ __forceinline__ f3 sh_to_rgb(f3 pos, const float* campos, int deg, co
     return {fmaxf(r0, 0.0f), fmaxf(r1, 0.0f), fmaxf(r2, 0.0f)};
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// Wave-cooperative (Gaussian, tile) candidate walk.  Every lane owns a Gaussian with tile rect
+// [x0,x1) x [y0,y1) (empty when culled).  The wave's candidates are enumerated in (lane, ty, tx) order --
+// the reference's duplicateWithKeys order -- 64 per step, so one huge Gaussian no longer makes all 64
+// lanes loop over its whole rect.  visit(owner, tile_x, tile_y, kept, valid, chunk_mask) is called once
+// per step for every lane; `kept` is the precise per-tile cull (max_contrib_power <= log(255 o)).
+struct CandLDS {
+    uint32_t pre[64];     // exclusive prefix of rect areas
+    int x0[64], y0[64], w[64], area[64];
+    float mx[64], my[64], thr[64];
+    float4 co[64];
+};
+
+template <typename Visit>
+__device__ __forceinline__ void wave_candidates(CandLDS& L, int lane, int x0, int y0, int x1, int y1, float mx, float my,
+                                                float4 co, float thr, Visit&& visit) {
+    const uint32_t area = (x1 > x0 && y1 > y0) ? (uint32_t)(x1 - x0) * (uint32_t)(y1 - y0) : 0u;
+    uint32_t incl = area;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    L.pre[lane] = incl - area;
+    L.x0[lane] = x0; L.y0[lane] = y0; L.w[lane] = x1 - x0; L.area[lane] = (int)area;
+    L.mx[lane] = mx; L.my[lane] = my; L.thr[lane] = thr; L.co[lane] = co;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i0 = 0; i0 < total; i0 += 64) {
+        const uint32_t item = i0 + (uint32_t)lane;
+        const bool valid = item < total;
+        int owner = 0;
+        bool kept = false;
+        int tx = 0, ty = 0;
+        if (valid) {
+            // largest lane with pre <= item (zero-area lanes share the next lane's prefix)
+            int lo = 0;
+#pragma unroll
+            for (int step = 32; step > 0; step >>= 1)
+                if (L.pre[lo + step] <= item) lo += step;
+            owner = lo;
+            const uint32_t r = item - L.pre[owner];
+            const uint32_t ww = (uint32_t)L.w[owner];
+            const uint32_t qy = r / ww;
+            tx = L.x0[owner] + (int)(r - qy * ww);
+            ty = L.y0[owner] + (int)qy;
+            const float4 c = L.co[owner];
+            const float p = max_contrib_power(f4{c.x, c.y, c.z, c.w}, L.mx[owner], L.my[owner], (float)(tx * GS_TILE_X),
+                                              (float)(ty * GS_TILE_Y), (float)((tx + 1) * GS_TILE_X - 1),
+                                              (float)((ty + 1) * GS_TILE_Y - 1));
+            kept = p <= L.thr[owner];
+        }
+        visit(owner, tx, ty, kept, valid, item);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Returns the rect area (0 when culled); fills the geometry outputs for kept Gaussians.
-__device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx) {
+struct RectOut { int x0, y0, x1, y1; float mx, my, thr; float4 co; };
+
+__device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, const float* lsh, RectOut& ro) {
     a.radii[idx] = 0;
-    a.cnt[idx] = 0;
     a.depthkey[idx] = 0xffffffffu;
     const f3 po = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
     // in_frustum (auxiliary.h:150-175)
@@ -126,33 +185,70 @@ __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx) {
     if (a.colors) {
         col = {a.colors[3 * idx], a.colors[3 * idx + 1], a.colors[3 * idx + 2]};
     } else {
-        col = sh_to_rgb(po, a.campos, a.D, a.dc + 3 * idx, a.sh ? a.sh + (size_t)idx * a.M * 3 : nullptr, nullptr);
+        col = sh_to_rgb(po, a.campos, a.sh ? a.D : 0, a.dc + 3 * idx, lsh, nullptr);
     }
     const float4 co = make_float4(conic.x, conic.y, conic.z, a.opacities[idx] * h_scale);
     a.radii[idx] = ir;
     a.xy[idx] = make_float2(px, py);
     a.co[idx] = co;
     a.rgbi[idx] = make_float4(col.x, col.y, col.z, 1.f / pv.z);
-    // precise per-tile cull (duplicateWithKeys, rasterizer_impl.cu:149-179)
-    const f4 c4 = {co.x, co.y, co.z, co.w};
-    const float thr = gs_logf(co.w / (1.0f / 255.0f));
-    uint32_t c = 0;
-    for (int ty = y0; ty < y1; ty++)
-        for (int tx = x0; tx < x1; tx++) {
-            const float pw_ = max_contrib_power(c4, px, py, (float)(tx * GS_TILE_X), (float)(ty * GS_TILE_Y),
-                                                (float)((tx + 1) * GS_TILE_X - 1), (float)((ty + 1) * GS_TILE_Y - 1));
-            c += (pw_ <= thr) ? 1u : 0u;
-        }
-    a.cnt[idx] = c;
-    a.depthkey[idx] = c > 0 ? __float_as_uint(pv.z) : 0xffffffffu;
+    a.depthkey[idx] = __float_as_uint(pv.z);
+    ro.x0 = x0; ro.y0 = y0; ro.x1 = x1; ro.y1 = y1; ro.mx = px; ro.my = py; ro.co = co;
+    ro.thr = gs_logf(co.w / (1.0f / 255.0f));
     return area;
 }
 
+// The block's [256][M][3] SH slab is staged through LDS with 16-B coalesced loads; read per thread at a
+// 45-dword stride (odd -> conflict-free) instead of 45 strided global loads per lane.
 __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float s_sh[];
     __shared__ unsigned long long s_sum[4];
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = threadIdx.x;
+    const int base = blockIdx.x * 256;
+    const int idx = base + t;
+    const int nloc = (a.P - base) < 256 ? (a.P - base) : 256;
+    const bool stage = a.sh != nullptr && a.colors == nullptr && a.M > 0;
+    if (stage) {
+        const int slab = nloc * a.M * 3;
+        const float* src = a.sh + (size_t)base * a.M * 3;
+        const int n4 = slab >> 2;
+        const float4* src4 = reinterpret_cast<const float4*>(src);
+        float4* dst4 = reinterpret_cast<float4*>(s_sh);
+        for (int i = t; i < n4; i += 256) dst4[i] = src4[i];
+        for (int i = (n4 << 2) + t; i < slab; i += 256) s_sh[i] = src[i];
+    }
+    __syncthreads();
     uint32_t area = 0;
-    if (idx < a.P) area = preprocess_one(a, idx);
+    RectOut ro = {0, 0, 0, 0, 0.f, 0.f, 0.f, make_float4(0.f, 0.f, 0.f, 0.f)};
+    if (idx < a.P) area = preprocess_one(a, idx, stage ? s_sh + t * a.M * 3 : nullptr, ro);
+    // precise per-tile cull counts (duplicateWithKeys, rasterizer_impl.cu:149-179), wave-cooperative.
+    // The candidate tables reuse the SH staging LDS (dead after preprocess_one).
+    __syncthreads();
+    {
+        CandLDS* s_cand = reinterpret_cast<CandLDS*>(s_sh);
+        uint32_t (*s_cnt)[64] = reinterpret_cast<uint32_t (*)[64]>(s_cand + 4);
+        const int lane = t & 63, w = t >> 6;
+        s_cnt[w][lane] = 0;
+        CandLDS& L = s_cand[w];
+        wave_candidates(L, lane, ro.x0, ro.y0, ro.x1, ro.y1, ro.mx, ro.my, ro.co, ro.thr,
+                        [&](int owner, int, int, bool kept, bool valid, uint32_t item) {
+                            const uint64_t km = __ballot(kept);
+                            // first item of each owner segment in this step adds the segment's kept count
+                            const bool seg_start = valid && (lane == 0 || item == L.pre[owner]);
+                            if (seg_start) {
+                                const uint32_t seg_end_item = L.pre[owner] + (uint32_t)L.area[owner];
+                                const int len = (int)min(seg_end_item - item, (uint32_t)(64 - lane));
+                                const uint64_t seg = (len >= 64 ? ~0ull : ((1ull << len) - 1ull)) << lane;
+                                s_cnt[w][owner] += (uint32_t)__popcll(km & seg);
+                            }
+                            __builtin_amdgcn_wave_barrier();
+                        });
+        if (idx < a.P) {
+            const uint32_t c = s_cnt[w][lane];
+            a.cnt[idx] = c;
+            if (c == 0) a.depthkey[idx] = 0xffffffffu;
+        }
+    }
     unsigned long long v = area;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -164,38 +260,54 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     }
 }
 
-// emission in depth order: instance e = off[p] + j for the j-th kept tile of Gaussian order[p]
+// emission in depth order: instance e = off[p] + j for the j-th kept tile of Gaussian order[p].  A wave
+// owns 64 consecutive depth ranks, so its instances form one contiguous run starting at off[p0]; the
+// cooperative candidate walk writes them in (p, ty, tx) order with consecutive lanes -> consecutive e.
 __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict__ order,
                                               const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
                                               const float2* __restrict__ xy, const float4* __restrict__ co,
                                               const int* __restrict__ radii, int tiles_x, int tiles_y,
                                               uint32_t* __restrict__ first_e, uint32_t* __restrict__ tilekey,
                                               uint32_t* __restrict__ eg) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= P) return;
-    const uint32_t g = order[p];
-    if (g >= (uint32_t)P) return;
-    const uint32_t c = cnt[g];
-    if (c == 0) return;
-    uint32_t e = off[p];
-    first_e[g] = e;
-    const float2 m = xy[g];
-    const float4 c4v = co[g];
-    const f4 c4 = {c4v.x, c4v.y, c4v.z, c4v.w};
-    int x0, y0, x1, y1;
-    get_rect_s(m.x, m.y, radii[g], tiles_x, tiles_y, x0, y0, x1, y1);
-    const float thr = gs_logf(c4.w / (1.0f / 255.0f));
-    const uint32_t e_end = e + c;
-    for (int ty = y0; ty < y1 && e < e_end; ty++)
-        for (int tx = x0; tx < x1; tx++) {
-            const float pw_ = max_contrib_power(c4, m.x, m.y, (float)(tx * GS_TILE_X), (float)(ty * GS_TILE_Y),
-                                                (float)((tx + 1) * GS_TILE_X - 1), (float)((ty + 1) * GS_TILE_Y - 1));
-            if (pw_ <= thr && e < e_end) {
-                tilekey[e] = (uint32_t)(ty * tiles_x + tx);
-                eg[e] = g;
-                e++;
+    __shared__ CandLDS s_cand[4];
+    __shared__ uint32_t s_g[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int p0 = blockIdx.x * blockDim.x + w * 64;
+    if (p0 >= P) return;  // whole wave
+    const int p = p0 + lane;
+    int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    float mx = 0.f, my = 0.f, thr = 0.f;
+    float4 c4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint32_t g = 0xffffffffu;
+    if (p < P) {
+        g = order[p];
+        if (g < (uint32_t)P) {
+            const uint32_t c = cnt[g];
+            if (c > 0) {
+                first_e[g] = off[p];
+                const float2 m = xy[g];
+                c4 = co[g];
+                mx = m.x; my = m.y;
+                get_rect_s(m.x, m.y, radii[g], tiles_x, tiles_y, x0, y0, x1, y1);
+                thr = gs_logf(c4.w / (1.0f / 255.0f));
             }
         }
+    }
+    s_g[w][lane] = g;
+    const uint32_t e0 = off[p0];
+    uint32_t running = 0;
+    CandLDS& L = s_cand[w];
+    wave_candidates(L, lane, x0, y0, x1, y1, mx, my, c4, thr,
+                    [&](int owner, int tx, int ty, bool kept, bool valid, uint32_t) {
+                        const uint64_t km = __ballot(kept);
+                        const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+                        if (kept) {
+                            const uint32_t e = e0 + running + (uint32_t)__popcll(km & lt);
+                            tilekey[e] = (uint32_t)(ty * tiles_x + tx);
+                            eg[e] = s_g[w][owner];
+                        }
+                        running += (uint32_t)__popcll(km);
+                    });
 }
 
 // identifyTileRanges over the sorted (all-valid) tile keys
@@ -216,93 +328,98 @@ __device__ __forceinline__ uint32_t bcast_u(uint32_t v, int lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
 }
 
-// renderCUDA (forward.cu:349-501) restructured for wave64: one wave per tile, 4 pixels per lane
-// (rows ly, ly+4, ly+8, ly+12), the 64-splat batch lives one splat per lane.
+// renderCUDA (forward.cu:349-501) restructured for wave64.  One workgroup per tile, one wave per 8x8
+// quadrant (one pixel per lane).  Each 64-splat batch is gathered one splat per lane, tested against the
+// wave's quadrant with the reference's own max-contribution rect test (quad_mask), and staged in a
+// wave-private LDS slot; the wave then walks only the splats whose footprint reaches its quadrant
+// (s_ff1 over a 64-bit ballot) and reads each one with broadcast ds_read_b128.  The per-pixel update is
+// branch-free: a rejected or finished pixel gets alpha = 0, which leaves C, D and T bit-identical.
+// The conic is prescaled by log2(e) at staging so the exponential is a bare v_exp_f32.
 __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (tile >= a.num_tiles) return;
+    __shared__ float4 s_b[4][64][3];
+    __shared__ uint32_t s_mx[4];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tile = blockIdx.x;
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
-    const int px = tx * GS_TILE_X + (lane & 15);
-    const int py0 = ty * GS_TILE_Y + (lane >> 4);
-    const float pxf = (float)px;
-    float T[4], C0[4], C1[4], C2[4], Dd[4];
-    uint32_t last[4];
-    bool done[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        T[k] = 1.0f; C0[k] = C1[k] = C2[k] = Dd[k] = 0.0f; last[k] = 0;
-        done[k] = !(px < a.W && (py0 + 4 * k) < a.H);
-    }
+    const int px = tx * GS_TILE_X + (w & 1) * 8 + (lane & 7);
+    const int py = ty * GS_TILE_Y + (w >> 1) * 8 + (lane >> 3);
+    const int qx0 = tx * GS_TILE_X + (w & 1) * 8, qy0 = ty * GS_TILE_Y + (w >> 1) * 8;
+    const float pxf = (float)px, pyf = (float)py;
+    const bool inside = px < a.W && py < a.H;
+    float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f, Dd = 0.0f, live = inside ? 1.0f : 0.0f;
+    uint32_t last = 0;
     const uint2 rg = a.ranges[tile];
     const int n = (int)(rg.y - rg.x);
+    float4* sb = &s_b[w][0][0];
     for (int base = 0; base < n; base += 64) {
-        if (__all(done[0] && done[1] && done[2] && done[3])) break;
+        if (!__any(live != 0.0f)) break;
         const int j = base + lane;
-        float gx = 0, gy = 0, ca = 0, cb = 0, cc = 0, op = 0, cr = 0, cg = 0, cbl = 0, ci = 0;
+        bool touch = false;
         if (j < n) {
             const uint32_t e = min(a.s_e[rg.x + j], a.K - 1);
             const uint32_t g = min(a.eg[e], a.P - 1);
             const float2 m = a.xy[g];
             const float4 c4 = a.co[g];
             const float4 q = a.rgbi[g];
-            gx = m.x; gy = m.y; ca = c4.x; cb = c4.y; cc = c4.z; op = c4.w;
-            cr = q.x; cg = q.y; cbl = q.z; ci = q.w;
+            const float thr = gs_logf(c4.w / (1.0f / 255.0f));
+            touch = (quad_mask({c4.x, c4.y, c4.z, c4.w}, m.x, m.y, thr, qx0 & ~15, qy0 & ~15) >> w) & 1u;
+            sb[lane * 3 + 0] = make_float4(m.x, m.y, c4.x * LOG2E, c4.y * LOG2E);
+            sb[lane * 3 + 1] = make_float4(c4.z * LOG2E, c4.w, q.x, q.y);
+            sb[lane * 3 + 2] = make_float4(q.z, q.w, 0.0f, 0.0f);
         }
-        const int cntb = (n - base) < 64 ? (n - base) : 64;
-        for (int jj = 0; jj < cntb; jj++) {
-            const float sx = bcast(gx, jj), sy = bcast(gy, jj);
-            const float sa = bcast(ca, jj), sb = bcast(cb, jj), sc = bcast(cc, jj), so = bcast(op, jj);
-            const float sr = bcast(cr, jj), sg = bcast(cg, jj), sbl = bcast(cbl, jj), si = bcast(ci, jj);
-            const uint32_t contrib = (uint32_t)(base + jj + 1);
-            const float dx = sx - pxf;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const float dy = sy - (float)(py0 + 4 * k);
-                const float power = splat_power(sa, sb, sc, dx, dy);
-                const float alpha = fminf(0.99f, so * __expf(power));
-                bool ok = !done[k] && !(power > 0.0f) && !(alpha < (1.0f / 255.0f));
-                const float test_T = T[k] * (1 - alpha);
-                const bool term = ok && (test_T < 0.0001f);
-                done[k] = done[k] || term;
-                ok = ok && !term;
-                if (ok) {
-                    C0[k] = fmaf(sr * alpha, T[k], C0[k]);
-                    C1[k] = fmaf(sg * alpha, T[k], C1[k]);
-                    C2[k] = fmaf(sbl * alpha, T[k], C2[k]);
-                    Dd[k] = fmaf(si * alpha, T[k], Dd[k]);
-                    T[k] = test_T;
-                    last[k] = contrib;
-                }
-            }
-            if (__all(done[0] && done[1] && done[2] && done[3])) break;
+        __builtin_amdgcn_wave_barrier();
+        uint64_t mask = __ballot(touch);
+        while (mask) {
+            const int jj = __ffsll((unsigned long long)mask) - 1;
+            mask &= mask - 1;
+            const float4 A = sb[jj * 3 + 0], B = sb[jj * 3 + 1], Cc = sb[jj * 3 + 2];
+            const float dx = A.x - pxf, dy = A.y - pyf;
+            const float p2 = splat_power(A.z, A.w, B.x, dx, dy);
+            float alpha = fminf(0.99f, B.y * __builtin_amdgcn_exp2f(p2));
+            alpha = (p2 > 0.0f) ? 0.0f : alpha;
+            alpha = (alpha < (1.0f / 255.0f)) ? 0.0f : alpha;
+            alpha = alpha * live;
+            const float test_T = T * (1 - alpha);
+            const bool term = test_T < 0.0001f;
+            live = term ? 0.0f : live;
+            alpha = term ? 0.0f : alpha;
+            C0 = fmaf(B.z * alpha, T, C0);
+            C1 = fmaf(B.w * alpha, T, C1);
+            C2 = fmaf(Cc.x * alpha, T, C2);
+            Dd = fmaf(Cc.y * alpha, T, Dd);
+            T = term ? T : test_T;
+            last = (alpha > 0.0f) ? (uint32_t)(base + jj + 1) : last;
+            if (!__any(live != 0.0f)) break;
         }
+        __builtin_amdgcn_wave_barrier();
     }
-    const size_t HW = (size_t)a.W * a.H;
     uint32_t mx = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int py = py0 + 4 * k;
-        if (px < a.W && py < a.H) {
-            const size_t pid = (size_t)py * a.W + px;
-            a.final_T[pid] = T[k];
-            a.n_contrib[pid] = last[k];
-            const float o0 = fmaf(T[k], a.bg[0], C0[k]);
-            const float o1 = fmaf(T[k], a.bg[1], C1[k]);
-            const float o2 = fmaf(T[k], a.bg[2], C2[k]);
-            a.out_color[pid] = o0; a.out_color[HW + pid] = o1; a.out_color[2 * HW + pid] = o2;
-            a.img_color[pid] = o0; a.img_color[HW + pid] = o1; a.img_color[2 * HW + pid] = o2;
-            a.out_invd[pid] = Dd[k];
-            a.img_invd[pid] = Dd[k];
-            mx = last[k] > mx ? last[k] : mx;
-        }
+    if (inside) {
+        const size_t HW = (size_t)a.W * a.H;
+        const size_t pid = (size_t)py * a.W + px;
+        a.final_T[pid] = T;
+        a.n_contrib[pid] = last;
+        const float o0 = fmaf(T, a.bg[0], C0);
+        const float o1 = fmaf(T, a.bg[1], C1);
+        const float o2 = fmaf(T, a.bg[2], C2);
+        a.out_color[pid] = o0; a.out_color[HW + pid] = o1; a.out_color[2 * HW + pid] = o2;
+        a.img_color[pid] = o0; a.img_color[HW + pid] = o1; a.img_color[2 * HW + pid] = o2;
+        a.out_invd[pid] = Dd;
+        a.img_invd[pid] = Dd;
+        mx = last;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const uint32_t y = __shfl_xor(mx, o);
         mx = y > mx ? y : mx;
     }
-    if (lane == 0) a.max_contrib[tile] = mx;
+    if (lane == 0) s_mx[w] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t m0 = s_mx[0] > s_mx[1] ? s_mx[0] : s_mx[1];
+        const uint32_t m1 = s_mx[2] > s_mx[3] ? s_mx[2] : s_mx[3];
+        a.max_contrib[tile] = m0 > m1 ? m0 : m1;
+    }
 }
 
 // checkFrustum (rasterizer_impl.cu:104-116)
@@ -349,7 +466,11 @@ __global__ void __launch_bounds__(256) k_filter(PreArgs a) {
 }
 
 void launch_preprocess(const PreArgs& a, hipStream_t s) {
-    if (a.P > 0) k_preprocess<<<(a.P + 255) / 256, 256, 0, s>>>(a);
+    const bool stage = a.sh != nullptr && a.colors == nullptr && a.M > 0;
+    size_t lds = stage ? (size_t)256 * a.M * 3 * sizeof(float) : 0;
+    const size_t cand = 4 * sizeof(CandLDS) + 4 * 64 * sizeof(uint32_t);
+    if (lds < cand) lds = cand;
+    if (a.P > 0) k_preprocess<<<(a.P + 255) / 256, 256, lds, s>>>(a);
 }
 void launch_emit(int P, const uint32_t* order, const uint32_t* cnt, const uint32_t* off, const float2* xy,
                  const float4* co, const int* radii, int tiles_x, int tiles_y, uint32_t* first_e, uint32_t* tilekey,
@@ -361,7 +482,7 @@ void launch_ranges(uint32_t K, const uint32_t* keys, uint2* ranges, uint32_t num
     if (K > 0) k_ranges<<<(K + 255) / 256, 256, 0, s>>>(K, keys, ranges, num_tiles);
 }
 void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
-    if (a.num_tiles > 0) k_render_fwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
+    if (a.num_tiles > 0) k_render_fwd<<<a.num_tiles, 256, 0, s>>>(a);
 }
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s) {
     if (P > 0) k_mark_visible<<<(P + 255) / 256, 256, 0, s>>>(P, means3D, view, present);

@@ -121,6 +121,11 @@ int dg_sort_pairs_u32(uint32_t* keys, uint32_t* vals, uint32_t n, int begin_bit,
 int dg_exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* total, dg_alloc_fn alloc,
                           void* user, dg_stream_t stream);
 
+/* Per-phase hipEvent profiling on the caller's stream (off by default).  collect() synchronises and
+ * writes "phase=total_ms/launches;..." for everything recorded since the previous collect. */
+void dg_profile_enable(int on);
+int dg_profile_collect(char* buf, int buflen);
+
 const char* dg_last_error(void);
 int dg_version(void);
 
