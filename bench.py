@@ -46,6 +46,7 @@ def phase_bytes(phase: str, N: int, K: int, HW: int) -> float:
         "render_fwd": 44.0 * K + 24.0 * HW,
         "flag_clear": 0.0,
         "render_bwd": 84.0 * K + 40.0 * HW,
+        "record_sum": 0.0,                  # implementation overhead (per-instance records -> sums)
         "gauss_bwd": 528.0 * N,
     }.get(phase, 0.0)
 

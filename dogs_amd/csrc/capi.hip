@@ -162,15 +162,17 @@ struct BwdScratch {
     uint8_t* flag;
     float* rec;
     uint32_t* invd_flag;
+    float4* sums;  // [P][3] per-Gaussian record sums
     size_t bytes;
 };
-BwdScratch carve_bwd(void* base, int64_t K) {
+BwdScratch carve_bwd(void* base, int64_t K, int P) {
     Carver c(base);
     BwdScratch s;
     const size_t n = (size_t)(K > 0 ? K : 1);
     s.flag = c.take<uint8_t>(n);
     s.rec = c.take<float>(12 * n);
     s.invd_flag = c.take<uint32_t>(4);
+    s.sums = c.take<float4>(3 * (size_t)(P > 0 ? P : 1));
     s.bytes = c.off;
     return s;
 }
@@ -375,10 +377,10 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     const int passes = (bits_for((uint32_t)T) + 7) / 8;
     const uint32_t* s_e = (passes & 1) ? b.se1 : b.se0;
 
-    const size_t sbytes = carve_bwd(nullptr, K).bytes;
+    const size_t sbytes = carve_bwd(nullptr, K, P).bytes;
     void* sbase = alloc(user, DG_BUF_BACKWARD, sbytes);
     if (!sbase) return fail("backward scratch allocation failed%s%d");
-    BwdScratch sc = carve_bwd(sbase, K);
+    BwdScratch sc = carve_bwd(sbase, K, P);
     if (K > 0) {
         { PROF("flag_clear"); HIP_OK(hipMemsetAsync(sc.flag, 0, (size_t)K, s)); }
         gs::RenderBwdArgs r;
@@ -403,10 +405,11 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     q.means3D = a->means3D; q.scales = a->scales; q.rotations = a->rotations; q.opacities = a->opacities;
     q.dc = a->dc; q.sh = (a->M > 0) ? a->sh : nullptr; q.cov3D_precomp = a->cov3D_precomp;
     q.view = a->viewmatrix; q.proj = a->projmatrix; q.campos = a->campos;
-    q.radii = radii; q.cnt = g.cnt; q.first_e = g.first_e; q.rec = sc.rec; q.flag = sc.flag;
+    q.radii = radii; q.cnt = g.cnt; q.first_e = g.first_e; q.co = g.co; q.rec = sc.rec; q.flag = sc.flag; q.sums = sc.sums;
     q.dmeans2D = dmeans2D; q.dcolors = dcolors; q.dopacity = dopacity; q.dmeans3D = dmeans3D; q.dcov3D = dcov3D;
     q.ddc = ddc; q.dsh = dsh; q.dscales = dscales; q.drot = drot; q.depth = depth;
     if (q.M > 0 && !dsh) return fail("dsh output required when M > 0%s%d");
+    { PROF("record_sum"); gs::launch_record_sum(q, s); }
     { PROF("gauss_bwd"); gs::launch_gauss_bwd(q, s); }
     DBG_SYNC(a->debug, s);
     HIP_OK(hipGetLastError());

@@ -202,4 +202,14 @@ __device__ __forceinline__ float splat_power(float cx, float cy, float cz, float
     return fmaf(-0.5f, fmaf(cz * dy, dy, (cx * dx) * dx), -((cy * dx) * dy));
 }
 
+// Two pixels of one row (same dy) at once: ext_vector_type(2) arithmetic lowers to gfx950's packed
+// v_pk_{fma,mul,add}_f32 (two fp32 lanes per VALU issue), each half bitwise equal to splat_power.
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2f bc2(float x) { return (v2f){x, x}; }
+__device__ __forceinline__ v2f fma2(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ v2f splat_power2(float cx, float cy, float cz, v2f dx, float dy) {
+    const float czdy = cz * dy;
+    return fma2(bc2(-0.5f), fma2(bc2(czdy), bc2(dy), (bc2(cx) * dx) * dx), -((bc2(cy) * dx) * bc2(dy)));
+}
+
 }  // namespace gs

@@ -64,8 +64,10 @@ struct GaussBwdArgs {
     const int* radii;
     const uint32_t* cnt;
     const uint32_t* first_e;
+    const float4* co;        // forward conic + AA-scaled opacity
     const float* rec;
     const uint8_t* flag;
+    float4* sums;            // [P][3] record sums (k_record_sum -> k_gauss_bwd)
     float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *ddc, *dsh, *dscales, *drot, *depth;
 };
 
@@ -78,6 +80,7 @@ void launch_render_fwd(const RenderArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);
 void launch_filter(const PreArgs& a, hipStream_t s);
 void launch_render_bwd(const RenderBwdArgs& a, uint32_t* invd_flag, hipStream_t s);
+void launch_record_sum(const GaussBwdArgs& a, hipStream_t s);
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s);
 
 }  // namespace gs

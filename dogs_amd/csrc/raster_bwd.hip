@@ -4,11 +4,12 @@
 //                max contributor. The reference (backward.cu:455-658) replays 32-splat buckets from
 //                ~2 GB of sampled forward state; here the state is recomputed on the fly, which is the
 //                same arithmetic (T *= 1 - alpha, ar += w c) without the sampled-state traffic.
-//                Per splat, the 10 gradient partials are summed over the wave with a transpose
+//                Per splat, the 10 gradient moments are summed over the wave with a transpose
 //                reduce-scatter (13 cross-lane exchanges instead of 60) and stored once as a 48-B record
 //                at the instance's emission slot -- no float atomics (the chip-wide atomic rate and the
 //                scattered-row penalty make per-instance atomicAdd the wrong tool on MI355X).
-// k_gauss_bwd    one thread per Gaussian: sums its records in emission order (deterministic), then
+// k_record_sum   a wave per 64 Gaussians sums their records in emission order (deterministic).
+// k_gauss_bwd    one thread per Gaussian: turns the summed moments into dL/d(mean2D, conic, opacity), then
 //                computeCov2DCUDA + preprocessCUDA backward (backward.cu:149-451) fused in one pass.
 #include <hip/hip_runtime.h>
 #include "gs_common.h"
@@ -61,12 +62,73 @@ __device__ __forceinline__ float wave_reduce10(const float (&p)[10], int lane, i
     return u;
 }
 
-// Front-to-back replay.  Lane l owns pixel (l&7, l>>3) of each 8x8 quadrant k of the tile.  Per
-// 64-splat batch each lane stages its splat in wave-private LDS together with a 4-bit mask of the
-// quadrants it can touch (quad_mask) that still have pixels before their last contributor; the wave
-// walks only splats with a non-empty mask and branches per quadrant on the (uniform) mask bits.
-// Inactive (pixel, splat) pairs inside a processed quadrant get alpha = 0 and dL/dalpha = 0, so the
-// body is branch-free.  HAS_INVD / HAS_BG drop the inverse-depth and background terms when zero.
+// Front-to-back replay.  Lane l owns pixels (l&7, l>>3) and (l&7 + 8, l>>3) of the tile's top half
+// (pair A = quadrants 0,1) and the same two of the bottom half (pair B = quadrants 2,3); each pair is
+// one row, evaluated with packed fp32.  Per 64-splat batch each lane stages its splat in wave-private
+// LDS with a 4-bit mask of the quadrants it can touch (quad_mask) that still have pixels before their
+// last contributor; the wave walks only splats with a non-empty mask and skips a pair whose two mask
+// bits are clear (wave-uniform branch).  Inactive (pixel, splat) pairs get alpha = 0, dL/dalpha = 0.
+//
+// The per-pixel gradient terms of backward.cu:600-650 are regrouped so that everything constant per
+// splat leaves the pixel loop (exact algebra, fp32 rounding differs from the per-term sums):
+//   dL/dalpha = T (c.g) + (ar.g)/(1 - alpha) [- T_final (bg.g)/(1 - alpha)]   g = dL/dpixel (+ invdepth)
+//   with S = ar.g carried as ONE scalar per pixel (S += w (c.g)) instead of 3-4 channel accumulators,
+// and with t = G dL/dalpha the splat's sums reduce to the moments
+//   SG = sum t, SGx = sum t dx, SGy = sum t dy, SGxx = sum t dx^2, SGxy = sum t dx dy, SGyy = sum t dy^2
+// from which k_gauss_bwd forms dL/dmean2D = -(W/2, H/2) o (a SGx + b SGy, c SGy + b SGx),
+// dL/dconic = -o/2 (SGxx, SGxy, SGyy) and dL/dopacity = SG once per Gaussian (the map is linear, so
+// summing the moments over instances first is exact).
+// Record slots: 0 SGx, 1 SGy, 2 SGxx, 3 SGxy, 4 SGyy, 5 SG, 6-8 sum w g_rgb, 9 sum w g_invdepth.
+struct PairState {
+    v2f T, S, g0, g1, g2, gd, ntb;  // transmittance, ar.g, dL/dpixel, dL/dinvdepth, -T_final (bg.g)
+    int last0, last1;
+    float py;
+};
+struct SplatAcc {
+    v2f SG, SGx, SGy, SGxx, SGxy, SGyy, C0, C1, C2, CD;
+};
+
+template <bool HAS_INVD, bool HAS_BG>
+__device__ __forceinline__ bool bwd_pair(PairState& P, SplatAcc& acc, const v2f pxv, int sidx, float sx, float sy,
+                                         float a2, float b2, float c2, float so, float sr, float sg, float sbl, float si) {
+    const v2f dx = bc2(sx) - pxv;
+    const float dy = sy - P.py;
+    const v2f p2 = splat_power2(a2, b2, c2, dx, dy);
+    const v2f G = {__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y)};
+    v2f al = bc2(so) * G;
+    al.x = fminf(0.99f, al.x);
+    al.y = fminf(0.99f, al.y);
+    const bool ok0 = (sidx < P.last0) && !(p2.x > 0.0f) && !(al.x < (1.0f / 255.0f));
+    const bool ok1 = (sidx < P.last1) && !(p2.y > 0.0f) && !(al.y < (1.0f / 255.0f));
+    al.x = ok0 ? al.x : 0.0f;
+    al.y = ok1 ? al.y : 0.0f;
+    const v2f wgt = al * P.T;
+    const v2f oma = bc2(1.0f) - al;
+    const v2f inv = {__builtin_amdgcn_rcpf(oma.x), __builtin_amdgcn_rcpf(oma.y)};
+    v2f cg = fma2(bc2(sbl), P.g2, fma2(bc2(sg), P.g1, bc2(sr) * P.g0));
+    if (HAS_INVD) cg = fma2(bc2(si), P.gd, cg);
+    P.S = fma2(wgt, cg, P.S);
+    v2f dLda = fma2(cg, P.T, inv * P.S);
+    if (HAS_BG) dLda = fma2(P.ntb, inv, dLda);
+    dLda.x = ok0 ? dLda.x : 0.0f;
+    dLda.y = ok1 ? dLda.y : 0.0f;
+    P.T = P.T * oma;
+    acc.C0 = fma2(wgt, P.g0, acc.C0);
+    acc.C1 = fma2(wgt, P.g1, acc.C1);
+    acc.C2 = fma2(wgt, P.g2, acc.C2);
+    if (HAS_INVD) acc.CD = fma2(wgt, P.gd, acc.CD);
+    const v2f t = G * dLda;
+    const v2f vdy = bc2(dy);
+    acc.SG = acc.SG + t;
+    acc.SGx = fma2(t, dx, acc.SGx);
+    acc.SGy = fma2(t, vdy, acc.SGy);
+    const v2f tdx = t * dx;
+    acc.SGxx = fma2(tdx, dx, acc.SGxx);
+    acc.SGxy = fma2(tdx, vdy, acc.SGxy);
+    acc.SGyy = fma2(t * vdy, vdy, acc.SGyy);
+    return ok0 || ok1;
+}
+
 template <bool HAS_INVD, bool HAS_BG>
 __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile, int lane, float4* sb) {
     const uint2 rg = a.ranges[tile];
@@ -78,35 +140,47 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
     const int tx0 = tx * GS_TILE_X, ty0 = ty * GS_TILE_Y;
     const size_t HW = (size_t)a.W * a.H;
     const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
-    const float hw = 0.5f * a.W, hh = 0.5f * a.H;
-    float T[4], ar0[4], ar1[4], ar2[4], ard[4], Tf[4], d0[4], d1[4], d2[4], dd[4], bgdot[4], pxf[4], pyf[4];
-    int last[4], qlast[4];
+    const v2f pxv = {(float)(tx0 + (lane & 7)), (float)(tx0 + (lane & 7) + 8)};
+    PairState PA, PB;
+    int qlast[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int px = tx0 + (k & 1) * 8 + (lane & 7), py = ty0 + (k >> 1) * 8 + (lane >> 3);
-        pxf[k] = (float)px;
-        pyf[k] = (float)py;
-        T[k] = 1.0f;
-        if (px < a.W && py < a.H) {
-            const size_t pid = (size_t)py * a.W + px;
-            last[k] = (int)a.n_contrib[pid];
-            ar0[k] = -a.img_color[pid]; ar1[k] = -a.img_color[HW + pid]; ar2[k] = -a.img_color[2 * HW + pid];
-            ard[k] = HAS_INVD ? -a.img_invd[pid] : 0.0f;
-            Tf[k] = a.final_T[pid];
-            d0[k] = a.dL_dpix[pid]; d1[k] = a.dL_dpix[HW + pid]; d2[k] = a.dL_dpix[2 * HW + pid];
-            dd[k] = HAS_INVD ? a.dL_dinvd[pid] : 0.0f;
-        } else {
-            last[k] = 0;
-            ar0[k] = ar1[k] = ar2[k] = ard[k] = Tf[k] = d0[k] = d1[k] = d2[k] = dd[k] = 0.0f;
-        }
-        bgdot[k] = HAS_BG ? fmaf(bg2, d2[k], fmaf(bg1, d1[k], bg0 * d0[k])) : 0.0f;
-        int m = last[k];
+    for (int h = 0; h < 2; h++) {
+        PairState& P = h ? PB : PA;
+        const int py = ty0 + h * 8 + (lane >> 3);
+        P.py = (float)py;
+        P.T = bc2(1.0f);
+        float S[2], g0[2], g1[2], g2[2], gd[2], ntb[2];
+        int last[2];
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const int y = __shfl_xor(m, o);
-            m = y > m ? y : m;
+        for (int c = 0; c < 2; c++) {
+            const int px = tx0 + (lane & 7) + 8 * c;
+            if (px < a.W && py < a.H) {
+                const size_t pid = (size_t)py * a.W + px;
+                last[c] = (int)a.n_contrib[pid];
+                g0[c] = a.dL_dpix[pid]; g1[c] = a.dL_dpix[HW + pid]; g2[c] = a.dL_dpix[2 * HW + pid];
+                gd[c] = HAS_INVD ? a.dL_dinvd[pid] : 0.0f;
+                // ar starts at -(final pixel colour) (backward.cu:538-546); S = ar . g
+                float s0 = -(fmaf(a.img_color[2 * HW + pid], g2[c], fmaf(a.img_color[HW + pid], g1[c], a.img_color[pid] * g0[c])));
+                if (HAS_INVD) s0 = fmaf(-a.img_invd[pid], gd[c], s0);
+                S[c] = s0;
+                const float Tf = a.final_T[pid];
+                ntb[c] = HAS_BG ? -Tf * fmaf(bg2, g2[c], fmaf(bg1, g1[c], bg0 * g0[c])) : 0.0f;
+            } else {
+                last[c] = 0;
+                S[c] = g0[c] = g1[c] = g2[c] = gd[c] = ntb[c] = 0.0f;
+            }
+            int m = last[c];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const int y = __shfl_xor(m, o);
+                m = y > m ? y : m;
+            }
+            qlast[2 * h + c] = __builtin_amdgcn_readfirstlane(m);
         }
-        qlast[k] = __builtin_amdgcn_readfirstlane(m);
+        P.S = (v2f){S[0], S[1]};
+        P.g0 = (v2f){g0[0], g0[1]}; P.g1 = (v2f){g1[0], g1[1]}; P.g2 = (v2f){g2[0], g2[1]};
+        P.gd = (v2f){gd[0], gd[1]}; P.ntb = (v2f){ntb[0], ntb[1]};
+        P.last0 = last[0]; P.last1 = last[1];
     }
     for (int base = 0; base < n; base += 64) {
         const int j = base + lane;
@@ -121,72 +195,34 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
             qm = quad_mask({c4.x, c4.y, c4.z, c4.w}, m.x, m.y, thr, tx0, ty0);
 #pragma unroll
             for (int k = 0; k < 4; k++) qm &= (j < qlast[k]) ? 0xfu : ~(1u << k);
-            sb[lane * 4 + 0] = make_float4(m.x, m.y, c4.x * LOG2E, c4.y * LOG2E);
-            sb[lane * 4 + 1] = make_float4(c4.z * LOG2E, c4.w, q.x, q.y);
-            sb[lane * 4 + 2] = make_float4(q.z, q.w, c4.x, c4.y);
-            sb[lane * 4 + 3] = make_float4(c4.z, __uint_as_float(ee), __uint_as_float(qm), 0.0f);
+            sb[lane * 3 + 0] = make_float4(m.x, m.y, c4.x * LOG2E, c4.y * LOG2E);
+            sb[lane * 3 + 1] = make_float4(c4.z * LOG2E, c4.w, q.x, q.y);
+            sb[lane * 3 + 2] = make_float4(q.z, q.w, __uint_as_float(ee), __uint_as_float(qm));
         }
         __builtin_amdgcn_wave_barrier();
         uint64_t smask = __ballot(qm != 0u);
         while (smask) {
             const int jj = __ffsll((unsigned long long)smask) - 1;
             smask &= smask - 1;
-            const float4 A = sb[jj * 4 + 0], B = sb[jj * 4 + 1], Cc = sb[jj * 4 + 2], Dv = sb[jj * 4 + 3];
-            const uint32_t m = __builtin_amdgcn_readfirstlane(__float_as_uint(Dv.z));
-            const float sx = A.x, sy = A.y, a2 = A.z, b2 = A.w, c2 = B.x, so = B.y, sr = B.z, sg = B.w;
-            const float sbl = Cc.x, si = HAS_INVD ? Cc.y : 0.0f, sa = Cc.z, sbb = Cc.w, sc = Dv.x;
+            const float4 A = sb[jj * 3 + 0], B = sb[jj * 3 + 1], Cc = sb[jj * 3 + 2];
+            const uint32_t m = __builtin_amdgcn_readfirstlane(__float_as_uint(Cc.w));
             const int sidx = base + jj;
-            float p[10];
-#pragma unroll
-            for (int v = 0; v < 10; v++) p[v] = 0.0f;
-            float anyf = 0.0f;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                if (!((m >> k) & 1u)) continue;  // wave-uniform
-                const float dx = sx - pxf[k], dy = sy - pyf[k];
-                const float p2 = splat_power(a2, b2, c2, dx, dy);
-                const float G = __builtin_amdgcn_exp2f(p2);
-                float alpha = fminf(0.99f, so * G);
-                const bool act = (sidx < last[k]) && !(p2 > 0.0f) && !(alpha < (1.0f / 255.0f));
-                const float actf = act ? 1.0f : 0.0f;
-                alpha = alpha * actf;
-                anyf += actf;
-                const float weight = alpha * T[k];
-                const float oma = 1.0f - alpha;
-                const float inv = __builtin_amdgcn_rcpf(oma);
-                ar0[k] = fmaf(weight, sr, ar0[k]);
-                ar1[k] = fmaf(weight, sg, ar1[k]);
-                ar2[k] = fmaf(weight, sbl, ar2[k]);
-                p[6] = fmaf(weight, d0[k], p[6]);
-                p[7] = fmaf(weight, d1[k], p[7]);
-                p[8] = fmaf(weight, d2[k], p[8]);
-                float dLda = fmaf(sr, T[k], inv * ar0[k]) * d0[k];
-                dLda = fmaf(fmaf(sg, T[k], inv * ar1[k]), d1[k], dLda);
-                dLda = fmaf(fmaf(sbl, T[k], inv * ar2[k]), d2[k], dLda);
-                if (HAS_INVD) {
-                    ard[k] = fmaf(weight, si, ard[k]);
-                    p[9] = fmaf(weight, dd[k], p[9]);
-                    dLda = fmaf(fmaf(si, T[k], inv * ard[k]), dd[k], dLda);
-                }
-                if (HAS_BG) dLda = fmaf(-Tf[k] * inv, bgdot[k], dLda);
-                dLda = dLda * actf;
-                T[k] = T[k] * oma;
-                const float dL_dG = so * dLda;
-                const float gdx = G * dx, gdy = G * dy;
-                const float dG_ddelx = fmaf(-gdx, sa, -(gdy * sbb));
-                const float dG_ddely = fmaf(-gdy, sc, -(gdx * sbb));
-                p[0] = fmaf(dL_dG * dG_ddelx, hw, p[0]);
-                p[1] = fmaf(dL_dG * dG_ddely, hh, p[1]);
-                const float h = -0.5f * dL_dG;
-                p[2] = fmaf(gdx * dx, h, p[2]);
-                p[3] = fmaf(gdx * dy, h, p[3]);
-                p[4] = fmaf(gdy * dy, h, p[4]);
-                p[5] = fmaf(G, dLda, p[5]);
-            }
-            if (__any(anyf > 0.0f)) {
+            SplatAcc acc;
+            acc.SG = acc.SGx = acc.SGy = acc.SGxx = acc.SGxy = acc.SGyy = bc2(0.0f);
+            acc.C0 = acc.C1 = acc.C2 = acc.CD = bc2(0.0f);
+            bool act = false;
+            if (m & 3u)
+                act |= bwd_pair<HAS_INVD, HAS_BG>(PA, acc, pxv, sidx, A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, Cc.x, Cc.y);
+            if (m & 12u)
+                act |= bwd_pair<HAS_INVD, HAS_BG>(PB, acc, pxv, sidx, A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, Cc.x, Cc.y);
+            if (__any(act)) {
+                const float p[10] = {acc.SGx.x + acc.SGx.y, acc.SGy.x + acc.SGy.y, acc.SGxx.x + acc.SGxx.y,
+                                     acc.SGxy.x + acc.SGxy.y, acc.SGyy.x + acc.SGyy.y, acc.SG.x + acc.SG.y,
+                                     acc.C0.x + acc.C0.y, acc.C1.x + acc.C1.y, acc.C2.x + acc.C2.y,
+                                     HAS_INVD ? acc.CD.x + acc.CD.y : 0.0f};
                 int slot;
                 const float tot = wave_reduce10(p, lane, slot);
-                const uint32_t e = __builtin_amdgcn_readfirstlane(__float_as_uint(Dv.y));
+                const uint32_t e = __builtin_amdgcn_readfirstlane(__float_as_uint(Cc.z));
                 if (slot >= 0) a.rec[(size_t)e * 12 + slot] = tot;
                 if (lane == 0) a.flag[e] = 1;
             }
@@ -196,7 +232,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
 }
 
 __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
-    __shared__ float4 s_b[4][64][4];
+    __shared__ float4 s_b[4][64][3];
     const int lane = threadIdx.x & 63;
     const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (tile >= a.num_tiles) return;
@@ -226,6 +262,78 @@ __global__ void __launch_bounds__(256) k_any_nonzero(const float* __restrict__ x
 __device__ __forceinline__ float sq(float x) { return x * x; }
 
 __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, float* lsh);
+
+// Sum each Gaussian's instance records (written by k_render_bwd at emission slots [first_e, first_e + cnt)
+// whose flag is set) into sums[idx].  A wave owns 64 consecutive Gaussians; their instances are walked
+// flattened, 64 per step (flag reads coalesced, no lane waits on the longest list), each step's flagged
+// records are parked in LDS, and every owner lane folds its own ones in increasing emission order --
+// the same sequential order as the reference-side sum, so the result is deterministic.
+__global__ void __launch_bounds__(256) k_record_sum(GaussBwdArgs a) {
+    __shared__ uint32_t s_pre[4][64];
+    __shared__ uint32_t s_e0[4][64];
+    __shared__ float4 s_rec[4][64][3];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    float acc[10];
+#pragma unroll
+    for (int v = 0; v < 10; v++) acc[v] = 0.f;
+    uint32_t c = 0, e0 = 0;
+    if (idx < a.P && a.radii[idx] > 0) {
+        c = a.cnt[idx];
+        e0 = c ? a.first_e[idx] : 0u;
+        if (e0 >= a.K || c > a.K - e0) c = 0;  // defensive: never read outside the record block
+    }
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t mybeg = incl - c;
+    s_pre[w][lane] = mybeg;
+    s_e0[w][lane] = e0;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i0 = 0; i0 < total; i0 += 64) {
+        const uint32_t item = i0 + (uint32_t)lane;
+        bool f = false;
+        if (item < total) {
+            int lo = 0;
+#pragma unroll
+            for (int step = 32; step > 0; step >>= 1)
+                if (s_pre[w][lo + step] <= item) lo += step;
+            const uint32_t e = s_e0[w][lo] + (item - s_pre[w][lo]);
+            f = a.flag[e] != 0;
+            if (f) {
+                const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
+                s_rec[w][lane][0] = r[0];
+                s_rec[w][lane][1] = r[1];
+                s_rec[w][lane][2] = r[2];
+            }
+        }
+        const uint64_t fm = __ballot(f);
+        __builtin_amdgcn_wave_barrier();
+        // this lane's items within the step: [lo, hi) relative to i0
+        const uint32_t lo = mybeg > i0 ? mybeg - i0 : 0u;
+        const uint32_t end = mybeg + c;
+        const uint32_t hi = end < i0 + 64 ? (end > i0 ? end - i0 : 0u) : 64u;
+        uint64_t m = 0;
+        if (hi > lo) m = fm & ((hi == 64 ? ~0ull : ((1ull << hi) - 1ull)) & (~0ull << lo));
+        while (m) {
+            const int b = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            const float4 r0 = s_rec[w][b][0], r1 = s_rec[w][b][1], r2 = s_rec[w][b][2];
+            acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w; acc[4] += r1.x;
+            acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w; acc[8] += r2.x; acc[9] += r2.y;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (idx < a.P) {
+        a.sums[3 * (size_t)idx + 0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        a.sums[3 * (size_t)idx + 1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+        a.sums[3 * (size_t)idx + 2] = make_float4(acc[8], acc[9], 0.f, 0.f);
+    }
+}
 
 // Block of 256 Gaussians; the [256][M][3] SH slab is staged through LDS so both the coefficient loads
 // and the dL/dsh stores are coalesced (a per-thread 180-B stride touches 64 lines per wave instruction).
@@ -273,30 +381,23 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
         for (int v = 0; v < 3 * M; v++) lsh[v] = 0.f;
         return;
     }
-    // ---- records -> dL/d(mean2D, conic, opacity, color, invdepth); flags read 4 at a time
+    // ---- records -> dL/d(mean2D, conic, opacity, color, invdepth): summed by the wave (see below)
     float acc[10];
-#pragma unroll
-    for (int v = 0; v < 10; v++) acc[v] = 0.f;
     {
-        uint32_t c = a.cnt[idx];
-        const uint32_t e0 = c ? a.first_e[idx] : 0u;
-        if (e0 >= a.K || c > a.K - e0) c = 0;  // defensive: never read outside the record block
-        const uint32_t e1 = e0 + c;
-        for (uint32_t w = e0 & ~3u; w < e1; w += 4) {
-            uint32_t f4 = *reinterpret_cast<const uint32_t*>(a.flag + w);
-            if (w < e0) f4 &= 0xffffffffu << (8 * (e0 - w));
-            if (e1 - w < 4) f4 &= 0xffffffffu >> (8 * (4 - (e1 - w)));
-            while (f4) {
-                const int b = (__ffs(f4) - 1) >> 3;
-                f4 &= ~(0xffu << (8 * b));
-                const uint32_t e = w + b;
-                const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
-                const float4 r0 = r[0], r1 = r[1], r2 = r[2];
-                acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
-                acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
-                acc[8] += r2.x; acc[9] += r2.y;
-            }
-        }
+        const float4 s0 = a.sums[3 * (size_t)idx + 0], s1 = a.sums[3 * (size_t)idx + 1], s2 = a.sums[3 * (size_t)idx + 2];
+        acc[0] = s0.x; acc[1] = s0.y; acc[2] = s0.z; acc[3] = s0.w; acc[4] = s1.x;
+        acc[5] = s1.y; acc[6] = s1.z; acc[7] = s1.w; acc[8] = s2.x; acc[9] = s2.y;
+    }
+    // moments -> dL/dmean2D, dL/dconic (see render_bwd_tile); o = the AA-scaled opacity of the forward
+    {
+        const float4 c4 = a.co[idx];
+        const float SGx = acc[0], SGy = acc[1], SGxx = acc[2], SGxy = acc[3], SGyy = acc[4];
+        const float so = c4.w;
+        acc[0] = -(0.5f * a.W) * (so * fmaf(c4.x, SGx, c4.y * SGy));
+        acc[1] = -(0.5f * a.H) * (so * fmaf(c4.z, SGy, c4.y * SGx));
+        acc[2] = (-0.5f * so) * SGxx;
+        acc[3] = (-0.5f * so) * SGxy;
+        acc[4] = (-0.5f * so) * SGyy;
     }
     a.dmeans2D[3 * idx + 0] = acc[0];
     a.dmeans2D[3 * idx + 1] = acc[1];
@@ -527,6 +628,9 @@ void launch_render_bwd(const RenderBwdArgs& a, uint32_t* invd_flag, hipStream_t 
     RenderBwdArgs b = a;
     b.invd_nonzero = invd_flag;
     if (a.num_tiles > 0) k_render_bwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(b);
+}
+void launch_record_sum(const GaussBwdArgs& a, hipStream_t s) {
+    if (a.P > 0) k_record_sum<<<(a.P + 255) / 256, 256, 0, s>>>(a);
 }
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s) {
     const size_t lds = (size_t)256 * (a.M > 0 ? a.M : 0) * 3 * sizeof(float);

@@ -9,8 +9,10 @@
 //   tile sort      stable radix sort by tile id only; input order is (depth, index) so the result is the
 //                  reference's (tile, depth bits, index) order, bit for bit
 //   k_ranges       per-tile [start, end)
-//   k_render_fwd   one wave64 per 16x16 tile, 4 pixels per lane; a batch of 64 splats is held one per
-//                  lane and broadcast with v_readlane (no LDS, no block barriers); wave-uniform early exit.
+//   k_render_fwd   two waves per 16x16 tile (one per 16x8 half), 2 pixels of one row per lane evaluated
+//                  with packed fp32 (v_pk_*_f32); a 64-splat batch is staged in wave-private LDS and read
+//                  back with broadcast ds_read_b128, splats whose quadrant pair cannot reach the half are
+//                  skipped by ballot; wave-uniform early exit once every pixel has saturated.
 #include <hip/hip_runtime.h>
 #include "gs_common.h"
 #include "raster.h"
@@ -335,24 +337,28 @@ __device__ __forceinline__ uint32_t bcast_u(uint32_t v, int lane) {
 // (s_ff1 over a 64-bit ballot) and reads each one with broadcast ds_read_b128.  The per-pixel update is
 // branch-free: a rejected or finished pixel gets alpha = 0, which leaves C, D and T bit-identical.
 // The conic is prescaled by log2(e) at staging so the exponential is a bare v_exp_f32.
-__global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a) {
-    __shared__ float4 s_b[4][64][3];
-    __shared__ uint32_t s_mx[4];
+__global__ void __launch_bounds__(128) k_render_fwd(RenderArgs a) {
+    __shared__ float4 s_b[2][64][3];
+    __shared__ uint32_t s_mx[2];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tile = blockIdx.x;
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
-    const int px = tx * GS_TILE_X + (w & 1) * 8 + (lane & 7);
-    const int py = ty * GS_TILE_Y + (w >> 1) * 8 + (lane >> 3);
-    const int qx0 = tx * GS_TILE_X + (w & 1) * 8, qy0 = ty * GS_TILE_Y + (w >> 1) * 8;
-    const float pxf = (float)px, pyf = (float)py;
-    const bool inside = px < a.W && py < a.H;
-    float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f, Dd = 0.0f, live = inside ? 1.0f : 0.0f;
-    uint32_t last = 0;
+    const int tx0 = tx * GS_TILE_X, ty0 = ty * GS_TILE_Y;
+    // wave w renders tile rows [8w, 8w+8); lane owns pixels (lane&7) and (lane&7)+8 of row lane>>3, i.e.
+    // the same pixel of quadrants 2w and 2w+1 -- one row, so dy and c*dy^2 are shared by the pair
+    const int px0 = tx0 + (lane & 7), px1 = px0 + 8;
+    const int py = ty0 + w * 8 + (lane >> 3);
+    const v2f pxv = {(float)px0, (float)px1};
+    const float pyf = (float)py;
+    const bool in0 = px0 < a.W && py < a.H, in1 = px1 < a.W && py < a.H;
+    v2f T = bc2(1.0f), C0 = bc2(0.0f), C1 = bc2(0.0f), C2 = bc2(0.0f), Dd = bc2(0.0f);
+    bool live0 = in0, live1 = in1;
+    uint32_t last0 = 0, last1 = 0;
     const uint2 rg = a.ranges[tile];
     const int n = (int)(rg.y - rg.x);
     float4* sb = &s_b[w][0][0];
     for (int base = 0; base < n; base += 64) {
-        if (!__any(live != 0.0f)) break;
+        if (!__any(live0 || live1)) break;
         const int j = base + lane;
         bool touch = false;
         if (j < n) {
@@ -362,7 +368,7 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a) {
             const float4 c4 = a.co[g];
             const float4 q = a.rgbi[g];
             const float thr = gs_logf(c4.w / (1.0f / 255.0f));
-            touch = (quad_mask({c4.x, c4.y, c4.z, c4.w}, m.x, m.y, thr, qx0 & ~15, qy0 & ~15) >> w) & 1u;
+            touch = ((quad_mask({c4.x, c4.y, c4.z, c4.w}, m.x, m.y, thr, tx0, ty0) >> (2 * w)) & 3u) != 0u;
             sb[lane * 3 + 0] = make_float4(m.x, m.y, c4.x * LOG2E, c4.y * LOG2E);
             sb[lane * 3 + 1] = make_float4(c4.z * LOG2E, c4.w, q.x, q.y);
             sb[lane * 3 + 2] = make_float4(q.z, q.w, 0.0f, 0.0f);
@@ -373,40 +379,55 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a) {
             const int jj = __ffsll((unsigned long long)mask) - 1;
             mask &= mask - 1;
             const float4 A = sb[jj * 3 + 0], B = sb[jj * 3 + 1], Cc = sb[jj * 3 + 2];
-            const float dx = A.x - pxf, dy = A.y - pyf;
-            const float p2 = splat_power(A.z, A.w, B.x, dx, dy);
-            float alpha = fminf(0.99f, B.y * __builtin_amdgcn_exp2f(p2));
-            alpha = (p2 > 0.0f) ? 0.0f : alpha;
-            alpha = (alpha < (1.0f / 255.0f)) ? 0.0f : alpha;
-            alpha = alpha * live;
-            const float test_T = T * (1 - alpha);
-            const bool term = test_T < 0.0001f;
-            live = term ? 0.0f : live;
-            alpha = term ? 0.0f : alpha;
-            C0 = fmaf(B.z * alpha, T, C0);
-            C1 = fmaf(B.w * alpha, T, C1);
-            C2 = fmaf(Cc.x * alpha, T, C2);
-            Dd = fmaf(Cc.y * alpha, T, Dd);
-            T = term ? T : test_T;
-            last = (alpha > 0.0f) ? (uint32_t)(base + jj + 1) : last;
-            if (!__any(live != 0.0f)) break;
+            const v2f dx = bc2(A.x) - pxv;
+            const float dy = A.y - pyf;
+            const v2f p2 = splat_power2(A.z, A.w, B.x, dx, dy);
+            v2f al = bc2(B.y) * (v2f){__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y)};
+            al.x = fminf(0.99f, al.x);
+            al.y = fminf(0.99f, al.y);
+            // forward.cu:451-475: skip power > 0 and alpha < 1/255, stop once T would fall below 1e-4
+            const bool ok0 = live0 && !(p2.x > 0.0f) && !(al.x < (1.0f / 255.0f));
+            const bool ok1 = live1 && !(p2.y > 0.0f) && !(al.y < (1.0f / 255.0f));
+            al.x = ok0 ? al.x : 0.0f;
+            al.y = ok1 ? al.y : 0.0f;
+            const v2f test_T = T * (bc2(1.0f) - al);
+            const bool t0 = test_T.x < 0.0001f, t1 = test_T.y < 0.0001f;
+            live0 = live0 && !t0;
+            live1 = live1 && !t1;
+            al.x = t0 ? 0.0f : al.x;
+            al.y = t1 ? 0.0f : al.y;
+            C0 = fma2(bc2(B.z) * al, T, C0);
+            C1 = fma2(bc2(B.w) * al, T, C1);
+            C2 = fma2(bc2(Cc.x) * al, T, C2);
+            Dd = fma2(bc2(Cc.y) * al, T, Dd);
+            T.x = t0 ? T.x : test_T.x;
+            T.y = t1 ? T.y : test_T.y;
+            const uint32_t c = (uint32_t)(base + jj + 1);
+            last0 = (ok0 && !t0) ? c : last0;
+            last1 = (ok1 && !t1) ? c : last1;
+            if (!__any(live0 || live1)) break;
         }
         __builtin_amdgcn_wave_barrier();
     }
+    const size_t HW = (size_t)a.W * a.H;
     uint32_t mx = 0;
-    if (inside) {
-        const size_t HW = (size_t)a.W * a.H;
-        const size_t pid = (size_t)py * a.W + px;
-        a.final_T[pid] = T;
-        a.n_contrib[pid] = last;
-        const float o0 = fmaf(T, a.bg[0], C0);
-        const float o1 = fmaf(T, a.bg[1], C1);
-        const float o2 = fmaf(T, a.bg[2], C2);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        if (!(h ? in1 : in0)) continue;
+        const size_t pid = (size_t)py * a.W + (h ? px1 : px0);
+        const float Th = h ? T.y : T.x;
+        const uint32_t lh = h ? last1 : last0;
+        a.final_T[pid] = Th;
+        a.n_contrib[pid] = lh;
+        const float o0 = fmaf(Th, a.bg[0], h ? C0.y : C0.x);
+        const float o1 = fmaf(Th, a.bg[1], h ? C1.y : C1.x);
+        const float o2 = fmaf(Th, a.bg[2], h ? C2.y : C2.x);
         a.out_color[pid] = o0; a.out_color[HW + pid] = o1; a.out_color[2 * HW + pid] = o2;
         a.img_color[pid] = o0; a.img_color[HW + pid] = o1; a.img_color[2 * HW + pid] = o2;
-        a.out_invd[pid] = Dd;
-        a.img_invd[pid] = Dd;
-        mx = last;
+        const float dh = h ? Dd.y : Dd.x;
+        a.out_invd[pid] = dh;
+        a.img_invd[pid] = dh;
+        mx = lh > mx ? lh : mx;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -415,11 +436,7 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a) {
     }
     if (lane == 0) s_mx[w] = mx;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t m0 = s_mx[0] > s_mx[1] ? s_mx[0] : s_mx[1];
-        const uint32_t m1 = s_mx[2] > s_mx[3] ? s_mx[2] : s_mx[3];
-        a.max_contrib[tile] = m0 > m1 ? m0 : m1;
-    }
+    if (threadIdx.x == 0) a.max_contrib[tile] = s_mx[0] > s_mx[1] ? s_mx[0] : s_mx[1];
 }
 
 // checkFrustum (rasterizer_impl.cu:104-116)
@@ -482,7 +499,7 @@ void launch_ranges(uint32_t K, const uint32_t* keys, uint2* ranges, uint32_t num
     if (K > 0) k_ranges<<<(K + 255) / 256, 256, 0, s>>>(K, keys, ranges, num_tiles);
 }
 void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
-    if (a.num_tiles > 0) k_render_fwd<<<a.num_tiles, 256, 0, s>>>(a);
+    if (a.num_tiles > 0) k_render_fwd<<<a.num_tiles, 128, 0, s>>>(a);
 }
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s) {
     if (P > 0) k_mark_visible<<<(P + 255) / 256, 256, 0, s>>>(P, means3D, view, present);
