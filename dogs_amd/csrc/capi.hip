@@ -89,8 +89,7 @@ inline int bits_for(uint32_t n) {  // bits needed for ids in [0, n)
 
 struct Geom {
     uint32_t* counters;  // [0] K total, [1] err, [2..3] u64 rect sum
-    float2* xy;
-    float4* co;
+    float4* sp;  // 2 per Gaussian (raster.h)
     float4* rgbi;
     uint32_t *k0, *v0, *k1, *v1, *cnt, *first_e, *off;
     void* sort_tmp;
@@ -102,8 +101,7 @@ Geom carve_geom(void* base, int P) {
     Geom g;
     const size_t n = (size_t)(P > 0 ? P : 1);
     g.counters = c.take<uint32_t>(16);
-    g.xy = c.take<float2>(n);
-    g.co = c.take<float4>(n);
+    g.sp = c.take<float4>(2 * n);
     g.rgbi = c.take<float4>(n);
     g.k0 = c.take<uint32_t>(n);
     g.v0 = c.take<uint32_t>(n);
@@ -300,17 +298,19 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     HIP_OK(hipMemsetAsync(g.counters, 0, 64, s));
     gs::PreArgs pre;
     fill_pre(pre, a);
-    pre.radii = radii; pre.xy = g.xy; pre.co = g.co; pre.rgbi = g.rgbi; pre.depthkey = g.k0; pre.cnt = g.cnt;
+    pre.radii = radii; pre.sp = g.sp; pre.rgbi = g.rgbi; pre.depthkey = g.k0; pre.cnt = g.cnt;
     pre.rect_sum = (unsigned long long*)(g.counters + 2); pre.err = g.counters + 1;
     { PROF("preprocess"); gs::launch_preprocess(pre, s); }
     DBG_SYNC(a->debug, s);
 
     // stable depth sort of (depth bits, index): 4 passes -> result back in k0/v0
     const uint32_t* order = g.v0;
+    const uint32_t* skey = g.k0;
     if (P > 0) {
         int which;
         { PROF("depth_sort"); which = gs::radix_sort_pairs(g.k0, g.v0, g.k1, g.v1, nullptr, (uint32_t)P, 0, 32, g.sort_tmp, s); }
         order = which ? g.v1 : g.v0;
+        skey = which ? g.k1 : g.k0;
         DBG_SYNC(a->debug, s);
         { PROF("count_scan"); gs::exclusive_scan(g.cnt, order, (uint32_t)P, g.off, g.counters, g.scan_tmp, s); }
         DBG_SYNC(a->debug, s);
@@ -332,7 +332,7 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     const uint32_t* s_e = b.se0;
     const uint32_t* s_keys = b.tk0;
     if (K > 0) {
-        { PROF("emit"); gs::launch_emit(P, order, g.cnt, g.off, g.xy, g.co, radii, tx, ty, g.first_e, b.tk0, b.eg, s); }
+        { PROF("emit"); gs::launch_emit(P, order, skey, g.off, g.sp, tx, g.first_e, b.tk0, b.eg, s); }
         DBG_SYNC(a->debug, s);
         int which;
         { PROF("tile_sort"); which = gs::radix_sort_pairs(b.tk0, b.se0, b.tk1, b.se1, nullptr, (uint32_t)K, 0,
@@ -351,7 +351,7 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     gs::RenderArgs r;
     r.W = W; r.H = H; r.tiles_x = tx; r.num_tiles = T;
     r.K = (uint32_t)(K > 0 ? K : 1); r.P = (uint32_t)(P > 0 ? P : 1);
-    r.ranges = im.ranges; r.s_e = s_e; r.eg = b.eg; r.xy = g.xy; r.co = g.co; r.rgbi = g.rgbi; r.bg = a->bg;
+    r.ranges = im.ranges; r.s_e = s_e; r.eg = b.eg; r.sp = g.sp; r.rgbi = g.rgbi; r.bg = a->bg;
     r.out_color = out_color; r.out_invd = out_invdepth; r.final_T = im.final_T; r.img_color = im.img_color;
     r.img_invd = im.img_invd; r.n_contrib = im.n_contrib; r.max_contrib = im.max_contrib;
     { PROF("render_fwd"); gs::launch_render_fwd(r, s); }
@@ -387,7 +387,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
         r.W = W; r.H = H; r.tiles_x = tx; r.num_tiles = T;
         r.K = (uint32_t)K; r.P = (uint32_t)P;
         r.ranges = im.ranges; r.max_contrib = im.max_contrib; r.s_e = s_e; r.eg = b.eg;
-        r.xy = g.xy; r.co = g.co; r.rgbi = g.rgbi; r.bg = a->bg;
+        r.sp = g.sp; r.rgbi = g.rgbi; r.bg = a->bg;
         r.final_T = im.final_T; r.img_color = im.img_color; r.img_invd = im.img_invd; r.n_contrib = im.n_contrib;
         r.dL_dpix = dL_dout_color; r.dL_dinvd = dL_dout_invdepth; r.rec = sc.rec; r.flag = sc.flag;
         r.invd_nonzero = nullptr;
@@ -405,7 +405,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     q.means3D = a->means3D; q.scales = a->scales; q.rotations = a->rotations; q.opacities = a->opacities;
     q.dc = a->dc; q.sh = (a->M > 0) ? a->sh : nullptr; q.cov3D_precomp = a->cov3D_precomp;
     q.view = a->viewmatrix; q.proj = a->projmatrix; q.campos = a->campos;
-    q.radii = radii; q.cnt = g.cnt; q.first_e = g.first_e; q.co = g.co; q.rec = sc.rec; q.flag = sc.flag; q.sums = sc.sums;
+    q.radii = radii; q.cnt = g.cnt; q.first_e = g.first_e; q.sp = g.sp; q.rec = sc.rec; q.flag = sc.flag; q.sums = sc.sums;
     q.dmeans2D = dmeans2D; q.dcolors = dcolors; q.dopacity = dopacity; q.dmeans3D = dmeans3D; q.dcov3D = dcov3D;
     q.ddc = ddc; q.dsh = dsh; q.dscales = dscales; q.drot = drot; q.depth = depth;
     if (q.M > 0 && !dsh) return fail("dsh output required when M > 0%s%d");
@@ -506,8 +506,9 @@ int dg_debug_geometry(const void* geom, int P, float* means2D, float* conic_opac
     if (P <= 0) return 0;
     hipStream_t s = (hipStream_t)stream;
     Geom g = carve_geom((void*)geom, P);
-    if (means2D) HIP_OK(hipMemcpyAsync(means2D, g.xy, 8 * (size_t)P, hipMemcpyDeviceToDevice, s));
-    if (conic_opacity) HIP_OK(hipMemcpyAsync(conic_opacity, g.co, 16 * (size_t)P, hipMemcpyDeviceToDevice, s));
+    if (means2D) HIP_OK(hipMemcpy2DAsync(means2D, 8, g.sp, 32, 8, (size_t)P, hipMemcpyDeviceToDevice, s));
+    if (conic_opacity)
+        HIP_OK(hipMemcpy2DAsync(conic_opacity, 16, (const char*)g.sp + 8, 32, 16, (size_t)P, hipMemcpyDeviceToDevice, s));
     if (rgb_invdepth) HIP_OK(hipMemcpyAsync(rgb_invdepth, g.rgbi, 16 * (size_t)P, hipMemcpyDeviceToDevice, s));
     if (tile_count) HIP_OK(hipMemcpyAsync(tile_count, g.cnt, 4 * (size_t)P, hipMemcpyDeviceToDevice, s));
     return 0;

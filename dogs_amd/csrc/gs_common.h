@@ -203,13 +203,39 @@ __device__ __forceinline__ float splat_power(float cx, float cy, float cz, float
 }
 
 // Two pixels of one row (same dy) at once: ext_vector_type(2) arithmetic lowers to gfx950's packed
-// v_pk_{fma,mul,add}_f32 (two fp32 lanes per VALU issue), each half bitwise equal to splat_power.
+// v_pk_{fma,mul,add}_f32.  On gfx950 a packed op issues in ~5 cycles for both halves whether or not it
+// depends on the previous instruction, while a dependent plain fp32 op costs ~5 cycles for one value
+// (tools/ubench_valu.hip) -- so the serial per-pixel compositing chain runs packed.
 typedef float v2f __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ v2f bc2(float x) { return (v2f){x, x}; }
 __device__ __forceinline__ v2f fma2(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ v2f splat_power2(float cx, float cy, float cz, v2f dx, float dy) {
-    const float czdy = cz * dy;
-    return fma2(bc2(-0.5f), fma2(bc2(czdy), bc2(dy), (bc2(cx) * dx) * dx), -((bc2(cy) * dx) * bc2(dy)));
+
+// Compositing exponent in base 2 for both pixels of a row pair, as Horner form in dx with the row terms
+// shared:  p = dx (A dx + B dy) + C dy^2,  A = -a/2 log2 e, B = -b log2 e, C = -c/2 log2 e, which is the
+// reference's  -0.5 (a dx^2 + c dy^2) - b dx dy  (forward.cu:451, backward.cu:596) times log2 e.
+// Forward and backward evaluate exactly this expression, so the backward replay sees the forward's
+// alpha bit for bit; against a per-term evaluation only the last bits of p differ.
+struct SplatExp { float A, B, C; };
+__device__ __forceinline__ SplatExp splat_exp_coeffs(float ca, float cb, float cc) {
+    return {(-0.5f * LOG2E) * ca, -LOG2E * cb, (-0.5f * LOG2E) * cc};
+}
+__device__ __forceinline__ v2f splat_power2(float A, float B, float C, v2f dx, float dy) {
+    const float bdy = B * dy, cdy2 = (C * dy) * dy;
+    return fma2(dx, fma2(bc2(A), dx, bc2(bdy)), bc2(cdy2));
+}
+
+// Four pixels per lane as {(c0, rA), (c0, rB), (c1, rA), (c1, rB)}: two columns c0, c0 + 8 of two rows
+// rA, rA + 8.  Each packed op's halves are independent rows, and lo + hi gives the two row sums.
+typedef float v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4f bc4(float x) { return (v4f){x, x, x, x}; }
+__device__ __forceinline__ v4f fma4(v4f a, v4f b, v4f c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ v4f cat4(v2f lo, v2f hi) { return (v4f){lo.x, lo.y, hi.x, hi.y}; }
+// p = dx (A dx + B dy) + C dy^2 for the 4 pixels; identical per-pixel arithmetic to splat_power2
+__device__ __forceinline__ v4f splat_power4(float A, float B, float C, float sx, float sy, v4f pxv, v2f pyv) {
+    const v2f dy = bc2(sy) - pyv;
+    const v2f bdy = bc2(B) * dy, cdy2 = (bc2(C) * dy) * dy;
+    const v4f dx = bc4(sx) - pxv;
+    return fma4(dx, fma4(bc4(A), dx, cat4(bdy, bdy)), cat4(cdy2, cdy2));
 }
 
 }  // namespace gs

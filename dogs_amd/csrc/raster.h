@@ -5,6 +5,15 @@
 
 namespace gs {
 
+// Splat record: everything binning and compositing read per Gaussian, in ONE 32-B record so a
+// depth-ordered or instance-ordered gather touches one cache line instead of one per array.
+//   sp[2g]     = {mean2D.x, mean2D.y, conic.a, conic.b}
+//   sp[2g + 1] = {conic.c, opacity * AA scale, bits(x0 | x1 << 16), bits(y0 | y1 << 16)}   (tile rect)
+__device__ __forceinline__ void sp_rect(const float4& s1, int& x0, int& y0, int& x1, int& y1) {
+    const uint32_t rx = __float_as_uint(s1.z), ry = __float_as_uint(s1.w);
+    x0 = (int)(rx & 0xffffu); x1 = (int)(rx >> 16); y0 = (int)(ry & 0xffffu); y1 = (int)(ry >> 16);
+}
+
 struct PreArgs {
     int P, D, M, W, H, tiles_x, tiles_y;
     int antialiasing, prefiltered;
@@ -12,8 +21,7 @@ struct PreArgs {
     const float *means3D, *scales, *rotations, *opacities, *dc, *sh, *colors, *cov3D_precomp;
     const float *view, *proj, *campos;
     int* radii;
-    float2* xy;         // means2D
-    float4* co;         // conic (a, b, c), opacity * AA scale
+    float4* sp;         // splat record, 2 x float4 per Gaussian (see SP_* below)
     float4* rgbi;       // rgb, 1 / view z
     uint32_t* depthkey; // float bits of view z, 0xffffffff when no tile survives the precise cull
     uint32_t* cnt;      // precise tile count
@@ -27,8 +35,7 @@ struct RenderArgs {
     const uint2* ranges;
     const uint32_t* s_e;   // sorted instance -> emission index
     const uint32_t* eg;    // emission index -> Gaussian
-    const float2* xy;
-    const float4* co;
+    const float4* sp;
     const float4* rgbi;
     const float* bg;
     float *out_color, *out_invd, *final_T, *img_color, *img_invd;
@@ -42,8 +49,7 @@ struct RenderBwdArgs {
     const uint32_t* max_contrib;
     const uint32_t* s_e;
     const uint32_t* eg;
-    const float2* xy;
-    const float4* co;
+    const float4* sp;
     const float4* rgbi;
     const float* bg;
     const float *final_T, *img_color, *img_invd;
@@ -64,7 +70,7 @@ struct GaussBwdArgs {
     const int* radii;
     const uint32_t* cnt;
     const uint32_t* first_e;
-    const float4* co;        // forward conic + AA-scaled opacity
+    const float4* sp;        // splat records (conic + AA-scaled opacity)
     const float* rec;
     const uint8_t* flag;
     float4* sums;            // [P][3] record sums (k_record_sum -> k_gauss_bwd)
@@ -72,9 +78,8 @@ struct GaussBwdArgs {
 };
 
 void launch_preprocess(const PreArgs& a, hipStream_t s);
-void launch_emit(int P, const uint32_t* order, const uint32_t* cnt, const uint32_t* off, const float2* xy,
-                 const float4* co, const int* radii, int tiles_x, int tiles_y, uint32_t* first_e, uint32_t* tilekey,
-                 uint32_t* eg, hipStream_t s);
+void launch_emit(int P, const uint32_t* order, const uint32_t* skey, const uint32_t* off, const float4* sp,
+                 int tiles_x, uint32_t* first_e, uint32_t* tilekey, uint32_t* eg, hipStream_t s);
 void launch_ranges(uint32_t K, const uint32_t* keys, uint2* ranges, uint32_t num_tiles, hipStream_t s);
 void launch_render_fwd(const RenderArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);

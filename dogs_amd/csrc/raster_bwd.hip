@@ -90,10 +90,10 @@ struct SplatAcc {
 
 template <bool HAS_INVD, bool HAS_BG>
 __device__ __forceinline__ bool bwd_pair(PairState& P, SplatAcc& acc, const v2f pxv, int sidx, float sx, float sy,
-                                         float a2, float b2, float c2, float so, float sr, float sg, float sbl, float si) {
+                                         float eA, float eB, float eC, float so, float sr, float sg, float sbl, float si) {
     const v2f dx = bc2(sx) - pxv;
     const float dy = sy - P.py;
-    const v2f p2 = splat_power2(a2, b2, c2, dx, dy);
+    const v2f p2 = splat_power2(eA, eB, eC, dx, dy);
     const v2f G = {__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y)};
     v2f al = bc2(so) * G;
     al.x = fminf(0.99f, al.x);
@@ -188,15 +188,17 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
         if (j < n) {
             const uint32_t ee = min(a.s_e[rg.x + j], a.K - 1);
             const uint32_t g = min(a.eg[ee], a.P - 1);
-            const float2 m = a.xy[g];
-            const float4 c4 = a.co[g];
+            const float4 s0 = a.sp[2 * g], s1 = a.sp[2 * g + 1];
+            const float2 m = make_float2(s0.x, s0.y);
+            const float4 c4 = make_float4(s0.z, s0.w, s1.x, s1.y);
             const float4 q = a.rgbi[g];
             const float thr = gs_logf(c4.w / (1.0f / 255.0f));
             qm = quad_mask({c4.x, c4.y, c4.z, c4.w}, m.x, m.y, thr, tx0, ty0);
 #pragma unroll
             for (int k = 0; k < 4; k++) qm &= (j < qlast[k]) ? 0xfu : ~(1u << k);
-            sb[lane * 3 + 0] = make_float4(m.x, m.y, c4.x * LOG2E, c4.y * LOG2E);
-            sb[lane * 3 + 1] = make_float4(c4.z * LOG2E, c4.w, q.x, q.y);
+            const SplatExp k = splat_exp_coeffs(c4.x, c4.y, c4.z);
+            sb[lane * 3 + 0] = make_float4(m.x, m.y, k.A, k.B);
+            sb[lane * 3 + 1] = make_float4(k.C, c4.w, q.x, q.y);
             sb[lane * 3 + 2] = make_float4(q.z, q.w, __uint_as_float(ee), __uint_as_float(qm));
         }
         __builtin_amdgcn_wave_barrier();
@@ -205,16 +207,14 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
             const int jj = __ffsll((unsigned long long)smask) - 1;
             smask &= smask - 1;
             const float4 A = sb[jj * 3 + 0], B = sb[jj * 3 + 1], Cc = sb[jj * 3 + 2];
-            const uint32_t m = __builtin_amdgcn_readfirstlane(__float_as_uint(Cc.w));
             const int sidx = base + jj;
             SplatAcc acc;
             acc.SG = acc.SGx = acc.SGy = acc.SGxx = acc.SGxy = acc.SGyy = bc2(0.0f);
             acc.C0 = acc.C1 = acc.C2 = acc.CD = bc2(0.0f);
             bool act = false;
-            if (m & 3u)
-                act |= bwd_pair<HAS_INVD, HAS_BG>(PA, acc, pxv, sidx, A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, Cc.x, Cc.y);
-            if (m & 12u)
-                act |= bwd_pair<HAS_INVD, HAS_BG>(PB, acc, pxv, sidx, A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, Cc.x, Cc.y);
+            // both pairs unconditionally (see k_render_fwd): the independent chains interleave
+            act |= bwd_pair<HAS_INVD, HAS_BG>(PA, acc, pxv, sidx, A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, Cc.x, Cc.y);
+            act |= bwd_pair<HAS_INVD, HAS_BG>(PB, acc, pxv, sidx, A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, Cc.x, Cc.y);
             if (__any(act)) {
                 const float p[10] = {acc.SGx.x + acc.SGx.y, acc.SGy.x + acc.SGy.y, acc.SGxx.x + acc.SGxx.y,
                                      acc.SGxy.x + acc.SGxy.y, acc.SGyy.x + acc.SGyy.y, acc.SG.x + acc.SG.y,
@@ -268,6 +268,8 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
 // flattened, 64 per step (flag reads coalesced, no lane waits on the longest list), each step's flagged
 // records are parked in LDS, and every owner lane folds its own ones in increasing emission order --
 // the same sequential order as the reference-side sum, so the result is deterministic.
+constexpr uint32_t RS_BIG = 256;
+
 __global__ void __launch_bounds__(256) k_record_sum(GaussBwdArgs a) {
     __shared__ uint32_t s_pre[4][64];
     __shared__ uint32_t s_e0[4][64];
@@ -283,6 +285,10 @@ __global__ void __launch_bounds__(256) k_record_sum(GaussBwdArgs a) {
         e0 = c ? a.first_e[idx] : 0u;
         if (e0 >= a.K || c > a.K - e0) c = 0;  // defensive: never read outside the record block
     }
+    // Gaussians with long instance lists are summed by the whole wave afterwards (below), so one lane
+    // never folds thousands of records alone while the rest of the wave idles.
+    const uint32_t cbig = c > RS_BIG ? c : 0u;
+    if (cbig) c = 0;
     uint32_t incl = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -325,6 +331,35 @@ __global__ void __launch_bounds__(256) k_record_sum(GaussBwdArgs a) {
             const float4 r0 = s_rec[w][b][0], r1 = s_rec[w][b][1], r2 = s_rec[w][b][2];
             acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w; acc[4] += r1.x;
             acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w; acc[8] += r2.x; acc[9] += r2.y;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    uint64_t bm = __ballot(cbig != 0u);
+    while (bm) {
+        const int b = __ffsll((unsigned long long)bm) - 1;
+        bm &= bm - 1;
+        const uint32_t eb = (uint32_t)__builtin_amdgcn_readlane((int)e0, b);
+        const uint32_t cb = (uint32_t)__builtin_amdgcn_readlane((int)cbig, b);
+        float part[10];
+#pragma unroll
+        for (int v = 0; v < 10; v++) part[v] = 0.f;
+        for (uint32_t i = (uint32_t)lane; i < cb; i += 64) {
+            const uint32_t e = eb + i;
+            if (a.flag[e]) {
+                const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
+                const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+                part[0] += r0.x; part[1] += r0.y; part[2] += r0.z; part[3] += r0.w; part[4] += r1.x;
+                part[5] += r1.y; part[6] += r1.z; part[7] += r1.w; part[8] += r2.x; part[9] += r2.y;
+            }
+        }
+        int slot;
+        const float tot = wave_reduce10(part, lane, slot);
+        float* st = reinterpret_cast<float*>(&s_rec[w][0][0]);
+        if (slot >= 0) st[slot] = tot;
+        __builtin_amdgcn_wave_barrier();
+        if (lane == b) {
+#pragma unroll
+            for (int v = 0; v < 10; v++) acc[v] = st[v];
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -390,7 +425,8 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
     }
     // moments -> dL/dmean2D, dL/dconic (see render_bwd_tile); o = the AA-scaled opacity of the forward
     {
-        const float4 c4 = a.co[idx];
+        const float4 s0 = a.sp[2 * (size_t)idx], s1 = a.sp[2 * (size_t)idx + 1];
+        const float4 c4 = make_float4(s0.z, s0.w, s1.x, s1.y);
         const float SGx = acc[0], SGy = acc[1], SGxx = acc[2], SGxy = acc[3], SGyy = acc[4];
         const float so = c4.w;
         acc[0] = -(0.5f * a.W) * (so * fmaf(c4.x, SGx, c4.y * SGy));

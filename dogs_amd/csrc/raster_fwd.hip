@@ -9,10 +9,9 @@
 //   tile sort      stable radix sort by tile id only; input order is (depth, index) so the result is the
 //                  reference's (tile, depth bits, index) order, bit for bit
 //   k_ranges       per-tile [start, end)
-//   k_render_fwd   two waves per 16x16 tile (one per 16x8 half), 2 pixels of one row per lane evaluated
-//                  with packed fp32 (v_pk_*_f32); a 64-splat batch is staged in wave-private LDS and read
-//                  back with broadcast ds_read_b128, splats whose quadrant pair cannot reach the half are
-//                  skipped by ballot; wave-uniform early exit once every pixel has saturated.
+//   k_render_fwd   one wave per 16x16 tile, 4 pixels per lane as two row pairs evaluated with packed fp32
+//                  (v_pk_*_f32); a 64-splat batch is staged in wave-private LDS and read back with broadcast
+//                  ds_read_b128; splats that cannot reach a quadrant pair skip it; wave-uniform early exit.
 #include <hip/hip_runtime.h>
 #include "gs_common.h"
 #include "raster.h"
@@ -191,8 +190,9 @@ __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, co
     }
     const float4 co = make_float4(conic.x, conic.y, conic.z, a.opacities[idx] * h_scale);
     a.radii[idx] = ir;
-    a.xy[idx] = make_float2(px, py);
-    a.co[idx] = co;
+    a.sp[2 * idx] = make_float4(px, py, co.x, co.y);
+    a.sp[2 * idx + 1] = make_float4(co.z, co.w, __uint_as_float((uint32_t)x0 | ((uint32_t)x1 << 16)),
+                                    __uint_as_float((uint32_t)y0 | ((uint32_t)y1 << 16)));
     a.rgbi[idx] = make_float4(col.x, col.y, col.z, 1.f / pv.z);
     a.depthkey[idx] = __float_as_uint(pv.z);
     ro.x0 = x0; ro.y0 = y0; ro.x1 = x1; ro.y1 = y1; ro.mx = px; ro.my = py; ro.co = co;
@@ -265,10 +265,11 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
 // emission in depth order: instance e = off[p] + j for the j-th kept tile of Gaussian order[p].  A wave
 // owns 64 consecutive depth ranks, so its instances form one contiguous run starting at off[p0]; the
 // cooperative candidate walk writes them in (p, ty, tx) order with consecutive lanes -> consecutive e.
+// Ranks whose sorted depth key is 0xffffffff are the culled tail (no kept tile) and are skipped; the
+// rest gather ONE 32-B splat record each.
 __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict__ order,
-                                              const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
-                                              const float2* __restrict__ xy, const float4* __restrict__ co,
-                                              const int* __restrict__ radii, int tiles_x, int tiles_y,
+                                              const uint32_t* __restrict__ skey, const uint32_t* __restrict__ off,
+                                              const float4* __restrict__ sp, int tiles_x,
                                               uint32_t* __restrict__ first_e, uint32_t* __restrict__ tilekey,
                                               uint32_t* __restrict__ eg) {
     __shared__ CandLDS s_cand[4];
@@ -276,23 +277,21 @@ __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict_
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int p0 = blockIdx.x * blockDim.x + w * 64;
     if (p0 >= P) return;  // whole wave
+    if (skey[p0] == 0xffffffffu) return;  // whole wave in the culled tail
     const int p = p0 + lane;
     int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
     float mx = 0.f, my = 0.f, thr = 0.f;
     float4 c4 = make_float4(0.f, 0.f, 0.f, 0.f);
     uint32_t g = 0xffffffffu;
-    if (p < P) {
+    if (p < P && skey[p] != 0xffffffffu) {
         g = order[p];
         if (g < (uint32_t)P) {
-            const uint32_t c = cnt[g];
-            if (c > 0) {
-                first_e[g] = off[p];
-                const float2 m = xy[g];
-                c4 = co[g];
-                mx = m.x; my = m.y;
-                get_rect_s(m.x, m.y, radii[g], tiles_x, tiles_y, x0, y0, x1, y1);
-                thr = gs_logf(c4.w / (1.0f / 255.0f));
-            }
+            first_e[g] = off[p];
+            const float4 s0 = sp[2 * g], s1 = sp[2 * g + 1];
+            c4 = make_float4(s0.z, s0.w, s1.x, s1.y);
+            mx = s0.x; my = s0.y;
+            sp_rect(s1, x0, y0, x1, y1);
+            thr = gs_logf(c4.w / (1.0f / 255.0f));
         }
     }
     s_g[w][lane] = g;
@@ -330,113 +329,114 @@ __device__ __forceinline__ uint32_t bcast_u(uint32_t v, int lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
 }
 
-// renderCUDA (forward.cu:349-501) restructured for wave64.  One workgroup per tile, one wave per 8x8
-// quadrant (one pixel per lane).  Each 64-splat batch is gathered one splat per lane, tested against the
-// wave's quadrant with the reference's own max-contribution rect test (quad_mask), and staged in a
-// wave-private LDS slot; the wave then walks only the splats whose footprint reaches its quadrant
-// (s_ff1 over a 64-bit ballot) and reads each one with broadcast ds_read_b128.  The per-pixel update is
-// branch-free: a rejected or finished pixel gets alpha = 0, which leaves C, D and T bit-identical.
-// The conic is prescaled by log2(e) at staging so the exponential is a bare v_exp_f32.
-__global__ void __launch_bounds__(128) k_render_fwd(RenderArgs a) {
-    __shared__ float4 s_b[2][64][3];
-    __shared__ uint32_t s_mx[2];
+// renderCUDA (forward.cu:349-501) restructured for wave64: one wave per 16x16 tile, 4 pixels per lane.
+// Lane l owns pixels (l&7, l>>3) and (l&7 + 8, l>>3) of the top half (pair A = quadrants 0,1) and the
+// same two of the bottom half (pair B = quadrants 2,3); each pair is one row, evaluated with packed fp32.
+// Each 64-splat batch is gathered one splat per lane (one 32-B splat record + colour), tested against
+// the four quadrants with the reference's own max-contribution rect test (quad_mask), and staged in
+// wave-private LDS; the wave then walks only splats that reach a quadrant (s_ff1 over a 64-bit ballot),
+// reads each with broadcast ds_read_b128 and skips a pair whose two quadrant bits are clear.  The
+// per-pixel update is branch-free: a rejected or finished pixel gets alpha = 0, which leaves C, D and T
+// unchanged.  Wave-uniform early exit once every pixel of the tile has saturated.
+__global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a) {
+    __shared__ float4 s_b[4][64][3];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = blockIdx.x;
+    const int tile = blockIdx.x * 4 + w;
+    if (tile >= a.num_tiles) return;
+    float4* sb = &s_b[w][0][0];
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
     const int tx0 = tx * GS_TILE_X, ty0 = ty * GS_TILE_Y;
-    // wave w renders tile rows [8w, 8w+8); lane owns pixels (lane&7) and (lane&7)+8 of row lane>>3, i.e.
-    // the same pixel of quadrants 2w and 2w+1 -- one row, so dy and c*dy^2 are shared by the pair
-    const int px0 = tx0 + (lane & 7), px1 = px0 + 8;
-    const int py = ty0 + w * 8 + (lane >> 3);
-    const v2f pxv = {(float)px0, (float)px1};
-    const float pyf = (float)py;
-    const bool in0 = px0 < a.W && py < a.H, in1 = px1 < a.W && py < a.H;
-    v2f T = bc2(1.0f), C0 = bc2(0.0f), C1 = bc2(0.0f), C2 = bc2(0.0f), Dd = bc2(0.0f);
-    bool live0 = in0, live1 = in1;
-    uint32_t last0 = 0, last1 = 0;
+    const int c0 = tx0 + (lane & 7), rA = ty0 + (lane >> 3);
+    const v4f pxv = {(float)c0, (float)c0, (float)(c0 + 8), (float)(c0 + 8)};
+    const v2f pyv = {(float)rA, (float)(rA + 8)};
+    // per-pixel state; a finished (or outside) pixel gets alpha threshold 2, which no alpha reaches
+    v4f T = bc4(1.0f), C0 = bc4(0.0f), C1 = bc4(0.0f), C2 = bc4(0.0f), D = bc4(0.0f), thr;
+    uint32_t last[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int px = c0 + (k >> 1) * 8, py = rA + (k & 1) * 8;
+        thr[k] = (px < a.W && py < a.H) ? (1.0f / 255.0f) : 2.0f;
+    }
     const uint2 rg = a.ranges[tile];
     const int n = (int)(rg.y - rg.x);
-    float4* sb = &s_b[w][0][0];
     for (int base = 0; base < n; base += 64) {
-        if (!__any(live0 || live1)) break;
+        if (!__any(fminf(fminf(thr.x, thr.y), fminf(thr.z, thr.w)) < 1.0f)) break;
         const int j = base + lane;
         bool touch = false;
         if (j < n) {
             const uint32_t e = min(a.s_e[rg.x + j], a.K - 1);
             const uint32_t g = min(a.eg[e], a.P - 1);
-            const float2 m = a.xy[g];
-            const float4 c4 = a.co[g];
+            const float4 s0 = a.sp[2 * g], s1 = a.sp[2 * g + 1];
             const float4 q = a.rgbi[g];
-            const float thr = gs_logf(c4.w / (1.0f / 255.0f));
-            touch = ((quad_mask({c4.x, c4.y, c4.z, c4.w}, m.x, m.y, thr, tx0, ty0) >> (2 * w)) & 3u) != 0u;
-            sb[lane * 3 + 0] = make_float4(m.x, m.y, c4.x * LOG2E, c4.y * LOG2E);
-            sb[lane * 3 + 1] = make_float4(c4.z * LOG2E, c4.w, q.x, q.y);
+            const float lthr = gs_logf(s1.y / (1.0f / 255.0f));
+            touch = quad_mask({s0.z, s0.w, s1.x, s1.y}, s0.x, s0.y, lthr, tx0, ty0) != 0u;
+            const SplatExp k = splat_exp_coeffs(s0.z, s0.w, s1.x);
+            sb[lane * 3 + 0] = make_float4(s0.x, s0.y, k.A, k.B);
+            sb[lane * 3 + 1] = make_float4(k.C, s1.y, q.x, q.y);
             sb[lane * 3 + 2] = make_float4(q.z, q.w, 0.0f, 0.0f);
         }
         __builtin_amdgcn_wave_barrier();
         uint64_t mask = __ballot(touch);
+        int step = 0;
         while (mask) {
-            const int jj = __ffsll((unsigned long long)mask) - 1;
+            const int jj = (int)__builtin_ctzll(mask);
             mask &= mask - 1;
-            const float4 A = sb[jj * 3 + 0], B = sb[jj * 3 + 1], Cc = sb[jj * 3 + 2];
-            const v2f dx = bc2(A.x) - pxv;
-            const float dy = A.y - pyf;
-            const v2f p2 = splat_power2(A.z, A.w, B.x, dx, dy);
-            v2f al = bc2(B.y) * (v2f){__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y)};
-            al.x = fminf(0.99f, al.x);
-            al.y = fminf(0.99f, al.y);
-            // forward.cu:451-475: skip power > 0 and alpha < 1/255, stop once T would fall below 1e-4
-            const bool ok0 = live0 && !(p2.x > 0.0f) && !(al.x < (1.0f / 255.0f));
-            const bool ok1 = live1 && !(p2.y > 0.0f) && !(al.y < (1.0f / 255.0f));
-            al.x = ok0 ? al.x : 0.0f;
-            al.y = ok1 ? al.y : 0.0f;
-            const v2f test_T = T * (bc2(1.0f) - al);
-            const bool t0 = test_T.x < 0.0001f, t1 = test_T.y < 0.0001f;
-            live0 = live0 && !t0;
-            live1 = live1 && !t1;
-            al.x = t0 ? 0.0f : al.x;
-            al.y = t1 ? 0.0f : al.y;
-            C0 = fma2(bc2(B.z) * al, T, C0);
-            C1 = fma2(bc2(B.w) * al, T, C1);
-            C2 = fma2(bc2(Cc.x) * al, T, C2);
-            Dd = fma2(bc2(Cc.y) * al, T, Dd);
-            T.x = t0 ? T.x : test_T.x;
-            T.y = t1 ? T.y : test_T.y;
+            const float4 Sa = s_b[w][jj][0], Sb = s_b[w][jj][1], Sc = s_b[w][jj][2];
             const uint32_t c = (uint32_t)(base + jj + 1);
-            last0 = (ok0 && !t0) ? c : last0;
-            last1 = (ok1 && !t1) ? c : last1;
-            if (!__any(live0 || live1)) break;
+            const v4f p2 = splat_power4(Sa.z, Sa.w, Sb.x, Sa.x, Sa.y, pxv, pyv);
+            v4f al = bc4(Sb.y) * (v4f){__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y),
+                                       __builtin_amdgcn_exp2f(p2.z), __builtin_amdgcn_exp2f(p2.w)};
+            // forward.cu:451-475: skip power > 0 and alpha < 1/255, stop once T would fall below 1e-4
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float ak = fminf(0.99f, al[k]);
+                al[k] = (p2[k] > 0.0f || ak < thr[k]) ? 0.0f : ak;
+            }
+            const v4f test_T = T * (bc4(1.0f) - al);
+            v4f Tn;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const bool term = test_T[k] < 0.0001f;
+                thr[k] = term ? 2.0f : thr[k];
+                al[k] = term ? 0.0f : al[k];
+                Tn[k] = term ? T[k] : test_T[k];
+                last[k] = al[k] > 0.0f ? c : last[k];
+            }
+            const v4f wt = al * T;
+            C0 = fma4(bc4(Sb.z), wt, C0);
+            C1 = fma4(bc4(Sb.w), wt, C1);
+            C2 = fma4(bc4(Sc.x), wt, C2);
+            D = fma4(bc4(Sc.y), wt, D);
+            T = Tn;
+            // early exit, checked every 8 splats (splats after saturation leave every pixel unchanged)
+            if ((++step & 7) == 0 && !__any(fminf(fminf(thr.x, thr.y), fminf(thr.z, thr.w)) < 1.0f)) break;
         }
         __builtin_amdgcn_wave_barrier();
     }
     const size_t HW = (size_t)a.W * a.H;
     uint32_t mx = 0;
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-        if (!(h ? in1 : in0)) continue;
-        const size_t pid = (size_t)py * a.W + (h ? px1 : px0);
-        const float Th = h ? T.y : T.x;
-        const uint32_t lh = h ? last1 : last0;
-        a.final_T[pid] = Th;
-        a.n_contrib[pid] = lh;
-        const float o0 = fmaf(Th, a.bg[0], h ? C0.y : C0.x);
-        const float o1 = fmaf(Th, a.bg[1], h ? C1.y : C1.x);
-        const float o2 = fmaf(Th, a.bg[2], h ? C2.y : C2.x);
+    for (int k = 0; k < 4; k++) {
+        const int px = c0 + (k >> 1) * 8, py = rA + (k & 1) * 8;
+        if (!(px < a.W && py < a.H)) continue;
+        const size_t pid = (size_t)py * a.W + px;
+        a.final_T[pid] = T[k];
+        a.n_contrib[pid] = last[k];
+        const float o0 = fmaf(T[k], a.bg[0], C0[k]);
+        const float o1 = fmaf(T[k], a.bg[1], C1[k]);
+        const float o2 = fmaf(T[k], a.bg[2], C2[k]);
         a.out_color[pid] = o0; a.out_color[HW + pid] = o1; a.out_color[2 * HW + pid] = o2;
         a.img_color[pid] = o0; a.img_color[HW + pid] = o1; a.img_color[2 * HW + pid] = o2;
-        const float dh = h ? Dd.y : Dd.x;
-        a.out_invd[pid] = dh;
-        a.img_invd[pid] = dh;
-        mx = lh > mx ? lh : mx;
+        a.out_invd[pid] = D[k];
+        a.img_invd[pid] = D[k];
+        mx = last[k] > mx ? last[k] : mx;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const uint32_t y = __shfl_xor(mx, o);
         mx = y > mx ? y : mx;
     }
-    if (lane == 0) s_mx[w] = mx;
-    __syncthreads();
-    if (threadIdx.x == 0) a.max_contrib[tile] = s_mx[0] > s_mx[1] ? s_mx[0] : s_mx[1];
+    if (lane == 0) a.max_contrib[tile] = mx;
 }
 
 // checkFrustum (rasterizer_impl.cu:104-116)
@@ -489,17 +489,15 @@ void launch_preprocess(const PreArgs& a, hipStream_t s) {
     if (lds < cand) lds = cand;
     if (a.P > 0) k_preprocess<<<(a.P + 255) / 256, 256, lds, s>>>(a);
 }
-void launch_emit(int P, const uint32_t* order, const uint32_t* cnt, const uint32_t* off, const float2* xy,
-                 const float4* co, const int* radii, int tiles_x, int tiles_y, uint32_t* first_e, uint32_t* tilekey,
-                 uint32_t* eg, hipStream_t s) {
-    if (P > 0) k_emit<<<(P + 255) / 256, 256, 0, s>>>(P, order, cnt, off, xy, co, radii, tiles_x, tiles_y, first_e,
-                                                      tilekey, eg);
+void launch_emit(int P, const uint32_t* order, const uint32_t* skey, const uint32_t* off, const float4* sp,
+                 int tiles_x, uint32_t* first_e, uint32_t* tilekey, uint32_t* eg, hipStream_t s) {
+    if (P > 0) k_emit<<<(P + 255) / 256, 256, 0, s>>>(P, order, skey, off, sp, tiles_x, first_e, tilekey, eg);
 }
 void launch_ranges(uint32_t K, const uint32_t* keys, uint2* ranges, uint32_t num_tiles, hipStream_t s) {
     if (K > 0) k_ranges<<<(K + 255) / 256, 256, 0, s>>>(K, keys, ranges, num_tiles);
 }
 void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
-    if (a.num_tiles > 0) k_render_fwd<<<a.num_tiles, 128, 0, s>>>(a);
+    if (a.num_tiles > 0) k_render_fwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
 }
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s) {
     if (P > 0) k_mark_visible<<<(P + 255) / 256, 256, 0, s>>>(P, means3D, view, present);

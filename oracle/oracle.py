@@ -97,7 +97,10 @@ class OracleForward:
 
     def __del__(self):
         if getattr(self, "_ctx", None):
-            lib().gso_free(self._ctx)
+            try:
+                lib().gso_free(self._ctx)
+            except TypeError:  # interpreter shutdown: module globals already cleared
+                pass
             self._ctx = None
 
     @property

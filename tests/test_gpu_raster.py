@@ -53,17 +53,14 @@ def test_forward_bitexact_keys(oracle, hip_device, n, W, H, deg, bg, aa):
     assert np.abs(col.cpu().numpy() - col_o).max() < 5e-3
 
 
-@pytest.mark.parametrize("n,W,H,deg,bg,aa", CASES)
-def test_backward_matches_oracle(oracle, hip_device, n, W, H, deg, bg, aa):
+def _backward_vs_oracle(s, W, H, deg, bg, aa, dev, seed):
     from dogs_amd.diff_gaussian_rasterization import _C
-    s = small_scene(n, W, H, seed=11 + n)
-    col_o, radii_o, inv_o, st = oracle_forward(oracle, s, bg, deg=deg, antialiasing=aa)
-    out = hip_forward(s, bg, hip_device, deg=deg, antialiasing=aa)
-    rng = np.random.default_rng(n)
+    col_o, radii_o, inv_o, st = oracle_forward(oracle_mod(), s, bg, deg=deg, antialiasing=aa)
+    out = hip_forward(s, bg, dev, deg=deg, antialiasing=aa)
+    rng = np.random.default_rng(seed)
     gcol = rng.standard_normal((3, H, W)).astype(np.float32)
     ginv = (0.1 * rng.standard_normal((1, H, W))).astype(np.float32)
     go = st.backward(gcol, ginv[0])
-    dev = hip_device
     c = s.camera.to(dev)
     e = torch.empty(0, device=dev)
     d = lambda t: t.to(dev).contiguous()  # noqa: E731
@@ -77,3 +74,26 @@ def test_backward_matches_oracle(oracle, hip_device, n, W, H, deg, bg, aa):
         ref = go[name]
         err = rel_err(h.cpu().numpy().reshape(ref.shape), ref)
         assert err < 1e-4, f"{name}: rel err {err}"
+    return st
+
+
+def oracle_mod():
+    from oracle import oracle as O
+    return O
+
+
+@pytest.mark.parametrize("n,W,H,deg,bg,aa", CASES)
+def test_backward_matches_oracle(oracle, hip_device, n, W, H, deg, bg, aa):
+    s = small_scene(n, W, H, seed=11 + n)
+    _backward_vs_oracle(s, W, H, deg, bg, aa, hip_device, seed=n)
+
+
+def test_backward_huge_splats(oracle, hip_device):
+    """A few splats spanning hundreds of tiles: their instance records take the whole-wave summation path
+    of k_record_sum (lists longer than 256) and the wide-rect candidate walk of preprocess/emit."""
+    n, W, H = 2000, 640, 480
+    s = small_scene(n, W, H, seed=5)
+    big = torch.arange(0, n, 97)
+    s.scales[big] = s.scales[big] * 40.0
+    st = _backward_vs_oracle(s, W, H, 3, (0.3, 0.2, 0.1), False, hip_device, seed=5)
+    assert int(st.geom()["tiles_touched"].max()) > 256

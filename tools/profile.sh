@@ -1,0 +1,19 @@
+#!/bin/bash
+# Kernel-trace stats + separate PMC passes of the bench workload (run on the GPU box from the repo root).
+# usage: tools/profile.sh OUTDIR [pmc]   -- each GPU step under its own timeout; stops at the first failure
+set -e
+OUT=${1:-gpurun_out/prof}
+ROOT=$(pwd)
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+BENCH="$ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-train-step"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- python3 $BENCH > "$OUT/trace.log" 2>&1
+if [ "$2" = "pmc" ]; then
+  i=0
+  while read -r line; do
+    case "$line" in pmc:*) ;; *) continue ;; esac
+    i=$((i+1))
+    ctrs=${line#pmc: }
+    timeout -k 10 300 rocprofv3 --pmc $ctrs -d "$OUT/pmc$i" -o run -- python3 $BENCH > "$OUT/pmc$i.log" 2>&1
+  done < "$ROOT/tools/pmc_counters.txt"
+fi
