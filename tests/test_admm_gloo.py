@@ -1,0 +1,97 @@
+"""ADMM block consensus over torch.distributed (gloo, world_size 2, CPU) vs a single-process restatement of the
+reference master's gather/average/scatter (master_gaussian_trainer.py:459-555, gaussian_splat_model.py:316-340),
+dual update (slave_gaussian_trainer.py:100-121), residuals (master :396-456) and penalty adaptation (:337-377)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+WIDTHS = (3, 3, 45, 3, 4, 1)
+N_GLOBAL = 97
+
+
+def _block(rank, world):
+    """Deterministic block data: overlapping global-index sets covering every Gaussian."""
+    g = torch.Generator().manual_seed(100 + rank)
+    base = torch.arange(rank, N_GLOBAL, world)                       # disjoint cover
+    extra = torch.randperm(N_GLOBAL, generator=g)[:30]                # shared Gaussians
+    idx = torch.unique(torch.cat([base, extra]))
+    params = tuple(torch.randn((idx.numel(), w), generator=g) for w in WIDTHS)
+    return idx, params
+
+
+def _reference(world):
+    blocks = [_block(k, world) for k in range(world)]
+    cnt = torch.zeros(N_GLOBAL)
+    sums = [torch.zeros(N_GLOBAL, w) for w in WIDTHS]
+    for idx, ps in blocks:
+        cnt.index_add_(0, idx, torch.ones(idx.numel()))
+        for s, p in zip(sums, ps):
+            s.index_add_(0, idx, p)
+    z = [s / cnt[:, None] for s in sums]
+    return blocks, cnt, z
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dogs_amd.admm import ADMMConfig, BlockConsensus, adapt_rho, admm_penalty, initial_rho
+        blocks, cnt, zref = _reference(world)
+        idx, params = blocks[rank]
+        bc = BlockConsensus(idx, N_GLOBAL, device=torch.device("cpu"))
+        assert torch.equal(bc.visibility_count.float(), cnt)
+        z = bc.consensus(params)
+        for zi, zr in zip(z, zref):
+            torch.testing.assert_close(zi, zr[idx], rtol=1e-6, atol=1e-6)
+        # Gaussians held by one block: z == x exactly, so their dual never moves
+        solo = cnt[idx] == 1
+        for zi, p in zip(z, params):
+            assert torch.equal(zi[solo], p[solo])
+        cfg = ADMMConfig()
+        rho = initial_rho(cfg, N_GLOBAL)
+        duals = [torch.zeros_like(p) for p in params]
+        bc.update_duals(duals, params, z, cfg.over_relaxation_coeff)
+        for u, p, zi in zip(duals, params, z):
+            torch.testing.assert_close(u, 1.5 * (p - zi))
+        # a second round with moved parameters -> residuals against the single-process restatement
+        params2 = tuple(p + 0.01 * (k + 1) for k, p in enumerate(params))
+        z2 = bc.consensus(params2)
+        primal, dual = bc.residuals(params2, z2, z, rho)
+        blocks2 = [(i, tuple(p + 0.01 * (k + 1) for k, p in enumerate(ps))) for i, ps in blocks]
+        z2ref = [zr + 0.01 * (k + 1) for k, zr in enumerate(zref)]
+        for k, name in enumerate(("xyz", "fdc", "fr", "s", "q", "o")):
+            pr = sum(torch.nn.functional.mse_loss(z2ref[k][i], ps[k]).item() for i, ps in blocks2)
+            du = rho[name] * torch.nn.functional.mse_loss(zref[k], z2ref[k]).item()
+            assert abs(primal[name] - pr) <= 1e-6 * max(1.0, abs(pr))
+            assert abs(dual[name] - du) <= 1e-6 * max(1e-12, abs(du)) + 1e-12
+        rho2 = adapt_rho(rho, primal, dual, cfg)
+        for name in rho:
+            assert rho2[name] in (rho[name], rho[name] * cfg.tau_inc, rho[name] / cfg.tau_dec)
+        pen = admm_penalty(params2, duals, z2, rho)
+        assert torch.isfinite(pen)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_consensus_gloo_matches_single_process(world):
+    mp.spawn(_worker, args=(world, _free_port()), nprocs=world, join=True)
+
+
+def test_consensus_single_rank_is_identity():
+    from dogs_amd.admm import BlockConsensus
+    idx, params = _block(0, 1)
+    bc = BlockConsensus(idx, N_GLOBAL, device=torch.device("cpu"))
+    z = bc.consensus(params)
+    for zi, p in zip(z, params):
+        assert torch.equal(zi, p)
