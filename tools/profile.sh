@@ -7,7 +7,7 @@ ROOT=$(pwd)
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 BENCH="$ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-train-step"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- python3 $BENCH > "$OUT/trace.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH > "$OUT/trace.log" 2>&1
 if [ "$2" = "pmc" ]; then
   i=0
   while read -r line; do
