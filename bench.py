@@ -35,7 +35,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
 def phase_bytes(phase: str, N: int, K: int, HW: int) -> float:
-    """Algorithmic bytes per launch of each phase (DESIGN.md 'Roofline')."""
+    """Algorithmic bytes per launch of each phase (DESIGN.md 'Roofline'), with K the reference's
+    precise instance count (its full per-tile lists), whatever this build bins."""
     return {
         "preprocess": 284.0 * N,            # 236 B params read + 48 B geometry written
         "depth_sort": 0.0,                  # implementation overhead (not algorithmic)
@@ -47,6 +48,9 @@ def phase_bytes(phase: str, N: int, K: int, HW: int) -> float:
         "flag_clear": 0.0,
         "render_bwd": 84.0 * K + 40.0 * HW,
         "record_sum": 0.0,                  # implementation overhead (per-instance records -> sums)
+        "phase2_count": 0.0,                # depth-prefix binning, phase 2 (only when tiles were left unfinished)
+        "phase2_bin": 0.0,
+        "render_fwd2": 0.0,
         "gauss_bwd": 528.0 * N,
     }.get(phase, 0.0)
 
@@ -78,6 +82,21 @@ class View:
         self.bg = torch.zeros(3, device=dev)
         self.e = torch.empty(0, device=dev)
         self.last = None
+
+    def forward(self):
+        s, c, e = self.s, self.c, self.e
+        return self._C.rasterize_gaussians(self.bg, s.means3D, e, s.opacities, s.scales, s.rotations, 1.0, e,
+                                           c.world_to_camera, c.projective_matrix, c.tanfovx, c.tanfovy, c.height,
+                                           c.width, s.dc, s.sh, 3, c.camera_center, False, False, False)
+
+    def reference_instances(self):
+        """The reference's precise instance count (its full per-tile lists): one untimed forward with
+        depth-prefix binning off.  The §8(d) byte formula is written in terms of it."""
+        old = self._C.set_prefix_per_tile(-1)
+        try:
+            return int(self.forward()[1])
+        finally:
+            self._C.set_prefix_per_tile(old)
 
     def step(self):
         s, c, e = self.s, self.c, self.e
@@ -235,7 +254,8 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    num_rendered, K = view.last
+    num_rendered, K_binned = view.last
+    K = view.reference_instances()
 
     # ---- one profiled step: per-phase hipEvent durations on the stream the kernels run on
     L.profile_enable(True)
@@ -289,6 +309,7 @@ def main():
             "config": {"workload": f"synthetic {W}x{H}, {n} Gaussians/rank, SH3, raster fwd+bwd per view",
                        "width": W, "height": H, "gaussians_per_rank": n, "sh_degree": 3,
                        "num_rendered": int(num_rendered), "instances_K": int(K),
+                       "instances_binned": int(K_binned),
                        "consensus_interval": args.consensus_interval if ws > 1 else None,
                        "shared_gaussians": (cons.num_shared if cons is not None else 0),
                        "parallelism": f"admm-blocks x{ws}" if ws > 1 else "single"},

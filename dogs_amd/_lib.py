@@ -20,7 +20,7 @@ _f32p = C.POINTER(C.c_float)
 class DgRasterArgs(C.Structure):
     _fields_ = [
         ("P", C.c_int), ("D", C.c_int), ("M", C.c_int), ("W", C.c_int), ("H", C.c_int),
-        ("prefiltered", C.c_int), ("antialiasing", C.c_int), ("debug", C.c_int),
+        ("prefiltered", C.c_int), ("antialiasing", C.c_int), ("debug", C.c_int), ("prefix_per_tile", C.c_int),
         ("scale_modifier", C.c_float), ("tanfovx", C.c_float), ("tanfovy", C.c_float),
         ("bg", C.c_void_p), ("means3D", C.c_void_p), ("colors", C.c_void_p), ("opacities", C.c_void_p),
         ("scales", C.c_void_p), ("rotations", C.c_void_p), ("cov3D_precomp", C.c_void_p),
@@ -30,7 +30,7 @@ class DgRasterArgs(C.Structure):
 
 
 ALLOC_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int, C.c_uint64)
-DG_BUF_GEOM, DG_BUF_BINNING, DG_BUF_IMAGE, DG_BUF_BACKWARD, DG_BUF_TEMP = range(5)
+DG_BUF_GEOM, DG_BUF_BINNING, DG_BUF_IMAGE, DG_BUF_BACKWARD, DG_BUF_TEMP, DG_BUF_BINNING2 = range(6)
 
 EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_mark_visible", "dg_rasterize_filter",
            "dg_adam_update", "dg_fused_ssim_forward", "dg_fused_ssim_backward", "dg_dist_cuda2",
@@ -57,9 +57,10 @@ def load(path: str | None = None):
         vp, i64p = C.c_void_p, C.POINTER(C.c_int64)
         L.dg_rasterize_forward.restype = C.c_int
         L.dg_rasterize_forward.argtypes = [C.POINTER(DgRasterArgs), vp, vp, vp, ALLOC_FN, vp,
-                                           C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), i64p, i64p, vp]
+                                           C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), i64p, i64p,
+                                           vp]
         L.dg_rasterize_backward.restype = C.c_int
-        L.dg_rasterize_backward.argtypes = [C.POINTER(DgRasterArgs), vp, vp, vp, vp, C.c_int64, C.c_int64, vp, vp,
+        L.dg_rasterize_backward.argtypes = [C.POINTER(DgRasterArgs), vp, vp, vp, vp, vp, C.c_int64, C.c_int64, vp, vp,
                                             vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, ALLOC_FN, vp, vp]
         L.dg_mark_visible.restype = C.c_int
         L.dg_mark_visible.argtypes = [C.c_int, vp, vp, vp, vp, vp]
@@ -81,7 +82,8 @@ def load(path: str | None = None):
         L.dg_binning_bytes.restype = C.c_uint64
         L.dg_binning_bytes.argtypes = [C.c_int64, C.c_int, C.c_int]
         L.dg_debug_sorted_instances.restype = C.c_int
-        L.dg_debug_sorted_instances.argtypes = [vp, C.c_int64, C.c_int, C.c_int, vp, vp, vp]
+        L.dg_debug_sorted_instances.argtypes = [C.POINTER(DgRasterArgs), vp, vp, vp, C.c_int64, vp, vp,
+                                                i64p, vp]
         L.dg_debug_geometry.restype = C.c_int
         L.dg_debug_geometry.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp]
         L.dg_debug_image_state.restype = C.c_int

@@ -92,6 +92,7 @@ struct Geom {
     float4* sp;  // 2 per Gaussian (raster.h)
     float4* rgbi;
     uint32_t *k0, *v0, *k1, *v1, *cnt, *first_e, *off;
+    uint32_t *rcnt, *cnt2, *off2;  // records per Gaussian; phase-2 counts / offsets by rank - R1
     void* sort_tmp;
     void* scan_tmp;
     size_t bytes;
@@ -110,6 +111,9 @@ Geom carve_geom(void* base, int P) {
     g.cnt = c.take<uint32_t>(n);
     g.first_e = c.take<uint32_t>(n);
     g.off = c.take<uint32_t>(n);
+    g.rcnt = c.take<uint32_t>(n);
+    g.cnt2 = c.take<uint32_t>(n);
+    g.off2 = c.take<uint32_t>(n);
     g.sort_tmp = c.take<char>(gs::radix_sort_temp_bytes((uint32_t)n));
     g.scan_tmp = c.take<char>(gs::scan_temp_bytes((uint32_t)n));
     g.bytes = c.off;
@@ -120,6 +124,10 @@ struct Image {
     float *final_T, *img_color, *img_invd;
     uint32_t *n_contrib, *max_contrib;
     uint2* ranges;
+    uint2* ranges2;         // phase-2 lists of unfinished tiles
+    uint8_t* unfinished;    // [T]
+    float4* resume;         // [HW] raw colour + live threshold of unfinished tiles' pixels
+    uint32_t* sat;          // [(ty+1)*(tx+1)] summed-area table of `unfinished`
     size_t bytes;
 };
 Image carve_image(void* base, int W, int H) {
@@ -133,6 +141,10 @@ Image carve_image(void* base, int W, int H) {
     im.img_invd = c.take<float>(HW);
     im.ranges = c.take<uint2>(T);
     im.max_contrib = c.take<uint32_t>(T);
+    im.ranges2 = c.take<uint2>(T);
+    im.unfinished = c.take<uint8_t>(T);
+    im.resume = c.take<float4>(HW);
+    im.sat = c.take<uint32_t>((size_t)(tiles_x_of(W) + 1) * (tiles_y_of(H) + 1));
     im.bytes = c.off;
     return im;
 }
@@ -154,6 +166,30 @@ Binning carve_binning(void* base, int64_t K) {
     b.sort_tmp = c.take<char>(gs::radix_sort_temp_bytes((uint32_t)n));
     b.bytes = c.off;
     return b;
+}
+
+// Pinned per-thread landing buffer + event for the forward's early counter read.
+struct HostCounters {
+    uint32_t* buf = nullptr;
+    hipEvent_t ev = nullptr;
+};
+HostCounters& host_counters() {
+    thread_local HostCounters h;
+    if (!h.buf) {
+        (void)hipHostMalloc((void**)&h.buf, 64 * sizeof(uint32_t), hipHostMallocDefault);
+        (void)hipEventCreateWithFlags(&h.ev, hipEventDisableTiming);
+    }
+    return h;
+}
+
+// Phase-1 binning capacity (instances): prefix_per_tile x tiles (0 -> default), or everything when < 0.
+constexpr int DEFAULT_PREFIX_PER_TILE = 256;
+bool prefix_enabled(const dg_raster_args* a) { return a->prefix_per_tile >= 0; }
+int64_t phase1_cap(const dg_raster_args* a, int T, int64_t K_all) {
+    if (!prefix_enabled(a)) return K_all;
+    const int64_t per = a->prefix_per_tile > 0 ? a->prefix_per_tile : DEFAULT_PREFIX_PER_TILE;
+    const int64_t c = per * (int64_t)T;
+    return c < 1 ? 1 : (c > 0xffffff00ll ? 0xffffff00ll : c);
 }
 
 struct BwdScratch {
@@ -275,13 +311,16 @@ uint64_t dg_binning_bytes(int64_t K, int W, int H) { (void)W; (void)H; return ca
 
 int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_invdepth, int* radii,
                          dg_alloc_fn alloc, void* user, void** geom_out, void** binning_out, void** image_out,
-                         int64_t* num_rendered, int64_t* num_instances, dg_stream_t stream_) {
+                         void** binning2_out, int64_t* num_rendered, int64_t* num_instances, dg_stream_t stream_) {
     if (check_args(a)) return 1;
     hipStream_t s = (hipStream_t)stream_;
     const int P = a->P, W = a->W, H = a->H;
     const int tx = tiles_x_of(W), ty = tiles_y_of(H), T = tx * ty;
+    const int tile_bits = bits_for((uint32_t)T);
     *num_rendered = 0;
     *num_instances = 0;
+    *binning_out = nullptr;
+    *binning2_out = nullptr;
 
     const size_t gbytes = carve_geom(nullptr, P).bytes;
     void* gbase = alloc(user, DG_BUF_GEOM, gbytes);
@@ -293,17 +332,16 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     Image im = carve_image(ibase, W, H);
     *geom_out = gbase;
     *image_out = ibase;
-    *binning_out = nullptr;
 
     HIP_OK(hipMemsetAsync(g.counters, 0, 64, s));
     gs::PreArgs pre;
     fill_pre(pre, a);
-    pre.radii = radii; pre.sp = g.sp; pre.rgbi = g.rgbi; pre.depthkey = g.k0; pre.cnt = g.cnt;
-    pre.rect_sum = (unsigned long long*)(g.counters + 2); pre.err = g.counters + 1;
+    pre.radii = radii; pre.sp = g.sp; pre.rgbi = g.rgbi; pre.depthkey = g.k0; pre.cnt = g.cnt; pre.rcnt = g.rcnt;
+    pre.rect_sum = (unsigned long long*)(g.counters + gs::CNT_RECT_LO); pre.err = g.counters + gs::CNT_ERR;
     { PROF("preprocess"); gs::launch_preprocess(pre, s); }
     DBG_SYNC(a->debug, s);
 
-    // stable depth sort of (depth bits, index): 4 passes -> result back in k0/v0
+    // stable depth sort of (depth bits, index), then the emission offsets in depth order
     const uint32_t* order = g.v0;
     const uint32_t* skey = g.k0;
     if (P > 0) {
@@ -312,59 +350,109 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
         order = which ? g.v1 : g.v0;
         skey = which ? g.k1 : g.k0;
         DBG_SYNC(a->debug, s);
-        { PROF("count_scan"); gs::exclusive_scan(g.cnt, order, (uint32_t)P, g.off, g.counters, g.scan_tmp, s); }
+        { PROF("count_scan"); gs::exclusive_scan(g.cnt, order, (uint32_t)P, g.off, g.counters + gs::CNT_K, g.scan_tmp, s); }
         DBG_SYNC(a->debug, s);
     }
-    uint32_t hc[4] = {0, 0, 0, 0};
-    HIP_OK(hipMemcpyAsync(hc, g.counters, 16, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
-    if (hc[1]) return fail("a Gaussian was filtered although prefiltered is set%s%d");
-    const int64_t K = hc[0];
-    *num_rendered = (int64_t)((uint64_t)hc[2] | ((uint64_t)hc[3] << 32));
-    *num_instances = K;
 
-    const size_t bbytes = carve_binning(nullptr, K).bytes;
+    // ---- phase 1: the depth prefix [0, E1) with E1 <= C1 (the counts stay on the device)
+    int64_t C1;
+    if (prefix_enabled(a)) {
+        C1 = phase1_cap(a, T, 0);
+    } else {  // everything in one phase: the capacity is K itself (one early sync)
+        uint32_t k = 0;
+        HIP_OK(hipMemcpyAsync(&k, g.counters + gs::CNT_K, 4, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+        C1 = k;
+    }
+    gs::launch_prefix_cut(g.off, (uint32_t)P, (uint32_t)(C1 < 0xffffffffll ? C1 : 0xffffffffll), g.counters, im.ranges,
+                          (uint32_t)T, s);
+    // the host's only wait is on this early copy (K, num_rendered, error flag, cut), and it happens after all of
+    // phase 1 is queued, so the GPU never idles on it
+    HostCounters& hcs = host_counters();
+    HIP_OK(hipMemcpyAsync(hcs.buf, g.counters, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipEventRecord(hcs.ev, s));
+
+    const size_t bbytes = carve_binning(nullptr, C1).bytes;
     void* bbase = alloc(user, DG_BUF_BINNING, bbytes);
     if (!bbase) return fail("binning allocation failed%s%d");
     *binning_out = bbase;
-    Binning b = carve_binning(bbase, K);
-
+    Binning b = carve_binning(bbase, C1);
+    const uint32_t* E1_dev = g.counters + gs::CNT_E1;
     const uint32_t* s_e = b.se0;
     const uint32_t* s_keys = b.tk0;
-    if (K > 0) {
-        { PROF("emit"); gs::launch_emit(P, order, skey, g.off, g.sp, tx, g.first_e, b.tk0, b.eg, s); }
+    if (C1 > 0 && P > 0) {
+        { PROF("emit"); gs::launch_emit(P, order, skey, g.off, g.sp, tx, g.counters, g.first_e, g.rcnt, b.tk0, b.eg, s); }
         DBG_SYNC(a->debug, s);
         int which;
-        { PROF("tile_sort"); which = gs::radix_sort_pairs(b.tk0, b.se0, b.tk1, b.se1, nullptr, (uint32_t)K, 0,
-                                                          bits_for((uint32_t)T), b.sort_tmp, s); }
+        { PROF("tile_sort"); which = gs::radix_sort_pairs(b.tk0, b.se0, b.tk1, b.se1, nullptr, (uint32_t)C1, 0,
+                                                          tile_bits, b.sort_tmp, s, E1_dev); }
         s_e = which ? b.se1 : b.se0;
         s_keys = which ? b.tk1 : b.tk0;
         DBG_SYNC(a->debug, s);
     }
-    {
-        PROF("ranges");
-        HIP_OK(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * (size_t)T, s));
-        gs::launch_ranges((uint32_t)K, s_keys, im.ranges, (uint32_t)T, s);
-    }
+    { PROF("ranges"); gs::launch_ranges((uint32_t)C1, E1_dev, s_keys, im.ranges, (uint32_t)T, s); }
     DBG_SYNC(a->debug, s);
 
     gs::RenderArgs r;
+    memset(&r, 0, sizeof(r));
     r.W = W; r.H = H; r.tiles_x = tx; r.num_tiles = T;
-    r.K = (uint32_t)(K > 0 ? K : 1); r.P = (uint32_t)(P > 0 ? P : 1);
+    r.K = (uint32_t)(C1 > 0 ? C1 : 1); r.P = (uint32_t)(P > 0 ? P : 1);
     r.ranges = im.ranges; r.s_e = s_e; r.eg = b.eg; r.sp = g.sp; r.rgbi = g.rgbi; r.bg = a->bg;
     r.out_color = out_color; r.out_invd = out_invdepth; r.final_T = im.final_T; r.img_color = im.img_color;
     r.img_invd = im.img_invd; r.n_contrib = im.n_contrib; r.max_contrib = im.max_contrib;
+    r.phase = 1; r.counters = g.counters; r.unfinished = im.unfinished; r.resume = im.resume;
+    r.ranges2_zero = im.ranges2;
     { PROF("render_fwd"); gs::launch_render_fwd(r, s); }
+    DBG_SYNC(a->debug, s);
+
+    HIP_OK(hipEventSynchronize(hcs.ev));
+    const uint32_t* hc = hcs.buf;
+    if (hc[gs::CNT_ERR]) return fail("a Gaussian was filtered although prefiltered is set%s%d");
+    *num_rendered = (int64_t)((uint64_t)hc[gs::CNT_RECT_LO] | ((uint64_t)hc[gs::CNT_RECT_LO + 1] << 32));
+    const uint32_t K = hc[gs::CNT_K], R1 = hc[gs::CNT_R1];
+    // the backward sizes records for K (>= phase-1 + phase-2 instances) and re-carves phase 2 at K
+    *num_instances = K;
+    if (!hc[gs::CNT_CUT] || (int)R1 >= P) {
+        HIP_OK(hipGetLastError());
+        return 0;
+    }
+
+    // ---- phase 2: the remaining ranks, only for tiles phase 1 left unfinished.  Every kernel is gated on the
+    // device-side unfinished count, so nothing waits for phase 1 and the common case costs a few empty launches.
+    const size_t b2bytes = carve_binning(nullptr, K).bytes;
+    void* b2base = alloc(user, DG_BUF_BINNING2, b2bytes);
+    if (!b2base) return fail("phase-2 binning allocation failed%s%d");
+    *binning2_out = b2base;
+    Binning b2 = carve_binning(b2base, K);
+    const uint32_t* K2_dev = g.counters + gs::CNT_K2;
+    const uint32_t* gate = g.counters + gs::CNT_UNFINISHED;
+    {
+        PROF("phase2");
+        gs::launch_unfinished_sat(g.counters, im.unfinished, tx, ty, im.sat, s);
+        gs::launch_count2(P, R1, g.counters, order, skey, g.sp, tx, ty, im.unfinished, im.sat, g.cnt2, s);
+        gs::exclusive_scan(g.cnt2, nullptr, (uint32_t)(P - (int)R1), g.off2, g.counters + gs::CNT_K2, g.scan_tmp, s,
+                           gate);
+        gs::launch_emit2(P, R1, g.counters, order, skey, g.sp, tx, ty, im.unfinished, im.sat, g.cnt2, g.off2,
+                         g.first_e, g.rcnt, b2.tk0, b2.eg, s);
+        const int which = gs::radix_sort_pairs(b2.tk0, b2.se0, b2.tk1, b2.se1, nullptr, K, 0, tile_bits,
+                                               b2.sort_tmp, s, K2_dev);
+        gs::launch_ranges(K, K2_dev, which ? b2.tk1 : b2.tk0, im.ranges2, (uint32_t)T, s);
+        gs::RenderArgs r2 = r;
+        r2.phase = 2;
+        r2.K = K;
+        r2.ranges = im.ranges2; r2.ranges1 = im.ranges; r2.s_e = which ? b2.se1 : b2.se0; r2.eg = b2.eg;
+        gs::launch_render_fwd(r2, s);
+    }
     DBG_SYNC(a->debug, s);
     HIP_OK(hipGetLastError());
     return 0;
 }
 
 int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void* geom, const void* binning,
-                          const void* image, int64_t num_rendered, int64_t K, const float* dL_dout_color,
-                          const float* dL_dout_invdepth, float* dmeans2D, float* dcolors, float* dopacity,
-                          float* dmeans3D, float* dcov3D, float* ddc, float* dsh, float* dscales, float* drot,
-                          float* depth, dg_alloc_fn alloc, void* user, dg_stream_t stream_) {
+                          const void* image, const void* binning2, int64_t num_rendered, int64_t K,
+                          const float* dL_dout_color, const float* dL_dout_invdepth, float* dmeans2D, float* dcolors,
+                          float* dopacity, float* dmeans3D, float* dcov3D, float* ddc, float* dsh, float* dscales,
+                          float* drot, float* depth, dg_alloc_fn alloc, void* user, dg_stream_t stream_) {
     (void)num_rendered;
     if (check_args(a)) return 1;
     hipStream_t s = (hipStream_t)stream_;
@@ -373,25 +461,34 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     if (P == 0) return 0;
     Geom g = carve_geom((void*)geom, P);
     Image im = carve_image((void*)image, W, H);
-    Binning b = carve_binning((void*)binning, K);
+    // the phase-1 block was carved at C1 (its capacity), the phase-2 block at K (see the forward)
+    const int64_t C1 = phase1_cap(a, T, K);
+    Binning b = carve_binning((void*)binning, C1);
     const int passes = (bits_for((uint32_t)T) + 7) / 8;
     const uint32_t* s_e = (passes & 1) ? b.se1 : b.se0;
+    const uint32_t* s_e2 = nullptr;
+    const uint32_t* eg2 = nullptr;
+    if (binning2) {
+        Binning b2 = carve_binning((void*)binning2, K);
+        s_e2 = (passes & 1) ? b2.se1 : b2.se0;
+        eg2 = b2.eg;
+    }
 
     const size_t sbytes = carve_bwd(nullptr, K, P).bytes;
     void* sbase = alloc(user, DG_BUF_BACKWARD, sbytes);
     if (!sbase) return fail("backward scratch allocation failed%s%d");
     BwdScratch sc = carve_bwd(sbase, K, P);
     if (K > 0) {
-        { PROF("flag_clear"); HIP_OK(hipMemsetAsync(sc.flag, 0, (size_t)K, s)); }
         gs::RenderBwdArgs r;
         r.W = W; r.H = H; r.tiles_x = tx; r.num_tiles = T;
         r.K = (uint32_t)K; r.P = (uint32_t)P;
         r.ranges = im.ranges; r.max_contrib = im.max_contrib; r.s_e = s_e; r.eg = b.eg;
+        r.ranges2 = binning2 ? im.ranges2 : nullptr; r.s_e2 = s_e2; r.eg2 = eg2; r.counters = g.counters;
+        r.unfinished = im.unfinished;
         r.sp = g.sp; r.rgbi = g.rgbi; r.bg = a->bg;
         r.final_T = im.final_T; r.img_color = im.img_color; r.img_invd = im.img_invd; r.n_contrib = im.n_contrib;
         r.dL_dpix = dL_dout_color; r.dL_dinvd = dL_dout_invdepth; r.rec = sc.rec; r.flag = sc.flag;
-        r.invd_nonzero = nullptr;
-        { PROF("render_bwd"); gs::launch_render_bwd(r, sc.invd_flag, s); }
+        { PROF("render_bwd"); gs::launch_render_bwd(r, g.counters, s); }
         DBG_SYNC(a->debug, s);
     }
     gs::GaussBwdArgs q;
@@ -405,7 +502,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     q.means3D = a->means3D; q.scales = a->scales; q.rotations = a->rotations; q.opacities = a->opacities;
     q.dc = a->dc; q.sh = (a->M > 0) ? a->sh : nullptr; q.cov3D_precomp = a->cov3D_precomp;
     q.view = a->viewmatrix; q.proj = a->projmatrix; q.campos = a->campos;
-    q.radii = radii; q.cnt = g.cnt; q.first_e = g.first_e; q.sp = g.sp; q.rec = sc.rec; q.flag = sc.flag; q.sums = sc.sums;
+    q.radii = radii; q.cnt = g.rcnt; q.first_e = g.first_e; q.sp = g.sp; q.rec = sc.rec; q.flag = sc.flag; q.sums = sc.sums;
     q.dmeans2D = dmeans2D; q.dcolors = dcolors; q.dopacity = dopacity; q.dmeans3D = dmeans3D; q.dcov3D = dcov3D;
     q.ddc = ddc; q.dsh = dsh; q.dscales = dscales; q.drot = drot; q.depth = depth;
     if (q.M > 0 && !dsh) return fail("dsh output required when M > 0%s%d");
@@ -487,16 +584,30 @@ __global__ void k_gather_g(uint32_t K, const uint32_t* s_e, const uint32_t* eg, 
 }
 }  // namespace
 
-int dg_debug_sorted_instances(const void* binning, int64_t K, int W, int H, uint32_t* tiles_out, uint32_t* gauss_out,
+int dg_debug_sorted_instances(const dg_raster_args* a, const void* geom, const void* binning, const void* binning2,
+                              int64_t K, uint32_t* tiles_out, uint32_t* gauss_out, int64_t* e1_out,
                               dg_stream_t stream) {
-    if (K <= 0) return 0;
     hipStream_t s = (hipStream_t)stream;
-    Binning b = carve_binning((void*)binning, K);
-    const int passes = (bits_for((uint32_t)(tiles_x_of(W) * tiles_y_of(H))) + 7) / 8;
-    const uint32_t* s_e = (passes & 1) ? b.se1 : b.se0;
-    const uint32_t* keys = (passes & 1) ? b.tk1 : b.tk0;
-    HIP_OK(hipMemcpyAsync(tiles_out, keys, 4 * (size_t)K, hipMemcpyDeviceToDevice, s));
-    k_gather_g<<<(unsigned)((K + 255) / 256), 256, 0, s>>>((uint32_t)K, s_e, b.eg, gauss_out);
+    const int T = tiles_x_of(a->W) * tiles_y_of(a->H);
+    Geom g = carve_geom((void*)geom, a->P);
+    uint32_t hc[16];
+    HIP_OK(hipMemcpyAsync(hc, g.counters, sizeof(hc), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    const uint32_t E1 = hc[gs::CNT_E1];
+    *e1_out = E1;
+    const int passes = (bits_for((uint32_t)T) + 7) / 8;
+    if (E1 > 0) {
+        Binning b = carve_binning((void*)binning, phase1_cap(a, T, K));
+        HIP_OK(hipMemcpyAsync(tiles_out, (passes & 1) ? b.tk1 : b.tk0, 4 * (size_t)E1, hipMemcpyDeviceToDevice, s));
+        k_gather_g<<<(E1 + 255) / 256, 256, 0, s>>>(E1, (passes & 1) ? b.se1 : b.se0, b.eg, gauss_out);
+    }
+    const int64_t K2 = binning2 ? (int64_t)hc[gs::CNT_K2] : 0;
+    if (binning2 && K2 > 0) {
+        Binning b2 = carve_binning((void*)binning2, K);
+        HIP_OK(hipMemcpyAsync(tiles_out + E1, (passes & 1) ? b2.tk1 : b2.tk0, 4 * (size_t)K2, hipMemcpyDeviceToDevice, s));
+        k_gather_g<<<(unsigned)((K2 + 255) / 256), 256, 0, s>>>((uint32_t)K2, (passes & 1) ? b2.se1 : b2.se0, b2.eg,
+                                                                  gauss_out + E1);
+    }
     HIP_OK(hipGetLastError());
     return 0;
 }

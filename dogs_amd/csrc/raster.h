@@ -25,16 +25,39 @@ struct PreArgs {
     float4* rgbi;       // rgb, 1 / view z
     uint32_t* depthkey; // float bits of view z, 0xffffffff when no tile survives the precise cull
     uint32_t* cnt;      // precise tile count
+    uint32_t* rcnt;     // records per Gaussian, zeroed here (written by the emission kernels)
     unsigned long long* rect_sum;  // num_rendered of the reference (sum of rect areas)
     uint32_t* err;
 };
 
+// Counters block at the head of the geometry state (device, uint32 slots).
+enum {
+    CNT_K = 0,          // precise instance total (all depth ranks)
+    CNT_ERR = 1,        // prefiltered violation
+    CNT_RECT_LO = 2,    // num_rendered (sum of rect areas), u64 in slots 2..3
+    CNT_R1 = 4,         // depth-rank cut: ranks [0, R1) are binned in phase 1
+    CNT_E1 = 5,         // instances of phase 1 (= emission offset of rank R1)
+    CNT_UNFINISHED = 6, // tiles with live pixels after phase 1 (only counted when CNT_CUT)
+    CNT_K2 = 7,         // phase-2 instances
+    CNT_CUT = 8,        // E1 < K: the phase-1 lists are prefixes
+    CNT_INVD = 9,       // backward: any(dL/dinvdepth != 0) (zeroed with the block by the forward)
+};
+
+// Depth-prefix binning (DESIGN.md "Binning"): phase 1 bins only the first E1 <= C1 instances of the global depth
+// order, which is a prefix of every tile's list; phase 2 bins the rest only for tiles phase 1 left unfinished.
 struct RenderArgs {
     int W, H, tiles_x, num_tiles;
     uint32_t K, P;          // bounds of s_e/eg and of the geometry arrays
     const uint2* ranges;
     const uint32_t* s_e;   // sorted instance -> emission index
     const uint32_t* eg;    // emission index -> Gaussian
+    // phase 2 (resume) / phase-1 bookkeeping
+    int phase;                  // 1 or 2
+    const uint2* ranges1;       // phase 2: the phase-1 ranges (contributor numbering continues after them)
+    uint32_t* counters;         // CNT_* (phase 1 reads CNT_CUT, counts CNT_UNFINISHED)
+    uint8_t* unfinished;        // [num_tiles]
+    float4* resume;             // [H*W] raw colour + live flag of unfinished tiles' pixels
+    uint2* ranges2_zero;        // phase 1: phase-2 range of each tile it marks unfinished, reset to empty
     const float4* sp;
     const float4* rgbi;
     const float* bg;
@@ -49,6 +72,11 @@ struct RenderBwdArgs {
     const uint32_t* max_contrib;
     const uint32_t* s_e;
     const uint32_t* eg;
+    const uint2* ranges2;       // phase-2 lists (nullptr when phase 2 did not run)
+    const uint32_t* s_e2;       // sorted phase-2 instance -> local emission index
+    const uint32_t* eg2;        // local phase-2 emission index -> Gaussian
+    const uint32_t* counters;   // CNT_E1: global emission index of phase-2 local index 0
+    const uint8_t* unfinished;  // ranges2[t] is valid only where unfinished[t]
     const float4* sp;
     const float4* rgbi;
     const float* bg;
@@ -58,7 +86,6 @@ struct RenderBwdArgs {
     const float* dL_dinvd;   // may be null
     float* rec;              // [K][12] per-instance gradient record
     uint8_t* flag;           // [K] record written
-    const uint32_t* invd_nonzero;  // device flag: any(dL_dinvd != 0)
 };
 
 struct GaussBwdArgs {
@@ -78,13 +105,31 @@ struct GaussBwdArgs {
 };
 
 void launch_preprocess(const PreArgs& a, hipStream_t s);
+// also zeroes the phase-1 tile ranges (ranges[num_tiles])
+void launch_prefix_cut(const uint32_t* off, uint32_t P, uint32_t cap, uint32_t* counters, uint2* ranges,
+                       uint32_t num_tiles, hipStream_t s);
+// phase 1: ranks [0, counters[CNT_R1]) -> instances [0, E1); rcnt/first_e of those Gaussians
 void launch_emit(int P, const uint32_t* order, const uint32_t* skey, const uint32_t* off, const float4* sp,
-                 int tiles_x, uint32_t* first_e, uint32_t* tilekey, uint32_t* eg, hipStream_t s);
-void launch_ranges(uint32_t K, const uint32_t* keys, uint2* ranges, uint32_t num_tiles, hipStream_t s);
+                 int tiles_x, const uint32_t* counters, uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey,
+                 uint32_t* eg, hipStream_t s);
+// phase 2 over ranks [R1, P): only (Gaussian, tile) instances whose tile is unfinished
+// all phase-2 kernels are gated on counters[CNT_UNFINISHED] (device): no-ops when phase 1 finished every tile
+void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, int tiles_x, int tiles_y,
+                           uint32_t* sat, hipStream_t s);
+void launch_count2(int P, uint32_t R1, const uint32_t* counters, const uint32_t* order, const uint32_t* skey,
+                   const float4* sp, int tiles_x, int tiles_y, const uint8_t* unfinished, const uint32_t* sat,
+                   uint32_t* cnt2, hipStream_t s);
+void launch_emit2(int P, uint32_t R1, const uint32_t* counters, const uint32_t* order, const uint32_t* skey,
+                  const float4* sp, int tiles_x, int tiles_y, const uint8_t* unfinished, const uint32_t* sat,
+                  const uint32_t* cnt2, const uint32_t* off2, uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey,
+                  uint32_t* eg, hipStream_t s);
+void launch_ranges(uint32_t Kcap, const uint32_t* n_dev, const uint32_t* keys, uint2* ranges, uint32_t num_tiles,
+                   hipStream_t s);
 void launch_render_fwd(const RenderArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);
 void launch_filter(const PreArgs& a, hipStream_t s);
-void launch_render_bwd(const RenderBwdArgs& a, uint32_t* invd_flag, hipStream_t s);
+// clears the record flags of the E1 + K2 binned instances and sets counters[CNT_INVD], then replays
+void launch_render_bwd(const RenderBwdArgs& a, uint32_t* counters, hipStream_t s);
 void launch_record_sum(const GaussBwdArgs& a, hipStream_t s);
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s);
 

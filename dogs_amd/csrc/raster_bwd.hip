@@ -131,8 +131,13 @@ __device__ __forceinline__ bool bwd_pair(PairState& P, SplatAcc& acc, const v2f 
 
 template <bool HAS_INVD, bool HAS_BG>
 __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile, int lane, float4* sb) {
+    // the tile's list = its phase-1 prefix followed by its phase-2 remainder (depth-prefix binning)
     const uint2 rg = a.ranges[tile];
-    const int nall = (int)(rg.y - rg.x);
+    const int n1 = (int)(rg.y - rg.x);
+    uint2 rg2 = make_uint2(0u, 0u);
+    if (a.ranges2 && a.unfinished[tile]) rg2 = a.ranges2[tile];
+    const int nall = n1 + (int)(rg2.y - rg2.x);
+    const uint32_t E1 = a.counters[CNT_E1];
     const int mc = (int)a.max_contrib[tile];
     const int n = nall < mc ? nall : mc;
     if (n <= 0) return;
@@ -186,8 +191,15 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
         const int j = base + lane;
         uint32_t qm = 0;
         if (j < n) {
-            const uint32_t ee = min(a.s_e[rg.x + j], a.K - 1);
-            const uint32_t g = min(a.eg[ee], a.P - 1);
+            uint32_t ee, g;
+            if (j < n1) {
+                ee = min(a.s_e[rg.x + j], a.K - 1);
+                g = min(a.eg[ee], a.P - 1);
+            } else {
+                const uint32_t el = min(a.s_e2[rg2.x + (uint32_t)(j - n1)], a.K - 1 - E1);
+                ee = E1 + el;
+                g = min(a.eg2[el], a.P - 1);
+            }
             const float4 s0 = a.sp[2 * g], s1 = a.sp[2 * g + 1];
             const float2 m = make_float2(s0.x, s0.y);
             const float4 c4 = make_float4(s0.z, s0.w, s1.x, s1.y);
@@ -238,7 +250,7 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
     if (tile >= a.num_tiles) return;
     float4* sb = &s_b[threadIdx.x >> 6][0][0];
     const bool has_bg = a.bg[0] != 0.0f || a.bg[1] != 0.0f || a.bg[2] != 0.0f;
-    const bool has_invd = a.dL_dinvd != nullptr && *a.invd_nonzero != 0u;
+    const bool has_invd = a.dL_dinvd != nullptr && a.counters[CNT_INVD] != 0u;
     if (has_invd) {
         if (has_bg) render_bwd_tile<true, true>(a, tile, lane, sb);
         else render_bwd_tile<true, false>(a, tile, lane, sb);
@@ -248,12 +260,21 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
     }
 }
 
-// flag = any(dL/dinvdepth != 0): lets the replay drop the inverse-depth terms when the loss ignores depth
-__global__ void __launch_bounds__(256) k_any_nonzero(const float* __restrict__ x, uint32_t n, uint32_t* __restrict__ flag) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    bool nz = false;
-    for (; i < n; i += gridDim.x * blockDim.x) nz |= (x[i] != 0.0f);
-    if (__any(nz) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+// Backward prologue, one launch: zero the record flags of the E1 + K2 binned instances (device-side count) and
+// set counters[CNT_INVD] = any(dL/dinvdepth != 0), which lets the replay drop the inverse-depth terms.
+__global__ void __launch_bounds__(256) k_bwd_prologue(uint32_t* __restrict__ counters, uint8_t* __restrict__ flag,
+                                                      uint32_t Kcap, const float* __restrict__ dinvd, uint32_t npix) {
+    const uint32_t nflags = min(counters[CNT_E1] + counters[CNT_K2], Kcap);
+    const uint32_t stride = gridDim.x * blockDim.x;
+    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t* f4 = reinterpret_cast<uint32_t*>(flag);  // the flag block is 256-B aligned
+    for (uint32_t i = i0; i < nflags / 4; i += stride) f4[i] = 0u;
+    for (uint32_t i = (nflags & ~3u) + i0; i < nflags; i += stride) flag[i] = 0;
+    if (dinvd) {
+        bool nz = false;
+        for (uint32_t i = i0; i < npix; i += stride) nz |= (dinvd[i] != 0.0f);
+        if (__any(nz) && (threadIdx.x & 63) == 0) atomicOr(counters + CNT_INVD, 1u);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -655,15 +676,9 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
     }
 }
 
-void launch_render_bwd(const RenderBwdArgs& a, uint32_t* invd_flag, hipStream_t s) {
-    if (a.dL_dinvd) {
-        (void)hipMemsetAsync(invd_flag, 0, sizeof(uint32_t), s);
-        const uint32_t n = (uint32_t)a.W * a.H;
-        k_any_nonzero<<<512, 256, 0, s>>>(a.dL_dinvd, n, invd_flag);
-    }
-    RenderBwdArgs b = a;
-    b.invd_nonzero = invd_flag;
-    if (a.num_tiles > 0) k_render_bwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(b);
+void launch_render_bwd(const RenderBwdArgs& a, uint32_t* counters, hipStream_t s) {
+    k_bwd_prologue<<<512, 256, 0, s>>>(counters, a.flag, a.K, a.dL_dinvd, (uint32_t)a.W * a.H);
+    if (a.num_tiles > 0) k_render_bwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
 }
 void launch_record_sum(const GaussBwdArgs& a, hipStream_t s) {
     if (a.P > 0) k_record_sum<<<(a.P + 255) / 256, 256, 0, s>>>(a);

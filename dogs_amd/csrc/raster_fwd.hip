@@ -141,6 +141,7 @@ struct RectOut { int x0, y0, x1, y1; float mx, my, thr; float4 co; };
 __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, const float* lsh, RectOut& ro) {
     a.radii[idx] = 0;
     a.depthkey[idx] = 0xffffffffu;
+    a.rcnt[idx] = 0u;
     const f3 po = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
     // in_frustum (auxiliary.h:150-175)
     const f3 pv = tp4x3(po, a.view);
@@ -262,31 +263,65 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     }
 }
 
-// emission in depth order: instance e = off[p] + j for the j-th kept tile of Gaussian order[p].  A wave
-// owns 64 consecutive depth ranks, so its instances form one contiguous run starting at off[p0]; the
+// Depth-prefix cut: the largest rank R1 whose instances [0, off[R1]) fit the phase-1 capacity `cap`.  Ranks
+// are in depth order and every tile's list is in depth order, so instances of ranks < R1 are a PREFIX of
+// every tile's list (DESIGN.md "Binning").  No cut when everything fits.
+__global__ void k_prefix_cut(const uint32_t* __restrict__ off, uint32_t P, uint32_t cap, uint32_t* __restrict__ counters,
+                             uint2* __restrict__ ranges, uint32_t num_tiles) {
+    for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) ranges[t] = make_uint2(0u, 0u);
+    if (threadIdx.x != 0) return;
+    const uint32_t K = counters[CNT_K];
+    uint32_t R1 = P, E1 = K, cut = 0;
+    if (K > cap && P > 0) {
+        uint32_t lo = 0, hi = P - 1;  // invariant: off[lo] <= cap (off[0] == 0)
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo + 1) / 2;
+            if (off[mid] <= cap) lo = mid; else hi = mid - 1;
+        }
+        R1 = lo;
+        E1 = off[lo];
+        cut = 1;
+    }
+    counters[CNT_R1] = R1;
+    counters[CNT_E1] = E1;
+    counters[CNT_CUT] = cut;
+    counters[CNT_UNFINISHED] = 0;
+    counters[CNT_K2] = 0;
+}
+
+constexpr int EMIT_RANKS = 16;
+
+// Phase-1 emission in depth order: instance e = off[p] + j for the j-th kept tile of Gaussian order[p], p < R1.
+// A wave owns 64 consecutive depth ranks, so its instances form one contiguous run starting at off[p0]; the
 // cooperative candidate walk writes them in (p, ty, tx) order with consecutive lanes -> consecutive e.
-// Ranks whose sorted depth key is 0xffffffff are the culled tail (no kept tile) and are skipped; the
-// rest gather ONE 32-B splat record each.
+// Ranks past the cut (and the culled tail, sorted key 0xffffffff) are skipped; the rest gather ONE 32-B splat
+// record each.  rcnt[g] = instances emitted for g (the record count of the backward).
 __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict__ order,
                                               const uint32_t* __restrict__ skey, const uint32_t* __restrict__ off,
                                               const float4* __restrict__ sp, int tiles_x,
-                                              uint32_t* __restrict__ first_e, uint32_t* __restrict__ tilekey,
-                                              uint32_t* __restrict__ eg) {
+                                              const uint32_t* __restrict__ counters,
+                                              uint32_t* __restrict__ first_e, uint32_t* __restrict__ rcnt,
+                                              uint32_t* __restrict__ tilekey, uint32_t* __restrict__ eg) {
     __shared__ CandLDS s_cand[4];
     __shared__ uint32_t s_g[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int p0 = blockIdx.x * blockDim.x + w * 64;
-    if (p0 >= P) return;  // whole wave
+    // EMIT_RANKS ranks per wave: the depth prefix holds the nearest, largest Gaussians (~100 candidate tiles
+    // each), so 64 ranks per wave would leave ~one long serial wave per SIMD
+    const int p0 = (blockIdx.x * 4 + w) * EMIT_RANKS;
+    const int R1 = (int)counters[CNT_R1];
+    if (p0 >= R1 || p0 >= P) return;      // whole wave
     if (skey[p0] == 0xffffffffu) return;  // whole wave in the culled tail
     const int p = p0 + lane;
     int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
     float mx = 0.f, my = 0.f, thr = 0.f;
     float4 c4 = make_float4(0.f, 0.f, 0.f, 0.f);
     uint32_t g = 0xffffffffu;
-    if (p < P && skey[p] != 0xffffffffu) {
+    if (lane < EMIT_RANKS && p < R1 && skey[p] != 0xffffffffu) {
         g = order[p];
         if (g < (uint32_t)P) {
-            first_e[g] = off[p];
+            const uint32_t e0 = off[p];
+            first_e[g] = e0;
+            rcnt[g] = ((p + 1 < P) ? off[p + 1] : counters[CNT_K]) - e0;
             const float4 s0 = sp[2 * g], s1 = sp[2 * g + 1];
             c4 = make_float4(s0.z, s0.w, s1.x, s1.y);
             mx = s0.x; my = s0.y;
@@ -311,15 +346,128 @@ __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict_
                     });
 }
 
+// Exclusive summed-area table of the unfinished-tile flags, [(tiles_y+1) x (tiles_x+1)]: O(1) "does this
+// rect touch an unfinished tile" for the phase-2 kernels.
+__global__ void __launch_bounds__(1024) k_unfinished_sat(const uint32_t* __restrict__ counters,
+                                                          const uint8_t* __restrict__ unf, int tx, int ty,
+                                                          uint32_t* __restrict__ sat) {
+    if (counters[CNT_UNFINISHED] == 0u) return;
+    const int W1 = tx + 1;
+    for (int x = threadIdx.x; x < W1; x += blockDim.x) sat[x] = 0u;
+    for (int y = threadIdx.x; y < ty; y += blockDim.x) {
+        uint32_t run = 0;
+        sat[(size_t)(y + 1) * W1] = 0u;
+        for (int x = 0; x < tx; x++) {
+            run += unf[(size_t)y * tx + x] ? 1u : 0u;
+            sat[(size_t)(y + 1) * W1 + x + 1] = run;
+        }
+    }
+    __syncthreads();
+    for (int x = threadIdx.x + 1; x < W1; x += blockDim.x) {
+        uint32_t run = 0;
+        for (int y = 1; y <= ty; y++) {
+            run += sat[(size_t)y * W1 + x];
+            sat[(size_t)y * W1 + x] = run;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t sat_rect(const uint32_t* sat, int tx, int x0, int y0, int x1, int y1) {
+    const int W1 = tx + 1;
+    return sat[(size_t)y1 * W1 + x1] - sat[(size_t)y0 * W1 + x1] - sat[(size_t)y1 * W1 + x0] + sat[(size_t)y0 * W1 + x0];
+}
+
+// Phase 2 over ranks [R1, P): the same wave-cooperative candidate walk, keeping only tiles phase 1 left
+// unfinished (Gaussians whose rect misses every unfinished tile skip the walk).  COUNT: cnt2[p - R1];
+// EMIT: instances at local index off2[p - R1] + j, first_e = E1 + that, rcnt = cnt2.
+template <bool EMIT>
+__global__ void __launch_bounds__(256) k_phase2(int P, uint32_t R1, const uint32_t* __restrict__ counters,
+                                                const uint32_t* __restrict__ order,
+                                                const uint32_t* __restrict__ skey, const float4* __restrict__ sp,
+                                                int tiles_x, int tiles_y, const uint8_t* __restrict__ unf,
+                                                const uint32_t* __restrict__ sat, uint32_t* __restrict__ cnt2,
+                                                const uint32_t* __restrict__ off2, uint32_t* __restrict__ first_e,
+                                                uint32_t* __restrict__ rcnt, uint32_t* __restrict__ tilekey,
+                                                uint32_t* __restrict__ eg) {
+    __shared__ CandLDS s_cand[4];
+    __shared__ uint32_t s_g[4][64];
+    __shared__ uint32_t s_cnt[4][64];
+    if (counters[CNT_UNFINISHED] == 0u) return;  // phase 1 finished every tile
+    const uint32_t E1 = counters[CNT_E1];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int p0 = (int)R1 + blockIdx.x * blockDim.x + w * 64;
+    if (p0 >= P) return;
+    if (skey[p0] == 0xffffffffu) {  // whole wave in the culled tail
+        if (!EMIT && p0 + lane < P) cnt2[p0 + lane - R1] = 0u;
+        return;
+    }
+    const int p = p0 + lane;
+    int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    float mx = 0.f, my = 0.f, thr = 0.f;
+    float4 c4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint32_t g = 0xffffffffu;
+    if (p < P && skey[p] != 0xffffffffu) {
+        g = order[p];
+        if (g < (uint32_t)P) {
+            const float4 s0 = sp[2 * g], s1 = sp[2 * g + 1];
+            sp_rect(s1, x0, y0, x1, y1);
+            bool any = x1 > x0 && y1 > y0 && sat_rect(sat, tiles_x, x0, y0, x1, y1) != 0u;
+            if (EMIT) {
+                const uint32_t c = cnt2[p - R1];
+                any = any && c != 0u;
+                if (c) { first_e[g] = E1 + off2[p - R1]; rcnt[g] = c; }
+            }
+            if (any) {
+                c4 = make_float4(s0.z, s0.w, s1.x, s1.y);
+                mx = s0.x; my = s0.y;
+                thr = gs_logf(c4.w / (1.0f / 255.0f));
+            } else {
+                x1 = x0; y1 = y0;
+            }
+        }
+    }
+    s_g[w][lane] = g;
+    s_cnt[w][lane] = 0u;
+    const uint32_t e0 = EMIT ? off2[p0 - R1] : 0u;
+    uint32_t running = 0;
+    CandLDS& L = s_cand[w];
+    wave_candidates(L, lane, x0, y0, x1, y1, mx, my, c4, thr,
+                    [&](int owner, int tx, int ty, bool kept, bool valid, uint32_t item) {
+                        kept = kept && unf[ty * tiles_x + tx] != 0;
+                        const uint64_t km = __ballot(kept);
+                        if (EMIT) {
+                            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+                            if (kept) {
+                                const uint32_t e = e0 + running + (uint32_t)__popcll(km & lt);
+                                tilekey[e] = (uint32_t)(ty * tiles_x + tx);
+                                eg[e] = s_g[w][owner];
+                            }
+                            running += (uint32_t)__popcll(km);
+                        } else {
+                            const bool seg_start = valid && (lane == 0 || item == L.pre[owner]);
+                            if (seg_start) {
+                                const uint32_t seg_end_item = L.pre[owner] + (uint32_t)L.area[owner];
+                                const int len = (int)min(seg_end_item - item, (uint32_t)(64 - lane));
+                                const uint64_t seg = (len >= 64 ? ~0ull : ((1ull << len) - 1ull)) << lane;
+                                s_cnt[w][owner] += (uint32_t)__popcll(km & seg);
+                            }
+                            __builtin_amdgcn_wave_barrier();
+                        }
+                    });
+    if (!EMIT && p < P) cnt2[p - R1] = s_cnt[w][lane];
+}
+
 // identifyTileRanges over the sorted (all-valid) tile keys
-__global__ void __launch_bounds__(256) k_ranges(uint32_t K, const uint32_t* __restrict__ keys,
-                                                uint2* __restrict__ ranges, uint32_t num_tiles) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= K) return;
-    const uint32_t t = keys[i];
-    if (t >= num_tiles) return;
-    if (i == 0 || keys[i - 1] != t) ranges[t].x = i;
-    if (i == K - 1 || keys[i + 1] != t) ranges[t].y = i + 1;
+__global__ void __launch_bounds__(256) k_ranges(uint32_t Kcap, const uint32_t* __restrict__ n_dev,
+                                                const uint32_t* __restrict__ keys, uint2* __restrict__ ranges,
+                                                uint32_t num_tiles) {
+    const uint32_t K = n_dev ? min(*n_dev, Kcap) : Kcap;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < K; i += gridDim.x * blockDim.x) {
+        const uint32_t t = keys[i];
+        if (t >= num_tiles) continue;
+        if (i == 0 || keys[i - 1] != t) ranges[t].x = i;
+        if (i == K - 1 || keys[i + 1] != t) ranges[t].y = i + 1;
+    }
 }
 
 __device__ __forceinline__ float bcast(float v, int lane) {
@@ -338,11 +486,13 @@ __device__ __forceinline__ uint32_t bcast_u(uint32_t v, int lane) {
 // reads each with broadcast ds_read_b128 and skips a pair whose two quadrant bits are clear.  The
 // per-pixel update is branch-free: a rejected or finished pixel gets alpha = 0, which leaves C, D and T
 // unchanged.  Wave-uniform early exit once every pixel of the tile has saturated.
+template <int PHASE>
 __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a) {
     __shared__ float4 s_b[4][64][3];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tile = blockIdx.x * 4 + w;
     if (tile >= a.num_tiles) return;
+    if (PHASE == 2 && !a.unfinished[tile]) return;  // finished in phase 1: outputs already final
     float4* sb = &s_b[w][0][0];
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
     const int tx0 = tx * GS_TILE_X, ty0 = ty * GS_TILE_Y;
@@ -352,11 +502,22 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a) {
     // per-pixel state; a finished (or outside) pixel gets alpha threshold 2, which no alpha reaches
     v4f T = bc4(1.0f), C0 = bc4(0.0f), C1 = bc4(0.0f), C2 = bc4(0.0f), D = bc4(0.0f), thr;
     uint32_t last[4] = {0, 0, 0, 0};
+    uint32_t cbase = 0;  // contributor numbering continues over the concatenated phase-1 + phase-2 list
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int px = c0 + (k >> 1) * 8, py = rA + (k & 1) * 8;
-        thr[k] = (px < a.W && py < a.H) ? (1.0f / 255.0f) : 2.0f;
+        const bool inside = px < a.W && py < a.H;
+        thr[k] = inside ? (1.0f / 255.0f) : 2.0f;
+        if (PHASE == 2 && inside) {  // resume the phase-1 state of this pixel
+            const size_t pid = (size_t)py * a.W + px;
+            const float4 rs = a.resume[pid];
+            T[k] = a.final_T[pid];
+            D[k] = a.img_invd[pid];
+            last[k] = a.n_contrib[pid];
+            C0[k] = rs.x; C1[k] = rs.y; C2[k] = rs.z; thr[k] = rs.w;
+        }
     }
+    if (PHASE == 2) cbase = a.ranges1[tile].y - a.ranges1[tile].x;
     const uint2 rg = a.ranges[tile];
     const int n = (int)(rg.y - rg.x);
     for (int base = 0; base < n; base += 64) {
@@ -382,7 +543,7 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a) {
             const int jj = (int)__builtin_ctzll(mask);
             mask &= mask - 1;
             const float4 Sa = s_b[w][jj][0], Sb = s_b[w][jj][1], Sc = s_b[w][jj][2];
-            const uint32_t c = (uint32_t)(base + jj + 1);
+            const uint32_t c = cbase + (uint32_t)(base + jj + 1);
             const v4f p2 = splat_power4(Sa.z, Sa.w, Sb.x, Sa.x, Sa.y, pxv, pyv);
             v4f al = bc4(Sb.y) * (v4f){__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y),
                                        __builtin_amdgcn_exp2f(p2.z), __builtin_amdgcn_exp2f(p2.w)};
@@ -437,6 +598,26 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a) {
         mx = y > mx ? y : mx;
     }
     if (lane == 0) a.max_contrib[tile] = mx;
+    if (PHASE == 1) {
+        // A tile with a live pixel after a truncated (prefix) list needs phase 2: keep its raw state.
+        const bool cut = a.counters[CNT_CUT] != 0u;
+        const bool live = fminf(fminf(thr.x, thr.y), fminf(thr.z, thr.w)) < 1.0f;
+        const bool unf = cut && __any(live);
+        if (lane == 0) {
+            a.unfinished[tile] = unf ? 1 : 0;
+            if (unf) {
+                atomicAdd(a.counters + CNT_UNFINISHED, 1u);
+                a.ranges2_zero[tile] = make_uint2(0u, 0u);  // empty unless phase 2 bins instances for it
+            }
+        }
+        if (unf) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int px = c0 + (k >> 1) * 8, py = rA + (k & 1) * 8;
+                if (px < a.W && py < a.H) a.resume[(size_t)py * a.W + px] = make_float4(C0[k], C1[k], C2[k], thr[k]);
+            }
+        }
+    }
 }
 
 // checkFrustum (rasterizer_impl.cu:104-116)
@@ -489,15 +670,49 @@ void launch_preprocess(const PreArgs& a, hipStream_t s) {
     if (lds < cand) lds = cand;
     if (a.P > 0) k_preprocess<<<(a.P + 255) / 256, 256, lds, s>>>(a);
 }
-void launch_emit(int P, const uint32_t* order, const uint32_t* skey, const uint32_t* off, const float4* sp,
-                 int tiles_x, uint32_t* first_e, uint32_t* tilekey, uint32_t* eg, hipStream_t s) {
-    if (P > 0) k_emit<<<(P + 255) / 256, 256, 0, s>>>(P, order, skey, off, sp, tiles_x, first_e, tilekey, eg);
+void launch_prefix_cut(const uint32_t* off, uint32_t P, uint32_t cap, uint32_t* counters, uint2* ranges,
+                       uint32_t num_tiles, hipStream_t s) {
+    k_prefix_cut<<<1, 1024, 0, s>>>(off, P, cap, counters, ranges, num_tiles);
 }
-void launch_ranges(uint32_t K, const uint32_t* keys, uint2* ranges, uint32_t num_tiles, hipStream_t s) {
-    if (K > 0) k_ranges<<<(K + 255) / 256, 256, 0, s>>>(K, keys, ranges, num_tiles);
+void launch_emit(int P, const uint32_t* order, const uint32_t* skey, const uint32_t* off, const float4* sp,
+                 int tiles_x, const uint32_t* counters, uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey,
+                 uint32_t* eg, hipStream_t s) {
+    const int per_block = 4 * EMIT_RANKS;
+    if (P > 0)
+        k_emit<<<(P + per_block - 1) / per_block, 256, 0, s>>>(P, order, skey, off, sp, tiles_x, counters, first_e,
+                                                               rcnt, tilekey, eg);
+}
+void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, int tiles_x, int tiles_y,
+                           uint32_t* sat, hipStream_t s) {
+    k_unfinished_sat<<<1, 1024, 0, s>>>(counters, unfinished, tiles_x, tiles_y, sat);
+}
+void launch_count2(int P, uint32_t R1, const uint32_t* counters, const uint32_t* order, const uint32_t* skey,
+                   const float4* sp, int tiles_x, int tiles_y, const uint8_t* unfinished, const uint32_t* sat,
+                   uint32_t* cnt2, hipStream_t s) {
+    const int n = P - (int)R1;
+    if (n > 0)
+        k_phase2<false><<<(n + 255) / 256, 256, 0, s>>>(P, R1, counters, order, skey, sp, tiles_x, tiles_y, unfinished,
+                                                         sat, cnt2, nullptr, nullptr, nullptr, nullptr, nullptr);
+}
+void launch_emit2(int P, uint32_t R1, const uint32_t* counters, const uint32_t* order, const uint32_t* skey,
+                  const float4* sp, int tiles_x, int tiles_y, const uint8_t* unfinished, const uint32_t* sat,
+                  const uint32_t* cnt2, const uint32_t* off2, uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey,
+                  uint32_t* eg, hipStream_t s) {
+    const int n = P - (int)R1;
+    if (n > 0)
+        k_phase2<true><<<(n + 255) / 256, 256, 0, s>>>(P, R1, counters, order, skey, sp, tiles_x, tiles_y, unfinished,
+                                                        sat, const_cast<uint32_t*>(cnt2), off2, first_e, rcnt,
+                                                        tilekey, eg);
+}
+void launch_ranges(uint32_t Kcap, const uint32_t* n_dev, const uint32_t* keys, uint2* ranges, uint32_t num_tiles,
+                   hipStream_t s) {
+    const uint32_t blocks = (Kcap + 255) / 256;
+    if (Kcap > 0) k_ranges<<<blocks < 2048u ? blocks : 2048u, 256, 0, s>>>(Kcap, n_dev, keys, ranges, num_tiles);
 }
 void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
-    if (a.num_tiles > 0) k_render_fwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
+    if (a.num_tiles <= 0) return;
+    if (a.phase == 2) k_render_fwd<2><<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
+    else k_render_fwd<1><<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
 }
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s) {
     if (P > 0) k_mark_visible<<<(P + 255) / 256, 256, 0, s>>>(P, means3D, view, present);

@@ -8,13 +8,16 @@ namespace gs {
 // Stable LSD radix sort of (key, value) pairs over bits [begin_bit, end_bit), 8 bits per pass.
 // Pass 0 reads values from vals_first (nullptr -> value = input index).  Ping-pongs between the
 // (keys0, vals0) and (keys1, vals1) buffers; keys0 holds the input.  Returns 1 when the result is in
-// keys1/vals1, 0 when it is in keys0/vals0.
+// keys1/vals1, 0 when it is in keys0/vals0.  n sizes the launch; when n_dev is given the kernels sort
+// only the first min(*n_dev, n) elements (device-side count, no host sync).
 size_t radix_sort_temp_bytes(uint32_t n);
 int radix_sort_pairs(uint32_t* keys0, uint32_t* vals0, uint32_t* keys1, uint32_t* vals1, const uint32_t* vals_first,
-                     uint32_t n, int begin_bit, int end_bit, void* temp, hipStream_t stream);
+                     uint32_t n, int begin_bit, int end_bit, void* temp, hipStream_t stream,
+                     const uint32_t* n_dev = nullptr);
 
-// out[i] = sum_{j<i} in[gather ? gather[j] : j];  *total = full sum (device pointer)
+// out[i] = sum_{j<i} in[gather ? gather[j] : j];  *total = full sum (device pointer).
+// gate (optional, device): when *gate == 0 nothing is read or written except *total = 0.
 size_t scan_temp_bytes(uint32_t n);
 void exclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t n, uint32_t* out, uint32_t* total,
-                    void* temp, hipStream_t stream);
+                    void* temp, hipStream_t stream, const uint32_t* gate = nullptr);
 }  // namespace gs

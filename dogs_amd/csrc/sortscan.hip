@@ -38,14 +38,29 @@ __device__ __forceinline__ uint64_t peer_mask(uint32_t digit, bool active) {
     return active ? m : 0ull;
 }
 
-__global__ void __launch_bounds__(RS_THREADS) rs_upsweep(const uint32_t* __restrict__ keys, uint32_t n, int shift,
+// n_dev (optional): element count read on the device, <= the capacity n the grid was sized for; tiles past
+// it count nothing and scatter nothing, so a launch sized for a capacity sorts a prefix without a host sync.
+__device__ __forceinline__ uint32_t eff_n(uint32_t n, const uint32_t* n_dev) {
+    if (!n_dev) return n;
+    const uint32_t d = *n_dev;
+    return d < n ? d : n;
+}
+
+__global__ void __launch_bounds__(RS_THREADS) rs_upsweep(const uint32_t* __restrict__ keys, uint32_t ncap,
+                                                         const uint32_t* __restrict__ n_dev, int shift,
                                                          uint32_t* __restrict__ counts, uint32_t ntiles) {
     __shared__ uint32_t hist[RS_RADIX];
     const int t = threadIdx.x;
     hist[t] = 0;
     __syncthreads();
+    const uint32_t n = eff_n(ncap, n_dev);
     const uint32_t tile = blockIdx.x;
     const uint32_t base = tile * RS_TILE;
+    if (n == 0u) return;  // nothing to sort (rs_scan and rs_downsweep leave too)
+    if (base >= n) {  // past the device-side count: nothing to count (uniform per block)
+        counts[(size_t)t * ntiles + tile] = 0u;
+        return;
+    }
     const int lane = __lane_id();
 #pragma unroll 4
     for (int r = 0; r < RS_ITEMS; r++) {
@@ -61,9 +76,11 @@ __global__ void __launch_bounds__(RS_THREADS) rs_upsweep(const uint32_t* __restr
 
 // one block per digit: exclusive scan over tiles in place, total -> digit_total[d]
 __global__ void __launch_bounds__(1024) rs_scan(uint32_t* __restrict__ counts, uint32_t ntiles,
-                                                uint32_t* __restrict__ digit_total) {
+                                                uint32_t* __restrict__ digit_total,
+                                                const uint32_t* __restrict__ n_dev) {
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t carry;
+    if (n_dev && *n_dev == 0u) return;  // nothing to sort: every downsweep tile leaves too
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint32_t* row = counts + (size_t)blockIdx.x * ntiles;
     if (t == 0) carry = 0;
@@ -101,7 +118,8 @@ __global__ void __launch_bounds__(1024) rs_scan(uint32_t* __restrict__ counts, u
 __global__ void __launch_bounds__(RS_THREADS) rs_downsweep(const uint32_t* __restrict__ keys_in,
                                                            const uint32_t* __restrict__ vals_in,
                                                            uint32_t* __restrict__ keys_out,
-                                                           uint32_t* __restrict__ vals_out, uint32_t n, int shift,
+                                                           uint32_t* __restrict__ vals_out, uint32_t ncap,
+                                                           const uint32_t* __restrict__ n_dev, int shift,
                                                            const uint32_t* __restrict__ counts, uint32_t ntiles,
                                                            const uint32_t* __restrict__ digit_total) {
     __shared__ uint32_t s_keys[RS_TILE];
@@ -112,8 +130,10 @@ __global__ void __launch_bounds__(RS_THREADS) rs_downsweep(const uint32_t* __res
     __shared__ uint32_t s_wtmp[RS_WAVES];
 
     const int t = threadIdx.x, lane = __lane_id(), w = t >> 6;
+    const uint32_t n = eff_n(ncap, n_dev);
     const uint32_t tile = blockIdx.x;
     const uint32_t base = tile * RS_TILE;
+    if (base >= n) return;  // whole block (uniform)
 #pragma unroll
     for (int k = 0; k < RS_WAVES; k++) whist[k][t] = 0;
     // exclusive scan of digit totals (256) -> global digit base
@@ -209,7 +229,7 @@ size_t radix_sort_temp_bytes(uint32_t n) {
 }
 
 int radix_sort_pairs(uint32_t* keys0, uint32_t* vals0, uint32_t* keys1, uint32_t* vals1, const uint32_t* vals_first,
-                     uint32_t n, int begin_bit, int end_bit, void* temp, hipStream_t stream) {
+                     uint32_t n, int begin_bit, int end_bit, void* temp, hipStream_t stream, const uint32_t* n_dev) {
     if (n == 0) return 0;
     const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
     uint32_t* counts = (uint32_t*)temp;
@@ -217,10 +237,10 @@ int radix_sort_pairs(uint32_t* keys0, uint32_t* vals0, uint32_t* keys1, uint32_t
     uint32_t *kin = keys0, *vin = vals0, *kout = keys1, *vout = vals1;
     int pass = 0;
     for (int b = begin_bit; b < end_bit; b += 8, pass++) {
-        rs_upsweep<<<ntiles, RS_THREADS, 0, stream>>>(kin, n, b, counts, ntiles);
-        rs_scan<<<RS_RADIX, 1024, 0, stream>>>(counts, ntiles, totals);
-        rs_downsweep<<<ntiles, RS_THREADS, 0, stream>>>(kin, pass == 0 ? vals_first : vin, kout, vout, n, b, counts,
-                                                        ntiles, totals);
+        rs_upsweep<<<ntiles, RS_THREADS, 0, stream>>>(kin, n, n_dev, b, counts, ntiles);
+        rs_scan<<<RS_RADIX, 1024, 0, stream>>>(counts, ntiles, totals, n_dev);
+        rs_downsweep<<<ntiles, RS_THREADS, 0, stream>>>(kin, pass == 0 ? vals_first : vin, kout, vout, n, n_dev, b,
+                                                        counts, ntiles, totals);
         uint32_t* tk = kin; kin = kout; kout = tk;
         uint32_t* tv = vin; vin = vout; vout = tv;
     }
@@ -252,8 +272,10 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
 
 __global__ void __launch_bounds__(SC_THREADS) sc_reduce(const uint32_t* __restrict__ in,
                                                         const uint32_t* __restrict__ gather, uint32_t n,
-                                                        uint32_t* __restrict__ block_sums) {
+                                                        uint32_t* __restrict__ block_sums,
+                                                        const uint32_t* __restrict__ gate) {
     __shared__ uint32_t s_w[SC_THREADS / 64];
+    if (gate && *gate == 0u) return;
     const uint32_t base = blockIdx.x * SC_TILE + threadIdx.x * SC_ITEMS;
     uint32_t s = 0;
 #pragma unroll
@@ -267,9 +289,14 @@ __global__ void __launch_bounds__(SC_THREADS) sc_reduce(const uint32_t* __restri
 }
 
 __global__ void __launch_bounds__(SC_THREADS) sc_scan_sums(uint32_t* __restrict__ sums, uint32_t nb,
-                                                           uint32_t* __restrict__ total_out) {
+                                                           uint32_t* __restrict__ total_out,
+                                                           const uint32_t* __restrict__ gate) {
     __shared__ uint32_t s_w[SC_THREADS / 64];
     __shared__ uint32_t carry;
+    if (gate && *gate == 0u) {
+        if (threadIdx.x == 0 && total_out) *total_out = 0u;
+        return;
+    }
     if (threadIdx.x == 0) carry = 0;
     __syncthreads();
     for (uint32_t b = 0; b < nb; b += SC_THREADS) {
@@ -289,8 +316,10 @@ __global__ void __launch_bounds__(SC_THREADS) sc_scan_sums(uint32_t* __restrict_
 __global__ void __launch_bounds__(SC_THREADS) sc_downsweep(const uint32_t* __restrict__ in,
                                                            const uint32_t* __restrict__ gather, uint32_t n,
                                                            const uint32_t* __restrict__ block_sums,
-                                                           uint32_t* __restrict__ out) {
+                                                           uint32_t* __restrict__ out,
+                                                           const uint32_t* __restrict__ gate) {
     __shared__ uint32_t s_w[SC_THREADS / 64];
+    if (gate && *gate == 0u) return;
     const uint32_t base = blockIdx.x * SC_TILE + threadIdx.x * SC_ITEMS;
     uint32_t v[SC_ITEMS];
     uint32_t s = 0;
@@ -316,16 +345,16 @@ size_t scan_temp_bytes(uint32_t n) {
 }
 
 void exclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t n, uint32_t* out, uint32_t* total,
-                    void* temp, hipStream_t stream) {
+                    void* temp, hipStream_t stream, const uint32_t* gate) {
     const uint32_t nb = (n + SC_TILE - 1) / SC_TILE;
     uint32_t* sums = (uint32_t*)temp;
     if (n == 0) {
         (void)hipMemsetAsync(total, 0, sizeof(uint32_t), stream);
         return;
     }
-    sc_reduce<<<nb, SC_THREADS, 0, stream>>>(in, gather, n, sums);
-    sc_scan_sums<<<1, SC_THREADS, 0, stream>>>(sums, nb, total);
-    sc_downsweep<<<nb, SC_THREADS, 0, stream>>>(in, gather, n, sums, out);
+    sc_reduce<<<nb, SC_THREADS, 0, stream>>>(in, gather, n, sums, gate);
+    sc_scan_sums<<<1, SC_THREADS, 0, stream>>>(sums, nb, total, gate);
+    sc_downsweep<<<nb, SC_THREADS, 0, stream>>>(in, gather, n, sums, out, gate);
 }
 
 }  // namespace gs

@@ -11,6 +11,17 @@ from .. import _lib
 
 _EMPTY_U8 = None
 
+# Depth-prefix binning policy (dg_raster_args.prefix_per_tile): phase-1 capacity = this x tiles; 0 -> the
+# library default (256), < 0 -> bin every instance in one phase.  Module-level so that the forward and the
+# backward of a view always agree; tests lower it to exercise the phase-2 path.
+PREFIX_PER_TILE = 0
+
+
+def set_prefix_per_tile(n: int) -> int:
+    global PREFIX_PER_TILE
+    old, PREFIX_PER_TILE = PREFIX_PER_TILE, int(n)
+    return old
+
 
 def _f32(t: torch.Tensor | None) -> torch.Tensor | None:
     if t is None or t.numel() == 0:
@@ -23,6 +34,7 @@ def _args(P, D, M, W, H, bg, means3D, colors, opacity, scales, rotations, scale_
     a = _lib.DgRasterArgs()
     a.P, a.D, a.M, a.W, a.H = int(P), int(D), int(M), int(W), int(H)
     a.prefiltered, a.antialiasing, a.debug = int(bool(prefiltered)), int(bool(antialiasing)), int(bool(debug))
+    a.prefix_per_tile = int(PREFIX_PER_TILE)
     a.scale_modifier, a.tanfovx, a.tanfovy = float(scale_modifier), float(tan_fovx), float(tan_fovy)
     keep = dict(bg=_f32(bg), means3D=_f32(means3D), colors=_f32(colors), opacities=_f32(opacity),
                 scales=_f32(scales), rotations=_f32(rotations), cov3D_precomp=_f32(cov3D_precomp),
@@ -61,14 +73,16 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dc, sh, campos, prefiltered,
                         antialiasing, debug)
         arena = _lib.TensorArena(dev)
-        gp, bp, ip = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        gp, bp, ip, b2p = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
         nr, nk = C.c_int64(0), C.c_int64(0)
         _lib.check(_lib.load().dg_rasterize_forward(
             C.byref(a), out_color.data_ptr(), out_invdepth.data_ptr(), radii.data_ptr(), arena.fn, None,
-            C.byref(gp), C.byref(bp), C.byref(ip), C.byref(nr), C.byref(nk), _lib.stream_of(dev)))
+            C.byref(gp), C.byref(bp), C.byref(ip), C.byref(b2p), C.byref(nr), C.byref(nk), _lib.stream_of(dev)))
         del keep
+    # the reference's sampleBuffer slot carries the phase-2 binning block (empty when phase 2 did not run)
     return (int(nr.value), int(nk.value), out_color, out_invdepth, radii, arena.get(_lib.DG_BUF_GEOM),
-            arena.get(_lib.DG_BUF_BINNING), arena.get(_lib.DG_BUF_IMAGE), torch.empty(0, **u8))
+            arena.get(_lib.DG_BUF_BINNING), arena.get(_lib.DG_BUF_IMAGE),
+            arena.get(_lib.DG_BUF_BINNING2) if b2p.value else torch.empty(0, **u8))
 
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, scales, rotations, scale_modifier,
@@ -106,7 +120,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
         arena = _lib.TensorArena(dev)
         _lib.check(_lib.load().dg_rasterize_backward(
             C.byref(a), radii_c.data_ptr(), geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
-            int(R), int(B), gc.data_ptr(), _lib.ptr(gi), dmeans2D.data_ptr(), dcolors.data_ptr(),
+            _lib.ptr(sampleBuffer), int(R), int(B), gc.data_ptr(), _lib.ptr(gi), dmeans2D.data_ptr(), dcolors.data_ptr(),
             dopacity.data_ptr(), dmeans3D.data_ptr(), dcov3D.data_ptr(), ddc.data_ptr(), _lib.ptr(dsh),
             dscales.data_ptr(), drot.data_ptr(), depth.data_ptr(), arena.fn, None, _lib.stream_of(dev)))
         del keep

@@ -26,7 +26,8 @@ typedef void* dg_stream_t; /* hipStream_t */
 
 /* which: DG_BUF_* below.  Must return a device pointer aligned to >= 256 bytes, or NULL. */
 typedef void* (*dg_alloc_fn)(void* user, int which, uint64_t nbytes);
-enum { DG_BUF_GEOM = 0, DG_BUF_BINNING = 1, DG_BUF_IMAGE = 2, DG_BUF_BACKWARD = 3, DG_BUF_TEMP = 4 };
+enum { DG_BUF_GEOM = 0, DG_BUF_BINNING = 1, DG_BUF_IMAGE = 2, DG_BUF_BACKWARD = 3, DG_BUF_TEMP = 4,
+       DG_BUF_BINNING2 = 5 };
 
 /* The scalar + tensor arguments of _C.rasterize_gaussians (rasterize_points.h:18-40). */
 typedef struct {
@@ -35,6 +36,9 @@ typedef struct {
     int M;              /* sh.size(1) (0 when sh is absent) */
     int W, H;           /* image_width, image_height */
     int prefiltered, antialiasing, debug;
+    int prefix_per_tile;        /* depth-prefix binning: phase-1 capacity = this x tiles (0 -> 256);
+                                   < 0 bins every instance in one phase.  Must match between forward and
+                                   backward of one view. */
     float scale_modifier, tanfovx, tanfovy;
     const float* bg;            /* [3] */
     const float* means3D;       /* [P,3] */
@@ -53,12 +57,15 @@ typedef struct {
 /* Replaces RasterizeGaussiansCUDA (rasterize_points.cu:55-154) / _C.rasterize_gaussians.
  * Outputs out_color [3,H,W], out_invdepth [1,H,W], radii [P] (int32).
  * *num_rendered = the reference's num_rendered (sum of tile-rect areas);
- * *num_instances = precise-culled (tile, Gaussian) instances (returned where the reference returns
- * num_buckets; both are opaque tokens handed back to the backward).
- * Allocates DG_BUF_GEOM, DG_BUF_IMAGE, DG_BUF_BINNING through `alloc`; the caller keeps the three
- * pointers (in the order requested) and passes them to dg_rasterize_backward.  One host sync. */
+ * *num_instances = (tile, Gaussian) instances binned (returned where the reference returns num_buckets;
+ * both are opaque tokens handed back to the backward).  Binning is depth-prefix (DESIGN.md "Binning"):
+ * phase 1 bins the first instances of the global depth order (a prefix of every tile's list), phase 2 bins
+ * the rest only for tiles that phase 1 left unfinished -- same images and gradients, far fewer instances.
+ * Allocates DG_BUF_GEOM, DG_BUF_IMAGE, DG_BUF_BINNING and, only when phase 2 runs, DG_BUF_BINNING2 through
+ * `alloc`; the caller keeps the four pointers (*binning2 = NULL when absent; the reference's sampleBuffer
+ * slot carries it) and passes them to dg_rasterize_backward.  One host sync (two when phase 2 runs). */
 int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_invdepth, int* radii,
-                         dg_alloc_fn alloc, void* user, void** geom, void** binning, void** image,
+                         dg_alloc_fn alloc, void* user, void** geom, void** binning, void** image, void** binning2,
                          int64_t* num_rendered, int64_t* num_instances, dg_stream_t stream);
 
 /* Replaces RasterizeGaussiansBackwardCUDA (rasterize_points.cu:157-252).  Every output is fully
@@ -66,7 +73,7 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
  * dcov3D [P,6], ddc [P,1,3], dsh [P,M,3] (may be NULL when M == 0), dscales [P,3], drot [P,4],
  * depth [P,1].  dL_dout_invdepth may be NULL (treated as zeros).  Allocates DG_BUF_BACKWARD. */
 int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void* geom, const void* binning,
-                          const void* image, int64_t num_rendered, int64_t num_instances,
+                          const void* image, const void* binning2, int64_t num_rendered, int64_t num_instances,
                           const float* dL_dout_color, const float* dL_dout_invdepth, float* dmeans2D,
                           float* dcolors, float* dopacity, float* dmeans3D, float* dcov3D, float* ddc,
                           float* dsh, float* dscales, float* drot, float* depth, dg_alloc_fn alloc, void* user,
@@ -105,10 +112,12 @@ uint64_t dg_geom_bytes(int P);
 uint64_t dg_image_bytes(int W, int H);
 uint64_t dg_binning_bytes(int64_t K, int W, int H);
 
-/* Introspection of the private forward state, for parity tests (device output pointers, async on stream):
- * the sorted (tile, Gaussian) instance list, per-Gaussian geometry, per-pixel/per-tile image state. */
-int dg_debug_sorted_instances(const void* binning, int64_t K, int W, int H, uint32_t* tiles_out,
-                              uint32_t* gauss_out, dg_stream_t stream);
+/* Introspection of the private forward state, for parity tests (device output pointers):
+ * the sorted (tile, Gaussian) instance lists -- phase 1 (*e1 entries) then phase 2 (num_instances - *e1),
+ * each sorted by tile -- per-Gaussian geometry, per-pixel/per-tile image state (ranges = phase 1). */
+int dg_debug_sorted_instances(const dg_raster_args* a, const void* geom, const void* binning, const void* binning2,
+                              int64_t num_instances, uint32_t* tiles_out, uint32_t* gauss_out, int64_t* e1,
+                              dg_stream_t stream);
 int dg_debug_geometry(const void* geom, int P, float* means2D, float* conic_opacity, float* rgb_invdepth,
                       uint32_t* tile_count, dg_stream_t stream);
 int dg_debug_image_state(const void* image, int W, int H, float* final_T, uint32_t* n_contrib,

@@ -45,15 +45,31 @@ def hip_forward(s, bg, dev, deg=3, antialiasing=False, colors=None, cov3D=None, 
     return out
 
 
-def hip_sorted_instances(out, W, H, dev):
+def hip_sorted_instances(out, W, H, dev, P):
+    """(tiles, gaussians, E1): the phase-1 instances (E1, sorted by tile) followed by the phase-2 ones."""
+    import ctypes as C
     from dogs_amd import _lib
+    from dogs_amd.diff_gaussian_rasterization import _C
     K = out[1]
+    a = _lib.DgRasterArgs()
+    a.P, a.W, a.H, a.prefix_per_tile = int(P), int(W), int(H), int(_C.PREFIX_PER_TILE)
     tiles = torch.empty(max(K, 1), dtype=torch.int32, device=dev)
     gs = torch.empty(max(K, 1), dtype=torch.int32, device=dev)
-    _lib.check(_lib.load().dg_debug_sorted_instances(out[6].data_ptr(), K, W, H, tiles.data_ptr(), gs.data_ptr(),
-                                                     _lib.stream_of(dev)))
+    e1 = C.c_int64(0)
+    _lib.check(_lib.load().dg_debug_sorted_instances(C.byref(a), out[5].data_ptr(), out[6].data_ptr(),
+                                                     _lib.ptr(out[8]), K, tiles.data_ptr(), gs.data_ptr(),
+                                                     C.byref(e1), _lib.stream_of(dev)))
     torch.cuda.synchronize()
-    return tiles[:K].cpu().numpy().view(np.uint32), gs[:K].cpu().numpy().view(np.uint32)
+    return tiles[:K].cpu().numpy().view(np.uint32), gs[:K].cpu().numpy().view(np.uint32), int(e1.value)
+
+
+def per_tile_lists(tiles, gids, e1):
+    """tile -> list of Gaussians: the tile's phase-1 entries followed by its phase-2 entries."""
+    lists = {}
+    for part in (slice(0, e1), slice(e1, len(tiles))):
+        for t, g in zip(tiles[part].tolist(), gids[part].tolist()):
+            lists.setdefault(t, []).append(g)
+    return lists
 
 
 def hip_geometry(out, P, dev):
