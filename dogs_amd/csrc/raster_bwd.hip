@@ -79,56 +79,6 @@ __device__ __forceinline__ float wave_reduce10(const float (&p)[10], int lane, i
 // dL/dconic = -o/2 (SGxx, SGxy, SGyy) and dL/dopacity = SG once per Gaussian (the map is linear, so
 // summing the moments over instances first is exact).
 // Record slots: 0 SGx, 1 SGy, 2 SGxx, 3 SGxy, 4 SGyy, 5 SG, 6-8 sum w g_rgb, 9 sum w g_invdepth.
-struct PairState {
-    v2f T, S, g0, g1, g2, gd, ntb;  // transmittance, ar.g, dL/dpixel, dL/dinvdepth, -T_final (bg.g)
-    int last0, last1;
-    float py;
-};
-struct SplatAcc {
-    v2f SG, SGx, SGy, SGxx, SGxy, SGyy, C0, C1, C2, CD;
-};
-
-template <bool HAS_INVD, bool HAS_BG>
-__device__ __forceinline__ bool bwd_pair(PairState& P, SplatAcc& acc, const v2f pxv, int sidx, float sx, float sy,
-                                         float eA, float eB, float eC, float so, float sr, float sg, float sbl, float si) {
-    const v2f dx = bc2(sx) - pxv;
-    const float dy = sy - P.py;
-    const v2f p2 = splat_power2(eA, eB, eC, dx, dy);
-    const v2f G = {__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y)};
-    v2f al = bc2(so) * G;
-    al.x = fminf(0.99f, al.x);
-    al.y = fminf(0.99f, al.y);
-    const bool ok0 = (sidx < P.last0) && !(p2.x > 0.0f) && !(al.x < (1.0f / 255.0f));
-    const bool ok1 = (sidx < P.last1) && !(p2.y > 0.0f) && !(al.y < (1.0f / 255.0f));
-    al.x = ok0 ? al.x : 0.0f;
-    al.y = ok1 ? al.y : 0.0f;
-    const v2f wgt = al * P.T;
-    const v2f oma = bc2(1.0f) - al;
-    const v2f inv = {__builtin_amdgcn_rcpf(oma.x), __builtin_amdgcn_rcpf(oma.y)};
-    v2f cg = fma2(bc2(sbl), P.g2, fma2(bc2(sg), P.g1, bc2(sr) * P.g0));
-    if (HAS_INVD) cg = fma2(bc2(si), P.gd, cg);
-    P.S = fma2(wgt, cg, P.S);
-    v2f dLda = fma2(cg, P.T, inv * P.S);
-    if (HAS_BG) dLda = fma2(P.ntb, inv, dLda);
-    dLda.x = ok0 ? dLda.x : 0.0f;
-    dLda.y = ok1 ? dLda.y : 0.0f;
-    P.T = P.T * oma;
-    acc.C0 = fma2(wgt, P.g0, acc.C0);
-    acc.C1 = fma2(wgt, P.g1, acc.C1);
-    acc.C2 = fma2(wgt, P.g2, acc.C2);
-    if (HAS_INVD) acc.CD = fma2(wgt, P.gd, acc.CD);
-    const v2f t = G * dLda;
-    const v2f vdy = bc2(dy);
-    acc.SG = acc.SG + t;
-    acc.SGx = fma2(t, dx, acc.SGx);
-    acc.SGy = fma2(t, vdy, acc.SGy);
-    const v2f tdx = t * dx;
-    acc.SGxx = fma2(tdx, dx, acc.SGxx);
-    acc.SGxy = fma2(tdx, vdy, acc.SGxy);
-    acc.SGyy = fma2(t * vdy, vdy, acc.SGyy);
-    return ok0 || ok1;
-}
-
 template <bool HAS_INVD, bool HAS_BG>
 __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile, int lane, float4* sb) {
     // the tile's list = its phase-1 prefix followed by its phase-2 remainder (depth-prefix binning)
@@ -145,47 +95,41 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
     const int tx0 = tx * GS_TILE_X, ty0 = ty * GS_TILE_Y;
     const size_t HW = (size_t)a.W * a.H;
     const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
-    const v2f pxv = {(float)(tx0 + (lane & 7)), (float)(tx0 + (lane & 7) + 8)};
-    PairState PA, PB;
+    // pixel k of the lane: column c0 + 8 (k >> 1), row rA + 8 (k & 1) -- the forward's layout
+    const int c0 = tx0 + (lane & 7), rA = ty0 + (lane >> 3);
+    const v4f pxv = {(float)c0, (float)c0, (float)(c0 + 8), (float)(c0 + 8)};
+    const v2f pyv = {(float)rA, (float)(rA + 8)};
+    v4f T = bc4(1.0f), S, g0, g1, g2, gd, ntb;
+    int last[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int px = c0 + (k >> 1) * 8, py = rA + (k & 1) * 8;
+        if (px < a.W && py < a.H) {
+            const size_t pid = (size_t)py * a.W + px;
+            last[k] = (int)a.n_contrib[pid];
+            g0[k] = a.dL_dpix[pid]; g1[k] = a.dL_dpix[HW + pid]; g2[k] = a.dL_dpix[2 * HW + pid];
+            gd[k] = HAS_INVD ? a.dL_dinvd[pid] : 0.0f;
+            // ar starts at -(final pixel colour) (backward.cu:538-546); S = ar . g
+            float s0 = -(fmaf(a.img_color[2 * HW + pid], g2[k], fmaf(a.img_color[HW + pid], g1[k], a.img_color[pid] * g0[k])));
+            if (HAS_INVD) s0 = fmaf(-a.img_invd[pid], gd[k], s0);
+            S[k] = s0;
+            ntb[k] = HAS_BG ? -a.final_T[pid] * fmaf(bg2, g2[k], fmaf(bg1, g1[k], bg0 * g0[k])) : 0.0f;
+        } else {
+            last[k] = 0;
+            S[k] = g0[k] = g1[k] = g2[k] = gd[k] = ntb[k] = 0.0f;
+        }
+    }
+    // per quadrant (qx = k >> 1, qy = k & 1 -> quadrant 2 qy + qx): max last contributor over the wave
     int qlast[4];
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-        PairState& P = h ? PB : PA;
-        const int py = ty0 + h * 8 + (lane >> 3);
-        P.py = (float)py;
-        P.T = bc2(1.0f);
-        float S[2], g0[2], g1[2], g2[2], gd[2], ntb[2];
-        int last[2];
+    for (int k = 0; k < 4; k++) {
+        int m = last[k];
 #pragma unroll
-        for (int c = 0; c < 2; c++) {
-            const int px = tx0 + (lane & 7) + 8 * c;
-            if (px < a.W && py < a.H) {
-                const size_t pid = (size_t)py * a.W + px;
-                last[c] = (int)a.n_contrib[pid];
-                g0[c] = a.dL_dpix[pid]; g1[c] = a.dL_dpix[HW + pid]; g2[c] = a.dL_dpix[2 * HW + pid];
-                gd[c] = HAS_INVD ? a.dL_dinvd[pid] : 0.0f;
-                // ar starts at -(final pixel colour) (backward.cu:538-546); S = ar . g
-                float s0 = -(fmaf(a.img_color[2 * HW + pid], g2[c], fmaf(a.img_color[HW + pid], g1[c], a.img_color[pid] * g0[c])));
-                if (HAS_INVD) s0 = fmaf(-a.img_invd[pid], gd[c], s0);
-                S[c] = s0;
-                const float Tf = a.final_T[pid];
-                ntb[c] = HAS_BG ? -Tf * fmaf(bg2, g2[c], fmaf(bg1, g1[c], bg0 * g0[c])) : 0.0f;
-            } else {
-                last[c] = 0;
-                S[c] = g0[c] = g1[c] = g2[c] = gd[c] = ntb[c] = 0.0f;
-            }
-            int m = last[c];
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const int y = __shfl_xor(m, o);
-                m = y > m ? y : m;
-            }
-            qlast[2 * h + c] = __builtin_amdgcn_readfirstlane(m);
+        for (int o = 32; o > 0; o >>= 1) {
+            const int y = __shfl_xor(m, o);
+            m = y > m ? y : m;
         }
-        P.S = (v2f){S[0], S[1]};
-        P.g0 = (v2f){g0[0], g0[1]}; P.g1 = (v2f){g1[0], g1[1]}; P.g2 = (v2f){g2[0], g2[1]};
-        P.gd = (v2f){gd[0], gd[1]}; P.ntb = (v2f){ntb[0], ntb[1]};
-        P.last0 = last[0]; P.last1 = last[1];
+        qlast[2 * (k & 1) + (k >> 1)] = __builtin_amdgcn_readfirstlane(m);
     }
     for (int base = 0; base < n; base += 64) {
         const int j = base + lane;
@@ -208,33 +152,79 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
             qm = quad_mask({c4.x, c4.y, c4.z, c4.w}, m.x, m.y, thr, tx0, ty0);
 #pragma unroll
             for (int k = 0; k < 4; k++) qm &= (j < qlast[k]) ? 0xfu : ~(1u << k);
-            const SplatExp k = splat_exp_coeffs(c4.x, c4.y, c4.z);
-            sb[lane * 3 + 0] = make_float4(m.x, m.y, k.A, k.B);
-            sb[lane * 3 + 1] = make_float4(k.C, c4.w, q.x, q.y);
-            sb[lane * 3 + 2] = make_float4(q.z, q.w, __uint_as_float(ee), __uint_as_float(qm));
+            const SplatExp kq = splat_exp_coeffs(c4.x, c4.y, c4.z);
+            sb[lane * 3 + 0] = make_float4(m.x, m.y, kq.A, kq.B);
+            sb[lane * 3 + 1] = make_float4(kq.C, c4.w, q.x, q.y);
+            sb[lane * 3 + 2] = make_float4(q.z, q.w, __uint_as_float(ee), 0.0f);
         }
         __builtin_amdgcn_wave_barrier();
         uint64_t smask = __ballot(qm != 0u);
         while (smask) {
-            const int jj = __ffsll((unsigned long long)smask) - 1;
+            const int jj = (int)__builtin_ctzll(smask);
             smask &= smask - 1;
-            const float4 A = sb[jj * 3 + 0], B = sb[jj * 3 + 1], Cc = sb[jj * 3 + 2];
+            const float4 Sa = sb[jj * 3 + 0], Sb = sb[jj * 3 + 1], Sc = sb[jj * 3 + 2];
             const int sidx = base + jj;
-            SplatAcc acc;
-            acc.SG = acc.SGx = acc.SGy = acc.SGxx = acc.SGxy = acc.SGyy = bc2(0.0f);
-            acc.C0 = acc.C1 = acc.C2 = acc.CD = bc2(0.0f);
-            bool act = false;
-            // both pairs unconditionally (see k_render_fwd): the independent chains interleave
-            act |= bwd_pair<HAS_INVD, HAS_BG>(PA, acc, pxv, sidx, A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, Cc.x, Cc.y);
-            act |= bwd_pair<HAS_INVD, HAS_BG>(PB, acc, pxv, sidx, A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, Cc.x, Cc.y);
-            if (__any(act)) {
-                const float p[10] = {acc.SGx.x + acc.SGx.y, acc.SGy.x + acc.SGy.y, acc.SGxx.x + acc.SGxx.y,
-                                     acc.SGxy.x + acc.SGxy.y, acc.SGyy.x + acc.SGyy.y, acc.SG.x + acc.SG.y,
-                                     acc.C0.x + acc.C0.y, acc.C1.x + acc.C1.y, acc.C2.x + acc.C2.y,
-                                     HAS_INVD ? acc.CD.x + acc.CD.y : 0.0f};
+            const float sx = Sa.x, sy = Sa.y, so = Sb.y, sr = Sb.z, sg = Sb.w, sbl = Sc.x, si = Sc.y;
+            // exponent, identical to the forward's splat_power4
+            const v2f dy = bc2(sy) - pyv;
+            const v4f dx = bc4(sx) - pxv;
+            const v2f bdy = bc2(Sa.w) * dy, cdy2 = (bc2(Sb.x) * dy) * dy;
+            const v4f p2 = fma4(dx, fma4(bc4(Sa.z), dx, cat4(bdy, bdy)), cat4(cdy2, cdy2));
+            const v4f G = {__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y), __builtin_amdgcn_exp2f(p2.z),
+                           __builtin_amdgcn_exp2f(p2.w)};
+            v4f al = bc4(so) * G;
+            bool ok[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float ak = fminf(0.99f, al[k]);
+                ok[k] = (sidx < last[k]) && !(p2[k] > 0.0f) && !(ak < (1.0f / 255.0f));
+                al[k] = ok[k] ? ak : 0.0f;
+            }
+            const v4f wgt = al * T;
+            const v4f oma = bc4(1.0f) - al;
+            const v4f inv = {__builtin_amdgcn_rcpf(oma.x), __builtin_amdgcn_rcpf(oma.y), __builtin_amdgcn_rcpf(oma.z),
+                             __builtin_amdgcn_rcpf(oma.w)};
+            v4f cg = fma4(bc4(sbl), g2, fma4(bc4(sg), g1, bc4(sr) * g0));
+            if (HAS_INVD) cg = fma4(bc4(si), gd, cg);
+            S = fma4(wgt, cg, S);
+            v4f dLda = fma4(cg, T, inv * S);
+            if (HAS_BG) dLda = fma4(ntb, inv, dLda);
+#pragma unroll
+            for (int k = 0; k < 4; k++) dLda[k] = ok[k] ? dLda[k] : 0.0f;
+            T = T * oma;
+            // per-splat moments over the lane's 4 pixels; lo + hi of a v4 = the two row sums {row A, row B}
+            const v4f t4 = G * dLda;
+            const v4f tdx = t4 * dx;
+            const v4f tdx2 = tdx * dx;
+            const v2f rt = (v2f){t4.x, t4.y} + (v2f){t4.z, t4.w};
+            const v2f rtx = (v2f){tdx.x, tdx.y} + (v2f){tdx.z, tdx.w};
+            const v2f rtxx = (v2f){tdx2.x, tdx2.y} + (v2f){tdx2.z, tdx2.w};
+            const v4f w0 = wgt * g0, w1 = wgt * g1, w2 = wgt * g2;
+            const v2f rc0 = (v2f){w0.x, w0.y} + (v2f){w0.z, w0.w};
+            const v2f rc1 = (v2f){w1.x, w1.y} + (v2f){w1.z, w1.w};
+            const v2f rc2 = (v2f){w2.x, w2.y} + (v2f){w2.z, w2.w};
+            const v2f u = rt * dy;  // {tA dyA, tB dyB}
+            float p[10];
+            p[0] = rtx.x + rtx.y;                            // SGx
+            p[1] = u.x + u.y;                                // SGy
+            p[2] = rtxx.x + rtxx.y;                          // SGxx
+            p[3] = fmaf(rtx.x, dy.x, rtx.y * dy.y);          // SGxy
+            p[4] = fmaf(u.x, dy.x, u.y * dy.y);              // SGyy
+            p[5] = rt.x + rt.y;                              // SG
+            p[6] = rc0.x + rc0.y;
+            p[7] = rc1.x + rc1.y;
+            p[8] = rc2.x + rc2.y;
+            if (HAS_INVD) {
+                const v4f wd = wgt * gd;
+                const v2f rcd = (v2f){wd.x, wd.y} + (v2f){wd.z, wd.w};
+                p[9] = rcd.x + rcd.y;
+            } else {
+                p[9] = 0.0f;
+            }
+            if (__any(ok[0] || ok[1] || ok[2] || ok[3])) {
                 int slot;
                 const float tot = wave_reduce10(p, lane, slot);
-                const uint32_t e = __builtin_amdgcn_readfirstlane(__float_as_uint(Cc.z));
+                const uint32_t e = __builtin_amdgcn_readfirstlane(__float_as_uint(Sc.z));
                 if (slot >= 0) a.rec[(size_t)e * 12 + slot] = tot;
                 if (lane == 0) a.flag[e] = 1;
             }
