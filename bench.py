@@ -108,7 +108,18 @@ class View:
                                                  c.tanfovy, self.gc, s.dc, s.sh, self.gi, 3, c.camera_center,
                                                  out[5], out[0], out[6], out[7], out[1], out[8], False, False)
         self.last = (out[0], out[1])
+        self.last_out = out
         return out, g
+
+    def binned_instances(self):
+        import ctypes as C
+        import dogs_amd._lib as L
+        v = C.c_int64(-1)
+        if not hasattr(L.load(), "dg_binned_instances"):
+            return -1
+        L.check(L.load().dg_binned_instances(self.last_out[5].data_ptr(), int(self.s.means3D.shape[0]), C.byref(v),
+                                             L.stream_of(self.dev)))
+        return int(v.value)
 
 
 class TrainStep:
@@ -207,9 +218,17 @@ def main():
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
+    # one rank per GPU over RCCL ("nccl" on ROCm).  DOGS_DIST_BACKEND=gloo + DOGS_BENCH_SHARE_DEVICE=1 rehearse the
+    # multi-rank control flow with several ranks on one GPU (RCCL needs distinct devices).
+    backend = os.environ.get("DOGS_DIST_BACKEND", "nccl")
+    if os.environ.get("DOGS_BENCH_SHARE_DEVICE") == "1":
+        local = local % max(torch.cuda.device_count(), 1)
     if ws > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local if ws > 1 else 0)
     import dogs_amd._lib as L
     L.load()
@@ -254,7 +273,8 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    num_rendered, K_binned = view.last
+    num_rendered = view.last[0]
+    K_binned = view.binned_instances()
     K = view.reference_instances()
 
     # ---- one profiled step: per-phase hipEvent durations on the stream the kernels run on

@@ -36,7 +36,7 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_mark_visible", "
            "dg_adam_update", "dg_fused_ssim_forward", "dg_fused_ssim_backward", "dg_dist_cuda2",
            "dg_geom_bytes", "dg_image_bytes", "dg_binning_bytes", "dg_debug_sorted_instances",
            "dg_debug_geometry", "dg_debug_image_state", "dg_sort_pairs_u32", "dg_exclusive_scan_u32",
-           "dg_profile_enable", "dg_profile_collect",
+           "dg_profile_enable", "dg_profile_collect", "dg_binned_instances",
            "dg_last_error", "dg_version")
 
 _lib = None
@@ -49,7 +49,7 @@ def load(path: str | None = None):
     with _lock:
         if _lib is not None and path is None:
             return _lib
-        p = path or LIB_PATH
+        p = path or os.environ.get("DOGS_HIP_LIB") or LIB_PATH  # env override: A/B of two builds on one box
         if not os.path.exists(p):
             raise ImportError(f"libdogs_hip.so not found at {p}: build it with "
                               "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
@@ -84,6 +84,9 @@ def load(path: str | None = None):
         L.dg_debug_sorted_instances.restype = C.c_int
         L.dg_debug_sorted_instances.argtypes = [C.POINTER(DgRasterArgs), vp, vp, vp, C.c_int64, vp, vp,
                                                 i64p, vp]
+        if hasattr(L, "dg_binned_instances"):  # introspection only; absent in older builds used for A/B runs
+            L.dg_binned_instances.restype = C.c_int
+            L.dg_binned_instances.argtypes = [vp, C.c_int, i64p, vp]
         L.dg_debug_geometry.restype = C.c_int
         L.dg_debug_geometry.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp]
         L.dg_debug_image_state.restype = C.c_int

@@ -612,6 +612,16 @@ int dg_debug_sorted_instances(const dg_raster_args* a, const void* geom, const v
     return 0;
 }
 
+int dg_binned_instances(const void* geom, int P, int64_t* binned, dg_stream_t stream) {
+    hipStream_t s = (hipStream_t)stream;
+    Geom g = carve_geom((void*)geom, P);
+    uint32_t hc[16];
+    HIP_OK(hipMemcpyAsync(hc, g.counters, sizeof(hc), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    *binned = (int64_t)hc[gs::CNT_E1] + (int64_t)hc[gs::CNT_K2];
+    return 0;
+}
+
 int dg_debug_geometry(const void* geom, int P, float* means2D, float* conic_opacity, float* rgb_invdepth,
                       uint32_t* tile_count, dg_stream_t stream) {
     if (P <= 0) return 0;

@@ -457,16 +457,17 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
 
     // ---- computeCov2DCUDA (backward.cu:149-326)
     const f3 mean = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+    // both sources land in registers (a pointer to either would put the local copy on the stack)
     float cbuf[6];
-    const float* cov3D;
     if (a.cov3D_precomp) {
-        cov3D = a.cov3D_precomp + 6 * idx;
+#pragma unroll
+        for (int i = 0; i < 6; i++) cbuf[i] = a.cov3D_precomp[6 * idx + i];
     } else {
         const f3 s = {a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
         const f4 q = {a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]};
         cov3d_fwd(s, a.scale_mod, q, cbuf);
-        cov3D = cbuf;
     }
+    const float* cov3D = cbuf;
     const float h_x = a.focal_x, h_y = a.focal_y;
     Cov2DState st;
     const f3 cv = cov2d_fwd(mean, h_x, h_y, a.tanfovx, a.tanfovy, cov3D, a.view, &st);

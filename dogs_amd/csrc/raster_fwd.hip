@@ -152,16 +152,17 @@ __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, co
     const f4 ph = tp4x4(po, a.proj);
     const float pw = 1.0f / (ph.w + 0.0000001f);
     const float ppx = ph.x * pw, ppy = ph.y * pw;
+    // both sources land in registers (a pointer to either would put the local copy on the stack)
     float cbuf[6];
-    const float* cov3D;
     if (a.cov3D_precomp) {
-        cov3D = a.cov3D_precomp + 6 * idx;
+#pragma unroll
+        for (int i = 0; i < 6; i++) cbuf[i] = a.cov3D_precomp[6 * idx + i];
     } else {
         const f3 s = {a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
         const f4 q = {a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]};
         cov3d_fwd(s, a.scale_mod, q, cbuf);
-        cov3D = cbuf;
     }
+    const float* cov3D = cbuf;
     f3 cov = cov2d_fwd(po, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy, cov3D, a.view, nullptr);
     const float h_var = 0.3f;
     const float det_cov = fmaf(cov.x, cov.z, -(cov.y * cov.y));
@@ -548,10 +549,12 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a) {
             v4f al = bc4(Sb.y) * (v4f){__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y),
                                        __builtin_amdgcn_exp2f(p2.z), __builtin_amdgcn_exp2f(p2.w)};
             // forward.cu:451-475: skip power > 0 and alpha < 1/255, stop once T would fall below 1e-4
+            bool acc[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const float ak = fminf(0.99f, al[k]);
-                al[k] = (p2[k] > 0.0f || ak < thr[k]) ? 0.0f : ak;
+                acc[k] = !(p2[k] > 0.0f || ak < thr[k]);
+                al[k] = acc[k] ? ak : 0.0f;
             }
             const v4f test_T = T * (bc4(1.0f) - al);
             v4f Tn;
@@ -561,7 +564,7 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a) {
                 thr[k] = term ? 2.0f : thr[k];
                 al[k] = term ? 0.0f : al[k];
                 Tn[k] = term ? T[k] : test_T[k];
-                last[k] = al[k] > 0.0f ? c : last[k];
+                last[k] = (acc[k] && !term) ? c : last[k];  // contributed: accepted and not the stopping splat
             }
             const v4f wt = al * T;
             C0 = fma4(bc4(Sb.z), wt, C0);
@@ -641,16 +644,17 @@ __global__ void __launch_bounds__(256) k_filter(PreArgs a) {
     }
     const f4 ph = tp4x4(po, a.proj);
     const float pw = 1.0f / (ph.w + 0.0000001f);
+    // both sources land in registers (a pointer to either would put the local copy on the stack)
     float cbuf[6];
-    const float* cov3D;
     if (a.cov3D_precomp) {
-        cov3D = a.cov3D_precomp + 6 * idx;
+#pragma unroll
+        for (int i = 0; i < 6; i++) cbuf[i] = a.cov3D_precomp[6 * idx + i];
     } else {
         const f3 s = {a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
         const f4 q = {a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]};
         cov3d_fwd(s, a.scale_mod, q, cbuf);
-        cov3D = cbuf;
     }
+    const float* cov3D = cbuf;
     const f3 cov = cov2d_fwd(po, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy, cov3D, a.view, nullptr);
     const float det = fmaf(cov.x, cov.z, -(cov.y * cov.y));
     if (det == 0.0f) return;

@@ -118,6 +118,8 @@ uint64_t dg_binning_bytes(int64_t K, int W, int H);
 int dg_debug_sorted_instances(const dg_raster_args* a, const void* geom, const void* binning, const void* binning2,
                               int64_t num_instances, uint32_t* tiles_out, uint32_t* gauss_out, int64_t* e1,
                               dg_stream_t stream);
+/* Instances actually binned by the last forward on this geometry block: phase 1 + phase 2 (synchronises). */
+int dg_binned_instances(const void* geom, int P, int64_t* binned, dg_stream_t stream);
 int dg_debug_geometry(const void* geom, int P, float* means2D, float* conic_opacity, float* rgb_invdepth,
                       uint32_t* tile_count, dg_stream_t stream);
 int dg_debug_image_state(const void* image, int W, int H, float* final_T, uint32_t* n_contrib,
