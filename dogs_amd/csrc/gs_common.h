@@ -109,10 +109,16 @@ __device__ __forceinline__ void get_rect(float px, float py, int r, int gx, int 
     a = f2i((((py + (float)r) + (float)GS_TILE_Y) - 1.0f) / (float)GS_TILE_Y); a = a > 0 ? a : 0; y1 = a < gy ? a : gy;
 }
 
-// max_contrib_power_rect_gaussian_float<PATCH,PATCH> (rasterizer_impl.cu:52-100); PATCH = rect size - 1
+// max_contrib_power_rect_gaussian_float<PATCH,PATCH> (rasterizer_impl.cu:52-100); PATCH = rect size - 1.
+// rcx/rcz = 1 / (PATCH^2 * conic.{x,z}) depend on the Gaussian only: callers that test many rects of one
+// Gaussian compute them once (mcp_recips) -- the same correctly rounded values, so the same result bits.
 template <int PATCH = 15>
-__device__ __forceinline__ float max_contrib_power(f4 co, float mx, float my, float rminx, float rminy, float rmaxx,
-                                                   float rmaxy) {
+__device__ __forceinline__ float2 mcp_recips(f4 co) {
+    return make_float2(1.0f / ((float)(PATCH * PATCH) * co.x), 1.0f / ((float)(PATCH * PATCH) * co.z));
+}
+template <int PATCH = 15>
+__device__ __forceinline__ float max_contrib_power_rc(f4 co, float mx, float my, float rminx, float rminy, float rmaxx,
+                                                      float rmaxy, float rcx, float rcz) {
     const float x_min_diff = rminx - mx;
     const float x_left = x_min_diff > 0.0f ? 1.0f : 0.0f;
     const float not_in_x = x_left + (mx > rmaxx ? 1.0f : 0.0f);
@@ -126,8 +132,6 @@ __device__ __forceinline__ float max_contrib_power(f4 co, float mx, float my, fl
         const float dx = copysignf((float)PATCH, x_min_diff);
         const float dy = copysignf((float)PATCH, y_min_diff);
         const float diffx = mx - px, diffy = my - py;
-        const float rcx = 1.0f / ((float)(PATCH * PATCH) * co.x);
-        const float rcz = 1.0f / ((float)(PATCH * PATCH) * co.z);
         float ax = fmaf(dx * co.y, diffy, (dx * co.x) * diffx) * rcx;
         float ay = fmaf(dy * co.z, diffy, (dy * co.y) * diffx) * rcz;
         ax = (ax != ax) ? 0.0f : fminf(fmaxf(ax, 0.0f), 1.0f);
@@ -138,6 +142,12 @@ __device__ __forceinline__ float max_contrib_power(f4 co, float mx, float my, fl
         power = fmaf(co.y * ddx, ddy, 0.5f * fmaf(co.z * ddy, ddy, (co.x * ddx) * ddx));
     }
     return power;
+}
+template <int PATCH = 15>
+__device__ __forceinline__ float max_contrib_power(f4 co, float mx, float my, float rminx, float rminy, float rmaxx,
+                                                   float rmaxy) {
+    const float2 rc = mcp_recips<PATCH>(co);
+    return max_contrib_power_rc<PATCH>(co, mx, my, rminx, rminy, rmaxx, rmaxy, rc.x, rc.y);
 }
 
 // forward.cu:119-153 (quaternion not normalised in-kernel, :128)
@@ -188,10 +198,11 @@ constexpr float LOG2E = 1.4426950408889634f;
 constexpr float QUAD_MARGIN = 0.01f;
 __device__ __forceinline__ uint32_t quad_mask(f4 co, float mx, float my, float thr, int tx0, int ty0) {
     uint32_t m = 0;
+    const float2 rc = mcp_recips<7>(co);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const float x0 = (float)(tx0 + (q & 1) * 8), y0 = (float)(ty0 + (q >> 1) * 8);
-        const float p = max_contrib_power<7>(co, mx, my, x0, y0, x0 + 7.0f, y0 + 7.0f);
+        const float p = max_contrib_power_rc<7>(co, mx, my, x0, y0, x0 + 7.0f, y0 + 7.0f, rc.x, rc.y);
         m |= (p <= thr + QUAD_MARGIN) ? (1u << q) : 0u;
     }
     return m;

@@ -86,9 +86,10 @@ __device__ __forceinline__ f3 sh_to_rgb(f3 pos, const float* campos, int deg, co
 // per step for every lane; `kept` is the precise per-tile cull (max_contrib_power <= log(255 o)).
 struct CandLDS {
     uint32_t pre[64];     // exclusive prefix of rect areas
-    int x0[64], y0[64], w[64], area[64];
-    float mx[64], my[64], thr[64];
-    float4 co[64];
+    int w[64], area[64];
+    float4 co[64];        // conic.xyz, opacity
+    float4 geo[64];       // mean2D.xy, log threshold, 1/rect width
+    float4 rc[64];        // max_contrib_power reciprocals (mcp_recips), rect x0, y0 (int bits)
 };
 
 template <typename Visit>
@@ -103,8 +104,12 @@ __device__ __forceinline__ void wave_candidates(CandLDS& L, int lane, int x0, in
     }
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     L.pre[lane] = incl - area;
-    L.x0[lane] = x0; L.y0[lane] = y0; L.w[lane] = x1 - x0; L.area[lane] = (int)area;
-    L.mx[lane] = mx; L.my[lane] = my; L.thr[lane] = thr; L.co[lane] = co;
+    L.w[lane] = x1 - x0; L.area[lane] = (int)area;
+    L.co[lane] = co;
+    // per-Gaussian constants of the per-tile test, hoisted out of the candidate loop (same values, same bits)
+    const float2 rcp = area ? mcp_recips<15>(f4{co.x, co.y, co.z, co.w}) : make_float2(0.f, 0.f);
+    L.geo[lane] = make_float4(mx, my, thr, area ? __builtin_amdgcn_rcpf((float)(x1 - x0)) : 0.f);
+    L.rc[lane] = make_float4(rcp.x, rcp.y, __int_as_float(x0), __int_as_float(y0));
     __builtin_amdgcn_wave_barrier();
     for (uint32_t i0 = 0; i0 < total; i0 += 64) {
         const uint32_t item = i0 + (uint32_t)lane;
@@ -119,16 +124,21 @@ __device__ __forceinline__ void wave_candidates(CandLDS& L, int lane, int x0, in
             for (int step = 32; step > 0; step >>= 1)
                 if (L.pre[lo + step] <= item) lo += step;
             owner = lo;
-            const uint32_t r = item - L.pre[owner];
-            const uint32_t ww = (uint32_t)L.w[owner];
-            const uint32_t qy = r / ww;
-            tx = L.x0[owner] + (int)(r - qy * ww);
-            ty = L.y0[owner] + (int)qy;
+            const int r = (int)(item - L.pre[owner]);
+            const int ww = L.w[owner];
+            const float4 g = L.geo[owner];
+            const float4 rc = L.rc[owner];
+            // r / ww from a float reciprocal, corrected to the exact quotient (r < 2^24, error < 1)
+            int qy = (int)((float)r * g.w);
+            int rx = r - qy * ww;
+            if (rx < 0) { qy--; rx += ww; } else if (rx >= ww) { qy++; rx -= ww; }
+            tx = __float_as_int(rc.z) + rx;
+            ty = __float_as_int(rc.w) + qy;
             const float4 c = L.co[owner];
-            const float p = max_contrib_power(f4{c.x, c.y, c.z, c.w}, L.mx[owner], L.my[owner], (float)(tx * GS_TILE_X),
-                                              (float)(ty * GS_TILE_Y), (float)((tx + 1) * GS_TILE_X - 1),
-                                              (float)((ty + 1) * GS_TILE_Y - 1));
-            kept = p <= L.thr[owner];
+            const float p = max_contrib_power_rc<15>(f4{c.x, c.y, c.z, c.w}, g.x, g.y, (float)(tx * GS_TILE_X),
+                                                     (float)(ty * GS_TILE_Y), (float)((tx + 1) * GS_TILE_X - 1),
+                                                     (float)((ty + 1) * GS_TILE_Y - 1), rc.x, rc.y);
+            kept = p <= g.z;
         }
         visit(owner, tx, ty, kept, valid, item);
     }
@@ -211,20 +221,38 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     const int base = blockIdx.x * 256;
     const int idx = base + t;
     const int nloc = (a.P - base) < 256 ? (a.P - base) : 256;
+#ifdef DG_ABLATE_NO_SH
+    const bool stage = false;
+#else
     const bool stage = a.sh != nullptr && a.colors == nullptr && a.M > 0;
+#endif
     if (stage) {
         const int slab = nloc * a.M * 3;
         const float* src = a.sh + (size_t)base * a.M * 3;
         const int n4 = slab >> 2;
         const float4* src4 = reinterpret_cast<const float4*>(src);
         float4* dst4 = reinterpret_cast<float4*>(s_sh);
-        for (int i = t; i < n4; i += 256) dst4[i] = src4[i];
+        // LDS-DMA (global_load_lds_dwordx4): each wave-instruction lands 1 KiB at a wave-uniform LDS base +
+        // lane*16, with no VGPR round trip -- all of the block's loads are in flight at once (a register-staged
+        // loop waits out one HBM latency per 16 B per lane).  Drained by the __syncthreads below.
+        const int lane = t & 63;
+        for (int i0 = t & ~63; i0 < n4; i0 += 256) {
+            if (i0 + lane < n4)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src4 + i0 + lane),
+                                                 (__attribute__((address_space(3))) void*)(dst4 + i0), 16, 0, 0);
+        }
         for (int i = (n4 << 2) + t; i < slab; i += 256) s_sh[i] = src[i];
     }
     __syncthreads();
     uint32_t area = 0;
     RectOut ro = {0, 0, 0, 0, 0.f, 0.f, 0.f, make_float4(0.f, 0.f, 0.f, 0.f)};
+#ifdef DG_ABLATE_NO_SH  // timing experiment only: colour from dc alone (degree 0, no SH read)
+    PreArgs a0 = a;
+    a0.sh = nullptr;
+    if (idx < a.P) area = preprocess_one(a0, idx, nullptr, ro);
+#else
     if (idx < a.P) area = preprocess_one(a, idx, stage ? s_sh + t * a.M * 3 : nullptr, ro);
+#endif
     // precise per-tile cull counts (duplicateWithKeys, rasterizer_impl.cu:149-179), wave-cooperative.
     // The candidate tables reuse the SH staging LDS (dead after preprocess_one).
     __syncthreads();
@@ -234,6 +262,10 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
         const int lane = t & 63, w = t >> 6;
         s_cnt[w][lane] = 0;
         CandLDS& L = s_cand[w];
+#ifdef DG_ABLATE_NO_WALK  // timing experiment only: counts = rect areas
+        s_cnt[w][lane] = area;
+        if (false)
+#endif
         wave_candidates(L, lane, ro.x0, ro.y0, ro.x1, ro.y1, ro.mx, ro.my, ro.co, ro.thr,
                         [&](int owner, int, int, bool kept, bool valid, uint32_t item) {
                             const uint64_t km = __ballot(kept);
