@@ -191,6 +191,19 @@ __device__ __forceinline__ f3 cov2d_fwd(f3 mean, float fx, float fy, float tfx, 
     return {cov.m[0][0], cov.m[0][1], cov.m[1][1]};
 }
 
+// Copy n4 float4s global -> LDS with LDS-DMA (global_load_lds_dwordx4) by a 256-thread block: each
+// wave-instruction lands 1 KiB at a wave-uniform LDS base + lane*16 with no VGPR round trip, so all of the
+// block's loads are in flight at once (a register-staged loop waits out one HBM latency per 16 B per lane).
+// The caller's next __syncthreads drains them (vmcnt(0) before the barrier).
+__device__ __forceinline__ void stage_lds_dma(float4* dst4, const float4* src4, int n4, int t) {
+    const int lane = t & 63;
+    for (int i0 = t & ~63; i0 < n4; i0 += 256) {
+        if (i0 + lane < n4)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src4 + i0 + lane),
+                                             (__attribute__((address_space(3))) void*)(dst4 + i0), 16, 0, 0);
+    }
+}
+
 constexpr float LOG2E = 1.4426950408889634f;
 // Quadrant refinement of the precise tile cull: an 8x8 quadrant whose best point is below the opacity
 // threshold holds no pixel with alpha >= 1/255.  The margin (in log units) keeps the skip conservative

@@ -396,8 +396,12 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
         const int n4 = slab >> 2;  // base*M*3*4 bytes is a multiple of 16 (256*M*12)
         const float4* src4 = reinterpret_cast<const float4*>(src);
         float4* dst4 = reinterpret_cast<float4*>(s_sh);
-        for (int i = t; i < n4; i += 256) dst4[i] = src4[i];
-        for (int i = (n4 << 2) + t; i < slab; i += 256) s_sh[i] = src[i];
+        if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0u) {
+            stage_lds_dma(dst4, src4, n4, t);
+            for (int i = (n4 << 2) + t; i < slab; i += 256) s_sh[i] = src[i];
+        } else {  // a caller's unaligned view: plain copy
+            for (int i = t; i < slab; i += 256) s_sh[i] = src[i];
+        }
     }
     __syncthreads();
     if (idx < a.P) gauss_bwd_one(a, idx, s_sh + t * M * 3);
@@ -407,15 +411,34 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
         const int n4 = slab >> 2;
         float4* dst4 = reinterpret_cast<float4*>(dst);
         const float4* src4 = reinterpret_cast<const float4*>(s_sh);
-        for (int i = t; i < n4; i += 256) dst4[i] = src4[i];
-        for (int i = (n4 << 2) + t; i < slab; i += 256) dst[i] = s_sh[i];
+        if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0u) {
+            for (int i = t; i < n4; i += 256) dst4[i] = src4[i];
+            for (int i = (n4 << 2) + t; i < slab; i += 256) dst[i] = s_sh[i];
+        } else {
+            for (int i = t; i < slab; i += 256) dst[i] = s_sh[i];
+        }
     }
 }
 
 // One Gaussian; `lsh` is its [M][3] SH row in LDS, overwritten in place with dL/dsh.
 __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, float* lsh) {
     const int M = a.M;
-    if (!(a.radii[idx] > 0)) {
+    // every per-Gaussian input is loaded up front: one HBM round trip instead of four dependent ones
+    // (radii -> records/splat -> means -> scales/rotations); culled Gaussians read bytes they ignore
+    const int rad = a.radii[idx];
+    const float4 r0 = a.sums[3 * (size_t)idx + 0], r1 = a.sums[3 * (size_t)idx + 1], r2 = a.sums[3 * (size_t)idx + 2];
+    const float4 sp0 = a.sp[2 * (size_t)idx], sp1 = a.sp[2 * (size_t)idx + 1];
+    const f3 mean = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+    f3 scl = {0.f, 0.f, 0.f};
+    f4 rot = {0.f, 0.f, 0.f, 0.f};
+    if (a.scales) {
+        scl = {a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
+        rot = {a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]};
+    }
+    const float opac = a.antialiasing ? a.opacities[idx] : 0.f;
+    f3 dcv = {0.f, 0.f, 0.f};
+    if (a.sh) dcv = {a.dc[3 * idx], a.dc[3 * idx + 1], a.dc[3 * idx + 2]};
+    if (!(rad > 0)) {
         for (int v = 0; v < 3; v++) {
             a.dmeans2D[3 * idx + v] = 0.f; a.dcolors[3 * idx + v] = 0.f; a.dmeans3D[3 * idx + v] = 0.f;
             a.ddc[3 * idx + v] = 0.f; a.dscales[3 * idx + v] = 0.f;
@@ -430,14 +453,13 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
     // ---- records -> dL/d(mean2D, conic, opacity, color, invdepth): summed by the wave (see below)
     float acc[10];
     {
-        const float4 s0 = a.sums[3 * (size_t)idx + 0], s1 = a.sums[3 * (size_t)idx + 1], s2 = a.sums[3 * (size_t)idx + 2];
+        const float4 s0 = r0, s1 = r1, s2 = r2;
         acc[0] = s0.x; acc[1] = s0.y; acc[2] = s0.z; acc[3] = s0.w; acc[4] = s1.x;
         acc[5] = s1.y; acc[6] = s1.z; acc[7] = s1.w; acc[8] = s2.x; acc[9] = s2.y;
     }
     // moments -> dL/dmean2D, dL/dconic (see render_bwd_tile); o = the AA-scaled opacity of the forward
     {
-        const float4 s0 = a.sp[2 * (size_t)idx], s1 = a.sp[2 * (size_t)idx + 1];
-        const float4 c4 = make_float4(s0.z, s0.w, s1.x, s1.y);
+        const float4 c4 = make_float4(sp0.z, sp0.w, sp1.x, sp1.y);
         const float SGx = acc[0], SGy = acc[1], SGxx = acc[2], SGxy = acc[3], SGyy = acc[4];
         const float so = c4.w;
         acc[0] = -(0.5f * a.W) * (so * fmaf(c4.x, SGx, c4.y * SGy));
@@ -456,16 +478,13 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
     const float dL_dinvd = acc[9];
 
     // ---- computeCov2DCUDA (backward.cu:149-326)
-    const f3 mean = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
     // both sources land in registers (a pointer to either would put the local copy on the stack)
     float cbuf[6];
     if (a.cov3D_precomp) {
 #pragma unroll
         for (int i = 0; i < 6; i++) cbuf[i] = a.cov3D_precomp[6 * idx + i];
     } else {
-        const f3 s = {a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
-        const f4 q = {a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]};
-        cov3d_fwd(s, a.scale_mod, q, cbuf);
+        cov3d_fwd(scl, a.scale_mod, rot, cbuf);
     }
     const float* cov3D = cbuf;
     const float h_x = a.focal_x, h_y = a.focal_y;
@@ -480,7 +499,7 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
         c_xx += h_var; c_yy += h_var;
         const float det_plus = fmaf(c_xx, c_yy, -(c_xy * c_xy));
         const float hs = sqrtf(fmaxf(0.000025f, det_cov / det_plus));
-        const float dhs = dLo * a.opacities[idx];
+        const float dhs = dLo * opac;
         dLo = dLo * hs;
         d_inside_root = (det_cov / det_plus) <= 0.000025f ? 0.f : dhs / (2 * hs);
     } else {
@@ -551,7 +570,7 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
     // ---- computeColorFromSH backward (backward.cu:23-144); clamped flags recomputed from the forward rgb
     if (a.sh) {
         const float* sh = lsh;
-        const float* d0p = a.dc + 3 * idx;
+        const float d0p[3] = {dcv.x, dcv.y, dcv.z};
         const int deg = a.D;
         const f3 dir_orig = {mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]};
         const float len = sqrtf(fmaf(dir_orig.z, dir_orig.z, fmaf(dir_orig.y, dir_orig.y, dir_orig.x * dir_orig.x)));
@@ -640,10 +659,9 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
 
     // ---- computeCov3D backward (backward.cu:330-393)
     if (a.scales) {
-        const float* q = a.rotations + 4 * idx;
-        const float r = q[0], x = q[1], y = q[2], z = q[3];
+        const float r = rot.x, x = rot.y, y = rot.z, z = rot.w;
         const m3 R = quat_to_R(r, x, y, z);
-        const f3 s = {a.scale_mod * a.scales[3 * idx], a.scale_mod * a.scales[3 * idx + 1], a.scale_mod * a.scales[3 * idx + 2]};
+        const f3 s = {a.scale_mod * scl.x, a.scale_mod * scl.y, a.scale_mod * scl.z};
         m3 S = m3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
         S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
         const m3 Mm = m3_mul(S, R);

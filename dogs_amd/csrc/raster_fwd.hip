@@ -37,12 +37,12 @@ __device__ __forceinline__ void get_rect_s(float px, float py, int r, int gx, in
 }
 
 // computeColorFromSH (forward.cu:24-76); clamped flags are recomputed by the backward instead of stored
-__device__ __forceinline__ f3 sh_to_rgb(f3 pos, const float* campos, int deg, const float* d0, const float* sh,
+__device__ __forceinline__ f3 sh_to_rgb(f3 pos, const float* campos, int deg, f3 d0, const float* sh,
                                         bool* clamped) {
     f3 dir = {pos.x - campos[0], pos.y - campos[1], pos.z - campos[2]};
     const float len = sqrtf(fmaf(dir.z, dir.z, fmaf(dir.y, dir.y, dir.x * dir.x)));
     dir.x = dir.x / len; dir.y = dir.y / len; dir.z = dir.z / len;
-    float r0 = SH_C0 * d0[0], r1 = SH_C0 * d0[1], r2 = SH_C0 * d0[2];
+    float r0 = SH_C0 * d0.x, r1 = SH_C0 * d0.y, r2 = SH_C0 * d0.z;
 #define ACC(b, k)                                    \
     {                                                \
         const float bb = (b);                        \
@@ -153,6 +153,17 @@ __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, co
     a.depthkey[idx] = 0xffffffffu;
     a.rcnt[idx] = 0u;
     const f3 po = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+    // every per-Gaussian input is loaded before the first use, so one HBM round trip covers them all
+    // (issued after the frustum test they would cost a second, dependent, round trip per wave)
+    f3 s = {0.f, 0.f, 0.f};
+    f4 q = {0.f, 0.f, 0.f, 0.f};
+    if (!a.cov3D_precomp) {
+        s = {a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
+        q = {a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]};
+    }
+    const float opac = a.opacities[idx];
+    f3 dcv = {0.f, 0.f, 0.f};
+    if (!a.colors) dcv = {a.dc[3 * idx], a.dc[3 * idx + 1], a.dc[3 * idx + 2]};
     // in_frustum (auxiliary.h:150-175)
     const f3 pv = tp4x3(po, a.view);
     if (pv.z <= 0.2f) {
@@ -168,8 +179,6 @@ __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, co
 #pragma unroll
         for (int i = 0; i < 6; i++) cbuf[i] = a.cov3D_precomp[6 * idx + i];
     } else {
-        const f3 s = {a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
-        const f4 q = {a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]};
         cov3d_fwd(s, a.scale_mod, q, cbuf);
     }
     const float* cov3D = cbuf;
@@ -198,9 +207,9 @@ __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, co
     if (a.colors) {
         col = {a.colors[3 * idx], a.colors[3 * idx + 1], a.colors[3 * idx + 2]};
     } else {
-        col = sh_to_rgb(po, a.campos, a.sh ? a.D : 0, a.dc + 3 * idx, lsh, nullptr);
+        col = sh_to_rgb(po, a.campos, a.sh ? a.D : 0, dcv, lsh, nullptr);
     }
-    const float4 co = make_float4(conic.x, conic.y, conic.z, a.opacities[idx] * h_scale);
+    const float4 co = make_float4(conic.x, conic.y, conic.z, opac * h_scale);
     a.radii[idx] = ir;
     a.sp[2 * idx] = make_float4(px, py, co.x, co.y);
     a.sp[2 * idx + 1] = make_float4(co.z, co.w, __uint_as_float((uint32_t)x0 | ((uint32_t)x1 << 16)),
@@ -232,16 +241,12 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
         const int n4 = slab >> 2;
         const float4* src4 = reinterpret_cast<const float4*>(src);
         float4* dst4 = reinterpret_cast<float4*>(s_sh);
-        // LDS-DMA (global_load_lds_dwordx4): each wave-instruction lands 1 KiB at a wave-uniform LDS base +
-        // lane*16, with no VGPR round trip -- all of the block's loads are in flight at once (a register-staged
-        // loop waits out one HBM latency per 16 B per lane).  Drained by the __syncthreads below.
-        const int lane = t & 63;
-        for (int i0 = t & ~63; i0 < n4; i0 += 256) {
-            if (i0 + lane < n4)
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src4 + i0 + lane),
-                                                 (__attribute__((address_space(3))) void*)(dst4 + i0), 16, 0, 0);
+        if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0u) {
+            stage_lds_dma(dst4, src4, n4, t);
+            for (int i = (n4 << 2) + t; i < slab; i += 256) s_sh[i] = src[i];
+        } else {  // a caller's unaligned view: plain copy
+            for (int i = t; i < slab; i += 256) s_sh[i] = src[i];
         }
-        for (int i = (n4 << 2) + t; i < slab; i += 256) s_sh[i] = src[i];
     }
     __syncthreads();
     uint32_t area = 0;
