@@ -197,9 +197,10 @@ struct BwdScratch {
     float* rec;
     uint32_t* invd_flag;
     float4* sums;  // [P][3] per-Gaussian record sums
+    uint32_t* order;  // [T] replay order of the tiles
     size_t bytes;
 };
-BwdScratch carve_bwd(void* base, int64_t K, int P) {
+BwdScratch carve_bwd(void* base, int64_t K, int P, int T) {
     Carver c(base);
     BwdScratch s;
     const size_t n = (size_t)(K > 0 ? K : 1);
@@ -207,6 +208,7 @@ BwdScratch carve_bwd(void* base, int64_t K, int P) {
     s.rec = c.take<float>(12 * n);
     s.invd_flag = c.take<uint32_t>(4);
     s.sums = c.take<float4>(3 * (size_t)(P > 0 ? P : 1));
+    s.order = c.take<uint32_t>((size_t)(T > 0 ? T : 1));
     s.bytes = c.off;
     return s;
 }
@@ -474,10 +476,10 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
         eg2 = b2.eg;
     }
 
-    const size_t sbytes = carve_bwd(nullptr, K, P).bytes;
+    const size_t sbytes = carve_bwd(nullptr, K, P, T).bytes;
     void* sbase = alloc(user, DG_BUF_BACKWARD, sbytes);
     if (!sbase) return fail("backward scratch allocation failed%s%d");
-    BwdScratch sc = carve_bwd(sbase, K, P);
+    BwdScratch sc = carve_bwd(sbase, K, P, T);
     if (K > 0) {
         gs::RenderBwdArgs r;
         r.W = W; r.H = H; r.tiles_x = tx; r.num_tiles = T;
@@ -488,6 +490,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
         r.sp = g.sp; r.rgbi = g.rgbi; r.bg = a->bg;
         r.final_T = im.final_T; r.img_color = im.img_color; r.img_invd = im.img_invd; r.n_contrib = im.n_contrib;
         r.dL_dpix = dL_dout_color; r.dL_dinvd = dL_dout_invdepth; r.rec = sc.rec; r.flag = sc.flag;
+        r.order = sc.order;
         { PROF("render_bwd"); gs::launch_render_bwd(r, g.counters, s); }
         DBG_SYNC(a->debug, s);
     }

@@ -86,6 +86,7 @@ struct RenderBwdArgs {
     const float* dL_dinvd;   // may be null
     float* rec;              // [K][12] per-instance gradient record
     uint8_t* flag;           // [K] record written
+    uint32_t* order;         // [num_tiles] scratch: tiles in descending replay length (launch order)
 };
 
 struct GaussBwdArgs {
