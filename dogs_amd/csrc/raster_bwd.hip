@@ -245,46 +245,10 @@ __device__ __forceinline__ uint32_t replay_len(const RenderBwdArgs& a, int tile)
     return n < mc ? n : mc;
 }
 
-// Longest-first launch order for the replay.  Per-tile work varies by ~10x across the image and a 1080p
-// view has only ~1.6 tiles per resident wave slot, so in raster order the launch ends on a tail of long
-// centre tiles; descending order lets the short tiles fill in behind the long ones.  One block: counting
-// sort on min(len / 4, 255), order within a bucket unspecified (records do not depend on launch order).
-constexpr int ORDER_BUCKETS = 256;
+// Longest-first launch order for the replay (tile_order_sort); the key is the exact replay length.  Per tile,
+// not per 4-tile block: ordering whole blocks by their longest tile measured 6% slower.
 __global__ void __launch_bounds__(1024) k_tile_order(RenderBwdArgs a) {
-    __shared__ uint32_t s_hist[ORDER_BUCKETS];
-    __shared__ uint32_t s_wsum[ORDER_BUCKETS / 64];
-    const int t = threadIdx.x;
-    if (t < ORDER_BUCKETS) s_hist[t] = 0u;
-    __syncthreads();
-    for (int tile = t; tile < a.num_tiles; tile += blockDim.x) {
-        const uint32_t l = replay_len(a, tile) >> 2;
-        atomicAdd(&s_hist[ORDER_BUCKETS - 1 - (l < ORDER_BUCKETS - 1 ? l : ORDER_BUCKETS - 1)], 1u);
-    }
-    __syncthreads();
-    uint32_t v = 0, incl = 0;
-    if (t < ORDER_BUCKETS) {
-        v = s_hist[t];
-        incl = v;
-        const int lane = t & 63;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
-        if (lane == 63) s_wsum[t >> 6] = incl;
-    }
-    __syncthreads();
-    if (t < ORDER_BUCKETS) {
-        uint32_t off = 0;
-        for (int w = 0; w < (t >> 6); w++) off += s_wsum[w];
-        s_hist[t] = off + incl - v;
-    }
-    __syncthreads();
-    for (int tile = t; tile < a.num_tiles; tile += blockDim.x) {
-        const uint32_t l = replay_len(a, tile) >> 2;
-        const uint32_t pos = atomicAdd(&s_hist[ORDER_BUCKETS - 1 - (l < ORDER_BUCKETS - 1 ? l : ORDER_BUCKETS - 1)], 1u);
-        a.order[pos] = (uint32_t)tile;
-    }
+    tile_order_sort(a.num_tiles, a.order, [&](int tile) { return replay_len(a, tile); });
 }
 
 __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
