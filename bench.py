@@ -39,8 +39,9 @@ def phase_bytes(phase: str, N: int, K: int, HW: int) -> float:
     precise instance count (its full per-tile lists), whatever this build bins."""
     return {
         "preprocess": 284.0 * N,            # 236 B params read + 48 B geometry written
-        "depth_sort": 0.0,                  # implementation overhead (not algorithmic)
+        "prefix_cut": 8.0 * N,              # depth histogram: key + count per Gaussian
         "count_scan": 8.0 * N,
+        "tile_dsort": 0.0,                  # implementation overhead: per-tile depth order of the binned lists
         "emit": 36.0 * N + 12.0 * K,
         "tile_sort": 24.0 * K,
         "ranges": 8.0 * K,

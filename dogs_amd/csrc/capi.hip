@@ -88,12 +88,12 @@ inline int bits_for(uint32_t n) {  // bits needed for ids in [0, n)
 }
 
 struct Geom {
-    uint32_t* counters;  // [0] K total, [1] err, [2..3] u64 rect sum
+    uint32_t* counters;  // CNT_* (raster.h)
     float4* sp;  // 2 per Gaussian (raster.h)
     float4* rgbi;
-    uint32_t *k0, *v0, *k1, *v1, *cnt, *first_e, *off;
-    uint32_t *rcnt, *cnt2, *off2;  // records per Gaussian; phase-2 counts / offsets by rank - R1
-    void* sort_tmp;
+    uint32_t *dkey, *cnt, *first_e, *off;
+    uint32_t *rcnt, *cnt2, *off2;  // records per Gaussian; phase-2 counts / offsets (index order)
+    uint32_t* hist;                // [DH_BINS] depth histogram of the prefix cut
     void* scan_tmp;
     size_t bytes;
 };
@@ -104,17 +104,14 @@ Geom carve_geom(void* base, int P) {
     g.counters = c.take<uint32_t>(16);
     g.sp = c.take<float4>(2 * n);
     g.rgbi = c.take<float4>(n);
-    g.k0 = c.take<uint32_t>(n);
-    g.v0 = c.take<uint32_t>(n);
-    g.k1 = c.take<uint32_t>(n);
-    g.v1 = c.take<uint32_t>(n);
+    g.dkey = c.take<uint32_t>(n);
     g.cnt = c.take<uint32_t>(n);
     g.first_e = c.take<uint32_t>(n);
     g.off = c.take<uint32_t>(n);
     g.rcnt = c.take<uint32_t>(n);
     g.cnt2 = c.take<uint32_t>(n);
     g.off2 = c.take<uint32_t>(n);
-    g.sort_tmp = c.take<char>(gs::radix_sort_temp_bytes((uint32_t)n));
+    g.hist = c.take<uint32_t>(gs::DH_BINS);
     g.scan_tmp = c.take<char>(gs::scan_temp_bytes((uint32_t)n));
     g.bytes = c.off;
     return g;
@@ -128,6 +125,7 @@ struct Image {
     uint8_t* unfinished;    // [T]
     float4* resume;         // [HW] raw colour + live threshold of unfinished tiles' pixels
     uint32_t* sat;          // [(ty+1)*(tx+1)] summed-area table of `unfinished`
+    uint32_t* long_tiles;   // [T] queue of the long-list tile depth sort
     size_t bytes;
 };
 Image carve_image(void* base, int W, int H) {
@@ -145,12 +143,15 @@ Image carve_image(void* base, int W, int H) {
     im.unfinished = c.take<uint8_t>(T);
     im.resume = c.take<float4>(HW);
     im.sat = c.take<uint32_t>((size_t)(tiles_x_of(W) + 1) * (tiles_y_of(H) + 1));
+    im.long_tiles = c.take<uint32_t>(T);
     im.bytes = c.off;
     return im;
 }
 
 struct Binning {
     uint32_t *tk0, *se0, *tk1, *se1, *eg;
+    uint32_t* ik;  // instance depth keys (emission order)
+    uint32_t* dk;  // depth-key scratch of the long-list tile sort
     void* sort_tmp;
     size_t bytes;
 };
@@ -163,6 +164,8 @@ Binning carve_binning(void* base, int64_t K) {
     b.tk1 = c.take<uint32_t>(n);
     b.se1 = c.take<uint32_t>(n);
     b.eg = c.take<uint32_t>(n);
+    b.ik = c.take<uint32_t>(n);
+    b.dk = c.take<uint32_t>(n);
     b.sort_tmp = c.take<char>(gs::radix_sort_temp_bytes((uint32_t)n));
     b.bytes = c.off;
     return b;
@@ -301,7 +304,7 @@ int dg_exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_
                           void* user, dg_stream_t stream) {
     void* tmp = alloc(user, DG_BUF_TEMP, gs::scan_temp_bytes(n));
     if (!tmp) return fail("scan scratch allocation failed%s%d");
-    gs::exclusive_scan(in, nullptr, n, out, total, tmp, (hipStream_t)stream);
+    gs::exclusive_scan(in, n, out, total, tmp, (hipStream_t)stream);
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -338,36 +341,38 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     HIP_OK(hipMemsetAsync(g.counters, 0, 64, s));
     gs::PreArgs pre;
     fill_pre(pre, a);
-    pre.radii = radii; pre.sp = g.sp; pre.rgbi = g.rgbi; pre.depthkey = g.k0; pre.cnt = g.cnt; pre.rcnt = g.rcnt;
+    pre.radii = radii; pre.sp = g.sp; pre.rgbi = g.rgbi; pre.depthkey = g.dkey; pre.cnt = g.cnt; pre.rcnt = g.rcnt;
+    pre.hist = g.hist;
     pre.rect_sum = (unsigned long long*)(g.counters + gs::CNT_RECT_LO); pre.err = g.counters + gs::CNT_ERR;
     { PROF("preprocess"); gs::launch_preprocess(pre, s); }
     DBG_SYNC(a->debug, s);
 
-    // stable depth sort of (depth bits, index), then the emission offsets in depth order
-    const uint32_t* order = g.v0;
-    const uint32_t* skey = g.k0;
-    if (P > 0) {
-        int which;
-        { PROF("depth_sort"); which = gs::radix_sort_pairs(g.k0, g.v0, g.k1, g.v1, nullptr, (uint32_t)P, 0, 32, g.sort_tmp, s); }
-        order = which ? g.v1 : g.v0;
-        skey = which ? g.k1 : g.k0;
-        DBG_SYNC(a->debug, s);
-        { PROF("count_scan"); gs::exclusive_scan(g.cnt, order, (uint32_t)P, g.off, g.counters + gs::CNT_K, g.scan_tmp, s); }
-        DBG_SYNC(a->debug, s);
-    }
-
-    // ---- phase 1: the depth prefix [0, E1) with E1 <= C1 (the counts stay on the device)
+    // ---- depth-threshold prefix: histogram of instance counts over depth bins -> threshold (no depth sort)
     int64_t C1;
-    if (prefix_enabled(a)) {
-        C1 = phase1_cap(a, T, 0);
-    } else {  // everything in one phase: the capacity is K itself (one early sync)
-        uint32_t k = 0;
-        HIP_OK(hipMemcpyAsync(&k, g.counters + gs::CNT_K, 4, hipMemcpyDeviceToHost, s));
-        HIP_OK(hipStreamSynchronize(s));
-        C1 = k;
+    if (P == 0) HIP_OK(hipMemsetAsync(g.hist, 0, gs::DH_BINS * sizeof(uint32_t), s));  // no preprocess to zero it
+    {
+        PROF("prefix_cut");
+        gs::launch_depth_hist(P, g.dkey, g.cnt, g.hist, s);
+        if (prefix_enabled(a)) {
+            C1 = phase1_cap(a, T, 0);
+            gs::launch_depth_cut(g.hist, (uint32_t)(C1 < 0xffffffffll ? C1 : 0xffffffffll), g.counters, im.ranges,
+                                 (uint32_t)T, s);
+        } else {  // everything in one phase: the capacity is K itself (one early sync)
+            gs::launch_depth_cut(g.hist, 0xffffffffu, g.counters, im.ranges, (uint32_t)T, s);
+            uint32_t k = 0;
+            HIP_OK(hipMemcpyAsync(&k, g.counters + gs::CNT_K, 4, hipMemcpyDeviceToHost, s));
+            HIP_OK(hipStreamSynchronize(s));
+            C1 = k;
+        }
     }
-    gs::launch_prefix_cut(g.off, (uint32_t)P, (uint32_t)(C1 < 0xffffffffll ? C1 : 0xffffffffll), g.counters, im.ranges,
-                          (uint32_t)T, s);
+    DBG_SYNC(a->debug, s);
+    // emission offsets of the prefix Gaussians (index order)
+    if (P > 0) {
+        PROF("count_scan");
+        gs::exclusive_scan(g.cnt, (uint32_t)P, g.off, g.counters + gs::CNT_E1CHK, g.scan_tmp, s, nullptr, g.dkey,
+                           g.counters + gs::CNT_THR);
+    }
+    DBG_SYNC(a->debug, s);
     // the host's only wait is on this early copy (K, num_rendered, error flag, cut), and it happens after all of
     // phase 1 is queued, so the GPU never idles on it
     HostCounters& hcs = host_counters();
@@ -380,20 +385,29 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     *binning_out = bbase;
     Binning b = carve_binning(bbase, C1);
     const uint32_t* E1_dev = g.counters + gs::CNT_E1;
-    const uint32_t* s_e = b.se0;
-    const uint32_t* s_keys = b.tk0;
+    const int passes = (tile_bits + 7) / 8;
+    uint32_t* s_e = (passes & 1) ? b.se1 : b.se0;
     if (C1 > 0 && P > 0) {
-        { PROF("emit"); gs::launch_emit(P, order, skey, g.off, g.sp, tx, g.counters, g.first_e, g.rcnt, b.tk0, b.eg, s); }
+        { PROF("emit"); gs::launch_emit(P, g.dkey, g.cnt, g.off, g.sp, tx, g.counters, g.first_e, g.rcnt, b.tk0, b.eg, b.ik, s); }
         DBG_SYNC(a->debug, s);
         int which;
         { PROF("tile_sort"); which = gs::radix_sort_pairs(b.tk0, b.se0, b.tk1, b.se1, nullptr, (uint32_t)C1, 0,
                                                           tile_bits, b.sort_tmp, s, E1_dev); }
-        s_e = which ? b.se1 : b.se0;
-        s_keys = which ? b.tk1 : b.tk0;
+        (void)which;  // == passes & 1
+        DBG_SYNC(a->debug, s);
+        { PROF("ranges"); gs::launch_ranges((uint32_t)C1, E1_dev, (passes & 1) ? b.tk1 : b.tk0, im.ranges, (uint32_t)T, s); }
+        DBG_SYNC(a->debug, s);
+        {
+            PROF("tile_dsort");
+            gs::DSortArgs d;
+            d.num_tiles = T; d.ranges = im.ranges; d.s_e = s_e; d.s_tmp = (passes & 1) ? b.se0 : b.se1;
+            d.k_a = b.dk; d.k_b = (passes & 1) ? b.tk0 : b.tk1; d.ikey = b.ik; d.n_inst = (uint32_t)C1;
+            d.only = nullptr; d.gate = nullptr; d.long_list = im.long_tiles;
+            d.long_cnt = g.counters + gs::CNT_LONG;
+            gs::tile_depth_sort(d, s);
+        }
         DBG_SYNC(a->debug, s);
     }
-    { PROF("ranges"); gs::launch_ranges((uint32_t)C1, E1_dev, s_keys, im.ranges, (uint32_t)T, s); }
-    DBG_SYNC(a->debug, s);
 
     gs::RenderArgs r;
     memset(&r, 0, sizeof(r));
@@ -410,17 +424,18 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     HIP_OK(hipEventSynchronize(hcs.ev));
     const uint32_t* hc = hcs.buf;
     if (hc[gs::CNT_ERR]) return fail("a Gaussian was filtered although prefiltered is set%s%d");
+    if (a->debug && hc[gs::CNT_E1CHK] != hc[gs::CNT_E1]) return fail("prefix scan total %s%d differs from the cut", "", (int)hc[gs::CNT_E1CHK]);
     *num_rendered = (int64_t)((uint64_t)hc[gs::CNT_RECT_LO] | ((uint64_t)hc[gs::CNT_RECT_LO + 1] << 32));
-    const uint32_t K = hc[gs::CNT_K], R1 = hc[gs::CNT_R1];
+    const uint32_t K = hc[gs::CNT_K];
     // the backward sizes records for K (>= phase-1 + phase-2 instances) and re-carves phase 2 at K
     *num_instances = K;
-    if (!hc[gs::CNT_CUT] || (int)R1 >= P) {
+    if (!hc[gs::CNT_CUT]) {
         HIP_OK(hipGetLastError());
         return 0;
     }
 
-    // ---- phase 2: the remaining ranks, only for tiles phase 1 left unfinished.  Every kernel is gated on the
-    // device-side unfinished count, so nothing waits for phase 1 and the common case costs a few empty launches.
+    // ---- phase 2: the Gaussians past the threshold, only for tiles phase 1 left unfinished.  Every kernel is gated
+    // on the device-side unfinished count, so nothing waits for phase 1 and the common case costs a few empty launches.
     const size_t b2bytes = carve_binning(nullptr, K).bytes;
     void* b2base = alloc(user, DG_BUF_BINNING2, b2bytes);
     if (!b2base) return fail("phase-2 binning allocation failed%s%d");
@@ -431,14 +446,19 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     {
         PROF("phase2");
         gs::launch_unfinished_sat(g.counters, im.unfinished, tx, ty, im.sat, s);
-        gs::launch_count2(P, R1, g.counters, order, skey, g.sp, tx, ty, im.unfinished, im.sat, g.cnt2, s);
-        gs::exclusive_scan(g.cnt2, nullptr, (uint32_t)(P - (int)R1), g.off2, g.counters + gs::CNT_K2, g.scan_tmp, s,
-                           gate);
-        gs::launch_emit2(P, R1, g.counters, order, skey, g.sp, tx, ty, im.unfinished, im.sat, g.cnt2, g.off2,
-                         g.first_e, g.rcnt, b2.tk0, b2.eg, s);
+        gs::launch_count2(P, g.counters, g.dkey, g.sp, tx, ty, im.unfinished, im.sat, g.cnt2, s);
+        gs::exclusive_scan(g.cnt2, (uint32_t)P, g.off2, g.counters + gs::CNT_K2, g.scan_tmp, s, gate);
+        gs::launch_emit2(P, g.counters, g.dkey, g.sp, tx, ty, im.unfinished, im.sat, g.cnt2, g.off2, g.first_e, g.rcnt,
+                         b2.tk0, b2.eg, b2.ik, s);
         const int which = gs::radix_sort_pairs(b2.tk0, b2.se0, b2.tk1, b2.se1, nullptr, K, 0, tile_bits,
                                                b2.sort_tmp, s, K2_dev);
         gs::launch_ranges(K, K2_dev, which ? b2.tk1 : b2.tk0, im.ranges2, (uint32_t)T, s);
+        gs::DSortArgs d;
+        d.num_tiles = T; d.ranges = im.ranges2; d.s_e = which ? b2.se1 : b2.se0; d.s_tmp = which ? b2.se0 : b2.se1;
+        d.k_a = b2.dk; d.k_b = which ? b2.tk0 : b2.tk1; d.ikey = b2.ik; d.n_inst = (uint32_t)K;
+        d.only = im.unfinished; d.gate = gate; d.long_list = im.long_tiles;
+        d.long_cnt = g.counters + gs::CNT_LONG2;
+        gs::tile_depth_sort(d, s);
         gs::RenderArgs r2 = r;
         r2.phase = 2;
         r2.K = K;

@@ -24,6 +24,7 @@ struct PreArgs {
     float4* sp;         // splat record, 2 x float4 per Gaussian (see SP_* below)
     float4* rgbi;       // rgb, 1 / view z
     uint32_t* depthkey; // float bits of view z, 0xffffffff when no tile survives the precise cull
+    uint32_t* hist;     // [DH_BINS] depth histogram, zeroed here
     uint32_t* cnt;      // precise tile count
     uint32_t* rcnt;     // records per Gaussian, zeroed here (written by the emission kernels)
     unsigned long long* rect_sum;  // num_rendered of the reference (sum of rect areas)
@@ -32,16 +33,24 @@ struct PreArgs {
 
 // Counters block at the head of the geometry state (device, uint32 slots).
 enum {
-    CNT_K = 0,          // precise instance total (all depth ranks)
+    CNT_K = 0,          // precise instance total
     CNT_ERR = 1,        // prefiltered violation
     CNT_RECT_LO = 2,    // num_rendered (sum of rect areas), u64 in slots 2..3
-    CNT_R1 = 4,         // depth-rank cut: ranks [0, R1) are binned in phase 1
-    CNT_E1 = 5,         // instances of phase 1 (= emission offset of rank R1)
+    CNT_THR = 4,        // depth-key threshold: Gaussians with key < thr are binned in phase 1
+    CNT_E1 = 5,         // instances of phase 1
     CNT_UNFINISHED = 6, // tiles with live pixels after phase 1 (only counted when CNT_CUT)
     CNT_K2 = 7,         // phase-2 instances
     CNT_CUT = 8,        // E1 < K: the phase-1 lists are prefixes
     CNT_INVD = 9,       // backward: any(dL/dinvdepth != 0) (zeroed with the block by the forward)
+    CNT_E1CHK = 10,     // the prefix scan's total (equals CNT_E1; a consistency check)
+    CNT_LONG = 11,      // phase-1 tiles queued for the long-list depth sort
+    CNT_LONG2 = 12,     // phase-2 tiles queued for the long-list depth sort
 };
+
+// Depth histogram of the prefix cut: bins of 2^DH_SHIFT key ulps (1/64 of a binade) from the near plane up;
+// DH_BINS covers 16 binades (z in [0.2, 13107)), farther keys share the last bin.
+constexpr int DH_SHIFT = 17;
+constexpr int DH_BINS = 1024;
 
 // Depth-prefix binning (DESIGN.md "Binning"): phase 1 bins only the first E1 <= C1 instances of the global depth
 // order, which is a prefix of every tile's list; phase 2 bins the rest only for tiles phase 1 left unfinished.
@@ -106,24 +115,26 @@ struct GaussBwdArgs {
 };
 
 void launch_preprocess(const PreArgs& a, hipStream_t s);
-// also zeroes the phase-1 tile ranges (ranges[num_tiles])
-void launch_prefix_cut(const uint32_t* off, uint32_t P, uint32_t cap, uint32_t* counters, uint2* ranges,
-                       uint32_t num_tiles, hipStream_t s);
-// phase 1: ranks [0, counters[CNT_R1]) -> instances [0, E1); rcnt/first_e of those Gaussians
-void launch_emit(int P, const uint32_t* order, const uint32_t* skey, const uint32_t* off, const float4* sp,
-                 int tiles_x, const uint32_t* counters, uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey,
-                 uint32_t* eg, hipStream_t s);
-// phase 2 over ranks [R1, P): only (Gaussian, tile) instances whose tile is unfinished
-// all phase-2 kernels are gated on counters[CNT_UNFINISHED] (device): no-ops when phase 1 finished every tile
+// hist[DH_BINS] (zeroed by the preprocess) += precise counts by depth bin
+void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_t* hist, hipStream_t s);
+// counters[K, THR, E1, CUT] from the histogram (phase-1 capacity cap); resets the per-view counters and zeroes
+// the phase-1 tile ranges (ranges[num_tiles])
+void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, uint2* ranges, uint32_t num_tiles,
+                      hipStream_t s);
+// phase 1: Gaussians with key < counters[CNT_THR] -> instances [0, E1) at off[g]; rcnt/first_e of those Gaussians
+// ikey[e] = the instance's depth key (read by the per-tile depth sort)
+void launch_emit(int P, const uint32_t* dkey, const uint32_t* cnt, const uint32_t* off, const float4* sp, int tiles_x,
+                 const uint32_t* counters, uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey, uint32_t* eg,
+                 uint32_t* ikey, hipStream_t s);
+// phase 2 over the Gaussians with key >= thr: only (Gaussian, tile) instances whose tile is unfinished.
+// All phase-2 kernels are gated on counters[CNT_UNFINISHED] (device): no-ops when phase 1 finished every tile.
 void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, int tiles_x, int tiles_y,
                            uint32_t* sat, hipStream_t s);
-void launch_count2(int P, uint32_t R1, const uint32_t* counters, const uint32_t* order, const uint32_t* skey,
-                   const float4* sp, int tiles_x, int tiles_y, const uint8_t* unfinished, const uint32_t* sat,
-                   uint32_t* cnt2, hipStream_t s);
-void launch_emit2(int P, uint32_t R1, const uint32_t* counters, const uint32_t* order, const uint32_t* skey,
-                  const float4* sp, int tiles_x, int tiles_y, const uint8_t* unfinished, const uint32_t* sat,
-                  const uint32_t* cnt2, const uint32_t* off2, uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey,
-                  uint32_t* eg, hipStream_t s);
+void launch_count2(int P, const uint32_t* counters, const uint32_t* dkey, const float4* sp, int tiles_x, int tiles_y,
+                   const uint8_t* unfinished, const uint32_t* sat, uint32_t* cnt2, hipStream_t s);
+void launch_emit2(int P, const uint32_t* counters, const uint32_t* dkey, const float4* sp, int tiles_x, int tiles_y,
+                  const uint8_t* unfinished, const uint32_t* sat, const uint32_t* cnt2, const uint32_t* off2,
+                  uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey, uint32_t* eg, uint32_t* ikey, hipStream_t s);
 void launch_ranges(uint32_t Kcap, const uint32_t* n_dev, const uint32_t* keys, uint2* ranges, uint32_t num_tiles,
                    hipStream_t s);
 void launch_render_fwd(const RenderArgs& a, hipStream_t s);

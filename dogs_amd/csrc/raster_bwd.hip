@@ -251,7 +251,12 @@ __global__ void __launch_bounds__(1024) k_tile_order(RenderBwdArgs a) {
     tile_order_sort(a.num_tiles, a.order, [&](int tile) { return replay_len(a, tile); });
 }
 
-__global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
+#ifdef DG_BWD_WPE  // occupancy experiment: cap VGPRs so that DG_BWD_WPE waves fit per SIMD
+#define BWD_WPE_ATTR __attribute__((amdgpu_waves_per_eu(DG_BWD_WPE)))
+#else
+#define BWD_WPE_ATTR
+#endif
+__global__ void __launch_bounds__(256) BWD_WPE_ATTR k_render_bwd(RenderBwdArgs a) {
     __shared__ float4 s_b[4][64][3];
     const int lane = threadIdx.x & 63;
     const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);

@@ -230,6 +230,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     const int base = blockIdx.x * 256;
     const int idx = base + t;
     const int nloc = (a.P - base) < 256 ? (a.P - base) : 256;
+    for (int i = base + t; i < DH_BINS; i += gridDim.x * 256) a.hist[i] = 0u;  // for k_depth_hist
 #ifdef DG_ABLATE_NO_SH
     const bool stage = false;
 #else
@@ -301,84 +302,156 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     }
 }
 
-// Depth-prefix cut: the largest rank R1 whose instances [0, off[R1]) fit the phase-1 capacity `cap`.  Ranks
-// are in depth order and every tile's list is in depth order, so instances of ranks < R1 are a PREFIX of
-// every tile's list (DESIGN.md "Binning").  No cut when everything fits.
-__global__ void k_prefix_cut(const uint32_t* __restrict__ off, uint32_t P, uint32_t cap, uint32_t* __restrict__ counters,
-                             uint2* __restrict__ ranges, uint32_t num_tiles) {
-    for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) ranges[t] = make_uint2(0u, 0u);
-    if (threadIdx.x != 0) return;
-    const uint32_t K = counters[CNT_K];
-    uint32_t R1 = P, E1 = K, cut = 0;
-    if (K > cap && P > 0) {
-        uint32_t lo = 0, hi = P - 1;  // invariant: off[lo] <= cap (off[0] == 0)
-        while (lo < hi) {
-            const uint32_t mid = lo + (hi - lo + 1) / 2;
-            if (off[mid] <= cap) lo = mid; else hi = mid - 1;
-        }
-        R1 = lo;
-        E1 = off[lo];
-        cut = 1;
-    }
-    counters[CNT_R1] = R1;
-    counters[CNT_E1] = E1;
-    counters[CNT_CUT] = cut;
-    counters[CNT_UNFINISHED] = 0;
-    counters[CNT_K2] = 0;
+// ---------------------------------------------------------------------------------------------------
+// Depth-threshold prefix (DESIGN.md "Binning").  Phase 1 bins the Gaussians whose depth key is below a
+// threshold `thr`; because every tile's list is in (depth bits, index) order, those instances are a PREFIX of
+// every tile's list, whatever the threshold.  thr is picked from a histogram of instance counts over coarse
+// depth bins so that the prefix fits the phase-1 capacity; no global depth sort is needed -- each tile's
+// prefix list is depth-sorted on its own (k_tile_dsort).
+// ---------------------------------------------------------------------------------------------------
+constexpr int DH_THREADS = 256;
+constexpr int DH_ITEMS = 16;                        // Gaussians per thread per block
+constexpr uint32_t DH_BASE = 0x3E4CCCCDu >> DH_SHIFT;  // bin of the near plane z = 0.2 (every visible key is above)
+
+__device__ __forceinline__ uint32_t depth_bin(uint32_t key) {
+    const uint32_t b = (key >> DH_SHIFT) - DH_BASE;
+    return b < (uint32_t)DH_BINS ? b : (uint32_t)(DH_BINS - 1);  // far keys share the last bin
 }
 
-constexpr int EMIT_RANKS = 16;
+// hist[bin] += cnt[g] over visible Gaussians: a private LDS histogram per block, flushed with one atomic per
+// non-empty bin (blocks cover DH_THREADS * DH_ITEMS Gaussians: ~245 blocks at 1e6).
+__global__ void __launch_bounds__(DH_THREADS) k_depth_hist(int P, const uint32_t* __restrict__ dkey,
+                                                          const uint32_t* __restrict__ cnt,
+                                                          uint32_t* __restrict__ hist) {
+    __shared__ uint32_t s_h[DH_BINS];
+    for (int i = threadIdx.x; i < DH_BINS; i += DH_THREADS) s_h[i] = 0u;
+    __syncthreads();
+    const int base = blockIdx.x * DH_THREADS * DH_ITEMS;
+    uint32_t key[DH_ITEMS], c[DH_ITEMS];
+#pragma unroll
+    for (int k = 0; k < DH_ITEMS; k++) {  // every load in flight before the first use
+        const int g = base + k * DH_THREADS + (int)threadIdx.x;
+        key[k] = g < P ? dkey[g] : 0xffffffffu;
+        c[k] = g < P ? cnt[g] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < DH_ITEMS; k++)
+        if (key[k] != 0xffffffffu && c[k]) atomicAdd(&s_h[depth_bin(key[k])], c[k]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < DH_BINS; i += DH_THREADS)
+        if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
+}
 
-// Phase-1 emission in depth order: instance e = off[p] + j for the j-th kept tile of Gaussian order[p], p < R1.
-// A wave owns 64 consecutive depth ranks, so its instances form one contiguous run starting at off[p0]; the
-// cooperative candidate walk writes them in (p, ty, tx) order with consecutive lanes -> consecutive e.
-// Ranks past the cut (and the culled tail, sorted key 0xffffffff) are skipped; the rest gather ONE 32-B splat
-// record each.  rcnt[g] = instances emitted for g (the record count of the backward).
-__global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict__ order,
-                                              const uint32_t* __restrict__ skey, const uint32_t* __restrict__ off,
+// One block: K = total instances, and the largest bin prefix [0, b] whose instances fit `cap`; thr = the first
+// key of bin b + 1 (S = {key < thr}).  No cut (thr = all visible) when K <= cap.  Also resets the per-view
+// counters and the phase-1 tile ranges.
+__global__ void __launch_bounds__(1024) k_depth_cut(const uint32_t* __restrict__ hist, uint32_t cap,
+                                                    uint32_t* __restrict__ counters, uint2* __restrict__ ranges,
+                                                    uint32_t num_tiles) {
+    __shared__ uint32_t s_w[16];
+    __shared__ int s_best;
+    constexpr int PER = DH_BINS / 1024;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (uint32_t i = t; i < num_tiles; i += 1024) ranges[i] = make_uint2(0u, 0u);
+    if (t == 0) s_best = -1;
+    uint32_t v[PER], loc = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) { v[k] = hist[t * PER + k]; loc += v[k]; }
+    uint32_t x = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint32_t off = 0, K = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) { if (k < w) off += s_w[k]; K += s_w[k]; }
+    // inclusive cumulative count at each of this thread's bins; C(b) is non-decreasing in b
+    uint32_t c = off + x - loc;
+    int best = -1;
+    uint32_t cbest = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        c += v[k];
+        if (c <= cap) { best = t * PER + k; cbest = c; }
+    }
+    if (best >= 0) atomicMax(&s_best, best);
+    __syncthreads();
+    const bool cut = K > cap;
+    if (t == 0 && s_best < 0) {  // not even bin 0 fits: phase 1 bins nothing, phase 2 everything
+        counters[CNT_K] = K;
+        counters[CNT_THR] = cut ? (DH_BASE << DH_SHIFT) : 0xffffffffu;
+        counters[CNT_E1] = cut ? 0u : K;
+        counters[CNT_CUT] = cut ? 1u : 0u;
+        counters[CNT_UNFINISHED] = 0; counters[CNT_K2] = 0; counters[CNT_LONG] = 0; counters[CNT_LONG2] = 0;
+    }
+    if (best >= 0 && best == s_best) {  // exactly one thread holds the best bin
+        counters[CNT_K] = K;
+        counters[CNT_THR] = cut ? ((DH_BASE + (uint32_t)best + 1u) << DH_SHIFT) : 0xffffffffu;
+        counters[CNT_E1] = cut ? cbest : K;
+        counters[CNT_CUT] = cut ? 1u : 0u;
+        counters[CNT_UNFINISHED] = 0; counters[CNT_K2] = 0; counters[CNT_LONG] = 0; counters[CNT_LONG2] = 0;
+    }
+}
+
+#ifndef DG_EMIT_RANKS
+#define DG_EMIT_RANKS 64
+#endif
+constexpr int EMIT_RANKS = DG_EMIT_RANKS;
+
+// Phase-1 emission in index order: instance e = off[g] + j for the j-th kept tile of a prefix Gaussian g
+// (key < thr; off = exclusive scan of cnt over the prefix set).  A wave owns EMIT_RANKS consecutive Gaussians,
+// so its instances form one contiguous run starting at off[g0]; the cooperative candidate walk writes them in
+// (g, ty, tx) order with consecutive lanes -> consecutive e.  rcnt[g] = instances emitted for g (the record
+// count of the backward), first_e[g] = off[g].
+__global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict__ dkey,
+                                              const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
                                               const float4* __restrict__ sp, int tiles_x,
                                               const uint32_t* __restrict__ counters,
                                               uint32_t* __restrict__ first_e, uint32_t* __restrict__ rcnt,
-                                              uint32_t* __restrict__ tilekey, uint32_t* __restrict__ eg) {
+                                              uint32_t* __restrict__ tilekey, uint32_t* __restrict__ eg,
+                                              uint32_t* __restrict__ ikey) {
     __shared__ CandLDS s_cand[4];
-    __shared__ uint32_t s_g[4][64];
+    __shared__ uint32_t s_key[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    // EMIT_RANKS ranks per wave: the depth prefix holds the nearest, largest Gaussians (~100 candidate tiles
-    // each), so 64 ranks per wave would leave ~one long serial wave per SIMD
-    const int p0 = (blockIdx.x * 4 + w) * EMIT_RANKS;
-    const int R1 = (int)counters[CNT_R1];
-    if (p0 >= R1 || p0 >= P) return;      // whole wave
-    if (skey[p0] == 0xffffffffu) return;  // whole wave in the culled tail
-    const int p = p0 + lane;
+    const int g0 = (blockIdx.x * 4 + w) * EMIT_RANKS;
+    if (g0 >= P) return;  // whole wave
+    const uint32_t thr = counters[CNT_THR];
+    const int g = g0 + lane;
     int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
-    float mx = 0.f, my = 0.f, thr = 0.f;
+    float mx = 0.f, my = 0.f, lthr = 0.f;
     float4 c4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    uint32_t g = 0xffffffffu;
-    if (lane < EMIT_RANKS && p < R1 && skey[p] != 0xffffffffu) {
-        g = order[p];
-        if (g < (uint32_t)P) {
-            const uint32_t e0 = off[p];
-            first_e[g] = e0;
-            rcnt[g] = ((p + 1 < P) ? off[p + 1] : counters[CNT_K]) - e0;
+    bool member = false;
+    if (lane < EMIT_RANKS && g < P) {
+        const uint32_t key = dkey[g];
+        s_key[w][lane] = key;
+        member = key < thr && key != 0xffffffffu;
+        if (member) {
+            const uint32_t c = cnt[g];
+            first_e[g] = off[g];
+            rcnt[g] = c;
             const float4 s0 = sp[2 * g], s1 = sp[2 * g + 1];
             c4 = make_float4(s0.z, s0.w, s1.x, s1.y);
             mx = s0.x; my = s0.y;
             sp_rect(s1, x0, y0, x1, y1);
-            thr = gs_logf(c4.w / (1.0f / 255.0f));
+            lthr = gs_logf(c4.w / (1.0f / 255.0f));
         }
     }
-    s_g[w][lane] = g;
-    const uint32_t e0 = off[p0];
+    if (!__any(member)) return;  // whole wave: no prefix Gaussian
+    const uint32_t e0 = off[g0];
     uint32_t running = 0;
     CandLDS& L = s_cand[w];
-    wave_candidates(L, lane, x0, y0, x1, y1, mx, my, c4, thr,
+    wave_candidates(L, lane, x0, y0, x1, y1, mx, my, c4, lthr,
                     [&](int owner, int tx, int ty, bool kept, bool valid, uint32_t) {
                         const uint64_t km = __ballot(kept);
                         const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
                         if (kept) {
                             const uint32_t e = e0 + running + (uint32_t)__popcll(km & lt);
                             tilekey[e] = (uint32_t)(ty * tiles_x + tx);
-                            eg[e] = s_g[w][owner];
+                            eg[e] = (uint32_t)(g0 + owner);
+                            ikey[e] = s_key[w][owner];
                         }
                         running += (uint32_t)__popcll(km);
                     });
@@ -415,61 +488,60 @@ __device__ __forceinline__ uint32_t sat_rect(const uint32_t* sat, int tx, int x0
     return sat[(size_t)y1 * W1 + x1] - sat[(size_t)y0 * W1 + x1] - sat[(size_t)y1 * W1 + x0] + sat[(size_t)y0 * W1 + x0];
 }
 
-// Phase 2 over ranks [R1, P): the same wave-cooperative candidate walk, keeping only tiles phase 1 left
-// unfinished (Gaussians whose rect misses every unfinished tile skip the walk).  COUNT: cnt2[p - R1];
-// EMIT: instances at local index off2[p - R1] + j, first_e = E1 + that, rcnt = cnt2.
+// Phase 2 over the Gaussians outside the prefix (key >= thr), in index order: the same wave-cooperative
+// candidate walk, keeping only tiles phase 1 left unfinished (Gaussians whose rect misses every unfinished tile
+// skip the walk).  COUNT: cnt2[g]; EMIT: instances at local index off2[g] + j, first_e = E1 + that, rcnt = cnt2.
 template <bool EMIT>
-__global__ void __launch_bounds__(256) k_phase2(int P, uint32_t R1, const uint32_t* __restrict__ counters,
-                                                const uint32_t* __restrict__ order,
-                                                const uint32_t* __restrict__ skey, const float4* __restrict__ sp,
+__global__ void __launch_bounds__(256) k_phase2(int P, const uint32_t* __restrict__ counters,
+                                                const uint32_t* __restrict__ dkey, const float4* __restrict__ sp,
                                                 int tiles_x, int tiles_y, const uint8_t* __restrict__ unf,
                                                 const uint32_t* __restrict__ sat, uint32_t* __restrict__ cnt2,
                                                 const uint32_t* __restrict__ off2, uint32_t* __restrict__ first_e,
                                                 uint32_t* __restrict__ rcnt, uint32_t* __restrict__ tilekey,
-                                                uint32_t* __restrict__ eg) {
+                                                uint32_t* __restrict__ eg, uint32_t* __restrict__ ikey) {
     __shared__ CandLDS s_cand[4];
-    __shared__ uint32_t s_g[4][64];
     __shared__ uint32_t s_cnt[4][64];
+    __shared__ uint32_t s_key[4][64];
     if (counters[CNT_UNFINISHED] == 0u) return;  // phase 1 finished every tile
     const uint32_t E1 = counters[CNT_E1];
+    const uint32_t thr = counters[CNT_THR];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int p0 = (int)R1 + blockIdx.x * blockDim.x + w * 64;
-    if (p0 >= P) return;
-    if (skey[p0] == 0xffffffffu) {  // whole wave in the culled tail
-        if (!EMIT && p0 + lane < P) cnt2[p0 + lane - R1] = 0u;
-        return;
-    }
-    const int p = p0 + lane;
+    const int g0 = blockIdx.x * blockDim.x + w * 64;
+    if (g0 >= P) return;
+    const int g = g0 + lane;
     int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
-    float mx = 0.f, my = 0.f, thr = 0.f;
+    float mx = 0.f, my = 0.f, lthr = 0.f;
     float4 c4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    uint32_t g = 0xffffffffu;
-    if (p < P && skey[p] != 0xffffffffu) {
-        g = order[p];
-        if (g < (uint32_t)P) {
+    bool any = false;
+    if (g < P) {
+        const uint32_t key = dkey[g];
+        s_key[w][lane] = key;
+        if (key >= thr && key != 0xffffffffu) {
             const float4 s0 = sp[2 * g], s1 = sp[2 * g + 1];
             sp_rect(s1, x0, y0, x1, y1);
-            bool any = x1 > x0 && y1 > y0 && sat_rect(sat, tiles_x, x0, y0, x1, y1) != 0u;
+            any = x1 > x0 && y1 > y0 && sat_rect(sat, tiles_x, x0, y0, x1, y1) != 0u;
             if (EMIT) {
-                const uint32_t c = cnt2[p - R1];
+                const uint32_t c = cnt2[g];
                 any = any && c != 0u;
-                if (c) { first_e[g] = E1 + off2[p - R1]; rcnt[g] = c; }
+                if (c) { first_e[g] = E1 + off2[g]; rcnt[g] = c; }
             }
             if (any) {
                 c4 = make_float4(s0.z, s0.w, s1.x, s1.y);
                 mx = s0.x; my = s0.y;
-                thr = gs_logf(c4.w / (1.0f / 255.0f));
-            } else {
-                x1 = x0; y1 = y0;
+                lthr = gs_logf(c4.w / (1.0f / 255.0f));
             }
         }
     }
-    s_g[w][lane] = g;
+    if (!any) { x1 = x0; y1 = y0; }
+    if (!__any(any)) {  // whole wave: nothing to walk
+        if (!EMIT && g < P) cnt2[g] = 0u;
+        return;
+    }
     s_cnt[w][lane] = 0u;
-    const uint32_t e0 = EMIT ? off2[p0 - R1] : 0u;
+    const uint32_t e0 = EMIT ? off2[g0] : 0u;
     uint32_t running = 0;
     CandLDS& L = s_cand[w];
-    wave_candidates(L, lane, x0, y0, x1, y1, mx, my, c4, thr,
+    wave_candidates(L, lane, x0, y0, x1, y1, mx, my, c4, lthr,
                     [&](int owner, int tx, int ty, bool kept, bool valid, uint32_t item) {
                         kept = kept && unf[ty * tiles_x + tx] != 0;
                         const uint64_t km = __ballot(kept);
@@ -478,7 +550,8 @@ __global__ void __launch_bounds__(256) k_phase2(int P, uint32_t R1, const uint32
                             if (kept) {
                                 const uint32_t e = e0 + running + (uint32_t)__popcll(km & lt);
                                 tilekey[e] = (uint32_t)(ty * tiles_x + tx);
-                                eg[e] = s_g[w][owner];
+                                eg[e] = (uint32_t)(g0 + owner);
+                                ikey[e] = s_key[w][owner];
                             }
                             running += (uint32_t)__popcll(km);
                         } else {
@@ -492,7 +565,7 @@ __global__ void __launch_bounds__(256) k_phase2(int P, uint32_t R1, const uint32
                             __builtin_amdgcn_wave_barrier();
                         }
                     });
-    if (!EMIT && p < P) cnt2[p - R1] = s_cnt[w][lane];
+    if (!EMIT && g < P) cnt2[g] = s_cnt[w][lane];
 }
 
 // identifyTileRanges over the sorted (all-valid) tile keys
@@ -524,8 +597,13 @@ __device__ __forceinline__ uint32_t bcast_u(uint32_t v, int lane) {
 // reads each with broadcast ds_read_b128 and skips a pair whose two quadrant bits are clear.  The
 // per-pixel update is branch-free: a rejected or finished pixel gets alpha = 0, which leaves C, D and T
 // unchanged.  Wave-uniform early exit once every pixel of the tile has saturated.
+#ifdef DG_FWD_WPE  // occupancy experiment: cap VGPRs so that DG_FWD_WPE waves fit per SIMD
+#define FWD_WPE_ATTR __attribute__((amdgpu_waves_per_eu(DG_FWD_WPE)))
+#else
+#define FWD_WPE_ATTR
+#endif
 template <int PHASE>
-__global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a) {
+__global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
     __shared__ float4 s_b[4][64][3];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tile = blockIdx.x * 4 + w;
@@ -711,39 +789,39 @@ void launch_preprocess(const PreArgs& a, hipStream_t s) {
     if (lds < cand) lds = cand;
     if (a.P > 0) k_preprocess<<<(a.P + 255) / 256, 256, lds, s>>>(a);
 }
-void launch_prefix_cut(const uint32_t* off, uint32_t P, uint32_t cap, uint32_t* counters, uint2* ranges,
-                       uint32_t num_tiles, hipStream_t s) {
-    k_prefix_cut<<<1, 1024, 0, s>>>(off, P, cap, counters, ranges, num_tiles);
+void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_t* hist, hipStream_t s) {
+    const int per = DH_THREADS * DH_ITEMS;
+    if (P > 0) k_depth_hist<<<(P + per - 1) / per, DH_THREADS, 0, s>>>(P, dkey, cnt, hist);
 }
-void launch_emit(int P, const uint32_t* order, const uint32_t* skey, const uint32_t* off, const float4* sp,
-                 int tiles_x, const uint32_t* counters, uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey,
-                 uint32_t* eg, hipStream_t s) {
+void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, uint2* ranges, uint32_t num_tiles,
+                      hipStream_t s) {
+    k_depth_cut<<<1, 1024, 0, s>>>(hist, cap, counters, ranges, num_tiles);
+}
+void launch_emit(int P, const uint32_t* dkey, const uint32_t* cnt, const uint32_t* off, const float4* sp, int tiles_x,
+                 const uint32_t* counters, uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey, uint32_t* eg,
+                 uint32_t* ikey, hipStream_t s) {
     const int per_block = 4 * EMIT_RANKS;
     if (P > 0)
-        k_emit<<<(P + per_block - 1) / per_block, 256, 0, s>>>(P, order, skey, off, sp, tiles_x, counters, first_e,
-                                                               rcnt, tilekey, eg);
+        k_emit<<<(P + per_block - 1) / per_block, 256, 0, s>>>(P, dkey, cnt, off, sp, tiles_x, counters, first_e, rcnt,
+                                                               tilekey, eg, ikey);
 }
 void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, int tiles_x, int tiles_y,
                            uint32_t* sat, hipStream_t s) {
     k_unfinished_sat<<<1, 1024, 0, s>>>(counters, unfinished, tiles_x, tiles_y, sat);
 }
-void launch_count2(int P, uint32_t R1, const uint32_t* counters, const uint32_t* order, const uint32_t* skey,
-                   const float4* sp, int tiles_x, int tiles_y, const uint8_t* unfinished, const uint32_t* sat,
-                   uint32_t* cnt2, hipStream_t s) {
-    const int n = P - (int)R1;
-    if (n > 0)
-        k_phase2<false><<<(n + 255) / 256, 256, 0, s>>>(P, R1, counters, order, skey, sp, tiles_x, tiles_y, unfinished,
-                                                         sat, cnt2, nullptr, nullptr, nullptr, nullptr, nullptr);
+void launch_count2(int P, const uint32_t* counters, const uint32_t* dkey, const float4* sp, int tiles_x, int tiles_y,
+                   const uint8_t* unfinished, const uint32_t* sat, uint32_t* cnt2, hipStream_t s) {
+    if (P > 0)
+        k_phase2<false><<<(P + 255) / 256, 256, 0, s>>>(P, counters, dkey, sp, tiles_x, tiles_y, unfinished, sat, cnt2,
+                                                         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
 }
-void launch_emit2(int P, uint32_t R1, const uint32_t* counters, const uint32_t* order, const uint32_t* skey,
-                  const float4* sp, int tiles_x, int tiles_y, const uint8_t* unfinished, const uint32_t* sat,
-                  const uint32_t* cnt2, const uint32_t* off2, uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey,
-                  uint32_t* eg, hipStream_t s) {
-    const int n = P - (int)R1;
-    if (n > 0)
-        k_phase2<true><<<(n + 255) / 256, 256, 0, s>>>(P, R1, counters, order, skey, sp, tiles_x, tiles_y, unfinished,
-                                                        sat, const_cast<uint32_t*>(cnt2), off2, first_e, rcnt,
-                                                        tilekey, eg);
+void launch_emit2(int P, const uint32_t* counters, const uint32_t* dkey, const float4* sp, int tiles_x, int tiles_y,
+                  const uint8_t* unfinished, const uint32_t* sat, const uint32_t* cnt2, const uint32_t* off2,
+                  uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey, uint32_t* eg, uint32_t* ikey, hipStream_t s) {
+    if (P > 0)
+        k_phase2<true><<<(P + 255) / 256, 256, 0, s>>>(P, counters, dkey, sp, tiles_x, tiles_y, unfinished, sat,
+                                                        const_cast<uint32_t*>(cnt2), off2, first_e, rcnt, tilekey, eg,
+                                                        ikey);
 }
 void launch_ranges(uint32_t Kcap, const uint32_t* n_dev, const uint32_t* keys, uint2* ranges, uint32_t num_tiles,
                    hipStream_t s) {

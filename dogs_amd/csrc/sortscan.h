@@ -15,9 +15,27 @@ int radix_sort_pairs(uint32_t* keys0, uint32_t* vals0, uint32_t* keys1, uint32_t
                      uint32_t n, int begin_bit, int end_bit, void* temp, hipStream_t stream,
                      const uint32_t* n_dev = nullptr);
 
-// out[i] = sum_{j<i} in[gather ? gather[j] : j];  *total = full sum (device pointer).
+// out[i] = sum_{j<i} v[j], v[j] = in[j] (or 0 when lt_keys is given and lt_keys[j] >= *lt_thr, a device-side
+// threshold);  *total = full sum (device pointer).
 // gate (optional, device): when *gate == 0 nothing is read or written except *total = 0.
 size_t scan_temp_bytes(uint32_t n);
-void exclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t n, uint32_t* out, uint32_t* total,
-                    void* temp, hipStream_t stream, const uint32_t* gate = nullptr);
+void exclusive_scan(const uint32_t* in, uint32_t n, uint32_t* out, uint32_t* total, void* temp, hipStream_t stream,
+                    const uint32_t* gate = nullptr, const uint32_t* lt_keys = nullptr, const uint32_t* lt_thr = nullptr);
+
+// Per-tile stable sort of instance lists by the depth key of their Gaussian (sortscan.hip k_tile_dsort):
+// s_e[ranges[t].x .. ranges[t].y) is reordered in place by ikey[v]; ties keep their input order.
+struct DSortArgs {
+    int num_tiles;
+    const uint2* ranges;
+    uint32_t* s_e;              // tile-sorted instance list (values are indices into eg)
+    uint32_t* s_tmp;            // scratch values, same indexing as s_e (long lists)
+    uint32_t *k_a, *k_b;        // scratch keys, same indexing as s_e (long lists)
+    const uint32_t* ikey;       // instance -> 32-bit depth key of its Gaussian
+    uint32_t n_inst;            // bound of ikey
+    const uint8_t* only;        // optional: sort only tiles t with only[t] != 0
+    const uint32_t* gate;       // optional (device): nothing when *gate == 0
+    uint32_t* long_list;        // [num_tiles] queue of tiles longer than the per-wave capacity
+    uint32_t* long_cnt;         // device queue length, zeroed beforehand
+};
+void tile_depth_sort(const DSortArgs& a, hipStream_t stream);
 }  // namespace gs

@@ -270,18 +270,26 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
     return off + x - v;
 }
 
+// element i of the scanned sequence: in[i], or 0 when a mask is given and lt_keys[i] >= *lt_thr
+__device__ __forceinline__ uint32_t sc_val(const uint32_t* in, const uint32_t* lt_keys, uint32_t thr, uint32_t i) {
+    const uint32_t v = in[i];
+    return (lt_keys && !(lt_keys[i] < thr)) ? 0u : v;
+}
+
 __global__ void __launch_bounds__(SC_THREADS) sc_reduce(const uint32_t* __restrict__ in,
-                                                        const uint32_t* __restrict__ gather, uint32_t n,
+                                                        const uint32_t* __restrict__ lt_keys,
+                                                        const uint32_t* __restrict__ lt_thr, uint32_t n,
                                                         uint32_t* __restrict__ block_sums,
                                                         const uint32_t* __restrict__ gate) {
     __shared__ uint32_t s_w[SC_THREADS / 64];
     if (gate && *gate == 0u) return;
+    const uint32_t thr = lt_keys ? *lt_thr : 0u;
     const uint32_t base = blockIdx.x * SC_TILE + threadIdx.x * SC_ITEMS;
     uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < SC_ITEMS; k++) {
         const uint32_t i = base + k;
-        if (i < n) s += in[gather ? gather[i] : i];
+        if (i < n) s += sc_val(in, lt_keys, thr, i);
     }
     uint32_t tot;
     block_excl_scan(s, s_w, tot);
@@ -314,19 +322,21 @@ __global__ void __launch_bounds__(SC_THREADS) sc_scan_sums(uint32_t* __restrict_
 }
 
 __global__ void __launch_bounds__(SC_THREADS) sc_downsweep(const uint32_t* __restrict__ in,
-                                                           const uint32_t* __restrict__ gather, uint32_t n,
+                                                           const uint32_t* __restrict__ lt_keys,
+                                                           const uint32_t* __restrict__ lt_thr, uint32_t n,
                                                            const uint32_t* __restrict__ block_sums,
                                                            uint32_t* __restrict__ out,
                                                            const uint32_t* __restrict__ gate) {
     __shared__ uint32_t s_w[SC_THREADS / 64];
     if (gate && *gate == 0u) return;
+    const uint32_t thr = lt_keys ? *lt_thr : 0u;
     const uint32_t base = blockIdx.x * SC_TILE + threadIdx.x * SC_ITEMS;
     uint32_t v[SC_ITEMS];
     uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < SC_ITEMS; k++) {
         const uint32_t i = base + k;
-        v[k] = i < n ? in[gather ? gather[i] : i] : 0u;
+        v[k] = i < n ? sc_val(in, lt_keys, thr, i) : 0u;
         s += v[k];
     }
     uint32_t tot;
@@ -344,17 +354,247 @@ size_t scan_temp_bytes(uint32_t n) {
     return (size_t)(nb ? nb : 1) * sizeof(uint32_t);
 }
 
-void exclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t n, uint32_t* out, uint32_t* total,
-                    void* temp, hipStream_t stream, const uint32_t* gate) {
+void exclusive_scan(const uint32_t* in, uint32_t n, uint32_t* out, uint32_t* total, void* temp, hipStream_t stream,
+                    const uint32_t* gate, const uint32_t* lt_keys, const uint32_t* lt_thr) {
     const uint32_t nb = (n + SC_TILE - 1) / SC_TILE;
     uint32_t* sums = (uint32_t*)temp;
     if (n == 0) {
         (void)hipMemsetAsync(total, 0, sizeof(uint32_t), stream);
         return;
     }
-    sc_reduce<<<nb, SC_THREADS, 0, stream>>>(in, gather, n, sums, gate);
+    sc_reduce<<<nb, SC_THREADS, 0, stream>>>(in, lt_keys, lt_thr, n, sums, gate);
     sc_scan_sums<<<1, SC_THREADS, 0, stream>>>(sums, nb, total, gate);
-    sc_downsweep<<<nb, SC_THREADS, 0, stream>>>(in, gather, n, sums, out, gate);
+    sc_downsweep<<<nb, SC_THREADS, 0, stream>>>(in, lt_keys, lt_thr, n, sums, out, gate);
+}
+
+
+// ---------------- per-tile depth sort (segmented, stable) ----------------
+// Each tile's instance list [ranges[t].x, ranges[t].y) of s_e arrives in index order (emission order, stably
+// sorted by tile); it is sorted in place by the 32-bit depth key dkey[eg[v]] of its Gaussian, stably, so ties
+// keep the index order: the reference's (tile, depth bits, index) order, tile by tile.
+//   k_tile_dsort       one wave per tile, lists up to DS_WAVE_MAX: items in registers (16 per lane), LSD radix
+//                      over the tile's key range (keys relative to the tile minimum, 8-bit digits, only as many
+//                      passes as the range needs), wave-level peer-mask ranking, LDS scatter.
+//   k_tile_dsort_long  longer lists (queued by k_tile_dsort): one block per tile, LSD radix through global
+//                      scratch in 256-item chunks.
+constexpr int DS_WAVE_MAX = 1024;
+constexpr int DS_ROWS = DS_WAVE_MAX / 64;
+
+__device__ __forceinline__ uint32_t ds_key(const DSortArgs& a, uint32_t v) {
+    return a.ikey[v < a.n_inst ? v : a.n_inst - 1];
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { const uint32_t y = __shfl_xor(x, o); x = y < x ? y : x; }
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { const uint32_t y = __shfl_xor(x, o); x = y > x ? y : x; }
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+}
+
+__global__ void __launch_bounds__(256) k_tile_dsort(DSortArgs a) {
+    __shared__ uint32_t s_cnt[4][RS_RADIX];
+    __shared__ uint32_t s_k[4][DS_WAVE_MAX];
+    __shared__ uint32_t s_v[4][DS_WAVE_MAX];
+    if (a.gate && *a.gate == 0u) return;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tile = blockIdx.x * 4 + w;
+    if (tile >= a.num_tiles) return;
+    if (a.only && !a.only[tile]) return;
+    const uint2 rg = a.ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    if (n <= 1) return;
+    if (n > DS_WAVE_MAX) {
+        if (lane == 0) a.long_list[atomicAdd(a.long_cnt, 1u)] = (uint32_t)tile;
+        return;
+    }
+    uint32_t* se = a.s_e + rg.x;
+    const int R = (n + 63) >> 6;
+    uint32_t k[DS_ROWS], v[DS_ROWS], rank[DS_ROWS];
+    // all loads of a stage are issued before any use: one latency round per stage (list, eg, dkey)
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        const int i = r * 64 + lane;
+        v[r] = (r < R && i < n) ? se[i] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        const int i = r * 64 + lane;
+        k[r] = (r < R && i < n) ? ds_key(a, v[r]) : 0u;
+    }
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        const int i = r * 64 + lane;
+        if (r < R && i < n) {
+            kmin = k[r] < kmin ? k[r] : kmin;
+            kmax = k[r] > kmax ? k[r] : kmax;
+        }
+    }
+    kmin = wave_min_u32(kmin);
+    kmax = wave_max_u32(kmax);
+    if (kmin == kmax) return;  // one key: the index order is already the sorted order
+    const uint32_t range = kmax - kmin;
+    const int passes = (32 - __clz((int)range) + 7) >> 3;
+    // padding slots (i >= n) sort last: all-ones relative key, and they come last in the input
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        const int i = r * 64 + lane;
+        k[r] = (i < n) ? k[r] - kmin : 0xffffffffu;
+    }
+    uint32_t* cnt = s_cnt[w];
+    uint32_t* lk = s_k[w];
+    uint32_t* lv = s_v[w];
+    const uint64_t lt = lanemask_lt();
+    for (int p = 0; p < passes; p++) {
+        const int shift = 8 * p;
+#pragma unroll
+        for (int q = 0; q < 4; q++) cnt[q * 64 + lane] = 0u;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < DS_ROWS; r++) {
+            if (r < R) {
+                const uint32_t d = (k[r] >> shift) & 0xffu;
+                const uint64_t m = peer_mask(d, true);
+                const uint32_t before = (uint32_t)__popcll(m & lt);
+                const uint32_t cur = cnt[d];
+                rank[r] = cur + before;
+                if (before == 0) cnt[d] = cur + (uint32_t)__popcll(m);  // LDS ops of one wave complete in order
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        {  // exclusive scan of the 256 digit counts, 4 per lane
+            const uint32_t c0 = cnt[4 * lane], c1 = cnt[4 * lane + 1], c2 = cnt[4 * lane + 2], c3 = cnt[4 * lane + 3];
+            const uint32_t loc = c0 + c1 + c2 + c3;
+            uint32_t x = loc;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o);
+                if (lane >= o) x += y;
+            }
+            const uint32_t ex = x - loc;
+            __builtin_amdgcn_wave_barrier();
+            cnt[4 * lane] = ex; cnt[4 * lane + 1] = ex + c0; cnt[4 * lane + 2] = ex + c0 + c1;
+            cnt[4 * lane + 3] = ex + c0 + c1 + c2;
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < DS_ROWS; r++) {
+            if (r < R) {
+                const uint32_t pos = cnt[(k[r] >> shift) & 0xffu] + rank[r];
+                lk[pos] = k[r];
+                lv[pos] = v[r];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < DS_ROWS; r++) {
+            if (r < R) { k[r] = lk[r * 64 + lane]; v[r] = lv[r * 64 + lane]; }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        const int i = r * 64 + lane;
+        if (r < R && i < n) se[i] = v[r];
+    }
+}
+
+// Long lists: one block per queued tile; keys gathered once into scratch, then LSD passes ping-pong between
+// (keys, s_e) and (keys2, tmp) in 256-item chunks (per-wave peer masks + per-wave digit counts give the stable
+// in-chunk rank).  Grid-stride over the queue; the queue length is device-side (no host sync).
+__global__ void __launch_bounds__(256) k_tile_dsort_long(DSortArgs a) {
+    __shared__ uint32_t s_base[RS_RADIX];
+    __shared__ uint32_t s_wh[RS_WAVES][RS_RADIX];
+    __shared__ uint32_t s_red[2][RS_WAVES];
+    if (a.gate && *a.gate == 0u) return;
+    const uint32_t nl = *a.long_cnt;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint64_t lt = lanemask_lt();
+    for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
+        const int tile = (int)a.long_list[li];
+        const uint2 rg = a.ranges[tile];
+        const uint32_t n = rg.y - rg.x;
+        uint32_t *va = a.s_e + rg.x, *vb = a.s_tmp + rg.x, *ka = a.k_a + rg.x, *kb = a.k_b + rg.x;
+        uint32_t kmin = 0xffffffffu, kmax = 0u;
+        for (uint32_t i = t; i < n; i += 256) {
+            const uint32_t key = ds_key(a, va[i]);
+            ka[i] = key;
+            kmin = key < kmin ? key : kmin;
+            kmax = key > kmax ? key : kmax;
+        }
+        kmin = wave_min_u32(kmin);
+        kmax = wave_max_u32(kmax);
+        if (lane == 0) { s_red[0][w] = kmin; s_red[1][w] = kmax; }
+        __syncthreads();
+        kmin = s_red[0][0]; kmax = s_red[1][0];
+        for (int q = 1; q < RS_WAVES; q++) {
+            kmin = s_red[0][q] < kmin ? s_red[0][q] : kmin;
+            kmax = s_red[1][q] > kmax ? s_red[1][q] : kmax;
+        }
+        const uint32_t range = kmax - kmin;
+        const int passes = range ? (32 - __clz((int)range) + 7) >> 3 : 0;
+        for (int p = 0; p < passes; p++) {
+            const int shift = 8 * p;
+            s_base[t] = 0u;
+            __syncthreads();
+            for (uint32_t i = t; i < n; i += 256) atomicAdd(&s_base[((ka[i] - kmin) >> shift) & 0xffu], 1u);
+            __syncthreads();
+            {  // exclusive scan of the digit counts (thread t = digit t)
+                const uint32_t c = s_base[t];
+                uint32_t x = c;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(x, o);
+                    if (lane >= o) x += y;
+                }
+                if (lane == 63) s_red[0][w] = x;
+                __syncthreads();
+                uint32_t off = 0;
+                for (int q = 0; q < w; q++) off += s_red[0][q];
+                s_base[t] = off + x - c;
+            }
+            __syncthreads();
+            for (uint32_t c0 = 0; c0 < n; c0 += 256) {
+                const uint32_t i = c0 + t;
+                const bool act = i < n;
+                const uint32_t key = act ? ka[i] : 0u;
+                const uint32_t val = act ? va[i] : 0u;
+                const uint32_t d = ((key - kmin) >> shift) & 0xffu;
+                const uint64_t m = peer_mask(d, act);
+                const uint32_t before = (uint32_t)__popcll(m & lt);
+#pragma unroll
+                for (int q = 0; q < RS_WAVES; q++) s_wh[q][t] = 0u;
+                __syncthreads();
+                if (act && before == 0) s_wh[w][d] = (uint32_t)__popcll(m);
+                __syncthreads();
+                if (act) {
+                    uint32_t pos = s_base[d] + before;
+                    for (int q = 0; q < w; q++) pos += s_wh[q][d];
+                    kb[pos] = key;
+                    vb[pos] = val;
+                }
+                __syncthreads();
+                s_base[t] += s_wh[0][t] + s_wh[1][t] + s_wh[2][t] + s_wh[3][t];
+                __syncthreads();
+            }
+            uint32_t* tk = ka; ka = kb; kb = tk;
+            uint32_t* tv = va; va = vb; vb = tv;
+            __syncthreads();
+        }
+        if (passes & 1)  // result in the scratch values: copy back into s_e
+            for (uint32_t i = t; i < n; i += 256) vb[i] = va[i];
+        __syncthreads();
+    }
+}
+
+void tile_depth_sort(const DSortArgs& a, hipStream_t stream) {
+    if (a.num_tiles <= 0) return;
+    k_tile_dsort<<<(a.num_tiles + 3) / 4, 256, 0, stream>>>(a);
+    k_tile_dsort_long<<<256, 256, 0, stream>>>(a);
 }
 
 }  // namespace gs
