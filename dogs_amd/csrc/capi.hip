@@ -199,7 +199,6 @@ struct BwdScratch {
     uint8_t* flag;
     float* rec;
     uint32_t* invd_flag;
-    float4* sums;  // [P][3] per-Gaussian record sums
     uint32_t* order;  // [T] replay order of the tiles
     size_t bytes;
 };
@@ -210,7 +209,6 @@ BwdScratch carve_bwd(void* base, int64_t K, int P, int T) {
     s.flag = c.take<uint8_t>(n);
     s.rec = c.take<float>(12 * n);
     s.invd_flag = c.take<uint32_t>(4);
-    s.sums = c.take<float4>(3 * (size_t)(P > 0 ? P : 1));
     s.order = c.take<uint32_t>((size_t)(T > 0 ? T : 1));
     s.bytes = c.off;
     return s;
@@ -525,11 +523,10 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     q.means3D = a->means3D; q.scales = a->scales; q.rotations = a->rotations; q.opacities = a->opacities;
     q.dc = a->dc; q.sh = (a->M > 0) ? a->sh : nullptr; q.cov3D_precomp = a->cov3D_precomp;
     q.view = a->viewmatrix; q.proj = a->projmatrix; q.campos = a->campos;
-    q.radii = radii; q.cnt = g.rcnt; q.first_e = g.first_e; q.sp = g.sp; q.rec = sc.rec; q.flag = sc.flag; q.sums = sc.sums;
+    q.radii = radii; q.cnt = g.rcnt; q.first_e = g.first_e; q.sp = g.sp; q.rec = sc.rec; q.flag = sc.flag;
     q.dmeans2D = dmeans2D; q.dcolors = dcolors; q.dopacity = dopacity; q.dmeans3D = dmeans3D; q.dcov3D = dcov3D;
     q.ddc = ddc; q.dsh = dsh; q.dscales = dscales; q.drot = drot; q.depth = depth;
     if (q.M > 0 && !dsh) return fail("dsh output required when M > 0%s%d");
-    { PROF("record_sum"); gs::launch_record_sum(q, s); }
     { PROF("gauss_bwd"); gs::launch_gauss_bwd(q, s); }
     DBG_SYNC(a->debug, s);
     HIP_OK(hipGetLastError());

@@ -208,18 +208,28 @@ __device__ __forceinline__ void stage_lds_dma(float4* dst4, const float4* src4, 
 // an image and a 1080p view has only ~1.6 tiles per resident wave slot, so in raster order a render launch
 // ends on a tail of long centre tiles; in descending order the short tiles fill in behind the long ones.
 // Counting sort on min(len(tile) / 4, 255); the order within a bucket is unspecified (no output depends on
-// the launch order).
+// the launch order).  Each thread evaluates all of its tiles' lengths up front (their loads in flight
+// together) and keeps them in registers for the scatter.
 template <typename LenFn>
 __device__ __forceinline__ void tile_order_sort(int num_tiles, uint32_t* order, LenFn&& len) {
-    constexpr int NB = 256;
+    constexpr int NB = 256, PER = 16;  // up to 1024 * 16 tiles in registers; more loop in chunks
     __shared__ uint32_t s_hist[NB];
     __shared__ uint32_t s_wsum[NB / 64];
     const int t = threadIdx.x;
     if (t < NB) s_hist[t] = 0u;
     __syncthreads();
-    for (int tile = t; tile < num_tiles; tile += blockDim.x) {
-        const uint32_t l = len(tile) >> 2;
-        atomicAdd(&s_hist[NB - 1 - (l < NB - 1 ? l : NB - 1)], 1u);
+    const int chunk = (int)blockDim.x * PER;
+    for (int c0 = 0; c0 < num_tiles; c0 += chunk) {
+        uint32_t b[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int tile = c0 + k * (int)blockDim.x + t;
+            const uint32_t l = tile < num_tiles ? len(tile) >> 2 : 0u;
+            b[k] = NB - 1 - (l < NB - 1 ? l : NB - 1);
+        }
+#pragma unroll
+        for (int k = 0; k < PER; k++)
+            if (c0 + k * (int)blockDim.x + t < num_tiles) atomicAdd(&s_hist[b[k]], 1u);
     }
     __syncthreads();
     uint32_t v = 0, incl = 0;
@@ -241,9 +251,19 @@ __device__ __forceinline__ void tile_order_sort(int num_tiles, uint32_t* order, 
         s_hist[t] = off + incl - v;
     }
     __syncthreads();
-    for (int tile = t; tile < num_tiles; tile += blockDim.x) {
-        const uint32_t l = len(tile) >> 2;
-        order[atomicAdd(&s_hist[NB - 1 - (l < NB - 1 ? l : NB - 1)], 1u)] = (uint32_t)tile;
+    for (int c0 = 0; c0 < num_tiles; c0 += chunk) {
+        uint32_t b[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int tile = c0 + k * (int)blockDim.x + t;
+            const uint32_t l = tile < num_tiles ? len(tile) >> 2 : 0u;
+            b[k] = NB - 1 - (l < NB - 1 ? l : NB - 1);
+        }
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int tile = c0 + k * (int)blockDim.x + t;
+            if (tile < num_tiles) order[atomicAdd(&s_hist[b[k]], 1u)] = (uint32_t)tile;
+        }
     }
 }
 

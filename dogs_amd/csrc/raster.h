@@ -110,7 +110,6 @@ struct GaussBwdArgs {
     const float4* sp;        // splat records (conic + AA-scaled opacity)
     const float* rec;
     const uint8_t* flag;
-    float4* sums;            // [P][3] record sums (k_record_sum -> k_gauss_bwd)
     float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *ddc, *dsh, *dscales, *drot, *depth;
 };
 
@@ -142,7 +141,6 @@ void launch_mark_visible(int P, const float* means3D, const float* view, bool* p
 void launch_filter(const PreArgs& a, hipStream_t s);
 // clears the record flags of the E1 + K2 binned instances and sets counters[CNT_INVD], then replays
 void launch_render_bwd(const RenderBwdArgs& a, uint32_t* counters, hipStream_t s);
-void launch_record_sum(const GaussBwdArgs& a, hipStream_t s);
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s);
 
 }  // namespace gs

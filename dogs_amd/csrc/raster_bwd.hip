@@ -8,8 +8,8 @@
 //                reduce-scatter (13 cross-lane exchanges instead of 60) and stored once as a 48-B record
 //                at the instance's emission slot -- no float atomics (the chip-wide atomic rate and the
 //                scattered-row penalty make per-instance atomicAdd the wrong tool on MI355X).
-// k_record_sum   a wave per 64 Gaussians sums their records in emission order (deterministic).
-// k_gauss_bwd    one thread per Gaussian: turns the summed moments into dL/d(mean2D, conic, opacity), then
+// k_gauss_bwd    a wave per 64 Gaussians first sums their records in emission order (deterministic), then one
+//                thread per Gaussian turns the summed moments into dL/d(mean2D, conic, opacity), then
 //                computeCov2DCUDA + preprocessCUDA backward (backward.cu:149-451) fused in one pass.
 #include <hip/hip_runtime.h>
 #include "gs_common.h"
@@ -296,22 +296,26 @@ __global__ void __launch_bounds__(256) k_bwd_prologue(uint32_t* __restrict__ cou
 // ---------------------------------------------------------------------------------------------------
 __device__ __forceinline__ float sq(float x) { return x * x; }
 
-__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, float* lsh);
+__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, float* lsh, const float (&acc)[10]);
 
 // Sum each Gaussian's instance records (written by k_render_bwd at emission slots [first_e, first_e + cnt)
-// whose flag is set) into sums[idx].  A wave owns 64 consecutive Gaussians; their instances are walked
+// whose flag is set) into acc (registers).  A wave owns 64 consecutive Gaussians; their instances are walked
 // flattened, 64 per step (flag reads coalesced, no lane waits on the longest list), each step's flagged
 // records are parked in LDS, and every owner lane folds its own ones in increasing emission order --
 // the same sequential order as the reference-side sum, so the result is deterministic.
 constexpr uint32_t RS_BIG = 256;
 
-__global__ void __launch_bounds__(256) k_record_sum(GaussBwdArgs a) {
-    __shared__ uint32_t s_pre[4][64];
-    __shared__ uint32_t s_e0[4][64];
-    __shared__ float4 s_rec[4][64][3];
+struct RecSumLDS {
+    uint32_t pre[4][64];
+    uint32_t e0[4][64];
+    float4 rec[4][64][3];
+};
+
+__device__ __forceinline__ void record_sum(const GaussBwdArgs& a, int idx, RecSumLDS& L, float (&acc)[10]) {
+    uint32_t (&s_pre)[4][64] = L.pre;
+    uint32_t (&s_e0)[4][64] = L.e0;
+    float4 (&s_rec)[4][64][3] = L.rec;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    float acc[10];
 #pragma unroll
     for (int v = 0; v < 10; v++) acc[v] = 0.f;
     uint32_t c = 0, e0 = 0;
@@ -398,15 +402,13 @@ __global__ void __launch_bounds__(256) k_record_sum(GaussBwdArgs a) {
         }
         __builtin_amdgcn_wave_barrier();
     }
-    if (idx < a.P) {
-        a.sums[3 * (size_t)idx + 0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-        a.sums[3 * (size_t)idx + 1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
-        a.sums[3 * (size_t)idx + 2] = make_float4(acc[8], acc[9], 0.f, 0.f);
-    }
 }
 
 // Block of 256 Gaussians; the [256][M][3] SH slab is staged through LDS so both the coefficient loads
 // and the dL/dsh stores are coalesced (a per-thread 180-B stride touches 64 lines per wave instruction).
+// One block of 256 Gaussians: (1) each wave sums its 64 Gaussians' instance records (record_sum, LDS scratch at
+// the head of the block's LDS), (2) the [256][M][3] SH slab is staged through the same LDS, (3) one thread per
+// Gaussian runs the per-Gaussian backward.  The record sums never leave registers.
 __global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     const int t = threadIdx.x;
@@ -415,6 +417,9 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
     const int nloc = (a.P - base) < 256 ? (a.P - base) : 256;
     const int M = a.M;
     const int slab = nloc * M * 3;  // floats
+    float acc[10];
+    record_sum(a, idx, *reinterpret_cast<RecSumLDS*>(s_sh), acc);
+    __syncthreads();  // the record-sum scratch is reused by the SH slab
     if (a.sh && M > 0) {
         const float* src = a.sh + (size_t)base * M * 3;
         const int n4 = slab >> 2;  // base*M*3*4 bytes is a multiple of 16 (256*M*12)
@@ -428,7 +433,7 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
         }
     }
     __syncthreads();
-    if (idx < a.P) gauss_bwd_one(a, idx, s_sh + t * M * 3);
+    if (idx < a.P) gauss_bwd_one(a, idx, s_sh + t * M * 3, acc);
     __syncthreads();
     if (a.dsh && M > 0) {
         float* dst = a.dsh + (size_t)base * M * 3;
@@ -445,12 +450,11 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
 }
 
 // One Gaussian; `lsh` is its [M][3] SH row in LDS, overwritten in place with dL/dsh.
-__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, float* lsh) {
+__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, float* lsh, const float (&sums)[10]) {
     const int M = a.M;
-    // every per-Gaussian input is loaded up front: one HBM round trip instead of four dependent ones
-    // (radii -> records/splat -> means -> scales/rotations); culled Gaussians read bytes they ignore
+    // every per-Gaussian input is loaded up front: one HBM round trip instead of three dependent ones
+    // (radii -> splat -> means -> scales/rotations); culled Gaussians read bytes they ignore
     const int rad = a.radii[idx];
-    const float4 r0 = a.sums[3 * (size_t)idx + 0], r1 = a.sums[3 * (size_t)idx + 1], r2 = a.sums[3 * (size_t)idx + 2];
     const float4 sp0 = a.sp[2 * (size_t)idx], sp1 = a.sp[2 * (size_t)idx + 1];
     const f3 mean = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
     f3 scl = {0.f, 0.f, 0.f};
@@ -476,11 +480,8 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
     }
     // ---- records -> dL/d(mean2D, conic, opacity, color, invdepth): summed by the wave (see below)
     float acc[10];
-    {
-        const float4 s0 = r0, s1 = r1, s2 = r2;
-        acc[0] = s0.x; acc[1] = s0.y; acc[2] = s0.z; acc[3] = s0.w; acc[4] = s1.x;
-        acc[5] = s1.y; acc[6] = s1.z; acc[7] = s1.w; acc[8] = s2.x; acc[9] = s2.y;
-    }
+#pragma unroll
+    for (int v = 0; v < 10; v++) acc[v] = sums[v];
     // moments -> dL/dmean2D, dL/dconic (see render_bwd_tile); o = the AA-scaled opacity of the forward
     {
         const float4 c4 = make_float4(sp0.z, sp0.w, sp1.x, sp1.y);
@@ -716,11 +717,9 @@ void launch_render_bwd(const RenderBwdArgs& a, uint32_t* counters, hipStream_t s
         k_render_bwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
     }
 }
-void launch_record_sum(const GaussBwdArgs& a, hipStream_t s) {
-    if (a.P > 0) k_record_sum<<<(a.P + 255) / 256, 256, 0, s>>>(a);
-}
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s) {
-    const size_t lds = (size_t)256 * (a.M > 0 ? a.M : 0) * 3 * sizeof(float);
+    size_t lds = (size_t)256 * (a.M > 0 ? a.M : 0) * 3 * sizeof(float);
+    if (lds < sizeof(RecSumLDS)) lds = sizeof(RecSumLDS);
     if (a.P > 0) k_gauss_bwd<<<(a.P + 255) / 256, 256, lds, s>>>(a);
 }
 

@@ -4,6 +4,7 @@ pybind11 functions in rasterize_points.cu; tensors are torch tensors on a HIP de
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -13,8 +14,9 @@ _EMPTY_U8 = None
 
 # Depth-prefix binning policy (dg_raster_args.prefix_per_tile): phase-1 capacity = this x tiles; 0 -> the
 # library default (256), < 0 -> bin every instance in one phase.  Module-level so that the forward and the
-# backward of a view always agree; tests lower it to exercise the phase-2 path.
-PREFIX_PER_TILE = 0
+# backward of a view always agree; tests lower it to exercise the phase-2 path.  DOGS_PREFIX_PER_TILE sets it
+# for experiments (tools/prefix_sweep.sh).
+PREFIX_PER_TILE = int(os.environ.get("DOGS_PREFIX_PER_TILE", "0"))
 
 
 def set_prefix_per_tile(n: int) -> int:
