@@ -81,11 +81,6 @@ struct Carver {
 
 inline int tiles_x_of(int W) { return (W + 15) / 16; }
 inline int tiles_y_of(int H) { return (H + 15) / 16; }
-inline int bits_for(uint32_t n) {  // bits needed for ids in [0, n)
-    int b = 1;
-    while ((1u << b) < n && b < 32) b++;
-    return b;
-}
 
 struct Geom {
     uint32_t* counters;  // CNT_* (raster.h)
@@ -126,6 +121,7 @@ struct Image {
     float4* resume;         // [HW] raw colour + live threshold of unfinished tiles' pixels
     uint32_t* sat;          // [(ty+1)*(tx+1)] summed-area table of `unfinished`
     uint32_t* long_tiles;   // [T] queue of the long-list tile depth sort
+    uint32_t *tile_cnt, *tile_cnt2;  // [T] per-tile instance counters of the phase-1 / phase-2 binning
     size_t bytes;
 };
 Image carve_image(void* base, int W, int H) {
@@ -144,31 +140,45 @@ Image carve_image(void* base, int W, int H) {
     im.resume = c.take<float4>(HW);
     im.sat = c.take<uint32_t>((size_t)(tiles_x_of(W) + 1) * (tiles_y_of(H) + 1));
     im.long_tiles = c.take<uint32_t>(T);
+    im.tile_cnt = c.take<uint32_t>(T);
+    im.tile_cnt2 = c.take<uint32_t>(T);
     im.bytes = c.off;
     return im;
 }
 
+// Per-instance arrays of one binning phase; instances are indexed by emission order.
 struct Binning {
-    uint32_t *tk0, *se0, *tk1, *se1, *eg;
-    uint32_t* ik;  // instance depth keys (emission order)
-    uint32_t* dk;  // depth-key scratch of the long-list tile sort
-    void* sort_tmp;
+    uint32_t* tk;    // tile of each instance
+    uint32_t* slot;  // arrival slot in its tile (counting sort); then scratch keys of the long-list depth sort
+    uint32_t* se;    // instances binned by tile, each tile in (depth, index) order
+    uint32_t* se_tmp;  // scratch values of the long-list depth sort
+    uint32_t* eg;    // Gaussian of each instance
+    uint32_t* ik;    // depth key of each instance
+    uint32_t* dk;    // scratch keys of the long-list depth sort
     size_t bytes;
 };
 Binning carve_binning(void* base, int64_t K) {
     Carver c(base);
     Binning b;
     const size_t n = (size_t)(K > 0 ? K : 1);
-    b.tk0 = c.take<uint32_t>(n);
-    b.se0 = c.take<uint32_t>(n);
-    b.tk1 = c.take<uint32_t>(n);
-    b.se1 = c.take<uint32_t>(n);
+    b.tk = c.take<uint32_t>(n);
+    b.slot = c.take<uint32_t>(n);
+    b.se = c.take<uint32_t>(n);
+    b.se_tmp = c.take<uint32_t>(n);
     b.eg = c.take<uint32_t>(n);
     b.ik = c.take<uint32_t>(n);
     b.dk = c.take<uint32_t>(n);
-    b.sort_tmp = c.take<char>(gs::radix_sort_temp_bytes((uint32_t)n));
     b.bytes = c.off;
     return b;
+}
+void bin_and_sort(const Binning& b, int64_t cap, const uint32_t* n_dev, int T, uint2* ranges, uint32_t* tile_cnt,
+                  const uint8_t* only, const uint32_t* gate, uint32_t* long_list, uint32_t* long_cnt, hipStream_t s) {
+    gs::tile_bin((uint32_t)cap, n_dev, b.tk, b.slot, tile_cnt, (uint32_t)T, ranges, b.se, s, gate);
+    gs::DSortArgs d;
+    d.num_tiles = T; d.ranges = ranges; d.s_e = b.se; d.s_tmp = b.se_tmp; d.k_a = b.dk; d.k_b = b.slot;
+    d.ikey = b.ik; d.eg = b.eg; d.n_inst = (uint32_t)(cap > 0 ? cap : 1); d.only = only; d.gate = gate;
+    d.long_list = long_list; d.long_cnt = long_cnt;
+    gs::tile_depth_sort(d, s);
 }
 
 // Pinned per-thread landing buffer + event for the forward's early counter read.
@@ -319,7 +329,6 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     hipStream_t s = (hipStream_t)stream_;
     const int P = a->P, W = a->W, H = a->H;
     const int tx = tiles_x_of(W), ty = tiles_y_of(H), T = tx * ty;
-    const int tile_bits = bits_for((uint32_t)T);
     *num_rendered = 0;
     *num_instances = 0;
     *binning_out = nullptr;
@@ -353,10 +362,10 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
         gs::launch_depth_hist(P, g.dkey, g.cnt, g.hist, s);
         if (prefix_enabled(a)) {
             C1 = phase1_cap(a, T, 0);
-            gs::launch_depth_cut(g.hist, (uint32_t)(C1 < 0xffffffffll ? C1 : 0xffffffffll), g.counters, im.ranges,
-                                 (uint32_t)T, s);
+            gs::launch_depth_cut(g.hist, (uint32_t)(C1 < 0xffffffffll ? C1 : 0xffffffffll), g.counters, im.tile_cnt,
+                                 im.tile_cnt2, (uint32_t)T, s);
         } else {  // everything in one phase: the capacity is K itself (one early sync)
-            gs::launch_depth_cut(g.hist, 0xffffffffu, g.counters, im.ranges, (uint32_t)T, s);
+            gs::launch_depth_cut(g.hist, 0xffffffffu, g.counters, im.tile_cnt, im.tile_cnt2, (uint32_t)T, s);
             uint32_t k = 0;
             HIP_OK(hipMemcpyAsync(&k, g.counters + gs::CNT_K, 4, hipMemcpyDeviceToHost, s));
             HIP_OK(hipStreamSynchronize(s));
@@ -383,35 +392,21 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     *binning_out = bbase;
     Binning b = carve_binning(bbase, C1);
     const uint32_t* E1_dev = g.counters + gs::CNT_E1;
-    const int passes = (tile_bits + 7) / 8;
-    uint32_t* s_e = (passes & 1) ? b.se1 : b.se0;
     if (C1 > 0 && P > 0) {
-        { PROF("emit"); gs::launch_emit(P, g.dkey, g.cnt, g.off, g.sp, tx, g.counters, g.first_e, g.rcnt, b.tk0, b.eg, b.ik, s); }
+        { PROF("emit"); gs::launch_emit(P, g.dkey, g.cnt, g.off, g.sp, tx, g.counters, g.first_e, g.rcnt, b.tk, b.eg, b.ik, s); }
         DBG_SYNC(a->debug, s);
-        int which;
-        { PROF("tile_sort"); which = gs::radix_sort_pairs(b.tk0, b.se0, b.tk1, b.se1, nullptr, (uint32_t)C1, 0,
-                                                          tile_bits, b.sort_tmp, s, E1_dev); }
-        (void)which;  // == passes & 1
+        { PROF("tile_bin"); bin_and_sort(b, C1, E1_dev, T, im.ranges, im.tile_cnt, nullptr, nullptr, im.long_tiles,
+                                         g.counters + gs::CNT_LONG, s); }
         DBG_SYNC(a->debug, s);
-        { PROF("ranges"); gs::launch_ranges((uint32_t)C1, E1_dev, (passes & 1) ? b.tk1 : b.tk0, im.ranges, (uint32_t)T, s); }
-        DBG_SYNC(a->debug, s);
-        {
-            PROF("tile_dsort");
-            gs::DSortArgs d;
-            d.num_tiles = T; d.ranges = im.ranges; d.s_e = s_e; d.s_tmp = (passes & 1) ? b.se0 : b.se1;
-            d.k_a = b.dk; d.k_b = (passes & 1) ? b.tk0 : b.tk1; d.ikey = b.ik; d.n_inst = (uint32_t)C1;
-            d.only = nullptr; d.gate = nullptr; d.long_list = im.long_tiles;
-            d.long_cnt = g.counters + gs::CNT_LONG;
-            gs::tile_depth_sort(d, s);
-        }
-        DBG_SYNC(a->debug, s);
+    } else {
+        HIP_OK(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * (size_t)T, s));
     }
 
     gs::RenderArgs r;
     memset(&r, 0, sizeof(r));
     r.W = W; r.H = H; r.tiles_x = tx; r.num_tiles = T;
     r.K = (uint32_t)(C1 > 0 ? C1 : 1); r.P = (uint32_t)(P > 0 ? P : 1);
-    r.ranges = im.ranges; r.s_e = s_e; r.eg = b.eg; r.sp = g.sp; r.rgbi = g.rgbi; r.bg = a->bg;
+    r.ranges = im.ranges; r.s_e = b.se; r.eg = b.eg; r.sp = g.sp; r.rgbi = g.rgbi; r.bg = a->bg;
     r.out_color = out_color; r.out_invd = out_invdepth; r.final_T = im.final_T; r.img_color = im.img_color;
     r.img_invd = im.img_invd; r.n_contrib = im.n_contrib; r.max_contrib = im.max_contrib;
     r.phase = 1; r.counters = g.counters; r.unfinished = im.unfinished; r.resume = im.resume;
@@ -447,20 +442,13 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
         gs::launch_count2(P, g.counters, g.dkey, g.sp, tx, ty, im.unfinished, im.sat, g.cnt2, s);
         gs::exclusive_scan(g.cnt2, (uint32_t)P, g.off2, g.counters + gs::CNT_K2, g.scan_tmp, s, gate);
         gs::launch_emit2(P, g.counters, g.dkey, g.sp, tx, ty, im.unfinished, im.sat, g.cnt2, g.off2, g.first_e, g.rcnt,
-                         b2.tk0, b2.eg, b2.ik, s);
-        const int which = gs::radix_sort_pairs(b2.tk0, b2.se0, b2.tk1, b2.se1, nullptr, K, 0, tile_bits,
-                                               b2.sort_tmp, s, K2_dev);
-        gs::launch_ranges(K, K2_dev, which ? b2.tk1 : b2.tk0, im.ranges2, (uint32_t)T, s);
-        gs::DSortArgs d;
-        d.num_tiles = T; d.ranges = im.ranges2; d.s_e = which ? b2.se1 : b2.se0; d.s_tmp = which ? b2.se0 : b2.se1;
-        d.k_a = b2.dk; d.k_b = which ? b2.tk0 : b2.tk1; d.ikey = b2.ik; d.n_inst = (uint32_t)K;
-        d.only = im.unfinished; d.gate = gate; d.long_list = im.long_tiles;
-        d.long_cnt = g.counters + gs::CNT_LONG2;
-        gs::tile_depth_sort(d, s);
+                         b2.tk, b2.eg, b2.ik, s);
+        bin_and_sort(b2, K, K2_dev, T, im.ranges2, im.tile_cnt2, im.unfinished, gate, im.long_tiles,
+                     g.counters + gs::CNT_LONG2, s);
         gs::RenderArgs r2 = r;
         r2.phase = 2;
         r2.K = K;
-        r2.ranges = im.ranges2; r2.ranges1 = im.ranges; r2.s_e = which ? b2.se1 : b2.se0; r2.eg = b2.eg;
+        r2.ranges = im.ranges2; r2.ranges1 = im.ranges; r2.s_e = b2.se; r2.eg = b2.eg;
         gs::launch_render_fwd(r2, s);
     }
     DBG_SYNC(a->debug, s);
@@ -484,13 +472,12 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     // the phase-1 block was carved at C1 (its capacity), the phase-2 block at K (see the forward)
     const int64_t C1 = phase1_cap(a, T, K);
     Binning b = carve_binning((void*)binning, C1);
-    const int passes = (bits_for((uint32_t)T) + 7) / 8;
-    const uint32_t* s_e = (passes & 1) ? b.se1 : b.se0;
+    const uint32_t* s_e = b.se;
     const uint32_t* s_e2 = nullptr;
     const uint32_t* eg2 = nullptr;
     if (binning2) {
         Binning b2 = carve_binning((void*)binning2, K);
-        s_e2 = (passes & 1) ? b2.se1 : b2.se0;
+        s_e2 = b2.se;
         eg2 = b2.eg;
     }
 
@@ -602,31 +589,37 @@ __global__ void k_gather_g(uint32_t K, const uint32_t* s_e, const uint32_t* eg, 
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < K) out[i] = eg[s_e[i]];
 }
+// tile id of every binned position: out[i] = t for i in ranges[t] (tiles with only[t] == 0 skipped)
+__global__ void k_tiles_of(int T, const uint2* ranges, const uint8_t* only, uint32_t* out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T || (only && !only[t])) return;
+    const uint2 r = ranges[t];
+    for (uint32_t i = r.x; i < r.y; i++) out[i] = (uint32_t)t;
+}
 }  // namespace
 
 int dg_debug_sorted_instances(const dg_raster_args* a, const void* geom, const void* binning, const void* binning2,
-                              int64_t K, uint32_t* tiles_out, uint32_t* gauss_out, int64_t* e1_out,
+                              const void* image, int64_t K, uint32_t* tiles_out, uint32_t* gauss_out, int64_t* e1_out,
                               dg_stream_t stream) {
     hipStream_t s = (hipStream_t)stream;
     const int T = tiles_x_of(a->W) * tiles_y_of(a->H);
     Geom g = carve_geom((void*)geom, a->P);
+    Image im = carve_image((void*)image, a->W, a->H);
     uint32_t hc[16];
     HIP_OK(hipMemcpyAsync(hc, g.counters, sizeof(hc), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     const uint32_t E1 = hc[gs::CNT_E1];
     *e1_out = E1;
-    const int passes = (bits_for((uint32_t)T) + 7) / 8;
     if (E1 > 0) {
         Binning b = carve_binning((void*)binning, phase1_cap(a, T, K));
-        HIP_OK(hipMemcpyAsync(tiles_out, (passes & 1) ? b.tk1 : b.tk0, 4 * (size_t)E1, hipMemcpyDeviceToDevice, s));
-        k_gather_g<<<(E1 + 255) / 256, 256, 0, s>>>(E1, (passes & 1) ? b.se1 : b.se0, b.eg, gauss_out);
+        k_gather_g<<<(E1 + 255) / 256, 256, 0, s>>>(E1, b.se, b.eg, gauss_out);
+        k_tiles_of<<<(T + 255) / 256, 256, 0, s>>>(T, im.ranges, nullptr, tiles_out);
     }
     const int64_t K2 = binning2 ? (int64_t)hc[gs::CNT_K2] : 0;
     if (binning2 && K2 > 0) {
         Binning b2 = carve_binning((void*)binning2, K);
-        HIP_OK(hipMemcpyAsync(tiles_out + E1, (passes & 1) ? b2.tk1 : b2.tk0, 4 * (size_t)K2, hipMemcpyDeviceToDevice, s));
-        k_gather_g<<<(unsigned)((K2 + 255) / 256), 256, 0, s>>>((uint32_t)K2, (passes & 1) ? b2.se1 : b2.se0, b2.eg,
-                                                                  gauss_out + E1);
+        k_gather_g<<<(unsigned)((K2 + 255) / 256), 256, 0, s>>>((uint32_t)K2, b2.se, b2.eg, gauss_out + E1);
+        k_tiles_of<<<(T + 255) / 256, 256, 0, s>>>(T, im.ranges2, im.unfinished, tiles_out + E1);
     }
     HIP_OK(hipGetLastError());
     return 0;

@@ -117,9 +117,9 @@ void launch_preprocess(const PreArgs& a, hipStream_t s);
 // hist[DH_BINS] (zeroed by the preprocess) += precise counts by depth bin
 void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_t* hist, hipStream_t s);
 // counters[K, THR, E1, CUT] from the histogram (phase-1 capacity cap); resets the per-view counters and zeroes
-// the phase-1 tile ranges (ranges[num_tiles])
-void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, uint2* ranges, uint32_t num_tiles,
-                      hipStream_t s);
+// the per-tile counters of both binning phases (tile_cnt, tile_cnt2 [num_tiles])
+void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, uint32_t* tile_cnt, uint32_t* tile_cnt2,
+                      uint32_t num_tiles, hipStream_t s);
 // phase 1: Gaussians with key < counters[CNT_THR] -> instances [0, E1) at off[g]; rcnt/first_e of those Gaussians
 // ikey[e] = the instance's depth key (read by the per-tile depth sort)
 void launch_emit(int P, const uint32_t* dkey, const uint32_t* cnt, const uint32_t* off, const float4* sp, int tiles_x,
@@ -134,8 +134,6 @@ void launch_count2(int P, const uint32_t* counters, const uint32_t* dkey, const 
 void launch_emit2(int P, const uint32_t* counters, const uint32_t* dkey, const float4* sp, int tiles_x, int tiles_y,
                   const uint8_t* unfinished, const uint32_t* sat, const uint32_t* cnt2, const uint32_t* off2,
                   uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey, uint32_t* eg, uint32_t* ikey, hipStream_t s);
-void launch_ranges(uint32_t Kcap, const uint32_t* n_dev, const uint32_t* keys, uint2* ranges, uint32_t num_tiles,
-                   hipStream_t s);
 void launch_render_fwd(const RenderArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);
 void launch_filter(const PreArgs& a, hipStream_t s);

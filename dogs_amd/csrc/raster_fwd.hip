@@ -2,13 +2,13 @@
 //
 // Pipeline (DESIGN.md "Forward"):
 //   k_preprocess   per Gaussian: EWA projection, SH->RGB, conic, radius, rect and the *precise* per-tile
-//                  cull count (rasterizer_impl.cu:57-190 semantics), depth sort key
-//   depth sort     stable radix sort of (depth bits, index) over Gaussians           (sortscan.hip)
-//   scan           exclusive scan of the precise counts in depth order -> emission offsets
-//   k_emit         per Gaussian in depth order: one (tile id, emission index) instance per kept tile
-//   tile sort      stable radix sort by tile id only; input order is (depth, index) so the result is the
-//                  reference's (tile, depth bits, index) order, bit for bit
-//   k_ranges       per-tile [start, end)
+//                  cull count (rasterizer_impl.cu:57-190 semantics), depth key
+//   k_depth_hist   instance counts over coarse depth bins;  k_depth_cut: the depth threshold of the phase-1
+//                  prefix (instances of Gaussians nearer than it are a prefix of every tile's list)
+//   scan           exclusive scan of the precise counts of the prefix Gaussians (index order) -> emission offsets
+//   k_emit         per prefix Gaussian: one (tile id, emission index, depth key) instance per kept tile
+//   tile binning   atomic counting sort by tile + per-tile sort into (depth bits, index) order (sortscan.hip):
+//                  the reference's (tile, depth bits, index) order, bit for bit
 //   k_render_fwd   one wave per 16x16 tile, 4 pixels per lane as two row pairs evaluated with packed fp32
 //                  (v_pk_*_f32); a 64-splat batch is staged in wave-private LDS and read back with broadcast
 //                  ds_read_b128; splats that cannot reach a quadrant pair skip it; wave-uniform early exit.
@@ -344,15 +344,15 @@ __global__ void __launch_bounds__(DH_THREADS) k_depth_hist(int P, const uint32_t
 
 // One block: K = total instances, and the largest bin prefix [0, b] whose instances fit `cap`; thr = the first
 // key of bin b + 1 (S = {key < thr}).  No cut (thr = all visible) when K <= cap.  Also resets the per-view
-// counters and the phase-1 tile ranges.
+// counters and the per-tile counters of both binning phases.
 __global__ void __launch_bounds__(1024) k_depth_cut(const uint32_t* __restrict__ hist, uint32_t cap,
-                                                    uint32_t* __restrict__ counters, uint2* __restrict__ ranges,
-                                                    uint32_t num_tiles) {
+                                                    uint32_t* __restrict__ counters, uint32_t* __restrict__ tile_cnt,
+                                                    uint32_t* __restrict__ tile_cnt2, uint32_t num_tiles) {
     __shared__ uint32_t s_w[16];
     __shared__ int s_best;
     constexpr int PER = DH_BINS / 1024;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    for (uint32_t i = t; i < num_tiles; i += 1024) ranges[i] = make_uint2(0u, 0u);
+    for (uint32_t i = t; i < num_tiles; i += 1024) { tile_cnt[i] = 0u; tile_cnt2[i] = 0u; }
     if (t == 0) s_best = -1;
     uint32_t v[PER], loc = 0;
 #pragma unroll
@@ -568,19 +568,6 @@ __global__ void __launch_bounds__(256) k_phase2(int P, const uint32_t* __restric
     if (!EMIT && g < P) cnt2[g] = s_cnt[w][lane];
 }
 
-// identifyTileRanges over the sorted (all-valid) tile keys
-__global__ void __launch_bounds__(256) k_ranges(uint32_t Kcap, const uint32_t* __restrict__ n_dev,
-                                                const uint32_t* __restrict__ keys, uint2* __restrict__ ranges,
-                                                uint32_t num_tiles) {
-    const uint32_t K = n_dev ? min(*n_dev, Kcap) : Kcap;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < K; i += gridDim.x * blockDim.x) {
-        const uint32_t t = keys[i];
-        if (t >= num_tiles) continue;
-        if (i == 0 || keys[i - 1] != t) ranges[t].x = i;
-        if (i == K - 1 || keys[i + 1] != t) ranges[t].y = i + 1;
-    }
-}
-
 __device__ __forceinline__ float bcast(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
@@ -793,9 +780,9 @@ void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_
     const int per = DH_THREADS * DH_ITEMS;
     if (P > 0) k_depth_hist<<<(P + per - 1) / per, DH_THREADS, 0, s>>>(P, dkey, cnt, hist);
 }
-void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, uint2* ranges, uint32_t num_tiles,
-                      hipStream_t s) {
-    k_depth_cut<<<1, 1024, 0, s>>>(hist, cap, counters, ranges, num_tiles);
+void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, uint32_t* tile_cnt, uint32_t* tile_cnt2,
+                      uint32_t num_tiles, hipStream_t s) {
+    k_depth_cut<<<1, 1024, 0, s>>>(hist, cap, counters, tile_cnt, tile_cnt2, num_tiles);
 }
 void launch_emit(int P, const uint32_t* dkey, const uint32_t* cnt, const uint32_t* off, const float4* sp, int tiles_x,
                  const uint32_t* counters, uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey, uint32_t* eg,
@@ -822,11 +809,6 @@ void launch_emit2(int P, const uint32_t* counters, const uint32_t* dkey, const f
         k_phase2<true><<<(P + 255) / 256, 256, 0, s>>>(P, counters, dkey, sp, tiles_x, tiles_y, unfinished, sat,
                                                         const_cast<uint32_t*>(cnt2), off2, first_e, rcnt, tilekey, eg,
                                                         ikey);
-}
-void launch_ranges(uint32_t Kcap, const uint32_t* n_dev, const uint32_t* keys, uint2* ranges, uint32_t num_tiles,
-                   hipStream_t s) {
-    const uint32_t blocks = (Kcap + 255) / 256;
-    if (Kcap > 0) k_ranges<<<blocks < 2048u ? blocks : 2048u, 256, 0, s>>>(Kcap, n_dev, keys, ranges, num_tiles);
 }
 void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
     if (a.num_tiles <= 0) return;

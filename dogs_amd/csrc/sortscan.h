@@ -22,16 +22,24 @@ size_t scan_temp_bytes(uint32_t n);
 void exclusive_scan(const uint32_t* in, uint32_t n, uint32_t* out, uint32_t* total, void* temp, hipStream_t stream,
                     const uint32_t* gate = nullptr, const uint32_t* lt_keys = nullptr, const uint32_t* lt_thr = nullptr);
 
-// Per-tile stable sort of instance lists by the depth key of their Gaussian (sortscan.hip k_tile_dsort):
-// s_e[ranges[t].x .. ranges[t].y) is reordered in place by ikey[v]; ties keep their input order.
+// Counting sort of n (device-side count n_dev, capacity ncap) instances by tile: slot[i] = arrival order of
+// instance i in its tile (atomics), ranges[t] = [start, end) of every tile (all num_tiles written),
+// s_e[ranges[tk[i]].x + slot[i]] = i.  tile_cnt[num_tiles] must be zero.  The order inside a tile is arbitrary
+// until tile_depth_sort.  gate (optional, device): nothing when *gate == 0.
+void tile_bin(uint32_t ncap, const uint32_t* n_dev, const uint32_t* tk, uint32_t* slot, uint32_t* tile_cnt,
+              uint32_t num_tiles, uint2* ranges, uint32_t* s_e, hipStream_t stream, const uint32_t* gate = nullptr);
+
+// Per-tile sort of instance lists into (depth key, Gaussian index) order (sortscan.hip k_tile_dsort):
+// s_e[ranges[t].x .. ranges[t].y) is reordered in place by (ikey[v], eg[v]), whatever its input order.
 struct DSortArgs {
     int num_tiles;
     const uint2* ranges;
-    uint32_t* s_e;              // tile-sorted instance list (values are indices into eg)
+    uint32_t* s_e;              // tile-binned instance list (values are instance indices)
     uint32_t* s_tmp;            // scratch values, same indexing as s_e (long lists)
     uint32_t *k_a, *k_b;        // scratch keys, same indexing as s_e (long lists)
     const uint32_t* ikey;       // instance -> 32-bit depth key of its Gaussian
-    uint32_t n_inst;            // bound of ikey
+    const uint32_t* eg;         // instance -> Gaussian index (tie order)
+    uint32_t n_inst;            // bound of ikey / eg
     const uint8_t* only;        // optional: sort only tiles t with only[t] != 0
     const uint32_t* gate;       // optional (device): nothing when *gate == 0
     uint32_t* long_list;        // [num_tiles] queue of tiles longer than the per-wave capacity

@@ -368,20 +368,83 @@ void exclusive_scan(const uint32_t* in, uint32_t n, uint32_t* out, uint32_t* tot
 }
 
 
-// ---------------- per-tile depth sort (segmented, stable) ----------------
-// Each tile's instance list [ranges[t].x, ranges[t].y) of s_e arrives in index order (emission order, stably
-// sorted by tile); it is sorted in place by the 32-bit depth key dkey[eg[v]] of its Gaussian, stably, so ties
-// keep the index order: the reference's (tile, depth bits, index) order, tile by tile.
-//   k_tile_dsort       one wave per tile, lists up to DS_WAVE_MAX: items in registers (16 per lane), LSD radix
+// ---------------- binning by tile: atomic counting sort + exact per-tile order ----------------
+// The instances of a phase are binned by tile with a counting sort (k_tile_count: per-instance slot from an
+// atomic per-tile counter; k_tile_offsets: one-block scan -> ranges; k_tile_scatter).  The order inside a tile
+// is then whatever the atomics produced; k_tile_dsort puts every tile's list into the reference's exact
+// (depth bits, Gaussian index) order -- a total order, so the result does not depend on the atomics.
+//   k_tile_dsort       one wave per tile, lists up to DS_WAVE_MAX: items in registers (8 per lane), LSD radix
 //                      over the tile's key range (keys relative to the tile minimum, 8-bit digits, only as many
-//                      passes as the range needs), wave-level peer-mask ranking, LDS scatter.
-//   k_tile_dsort_long  longer lists (queued by k_tile_dsort): one block per tile, LSD radix through global
-//                      scratch in 256-item chunks.
-constexpr int DS_WAVE_MAX = 1024;
+//                      passes as the range needs), wave-level peer-mask ranking, LDS scatter.  Runs of equal
+//                      depth keys are put in Gaussian index order by odd-even transposition between neighbours.
+//   k_tile_dsort_long  longer lists (queued by k_tile_dsort): one block per tile, LSD radix through global scratch
+//                      in 256-item chunks; with equal keys it sorts by Gaussian index first and then, stably, by key.
+__global__ void __launch_bounds__(256) k_tile_count(uint32_t ncap, const uint32_t* __restrict__ n_dev,
+                                                    const uint32_t* __restrict__ tk, uint32_t* __restrict__ slot,
+                                                    uint32_t* __restrict__ tile_cnt, const uint32_t* __restrict__ gate) {
+    if (gate && *gate == 0u) return;
+    const uint32_t n = eff_n(ncap, n_dev);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        slot[i] = atomicAdd(&tile_cnt[tk[i]], 1u);
+}
+
+__global__ void __launch_bounds__(1024) k_tile_offsets(const uint32_t* __restrict__ tile_cnt, uint32_t num_tiles,
+                                                       uint2* __restrict__ ranges, const uint32_t* __restrict__ gate) {
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_carry;
+    if (gate && *gate == 0u) return;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (t == 0) s_carry = 0u;
+    __syncthreads();
+    for (uint32_t b = 0; b < num_tiles; b += 1024) {
+        const uint32_t i = b + t;
+        const uint32_t v = i < num_tiles ? tile_cnt[i] : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_w[w] = x;
+        __syncthreads();
+        uint32_t off = s_carry, tot = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) { if (k < w) off += s_w[k]; tot += s_w[k]; }
+        const uint32_t ex = off + x - v;
+        if (i < num_tiles) ranges[i] = make_uint2(ex, ex + v);
+        __syncthreads();
+        if (t == 0) s_carry += tot;
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(256) k_tile_scatter(uint32_t ncap, const uint32_t* __restrict__ n_dev,
+                                                      const uint32_t* __restrict__ tk, const uint32_t* __restrict__ slot,
+                                                      const uint2* __restrict__ ranges, uint32_t* __restrict__ s_e,
+                                                      const uint32_t* __restrict__ gate) {
+    if (gate && *gate == 0u) return;
+    const uint32_t n = eff_n(ncap, n_dev);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        s_e[ranges[tk[i]].x + slot[i]] = i;
+}
+
+void tile_bin(uint32_t ncap, const uint32_t* n_dev, const uint32_t* tk, uint32_t* slot, uint32_t* tile_cnt,
+              uint32_t num_tiles, uint2* ranges, uint32_t* s_e, hipStream_t stream, const uint32_t* gate) {
+    if (ncap == 0 || num_tiles == 0) return;
+    const uint32_t blocks = (ncap + 255) / 256 < 2048u ? (ncap + 255) / 256 : 2048u;
+    k_tile_count<<<blocks, 256, 0, stream>>>(ncap, n_dev, tk, slot, tile_cnt, gate);
+    k_tile_offsets<<<1, 1024, 0, stream>>>(tile_cnt, num_tiles, ranges, gate);
+    k_tile_scatter<<<blocks, 256, 0, stream>>>(ncap, n_dev, tk, slot, ranges, s_e, gate);
+}
+
+constexpr int DS_WAVE_MAX = 512;
 constexpr int DS_ROWS = DS_WAVE_MAX / 64;
 
 __device__ __forceinline__ uint32_t ds_key(const DSortArgs& a, uint32_t v) {
     return a.ikey[v < a.n_inst ? v : a.n_inst - 1];
+}
+__device__ __forceinline__ uint32_t ds_gid(const DSortArgs& a, uint32_t v) {
+    return a.eg[v < a.n_inst ? v : a.n_inst - 1];
 }
 
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
@@ -394,60 +457,13 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
     for (int o = 32; o > 0; o >>= 1) { const uint32_t y = __shfl_xor(x, o); x = y > x ? y : x; }
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
 }
+__device__ __forceinline__ int passes_for(uint32_t range) { return range ? (32 - __clz((int)range) + 7) >> 3 : 0; }
 
-__global__ void __launch_bounds__(256) k_tile_dsort(DSortArgs a) {
-    __shared__ uint32_t s_cnt[4][RS_RADIX];
-    __shared__ uint32_t s_k[4][DS_WAVE_MAX];
-    __shared__ uint32_t s_v[4][DS_WAVE_MAX];
-    if (a.gate && *a.gate == 0u) return;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * 4 + w;
-    if (tile >= a.num_tiles) return;
-    if (a.only && !a.only[tile]) return;
-    const uint2 rg = a.ranges[tile];
-    const int n = (int)(rg.y - rg.x);
-    if (n <= 1) return;
-    if (n > DS_WAVE_MAX) {
-        if (lane == 0) a.long_list[atomicAdd(a.long_cnt, 1u)] = (uint32_t)tile;
-        return;
-    }
-    uint32_t* se = a.s_e + rg.x;
-    const int R = (n + 63) >> 6;
-    uint32_t k[DS_ROWS], v[DS_ROWS], rank[DS_ROWS];
-    // all loads of a stage are issued before any use: one latency round per stage (list, eg, dkey)
-#pragma unroll
-    for (int r = 0; r < DS_ROWS; r++) {
-        const int i = r * 64 + lane;
-        v[r] = (r < R && i < n) ? se[i] : 0u;
-    }
-#pragma unroll
-    for (int r = 0; r < DS_ROWS; r++) {
-        const int i = r * 64 + lane;
-        k[r] = (r < R && i < n) ? ds_key(a, v[r]) : 0u;
-    }
-    uint32_t kmin = 0xffffffffu, kmax = 0u;
-#pragma unroll
-    for (int r = 0; r < DS_ROWS; r++) {
-        const int i = r * 64 + lane;
-        if (r < R && i < n) {
-            kmin = k[r] < kmin ? k[r] : kmin;
-            kmax = k[r] > kmax ? k[r] : kmax;
-        }
-    }
-    kmin = wave_min_u32(kmin);
-    kmax = wave_max_u32(kmax);
-    if (kmin == kmax) return;  // one key: the index order is already the sorted order
-    const uint32_t range = kmax - kmin;
-    const int passes = (32 - __clz((int)range) + 7) >> 3;
-    // padding slots (i >= n) sort last: all-ones relative key, and they come last in the input
-#pragma unroll
-    for (int r = 0; r < DS_ROWS; r++) {
-        const int i = r * 64 + lane;
-        k[r] = (i < n) ? k[r] - kmin : 0xffffffffu;
-    }
-    uint32_t* cnt = s_cnt[w];
-    uint32_t* lk = s_k[w];
-    uint32_t* lv = s_v[w];
+// Stable in-wave LSD radix sort of (k, v) over the R = ceil(n/64) register rows, digits of k below 8*passes.
+// Items i >= n must carry k = 0xffffffff (they stay last).
+__device__ __forceinline__ void wave_radix(uint32_t (&k)[DS_ROWS], uint32_t (&v)[DS_ROWS], int R, int passes,
+                                           uint32_t* cnt, uint32_t* lk, uint32_t* lv, int lane) {
+    uint32_t rank[DS_ROWS];
     const uint64_t lt = lanemask_lt();
     for (int p = 0; p < passes; p++) {
         const int shift = 8 * p;
@@ -496,6 +512,125 @@ __global__ void __launch_bounds__(256) k_tile_dsort(DSortArgs a) {
         }
         __builtin_amdgcn_wave_barrier();
     }
+}
+
+// Relative sort keys of the wave's items (key(v) - min over the list; 0xffffffff padding); returns the range.
+template <typename KeyFn>
+__device__ __forceinline__ uint32_t wave_rel_keys(uint32_t (&k)[DS_ROWS], const uint32_t (&v)[DS_ROWS], int R, int n,
+                                                  int lane, KeyFn&& key) {
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        const int i = r * 64 + lane;
+        k[r] = (r < R && i < n) ? key(v[r]) : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        const int i = r * 64 + lane;
+        if (r < R && i < n) {
+            kmin = k[r] < kmin ? k[r] : kmin;
+            kmax = k[r] > kmax ? k[r] : kmax;
+        }
+    }
+    kmin = wave_min_u32(kmin);
+    kmax = wave_max_u32(kmax);
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        const int i = r * 64 + lane;
+        k[r] = (i < n) ? k[r] - kmin : 0xffffffffu;
+    }
+    return kmax - kmin;
+}
+
+__global__ void __launch_bounds__(256) k_tile_dsort(DSortArgs a) {
+    __shared__ uint32_t s_cnt[4][RS_RADIX];
+    __shared__ uint32_t s_k[4][DS_WAVE_MAX];
+    __shared__ uint32_t s_v[4][DS_WAVE_MAX];
+    if (a.gate && *a.gate == 0u) return;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tile = blockIdx.x * 4 + w;
+    if (tile >= a.num_tiles) return;
+    if (a.only && !a.only[tile]) return;
+    const uint2 rg = a.ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    if (n <= 1) return;
+    if (n > DS_WAVE_MAX) {
+        if (lane == 0) a.long_list[atomicAdd(a.long_cnt, 1u)] = (uint32_t)tile;
+        return;
+    }
+    uint32_t* se = a.s_e + rg.x;
+    const int R = (n + 63) >> 6;
+    uint32_t k[DS_ROWS], v[DS_ROWS];
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        const int i = r * 64 + lane;
+        v[r] = (r < R && i < n) ? se[i] : 0u;
+    }
+    const uint32_t range = wave_rel_keys(k, v, R, n, lane, [&](uint32_t x) { return ds_key(a, x); });
+#ifndef DG_DSORT_NOSORT
+    wave_radix(k, v, R, passes_for(range), s_cnt[w], s_k[w], s_v[w], lane);
+#endif
+    // Equal depth keys (i >= n carry 0xffffffff and never match a real relative key) must end up in Gaussian
+    // index order; the counting sort left them in arrival order.  They sit next to each other after the sort, so
+    // odd-even transposition between equal-key neighbours fixes them (one round per element of the longest run).
+    bool tie = false;
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        if (r < R) {
+            uint32_t prev = __shfl_up(k[r], 1);
+            if (lane == 0) prev = r > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)k[r > 0 ? r - 1 : 0], 63) : ~k[r];
+            const int i = r * 64 + lane;
+            tie |= (i < n) && prev == k[r];
+        }
+    }
+    if (__any(tie)) {
+        uint32_t gid[DS_ROWS];
+#pragma unroll
+        for (int r = 0; r < DS_ROWS; r++) {
+            const int i = r * 64 + lane;
+            gid[r] = (r < R && i < n) ? ds_gid(a, v[r]) : 0xffffffffu;
+        }
+        for (int round = 0; round < DS_WAVE_MAX; round++) {
+            bool changed = false;
+#pragma unroll
+            for (int par = 0; par < 2; par++) {
+                uint32_t nv[DS_ROWS], ng[DS_ROWS];
+#pragma unroll
+                for (int r = 0; r < DS_ROWS; r++) {
+                    nv[r] = v[r]; ng[r] = gid[r];
+                    if (r >= R) continue;
+                    const int i = r * 64 + lane;
+                    // right neighbour (i + 1) and left neighbour (i - 1)
+                    uint32_t kr = __shfl_down(k[r], 1), vr = __shfl_down(v[r], 1), gr = __shfl_down(gid[r], 1);
+                    uint32_t kl = __shfl_up(k[r], 1), vl = __shfl_up(v[r], 1), gl = __shfl_up(gid[r], 1);
+                    if (r + 1 < DS_ROWS) {
+                        const int rn = r + 1 < DS_ROWS ? r + 1 : r;
+                        const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)k[rn], 0);
+                        const uint32_t v0 = (uint32_t)__builtin_amdgcn_readlane((int)v[rn], 0);
+                        const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)gid[rn], 0);
+                        if (lane == 63) { kr = k0; vr = v0; gr = g0; }
+                    }
+                    if (r > 0) {
+                        const int rp = r > 0 ? r - 1 : 0;
+                        const uint32_t k63 = (uint32_t)__builtin_amdgcn_readlane((int)k[rp], 63);
+                        const uint32_t v63 = (uint32_t)__builtin_amdgcn_readlane((int)v[rp], 63);
+                        const uint32_t g63 = (uint32_t)__builtin_amdgcn_readlane((int)gid[rp], 63);
+                        if (lane == 0) { kl = k63; vl = v63; gl = g63; }
+                    }
+                    if (i < n) {
+                        if ((i & 1) == par) {  // left element of the pair (i, i + 1)
+                            if (i + 1 < n && kr == k[r] && gr < gid[r]) { nv[r] = vr; ng[r] = gr; changed = true; }
+                        } else if (i > 0) {    // right element of the pair (i - 1, i)
+                            if (kl == k[r] && gid[r] < gl) { nv[r] = vl; ng[r] = gl; changed = true; }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < DS_ROWS; r++) { v[r] = nv[r]; gid[r] = ng[r]; }
+            }
+            if (!__any(changed)) break;
+        }
+    }
 #pragma unroll
     for (int r = 0; r < DS_ROWS; r++) {
         const int i = r * 64 + lane;
@@ -503,90 +638,110 @@ __global__ void __launch_bounds__(256) k_tile_dsort(DSortArgs a) {
     }
 }
 
-// Long lists: one block per queued tile; keys gathered once into scratch, then LSD passes ping-pong between
-// (keys, s_e) and (keys2, tmp) in 256-item chunks (per-wave peer masks + per-wave digit counts give the stable
-// in-chunk rank).  Grid-stride over the queue; the queue length is device-side (no host sync).
+// One stable LSD step of the long-list sort by the 256-thread block: (key(v) - kmin) digits, (keys, vals) ping-pong
+// through global scratch in 256-item chunks.  `key` maps a value to its sort key.  Result in va.
+template <typename KeyFn>
+__device__ void block_radix_global(uint32_t*& va, uint32_t*& vb, uint32_t* ka, uint32_t* kb, uint32_t n,
+                                   KeyFn&& key, uint32_t* s_base, uint32_t (*s_wh)[RS_RADIX], uint32_t (*s_red)[RS_WAVES]) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint64_t lt = lanemask_lt();
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+    for (uint32_t i = t; i < n; i += 256) {
+        const uint32_t kk = key(va[i]);
+        ka[i] = kk;
+        kmin = kk < kmin ? kk : kmin;
+        kmax = kk > kmax ? kk : kmax;
+    }
+    kmin = wave_min_u32(kmin);
+    kmax = wave_max_u32(kmax);
+    __syncthreads();
+    if (lane == 0) { s_red[0][w] = kmin; s_red[1][w] = kmax; }
+    __syncthreads();
+    kmin = s_red[0][0]; kmax = s_red[1][0];
+    for (int q = 1; q < RS_WAVES; q++) {
+        kmin = s_red[0][q] < kmin ? s_red[0][q] : kmin;
+        kmax = s_red[1][q] > kmax ? s_red[1][q] : kmax;
+    }
+    const int passes = passes_for(kmax - kmin);
+    for (int p = 0; p < passes; p++) {
+        const int shift = 8 * p;
+        __syncthreads();
+        s_base[t] = 0u;
+        __syncthreads();
+        for (uint32_t i = t; i < n; i += 256) atomicAdd(&s_base[((ka[i] - kmin) >> shift) & 0xffu], 1u);
+        __syncthreads();
+        {  // exclusive scan of the digit counts (thread t = digit t)
+            const uint32_t c = s_base[t];
+            uint32_t x = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o);
+                if (lane >= o) x += y;
+            }
+            if (lane == 63) s_red[0][w] = x;
+            __syncthreads();
+            uint32_t off = 0;
+            for (int q = 0; q < w; q++) off += s_red[0][q];
+            s_base[t] = off + x - c;
+        }
+        __syncthreads();
+        for (uint32_t c0 = 0; c0 < n; c0 += 256) {
+            const uint32_t i = c0 + t;
+            const bool act = i < n;
+            const uint32_t kk = act ? ka[i] : 0u;
+            const uint32_t val = act ? va[i] : 0u;
+            const uint32_t d = ((kk - kmin) >> shift) & 0xffu;
+            const uint64_t m = peer_mask(d, act);
+            const uint32_t before = (uint32_t)__popcll(m & lt);
+#pragma unroll
+            for (int q = 0; q < RS_WAVES; q++) s_wh[q][t] = 0u;
+            __syncthreads();
+            if (act && before == 0) s_wh[w][d] = (uint32_t)__popcll(m);
+            __syncthreads();
+            if (act) {
+                uint32_t pos = s_base[d] + before;
+                for (int q = 0; q < w; q++) pos += s_wh[q][d];
+                kb[pos] = kk;
+                vb[pos] = val;
+            }
+            __syncthreads();
+            s_base[t] += s_wh[0][t] + s_wh[1][t] + s_wh[2][t] + s_wh[3][t];
+            __syncthreads();
+        }
+        uint32_t* tk = ka; ka = kb; kb = tk;
+        uint32_t* tv = va; va = vb; vb = tv;
+    }
+    __syncthreads();
+}
+
+// Long lists: one block per queued tile.  Grid-stride over the queue; its length is device-side (no host sync).
 __global__ void __launch_bounds__(256) k_tile_dsort_long(DSortArgs a) {
     __shared__ uint32_t s_base[RS_RADIX];
     __shared__ uint32_t s_wh[RS_WAVES][RS_RADIX];
     __shared__ uint32_t s_red[2][RS_WAVES];
+    __shared__ int s_tie;
     if (a.gate && *a.gate == 0u) return;
     const uint32_t nl = *a.long_cnt;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const uint64_t lt = lanemask_lt();
+    const int t = threadIdx.x;
     for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
         const int tile = (int)a.long_list[li];
         const uint2 rg = a.ranges[tile];
         const uint32_t n = rg.y - rg.x;
-        uint32_t *va = a.s_e + rg.x, *vb = a.s_tmp + rg.x, *ka = a.k_a + rg.x, *kb = a.k_b + rg.x;
-        uint32_t kmin = 0xffffffffu, kmax = 0u;
-        for (uint32_t i = t; i < n; i += 256) {
-            const uint32_t key = ds_key(a, va[i]);
-            ka[i] = key;
-            kmin = key < kmin ? key : kmin;
-            kmax = key > kmax ? key : kmax;
-        }
-        kmin = wave_min_u32(kmin);
-        kmax = wave_max_u32(kmax);
-        if (lane == 0) { s_red[0][w] = kmin; s_red[1][w] = kmax; }
+        uint32_t *va = a.s_e + rg.x, *vb = a.s_tmp + rg.x;
+        auto dkey = [&](uint32_t x) { return ds_key(a, x); };
+        block_radix_global(va, vb, a.k_a + rg.x, a.k_b + rg.x, n, dkey, s_base, s_wh, s_red);
+        if (t == 0) s_tie = 0;
         __syncthreads();
-        kmin = s_red[0][0]; kmax = s_red[1][0];
-        for (int q = 1; q < RS_WAVES; q++) {
-            kmin = s_red[0][q] < kmin ? s_red[0][q] : kmin;
-            kmax = s_red[1][q] > kmax ? s_red[1][q] : kmax;
+        for (uint32_t i = t + 1; i < n; i += 256)
+            if (ds_key(a, va[i]) == ds_key(a, va[i - 1])) s_tie = 1;
+        __syncthreads();
+        if (s_tie) {  // rare: order by Gaussian index first, then stably by key
+            block_radix_global(va, vb, a.k_a + rg.x, a.k_b + rg.x, n, [&](uint32_t x) { return ds_gid(a, x); }, s_base,
+                               s_wh, s_red);
+            block_radix_global(va, vb, a.k_a + rg.x, a.k_b + rg.x, n, dkey, s_base, s_wh, s_red);
         }
-        const uint32_t range = kmax - kmin;
-        const int passes = range ? (32 - __clz((int)range) + 7) >> 3 : 0;
-        for (int p = 0; p < passes; p++) {
-            const int shift = 8 * p;
-            s_base[t] = 0u;
-            __syncthreads();
-            for (uint32_t i = t; i < n; i += 256) atomicAdd(&s_base[((ka[i] - kmin) >> shift) & 0xffu], 1u);
-            __syncthreads();
-            {  // exclusive scan of the digit counts (thread t = digit t)
-                const uint32_t c = s_base[t];
-                uint32_t x = c;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const uint32_t y = __shfl_up(x, o);
-                    if (lane >= o) x += y;
-                }
-                if (lane == 63) s_red[0][w] = x;
-                __syncthreads();
-                uint32_t off = 0;
-                for (int q = 0; q < w; q++) off += s_red[0][q];
-                s_base[t] = off + x - c;
-            }
-            __syncthreads();
-            for (uint32_t c0 = 0; c0 < n; c0 += 256) {
-                const uint32_t i = c0 + t;
-                const bool act = i < n;
-                const uint32_t key = act ? ka[i] : 0u;
-                const uint32_t val = act ? va[i] : 0u;
-                const uint32_t d = ((key - kmin) >> shift) & 0xffu;
-                const uint64_t m = peer_mask(d, act);
-                const uint32_t before = (uint32_t)__popcll(m & lt);
-#pragma unroll
-                for (int q = 0; q < RS_WAVES; q++) s_wh[q][t] = 0u;
-                __syncthreads();
-                if (act && before == 0) s_wh[w][d] = (uint32_t)__popcll(m);
-                __syncthreads();
-                if (act) {
-                    uint32_t pos = s_base[d] + before;
-                    for (int q = 0; q < w; q++) pos += s_wh[q][d];
-                    kb[pos] = key;
-                    vb[pos] = val;
-                }
-                __syncthreads();
-                s_base[t] += s_wh[0][t] + s_wh[1][t] + s_wh[2][t] + s_wh[3][t];
-                __syncthreads();
-            }
-            uint32_t* tk = ka; ka = kb; kb = tk;
-            uint32_t* tv = va; va = vb; vb = tv;
-            __syncthreads();
-        }
-        if (passes & 1)  // result in the scratch values: copy back into s_e
-            for (uint32_t i = t; i < n; i += 256) vb[i] = va[i];
+        if (va != a.s_e + rg.x)  // result in the scratch values: copy back into s_e
+            for (uint32_t i = t; i < n; i += 256) a.s_e[rg.x + i] = va[i];
         __syncthreads();
     }
 }

@@ -119,3 +119,33 @@ def test_backward_huge_splats(oracle, hip_device, prefix_policy):
     s.scales[big] = s.scales[big] * 40.0
     st = _backward_vs_oracle(s, W, H, 3, (0.3, 0.2, 0.1), False, hip_device, seed=5)
     assert int(st.geom()["tiles_touched"].max()) > 256
+
+
+@pytest.mark.parametrize("n,W,H,mode", [(3000, 256, 192, "clones"), (600, 64, 48, "planar"),
+                                        (20000, 128, 96, "dense-clones")])
+@pytest.mark.parametrize("prefix", [0, 2, -1], ids=["prefix-default", "prefix-2-per-tile", "no-prefix"])
+def test_equal_depth_order(oracle, hip_device, n, W, H, mode, prefix):
+    """Equal view depths (cloned Gaussians, a camera-facing plane) must come out in Gaussian index order, as the
+    reference's stable radix sort leaves them; 'dense' lists exceed the per-wave sort capacity (block kernel)."""
+    from dogs_amd.diff_gaussian_rasterization import _C
+    s = small_scene(n, W, H, seed=21)
+    if mode in ("clones", "dense-clones"):  # second half: copies of the first half's depth, shifted in x/y
+        h = n // 2
+        s.means3D[h:2 * h, 2] = s.means3D[:h, 2]
+        s.means3D[h:2 * h, :2] = s.means3D[:h, :2] * 0.97
+    else:  # every Gaussian at one depth
+        s.means3D[:, 2] = float(s.means3D[0, 2])
+    old = _C.set_prefix_per_tile(prefix)
+    try:
+        col_o, radii_o, inv_o, st = oracle_forward(oracle, s, (0.1, 0.2, 0.3))
+        out = hip_forward(s, (0.1, 0.2, 0.3), hip_device)
+        t_o, i_o, _ = st.sorted_list()
+        t_h, i_h, e1 = hip_sorted_instances(out, W, H, hip_device, n)
+        full = per_tile_lists(t_o, i_o, len(t_o))
+        got = per_tile_lists(t_h, i_h, e1)
+        assert max(len(v) for v in full.values()) > (512 if mode == "dense-clones" else 0)
+        for t, lst in got.items():
+            assert lst == full[t][:len(lst)], f"tile {t}: not a prefix of the reference list"
+        assert psnr(out[2].cpu().numpy(), col_o) > 80.0
+    finally:
+        _C.set_prefix_per_tile(old)
