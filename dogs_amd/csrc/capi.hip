@@ -86,9 +86,10 @@ struct Geom {
     uint32_t* counters;  // CNT_* (raster.h)
     float4* sp;  // 2 per Gaussian (raster.h)
     float4* rgbi;
-    uint32_t *dkey, *cnt, *first_e, *off;
-    uint32_t *rcnt, *cnt2, *off2;  // records per Gaussian; phase-2 counts / offsets (index order)
-    uint32_t* hist;                // [DH_BINS] depth histogram of the prefix cut
+    uint32_t *dkey, *cnt, *first_e;  // depth key, tile-rect area, first instance
+    uint32_t* rcnt;                  // instances (= records of the backward) per Gaussian
+    uint32_t* hist;                  // [DH_BINS] depth histogram of the prefix cut
+    uint32_t* wtot;                  // [bin_waves(P)] per-wave instance totals of the binning walk
     void* scan_tmp;
     size_t bytes;
 };
@@ -102,12 +103,10 @@ Geom carve_geom(void* base, int P) {
     g.dkey = c.take<uint32_t>(n);
     g.cnt = c.take<uint32_t>(n);
     g.first_e = c.take<uint32_t>(n);
-    g.off = c.take<uint32_t>(n);
     g.rcnt = c.take<uint32_t>(n);
-    g.cnt2 = c.take<uint32_t>(n);
-    g.off2 = c.take<uint32_t>(n);
     g.hist = c.take<uint32_t>(gs::DH_BINS);
-    g.scan_tmp = c.take<char>(gs::scan_temp_bytes((uint32_t)n));
+    g.wtot = c.take<uint32_t>((size_t)gs::bin_waves(P > 0 ? P : 1));
+    g.scan_tmp = c.take<char>(gs::bin_scan_temp_bytes(P > 0 ? P : 1));
     g.bytes = c.off;
     return g;
 }
@@ -171,6 +170,13 @@ Binning carve_binning(void* base, int64_t K) {
     b.bytes = c.off;
     return b;
 }
+gs::BinArgs bin_args(const Geom& g, const Image& im, int P, int tx, uint32_t cap, const Binning& b) {
+    gs::BinArgs a;
+    a.P = P; a.tiles_x = tx; a.dkey = g.dkey; a.sp = g.sp; a.counters = g.counters; a.unf = im.unfinished;
+    a.sat = im.sat; a.wtot = g.wtot; a.cap = cap; a.first_e = g.first_e; a.rcnt = g.rcnt;
+    a.tilekey = b.tk; a.eg = b.eg; a.ikey = b.ik;
+    return a;
+}
 void bin_and_sort(const Binning& b, int64_t cap, const uint32_t* n_dev, int T, uint2* ranges, uint32_t* tile_cnt,
                   const uint8_t* only, const uint32_t* gate, uint32_t* long_list, uint32_t* long_cnt, hipStream_t s) {
     gs::tile_bin((uint32_t)cap, n_dev, b.tk, b.slot, tile_cnt, (uint32_t)T, ranges, b.se, s, gate);
@@ -195,8 +201,12 @@ HostCounters& host_counters() {
     return h;
 }
 
-// Phase-1 binning capacity (instances): prefix_per_tile x tiles (0 -> default), or everything when < 0.
-constexpr int DEFAULT_PREFIX_PER_TILE = 256;
+// Phase-1 binning capacity, in tile-rect area units (the depth cut bounds the precise instances by the rect areas):
+// prefix_per_tile x tiles (0 -> default), or everything when < 0.  448 rect units are ~256 precise instances per
+// tile on the bench scene.
+constexpr int DEFAULT_PREFIX_PER_TILE = 448;
+// capacity of any per-instance array: the total rect area bounds every phase's instance count
+inline int64_t inst_cap(uint64_t rect) { return (int64_t)(rect < 0xffffff00ull ? (rect ? rect : 1) : 0xffffff00ull); }
 bool prefix_enabled(const dg_raster_args* a) { return a->prefix_per_tile >= 0; }
 int64_t phase1_cap(const dg_raster_args* a, int T, int64_t K_all) {
     if (!prefix_enabled(a)) return K_all;
@@ -354,7 +364,7 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     { PROF("preprocess"); gs::launch_preprocess(pre, s); }
     DBG_SYNC(a->debug, s);
 
-    // ---- depth-threshold prefix: histogram of instance counts over depth bins -> threshold (no depth sort)
+    // ---- depth-threshold prefix: histogram of tile-rect areas over depth bins -> threshold (no depth sort)
     int64_t C1;
     if (P == 0) HIP_OK(hipMemsetAsync(g.hist, 0, gs::DH_BINS * sizeof(uint32_t), s));  // no preprocess to zero it
     {
@@ -362,9 +372,8 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
         gs::launch_depth_hist(P, g.dkey, g.cnt, g.hist, s);
         if (prefix_enabled(a)) {
             C1 = phase1_cap(a, T, 0);
-            gs::launch_depth_cut(g.hist, (uint32_t)(C1 < 0xffffffffll ? C1 : 0xffffffffll), g.counters, im.tile_cnt,
-                                 im.tile_cnt2, (uint32_t)T, s);
-        } else {  // everything in one phase: the capacity is K itself (one early sync)
+            gs::launch_depth_cut(g.hist, (uint32_t)C1, g.counters, im.tile_cnt, im.tile_cnt2, (uint32_t)T, s);
+        } else {  // everything in one phase: the capacity is the total rect area itself (one early sync)
             gs::launch_depth_cut(g.hist, 0xffffffffu, g.counters, im.tile_cnt, im.tile_cnt2, (uint32_t)T, s);
             uint32_t k = 0;
             HIP_OK(hipMemcpyAsync(&k, g.counters + gs::CNT_K, 4, hipMemcpyDeviceToHost, s));
@@ -373,18 +382,6 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
         }
     }
     DBG_SYNC(a->debug, s);
-    // emission offsets of the prefix Gaussians (index order)
-    if (P > 0) {
-        PROF("count_scan");
-        gs::exclusive_scan(g.cnt, (uint32_t)P, g.off, g.counters + gs::CNT_E1CHK, g.scan_tmp, s, nullptr, g.dkey,
-                           g.counters + gs::CNT_THR);
-    }
-    DBG_SYNC(a->debug, s);
-    // the host's only wait is on this early copy (K, num_rendered, error flag, cut), and it happens after all of
-    // phase 1 is queued, so the GPU never idles on it
-    HostCounters& hcs = host_counters();
-    HIP_OK(hipMemcpyAsync(hcs.buf, g.counters, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_OK(hipEventRecord(hcs.ev, s));
 
     const size_t bbytes = carve_binning(nullptr, C1).bytes;
     void* bbase = alloc(user, DG_BUF_BINNING, bbytes);
@@ -393,8 +390,16 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     Binning b = carve_binning(bbase, C1);
     const uint32_t* E1_dev = g.counters + gs::CNT_E1;
     if (C1 > 0 && P > 0) {
-        { PROF("emit"); gs::launch_emit(P, g.dkey, g.cnt, g.off, g.sp, tx, g.counters, g.first_e, g.rcnt, b.tk, b.eg, b.ik, s); }
+        gs::BinArgs ba = bin_args(g, im, P, tx, (uint32_t)C1, b);
+        { PROF("emit"); gs::launch_bin(1, ba, g.counters + gs::CNT_E1, g.scan_tmp, s); }
         DBG_SYNC(a->debug, s);
+    }
+    // the host's only wait is on this early copy (num_rendered, E1, error flag, cut), and it happens after all of
+    // phase 1 is queued, so the GPU never idles on it
+    HostCounters& hcs = host_counters();
+    HIP_OK(hipMemcpyAsync(hcs.buf, g.counters, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipEventRecord(hcs.ev, s));
+    if (C1 > 0 && P > 0) {
         { PROF("tile_bin"); bin_and_sort(b, C1, E1_dev, T, im.ranges, im.tile_cnt, nullptr, nullptr, im.long_tiles,
                                          g.counters + gs::CNT_LONG, s); }
         DBG_SYNC(a->debug, s);
@@ -417,11 +422,11 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     HIP_OK(hipEventSynchronize(hcs.ev));
     const uint32_t* hc = hcs.buf;
     if (hc[gs::CNT_ERR]) return fail("a Gaussian was filtered although prefiltered is set%s%d");
-    if (a->debug && hc[gs::CNT_E1CHK] != hc[gs::CNT_E1]) return fail("prefix scan total %s%d differs from the cut", "", (int)hc[gs::CNT_E1CHK]);
-    *num_rendered = (int64_t)((uint64_t)hc[gs::CNT_RECT_LO] | ((uint64_t)hc[gs::CNT_RECT_LO + 1] << 32));
-    const uint32_t K = hc[gs::CNT_K];
-    // the backward sizes records for K (>= phase-1 + phase-2 instances) and re-carves phase 2 at K
-    *num_instances = K;
+    const uint64_t rect = (uint64_t)hc[gs::CNT_RECT_LO] | ((uint64_t)hc[gs::CNT_RECT_LO + 1] << 32);
+    *num_rendered = (int64_t)rect;
+    // the num_buckets slot: the precise phase-1 instance count (all instances when nothing was cut).  The backward
+    // sizes its per-instance state by num_rendered, which bounds phase 1 + phase 2.
+    *num_instances = hc[gs::CNT_E1];
     if (!hc[gs::CNT_CUT]) {
         HIP_OK(hipGetLastError());
         return 0;
@@ -429,6 +434,7 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
 
     // ---- phase 2: the Gaussians past the threshold, only for tiles phase 1 left unfinished.  Every kernel is gated
     // on the device-side unfinished count, so nothing waits for phase 1 and the common case costs a few empty launches.
+    const int64_t K = inst_cap(rect);
     const size_t b2bytes = carve_binning(nullptr, K).bytes;
     void* b2base = alloc(user, DG_BUF_BINNING2, b2bytes);
     if (!b2base) return fail("phase-2 binning allocation failed%s%d");
@@ -439,15 +445,13 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     {
         PROF("phase2");
         gs::launch_unfinished_sat(g.counters, im.unfinished, tx, ty, im.sat, s);
-        gs::launch_count2(P, g.counters, g.dkey, g.sp, tx, ty, im.unfinished, im.sat, g.cnt2, s);
-        gs::exclusive_scan(g.cnt2, (uint32_t)P, g.off2, g.counters + gs::CNT_K2, g.scan_tmp, s, gate);
-        gs::launch_emit2(P, g.counters, g.dkey, g.sp, tx, ty, im.unfinished, im.sat, g.cnt2, g.off2, g.first_e, g.rcnt,
-                         b2.tk, b2.eg, b2.ik, s);
+        gs::BinArgs ba = bin_args(g, im, P, tx, (uint32_t)K, b2);
+        gs::launch_bin(2, ba, g.counters + gs::CNT_K2, g.scan_tmp, s);
         bin_and_sort(b2, K, K2_dev, T, im.ranges2, im.tile_cnt2, im.unfinished, gate, im.long_tiles,
                      g.counters + gs::CNT_LONG2, s);
-        gs::RenderArgs r2 = r;
+    gs::RenderArgs r2 = r;
         r2.phase = 2;
-        r2.K = K;
+        r2.K = (uint32_t)K;
         r2.ranges = im.ranges2; r2.ranges1 = im.ranges; r2.s_e = b2.se; r2.eg = b2.eg;
         gs::launch_render_fwd(r2, s);
     }
@@ -461,7 +465,6 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
                           const float* dL_dout_color, const float* dL_dout_invdepth, float* dmeans2D, float* dcolors,
                           float* dopacity, float* dmeans3D, float* dcov3D, float* ddc, float* dsh, float* dscales,
                           float* drot, float* depth, dg_alloc_fn alloc, void* user, dg_stream_t stream_) {
-    (void)num_rendered;
     if (check_args(a)) return 1;
     hipStream_t s = (hipStream_t)stream_;
     const int P = a->P, W = a->W, H = a->H;
@@ -469,26 +472,28 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     if (P == 0) return 0;
     Geom g = carve_geom((void*)geom, P);
     Image im = carve_image((void*)image, W, H);
-    // the phase-1 block was carved at C1 (its capacity), the phase-2 block at K (see the forward)
-    const int64_t C1 = phase1_cap(a, T, K);
+    // the phase-1 block was carved at C1 (its capacity), the phase-2 block at the rect total (see the forward)
+    const int64_t Kcap = inst_cap((uint64_t)num_rendered);
+    const int64_t C1 = prefix_enabled(a) ? phase1_cap(a, T, 0) : Kcap;
     Binning b = carve_binning((void*)binning, C1);
     const uint32_t* s_e = b.se;
     const uint32_t* s_e2 = nullptr;
     const uint32_t* eg2 = nullptr;
     if (binning2) {
-        Binning b2 = carve_binning((void*)binning2, K);
+        Binning b2 = carve_binning((void*)binning2, Kcap);
         s_e2 = b2.se;
         eg2 = b2.eg;
     }
 
-    const size_t sbytes = carve_bwd(nullptr, K, P, T).bytes;
+    (void)K;  // the phase-1 instance count (informational)
+    const size_t sbytes = carve_bwd(nullptr, Kcap, P, T).bytes;
     void* sbase = alloc(user, DG_BUF_BACKWARD, sbytes);
     if (!sbase) return fail("backward scratch allocation failed%s%d");
-    BwdScratch sc = carve_bwd(sbase, K, P, T);
-    if (K > 0) {
+    BwdScratch sc = carve_bwd(sbase, Kcap, P, T);
+    {
         gs::RenderBwdArgs r;
         r.W = W; r.H = H; r.tiles_x = tx; r.num_tiles = T;
-        r.K = (uint32_t)K; r.P = (uint32_t)P;
+        r.K = (uint32_t)Kcap; r.K1 = (uint32_t)C1; r.P = (uint32_t)P;
         r.ranges = im.ranges; r.max_contrib = im.max_contrib; r.s_e = s_e; r.eg = b.eg;
         r.ranges2 = binning2 ? im.ranges2 : nullptr; r.s_e2 = s_e2; r.eg2 = eg2; r.counters = g.counters;
         r.unfinished = im.unfinished;
@@ -502,7 +507,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     gs::GaussBwdArgs q;
     memset(&q, 0, sizeof(q));
     q.P = P; q.D = a->D; q.M = a->M; q.W = W; q.H = H; q.antialiasing = a->antialiasing;
-    q.K = (uint32_t)K;
+    q.K = (uint32_t)Kcap;
     q.tanfovx = a->tanfovx; q.tanfovy = a->tanfovy;
     q.focal_y = H / (2.0f * a->tanfovy);
     q.focal_x = W / (2.0f * a->tanfovx);
@@ -599,8 +604,8 @@ __global__ void k_tiles_of(int T, const uint2* ranges, const uint8_t* only, uint
 }  // namespace
 
 int dg_debug_sorted_instances(const dg_raster_args* a, const void* geom, const void* binning, const void* binning2,
-                              const void* image, int64_t K, uint32_t* tiles_out, uint32_t* gauss_out, int64_t* e1_out,
-                              dg_stream_t stream) {
+                              const void* image, int64_t num_rendered, uint32_t* tiles_out, uint32_t* gauss_out,
+                              int64_t* e1_out, dg_stream_t stream) {
     hipStream_t s = (hipStream_t)stream;
     const int T = tiles_x_of(a->W) * tiles_y_of(a->H);
     Geom g = carve_geom((void*)geom, a->P);
@@ -610,14 +615,15 @@ int dg_debug_sorted_instances(const dg_raster_args* a, const void* geom, const v
     HIP_OK(hipStreamSynchronize(s));
     const uint32_t E1 = hc[gs::CNT_E1];
     *e1_out = E1;
+    const int64_t Kcap = inst_cap((uint64_t)num_rendered);
     if (E1 > 0) {
-        Binning b = carve_binning((void*)binning, phase1_cap(a, T, K));
+        Binning b = carve_binning((void*)binning, prefix_enabled(a) ? phase1_cap(a, T, 0) : Kcap);
         k_gather_g<<<(E1 + 255) / 256, 256, 0, s>>>(E1, b.se, b.eg, gauss_out);
         k_tiles_of<<<(T + 255) / 256, 256, 0, s>>>(T, im.ranges, nullptr, tiles_out);
     }
     const int64_t K2 = binning2 ? (int64_t)hc[gs::CNT_K2] : 0;
     if (binning2 && K2 > 0) {
-        Binning b2 = carve_binning((void*)binning2, K);
+        Binning b2 = carve_binning((void*)binning2, Kcap);
         k_gather_g<<<(unsigned)((K2 + 255) / 256), 256, 0, s>>>((uint32_t)K2, b2.se, b2.eg, gauss_out + E1);
         k_tiles_of<<<(T + 255) / 256, 256, 0, s>>>(T, im.ranges2, im.unfinished, tiles_out + E1);
     }
@@ -644,7 +650,7 @@ int dg_debug_geometry(const void* geom, int P, float* means2D, float* conic_opac
     if (conic_opacity)
         HIP_OK(hipMemcpy2DAsync(conic_opacity, 16, (const char*)g.sp + 8, 32, 16, (size_t)P, hipMemcpyDeviceToDevice, s));
     if (rgb_invdepth) HIP_OK(hipMemcpyAsync(rgb_invdepth, g.rgbi, 16 * (size_t)P, hipMemcpyDeviceToDevice, s));
-    if (tile_count) HIP_OK(hipMemcpyAsync(tile_count, g.cnt, 4 * (size_t)P, hipMemcpyDeviceToDevice, s));
+    if (tile_count) HIP_OK(hipMemcpyAsync(tile_count, g.rcnt, 4 * (size_t)P, hipMemcpyDeviceToDevice, s));
     return 0;
 }
 

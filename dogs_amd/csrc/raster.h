@@ -23,9 +23,9 @@ struct PreArgs {
     int* radii;
     float4* sp;         // splat record, 2 x float4 per Gaussian (see SP_* below)
     float4* rgbi;       // rgb, 1 / view z
-    uint32_t* depthkey; // float bits of view z, 0xffffffff when no tile survives the precise cull
+    uint32_t* depthkey; // float bits of view z, 0xffffffff when culled (empty tile rect)
     uint32_t* hist;     // [DH_BINS] depth histogram, zeroed here
-    uint32_t* cnt;      // precise tile count
+    uint32_t* cnt;      // tile-rect area (0 when culled)
     uint32_t* rcnt;     // records per Gaussian, zeroed here (written by the emission kernels)
     unsigned long long* rect_sum;  // num_rendered of the reference (sum of rect areas)
     uint32_t* err;
@@ -33,16 +33,15 @@ struct PreArgs {
 
 // Counters block at the head of the geometry state (device, uint32 slots).
 enum {
-    CNT_K = 0,          // precise instance total
+    CNT_K = 0,          // total tile-rect area of the visible Gaussians (bounds the instance count)
     CNT_ERR = 1,        // prefiltered violation
     CNT_RECT_LO = 2,    // num_rendered (sum of rect areas), u64 in slots 2..3
     CNT_THR = 4,        // depth-key threshold: Gaussians with key < thr are binned in phase 1
-    CNT_E1 = 5,         // instances of phase 1
+    CNT_E1 = 5,         // instances of phase 1 (allocated by the emission)
     CNT_UNFINISHED = 6, // tiles with live pixels after phase 1 (only counted when CNT_CUT)
     CNT_K2 = 7,         // phase-2 instances
     CNT_CUT = 8,        // E1 < K: the phase-1 lists are prefixes
     CNT_INVD = 9,       // backward: any(dL/dinvdepth != 0) (zeroed with the block by the forward)
-    CNT_E1CHK = 10,     // the prefix scan's total (equals CNT_E1; a consistency check)
     CNT_LONG = 11,      // phase-1 tiles queued for the long-list depth sort
     CNT_LONG2 = 12,     // phase-2 tiles queued for the long-list depth sort
 };
@@ -76,7 +75,7 @@ struct RenderArgs {
 
 struct RenderBwdArgs {
     int W, H, tiles_x, num_tiles;
-    uint32_t K, P;
+    uint32_t K, K1, P;       // capacities: per-instance state (global index), phase-1 binning, Gaussians
     const uint2* ranges;
     const uint32_t* max_contrib;
     const uint32_t* s_e;
@@ -120,20 +119,27 @@ void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_
 // the per-tile counters of both binning phases (tile_cnt, tile_cnt2 [num_tiles])
 void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, uint32_t* tile_cnt, uint32_t* tile_cnt2,
                       uint32_t num_tiles, hipStream_t s);
-// phase 1: Gaussians with key < counters[CNT_THR] -> instances [0, E1) at off[g]; rcnt/first_e of those Gaussians
-// ikey[e] = the instance's depth key (read by the per-tile depth sort)
-void launch_emit(int P, const uint32_t* dkey, const uint32_t* cnt, const uint32_t* off, const float4* sp, int tiles_x,
-                 const uint32_t* counters, uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey, uint32_t* eg,
-                 uint32_t* ikey, hipStream_t s);
-// phase 2 over the Gaussians with key >= thr: only (Gaussian, tile) instances whose tile is unfinished.
-// All phase-2 kernels are gated on counters[CNT_UNFINISHED] (device): no-ops when phase 1 finished every tile.
+// Binning walk of one phase (phase 1: Gaussians with key < counters[CNT_THR]; phase 2: those past it, only instances
+// in tiles phase 1 left unfinished): k_bin_count (precise cull walk -> rcnt, per-wave totals), exclusive scan of
+// the wave totals (*total = the phase's instance count), k_bin_emit (first_e; tilekey/eg/ikey per instance).
+// Phase-2 kernels are gated on counters[CNT_UNFINISHED] (device): no-ops when phase 1 finished every tile.
+struct BinArgs {
+    int P, tiles_x;
+    const uint32_t* dkey;
+    const float4* sp;
+    const uint32_t* counters;    // CNT_THR, CNT_E1 (phase 2), CNT_UNFINISHED
+    const uint8_t* unf;          // phase 2: unfinished tiles
+    const uint32_t* sat;         // phase 2: summed-area table of unf
+    uint32_t* wtot;              // [bin_waves(P)] per-wave totals, scanned in place
+    uint32_t cap;                // capacity of the instance arrays
+    uint32_t *first_e, *rcnt;
+    uint32_t *tilekey, *eg, *ikey;
+};
+void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s);
+size_t bin_scan_temp_bytes(int P);
+int bin_waves(int P);
 void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, int tiles_x, int tiles_y,
                            uint32_t* sat, hipStream_t s);
-void launch_count2(int P, const uint32_t* counters, const uint32_t* dkey, const float4* sp, int tiles_x, int tiles_y,
-                   const uint8_t* unfinished, const uint32_t* sat, uint32_t* cnt2, hipStream_t s);
-void launch_emit2(int P, const uint32_t* counters, const uint32_t* dkey, const float4* sp, int tiles_x, int tiles_y,
-                  const uint8_t* unfinished, const uint32_t* sat, const uint32_t* cnt2, const uint32_t* off2,
-                  uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey, uint32_t* eg, uint32_t* ikey, hipStream_t s);
 void launch_render_fwd(const RenderArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);
 void launch_filter(const PreArgs& a, hipStream_t s);

@@ -137,7 +137,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
         if (j < n) {
             uint32_t ee, g;
             if (j < n1) {
-                ee = min(a.s_e[rg.x + j], a.K - 1);
+                ee = min(a.s_e[rg.x + j], a.K1 - 1);
                 g = min(a.eg[ee], a.P - 1);
             } else {
                 const uint32_t el = min(a.s_e2[rg2.x + (uint32_t)(j - n1)], a.K - 1 - E1);

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include "gs_common.h"
 #include "raster.h"
+#include "sortscan.h"
 
 namespace gs {
 
@@ -145,12 +146,11 @@ __device__ __forceinline__ void wave_candidates(CandLDS& L, int lane, int x0, in
     __builtin_amdgcn_wave_barrier();
 }
 
-// Returns the rect area (0 when culled); fills the geometry outputs for kept Gaussians.
-struct RectOut { int x0, y0, x1, y1; float mx, my, thr; float4 co; };
-
-__device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, const float* lsh, RectOut& ro) {
+// Returns the tile-rect area (0 when culled); fills the geometry outputs of kept Gaussians.
+__device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, const float* lsh) {
     a.radii[idx] = 0;
     a.depthkey[idx] = 0xffffffffu;
+    a.cnt[idx] = 0u;
     a.rcnt[idx] = 0u;
     const f3 po = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
     // every per-Gaussian input is loaded before the first use, so one HBM round trip covers them all
@@ -216,13 +216,13 @@ __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, co
                                     __uint_as_float((uint32_t)y0 | ((uint32_t)y1 << 16)));
     a.rgbi[idx] = make_float4(col.x, col.y, col.z, 1.f / pv.z);
     a.depthkey[idx] = __float_as_uint(pv.z);
-    ro.x0 = x0; ro.y0 = y0; ro.x1 = x1; ro.y1 = y1; ro.mx = px; ro.my = py; ro.co = co;
-    ro.thr = gs_logf(co.w / (1.0f / 255.0f));
+    a.cnt[idx] = area;
     return area;
 }
 
 // The block's [256][M][3] SH slab is staged through LDS with 16-B coalesced loads; read per thread at a
-// 45-dword stride (odd -> conflict-free) instead of 45 strided global loads per lane.
+// 45-dword stride (odd -> conflict-free) instead of 45 strided global loads per lane.  The precise per-tile
+// cull is not done here: only the prefix Gaussians are walked, by k_emit.
 __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     __shared__ unsigned long long s_sum[4];
@@ -231,11 +231,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     const int idx = base + t;
     const int nloc = (a.P - base) < 256 ? (a.P - base) : 256;
     for (int i = base + t; i < DH_BINS; i += gridDim.x * 256) a.hist[i] = 0u;  // for k_depth_hist
-#ifdef DG_ABLATE_NO_SH
-    const bool stage = false;
-#else
     const bool stage = a.sh != nullptr && a.colors == nullptr && a.M > 0;
-#endif
     if (stage) {
         const int slab = nloc * a.M * 3;
         const float* src = a.sh + (size_t)base * a.M * 3;
@@ -251,46 +247,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     }
     __syncthreads();
     uint32_t area = 0;
-    RectOut ro = {0, 0, 0, 0, 0.f, 0.f, 0.f, make_float4(0.f, 0.f, 0.f, 0.f)};
-#ifdef DG_ABLATE_NO_SH  // timing experiment only: colour from dc alone (degree 0, no SH read)
-    PreArgs a0 = a;
-    a0.sh = nullptr;
-    if (idx < a.P) area = preprocess_one(a0, idx, nullptr, ro);
-#else
-    if (idx < a.P) area = preprocess_one(a, idx, stage ? s_sh + t * a.M * 3 : nullptr, ro);
-#endif
-    // precise per-tile cull counts (duplicateWithKeys, rasterizer_impl.cu:149-179), wave-cooperative.
-    // The candidate tables reuse the SH staging LDS (dead after preprocess_one).
-    __syncthreads();
-    {
-        CandLDS* s_cand = reinterpret_cast<CandLDS*>(s_sh);
-        uint32_t (*s_cnt)[64] = reinterpret_cast<uint32_t (*)[64]>(s_cand + 4);
-        const int lane = t & 63, w = t >> 6;
-        s_cnt[w][lane] = 0;
-        CandLDS& L = s_cand[w];
-#ifdef DG_ABLATE_NO_WALK  // timing experiment only: counts = rect areas
-        s_cnt[w][lane] = area;
-        if (false)
-#endif
-        wave_candidates(L, lane, ro.x0, ro.y0, ro.x1, ro.y1, ro.mx, ro.my, ro.co, ro.thr,
-                        [&](int owner, int, int, bool kept, bool valid, uint32_t item) {
-                            const uint64_t km = __ballot(kept);
-                            // first item of each owner segment in this step adds the segment's kept count
-                            const bool seg_start = valid && (lane == 0 || item == L.pre[owner]);
-                            if (seg_start) {
-                                const uint32_t seg_end_item = L.pre[owner] + (uint32_t)L.area[owner];
-                                const int len = (int)min(seg_end_item - item, (uint32_t)(64 - lane));
-                                const uint64_t seg = (len >= 64 ? ~0ull : ((1ull << len) - 1ull)) << lane;
-                                s_cnt[w][owner] += (uint32_t)__popcll(km & seg);
-                            }
-                            __builtin_amdgcn_wave_barrier();
-                        });
-        if (idx < a.P) {
-            const uint32_t c = s_cnt[w][lane];
-            a.cnt[idx] = c;
-            if (c == 0) a.depthkey[idx] = 0xffffffffu;
-        }
-    }
+    if (idx < a.P) area = preprocess_one(a, idx, stage ? s_sh + t * a.M * 3 : nullptr);
     unsigned long long v = area;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -305,9 +262,9 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
 // ---------------------------------------------------------------------------------------------------
 // Depth-threshold prefix (DESIGN.md "Binning").  Phase 1 bins the Gaussians whose depth key is below a
 // threshold `thr`; because every tile's list is in (depth bits, index) order, those instances are a PREFIX of
-// every tile's list, whatever the threshold.  thr is picked from a histogram of instance counts over coarse
-// depth bins so that the prefix fits the phase-1 capacity; no global depth sort is needed -- each tile's
-// prefix list is depth-sorted on its own (k_tile_dsort).
+// every tile's list, whatever the threshold.  thr is picked from a histogram of tile-rect areas (an upper bound
+// of the precise instance counts) over coarse depth bins so that the prefix surely fits the phase-1 capacity; no
+// global depth sort is needed -- each tile's prefix list is depth-sorted on its own (k_tile_dsort).
 // ---------------------------------------------------------------------------------------------------
 constexpr int DH_THREADS = 256;
 constexpr int DH_ITEMS = 16;                        // Gaussians per thread per block
@@ -318,7 +275,7 @@ __device__ __forceinline__ uint32_t depth_bin(uint32_t key) {
     return b < (uint32_t)DH_BINS ? b : (uint32_t)(DH_BINS - 1);  // far keys share the last bin
 }
 
-// hist[bin] += cnt[g] over visible Gaussians: a private LDS histogram per block, flushed with one atomic per
+// hist[bin] += rect area of g over visible Gaussians: a private LDS histogram per block, flushed with one atomic per
 // non-empty bin (blocks cover DH_THREADS * DH_ITEMS Gaussians: ~245 blocks at 1e6).
 __global__ void __launch_bounds__(DH_THREADS) k_depth_hist(int P, const uint32_t* __restrict__ dkey,
                                                           const uint32_t* __restrict__ cnt,
@@ -342,7 +299,7 @@ __global__ void __launch_bounds__(DH_THREADS) k_depth_hist(int P, const uint32_t
         if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
 }
 
-// One block: K = total instances, and the largest bin prefix [0, b] whose instances fit `cap`; thr = the first
+// One block: K = total rect area, and the largest bin prefix [0, b] whose rect areas fit `cap`; thr = the first
 // key of bin b + 1 (S = {key < thr}).  No cut (thr = all visible) when K <= cap.  Also resets the per-view
 // counters and the per-tile counters of both binning phases.
 __global__ void __launch_bounds__(1024) k_depth_cut(const uint32_t* __restrict__ hist, uint32_t cap,
@@ -371,11 +328,10 @@ __global__ void __launch_bounds__(1024) k_depth_cut(const uint32_t* __restrict__
     // inclusive cumulative count at each of this thread's bins; C(b) is non-decreasing in b
     uint32_t c = off + x - loc;
     int best = -1;
-    uint32_t cbest = 0;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
         c += v[k];
-        if (c <= cap) { best = t * PER + k; cbest = c; }
+        if (c <= cap) best = t * PER + k;
     }
     if (best >= 0) atomicMax(&s_best, best);
     __syncthreads();
@@ -383,75 +339,144 @@ __global__ void __launch_bounds__(1024) k_depth_cut(const uint32_t* __restrict__
     if (t == 0 && s_best < 0) {  // not even bin 0 fits: phase 1 bins nothing, phase 2 everything
         counters[CNT_K] = K;
         counters[CNT_THR] = cut ? (DH_BASE << DH_SHIFT) : 0xffffffffu;
-        counters[CNT_E1] = cut ? 0u : K;
+        counters[CNT_E1] = 0u;  // accumulated by the emission
         counters[CNT_CUT] = cut ? 1u : 0u;
         counters[CNT_UNFINISHED] = 0; counters[CNT_K2] = 0; counters[CNT_LONG] = 0; counters[CNT_LONG2] = 0;
     }
     if (best >= 0 && best == s_best) {  // exactly one thread holds the best bin
         counters[CNT_K] = K;
         counters[CNT_THR] = cut ? ((DH_BASE + (uint32_t)best + 1u) << DH_SHIFT) : 0xffffffffu;
-        counters[CNT_E1] = cut ? cbest : K;
+        counters[CNT_E1] = 0u;  // accumulated by the emission
         counters[CNT_CUT] = cut ? 1u : 0u;
         counters[CNT_UNFINISHED] = 0; counters[CNT_K2] = 0; counters[CNT_LONG] = 0; counters[CNT_LONG2] = 0;
     }
 }
 
+
+// Precise per-tile count of each lane's Gaussian (duplicateWithKeys' cull, rasterizer_impl.cu:149-179) by the
+// wave-cooperative candidate walk, into cnt[lane] (LDS, zeroed here).  keep(tx, ty) filters tiles further.
+template <typename Keep>
+__device__ __forceinline__ void wave_count(CandLDS& L, uint32_t* cnt, int lane, int x0, int y0, int x1, int y1,
+                                           float mx, float my, float4 co, float thr, Keep&& keep) {
+    cnt[lane] = 0u;
+    wave_candidates(L, lane, x0, y0, x1, y1, mx, my, co, thr,
+                    [&](int owner, int tx, int ty, bool kept, bool valid, uint32_t item) {
+                        const uint64_t km = __ballot(kept && keep(tx, ty));
+                        // first item of each owner segment in this step adds the segment's kept count
+                        const bool seg_start = valid && (lane == 0 || item == L.pre[owner]);
+                        if (seg_start) {
+                            const uint32_t seg_end_item = L.pre[owner] + (uint32_t)L.area[owner];
+                            const int len = (int)min(seg_end_item - item, (uint32_t)(64 - lane));
+                            const uint64_t seg = (len >= 64 ? ~0ull : ((1ull << len) - 1ull)) << lane;
+                            cnt[owner] += (uint32_t)__popcll(km & seg);
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                    });
+}
+
 #ifndef DG_EMIT_RANKS
 #define DG_EMIT_RANKS 64
 #endif
-constexpr int EMIT_RANKS = DG_EMIT_RANKS;
+constexpr int EMIT_RANKS = DG_EMIT_RANKS;  // Gaussians per wave of the binning walks
 
-// Phase-1 emission in index order: instance e = off[g] + j for the j-th kept tile of a prefix Gaussian g
-// (key < thr; off = exclusive scan of cnt over the prefix set).  A wave owns EMIT_RANKS consecutive Gaussians,
-// so its instances form one contiguous run starting at off[g0]; the cooperative candidate walk writes them in
-// (g, ty, tx) order with consecutive lanes -> consecutive e.  rcnt[g] = instances emitted for g (the record
-// count of the backward), first_e[g] = off[g].
-__global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict__ dkey,
-                                              const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
-                                              const float4* __restrict__ sp, int tiles_x,
-                                              const uint32_t* __restrict__ counters,
-                                              uint32_t* __restrict__ first_e, uint32_t* __restrict__ rcnt,
-                                              uint32_t* __restrict__ tilekey, uint32_t* __restrict__ eg,
-                                              uint32_t* __restrict__ ikey) {
+__device__ __forceinline__ uint32_t sat_rect(const uint32_t* sat, int tx, int x0, int y0, int x1, int y1);
+
+// The binned Gaussians of a wave (EMIT_RANKS consecutive indices) and their walk inputs.
+//   phase 1: the prefix Gaussians (key < thr);
+//   phase 2: Gaussians past the threshold whose rect touches a tile phase 1 left unfinished (only those tiles kept).
+struct BinLane {
+    int x0, y0, x1, y1;
+    float mx, my, lthr;
+    float4 co;
+    bool member;
+};
+template <int PHASE>
+__device__ __forceinline__ BinLane bin_lane(const BinArgs& a, int g, int lane, uint32_t thr, uint32_t* s_key) {
+    BinLane b = {0, 0, 0, 0, 0.f, 0.f, 0.f, make_float4(0.f, 0.f, 0.f, 0.f), false};
+    if (lane < EMIT_RANKS && g < a.P) {
+        const uint32_t key = a.dkey[g];
+        s_key[lane] = key;
+        bool m = key != 0xffffffffu && (PHASE == 1 ? key < thr : key >= thr);
+        if (m) {
+            const float4 s0 = a.sp[2 * g], s1 = a.sp[2 * g + 1];
+            sp_rect(s1, b.x0, b.y0, b.x1, b.y1);
+            if (PHASE == 2) m = b.x1 > b.x0 && b.y1 > b.y0 && sat_rect(a.sat, a.tiles_x, b.x0, b.y0, b.x1, b.y1) != 0u;
+            if (m) {
+                b.co = make_float4(s0.z, s0.w, s1.x, s1.y);
+                b.mx = s0.x; b.my = s0.y;
+                b.lthr = gs_logf(b.co.w / (1.0f / 255.0f));
+            }
+        }
+        b.member = m;
+    }
+    if (!b.member) { b.x1 = b.x0; b.y1 = b.y0; }
+    return b;
+}
+
+// Pass 1 of the binning: each wave's precise per-tile counts (rcnt of its Gaussians) and the wave total (wtot).
+template <int PHASE>
+__global__ void __launch_bounds__(256) k_bin_count(BinArgs a) {
     __shared__ CandLDS s_cand[4];
     __shared__ uint32_t s_key[4][64];
+    __shared__ uint32_t s_cnt[4][64];
+    if (PHASE == 2 && a.counters[CNT_UNFINISHED] == 0u) return;  // phase 1 finished every tile
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int g0 = (blockIdx.x * 4 + w) * EMIT_RANKS;
-    if (g0 >= P) return;  // whole wave
-    const uint32_t thr = counters[CNT_THR];
+    const int wave = blockIdx.x * 4 + w;
+    const int g0 = wave * EMIT_RANKS;
+    if (g0 >= a.P) return;  // whole wave (past the last one the scan reads)
     const int g = g0 + lane;
-    int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
-    float mx = 0.f, my = 0.f, lthr = 0.f;
-    float4 c4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    bool member = false;
-    if (lane < EMIT_RANKS && g < P) {
-        const uint32_t key = dkey[g];
-        s_key[w][lane] = key;
-        member = key < thr && key != 0xffffffffu;
-        if (member) {
-            const uint32_t c = cnt[g];
-            first_e[g] = off[g];
-            rcnt[g] = c;
-            const float4 s0 = sp[2 * g], s1 = sp[2 * g + 1];
-            c4 = make_float4(s0.z, s0.w, s1.x, s1.y);
-            mx = s0.x; my = s0.y;
-            sp_rect(s1, x0, y0, x1, y1);
-            lthr = gs_logf(c4.w / (1.0f / 255.0f));
-        }
+    const BinLane b = bin_lane<PHASE>(a, g, lane, a.counters[CNT_THR], s_key[w]);
+    uint32_t c = 0;
+    if (__any(b.member)) {
+        wave_count(s_cand[w], s_cnt[w], lane, b.x0, b.y0, b.x1, b.y1, b.mx, b.my, b.co, b.lthr, [&](int tx, int ty) {
+            return PHASE == 1 || a.unf[ty * a.tiles_x + tx] != 0;
+        });
+        c = s_cnt[w][lane];
+        if (b.member) a.rcnt[g] = c;
     }
-    if (!__any(member)) return;  // whole wave: no prefix Gaussian
-    const uint32_t e0 = off[g0];
+    uint32_t tot = c;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+    if (lane == 0) a.wtot[wave] = tot;
+}
+
+// Pass 2: wave base = exclusive scan of the wave totals (wtot, scanned in place); first_e of every binned
+// Gaussian, and a second walk writes its instances (tile, Gaussian, depth key) at consecutive indices in
+// (lane, ty, tx) order, so every Gaussian's instances are contiguous: [first_e, first_e + rcnt).
+template <int PHASE>
+__global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
+    __shared__ CandLDS s_cand[4];
+    __shared__ uint32_t s_key[4][64];
+    if (PHASE == 2 && a.counters[CNT_UNFINISHED] == 0u) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wave = blockIdx.x * 4 + w;
+    const int g0 = wave * EMIT_RANKS;
+    if (g0 >= a.P) return;
+    const int g = g0 + lane;
+    const BinLane b = bin_lane<PHASE>(a, g, lane, a.counters[CNT_THR], s_key[w]);
+    if (!__any(b.member)) return;
+    const uint32_t base = a.wtot[wave];
+    const uint32_t c = b.member ? a.rcnt[g] : 0u;
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    const uint32_t wt = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (wt == 0u || base + wt > a.cap) return;  // nothing kept; (capacity: never with consistent inputs)
+    if (b.member && c) a.first_e[g] = (PHASE == 2 ? a.counters[CNT_E1] : 0u) + base + incl - c;
     uint32_t running = 0;
-    CandLDS& L = s_cand[w];
-    wave_candidates(L, lane, x0, y0, x1, y1, mx, my, c4, lthr,
-                    [&](int owner, int tx, int ty, bool kept, bool valid, uint32_t) {
+    wave_candidates(s_cand[w], lane, b.x0, b.y0, b.x1, b.y1, b.mx, b.my, b.co, b.lthr,
+                    [&](int owner, int tx, int ty, bool kept, bool, uint32_t) {
+                        kept = kept && (PHASE == 1 || a.unf[ty * a.tiles_x + tx] != 0);
                         const uint64_t km = __ballot(kept);
                         const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
                         if (kept) {
-                            const uint32_t e = e0 + running + (uint32_t)__popcll(km & lt);
-                            tilekey[e] = (uint32_t)(ty * tiles_x + tx);
-                            eg[e] = (uint32_t)(g0 + owner);
-                            ikey[e] = s_key[w][owner];
+                            const uint32_t e = base + running + (uint32_t)__popcll(km & lt);
+                            a.tilekey[e] = (uint32_t)(ty * a.tiles_x + tx);
+                            a.eg[e] = (uint32_t)(g0 + owner);
+                            a.ikey[e] = s_key[w][owner];
                         }
                         running += (uint32_t)__popcll(km);
                     });
@@ -486,86 +511,6 @@ __global__ void __launch_bounds__(1024) k_unfinished_sat(const uint32_t* __restr
 __device__ __forceinline__ uint32_t sat_rect(const uint32_t* sat, int tx, int x0, int y0, int x1, int y1) {
     const int W1 = tx + 1;
     return sat[(size_t)y1 * W1 + x1] - sat[(size_t)y0 * W1 + x1] - sat[(size_t)y1 * W1 + x0] + sat[(size_t)y0 * W1 + x0];
-}
-
-// Phase 2 over the Gaussians outside the prefix (key >= thr), in index order: the same wave-cooperative
-// candidate walk, keeping only tiles phase 1 left unfinished (Gaussians whose rect misses every unfinished tile
-// skip the walk).  COUNT: cnt2[g]; EMIT: instances at local index off2[g] + j, first_e = E1 + that, rcnt = cnt2.
-template <bool EMIT>
-__global__ void __launch_bounds__(256) k_phase2(int P, const uint32_t* __restrict__ counters,
-                                                const uint32_t* __restrict__ dkey, const float4* __restrict__ sp,
-                                                int tiles_x, int tiles_y, const uint8_t* __restrict__ unf,
-                                                const uint32_t* __restrict__ sat, uint32_t* __restrict__ cnt2,
-                                                const uint32_t* __restrict__ off2, uint32_t* __restrict__ first_e,
-                                                uint32_t* __restrict__ rcnt, uint32_t* __restrict__ tilekey,
-                                                uint32_t* __restrict__ eg, uint32_t* __restrict__ ikey) {
-    __shared__ CandLDS s_cand[4];
-    __shared__ uint32_t s_cnt[4][64];
-    __shared__ uint32_t s_key[4][64];
-    if (counters[CNT_UNFINISHED] == 0u) return;  // phase 1 finished every tile
-    const uint32_t E1 = counters[CNT_E1];
-    const uint32_t thr = counters[CNT_THR];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int g0 = blockIdx.x * blockDim.x + w * 64;
-    if (g0 >= P) return;
-    const int g = g0 + lane;
-    int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
-    float mx = 0.f, my = 0.f, lthr = 0.f;
-    float4 c4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    bool any = false;
-    if (g < P) {
-        const uint32_t key = dkey[g];
-        s_key[w][lane] = key;
-        if (key >= thr && key != 0xffffffffu) {
-            const float4 s0 = sp[2 * g], s1 = sp[2 * g + 1];
-            sp_rect(s1, x0, y0, x1, y1);
-            any = x1 > x0 && y1 > y0 && sat_rect(sat, tiles_x, x0, y0, x1, y1) != 0u;
-            if (EMIT) {
-                const uint32_t c = cnt2[g];
-                any = any && c != 0u;
-                if (c) { first_e[g] = E1 + off2[g]; rcnt[g] = c; }
-            }
-            if (any) {
-                c4 = make_float4(s0.z, s0.w, s1.x, s1.y);
-                mx = s0.x; my = s0.y;
-                lthr = gs_logf(c4.w / (1.0f / 255.0f));
-            }
-        }
-    }
-    if (!any) { x1 = x0; y1 = y0; }
-    if (!__any(any)) {  // whole wave: nothing to walk
-        if (!EMIT && g < P) cnt2[g] = 0u;
-        return;
-    }
-    s_cnt[w][lane] = 0u;
-    const uint32_t e0 = EMIT ? off2[g0] : 0u;
-    uint32_t running = 0;
-    CandLDS& L = s_cand[w];
-    wave_candidates(L, lane, x0, y0, x1, y1, mx, my, c4, lthr,
-                    [&](int owner, int tx, int ty, bool kept, bool valid, uint32_t item) {
-                        kept = kept && unf[ty * tiles_x + tx] != 0;
-                        const uint64_t km = __ballot(kept);
-                        if (EMIT) {
-                            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-                            if (kept) {
-                                const uint32_t e = e0 + running + (uint32_t)__popcll(km & lt);
-                                tilekey[e] = (uint32_t)(ty * tiles_x + tx);
-                                eg[e] = (uint32_t)(g0 + owner);
-                                ikey[e] = s_key[w][owner];
-                            }
-                            running += (uint32_t)__popcll(km);
-                        } else {
-                            const bool seg_start = valid && (lane == 0 || item == L.pre[owner]);
-                            if (seg_start) {
-                                const uint32_t seg_end_item = L.pre[owner] + (uint32_t)L.area[owner];
-                                const int len = (int)min(seg_end_item - item, (uint32_t)(64 - lane));
-                                const uint64_t seg = (len >= 64 ? ~0ull : ((1ull << len) - 1ull)) << lane;
-                                s_cnt[w][owner] += (uint32_t)__popcll(km & seg);
-                            }
-                            __builtin_amdgcn_wave_barrier();
-                        }
-                    });
-    if (!EMIT && g < P) cnt2[g] = s_cnt[w][lane];
 }
 
 __device__ __forceinline__ float bcast(float v, int lane) {
@@ -771,9 +716,7 @@ __global__ void __launch_bounds__(256) k_filter(PreArgs a) {
 
 void launch_preprocess(const PreArgs& a, hipStream_t s) {
     const bool stage = a.sh != nullptr && a.colors == nullptr && a.M > 0;
-    size_t lds = stage ? (size_t)256 * a.M * 3 * sizeof(float) : 0;
-    const size_t cand = 4 * sizeof(CandLDS) + 4 * 64 * sizeof(uint32_t);
-    if (lds < cand) lds = cand;
+    const size_t lds = stage ? (size_t)256 * a.M * 3 * sizeof(float) : 0;
     if (a.P > 0) k_preprocess<<<(a.P + 255) / 256, 256, lds, s>>>(a);
 }
 void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_t* hist, hipStream_t s) {
@@ -784,31 +727,22 @@ void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, ui
                       uint32_t num_tiles, hipStream_t s) {
     k_depth_cut<<<1, 1024, 0, s>>>(hist, cap, counters, tile_cnt, tile_cnt2, num_tiles);
 }
-void launch_emit(int P, const uint32_t* dkey, const uint32_t* cnt, const uint32_t* off, const float4* sp, int tiles_x,
-                 const uint32_t* counters, uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey, uint32_t* eg,
-                 uint32_t* ikey, hipStream_t s) {
-    const int per_block = 4 * EMIT_RANKS;
-    if (P > 0)
-        k_emit<<<(P + per_block - 1) / per_block, 256, 0, s>>>(P, dkey, cnt, off, sp, tiles_x, counters, first_e, rcnt,
-                                                               tilekey, eg, ikey);
+void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s) {
+    if (a.P <= 0) return;
+    const int waves = (a.P + EMIT_RANKS - 1) / EMIT_RANKS;
+    const int blocks = (waves + 3) / 4;
+    const uint32_t* gate = phase == 2 ? a.counters + CNT_UNFINISHED : nullptr;
+    if (phase == 2) k_bin_count<2><<<blocks, 256, 0, s>>>(a);
+    else k_bin_count<1><<<blocks, 256, 0, s>>>(a);
+    exclusive_scan(a.wtot, (uint32_t)waves, a.wtot, total, scan_tmp, s, gate);
+    if (phase == 2) k_bin_emit<2><<<blocks, 256, 0, s>>>(a);
+    else k_bin_emit<1><<<blocks, 256, 0, s>>>(a);
 }
+size_t bin_scan_temp_bytes(int P) { return scan_temp_bytes((uint32_t)((P + EMIT_RANKS - 1) / EMIT_RANKS)); }
+int bin_waves(int P) { return (P + EMIT_RANKS - 1) / EMIT_RANKS; }
 void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, int tiles_x, int tiles_y,
                            uint32_t* sat, hipStream_t s) {
     k_unfinished_sat<<<1, 1024, 0, s>>>(counters, unfinished, tiles_x, tiles_y, sat);
-}
-void launch_count2(int P, const uint32_t* counters, const uint32_t* dkey, const float4* sp, int tiles_x, int tiles_y,
-                   const uint8_t* unfinished, const uint32_t* sat, uint32_t* cnt2, hipStream_t s) {
-    if (P > 0)
-        k_phase2<false><<<(P + 255) / 256, 256, 0, s>>>(P, counters, dkey, sp, tiles_x, tiles_y, unfinished, sat, cnt2,
-                                                         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
-}
-void launch_emit2(int P, const uint32_t* counters, const uint32_t* dkey, const float4* sp, int tiles_x, int tiles_y,
-                  const uint8_t* unfinished, const uint32_t* sat, const uint32_t* cnt2, const uint32_t* off2,
-                  uint32_t* first_e, uint32_t* rcnt, uint32_t* tilekey, uint32_t* eg, uint32_t* ikey, hipStream_t s) {
-    if (P > 0)
-        k_phase2<true><<<(P + 255) / 256, 256, 0, s>>>(P, counters, dkey, sp, tiles_x, tiles_y, unfinished, sat,
-                                                        const_cast<uint32_t*>(cnt2), off2, first_e, rcnt, tilekey, eg,
-                                                        ikey);
 }
 void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
     if (a.num_tiles <= 0) return;

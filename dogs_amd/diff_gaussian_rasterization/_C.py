@@ -12,8 +12,8 @@ from .. import _lib
 
 _EMPTY_U8 = None
 
-# Depth-prefix binning policy (dg_raster_args.prefix_per_tile): phase-1 capacity = this x tiles; 0 -> the
-# library default (256), < 0 -> bin every instance in one phase.  Module-level so that the forward and the
+# Depth-prefix binning policy (dg_raster_args.prefix_per_tile): phase-1 capacity = this x tiles in tile-rect area
+# units; 0 -> the library default (448), < 0 -> bin every instance in one phase.  Module-level so that the forward and the
 # backward of a view always agree; tests lower it to exercise the phase-2 path.  DOGS_PREFIX_PER_TILE sets it
 # for experiments (tools/prefix_sweep.sh).
 PREFIX_PER_TILE = int(os.environ.get("DOGS_PREFIX_PER_TILE", "0"))

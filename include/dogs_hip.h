@@ -36,9 +36,9 @@ typedef struct {
     int M;              /* sh.size(1) (0 when sh is absent) */
     int W, H;           /* image_width, image_height */
     int prefiltered, antialiasing, debug;
-    int prefix_per_tile;        /* depth-prefix binning: phase-1 capacity = this x tiles (0 -> 256);
-                                   < 0 bins every instance in one phase.  Must match between forward and
-                                   backward of one view. */
+    int prefix_per_tile;        /* depth-prefix binning: phase-1 capacity = this x tiles in tile-rect area
+                                   units (0 -> 448); < 0 bins every instance in one phase.  Must match
+                                   between forward and backward of one view. */
     float scale_modifier, tanfovx, tanfovy;
     const float* bg;            /* [3] */
     const float* means3D;       /* [P,3] */
@@ -113,11 +113,12 @@ uint64_t dg_image_bytes(int W, int H);
 uint64_t dg_binning_bytes(int64_t K, int W, int H);
 
 /* Introspection of the private forward state, for parity tests (device output pointers):
- * the sorted (tile, Gaussian) instance lists -- phase 1 (*e1 entries) then phase 2 (num_instances - *e1),
- * each sorted by tile -- per-Gaussian geometry, per-pixel/per-tile image state (ranges = phase 1). */
+ * the binned (tile, Gaussian) instance lists -- phase 1 (*e1 entries) then phase 2 (dg_binned_instances - *e1),
+ * each grouped by tile in (depth, index) order -- per-Gaussian geometry (tile_count = instances binned for the
+ * Gaussian), per-pixel/per-tile image state (ranges = phase 1).  num_rendered: the forward's first return. */
 int dg_debug_sorted_instances(const dg_raster_args* a, const void* geom, const void* binning, const void* binning2,
-                              int64_t num_instances, uint32_t* tiles_out, uint32_t* gauss_out, int64_t* e1,
-                              dg_stream_t stream);
+                              const void* image, int64_t num_rendered, uint32_t* tiles_out, uint32_t* gauss_out,
+                              int64_t* e1, dg_stream_t stream);
 /* Instances actually binned by the last forward on this geometry block: phase 1 + phase 2 (synchronises). */
 int dg_binned_instances(const void* geom, int P, int64_t* binned, dg_stream_t stream);
 int dg_debug_geometry(const void* geom, int P, float* means2D, float* conic_opacity, float* rgb_invdepth,

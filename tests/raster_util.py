@@ -46,20 +46,22 @@ def hip_forward(s, bg, dev, deg=3, antialiasing=False, colors=None, cov3D=None, 
 
 
 def hip_sorted_instances(out, W, H, dev, P):
-    """(tiles, gaussians, E1): the phase-1 instances (E1, sorted by tile) followed by the phase-2 ones."""
+    """(tiles, gaussians, E1): the phase-1 instances (E1, grouped by tile) followed by the phase-2 ones."""
     import ctypes as C
     from dogs_amd import _lib
     from dogs_amd.diff_gaussian_rasterization import _C
-    K = out[1]
+    L = _lib.load()
+    nb = C.c_int64(0)
+    _lib.check(L.dg_binned_instances(out[5].data_ptr(), int(P), C.byref(nb), _lib.stream_of(dev)))
+    K = int(nb.value)
     a = _lib.DgRasterArgs()
     a.P, a.W, a.H, a.prefix_per_tile = int(P), int(W), int(H), int(_C.PREFIX_PER_TILE)
     tiles = torch.empty(max(K, 1), dtype=torch.int32, device=dev)
     gs = torch.empty(max(K, 1), dtype=torch.int32, device=dev)
     e1 = C.c_int64(0)
-    _lib.check(_lib.load().dg_debug_sorted_instances(C.byref(a), out[5].data_ptr(), out[6].data_ptr(),
-                                                     _lib.ptr(out[8]), out[7].data_ptr(), K, tiles.data_ptr(),
-                                                     gs.data_ptr(),
-                                                     C.byref(e1), _lib.stream_of(dev)))
+    _lib.check(L.dg_debug_sorted_instances(C.byref(a), out[5].data_ptr(), out[6].data_ptr(), _lib.ptr(out[8]),
+                                           out[7].data_ptr(), int(out[0]), tiles.data_ptr(), gs.data_ptr(),
+                                           C.byref(e1), _lib.stream_of(dev)))
     torch.cuda.synchronize()
     return tiles[:K].cpu().numpy().view(np.uint32), gs[:K].cpu().numpy().view(np.uint32), int(e1.value)
 
