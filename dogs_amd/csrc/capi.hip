@@ -147,41 +147,39 @@ Image carve_image(void* base, int W, int H) {
 
 // Per-instance arrays of one binning phase; instances are indexed by emission order.
 struct Binning {
-    uint32_t* tk;    // tile of each instance
-    uint32_t* slot;  // arrival slot in its tile (counting sort); then scratch keys of the long-list depth sort
-    uint32_t* se;    // instances binned by tile, each tile in (depth, index) order
+    uint32_t* se;      // instances binned by tile, each tile in (depth, index) order
     uint32_t* se_tmp;  // scratch values of the long-list depth sort
-    uint32_t* eg;    // Gaussian of each instance
-    uint32_t* ik;    // depth key of each instance
-    uint32_t* dk;    // scratch keys of the long-list depth sort
+    uint32_t* eg;      // Gaussian of each instance
+    uint32_t* ik;      // depth key of each instance
+    uint32_t *dk, *dk2;  // scratch keys of the long-list depth sort
     size_t bytes;
 };
 Binning carve_binning(void* base, int64_t K) {
     Carver c(base);
     Binning b;
     const size_t n = (size_t)(K > 0 ? K : 1);
-    b.tk = c.take<uint32_t>(n);
-    b.slot = c.take<uint32_t>(n);
     b.se = c.take<uint32_t>(n);
     b.se_tmp = c.take<uint32_t>(n);
     b.eg = c.take<uint32_t>(n);
     b.ik = c.take<uint32_t>(n);
     b.dk = c.take<uint32_t>(n);
+    b.dk2 = c.take<uint32_t>(n);
     b.bytes = c.off;
     return b;
 }
-gs::BinArgs bin_args(const Geom& g, const Image& im, int P, int tx, uint32_t cap, const Binning& b) {
+gs::BinArgs bin_args(const Geom& g, const Image& im, int P, int tx, int T, uint32_t cap, const Binning& b,
+                     uint32_t* tile_cnt, uint2* ranges) {
     gs::BinArgs a;
-    a.P = P; a.tiles_x = tx; a.dkey = g.dkey; a.sp = g.sp; a.counters = g.counters; a.unf = im.unfinished;
-    a.sat = im.sat; a.wtot = g.wtot; a.cap = cap; a.first_e = g.first_e; a.rcnt = g.rcnt;
-    a.tilekey = b.tk; a.eg = b.eg; a.ikey = b.ik;
+    a.P = P; a.tiles_x = tx; a.num_tiles = T; a.dkey = g.dkey; a.sp = g.sp; a.counters = g.counters;
+    a.unf = im.unfinished; a.sat = im.sat; a.wtot = g.wtot; a.cap = cap; a.first_e = g.first_e; a.rcnt = g.rcnt;
+    a.eg = b.eg; a.ikey = b.ik; a.tile_cnt = tile_cnt; a.ranges = ranges; a.s_e = b.se;
     return a;
 }
-void bin_and_sort(const Binning& b, int64_t cap, const uint32_t* n_dev, int T, uint2* ranges, uint32_t* tile_cnt,
-                  const uint8_t* only, const uint32_t* gate, uint32_t* long_list, uint32_t* long_cnt, hipStream_t s) {
-    gs::tile_bin((uint32_t)cap, n_dev, b.tk, b.slot, tile_cnt, (uint32_t)T, ranges, b.se, s, gate);
+// per-tile (depth, index) order of a phase's binned lists
+void tile_sort(const Binning& b, int64_t cap, int T, uint2* ranges, const uint8_t* only, const uint32_t* gate,
+               uint32_t* long_list, uint32_t* long_cnt, hipStream_t s) {
     gs::DSortArgs d;
-    d.num_tiles = T; d.ranges = ranges; d.s_e = b.se; d.s_tmp = b.se_tmp; d.k_a = b.dk; d.k_b = b.slot;
+    d.num_tiles = T; d.ranges = ranges; d.s_e = b.se; d.s_tmp = b.se_tmp; d.k_a = b.dk; d.k_b = b.dk2;
     d.ikey = b.ik; d.eg = b.eg; d.n_inst = (uint32_t)(cap > 0 ? cap : 1); d.only = only; d.gate = gate;
     d.long_list = long_list; d.long_cnt = long_cnt;
     gs::tile_depth_sort(d, s);
@@ -388,9 +386,8 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     if (!bbase) return fail("binning allocation failed%s%d");
     *binning_out = bbase;
     Binning b = carve_binning(bbase, C1);
-    const uint32_t* E1_dev = g.counters + gs::CNT_E1;
     if (C1 > 0 && P > 0) {
-        gs::BinArgs ba = bin_args(g, im, P, tx, (uint32_t)C1, b);
+        gs::BinArgs ba = bin_args(g, im, P, tx, T, (uint32_t)C1, b, im.tile_cnt, im.ranges);
         { PROF("emit"); gs::launch_bin(1, ba, g.counters + gs::CNT_E1, g.scan_tmp, s); }
         DBG_SYNC(a->debug, s);
     }
@@ -400,8 +397,7 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     HIP_OK(hipMemcpyAsync(hcs.buf, g.counters, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_OK(hipEventRecord(hcs.ev, s));
     if (C1 > 0 && P > 0) {
-        { PROF("tile_bin"); bin_and_sort(b, C1, E1_dev, T, im.ranges, im.tile_cnt, nullptr, nullptr, im.long_tiles,
-                                         g.counters + gs::CNT_LONG, s); }
+        { PROF("tile_bin"); tile_sort(b, C1, T, im.ranges, nullptr, nullptr, im.long_tiles, g.counters + gs::CNT_LONG, s); }
         DBG_SYNC(a->debug, s);
     } else {
         HIP_OK(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * (size_t)T, s));
@@ -440,15 +436,13 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     if (!b2base) return fail("phase-2 binning allocation failed%s%d");
     *binning2_out = b2base;
     Binning b2 = carve_binning(b2base, K);
-    const uint32_t* K2_dev = g.counters + gs::CNT_K2;
     const uint32_t* gate = g.counters + gs::CNT_UNFINISHED;
     {
         PROF("phase2");
         gs::launch_unfinished_sat(g.counters, im.unfinished, tx, ty, im.sat, s);
-        gs::BinArgs ba = bin_args(g, im, P, tx, (uint32_t)K, b2);
+        gs::BinArgs ba = bin_args(g, im, P, tx, T, (uint32_t)K, b2, im.tile_cnt2, im.ranges2);
         gs::launch_bin(2, ba, g.counters + gs::CNT_K2, g.scan_tmp, s);
-        bin_and_sort(b2, K, K2_dev, T, im.ranges2, im.tile_cnt2, im.unfinished, gate, im.long_tiles,
-                     g.counters + gs::CNT_LONG2, s);
+        tile_sort(b2, K, T, im.ranges2, im.unfinished, gate, im.long_tiles, g.counters + gs::CNT_LONG2, s);
     gs::RenderArgs r2 = r;
         r2.phase = 2;
         r2.K = (uint32_t)K;

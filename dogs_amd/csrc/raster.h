@@ -120,11 +120,12 @@ void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_
 void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, uint32_t* tile_cnt, uint32_t* tile_cnt2,
                       uint32_t num_tiles, hipStream_t s);
 // Binning walk of one phase (phase 1: Gaussians with key < counters[CNT_THR]; phase 2: those past it, only instances
-// in tiles phase 1 left unfinished): k_bin_count (precise cull walk -> rcnt, per-wave totals), exclusive scan of
-// the wave totals (*total = the phase's instance count), k_bin_emit (first_e; tilekey/eg/ikey per instance).
+// in tiles phase 1 left unfinished): k_bin_count (precise cull walk -> rcnt, per-wave totals, per-tile counts),
+// exclusive scan of the wave totals (*total = the phase's instance count), per-tile ranges, k_bin_emit (first_e;
+// eg/ikey per instance; instances grouped by tile in s_e, in arrival order until tile_depth_sort).
 // Phase-2 kernels are gated on counters[CNT_UNFINISHED] (device): no-ops when phase 1 finished every tile.
 struct BinArgs {
-    int P, tiles_x;
+    int P, tiles_x, num_tiles;
     const uint32_t* dkey;
     const float4* sp;
     const uint32_t* counters;    // CNT_THR, CNT_E1 (phase 2), CNT_UNFINISHED
@@ -133,7 +134,10 @@ struct BinArgs {
     uint32_t* wtot;              // [bin_waves(P)] per-wave totals, scanned in place
     uint32_t cap;                // capacity of the instance arrays
     uint32_t *first_e, *rcnt;
-    uint32_t *tilekey, *eg, *ikey;
+    uint32_t *eg, *ikey;         // per instance: Gaussian, depth key
+    uint32_t* tile_cnt;          // [num_tiles] zero on entry: counts, then arrival cursors
+    uint2* ranges;               // [num_tiles] per-tile [start, end) of s_e
+    uint32_t* s_e;               // instances grouped by tile
 };
 void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s);
 size_t bin_scan_temp_bytes(int P);

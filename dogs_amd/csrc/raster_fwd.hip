@@ -355,13 +355,15 @@ __global__ void __launch_bounds__(1024) k_depth_cut(const uint32_t* __restrict__
 
 // Precise per-tile count of each lane's Gaussian (duplicateWithKeys' cull, rasterizer_impl.cu:149-179) by the
 // wave-cooperative candidate walk, into cnt[lane] (LDS, zeroed here).  keep(tx, ty) filters tiles further.
-template <typename Keep>
+template <typename Keep, typename OnKept>
 __device__ __forceinline__ void wave_count(CandLDS& L, uint32_t* cnt, int lane, int x0, int y0, int x1, int y1,
-                                           float mx, float my, float4 co, float thr, Keep&& keep) {
+                                           float mx, float my, float4 co, float thr, Keep&& keep, OnKept&& on_kept) {
     cnt[lane] = 0u;
     wave_candidates(L, lane, x0, y0, x1, y1, mx, my, co, thr,
                     [&](int owner, int tx, int ty, bool kept, bool valid, uint32_t item) {
-                        const uint64_t km = __ballot(kept && keep(tx, ty));
+                        kept = kept && keep(tx, ty);
+                        if (kept) on_kept(tx, ty);
+                        const uint64_t km = __ballot(kept);
                         // first item of each owner segment in this step adds the segment's kept count
                         const bool seg_start = valid && (lane == 0 || item == L.pre[owner]);
                         if (seg_start) {
@@ -413,7 +415,8 @@ __device__ __forceinline__ BinLane bin_lane(const BinArgs& a, int g, int lane, u
     return b;
 }
 
-// Pass 1 of the binning: each wave's precise per-tile counts (rcnt of its Gaussians) and the wave total (wtot).
+// Pass 1 of the binning: each wave's precise per-tile counts (rcnt of its Gaussians), the wave total (wtot) and
+// the per-tile instance counts (tile_cnt, atomics without return).
 template <int PHASE>
 __global__ void __launch_bounds__(256) k_bin_count(BinArgs a) {
     __shared__ CandLDS s_cand[4];
@@ -428,9 +431,9 @@ __global__ void __launch_bounds__(256) k_bin_count(BinArgs a) {
     const BinLane b = bin_lane<PHASE>(a, g, lane, a.counters[CNT_THR], s_key[w]);
     uint32_t c = 0;
     if (__any(b.member)) {
-        wave_count(s_cand[w], s_cnt[w], lane, b.x0, b.y0, b.x1, b.y1, b.mx, b.my, b.co, b.lthr, [&](int tx, int ty) {
-            return PHASE == 1 || a.unf[ty * a.tiles_x + tx] != 0;
-        });
+        wave_count(s_cand[w], s_cnt[w], lane, b.x0, b.y0, b.x1, b.y1, b.mx, b.my, b.co, b.lthr,
+                   [&](int tx, int ty) { return PHASE == 1 || a.unf[ty * a.tiles_x + tx] != 0; },
+                   [&](int tx, int ty) { atomicAdd(&a.tile_cnt[ty * a.tiles_x + tx], 1u); });
         c = s_cnt[w][lane];
         if (b.member) a.rcnt[g] = c;
     }
@@ -441,8 +444,10 @@ __global__ void __launch_bounds__(256) k_bin_count(BinArgs a) {
 }
 
 // Pass 2: wave base = exclusive scan of the wave totals (wtot, scanned in place); first_e of every binned
-// Gaussian, and a second walk writes its instances (tile, Gaussian, depth key) at consecutive indices in
-// (lane, ty, tx) order, so every Gaussian's instances are contiguous: [first_e, first_e + rcnt).
+// Gaussian, and a second walk writes its instances (Gaussian, depth key) at consecutive indices in (lane, ty, tx)
+// order, so every Gaussian's instances are contiguous: [first_e, first_e + rcnt); each instance index is also
+// placed in its tile's list, s_e[ranges[t].x + atomic arrival slot] (counting sort; the order inside a tile is
+// fixed afterwards by k_tile_dsort).
 template <int PHASE>
 __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
     __shared__ CandLDS s_cand[4];
@@ -474,9 +479,10 @@ __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
                         const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
                         if (kept) {
                             const uint32_t e = base + running + (uint32_t)__popcll(km & lt);
-                            a.tilekey[e] = (uint32_t)(ty * a.tiles_x + tx);
+                            const int t = ty * a.tiles_x + tx;
                             a.eg[e] = (uint32_t)(g0 + owner);
                             a.ikey[e] = s_key[w][owner];
+                            a.s_e[a.ranges[t].x + atomicAdd(&a.tile_cnt[t], 1u)] = e;
                         }
                         running += (uint32_t)__popcll(km);
                     });
@@ -735,6 +741,7 @@ void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hi
     if (phase == 2) k_bin_count<2><<<blocks, 256, 0, s>>>(a);
     else k_bin_count<1><<<blocks, 256, 0, s>>>(a);
     exclusive_scan(a.wtot, (uint32_t)waves, a.wtot, total, scan_tmp, s, gate);
+    tile_offsets(a.tile_cnt, (uint32_t)a.num_tiles, a.ranges, s, gate);  // ranges; tile_cnt -> 0 (arrival cursors)
     if (phase == 2) k_bin_emit<2><<<blocks, 256, 0, s>>>(a);
     else k_bin_emit<1><<<blocks, 256, 0, s>>>(a);
 }

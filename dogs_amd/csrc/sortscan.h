@@ -22,12 +22,10 @@ size_t scan_temp_bytes(uint32_t n);
 void exclusive_scan(const uint32_t* in, uint32_t n, uint32_t* out, uint32_t* total, void* temp, hipStream_t stream,
                     const uint32_t* gate = nullptr, const uint32_t* lt_keys = nullptr, const uint32_t* lt_thr = nullptr);
 
-// Counting sort of n (device-side count n_dev, capacity ncap) instances by tile: slot[i] = arrival order of
-// instance i in its tile (atomics), ranges[t] = [start, end) of every tile (all num_tiles written),
-// s_e[ranges[tk[i]].x + slot[i]] = i.  tile_cnt[num_tiles] must be zero.  The order inside a tile is arbitrary
-// until tile_depth_sort.  gate (optional, device): nothing when *gate == 0.
-void tile_bin(uint32_t ncap, const uint32_t* n_dev, const uint32_t* tk, uint32_t* slot, uint32_t* tile_cnt,
-              uint32_t num_tiles, uint2* ranges, uint32_t* s_e, hipStream_t stream, const uint32_t* gate = nullptr);
+// ranges[t] = [start, end) from the per-tile counts (exclusive scan, one block), and tile_cnt reset to 0 so that it
+// serves as the per-tile arrival cursor.  gate (optional, device): nothing when *gate == 0.
+void tile_offsets(uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges, hipStream_t stream,
+                  const uint32_t* gate = nullptr);
 
 // Per-tile sort of instance lists into (depth key, Gaussian index) order (sortscan.hip k_tile_dsort):
 // s_e[ranges[t].x .. ranges[t].y) is reordered in place by (ikey[v], eg[v]), whatever its input order.

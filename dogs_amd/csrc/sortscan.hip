@@ -368,27 +368,19 @@ void exclusive_scan(const uint32_t* in, uint32_t n, uint32_t* out, uint32_t* tot
 }
 
 
-// ---------------- binning by tile: atomic counting sort + exact per-tile order ----------------
-// The instances of a phase are binned by tile with a counting sort (k_tile_count: per-instance slot from an
-// atomic per-tile counter; k_tile_offsets: one-block scan -> ranges; k_tile_scatter).  The order inside a tile
-// is then whatever the atomics produced; k_tile_dsort puts every tile's list into the reference's exact
-// (depth bits, Gaussian index) order -- a total order, so the result does not depend on the atomics.
+// ---------------- binning by tile: counting sort + exact per-tile order ----------------
+// The instances of a phase are binned by tile with a counting sort: the binning walk counts per tile (atomics),
+// k_tile_offsets turns the counts into ranges, and the emission walk places each instance at an atomic arrival
+// slot of its tile (raster_fwd.hip k_bin_emit).  The order inside a tile is then whatever the atomics produced;
+// k_tile_dsort puts every tile's list into the reference's exact (depth bits, Gaussian index) order -- a total
+// order, so the result does not depend on the atomics.
 //   k_tile_dsort       one wave per tile, lists up to DS_WAVE_MAX: items in registers (8 per lane), LSD radix
 //                      over the tile's key range (keys relative to the tile minimum, 8-bit digits, only as many
 //                      passes as the range needs), wave-level peer-mask ranking, LDS scatter.  Runs of equal
 //                      depth keys are put in Gaussian index order by odd-even transposition between neighbours.
 //   k_tile_dsort_long  longer lists (queued by k_tile_dsort): one block per tile, LSD radix through global scratch
 //                      in 256-item chunks; with equal keys it sorts by Gaussian index first and then, stably, by key.
-__global__ void __launch_bounds__(256) k_tile_count(uint32_t ncap, const uint32_t* __restrict__ n_dev,
-                                                    const uint32_t* __restrict__ tk, uint32_t* __restrict__ slot,
-                                                    uint32_t* __restrict__ tile_cnt, const uint32_t* __restrict__ gate) {
-    if (gate && *gate == 0u) return;
-    const uint32_t n = eff_n(ncap, n_dev);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        slot[i] = atomicAdd(&tile_cnt[tk[i]], 1u);
-}
-
-__global__ void __launch_bounds__(1024) k_tile_offsets(const uint32_t* __restrict__ tile_cnt, uint32_t num_tiles,
+__global__ void __launch_bounds__(1024) k_tile_offsets(uint32_t* __restrict__ tile_cnt, uint32_t num_tiles,
                                                        uint2* __restrict__ ranges, const uint32_t* __restrict__ gate) {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_carry;
@@ -411,30 +403,15 @@ __global__ void __launch_bounds__(1024) k_tile_offsets(const uint32_t* __restric
 #pragma unroll
         for (int k = 0; k < 16; k++) { if (k < w) off += s_w[k]; tot += s_w[k]; }
         const uint32_t ex = off + x - v;
-        if (i < num_tiles) ranges[i] = make_uint2(ex, ex + v);
+        if (i < num_tiles) { ranges[i] = make_uint2(ex, ex + v); tile_cnt[i] = 0u; }
         __syncthreads();
         if (t == 0) s_carry += tot;
         __syncthreads();
     }
 }
 
-__global__ void __launch_bounds__(256) k_tile_scatter(uint32_t ncap, const uint32_t* __restrict__ n_dev,
-                                                      const uint32_t* __restrict__ tk, const uint32_t* __restrict__ slot,
-                                                      const uint2* __restrict__ ranges, uint32_t* __restrict__ s_e,
-                                                      const uint32_t* __restrict__ gate) {
-    if (gate && *gate == 0u) return;
-    const uint32_t n = eff_n(ncap, n_dev);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        s_e[ranges[tk[i]].x + slot[i]] = i;
-}
-
-void tile_bin(uint32_t ncap, const uint32_t* n_dev, const uint32_t* tk, uint32_t* slot, uint32_t* tile_cnt,
-              uint32_t num_tiles, uint2* ranges, uint32_t* s_e, hipStream_t stream, const uint32_t* gate) {
-    if (ncap == 0 || num_tiles == 0) return;
-    const uint32_t blocks = (ncap + 255) / 256 < 2048u ? (ncap + 255) / 256 : 2048u;
-    k_tile_count<<<blocks, 256, 0, stream>>>(ncap, n_dev, tk, slot, tile_cnt, gate);
-    k_tile_offsets<<<1, 1024, 0, stream>>>(tile_cnt, num_tiles, ranges, gate);
-    k_tile_scatter<<<blocks, 256, 0, stream>>>(ncap, n_dev, tk, slot, ranges, s_e, gate);
+void tile_offsets(uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges, hipStream_t stream, const uint32_t* gate) {
+    if (num_tiles) k_tile_offsets<<<1, 1024, 0, stream>>>(tile_cnt, num_tiles, ranges, gate);
 }
 
 constexpr int DS_WAVE_MAX = 512;
