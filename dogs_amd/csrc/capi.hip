@@ -167,9 +167,12 @@ Binning carve_binning(void* base, int64_t K) {
     b.bytes = c.off;
     return b;
 }
-gs::BinArgs bin_args(const Geom& g, const Image& im, int P, int tx, int T, uint32_t cap, const Binning& b,
+gs::BinArgs bin_args(const dg_raster_args* r, const Geom& g, const Image& im, int T, uint32_t cap, const Binning& b,
                      uint32_t* tile_cnt, uint2* ranges) {
     gs::BinArgs a;
+    const int P = r->P, tx = tiles_x_of(r->W);
+    a.D = (r->sh && r->M > 0) ? r->D : 0; a.M = r->M; a.means3D = r->means3D; a.campos = r->campos; a.dc = r->dc;
+    a.sh = (r->sh && r->M > 0) ? r->sh : nullptr; a.colors = r->colors; a.rgbi = g.rgbi;
     a.P = P; a.tiles_x = tx; a.num_tiles = T; a.dkey = g.dkey; a.sp = g.sp; a.counters = g.counters;
     a.unf = im.unfinished; a.sat = im.sat; a.wtot = g.wtot; a.cap = cap; a.first_e = g.first_e; a.rcnt = g.rcnt;
     a.eg = b.eg; a.ikey = b.ik; a.tile_cnt = tile_cnt; a.ranges = ranges; a.s_e = b.se;
@@ -216,6 +219,8 @@ int64_t phase1_cap(const dg_raster_args* a, int T, int64_t K_all) {
 struct BwdScratch {
     uint8_t* flag;
     float* rec;
+    uint32_t *live_idx, *live_cnt;  // compacted contributing Gaussians (k_gauss_prep -> k_gauss_live)
+    float* live_acc;
     uint32_t* invd_flag;
     uint32_t* order;  // [T] replay order of the tiles
     size_t bytes;
@@ -226,6 +231,10 @@ BwdScratch carve_bwd(void* base, int64_t K, int P, int T) {
     const size_t n = (size_t)(K > 0 ? K : 1);
     s.flag = c.take<uint8_t>(n);
     s.rec = c.take<float>(12 * n);
+    const size_t np = (size_t)(P > 0 ? P : 1);
+    s.live_idx = c.take<uint32_t>(np);
+    s.live_acc = c.take<float>(10 * np);
+    s.live_cnt = c.take<uint32_t>((np + 255) / 256);
     s.invd_flag = c.take<uint32_t>(4);
     s.order = c.take<uint32_t>((size_t)(T > 0 ? T : 1));
     s.bytes = c.off;
@@ -356,7 +365,7 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     HIP_OK(hipMemsetAsync(g.counters, 0, 64, s));
     gs::PreArgs pre;
     fill_pre(pre, a);
-    pre.radii = radii; pre.sp = g.sp; pre.rgbi = g.rgbi; pre.depthkey = g.dkey; pre.cnt = g.cnt; pre.rcnt = g.rcnt;
+    pre.radii = radii; pre.sp = g.sp; pre.depthkey = g.dkey; pre.cnt = g.cnt; pre.rcnt = g.rcnt;
     pre.hist = g.hist;
     pre.rect_sum = (unsigned long long*)(g.counters + gs::CNT_RECT_LO); pre.err = g.counters + gs::CNT_ERR;
     { PROF("preprocess"); gs::launch_preprocess(pre, s); }
@@ -387,7 +396,7 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     *binning_out = bbase;
     Binning b = carve_binning(bbase, C1);
     if (C1 > 0 && P > 0) {
-        gs::BinArgs ba = bin_args(g, im, P, tx, T, (uint32_t)C1, b, im.tile_cnt, im.ranges);
+        gs::BinArgs ba = bin_args(a, g, im, T, (uint32_t)C1, b, im.tile_cnt, im.ranges);
         { PROF("emit"); gs::launch_bin(1, ba, g.counters + gs::CNT_E1, g.scan_tmp, s); }
         DBG_SYNC(a->debug, s);
     }
@@ -440,7 +449,7 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     {
         PROF("phase2");
         gs::launch_unfinished_sat(g.counters, im.unfinished, tx, ty, im.sat, s);
-        gs::BinArgs ba = bin_args(g, im, P, tx, T, (uint32_t)K, b2, im.tile_cnt2, im.ranges2);
+        gs::BinArgs ba = bin_args(a, g, im, T, (uint32_t)K, b2, im.tile_cnt2, im.ranges2);
         gs::launch_bin(2, ba, g.counters + gs::CNT_K2, g.scan_tmp, s);
         tile_sort(b2, K, T, im.ranges2, im.unfinished, gate, im.long_tiles, g.counters + gs::CNT_LONG2, s);
     gs::RenderArgs r2 = r;
@@ -484,6 +493,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     void* sbase = alloc(user, DG_BUF_BACKWARD, sbytes);
     if (!sbase) return fail("backward scratch allocation failed%s%d");
     BwdScratch sc = carve_bwd(sbase, Kcap, P, T);
+    if (a->M > 0 && !dsh) return fail("dsh output required when M > 0%s%d");
     {
         gs::RenderBwdArgs r;
         r.W = W; r.H = H; r.tiles_x = tx; r.num_tiles = T;
@@ -509,10 +519,10 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     q.means3D = a->means3D; q.scales = a->scales; q.rotations = a->rotations; q.opacities = a->opacities;
     q.dc = a->dc; q.sh = (a->M > 0) ? a->sh : nullptr; q.cov3D_precomp = a->cov3D_precomp;
     q.view = a->viewmatrix; q.proj = a->projmatrix; q.campos = a->campos;
-    q.radii = radii; q.cnt = g.rcnt; q.first_e = g.first_e; q.sp = g.sp; q.rec = sc.rec; q.flag = sc.flag;
+    q.radii = radii; q.dkey = g.dkey; q.cnt = g.rcnt; q.first_e = g.first_e; q.sp = g.sp; q.rec = sc.rec; q.flag = sc.flag;
     q.dmeans2D = dmeans2D; q.dcolors = dcolors; q.dopacity = dopacity; q.dmeans3D = dmeans3D; q.dcov3D = dcov3D;
     q.ddc = ddc; q.dsh = dsh; q.dscales = dscales; q.drot = drot; q.depth = depth;
-    if (q.M > 0 && !dsh) return fail("dsh output required when M > 0%s%d");
+    q.live_idx = sc.live_idx; q.live_acc = sc.live_acc; q.live_cnt = sc.live_cnt;
     { PROF("gauss_bwd"); gs::launch_gauss_bwd(q, s); }
     DBG_SYNC(a->debug, s);
     HIP_OK(hipGetLastError());

@@ -22,7 +22,6 @@ struct PreArgs {
     const float *view, *proj, *campos;
     int* radii;
     float4* sp;         // splat record, 2 x float4 per Gaussian (see SP_* below)
-    float4* rgbi;       // rgb, 1 / view z
     uint32_t* depthkey; // float bits of view z, 0xffffffff when culled (empty tile rect)
     uint32_t* hist;     // [DH_BINS] depth histogram, zeroed here
     uint32_t* cnt;      // tile-rect area (0 when culled)
@@ -104,12 +103,17 @@ struct GaussBwdArgs {
     const float *means3D, *scales, *rotations, *opacities, *dc, *sh, *cov3D_precomp;
     const float *view, *proj, *campos;
     const int* radii;
+    const uint32_t* dkey;    // forward depth keys (bits of the view z)
     const uint32_t* cnt;
     const uint32_t* first_e;
     const float4* sp;        // splat records (conic + AA-scaled opacity)
     const float* rec;
     const uint8_t* flag;
     float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *ddc, *dsh, *dscales, *drot, *depth;
+    // k_gauss_prep -> k_gauss_live: per block of 256 Gaussians, the contributing ones (slots [256 b, 256 b + cnt))
+    uint32_t* live_idx;      // [P]
+    float* live_acc;         // [P][10] record sums
+    uint32_t* live_cnt;      // [ceil(P / 256)]
 };
 
 void launch_preprocess(const PreArgs& a, hipStream_t s);
@@ -135,6 +139,10 @@ struct BinArgs {
     uint32_t cap;                // capacity of the instance arrays
     uint32_t *first_e, *rcnt;
     uint32_t *eg, *ikey;         // per instance: Gaussian, depth key
+    // colour of the binned Gaussians (computeColorFromSH), written by k_bin_emit
+    int D, M;
+    const float *means3D, *campos, *dc, *sh, *colors;
+    float4* rgbi;
     uint32_t* tile_cnt;          // [num_tiles] zero on entry: counts, then arrival cursors
     uint2* ranges;               // [num_tiles] per-tile [start, end) of s_e
     uint32_t* s_e;               // instances grouped by tile

@@ -8,9 +8,10 @@
 //                reduce-scatter (13 cross-lane exchanges instead of 60) and stored once as a 48-B record
 //                at the instance's emission slot -- no float atomics (the chip-wide atomic rate and the
 //                scattered-row penalty make per-instance atomicAdd the wrong tool on MI355X).
-// k_gauss_bwd    a wave per 64 Gaussians first sums their records in emission order (deterministic), then one
-//                thread per Gaussian turns the summed moments into dL/d(mean2D, conic, opacity), then
-//                computeCov2DCUDA + preprocessCUDA backward (backward.cu:149-451) fused in one pass.
+// k_gauss_prep   a wave per 64 Gaussians sums their records (deterministic order), zero-fills the gradient
+//                outputs and compacts the contributing Gaussians;
+// k_gauss_live   one thread per contributing Gaussian turns the summed moments into dL/d(mean2D, conic,
+//                opacity), then computeCov2DCUDA + preprocessCUDA backward (backward.cu:149-451) fused in one pass.
 #include <hip/hip_runtime.h>
 #include "gs_common.h"
 #include "raster.h"
@@ -296,38 +297,33 @@ __global__ void __launch_bounds__(256) k_bwd_prologue(uint32_t* __restrict__ cou
 // ---------------------------------------------------------------------------------------------------
 __device__ __forceinline__ float sq(float x) { return x * x; }
 
-__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, float* lsh, const float (&acc)[10]);
-
-// Sum each Gaussian's instance records (written by k_render_bwd at emission slots [first_e, first_e + cnt)
-// whose flag is set) into acc (registers).  A wave owns 64 consecutive Gaussians; their instances are walked
-// flattened, 64 per step (flag reads coalesced, no lane waits on the longest list), each step's flagged
-// records are parked in LDS, and every owner lane folds its own ones in increasing emission order --
-// the same sequential order as the reference-side sum, so the result is deterministic.
-constexpr uint32_t RS_BIG = 256;
+__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, const float (&acc)[10]);
 
 struct RecSumLDS {
     uint32_t pre[4][64];
     uint32_t e0[4][64];
-    float4 rec[4][64][3];
+    float acc[4][64][11];  // per-Gaussian accumulators (odd stride: conflict-free per-lane rows)
 };
 
+// Sum each Gaussian's instance records (written by k_render_bwd at emission slots [first_e, first_e + cnt) whose
+// flag is set) into acc (registers).  A wave owns 64 consecutive Gaussians; their instances are walked flattened,
+// 64 per step (one per lane; the records of a step are contiguous, so the loads are coalesced, and the flag and
+// the record are loaded together -- an unflagged slot counts zero).  A segmented scan over the lanes (segments =
+// owners, contiguous) sums each owner's part of the step; the segment's last lane adds it to the owner's LDS
+// accumulator.  Fixed summation order: deterministic.
 __device__ __forceinline__ void record_sum(const GaussBwdArgs& a, int idx, RecSumLDS& L, float (&acc)[10]) {
     uint32_t (&s_pre)[4][64] = L.pre;
     uint32_t (&s_e0)[4][64] = L.e0;
-    float4 (&s_rec)[4][64][3] = L.rec;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float* my_acc = L.acc[w][lane];
 #pragma unroll
-    for (int v = 0; v < 10; v++) acc[v] = 0.f;
+    for (int v = 0; v < 10; v++) my_acc[v] = 0.f;
     uint32_t c = 0, e0 = 0;
     if (idx < a.P && a.radii[idx] > 0) {
         c = a.cnt[idx];
         e0 = c ? a.first_e[idx] : 0u;
         if (e0 >= a.K || c > a.K - e0) c = 0;  // defensive: never read outside the record block
     }
-    // Gaussians with long instance lists are summed by the whole wave afterwards (below), so one lane
-    // never folds thousands of records alone while the rest of the wave idles.
-    const uint32_t cbig = c > RS_BIG ? c : 0u;
-    if (cbig) c = 0;
     uint32_t incl = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -335,126 +331,139 @@ __device__ __forceinline__ void record_sum(const GaussBwdArgs& a, int idx, RecSu
         if (lane >= o) incl += y;
     }
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    const uint32_t mybeg = incl - c;
-    s_pre[w][lane] = mybeg;
+    s_pre[w][lane] = incl - c;
     s_e0[w][lane] = e0;
     __builtin_amdgcn_wave_barrier();
     for (uint32_t i0 = 0; i0 < total; i0 += 64) {
         const uint32_t item = i0 + (uint32_t)lane;
-        bool f = false;
-        if (item < total) {
+        const bool valid = item < total;
+        int owner = 64 + lane;  // invalid lanes: a segment of their own
+        float v[10];
+#pragma unroll
+        for (int k = 0; k < 10; k++) v[k] = 0.f;
+        if (valid) {
             int lo = 0;
 #pragma unroll
             for (int step = 32; step > 0; step >>= 1)
                 if (s_pre[w][lo + step] <= item) lo += step;
+            owner = lo;
             const uint32_t e = s_e0[w][lo] + (item - s_pre[w][lo]);
-            f = a.flag[e] != 0;
+            const bool f = a.flag[e] != 0;
+            const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
+            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
             if (f) {
-                const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
-                s_rec[w][lane][0] = r[0];
-                s_rec[w][lane][1] = r[1];
-                s_rec[w][lane][2] = r[2];
+                v[0] = r0.x; v[1] = r0.y; v[2] = r0.z; v[3] = r0.w; v[4] = r1.x;
+                v[5] = r1.y; v[6] = r1.z; v[7] = r1.w; v[8] = r2.x; v[9] = r2.y;
             }
         }
-        const uint64_t fm = __ballot(f);
-        __builtin_amdgcn_wave_barrier();
-        // this lane's items within the step: [lo, hi) relative to i0
-        const uint32_t lo = mybeg > i0 ? mybeg - i0 : 0u;
-        const uint32_t end = mybeg + c;
-        const uint32_t hi = end < i0 + 64 ? (end > i0 ? end - i0 : 0u) : 64u;
-        uint64_t m = 0;
-        if (hi > lo) m = fm & ((hi == 64 ? ~0ull : ((1ull << hi) - 1ull)) & (~0ull << lo));
-        while (m) {
-            const int b = __ffsll((unsigned long long)m) - 1;
-            m &= m - 1;
-            const float4 r0 = s_rec[w][b][0], r1 = s_rec[w][b][1], r2 = s_rec[w][b][2];
-            acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w; acc[4] += r1.x;
-            acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w; acc[8] += r2.x; acc[9] += r2.y;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int up = __shfl_up(owner, d);  // every lane shuffles (a bpermute from an inactive lane reads 0)
+            const bool same = lane >= d && up == owner;
+#pragma unroll
+            for (int k = 0; k < 10; k++) {
+                const float t = __shfl_up(v[k], d);
+                v[k] += same ? t : 0.f;
+            }
+        }
+        const int next = __shfl_down(owner, 1);
+        if (valid && (lane == 63 || next != owner)) {  // the segment's last lane: one per owner and step
+            float* dst = L.acc[w][owner];
+#pragma unroll
+            for (int k = 0; k < 10; k++) dst[k] += v[k];
         }
         __builtin_amdgcn_wave_barrier();
     }
-    uint64_t bm = __ballot(cbig != 0u);
-    while (bm) {
-        const int b = __ffsll((unsigned long long)bm) - 1;
-        bm &= bm - 1;
-        const uint32_t eb = (uint32_t)__builtin_amdgcn_readlane((int)e0, b);
-        const uint32_t cb = (uint32_t)__builtin_amdgcn_readlane((int)cbig, b);
-        float part[10];
 #pragma unroll
-        for (int v = 0; v < 10; v++) part[v] = 0.f;
-        for (uint32_t i = (uint32_t)lane; i < cb; i += 64) {
-            const uint32_t e = eb + i;
-            if (a.flag[e]) {
-                const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
-                const float4 r0 = r[0], r1 = r[1], r2 = r[2];
-                part[0] += r0.x; part[1] += r0.y; part[2] += r0.z; part[3] += r0.w; part[4] += r1.x;
-                part[5] += r1.y; part[6] += r1.z; part[7] += r1.w; part[8] += r2.x; part[9] += r2.y;
-            }
-        }
-        int slot;
-        const float tot = wave_reduce10(part, lane, slot);
-        float* st = reinterpret_cast<float*>(&s_rec[w][0][0]);
-        if (slot >= 0) st[slot] = tot;
-        __builtin_amdgcn_wave_barrier();
-        if (lane == b) {
-#pragma unroll
-            for (int v = 0; v < 10; v++) acc[v] = st[v];
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
+    for (int k = 0; k < 10; k++) acc[k] = my_acc[k];
 }
 
 // Block of 256 Gaussians; the [256][M][3] SH slab is staged through LDS so both the coefficient loads
 // and the dL/dsh stores are coalesced (a per-thread 180-B stride touches 64 lines per wave instruction).
-// One block of 256 Gaussians: (1) each wave sums its 64 Gaussians' instance records (record_sum, LDS scratch at
-// the head of the block's LDS), (2) the [256][M][3] SH slab is staged through the same LDS, (3) one thread per
-// Gaussian runs the per-Gaussian backward.  The record sums never leave registers.
-__global__ void __launch_bounds__(256) k_gauss_bwd(GaussBwdArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float s_sh[];
-    const int t = threadIdx.x;
-    const int base = blockIdx.x * 256;
-    const int idx = base + t;
-    const int nloc = (a.P - base) < 256 ? (a.P - base) : 256;
-    const int M = a.M;
-    const int slab = nloc * M * 3;  // floats
-    float acc[10];
-    record_sum(a, idx, *reinterpret_cast<RecSumLDS*>(s_sh), acc);
-    __syncthreads();  // the record-sum scratch is reused by the SH slab
-    if (a.sh && M > 0) {
-        const float* src = a.sh + (size_t)base * M * 3;
-        const int n4 = slab >> 2;  // base*M*3*4 bytes is a multiple of 16 (256*M*12)
-        const float4* src4 = reinterpret_cast<const float4*>(src);
-        float4* dst4 = reinterpret_cast<float4*>(s_sh);
-        if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0u) {
-            stage_lds_dma(dst4, src4, n4, t);
-            for (int i = (n4 << 2) + t; i < slab; i += 256) s_sh[i] = src[i];
-        } else {  // a caller's unaligned view: plain copy
-            for (int i = t; i < slab; i += 256) s_sh[i] = src[i];
-        }
+// The per-Gaussian backward in two passes, so that only the contributing Gaussians pay for the heavy math:
+// k_gauss_prep  one block per 256 consecutive Gaussians: zero-fills the block's slices of the nine gradient
+//               outputs (coalesced 16-B stores), writes the view depth, sums every Gaussian's instance records
+//               (record_sum, a wave per 64) and compacts the contributing ones -- any record sum nonzero -- into the
+//               block's slot list (index + the 10 sums).  A Gaussian without contribution has exactly zero
+//               gradients, as in the reference.
+// k_gauss_live  one wave per prep block: the per-Gaussian backward of its compacted Gaussians.
+__device__ __forceinline__ void zero_slice(float* out, size_t first, size_t count) {
+    float* p = out + first;
+    size_t i = threadIdx.x;
+    if ((reinterpret_cast<uintptr_t>(p) & 15u) == 0u) {
+        float4* p4 = reinterpret_cast<float4*>(p);
+        for (; i < count / 4; i += 256) p4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        i = (count & ~(size_t)3) + threadIdx.x;
     }
+    for (; i < count; i += 256) p[i] = 0.f;
+}
+
+__global__ void __launch_bounds__(256) k_gauss_prep(GaussBwdArgs a) {
+    __shared__ RecSumLDS s_rs;
+    __shared__ uint32_t s_wcnt[4];
+    const int base = blockIdx.x * 256;
+    const int idx = base + threadIdx.x;
+    const size_t nloc = (size_t)((a.P - base) < 256 ? (a.P - base) : 256);
+    const size_t b0 = (size_t)base, M = (size_t)a.M;
+    zero_slice(a.dmeans2D, 3 * b0, 3 * nloc);
+    zero_slice(a.dcolors, 3 * b0, 3 * nloc);
+    zero_slice(a.dopacity, b0, nloc);
+    zero_slice(a.dmeans3D, 3 * b0, 3 * nloc);
+    zero_slice(a.dcov3D, 6 * b0, 6 * nloc);
+    zero_slice(a.ddc, 3 * b0, 3 * nloc);
+    if (a.dsh && M) zero_slice(a.dsh, 3 * M * b0, 3 * M * nloc);
+    zero_slice(a.dscales, 3 * b0, 3 * nloc);
+    zero_slice(a.drot, 4 * b0, 4 * nloc);
+    float acc[10];
+#ifdef DG_ABLATE_RECSUM  // timing experiment only: no records summed (every Gaussian takes the zero path)
+    for (int v = 0; v < 10; v++) acc[v] = 0.f;
+#else
+    record_sum(a, idx, s_rs, acc);
+#endif
+    bool live = false;
+    if (idx < a.P) {
+        const uint32_t key = a.dkey[idx];
+        const int rad = a.radii[idx];
+        // depth: the view z of the forward (its depth key) for rendered Gaussians, 0 otherwise
+        a.depth[idx] = (rad > 0 && key != 0xffffffffu) ? __uint_as_float(key) : 0.f;
+#pragma unroll
+        for (int v = 0; v < 10; v++) live |= acc[v] != 0.0f;
+        live = live && rad > 0;
+    }
+    // block-local compaction of the contributing Gaussians, in index order
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t lm = __ballot(live);
+    if (lane == 0) s_wcnt[w] = (uint32_t)__popcll(lm);
     __syncthreads();
-    if (idx < a.P) gauss_bwd_one(a, idx, s_sh + t * M * 3, acc);
-    __syncthreads();
-    if (a.dsh && M > 0) {
-        float* dst = a.dsh + (size_t)base * M * 3;
-        const int n4 = slab >> 2;
-        float4* dst4 = reinterpret_cast<float4*>(dst);
-        const float4* src4 = reinterpret_cast<const float4*>(s_sh);
-        if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0u) {
-            for (int i = t; i < n4; i += 256) dst4[i] = src4[i];
-            for (int i = (n4 << 2) + t; i < slab; i += 256) dst[i] = s_sh[i];
-        } else {
-            for (int i = t; i < slab; i += 256) dst[i] = s_sh[i];
-        }
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) { if (q < w) off += s_wcnt[q]; tot += s_wcnt[q]; }
+    if (live) {
+        const uint32_t j = (uint32_t)base + off + (uint32_t)__popcll(lm & (lane ? (~0ull >> (64 - lane)) : 0ull));
+        a.live_idx[j] = (uint32_t)idx;
+#pragma unroll
+        for (int v = 0; v < 10; v++) a.live_acc[(size_t)j * 10 + v] = acc[v];
+    }
+    if (threadIdx.x == 0) a.live_cnt[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(64) k_gauss_live(GaussBwdArgs a) {
+    const uint32_t n = a.live_cnt[blockIdx.x];
+    const uint32_t base = blockIdx.x * 256u;
+    for (uint32_t j = threadIdx.x; j < n; j += 64) {
+        const uint32_t idx = a.live_idx[base + j];
+        float acc[10];
+#pragma unroll
+        for (int v = 0; v < 10; v++) acc[v] = a.live_acc[(size_t)(base + j) * 10 + v];
+        gauss_bwd_one(a, (int)idx, acc);
     }
 }
 
-// One Gaussian; `lsh` is its [M][3] SH row in LDS, overwritten in place with dL/dsh.
-__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, float* lsh, const float (&sums)[10]) {
+// One contributing Gaussian: every gradient output of it (dL/dsh row included) is written here.
+__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, const float (&sums)[10]) {
     const int M = a.M;
-    // every per-Gaussian input is loaded up front: one HBM round trip instead of three dependent ones
-    // (radii -> splat -> means -> scales/rotations); culled Gaussians read bytes they ignore
-    const int rad = a.radii[idx];
+    float* dsh_row = a.dsh ? a.dsh + (size_t)idx * M * 3 : nullptr;
+    // every per-Gaussian input is loaded up front: one HBM round trip instead of dependent ones
     const float4 sp0 = a.sp[2 * (size_t)idx], sp1 = a.sp[2 * (size_t)idx + 1];
     const f3 mean = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
     f3 scl = {0.f, 0.f, 0.f};
@@ -466,18 +475,6 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
     const float opac = a.antialiasing ? a.opacities[idx] : 0.f;
     f3 dcv = {0.f, 0.f, 0.f};
     if (a.sh) dcv = {a.dc[3 * idx], a.dc[3 * idx + 1], a.dc[3 * idx + 2]};
-    if (!(rad > 0)) {
-        for (int v = 0; v < 3; v++) {
-            a.dmeans2D[3 * idx + v] = 0.f; a.dcolors[3 * idx + v] = 0.f; a.dmeans3D[3 * idx + v] = 0.f;
-            a.ddc[3 * idx + v] = 0.f; a.dscales[3 * idx + v] = 0.f;
-        }
-        for (int v = 0; v < 6; v++) a.dcov3D[6 * idx + v] = 0.f;
-        for (int v = 0; v < 4; v++) a.drot[4 * idx + v] = 0.f;
-        a.dopacity[idx] = 0.f;
-        a.depth[idx] = 0.f;
-        for (int v = 0; v < 3 * M; v++) lsh[v] = 0.f;
-        return;
-    }
     // ---- records -> dL/d(mean2D, conic, opacity, color, invdepth): summed by the wave (see below)
     float acc[10];
 #pragma unroll
@@ -515,7 +512,6 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
     const float h_x = a.focal_x, h_y = a.focal_y;
     Cov2DState st;
     const f3 cv = cov2d_fwd(mean, h_x, h_y, a.tanfovx, a.tanfovy, cov3D, a.view, &st);
-    a.depth[idx] = tp4x3(mean, a.view).z;
     float c_xx = cv.x, c_xy = cv.y, c_yy = cv.z;
     const float h_var = 0.3f;
     float d_inside_root = 0.f;
@@ -594,7 +590,7 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
 
     // ---- computeColorFromSH backward (backward.cu:23-144); clamped flags recomputed from the forward rgb
     if (a.sh) {
-        const float* sh = lsh;
+        const float* __restrict__ sh = a.sh + (size_t)idx * M * 3;
         const float d0p[3] = {dcv.x, dcv.y, dcv.z};
         const int deg = a.D;
         const f3 dir_orig = {mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]};
@@ -663,8 +659,8 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
         }
 #undef SHV
         // dL/dsh overwrites the staged coefficients in place (all reads of them are above)
-        for (int k = 0; k < M; k++)
-            for (int ch = 0; ch < 3; ch++) lsh[3 * k + ch] = k < nb ? basis[k] * dRGB[ch] : 0.0f;
+        for (int k = 0; k < nb; k++)
+            for (int ch = 0; ch < 3; ch++) dsh_row[3 * k + ch] = basis[k] * dRGB[ch];  // the rest stays zero
         const f3 ddir = {dx[0] * dRGB[0] + dx[1] * dRGB[1] + dx[2] * dRGB[2], dy[0] * dRGB[0] + dy[1] * dRGB[1] + dy[2] * dRGB[2],
                          dz[0] * dRGB[0] + dz[1] * dRGB[1] + dz[2] * dRGB[2]};
         // dnormvdv (auxiliary.h:118-128)
@@ -676,7 +672,6 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
         dmean.z += (-v.x * v.z * ddir.x - v.y * v.z * ddir.y + (sum2 - v.z * v.z) * ddir.z) * invsum32;
     } else {
         for (int ch = 0; ch < 3; ch++) a.ddc[3 * idx + ch] = 0.f;
-        for (int v = 0; v < 3 * M; v++) lsh[v] = 0.f;
     }
     a.dmeans3D[3 * idx + 0] = dmean.x;
     a.dmeans3D[3 * idx + 1] = dmean.y;
@@ -718,9 +713,10 @@ void launch_render_bwd(const RenderBwdArgs& a, uint32_t* counters, hipStream_t s
     }
 }
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s) {
-    size_t lds = (size_t)256 * (a.M > 0 ? a.M : 0) * 3 * sizeof(float);
-    if (lds < sizeof(RecSumLDS)) lds = sizeof(RecSumLDS);
-    if (a.P > 0) k_gauss_bwd<<<(a.P + 255) / 256, 256, lds, s>>>(a);
+    if (a.P <= 0) return;
+    const int blocks = (a.P + 255) / 256;
+    k_gauss_prep<<<blocks, 256, 0, s>>>(a);
+    k_gauss_live<<<blocks, 64, 0, s>>>(a);
 }
 
 }  // namespace gs

@@ -146,8 +146,9 @@ __device__ __forceinline__ void wave_candidates(CandLDS& L, int lane, int x0, in
     __builtin_amdgcn_wave_barrier();
 }
 
-// Returns the tile-rect area (0 when culled); fills the geometry outputs of kept Gaussians.
-__device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, const float* lsh) {
+// Returns the tile-rect area (0 when culled); fills the geometry outputs of kept Gaussians.  The colour
+// (computeColorFromSH) is not evaluated here: only binned Gaussians need it, and k_bin_emit computes it for them.
+__device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx) {
     a.radii[idx] = 0;
     a.depthkey[idx] = 0xffffffffu;
     a.cnt[idx] = 0u;
@@ -162,8 +163,6 @@ __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, co
         q = {a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]};
     }
     const float opac = a.opacities[idx];
-    f3 dcv = {0.f, 0.f, 0.f};
-    if (!a.colors) dcv = {a.dc[3 * idx], a.dc[3 * idx + 1], a.dc[3 * idx + 2]};
     // in_frustum (auxiliary.h:150-175)
     const f3 pv = tp4x3(po, a.view);
     if (pv.z <= 0.2f) {
@@ -203,51 +202,26 @@ __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, co
     get_rect_s(px, py, ir, a.tiles_x, a.tiles_y, x0, y0, x1, y1);
     const uint32_t area = (uint32_t)(x1 - x0) * (uint32_t)(y1 - y0);
     if (area == 0) return 0;
-    f3 col;
-    if (a.colors) {
-        col = {a.colors[3 * idx], a.colors[3 * idx + 1], a.colors[3 * idx + 2]};
-    } else {
-        col = sh_to_rgb(po, a.campos, a.sh ? a.D : 0, dcv, lsh, nullptr);
-    }
     const float4 co = make_float4(conic.x, conic.y, conic.z, opac * h_scale);
     a.radii[idx] = ir;
     a.sp[2 * idx] = make_float4(px, py, co.x, co.y);
     a.sp[2 * idx + 1] = make_float4(co.z, co.w, __uint_as_float((uint32_t)x0 | ((uint32_t)x1 << 16)),
                                     __uint_as_float((uint32_t)y0 | ((uint32_t)y1 << 16)));
-    a.rgbi[idx] = make_float4(col.x, col.y, col.z, 1.f / pv.z);
     a.depthkey[idx] = __float_as_uint(pv.z);
     a.cnt[idx] = area;
     return area;
 }
 
-// The block's [256][M][3] SH slab is staged through LDS with 16-B coalesced loads; read per thread at a
-// 45-dword stride (odd -> conflict-free) instead of 45 strided global loads per lane.  The precise per-tile
-// cull is not done here: only the prefix Gaussians are walked, by k_emit.
+// One thread per Gaussian.  Neither the precise per-tile cull nor the colour is computed here: only the binned
+// Gaussians need them, and the binning walk (k_bin_count / k_bin_emit) computes them for those.
 __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float s_sh[];
     __shared__ unsigned long long s_sum[4];
     const int t = threadIdx.x;
     const int base = blockIdx.x * 256;
     const int idx = base + t;
-    const int nloc = (a.P - base) < 256 ? (a.P - base) : 256;
     for (int i = base + t; i < DH_BINS; i += gridDim.x * 256) a.hist[i] = 0u;  // for k_depth_hist
-    const bool stage = a.sh != nullptr && a.colors == nullptr && a.M > 0;
-    if (stage) {
-        const int slab = nloc * a.M * 3;
-        const float* src = a.sh + (size_t)base * a.M * 3;
-        const int n4 = slab >> 2;
-        const float4* src4 = reinterpret_cast<const float4*>(src);
-        float4* dst4 = reinterpret_cast<float4*>(s_sh);
-        if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0u) {
-            stage_lds_dma(dst4, src4, n4, t);
-            for (int i = (n4 << 2) + t; i < slab; i += 256) s_sh[i] = src[i];
-        } else {  // a caller's unaligned view: plain copy
-            for (int i = t; i < slab; i += 256) s_sh[i] = src[i];
-        }
-    }
-    __syncthreads();
     uint32_t area = 0;
-    if (idx < a.P) area = preprocess_one(a, idx, stage ? s_sh + t * a.M * 3 : nullptr);
+    if (idx < a.P) area = preprocess_one(a, idx);
     unsigned long long v = area;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -470,7 +444,20 @@ __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
     }
     const uint32_t wt = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (wt == 0u || base + wt > a.cap) return;  // nothing kept; (capacity: never with consistent inputs)
-    if (b.member && c) a.first_e[g] = (PHASE == 2 ? a.counters[CNT_E1] : 0u) + base + incl - c;
+    if (b.member && c) {
+        a.first_e[g] = (PHASE == 2 ? a.counters[CNT_E1] : 0u) + base + incl - c;
+        // colour + inverse depth of a binned Gaussian (computeColorFromSH, forward.cu:24-76; 1 / view z)
+        const uint32_t key = s_key[w][lane];
+        f3 col;
+        if (a.colors) {
+            col = {a.colors[3 * g], a.colors[3 * g + 1], a.colors[3 * g + 2]};
+        } else {
+            const f3 po = {a.means3D[3 * g], a.means3D[3 * g + 1], a.means3D[3 * g + 2]};
+            const f3 d0 = {a.dc[3 * g], a.dc[3 * g + 1], a.dc[3 * g + 2]};
+            col = sh_to_rgb(po, a.campos, a.sh ? a.D : 0, d0, a.sh ? a.sh + (size_t)g * a.M * 3 : nullptr, nullptr);
+        }
+        a.rgbi[g] = make_float4(col.x, col.y, col.z, 1.f / __uint_as_float(key));
+    }
     uint32_t running = 0;
     wave_candidates(s_cand[w], lane, b.x0, b.y0, b.x1, b.y1, b.mx, b.my, b.co, b.lthr,
                     [&](int owner, int tx, int ty, bool kept, bool, uint32_t) {
@@ -721,9 +708,7 @@ __global__ void __launch_bounds__(256) k_filter(PreArgs a) {
 }
 
 void launch_preprocess(const PreArgs& a, hipStream_t s) {
-    const bool stage = a.sh != nullptr && a.colors == nullptr && a.M > 0;
-    const size_t lds = stage ? (size_t)256 * a.M * 3 * sizeof(float) : 0;
-    if (a.P > 0) k_preprocess<<<(a.P + 255) / 256, 256, lds, s>>>(a);
+    if (a.P > 0) k_preprocess<<<(a.P + 255) / 256, 256, 0, s>>>(a);
 }
 void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_t* hist, hipStream_t s) {
     const int per = DH_THREADS * DH_ITEMS;

@@ -4,6 +4,7 @@ pybind11 functions in rasterize_points.cu; tensors are torch tensors on a HIP de
 from __future__ import annotations
 
 import ctypes as C
+import math
 import os
 
 import torch
@@ -103,16 +104,12 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
         z = lambda *s: torch.zeros(s, **fopt)  # noqa: E731
         return (z(0, 3), z(0, 3), z(0, 1), z(0, 3), z(0, 6), z(0, 1, 3), z(0, M, 3), z(0, 3), z(0, 4), z(0, 1))
     with torch.cuda.device(dev):
-        dmeans2D = torch.empty((P, 3), **fopt)
-        dcolors = torch.empty((P, 3), **fopt)
-        dopacity = torch.empty((P, 1), **fopt)
-        dmeans3D = torch.empty((P, 3), **fopt)
-        dcov3D = torch.empty((P, 6), **fopt)
-        ddc = torch.empty((P, 1, 3), **fopt)
-        dsh = torch.empty((P, M, 3), **fopt)
-        dscales = torch.empty((P, 3), **fopt)
-        drot = torch.empty((P, 4), **fopt)
-        depth = torch.empty((P, 1), **fopt)
+        # one buffer, outputs back to back in the C ABI's order: the library zero-fills it with a single memset
+        shapes = [(P, 3), (P, 3), (P, 1), (P, 3), (P, 6), (P, 1, 3), (P, M, 3), (P, 3), (P, 4), (P, 1)]
+        sizes = [math.prod(sh) for sh in shapes]
+        buf = torch.empty(sum(sizes), **fopt)
+        dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, ddc, dsh, dscales, drot, depth = (
+            t.view(sh) for t, sh in zip(torch.split(buf, sizes), shapes))
         a, keep = _args(P, degree, M, W, H, background, means3D, colors, opacities, scales, rotations, scale_modifier,
                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dc, sh, campos, False,
                         antialiasing, debug)
