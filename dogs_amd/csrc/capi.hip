@@ -494,8 +494,24 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     if (!sbase) return fail("backward scratch allocation failed%s%d");
     BwdScratch sc = carve_bwd(sbase, Kcap, P, T);
     if (a->M > 0 && !dsh) return fail("dsh output required when M > 0%s%d");
+    // the nine gradient outputs back to back (the Python side allocates them as views of one buffer): the replay
+    // zero-fills them while it is VALU-bound; otherwise k_gauss_prep does
+    size_t zero_count = 0;
+    {
+        const size_t Pz = (size_t)P, Mz = (size_t)(a->M > 0 ? a->M : 0);
+        float* const ptrs[9] = {dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, ddc, dsh, dscales, drot};
+        const size_t counts[9] = {3 * Pz, 3 * Pz, Pz, 3 * Pz, 6 * Pz, 3 * Pz, 3 * Mz * Pz, 3 * Pz, 4 * Pz};
+        bool adjacent = (reinterpret_cast<uintptr_t>(dmeans2D) & 15u) == 0u;
+        size_t total = counts[0];
+        for (int i = 1; i < 9; i++) {
+            adjacent = adjacent && (counts[i] == 0 || ptrs[i] == dmeans2D + total);
+            total += counts[i];
+        }
+        if (adjacent) zero_count = total;
+    }
     {
         gs::RenderBwdArgs r;
+        r.zero_base = zero_count ? dmeans2D : nullptr; r.zero_count = zero_count;
         r.W = W; r.H = H; r.tiles_x = tx; r.num_tiles = T;
         r.K = (uint32_t)Kcap; r.K1 = (uint32_t)C1; r.P = (uint32_t)P;
         r.ranges = im.ranges; r.max_contrib = im.max_contrib; r.s_e = s_e; r.eg = b.eg;
@@ -523,6 +539,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     q.dmeans2D = dmeans2D; q.dcolors = dcolors; q.dopacity = dopacity; q.dmeans3D = dmeans3D; q.dcov3D = dcov3D;
     q.ddc = ddc; q.dsh = dsh; q.dscales = dscales; q.drot = drot; q.depth = depth;
     q.live_idx = sc.live_idx; q.live_acc = sc.live_acc; q.live_cnt = sc.live_cnt;
+    q.outputs_zeroed = zero_count != 0;
     { PROF("gauss_bwd"); gs::launch_gauss_bwd(q, s); }
     DBG_SYNC(a->debug, s);
     HIP_OK(hipGetLastError());

@@ -94,6 +94,8 @@ struct RenderBwdArgs {
     float* rec;              // [K][12] per-instance gradient record
     uint8_t* flag;           // [K] record written
     uint32_t* order;         // [num_tiles] scratch: tiles in descending replay length (launch order)
+    float* zero_base;        // optional: [zero_count] floats zero-filled by the replay waves (gradient outputs)
+    size_t zero_count;
 };
 
 struct GaussBwdArgs {
@@ -110,6 +112,7 @@ struct GaussBwdArgs {
     const float* rec;
     const uint8_t* flag;
     float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *ddc, *dsh, *dscales, *drot, *depth;
+    int outputs_zeroed;      // the nine gradient outputs were zero-filled by k_render_bwd
     // k_gauss_prep -> k_gauss_live: per block of 256 Gaussians, the contributing ones (slots [256 b, 256 b + cnt))
     uint32_t* live_idx;      // [P]
     float* live_acc;         // [P][10] record sums

@@ -260,6 +260,19 @@ __global__ void __launch_bounds__(1024) k_tile_order(RenderBwdArgs a) {
 __global__ void __launch_bounds__(256) BWD_WPE_ATTR k_render_bwd(RenderBwdArgs a) {
     __shared__ float4 s_b[4][64][3];
     const int lane = threadIdx.x & 63;
+    if (a.zero_base) {
+        // The replay is VALU-bound and leaves HBM mostly idle: each wave zero-fills its share of the gradient
+        // outputs (fire-and-forget 16-B stores) for the per-Gaussian pass, which then writes only the contributing
+        // Gaussians.  Shares are whole 1-KiB chunks, so every store is aligned.
+        const size_t nw = (size_t)gridDim.x * 4, gw = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+        const size_t n4 = a.zero_count / 4;
+        const size_t per = ((n4 + nw - 1) / nw + 63) & ~(size_t)63;
+        float4* z4 = reinterpret_cast<float4*>(a.zero_base);
+        const size_t e4 = (gw + 1) * per < n4 ? (gw + 1) * per : n4;
+        for (size_t i = gw * per + lane; i < e4; i += 64) z4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gw == 0)
+            for (size_t i = (n4 << 2) + lane; i < a.zero_count; i += 64) a.zero_base[i] = 0.f;
+    }
     const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (slot >= a.num_tiles) return;
     const int tile = a.order ? (int)a.order[slot] : slot;
@@ -382,7 +395,8 @@ __device__ __forceinline__ void record_sum(const GaussBwdArgs& a, int idx, RecSu
 // and the dL/dsh stores are coalesced (a per-thread 180-B stride touches 64 lines per wave instruction).
 // The per-Gaussian backward in two passes, so that only the contributing Gaussians pay for the heavy math:
 // k_gauss_prep  one block per 256 consecutive Gaussians: zero-fills the block's slices of the nine gradient
-//               outputs (coalesced 16-B stores), writes the view depth, sums every Gaussian's instance records
+//               outputs (coalesced 16-B stores; skipped when k_render_bwd already zero-filled them), writes the view
+//               depth, sums every Gaussian's instance records
 //               (record_sum, a wave per 64) and compacts the contributing ones -- any record sum nonzero -- into the
 //               block's slot list (index + the 10 sums).  A Gaussian without contribution has exactly zero
 //               gradients, as in the reference.
@@ -405,15 +419,17 @@ __global__ void __launch_bounds__(256) k_gauss_prep(GaussBwdArgs a) {
     const int idx = base + threadIdx.x;
     const size_t nloc = (size_t)((a.P - base) < 256 ? (a.P - base) : 256);
     const size_t b0 = (size_t)base, M = (size_t)a.M;
-    zero_slice(a.dmeans2D, 3 * b0, 3 * nloc);
-    zero_slice(a.dcolors, 3 * b0, 3 * nloc);
-    zero_slice(a.dopacity, b0, nloc);
-    zero_slice(a.dmeans3D, 3 * b0, 3 * nloc);
-    zero_slice(a.dcov3D, 6 * b0, 6 * nloc);
-    zero_slice(a.ddc, 3 * b0, 3 * nloc);
-    if (a.dsh && M) zero_slice(a.dsh, 3 * M * b0, 3 * M * nloc);
-    zero_slice(a.dscales, 3 * b0, 3 * nloc);
-    zero_slice(a.drot, 4 * b0, 4 * nloc);
+    if (!a.outputs_zeroed) {  // else k_render_bwd zero-filled them (contiguous outputs)
+        zero_slice(a.dmeans2D, 3 * b0, 3 * nloc);
+        zero_slice(a.dcolors, 3 * b0, 3 * nloc);
+        zero_slice(a.dopacity, b0, nloc);
+        zero_slice(a.dmeans3D, 3 * b0, 3 * nloc);
+        zero_slice(a.dcov3D, 6 * b0, 6 * nloc);
+        zero_slice(a.ddc, 3 * b0, 3 * nloc);
+        if (a.dsh && M) zero_slice(a.dsh, 3 * M * b0, 3 * M * nloc);
+        zero_slice(a.dscales, 3 * b0, 3 * nloc);
+        zero_slice(a.drot, 4 * b0, 4 * nloc);
+    }
     float acc[10];
 #ifdef DG_ABLATE_RECSUM  // timing experiment only: no records summed (every Gaussian takes the zero path)
     for (int v = 0; v < 10; v++) acc[v] = 0.f;
