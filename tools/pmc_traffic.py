@@ -11,9 +11,11 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import avg, load_counters  # noqa: E402
 
+# bench phase -> its kernels (names as pmc_summary._short gives them; phases whose kernels are also launched by the
+# gated phase-2 path under the same name are left out)
 PHASE_KERNEL = {
-    "preprocess": "k_preprocess", "emit": "k_emit", "ranges": "k_ranges", "render_fwd": "k_render_fwd",
-    "render_bwd": "k_render_bwd", "record_sum": "k_record_sum", "gauss_bwd": "k_gauss_bwd",
+    "preprocess": ["k_preprocess"], "emit": ["k_bin_count<1>", "k_bin_emit<1>"], "render_fwd": ["k_render_fwd<1>"],
+    "render_bwd": ["k_bwd_prologue", "k_tile_order", "k_render_bwd"], "gauss_bwd": ["k_gauss_prep", "k_gauss_live"],
 }
 
 
@@ -24,11 +26,11 @@ def main(root, n, W, H):
     d = json.load(open(out_path)) if os.path.exists(out_path) else {}
     key = f"{n}x{W}x{H}"
     ent = {}
-    for phase, kern in PHASE_KERNEL.items():
-        c = acc.get(kern)
-        if not c or "FETCH_SIZE" not in c:
+    for phase, kerns in PHASE_KERNEL.items():
+        cs = [acc.get(k) for k in kerns]
+        if not all(c and "FETCH_SIZE" in c for c in cs):
             continue
-        ent[phase] = (2.0 * avg(c["FETCH_SIZE"]) + avg(c.get("WRITE_SIZE", [0.0]))) * 1024.0
+        ent[phase] = sum((2.0 * avg(c["FETCH_SIZE"]) + avg(c.get("WRITE_SIZE", [0.0]))) * 1024.0 for c in cs)
     d[key] = ent
     json.dump(d, open(out_path, "w"), indent=1, sort_keys=True)
     print(key, {k: round(v / 1e6, 1) for k, v in ent.items()}, "MB")
