@@ -522,6 +522,11 @@ __device__ __forceinline__ uint32_t bcast_u(uint32_t v, int lane) {
 // reads each with broadcast ds_read_b128 and skips a pair whose two quadrant bits are clear.  The
 // per-pixel update is branch-free: a rejected or finished pixel gets alpha = 0, which leaves C, D and T
 // unchanged.  Wave-uniform early exit once every pixel of the tile has saturated.
+#ifndef DG_FWD_GROUP
+#define DG_FWD_GROUP 4
+#endif
+constexpr int FWD_GROUP = DG_FWD_GROUP;  // splats per branch-free group of the compositing loop
+
 #ifdef DG_FWD_WPE  // occupancy experiment: cap VGPRs so that DG_FWD_WPE waves fit per SIMD
 #define FWD_WPE_ATTR __attribute__((amdgpu_waves_per_eu(DG_FWD_WPE)))
 #else
@@ -529,12 +534,13 @@ __device__ __forceinline__ uint32_t bcast_u(uint32_t v, int lane) {
 #endif
 template <int PHASE>
 __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
-    __shared__ float4 s_b[4][64][3];
+    __shared__ float4 s_b[4][65][3];  // 64 staged splats + a null splat (opacity 0: no pixel accepts it)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tile = blockIdx.x * 4 + w;
     if (tile >= a.num_tiles) return;
     if (PHASE == 2 && !a.unfinished[tile]) return;  // finished in phase 1: outputs already final
     float4* sb = &s_b[w][0][0];
+    if (lane < 3) sb[64 * 3 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
     const int tx0 = tx * GS_TILE_X, ty0 = ty * GS_TILE_Y;
     const int c0 = tx0 + (lane & 7), rA = ty0 + (lane >> 3);
@@ -579,9 +585,12 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
         }
         __builtin_amdgcn_wave_barrier();
         uint64_t mask = __ballot(touch);
-        int step = 0;
+        // Splats go in groups of FWD_GROUP with no branch between them (a group's missing tail is the null splat), and the
+        // saturation exit is tested once per group: per-splat control flow costs more than the null splats do.
         while (mask) {
-            const int jj = (int)__builtin_ctzll(mask);
+#pragma unroll
+          for (int u = 0; u < FWD_GROUP; u++) {
+            const int jj = mask ? (int)__builtin_ctzll(mask) : 64;
             mask &= mask - 1;
             const float4 Sa = s_b[w][jj][0], Sb = s_b[w][jj][1], Sc = s_b[w][jj][2];
             const uint32_t c = cbase + (uint32_t)(base + jj + 1);
@@ -612,8 +621,9 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
             C2 = fma4(bc4(Sc.x), wt, C2);
             D = fma4(bc4(Sc.y), wt, D);
             T = Tn;
+          }
             // early exit, checked every 8 splats (splats after saturation leave every pixel unchanged)
-            if ((++step & 7) == 0 && !__any(fminf(fminf(thr.x, thr.y), fminf(thr.z, thr.w)) < 1.0f)) break;
+            if (!__any(fminf(fminf(thr.x, thr.y), fminf(thr.z, thr.w)) < 1.0f)) break;
         }
         __builtin_amdgcn_wave_barrier();
     }
