@@ -32,7 +32,7 @@ class DgRasterArgs(C.Structure):
 ALLOC_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int, C.c_uint64)
 DG_BUF_GEOM, DG_BUF_BINNING, DG_BUF_IMAGE, DG_BUF_BACKWARD, DG_BUF_TEMP, DG_BUF_BINNING2 = range(6)
 
-EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_mark_visible", "dg_rasterize_filter",
+EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count", "dg_mark_visible", "dg_rasterize_filter",
            "dg_adam_update", "dg_fused_ssim_forward", "dg_fused_ssim_backward", "dg_dist_cuda2",
            "dg_geom_bytes", "dg_image_bytes", "dg_binning_bytes", "dg_debug_sorted_instances",
            "dg_debug_geometry", "dg_debug_image_state", "dg_sort_pairs_u32", "dg_exclusive_scan_u32",
@@ -59,6 +59,9 @@ def load(path: str | None = None):
         L.dg_rasterize_forward.argtypes = [C.POINTER(DgRasterArgs), vp, vp, vp, ALLOC_FN, vp,
                                            C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), i64p, i64p,
                                            vp]
+        if hasattr(L, "dg_rasterize_count"):  # absent in older builds used for A/B runs
+            L.dg_rasterize_count.restype = C.c_int
+            L.dg_rasterize_count.argtypes = [C.POINTER(DgRasterArgs), vp, vp, vp, vp, ALLOC_FN, vp, i64p, vp]
         L.dg_rasterize_backward.restype = C.c_int
         L.dg_rasterize_backward.argtypes = [C.POINTER(DgRasterArgs), vp, vp, vp, vp, vp, C.c_int64, C.c_int64, vp, vp,
                                             vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, ALLOC_FN, vp, vp]

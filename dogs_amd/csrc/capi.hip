@@ -339,9 +339,13 @@ uint64_t dg_geom_bytes(int P) { return carve_geom(nullptr, P).bytes; }
 uint64_t dg_image_bytes(int W, int H) { return carve_image(nullptr, W, H).bytes; }
 uint64_t dg_binning_bytes(int64_t K, int W, int H) { (void)W; (void)H; return carve_binning(nullptr, K).bytes; }
 
-int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_invdepth, int* radii,
-                         dg_alloc_fn alloc, void* user, void** geom_out, void** binning_out, void** image_out,
-                         void** binning2_out, int64_t* num_rendered, int64_t* num_instances, dg_stream_t stream_) {
+}  // extern "C"
+
+namespace {
+// Rasterizer::forward (rasterizer_impl.cu:334-498); gcount (optional): count mode, contributing pixels per Gaussian
+int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth, int* radii, dg_alloc_fn alloc,
+                 void* user, void** geom_out, void** binning_out, void** image_out, void** binning2_out,
+                 int64_t* num_rendered, int64_t* num_instances, dg_stream_t stream_, uint32_t* gcount) {
     if (check_args(a)) return 1;
     hipStream_t s = (hipStream_t)stream_;
     const int P = a->P, W = a->W, H = a->H;
@@ -421,6 +425,8 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
     r.img_invd = im.img_invd; r.n_contrib = im.n_contrib; r.max_contrib = im.max_contrib;
     r.phase = 1; r.counters = g.counters; r.unfinished = im.unfinished; r.resume = im.resume;
     r.ranges2_zero = im.ranges2;
+    r.gcount = gcount;
+    if (gcount && P > 0) HIP_OK(hipMemsetAsync(gcount, 0, sizeof(uint32_t) * (size_t)P, s));
     { PROF("render_fwd"); gs::launch_render_fwd(r, s); }
     DBG_SYNC(a->debug, s);
 
@@ -459,6 +465,39 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
         gs::launch_render_fwd(r2, s);
     }
     DBG_SYNC(a->debug, s);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_invdepth, int* radii,
+                         dg_alloc_fn alloc, void* user, void** geom_out, void** binning_out, void** image_out,
+                         void** binning2_out, int64_t* num_rendered, int64_t* num_instances, dg_stream_t stream) {
+    return forward_impl(a, out_color, out_invdepth, radii, alloc, user, geom_out, binning_out, image_out,
+                        binning2_out, num_rendered, num_instances, stream, nullptr);
+}
+
+int dg_rasterize_count(const dg_raster_args* a, float* out_color, int* radii, int32_t* gaussians_count,
+                       float* important_score, dg_alloc_fn alloc, void* user, int64_t* num_rendered,
+                       dg_stream_t stream) {
+    if (check_args(a)) return 1;
+    if (a->P > 0 && (!gaussians_count || !important_score)) return fail("count outputs required%s%d");
+    hipStream_t s = (hipStream_t)stream;
+    const size_t HW = (size_t)a->W * a->H;
+    float* invd = nullptr;
+    HIP_OK(hipMallocAsync((void**)&invd, (HW ? HW : 1) * sizeof(float), s));
+    void *g = nullptr, *b = nullptr, *im = nullptr, *b2 = nullptr;
+    int64_t ninst = 0;
+    const int rc = forward_impl(a, out_color, invd, radii, alloc, user, &g, &b, &im, &b2, num_rendered, &ninst, stream,
+                                reinterpret_cast<uint32_t*>(gaussians_count));
+    if (rc == 0 && a->P > 0)
+        gs::launch_count_score(a->P, radii, carve_geom(g, a->P).sp, reinterpret_cast<const uint32_t*>(gaussians_count),
+                               important_score, s);
+    HIP_OK(hipFreeAsync(invd, s));
+    if (rc) return rc;
     HIP_OK(hipGetLastError());
     return 0;
 }

@@ -70,6 +70,7 @@ struct RenderArgs {
     const float* bg;
     float *out_color, *out_invd, *final_T, *img_color, *img_invd;
     uint32_t *n_contrib, *max_contrib;
+    uint32_t* gcount;           // optional (count mode): contributing pixels per Gaussian, accumulated
 };
 
 struct RenderBwdArgs {
@@ -156,6 +157,9 @@ int bin_waves(int P);
 void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, int tiles_x, int tiles_y,
                            uint32_t* sat, hipStream_t s);
 void launch_render_fwd(const RenderArgs& a, hipStream_t s);
+// count mode: score[i] = gcount[i] x the (AA-scaled) opacity of splat record i (0 when culled)
+void launch_count_score(int P, const int* radii, const float4* sp, const uint32_t* gcount, float* score,
+                        hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);
 void launch_filter(const PreArgs& a, hipStream_t s);
 // clears the record flags of the E1 + K2 binned instances and sets counters[CNT_INVD], then replays

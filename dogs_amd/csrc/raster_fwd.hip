@@ -532,7 +532,7 @@ constexpr int FWD_GROUP = DG_FWD_GROUP;  // splats per branch-free group of the 
 #else
 #define FWD_WPE_ATTR
 #endif
-template <int PHASE>
+template <int PHASE, bool COUNT>
 __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
     __shared__ float4 s_b[4][65][3];  // 64 staged splats + a null splat (opacity 0: no pixel accepts it)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -581,7 +581,7 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
             const SplatExp k = splat_exp_coeffs(s0.z, s0.w, s1.x);
             sb[lane * 3 + 0] = make_float4(s0.x, s0.y, k.A, k.B);
             sb[lane * 3 + 1] = make_float4(k.C, s1.y, q.x, q.y);
-            sb[lane * 3 + 2] = make_float4(q.z, q.w, 0.0f, 0.0f);
+            sb[lane * 3 + 2] = make_float4(q.z, q.w, __uint_as_float(g), 0.0f);
         }
         __builtin_amdgcn_wave_barrier();
         uint64_t mask = __ballot(touch);
@@ -614,6 +614,12 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
                 al[k] = term ? 0.0f : al[k];
                 Tn[k] = term ? T[k] : test_T[k];
                 last[k] = (acc[k] && !term) ? c : last[k];  // contributed: accepted and not the stopping splat
+            }
+            if (COUNT) {  // LightGaussian count mode: pixels the splat contributes to (old forward.cu:481-487)
+                uint32_t n = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) n += (uint32_t)__popcll(__ballot(acc[k] && al[k] != 0.0f));
+                if (n && lane == 0) atomicAdd(a.gcount + __float_as_uint(Sc.z), n);
             }
             const v4f wt = al * T;
             C0 = fma4(bc4(Sb.z), wt, C0);
@@ -748,8 +754,29 @@ void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, 
 }
 void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
     if (a.num_tiles <= 0) return;
-    if (a.phase == 2) k_render_fwd<2><<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
-    else k_render_fwd<1><<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
+    const int blocks = (a.num_tiles + 3) / 4;
+    if (a.gcount) {
+        if (a.phase == 2) k_render_fwd<2, true><<<blocks, 256, 0, s>>>(a);
+        else k_render_fwd<1, true><<<blocks, 256, 0, s>>>(a);
+    } else {
+        if (a.phase == 2) k_render_fwd<2, false><<<blocks, 256, 0, s>>>(a);
+        else k_render_fwd<1, false><<<blocks, 256, 0, s>>>(a);
+    }
+}
+
+// important_score = opacity x contributing pixels: the reference adds the opacity once per contributing pixel
+// (old forward.cu:486); here the count is exact (integer atomics) and the product is formed once.
+__global__ void __launch_bounds__(256) k_count_score(int P, const int* __restrict__ radii,
+                                                     const float4* __restrict__ sp, const uint32_t* __restrict__ gcount,
+                                                     float* __restrict__ score) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const uint32_t n = gcount[i];
+    score[i] = (radii[i] > 0 && n) ? (float)n * sp[2 * i + 1].y : 0.0f;
+}
+void launch_count_score(int P, const int* radii, const float4* sp, const uint32_t* gcount, float* score,
+                        hipStream_t s) {
+    if (P > 0) k_count_score<<<(P + 255) / 256, 256, 0, s>>>(P, radii, sp, gcount, score);
 }
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s) {
     if (P > 0) k_mark_visible<<<(P + 255) / 256, 256, 0, s>>>(P, means3D, view, present);

@@ -139,6 +139,43 @@ def mark_visible(means3D, viewmatrix, projmatrix):
     return present
 
 
+def count_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                    viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                    prefiltered, debug, f_count=True, antialiasing=False):
+    """CountGaussiansCUDA of old_diff-gaussian-rasterization (rasterize_points.cu:148-233; ext.cpp:19), the
+    LightGaussian count forward: returns (gaussians_count int32[P], important_score float[P], num_rendered,
+    color[3,H,W], radii, geomBuffer, binningBuffer, imgBuffer).  `sh` holds the full SH features [P,(D+1)^2,3]
+    (dc first) as in the old binding.  The private buffers are not needed after this call (empty tensors)."""
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    _lib.require_device(means3D, "means3D")
+    dev = means3D.device
+    P, H, W = int(means3D.size(0)), int(image_height), int(image_width)
+    fopt = dict(dtype=torch.float32, device=dev)
+    u8 = dict(dtype=torch.uint8, device=dev)
+    color = torch.zeros((3, H, W), **fopt)
+    radii = torch.zeros((P,), dtype=torch.int32, device=dev)
+    count = torch.zeros((P,), dtype=torch.int32, device=dev)
+    score = torch.zeros((P,), **fopt)
+    nr = C.c_int64(0)
+    if P:
+        dc = rest = None
+        if sh is not None and sh.numel() and sh.dim() == 3 and sh.size(0) == P:
+            dc, rest = sh[:, :1, :], sh[:, 1:, :]
+        M = _sh_m(rest) if rest is not None else 0
+        with torch.cuda.device(dev):
+            a, keep = _args(P, degree, M, W, H, background, means3D, colors, opacity, scales, rotations,
+                            scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dc, rest, campos,
+                            prefiltered, antialiasing, debug)
+            arena = _lib.TensorArena(dev)
+            _lib.check(_lib.load().dg_rasterize_count(C.byref(a), color.data_ptr(), radii.data_ptr(), count.data_ptr(),
+                                                      score.data_ptr(), arena.fn, None, C.byref(nr),
+                                                      _lib.stream_of(dev)))
+            del keep
+    e = torch.empty(0, **u8)
+    return count, score, int(nr.value), color, radii, e, e, e
+
+
 def rasterize_gaussians_filter(means3D, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
                                tan_fovx, tan_fovy, image_height, image_width, prefiltered, debug):
     """RasterizeGaussiansFilterCUDA (rasterize_points.cu:276-334)."""

@@ -100,8 +100,12 @@ class GaussianRasterizationSettings(NamedTuple):
     campos: torch.Tensor
     prefiltered: bool
     debug: bool
-    antialiasing: bool
-    depth_threshold: float
+    antialiasing: bool = False
+    depth_threshold: float = 0.0
+    # LightGaussian count mode (old_diff-gaussian-rasterization __init__.py:284-298 `f_count`, used by
+    # conerf/render/gaussian_render.py:161-278 count_render): the rasterizer returns per-Gaussian contribution
+    # counts and importance scores instead of a differentiable image
+    f_count: bool = False
 
 
 def _empty_like_device(ref: torch.Tensor) -> torch.Tensor:
@@ -126,6 +130,8 @@ class GaussianRasterizer(nn.Module):
         if ((scales is None or rotations is None) and cov3D_precomp is None) or (
                 (scales is not None or rotations is not None) and cov3D_precomp is not None):
             raise Exception("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!")
+        if getattr(rs, "f_count", False):
+            return self._forward_count(means3D, opacities, dc, shs, colors_precomp, scales, rotations, cov3D_precomp)
         # extension: full SH features [N,(D+1)^2,3] without a separate dc (the reference requires dc)
         if shs is not None and (dc is None or dc.numel() == 0) and shs.dim() == 3 and shs.size(1) >= 1:
             dc, shs = shs[:, :1, :], shs[:, 1:, :]
@@ -138,6 +144,22 @@ class GaussianRasterizer(nn.Module):
         cov3D_precomp = e if cov3D_precomp is None else cov3D_precomp
         return rasterize_gaussians(means3D, means2D, dc, shs, colors_precomp, opacities, scales, rotations,
                                    cov3D_precomp, rs)
+
+    @torch.no_grad()
+    def _forward_count(self, means3D, opacities, dc, shs, colors_precomp, scales, rotations, cov3D_precomp):
+        """_RasterizeGaussians.forward_count (old __init__.py:150-199): (gaussians_count, important_score,
+        color, radii); no autograd.  `shs` is the full feature tensor (dc first), or dc + the rest separately."""
+        rs = self.raster_settings
+        if shs is not None and dc is not None and dc.numel():
+            shs = torch.cat([dc, shs], dim=1)
+        e = _empty_like_device(means3D)
+        count, score, _, color, radii, _, _, _ = _C.count_gaussians(
+            rs.bg, means3D, e if colors_precomp is None else colors_precomp, opacities,
+            e if scales is None else scales, e if rotations is None else rotations, rs.scale_modifier,
+            e if cov3D_precomp is None else cov3D_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy,
+            rs.image_height, rs.image_width, e if shs is None else shs, rs.sh_degree, rs.campos, rs.prefiltered,
+            rs.debug, True, getattr(rs, "antialiasing", False))
+        return count, score, color, radii
 
     def visible_filter(self, means3D, scales=None, rotations=None, cov3D_precomp=None):
         rs = self.raster_settings

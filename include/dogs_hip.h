@@ -72,6 +72,15 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
  * written (no zero-fill needed): dmeans2D [P,3], dcolors [P,3], dopacity [P,1], dmeans3D [P,3],
  * dcov3D [P,6], ddc [P,1,3], dsh [P,M,3] (may be NULL when M == 0), dscales [P,3], drot [P,4],
  * depth [P,1].  dL_dout_invdepth may be NULL (treated as zeros).  Allocates DG_BUF_BACKWARD. */
+/* LightGaussian count mode (old_diff-gaussian-rasterization: CountGaussiansCUDA, rasterize_points.cu:148-233, and
+ * renderCUDA_count, forward.cu:392-500): the forward above plus, per Gaussian, the number of pixels it contributes
+ * to (gaussians_count, int32[P]) and important_score = opacity x that count (float[P]).  The counts are exact
+ * (integer atomics; the reference's non-atomic increments race).  The private state blocks are requested from
+ * alloc as in dg_rasterize_forward and are not needed afterwards. */
+int dg_rasterize_count(const dg_raster_args* a, float* out_color, int* radii, int32_t* gaussians_count,
+                       float* important_score, dg_alloc_fn alloc, void* user, int64_t* num_rendered,
+                       dg_stream_t stream);
+
 int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void* geom, const void* binning,
                           const void* image, const void* binning2, int64_t num_rendered, int64_t num_instances,
                           const float* dL_dout_color, const float* dL_dout_invdepth, float* dmeans2D,

@@ -180,6 +180,8 @@ typedef struct {
     uint32_t* ranges;              /* [num_tiles][2] */
     /* image */
     float* final_T; uint32_t* n_contrib; uint32_t* max_contrib; float* pix_color; float* pix_invdepth;
+    /* LightGaussian count mode (old forward.cu:481-487): contributing pixels and sum of opacity per Gaussian */
+    int32_t* gcount; float* gscore;
     /* samples (SampleState) */
     uint32_t* bucket_offsets; int64_t num_buckets;
     float* sT; float* sar; float* sard;
@@ -386,6 +388,7 @@ void gso_free(gso_ctx* c) {
     free(c->depths); free(c->radii); free(c->means2D); free(c->cov3D); free(c->conic_opacity); free(c->rgb);
     free(c->clamped); free(c->tiles_touched); free(c->keys); free(c->vals); free(c->ranges); free(c->final_T);
     free(c->n_contrib); free(c->max_contrib); free(c->pix_color); free(c->pix_invdepth); free(c->bucket_offsets);
+    free(c->gcount); free(c->gscore);
     free(c->sT); free(c->sar); free(c->sard);
     free(c);
 }
@@ -409,6 +412,7 @@ gso_ctx* gso_forward(const gso_params* prm, float* out_color, float* out_invdept
     c->tiles_touched = calloc(Pn, 4);
     const size_t HW = (size_t)W * H;
     c->final_T = calloc(HW ? HW : 1, 4); c->n_contrib = calloc(HW ? HW : 1, 4);
+    c->gcount = calloc(prm->P ? prm->P : 1, 4); c->gscore = calloc(prm->P ? prm->P : 1, 4);
     c->max_contrib = calloc(c->num_tiles ? c->num_tiles : 1, 4);
     c->pix_color = calloc(3 * HW + 1, 4); c->pix_invdepth = calloc(HW + 1, 4);
     c->ranges = calloc(2 * (size_t)(c->num_tiles ? c->num_tiles : 1), 4);
@@ -510,6 +514,8 @@ gso_ctx* gso_forward(const gso_params* prm, float* out_color, float* out_invdept
                     ed = fmaf((1.f / c->depths[g]) * alpha, T, ed);
                     T = test_T;
                     last = contributor;
+                    c->gcount[g]++;            /* gaussian_count[collected_id[j]]++ */
+                    c->gscore[g] += co[3];     /* important_score[collected_id[j]] += con_o.w */
                 }
                 const size_t pid = (size_t)W * py + px;
                 c->final_T[pid] = T;
@@ -851,6 +857,12 @@ void gso_copy_list(const gso_ctx* c, uint32_t* tiles, uint32_t* idx, uint32_t* d
         idx[i] = c->vals[i];
         if (depth_bits) depth_bits[i] = (uint32_t)(c->keys[i] & 0xffffffffu);
     }
+}
+/* count mode outputs (CountGaussiansCUDA, old rasterize_points.cu:148-233): per-Gaussian contributing pixels and
+ * the opacity summed over them, in this restatement's sequential (tile, pixel, splat) order */
+void gso_copy_counts(const gso_ctx* c, int32_t* count, float* score) {
+    memcpy(count, c->gcount, 4 * (size_t)c->p.P);
+    memcpy(score, c->gscore, 4 * (size_t)c->p.P);
 }
 void gso_copy_ranges(const gso_ctx* c, uint32_t* ranges) { memcpy(ranges, c->ranges, 8 * (size_t)c->num_tiles); }
 void gso_copy_geom(const gso_ctx* c, float* depths, float* means2D, float* conic, float* rgb, float* cov3D,

@@ -63,6 +63,7 @@ def lib():
         L.gso_copy_ranges.argtypes = [C.c_void_p, u32p]
         L.gso_copy_geom.argtypes = [C.c_void_p, f32p, f32p, f32p, f32p, f32p, u8p, u32p]
         L.gso_copy_image_state.argtypes = [C.c_void_p, f32p, u32p, u32p]
+        L.gso_copy_counts.argtypes = [C.c_void_p, i32p, f32p]
         L.gso_mark_visible.argtypes = [C.c_int, f32p, f32p, f32p, u8p]
         L.gso_filter_radii.argtypes = [C.POINTER(GsoParams), i32p]
         L.gso_adam.argtypes = [f32p, f32p, f32p, f32p, u8p, C.c_float, C.c_float, C.c_float, C.c_float,
@@ -146,6 +147,13 @@ class OracleForward:
         mc = np.zeros(self.num_tiles, np.uint32)
         lib().gso_copy_image_state(self._ctx, _p(fT), _p(nc, u32p), _p(mc, u32p))
         return fT.reshape(self.H, self.W), nc.reshape(self.H, self.W), mc
+
+    def counts(self):
+        """LightGaussian count mode: (gaussians_count int32[P], important_score float32[P])."""
+        cnt = np.zeros(self.P, np.int32)
+        score = np.zeros(self.P, np.float32)
+        lib().gso_copy_counts(self._ctx, _p(cnt, i32p), _p(score))
+        return cnt, score
 
     def backward(self, dL_dpix, dL_dinvdepth=None):
         P, M = self.P, self.M

@@ -121,3 +121,40 @@ def test_gaussian_rasterizer_autograd(oracle, hip_device):
     for k, o in pairs.items():
         assert rel_err(leaf[k].grad.cpu().numpy().reshape(go[o].shape), go[o]) < 1e-4, k
     assert rel_err(means2D.grad.cpu().numpy(), go["dmeans2D"]) < 1e-4
+
+
+@pytest.mark.parametrize("prefix", [0, 2], ids=["prefix-default", "prefix-2-per-tile"])
+def test_count_mode_matches_oracle(oracle, hip_device, prefix):
+    """LightGaussian count mode (GaussianRasterizationSettings(f_count=True), as count_render,
+    conerf/render/gaussian_render.py:161-278, calls it with the full SH features): per-Gaussian contributing-pixel
+    counts and importance scores against the oracle's restatement of renderCUDA_count (old forward.cu:392-500).
+    Counts are exact integers here; a decision at the alpha/T thresholds may flip between v_exp_f32 and expf."""
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from dogs_amd.diff_gaussian_rasterization import _C
+    n, W, H = 2000, 160, 120
+    s = small_scene(n, W, H, seed=17)
+    c = s.camera.to(hip_device)
+    bg = torch.tensor([0.1, 0.2, 0.3], device=hip_device)
+    st = GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=c.tanfovx, tanfovy=c.tanfovy, bg=bg,
+                                       scale_modifier=1.0, depth_threshold=0.0, viewmatrix=c.world_to_camera,
+                                       projmatrix=c.projective_matrix, sh_degree=3, campos=c.camera_center,
+                                       prefiltered=False, debug=False, f_count=True)
+    feats = torch.cat([s.dc, s.sh], dim=1).to(hip_device)
+    old = _C.set_prefix_per_tile(prefix)
+    try:
+        count, score, img, radii = GaussianRasterizer(st)(means3D=s.means3D.to(hip_device), means2D=None,
+                                                          opacities=s.opacities.to(hip_device), shs=feats,
+                                                          scales=s.scales.to(hip_device),
+                                                          rotations=s.rotations.to(hip_device))
+    finally:
+        _C.set_prefix_per_tile(old)
+    col_o, radii_o, _, sto = oracle_forward(oracle, s, bg.cpu().numpy())
+    cnt_o, score_o = sto.counts()
+    np.testing.assert_array_equal(radii.cpu().numpy(), radii_o)
+    assert np.abs(img.cpu().numpy() - col_o).max() < 5e-3
+    cnt = count.cpu().numpy()
+    assert count.dtype == torch.int32 and cnt.sum() > 0
+    assert (cnt == cnt_o).mean() > 0.99
+    assert np.abs(cnt.astype(np.int64) - cnt_o).sum() <= 1e-3 * cnt_o.sum()
+    same = cnt == cnt_o
+    np.testing.assert_allclose(score.cpu().numpy()[same], score_o[same], rtol=1e-4, atol=1e-6)
