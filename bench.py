@@ -95,7 +95,8 @@ class View:
         depth-prefix binning off.  The §8(d) byte formula is written in terms of it."""
         old = self._C.set_prefix_per_tile(-1)
         try:
-            return int(self.forward()[1])
+            self.last_out = self.forward()
+            return self.binned_instances()
         finally:
             self._C.set_prefix_per_tile(old)
 

@@ -85,8 +85,8 @@ def load(path: str | None = None):
         L.dg_binning_bytes.restype = C.c_uint64
         L.dg_binning_bytes.argtypes = [C.c_int64, C.c_int, C.c_int]
         L.dg_debug_sorted_instances.restype = C.c_int
-        L.dg_debug_sorted_instances.argtypes = [C.POINTER(DgRasterArgs), vp, vp, vp, vp, C.c_int64, vp, vp,
-                                                i64p, vp]
+        L.dg_debug_sorted_instances.argtypes = [C.POINTER(DgRasterArgs), vp, vp, vp, vp, C.c_int64, C.c_int64,
+                                                vp, vp, i64p, vp]
         if hasattr(L, "dg_binned_instances"):  # introspection only; absent in older builds used for A/B runs
             L.dg_binned_instances.restype = C.c_int
             L.dg_binned_instances.argtypes = [vp, C.c_int, i64p, vp]

@@ -203,17 +203,59 @@ HostCounters& host_counters() {
 }
 
 // Phase-1 binning capacity, in tile-rect area units (the depth cut bounds the precise instances by the rect areas):
-// prefix_per_tile x tiles (0 -> default), or everything when < 0.  448 rect units are ~256 precise instances per
-// tile on the bench scene.
+// prefix_per_tile x tiles when > 0, adaptive when 0, everything when < 0.  448 rect units are ~256 precise
+// instances per tile on the bench scene.
 constexpr int DEFAULT_PREFIX_PER_TILE = 448;
+constexpr int MAX_PREFIX_PER_TILE = 8192;
 // capacity of any per-instance array: the total rect area bounds every phase's instance count
 inline int64_t inst_cap(uint64_t rect) { return (int64_t)(rect < 0xffffff00ull ? (rect ? rect : 1) : 0xffffff00ull); }
 bool prefix_enabled(const dg_raster_args* a) { return a->prefix_per_tile >= 0; }
-int64_t phase1_cap(const dg_raster_args* a, int T, int64_t K_all) {
-    if (!prefix_enabled(a)) return K_all;
-    const int64_t per = a->prefix_per_tile > 0 ? a->prefix_per_tile : DEFAULT_PREFIX_PER_TILE;
+int64_t clamp_cap(int64_t per, int T) {
     const int64_t c = per * (int64_t)T;
     return c < 1 ? 1 : (c > 0xffffff00ll ? 0xffffff00ll : c);
+}
+
+// Adaptive phase-1 capacity (prefix_per_tile == 0).  Phase 2 costs 100-400 us whenever it runs (a full walk of the
+// Gaussians past the threshold), so a scene whose views keep leaving tiles unfinished wants a deeper prefix.  Per
+// image size on this thread: after each view the unfinished-tile count lands in pinned memory behind an event; the
+// next forward of that size reads it without waiting (hipEventQuery) and grows the per-tile capacity x1.5 when any
+// tile needed phase 2 (its cost is mostly per view, not per tile: the walk over the Gaussians past the threshold and
+// the block sort of the few, very long, phase-2 lists).  Grow-only: a capacity that was once needed stays, and a
+// too-deep prefix costs only proportionally more phase-1 work.  The capacity a view used travels to its backward as
+// the num_instances token, so later growth never desynchronises a forward/backward pair.
+struct AdaptiveCap {
+    int per_tile = DEFAULT_PREFIX_PER_TILE;
+    uint32_t* unfinished = nullptr;  // pinned landing slot
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+};
+AdaptiveCap& adaptive_cap(int W, int H) {
+    thread_local std::map<std::pair<int, int>, AdaptiveCap> caps;
+    AdaptiveCap& c = caps[{W, H}];
+    if (!c.unfinished) {
+        (void)hipHostMalloc((void**)&c.unfinished, 64, hipHostMallocDefault);
+        (void)hipEventCreateWithFlags(&c.ev, hipEventDisableTiming);
+    }
+    return c;
+}
+int64_t phase1_cap(const dg_raster_args* a, int T) {
+    if (a->prefix_per_tile > 0) return clamp_cap(a->prefix_per_tile, T);
+    AdaptiveCap& c = adaptive_cap(a->W, a->H);
+    if (c.pending && hipEventQuery(c.ev) == hipSuccess) {
+        c.pending = false;
+        if (*c.unfinished > 0u && c.per_tile < MAX_PREFIX_PER_TILE)
+            c.per_tile = c.per_tile * 3 / 2 < MAX_PREFIX_PER_TILE ? c.per_tile * 3 / 2 : MAX_PREFIX_PER_TILE;
+    }
+    return clamp_cap(c.per_tile, T);
+}
+// after the phase-1 render of an adaptive view: queue the unfinished count for the next forward of this size
+void note_unfinished(const dg_raster_args* a, const uint32_t* counters, hipStream_t s) {
+    if (a->prefix_per_tile != 0) return;
+    AdaptiveCap& c = adaptive_cap(a->W, a->H);
+    if (c.pending) return;  // one outstanding probe per size
+    (void)hipMemcpyAsync(c.unfinished, counters + gs::CNT_UNFINISHED, 4, hipMemcpyDeviceToHost, s);
+    (void)hipEventRecord(c.ev, s);
+    c.pending = true;
 }
 
 struct BwdScratch {
@@ -382,7 +424,7 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
         PROF("prefix_cut");
         gs::launch_depth_hist(P, g.dkey, g.cnt, g.hist, s);
         if (prefix_enabled(a)) {
-            C1 = phase1_cap(a, T, 0);
+            C1 = phase1_cap(a, T);
             gs::launch_depth_cut(g.hist, (uint32_t)C1, g.counters, im.tile_cnt, im.tile_cnt2, (uint32_t)T, s);
         } else {  // everything in one phase: the capacity is the total rect area itself (one early sync)
             gs::launch_depth_cut(g.hist, 0xffffffffu, g.counters, im.tile_cnt, im.tile_cnt2, (uint32_t)T, s);
@@ -429,15 +471,17 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     if (gcount && P > 0) HIP_OK(hipMemsetAsync(gcount, 0, sizeof(uint32_t) * (size_t)P, s));
     { PROF("render_fwd"); gs::launch_render_fwd(r, s); }
     DBG_SYNC(a->debug, s);
+    if (prefix_enabled(a) && C1 > 0 && P > 0) note_unfinished(a, g.counters, s);
 
     HIP_OK(hipEventSynchronize(hcs.ev));
     const uint32_t* hc = hcs.buf;
     if (hc[gs::CNT_ERR]) return fail("a Gaussian was filtered although prefiltered is set%s%d");
     const uint64_t rect = (uint64_t)hc[gs::CNT_RECT_LO] | ((uint64_t)hc[gs::CNT_RECT_LO + 1] << 32);
     *num_rendered = (int64_t)rect;
-    // the num_buckets slot: the precise phase-1 instance count (all instances when nothing was cut).  The backward
-    // sizes its per-instance state by num_rendered, which bounds phase 1 + phase 2.
-    *num_instances = hc[gs::CNT_E1];
+    // the num_buckets slot: the phase-1 capacity this view was binned with (the backward carves the phase-1 block
+    // at it; with the adaptive policy it can change between views).  Phase 2 and the backward's per-instance state
+    // are sized by num_rendered, which bounds phase 1 + phase 2.
+    *num_instances = C1;
     if (!hc[gs::CNT_CUT]) {
         HIP_OK(hipGetLastError());
         return 0;
@@ -514,9 +558,11 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     if (P == 0) return 0;
     Geom g = carve_geom((void*)geom, P);
     Image im = carve_image((void*)image, W, H);
-    // the phase-1 block was carved at C1 (its capacity), the phase-2 block at the rect total (see the forward)
+    // the phase-1 block was carved at C1 = the forward's num_instances token, the phase-2 block at the rect total
     const int64_t Kcap = inst_cap((uint64_t)num_rendered);
-    const int64_t C1 = prefix_enabled(a) ? phase1_cap(a, T, 0) : Kcap;
+    const int64_t C1 = K;
+    if (C1 < 0 || C1 > Kcap + (prefix_enabled(a) ? clamp_cap(MAX_PREFIX_PER_TILE, T) : 0))
+        return fail("num_instances is not the forward's token%s (%d)", "", (int)C1);
     Binning b = carve_binning((void*)binning, C1);
     const uint32_t* s_e = b.se;
     const uint32_t* s_e2 = nullptr;
@@ -527,7 +573,6 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
         eg2 = b2.eg;
     }
 
-    (void)K;  // the phase-1 instance count (informational)
     const size_t sbytes = carve_bwd(nullptr, Kcap, P, T).bytes;
     void* sbase = alloc(user, DG_BUF_BACKWARD, sbytes);
     if (!sbase) return fail("backward scratch allocation failed%s%d");
@@ -664,8 +709,8 @@ __global__ void k_tiles_of(int T, const uint2* ranges, const uint8_t* only, uint
 }  // namespace
 
 int dg_debug_sorted_instances(const dg_raster_args* a, const void* geom, const void* binning, const void* binning2,
-                              const void* image, int64_t num_rendered, uint32_t* tiles_out, uint32_t* gauss_out,
-                              int64_t* e1_out, dg_stream_t stream) {
+                              const void* image, int64_t num_rendered, int64_t num_instances, uint32_t* tiles_out,
+                              uint32_t* gauss_out, int64_t* e1_out, dg_stream_t stream) {
     hipStream_t s = (hipStream_t)stream;
     const int T = tiles_x_of(a->W) * tiles_y_of(a->H);
     Geom g = carve_geom((void*)geom, a->P);
@@ -677,7 +722,7 @@ int dg_debug_sorted_instances(const dg_raster_args* a, const void* geom, const v
     *e1_out = E1;
     const int64_t Kcap = inst_cap((uint64_t)num_rendered);
     if (E1 > 0) {
-        Binning b = carve_binning((void*)binning, prefix_enabled(a) ? phase1_cap(a, T, 0) : Kcap);
+        Binning b = carve_binning((void*)binning, num_instances);
         k_gather_g<<<(E1 + 255) / 256, 256, 0, s>>>(E1, b.se, b.eg, gauss_out);
         k_tiles_of<<<(T + 255) / 256, 256, 0, s>>>(T, im.ranges, nullptr, tiles_out);
     }

@@ -476,28 +476,47 @@ __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
 }
 
 // Exclusive summed-area table of the unfinished-tile flags, [(tiles_y+1) x (tiles_x+1)]: O(1) "does this
-// rect touch an unfinished tile" for the phase-2 kernels.
-__global__ void __launch_bounds__(1024) k_unfinished_sat(const uint32_t* __restrict__ counters,
-                                                          const uint8_t* __restrict__ unf, int tx, int ty,
-                                                          uint32_t* __restrict__ sat) {
-    if (counters[CNT_UNFINISHED] == 0u) return;
-    const int W1 = tx + 1;
-    for (int x = threadIdx.x; x < W1; x += blockDim.x) sat[x] = 0u;
-    for (int y = threadIdx.x; y < ty; y += blockDim.x) {
-        uint32_t run = 0;
-        sat[(size_t)(y + 1) * W1] = 0u;
-        for (int x = 0; x < tx; x++) {
-            run += unf[(size_t)y * tx + x] ? 1u : 0u;
-            sat[(size_t)(y + 1) * W1 + x + 1] = run;
-        }
+// rect touch an unfinished tile" for the phase-2 kernels.  Two wave-parallel passes (one wave per row, then one
+// per column, 64-wide shuffle scans), so no lane walks a dependent chain of global accesses.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
     }
-    __syncthreads();
-    for (int x = threadIdx.x + 1; x < W1; x += blockDim.x) {
-        uint32_t run = 0;
-        for (int y = 1; y <= ty; y++) {
-            run += sat[(size_t)y * W1 + x];
-            sat[(size_t)y * W1 + x] = run;
-        }
+    return x;
+}
+__global__ void __launch_bounds__(256) k_sat_rows(const uint32_t* __restrict__ counters,
+                                                  const uint8_t* __restrict__ unf, int tx, int ty,
+                                                  uint32_t* __restrict__ sat) {
+    if (counters[CNT_UNFINISHED] == 0u) return;
+    const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);  // sat row r = tile row r - 1
+    if (r > ty) return;
+    const int W1 = tx + 1;
+    uint32_t* row = sat + (size_t)r * W1;
+    if (lane == 0) row[0] = 0u;
+    uint32_t carry = 0u;
+    for (int x0 = 0; x0 < tx; x0 += 64) {
+        const int x = x0 + lane;
+        const uint32_t v = (r > 0 && x < tx && unf[(size_t)(r - 1) * tx + x]) ? 1u : 0u;
+        const uint32_t inc = wave_incl_scan(v, lane) + carry;
+        if (x < tx) row[x + 1] = inc;
+        carry = __shfl(inc, 63);
+    }
+}
+__global__ void __launch_bounds__(256) k_sat_cols(const uint32_t* __restrict__ counters, int tx, int ty,
+                                                  uint32_t* __restrict__ sat) {
+    if (counters[CNT_UNFINISHED] == 0u) return;
+    const int lane = threadIdx.x & 63, c = 1 + blockIdx.x * 4 + (threadIdx.x >> 6);  // column 0 is all zero
+    if (c > tx) return;
+    const int W1 = tx + 1;
+    uint32_t carry = 0u;
+    for (int y0 = 1; y0 <= ty; y0 += 64) {
+        const int y = y0 + lane;
+        const uint32_t v = y <= ty ? sat[(size_t)y * W1 + c] : 0u;
+        const uint32_t inc = wave_incl_scan(v, lane) + carry;
+        if (y <= ty) sat[(size_t)y * W1 + c] = inc;
+        carry = __shfl(inc, 63);
     }
 }
 
@@ -750,7 +769,8 @@ size_t bin_scan_temp_bytes(int P) { return scan_temp_bytes((uint32_t)((P + EMIT_
 int bin_waves(int P) { return (P + EMIT_RANKS - 1) / EMIT_RANKS; }
 void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, int tiles_x, int tiles_y,
                            uint32_t* sat, hipStream_t s) {
-    k_unfinished_sat<<<1, 1024, 0, s>>>(counters, unfinished, tiles_x, tiles_y, sat);
+    k_sat_rows<<<(tiles_y + 1 + 3) / 4, 256, 0, s>>>(counters, unfinished, tiles_x, tiles_y, sat);
+    k_sat_cols<<<(tiles_x + 3) / 4, 256, 0, s>>>(counters, tiles_x, tiles_y, sat);
 }
 void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
     if (a.num_tiles <= 0) return;

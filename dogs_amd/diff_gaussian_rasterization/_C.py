@@ -14,8 +14,8 @@ from .. import _lib
 _EMPTY_U8 = None
 
 # Depth-prefix binning policy (dg_raster_args.prefix_per_tile): phase-1 capacity = this x tiles in tile-rect area
-# units; 0 -> the library default (448), < 0 -> bin every instance in one phase.  Module-level so that the forward and the
-# backward of a view always agree; tests lower it to exercise the phase-2 path.  DOGS_PREFIX_PER_TILE sets it
+# units; 0 -> the library's adaptive capacity (448 per tile, grown while views keep needing phase 2), < 0 -> bin every
+# instance in one phase.  Module-level so that the forward and the backward of a view always agree; tests lower it to exercise the phase-2 path.  DOGS_PREFIX_PER_TILE sets it
 # for experiments (tools/prefix_sweep.sh).
 PREFIX_PER_TILE = int(os.environ.get("DOGS_PREFIX_PER_TILE", "0"))
 
@@ -92,8 +92,8 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, dc, sh,
                                  dL_dout_invdepth, degree, campos, geomBuffer, R, binningBuffer, imageBuffer, B,
                                  sampleBuffer, antialiasing, debug):
-    """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:157-252).  B is the instance count the forward
-    returned in the num_buckets slot."""
+    """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:157-252).  B is the token the forward returned in the
+    num_buckets slot (the phase-1 binning capacity of that view)."""
     _lib.require_device(means3D, "means3D")
     dev = means3D.device
     P = int(means3D.size(0))

@@ -37,8 +37,9 @@ typedef struct {
     int W, H;           /* image_width, image_height */
     int prefiltered, antialiasing, debug;
     int prefix_per_tile;        /* depth-prefix binning: phase-1 capacity = this x tiles in tile-rect area
-                                   units (0 -> 448); < 0 bins every instance in one phase.  Must match
-                                   between forward and backward of one view. */
+                                   units; 0 -> adaptive (448, grown x1.5 per image size while views keep
+                                   needing phase 2); < 0 bins every instance in one phase.  Must agree in
+                                   sign between forward and backward of one view. */
     float scale_modifier, tanfovx, tanfovy;
     const float* bg;            /* [3] */
     const float* means3D;       /* [P,3] */
@@ -57,8 +58,8 @@ typedef struct {
 /* Replaces RasterizeGaussiansCUDA (rasterize_points.cu:55-154) / _C.rasterize_gaussians.
  * Outputs out_color [3,H,W], out_invdepth [1,H,W], radii [P] (int32).
  * *num_rendered = the reference's num_rendered (sum of tile-rect areas);
- * *num_instances = (tile, Gaussian) instances binned (returned where the reference returns num_buckets;
- * both are opaque tokens handed back to the backward).  Binning is depth-prefix (DESIGN.md "Binning"):
+ * *num_instances = the phase-1 binning capacity this view used (returned where the reference returns num_buckets;
+ * both are opaque tokens handed back to the backward; dg_binned_instances gives the instance count).  Binning is depth-prefix (DESIGN.md "Binning"):
  * phase 1 bins the first instances of the global depth order (a prefix of every tile's list), phase 2 bins
  * the rest only for tiles that phase 1 left unfinished -- same images and gradients, far fewer instances.
  * Allocates DG_BUF_GEOM, DG_BUF_IMAGE, DG_BUF_BINNING and, only when phase 2 runs, DG_BUF_BINNING2 through
@@ -126,8 +127,8 @@ uint64_t dg_binning_bytes(int64_t K, int W, int H);
  * each grouped by tile in (depth, index) order -- per-Gaussian geometry (tile_count = instances binned for the
  * Gaussian), per-pixel/per-tile image state (ranges = phase 1).  num_rendered: the forward's first return. */
 int dg_debug_sorted_instances(const dg_raster_args* a, const void* geom, const void* binning, const void* binning2,
-                              const void* image, int64_t num_rendered, uint32_t* tiles_out, uint32_t* gauss_out,
-                              int64_t* e1, dg_stream_t stream);
+                              const void* image, int64_t num_rendered, int64_t num_instances, uint32_t* tiles_out,
+                              uint32_t* gauss_out, int64_t* e1, dg_stream_t stream);
 /* Instances actually binned by the last forward on this geometry block: phase 1 + phase 2 (synchronises). */
 int dg_binned_instances(const void* geom, int P, int64_t* binned, dg_stream_t stream);
 int dg_debug_geometry(const void* geom, int P, float* means2D, float* conic_opacity, float* rgb_invdepth,

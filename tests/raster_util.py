@@ -60,7 +60,8 @@ def hip_sorted_instances(out, W, H, dev, P):
     gs = torch.empty(max(K, 1), dtype=torch.int32, device=dev)
     e1 = C.c_int64(0)
     _lib.check(L.dg_debug_sorted_instances(C.byref(a), out[5].data_ptr(), out[6].data_ptr(), _lib.ptr(out[8]),
-                                           out[7].data_ptr(), int(out[0]), tiles.data_ptr(), gs.data_ptr(),
+                                           out[7].data_ptr(), int(out[0]), int(out[1]), tiles.data_ptr(),
+                                           gs.data_ptr(),
                                            C.byref(e1), _lib.stream_of(dev)))
     torch.cuda.synchronize()
     return tiles[:K].cpu().numpy().view(np.uint32), gs[:K].cpu().numpy().view(np.uint32), int(e1.value)

@@ -40,11 +40,12 @@ def test_forward_bitexact_keys(oracle, hip_device, prefix_policy, n, W, H, deg, 
     out = hip_forward(s, bg, hip_device, deg=deg, antialiasing=aa)
     num_rendered, K, col, inv, radii = out[:5]
     assert num_rendered == st.num_rendered
-    assert K <= st.num_valid
+    assert K >= 1  # the phase-1 capacity token
     np.testing.assert_array_equal(radii.cpu().numpy(), radii_o)
     # every tile's binned list is a prefix of the reference order (tile, depth bits, index) ...
     t_o, i_o, _ = st.sorted_list()
     t_h, i_h, e1 = hip_sorted_instances(out, W, H, hip_device, n)
+    assert e1 <= len(t_h) <= st.num_valid
     full = per_tile_lists(t_o, i_o, len(t_o))
     got = per_tile_lists(t_h, i_h, e1)
     for t, lst in got.items():
@@ -57,7 +58,7 @@ def test_forward_bitexact_keys(oracle, hip_device, prefix_policy, n, W, H, deg, 
     for t in range(T):
         m = int(mc[t])
         assert m <= len(got.get(t, [])), f"tile {t}: max contributor {m} beyond its binned list"
-    if prefix_policy == 0 and K == st.num_valid:
+    if e1 == st.num_valid:  # phase 1 binned everything: the whole reference order
         np.testing.assert_array_equal(t_h, t_o)
         np.testing.assert_array_equal(i_h, i_o)
         np.testing.assert_array_equal(rg, st.ranges())
@@ -149,5 +150,46 @@ def test_equal_depth_order(oracle, hip_device, n, W, H, mode, prefix):
         for t, lst in got.items():
             assert lst == full[t][:len(lst)], f"tile {t}: not a prefix of the reference list"
         assert psnr(out[2].cpu().numpy(), col_o) > 80.0
+    finally:
+        _C.set_prefix_per_tile(old)
+
+
+def test_adaptive_prefix_capacity(oracle, hip_device):
+    """prefix_per_tile = 0: the phase-1 capacity grows while views leave tiles unfinished (translucent scene, phase 2
+    on every early view), images do not depend on it, and a view's backward uses the capacity its forward returned
+    even after later forwards grew it."""
+    from dogs_amd.diff_gaussian_rasterization import _C
+    n, W, H = 20000, 112, 80  # an image size no other test uses: fresh adaptive state
+    s = small_scene(n, W, H, seed=31)
+    s.opacities = (s.opacities * 0.05).contiguous()
+    bg = (0.1, 0.2, 0.3)
+    col_o, radii_o, inv_o, st = oracle_forward(oracle, s, bg)
+    old = _C.set_prefix_per_tile(0)
+    try:
+        first = hip_forward(s, bg, hip_device)
+        tokens = [int(first[1])]
+        for _ in range(10):
+            o = hip_forward(s, bg, hip_device)
+            torch.cuda.synchronize()
+            tokens.append(int(o[1]))
+            assert psnr(o[2].cpu().numpy(), col_o) > 80.0
+        assert tokens == sorted(tokens) and tokens[-1] > tokens[0], tokens
+        # backward of the first view (small capacity, phase 2) after the capacity grew
+        dev = hip_device
+        c = s.camera.to(dev)
+        e = torch.empty(0, device=dev)
+        d = lambda t: t.to(dev).contiguous()  # noqa: E731
+        rng = np.random.default_rng(3)
+        gcol = rng.standard_normal((3, H, W)).astype(np.float32)
+        go = st.backward(gcol)
+        gr = _C.rasterize_gaussians_backward(
+            torch.as_tensor(bg, dtype=torch.float32, device=dev), d(s.means3D), first[4], e, d(s.opacities),
+            d(s.scales), d(s.rotations), 1.0, e, c.world_to_camera, c.projective_matrix, c.tanfovx, c.tanfovy,
+            torch.from_numpy(gcol).to(dev), d(s.dc), d(s.sh), torch.zeros((1, H, W), device=dev), 3,
+            c.camera_center, first[5], first[0], first[6], first[7], first[1], first[8], False, False)
+        for name, h in zip(["dmeans2D", "dcolors", "dopacity", "dmeans3D"], gr):
+            ref = go[name]
+            assert rel_err(h.cpu().numpy().reshape(ref.shape), ref) < 1e-4, name
+        assert psnr(first[2].cpu().numpy(), col_o) > 80.0
     finally:
         _C.set_prefix_per_tile(old)
