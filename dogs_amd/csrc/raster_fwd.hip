@@ -760,8 +760,12 @@ void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hi
     const uint32_t* gate = phase == 2 ? a.counters + CNT_UNFINISHED : nullptr;
     if (phase == 2) k_bin_count<2><<<blocks, 256, 0, s>>>(a);
     else k_bin_count<1><<<blocks, 256, 0, s>>>(a);
-    exclusive_scan(a.wtot, (uint32_t)waves, a.wtot, total, scan_tmp, s, gate);
-    tile_offsets(a.tile_cnt, (uint32_t)a.num_tiles, a.ranges, s, gate);  // ranges; tile_cnt -> 0 (arrival cursors)
+    if ((uint32_t)waves <= BIN_OFFSETS_MAX_N) {  // one launch: wave offsets + tile ranges, tile_cnt -> 0 (cursors)
+        bin_offsets(a.wtot, (uint32_t)waves, total, a.tile_cnt, (uint32_t)a.num_tiles, a.ranges, s, gate);
+    } else {
+        exclusive_scan(a.wtot, (uint32_t)waves, a.wtot, total, scan_tmp, s, gate);
+        tile_offsets(a.tile_cnt, (uint32_t)a.num_tiles, a.ranges, s, gate);
+    }
     if (phase == 2) k_bin_emit<2><<<blocks, 256, 0, s>>>(a);
     else k_bin_emit<1><<<blocks, 256, 0, s>>>(a);
 }

@@ -414,6 +414,62 @@ void tile_offsets(uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges, hipStre
     if (num_tiles) k_tile_offsets<<<1, 1024, 0, stream>>>(tile_cnt, num_tiles, ranges, gate);
 }
 
+// Block 0: exclusive scan of the wave totals in place (+ total); block 1: the per-tile ranges (tile_offsets).
+// 4 items per thread per 4096-item round, wave shuffle scan + 16 wave sums in LDS, running carry.
+__global__ void __launch_bounds__(1024) k_bin_offsets(uint32_t* __restrict__ wtot, uint32_t n,
+                                                      uint32_t* __restrict__ total, uint32_t* __restrict__ tile_cnt,
+                                                      uint32_t num_tiles, uint2* __restrict__ ranges,
+                                                      const uint32_t* __restrict__ gate) {
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_carry;
+    const bool tiles = blockIdx.x == 1;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (gate && *gate == 0u) {
+        if (!tiles && t == 0) *total = 0u;
+        return;
+    }
+    const uint32_t N = tiles ? num_tiles : n;
+    uint32_t* src = tiles ? tile_cnt : wtot;
+    if (t == 0) s_carry = 0u;
+    __syncthreads();
+    for (uint32_t b = 0; b < N; b += 4096) {
+        const uint32_t i0 = b + 4u * (uint32_t)t;
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = i0 + k < N ? src[i0 + k] : 0u;
+        const uint32_t loc = v[0] + v[1] + v[2] + v[3];
+        uint32_t x = loc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_w[w] = x;
+        __syncthreads();
+        uint32_t off = s_carry, tot = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) { if (k < w) off += s_w[k]; tot += s_w[k]; }
+        uint32_t ex = off + x - loc;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (i0 + k < N) {
+                if (tiles) { ranges[i0 + k] = make_uint2(ex, ex + v[k]); tile_cnt[i0 + k] = 0u; }
+                else wtot[i0 + k] = ex;
+            }
+            ex += v[k];
+        }
+        __syncthreads();
+        if (t == 0) s_carry += tot;
+        __syncthreads();
+    }
+    if (!tiles && t == 0) *total = s_carry;
+}
+
+void bin_offsets(uint32_t* wtot, uint32_t n, uint32_t* total, uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges,
+                 hipStream_t stream, const uint32_t* gate) {
+    k_bin_offsets<<<2, 1024, 0, stream>>>(wtot, n, total, tile_cnt, num_tiles, ranges, gate);
+}
+
 constexpr int DS_WAVE_MAX = 512;
 constexpr int DS_ROWS = DS_WAVE_MAX / 64;
 
