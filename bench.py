@@ -12,7 +12,8 @@ Also reported on the same JSON line:
                 PMC summary of the same command when present (profiles/), else null
   cpu_baseline  the CPU oracle (oracle/gs_oracle.c restating the reference kernels) on one view of the
                 same scene, rank 0 at N = 1 only
-  train_step    secondary figure: fwd + L1 + fused-SSIM fwd/bwd + bwd + SparseGaussianAdam (6 groups)
+  train_step    secondary figure: fwd + L1 + fused-SSIM fwd/bwd + bwd + densification stats + SparseGaussianAdam
+                (6 groups, one launch), and one densify_and_prune timed on the trained state
 """
 from __future__ import annotations
 
@@ -125,8 +126,10 @@ class View:
 
 
 class TrainStep:
-    """Full training iteration of GaussianSplatTrainer.train_iteration (gaussian_trainer.py:324-513) minus
-    densification: activations, raster, L1 + fused-SSIM, backward, SparseGaussianAdam.step(visible, N)."""
+    """Training iteration of GaussianSplatTrainer.train_iteration (gaussian_trainer.py:324-513) before
+    densify_end_iter, without the periodic densify_and_prune: activations, raster, L1 + fused-SSIM, backward, the
+    view's densification statistics (:433-438) and SparseGaussianAdam.step(visible, N) -- the last two in one
+    launch.  densify() times one densify_and_prune (dogs_amd.densify) on the trained state."""
 
     def __init__(self, s, dev, seed):
         from dogs_amd.diff_gaussian_rasterization import (GaussianRasterizationSettings, GaussianRasterizer,
@@ -144,29 +147,48 @@ class TrainStep:
             "f_dc": s.dc.clone().requires_grad_(True),
             "f_rest": s.sh.clone().requires_grad_(True),
             "scaling": s.raw_scales.to(dev).clone().requires_grad_(True),
-            "rotation": s.raw_rotations.to(dev).clone().requires_grad_(True),
+            "quaternion": s.raw_rotations.to(dev).clone().requires_grad_(True),
             "opacity": s.raw_opacities.to(dev).clone().requires_grad_(True),
         }
-        lrs = {"xyz": 1.6e-4, "f_dc": 2.5e-3, "f_rest": 1.25e-4, "scaling": 5e-3, "rotation": 1e-3, "opacity": 2.5e-2}
+        lrs = {"xyz": 1.6e-4, "f_dc": 2.5e-3, "f_rest": 1.25e-4, "scaling": 5e-3, "quaternion": 1e-3, "opacity": 2.5e-2}
         self.opt = SparseGaussianAdam([{"params": [p], "lr": lrs[k], "name": k} for k, p in self.params.items()],
                                       lr=0.0, eps=1e-15)
         g = torch.Generator().manual_seed(seed + 7)
         self.gt = torch.rand((3, c.height, c.width), generator=g).to(dev)
+        N = s.means3D.shape[0]
+        self.stats = {"max_radii2D": torch.zeros(N, device=dev), "grad_accum": torch.zeros((N, 1), device=dev),
+                      "denom": torch.zeros((N, 1), device=dev)}
 
     def step(self):
         p = self.params
         m2d = torch.zeros_like(p["xyz"], requires_grad=True)
         img, radii, _ = self.rast(means3D=p["xyz"], means2D=m2d, opacities=torch.sigmoid(p["opacity"]),
                                   dc=p["f_dc"], shs=p["f_rest"], scales=torch.exp(p["scaling"]),
-                                  rotations=torch.nn.functional.normalize(p["rotation"]))
+                                  rotations=torch.nn.functional.normalize(p["quaternion"]))
         img = img.clamp(0, 1)
         l1 = (img - self.gt).abs().mean()
         ssim = self.fused_ssim(img.unsqueeze(0), self.gt.unsqueeze(0))
         loss = 0.8 * l1 + 0.2 * (1.0 - ssim)
         loss.backward()
         vis = radii > 0
-        self.opt.step(vis, radii.shape[0])
+        self.opt.step(vis, radii.shape[0], stats=dict(self.stats, radii=radii, dmeans2D=m2d.grad))
         self.opt.zero_grad(set_to_none=True)
+
+    def densify(self):
+        """One densify_and_prune (urban3d.yaml thresholds: grad 2e-4, percent_dense 0.01, min opacity 0.005,
+        max_screen_size 20) on the current state: wall ms including its two host syncs."""
+        import types
+        from dogs_amd import densify
+        p = self.params
+        model = types.SimpleNamespace(percent_dense=0.01, xyz_gradient_accum=self.stats["grad_accum"],
+                                      denom=self.stats["denom"], max_radii2D=self.stats["max_radii2D"])
+        for k, a in zip(densify.NAMES, densify.ATTRS):
+            setattr(model, a, p[k])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n_out = densify.densify_and_prune(model, 2e-4, 0.005, 5.0, 20.0, self.opt)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3, n_out
 
 
 def cpu_baseline(n, W, H, seed):
@@ -307,8 +329,11 @@ def main():
             ts.step()
         torch.cuda.synchronize()
         tms = (time.perf_counter() - tt) / nts * 1e3
+        dms, n_after = ts.densify()
         train = {"views_per_s": round(1e3 / tms, 2), "ms_per_step": round(tms, 3),
-                 "includes": "activations + raster fwd/bwd + L1 + fused-SSIM fwd/bwd + SparseGaussianAdam"}
+                 "includes": "activations + raster fwd/bwd + L1 + fused-SSIM fwd/bwd + densification stats + "
+                             "SparseGaussianAdam (one launch)",
+                 "densify_and_prune_ms": round(dms, 3), "gaussians_after_densify": n_after}
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:

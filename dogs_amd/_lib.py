@@ -29,14 +29,42 @@ class DgRasterArgs(C.Structure):
     ]
 
 
+class DgAdamGroup(C.Structure):
+    _fields_ = [("param", C.c_void_p), ("grad", C.c_void_p), ("exp_avg", C.c_void_p), ("exp_avg_sq", C.c_void_p),
+                ("lr", C.c_float), ("eps", C.c_float), ("M", C.c_uint32)]
+
+
+class DgDensifyStats(C.Structure):
+    _fields_ = [("radii", C.c_void_p), ("dmeans2D", C.c_void_p), ("dmeans2D_stride", C.c_uint32),
+                ("max_radii2D", C.c_void_p), ("grad_accum", C.c_void_p), ("denom", C.c_void_p)]
+
+
+class DgGaussianSet(C.Structure):
+    _fields_ = [("N", C.c_uint32), ("params", C.c_void_p * 6), ("exp_avg", C.c_void_p * 6),
+                ("exp_avg_sq", C.c_void_p * 6), ("width", C.c_uint32 * 6), ("grad_accum", C.c_void_p),
+                ("denom", C.c_void_p)]
+
+
+class DgDensifyArgs(C.Structure):
+    _fields_ = [("set", DgGaussianSet), ("max_grad", C.c_float), ("dense_extent", C.c_float),
+                ("replicas", C.c_uint32), ("min_opacity", C.c_float), ("use_bbox", C.c_int), ("bbox_z", C.c_float),
+                ("use_screen", C.c_int), ("max_screen_size", C.c_float), ("big_extent", C.c_float),
+                ("samples", C.c_void_p), ("out_params", C.c_void_p * 6), ("out_exp_avg", C.c_void_p * 6),
+                ("out_exp_avg_sq", C.c_void_p * 6), ("state", C.c_void_p), ("state2", C.c_void_p),
+                ("nc", C.c_uint32), ("ns", C.c_uint32), ("n_out", C.c_uint32)]
+
+
 ALLOC_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int, C.c_uint64)
-DG_BUF_GEOM, DG_BUF_BINNING, DG_BUF_IMAGE, DG_BUF_BACKWARD, DG_BUF_TEMP, DG_BUF_BINNING2 = range(6)
+DG_BUF_GEOM, DG_BUF_BINNING, DG_BUF_IMAGE, DG_BUF_BACKWARD, DG_BUF_TEMP, DG_BUF_BINNING2, DG_BUF_DENSIFY, \
+    DG_BUF_DENSIFY2 = range(8)
 
 EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count", "dg_mark_visible", "dg_rasterize_filter",
            "dg_adam_update", "dg_fused_ssim_forward", "dg_fused_ssim_backward", "dg_dist_cuda2",
            "dg_geom_bytes", "dg_image_bytes", "dg_binning_bytes", "dg_debug_sorted_instances",
            "dg_debug_geometry", "dg_debug_image_state", "dg_sort_pairs_u32", "dg_exclusive_scan_u32",
-           "dg_profile_enable", "dg_profile_collect", "dg_binned_instances",
+           "dg_profile_enable", "dg_profile_collect", "dg_binned_instances", "dg_adam_update_groups",
+           "dg_add_densification_stats", "dg_densify_select", "dg_densify_split_stds", "dg_densify_count",
+           "dg_densify_gather",
            "dg_last_error", "dg_version")
 
 _lib = None
@@ -102,6 +130,21 @@ def load(path: str | None = None):
         L.dg_profile_enable.argtypes = [C.c_int]
         L.dg_profile_collect.restype = C.c_int
         L.dg_profile_collect.argtypes = [C.c_char_p, C.c_int]
+        if hasattr(L, "dg_adam_update_groups"):  # absent in older builds used for A/B runs
+            L.dg_adam_update_groups.restype = C.c_int
+            L.dg_adam_update_groups.argtypes = [C.POINTER(DgAdamGroup), C.c_int, vp, C.c_uint32, C.c_float,
+                                                C.c_float, C.POINTER(DgDensifyStats), vp]
+            L.dg_add_densification_stats.restype = C.c_int
+            L.dg_add_densification_stats.argtypes = [C.POINTER(DgDensifyStats), vp, C.c_uint32, vp]
+            dp = C.POINTER(DgDensifyArgs)
+            L.dg_densify_select.restype = C.c_int
+            L.dg_densify_select.argtypes = [dp, ALLOC_FN, vp, vp]
+            L.dg_densify_split_stds.restype = C.c_int
+            L.dg_densify_split_stds.argtypes = [dp, vp, vp]
+            L.dg_densify_count.restype = C.c_int
+            L.dg_densify_count.argtypes = [dp, ALLOC_FN, vp, vp]
+            L.dg_densify_gather.restype = C.c_int
+            L.dg_densify_gather.argtypes = [dp, vp]
         L.dg_last_error.restype = C.c_char_p
         L.dg_last_error.argtypes = []
         L.dg_version.restype = C.c_int

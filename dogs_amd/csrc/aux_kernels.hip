@@ -142,20 +142,196 @@ __global__ void __launch_bounds__(256) k_ssim_bwd(int H, int W, const float* __r
     }
 }
 
+// ---- wave-strip variant (the one launched).  One wave per strip of 54 output columns x 32 output rows of one
+// plane: the 64 lanes hold 54 + 10 halo columns, so the horizontal 11-tap pass is a chain of DPP wave_shl:1 moves
+// (lane i <- lane i+1) with no LDS at all, and the vertical pass runs over a ring of the last 11 rows' horizontal
+// moments in registers (the 11-row loop is unrolled so every ring slot is a compile-time register).  Same products
+// and the same fma order per moment as k_ssim_fwd/k_ssim_bwd above (x taps 0..10, then y taps 0..10): identical
+// results.  Rows are read 2 ahead of use.
+constexpr int SSW_OUT = 54;   // output columns per wave
+#ifndef DG_SSW_ROWS
+#define DG_SSW_ROWS 32
+#endif
+constexpr int SSW_ROWS = DG_SSW_ROWS;  // output rows per wave
+constexpr int SSW_IN = SSW_ROWS + 10;
+constexpr float GW[11] = {0.001028380123898387f, 0.0075987582094967365f, 0.036000773310661316f,
+                          0.10936068743467331f, 0.21300552785396576f, 0.26601171493530273f,
+                          0.21300552785396576f, 0.10936068743467331f, 0.036000773310661316f,
+                          0.0075987582094967365f, 0.001028380123898387f};
+
+__device__ __forceinline__ float wave_shl1(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x130, 0xf, 0xf, false));
+}
+// sum_k GW[k] * x(lane + k), k = 0..10, as the x-pass of k_ssim_fwd accumulates it
+__device__ __forceinline__ float hconv11(float x) {
+    float acc = fmaf(GW[0], x, 0.0f);
+#pragma unroll
+    for (int k = 1; k < 11; k++) {
+        x = wave_shl1(x);
+        acc = fmaf(GW[k], x, acc);
+    }
+    return acc;
+}
+
+struct StripPos { int x, y0, plane; bool valid; };
+__device__ __forceinline__ StripPos strip_of(int H, int W, int planes) {
+    const int sxn = (W + SSW_OUT - 1) / SSW_OUT, syn = (H + SSW_ROWS - 1) / SSW_ROWS;
+    const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+    StripPos p;
+    p.valid = wid < sxn * syn * planes;
+    const int sx = wid % sxn, sy = (wid / sxn) % syn;
+    p.plane = wid / (sxn * syn);
+    p.x = sx * SSW_OUT - 5 + (threadIdx.x & 63);
+    p.y0 = sy * SSW_ROWS;
+    return p;
+}
+
+template <bool TRAIN>
+__global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes, float C1, float C2,
+                                                        const float* __restrict__ img1, const float* __restrict__ img2,
+                                                        float* __restrict__ map, float* __restrict__ dmu1,
+                                                        float* __restrict__ ds1, float* __restrict__ ds12) {
+    const StripPos sp = strip_of(H, W, planes);
+    if (!sp.valid) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const size_t plane = (size_t)sp.plane * H * W;
+    const float* a = img1 + plane;
+    const float* b = img2 + plane;
+    const bool colok = sp.x >= 0 && sp.x < W;
+    // the lane's window covers columns x .. x+10: its output is column x+5
+    const int ox = sp.x + 5;
+    const bool out_col = lane < SSW_OUT && ox < W;
+    auto ld = [&](const float* img, int row) -> float {
+        return (colok && row >= 0 && row < H) ? img[(size_t)row * W + sp.x] : 0.0f;
+    };
+    float ring[11][5];
+    float ua = ld(a, sp.y0 - 5), va = ld(b, sp.y0 - 5);
+    float ub = ld(a, sp.y0 - 4), vb = ld(b, sp.y0 - 4);
+    for (int base = 0; base < SSW_IN; base += 11) {
+#pragma unroll
+        for (int j = 0; j < 11; j++) {
+            const int rr = base + j;
+            if (rr < SSW_IN) {
+                const float u = ua, v = va;
+                ua = ub; va = vb;
+                ub = ld(a, sp.y0 - 5 + rr + 2);
+                vb = ld(b, sp.y0 - 5 + rr + 2);
+                ring[j][0] = hconv11(u);
+                ring[j][1] = hconv11(u * u);
+                ring[j][2] = hconv11(v);
+                ring[j][3] = hconv11(v * v);
+                ring[j][4] = hconv11(u * v);
+                const int y = sp.y0 + rr - 10;
+                if (rr >= 10 && y < H) {
+                    float m[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+                    for (int k = 0; k < 11; k++) {
+#pragma unroll
+                        for (int q = 0; q < 5; q++) m[q] = fmaf(GW[k], ring[(j + 1 + k) % 11][q], m[q]);
+                    }
+                    if (out_col) {
+                        const float mu1 = m[0], mu2 = m[2];
+                        const float sigma1_sq = fmaf(-mu1, mu1, m[1]);
+                        const float sigma2_sq = fmaf(-mu2, mu2, m[3]);
+                        const float sigma12 = fmaf(-mu1, mu2, m[4]);
+                        const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu1_mu2 = mu1 * mu2;
+                        const float Cc = fmaf(2.0f, mu1_mu2, C1);
+                        const float D = fmaf(2.0f, sigma12, C2);
+                        const float A = (mu1_sq + mu2_sq) + C1;
+                        const float B = (sigma1_sq + sigma2_sq) + C2;
+                        const size_t gi = plane + (size_t)y * W + ox;
+                        map[gi] = (Cc * D) / (A * B);
+                        if (TRAIN) {
+                            dmu1[gi] = ((mu2 * 2.0f * D) / (A * B) - (mu2 * 2.0f * Cc) / (A * B) -
+                                        (mu1 * 2.0f * Cc * D) / (A * A * B) + (mu1 * 2.0f * Cc * D) / (A * B * B));
+                            ds1[gi] = ((-Cc * D) / (A * B * B));
+                            ds12[gi] = ((2 * Cc) / (A * B));
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ssim_bwd_strip(int H, int W, int planes, const float* __restrict__ img1,
+                                                        const float* __restrict__ img2, const float* __restrict__ dL,
+                                                        const float* __restrict__ dmu1, const float* __restrict__ ds1,
+                                                        const float* __restrict__ ds12, float* __restrict__ dimg1) {
+    const StripPos sp = strip_of(H, W, planes);
+    if (!sp.valid) return;
+    const int lane = threadIdx.x & 63;
+    const size_t plane = (size_t)sp.plane * H * W;
+    const bool colok = sp.x >= 0 && sp.x < W;
+    const int ox = sp.x + 5;
+    const bool out_col = lane < SSW_OUT && ox < W;
+    auto ld3 = [&](int row, float& s0, float& s1, float& s2) {
+        if (colok && row >= 0 && row < H) {
+            const size_t gi = plane + (size_t)row * W + sp.x;
+            const float l = dL[gi];
+            s0 = dmu1[gi] * l; s1 = ds1[gi] * l; s2 = ds12[gi] * l;
+        } else {
+            s0 = s1 = s2 = 0.0f;
+        }
+    };
+    float ring[11][3];
+    float a0, a1, a2, b0, b1, b2;
+    ld3(sp.y0 - 5, a0, a1, a2);
+    ld3(sp.y0 - 4, b0, b1, b2);
+    for (int base = 0; base < SSW_IN; base += 11) {
+#pragma unroll
+        for (int j = 0; j < 11; j++) {
+            const int rr = base + j;
+            if (rr < SSW_IN) {
+                const float s0 = a0, s1 = a1, s2 = a2;
+                a0 = b0; a1 = b1; a2 = b2;
+                ld3(sp.y0 - 5 + rr + 2, b0, b1, b2);
+                ring[j][0] = hconv11(s0);
+                ring[j][1] = hconv11(s1);
+                ring[j][2] = hconv11(s2);
+                const int y = sp.y0 + rr - 10;
+                if (rr >= 10 && y < H) {
+                    float v0 = 0, v1 = 0, v2 = 0;
+#pragma unroll
+                    for (int k = 0; k < 11; k++) {
+                        const int q = (j + 1 + k) % 11;
+                        v0 = fmaf(GW[k], ring[q][0], v0);
+                        v1 = fmaf(GW[k], ring[q][1], v1);
+                        v2 = fmaf(GW[k], ring[q][2], v2);
+                    }
+                    if (out_col) {
+                        const size_t gi = plane + (size_t)y * W + ox;
+                        float d = v0;
+                        d += (img1[gi] * 2.0f) * v1;
+                        d += img2[gi] * v2;
+                        dimg1[gi] = d;
+                    }
+                }
+            }
+        }
+    }
+}
+
+static unsigned ssim_strip_blocks(int planes, int H, int W) {
+    const long waves = (long)((W + SSW_OUT - 1) / SSW_OUT) * ((H + SSW_ROWS - 1) / SSW_ROWS) * planes;
+    return (unsigned)((waves + 3) / 4);
+}
+
 void launch_ssim_fwd(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2, float* map,
                      float* dmu1, float* ds1, float* ds12, hipStream_t s) {
     if ((size_t)B * CH * H * W == 0) return;
-    dim3 grid((W + SB - 1) / SB, (H + SB - 1) / SB, B * CH);
+    const unsigned blocks = ssim_strip_blocks(B * CH, H, W);
     if (dmu1)
-        k_ssim_fwd<true><<<grid, 256, 0, s>>>(H, W, C1, C2, img1, img2, map, dmu1, ds1, ds12);
+        k_ssim_fwd_strip<true><<<blocks, 256, 0, s>>>(H, W, B * CH, C1, C2, img1, img2, map, dmu1, ds1, ds12);
     else
-        k_ssim_fwd<false><<<grid, 256, 0, s>>>(H, W, C1, C2, img1, img2, map, nullptr, nullptr, nullptr);
+        k_ssim_fwd_strip<false><<<blocks, 256, 0, s>>>(H, W, B * CH, C1, C2, img1, img2, map, nullptr, nullptr,
+                                                        nullptr);
 }
 void launch_ssim_bwd(int B, int CH, int H, int W, const float* img1, const float* img2, const float* dL,
                      const float* dmu1, const float* ds1, const float* ds12, float* dimg1, hipStream_t s) {
     if ((size_t)B * CH * H * W == 0) return;
-    dim3 grid((W + SB - 1) / SB, (H + SB - 1) / SB, B * CH);
-    k_ssim_bwd<<<grid, 256, 0, s>>>(H, W, img1, img2, dL, dmu1, ds1, ds12, dimg1);
+    k_ssim_bwd_strip<<<ssim_strip_blocks(B * CH, H, W), 256, 0, s>>>(H, W, B * CH, img1, img2, dL, dmu1, ds1, ds12,
+                                                                      dimg1);
 }
 
 // ------------------------------------------------------------------------------------------------

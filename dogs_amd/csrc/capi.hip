@@ -11,6 +11,7 @@
 
 #include "../../include/dogs_hip.h"
 #include "aux_kernels.h"
+#include "optim.h"
 #include "raster.h"
 #include "sortscan.h"
 
@@ -654,6 +655,213 @@ int dg_rasterize_filter(const dg_raster_args* a, int* radii, dg_stream_t stream)
     HIP_OK(hipFreeAsync(err, (hipStream_t)stream));
     HIP_OK(hipStreamSynchronize((hipStream_t)stream));
     if (h) return fail("a Gaussian was filtered although prefiltered is set%s%d");
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+static int fill_stats(gs::AdamMultiArgs& m, const dg_densify_stats* st) {
+    if (!st) return 0;
+    if (!st->radii || !st->dmeans2D || !st->max_radii2D || !st->grad_accum || !st->denom)
+        return fail("densification statistics need radii, dmeans2D, max_radii2D, grad_accum and denom%s%d");
+    if (st->dmeans2D_stride < 2) return fail("dmeans2D_stride must be >= 2%s%d");
+    m.radii = st->radii; m.dmeans2D = st->dmeans2D; m.dm_stride = st->dmeans2D_stride;
+    m.max_radii2D = st->max_radii2D; m.grad_accum = st->grad_accum; m.denom = st->denom;
+    return 0;
+}
+
+int dg_adam_update_groups(const dg_adam_group* groups, int n_groups, const uint8_t* visible, uint32_t N, float b1,
+                          float b2, const dg_densify_stats* stats, dg_stream_t stream) {
+    if (n_groups < 0 || n_groups > gs::MAX_ADAM_GROUPS) return fail("n_groups must be 0..8%s (got %d)", "", n_groups);
+    if (N && !visible) return fail("visible mask required%s%d");
+    gs::AdamMultiArgs m;
+    memset(&m, 0, sizeof(m));
+    m.visible = visible; m.N = N; m.b1 = b1; m.b2 = b2;
+    int n = 0;
+    for (int k = 0; k < n_groups; k++) {
+        const dg_adam_group& g = groups[k];
+        if (g.M == 0) continue;
+        if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq) return fail("adam group %s%d has a NULL tensor", "", k);
+        if ((uint64_t)N * g.M >= 0xfffff000ull) return fail("adam group %s%d: N * M must be < 2^32", "", k);
+        gs::AdamGroup& d = m.g[n++];
+        d.param = g.param; d.grad = g.grad; d.m = g.exp_avg; d.v = g.exp_avg_sq; d.lr = g.lr; d.eps = g.eps; d.M = g.M;
+        const uintptr_t al = reinterpret_cast<uintptr_t>(g.param) | reinterpret_cast<uintptr_t>(g.grad) |
+                             reinterpret_cast<uintptr_t>(g.exp_avg) | reinterpret_cast<uintptr_t>(g.exp_avg_sq);
+        d.vec = (al & 15u) == 0u;
+    }
+    m.n = n;
+    if (fill_stats(m, stats)) return 1;
+    if (N) gs::launch_adam_multi(m, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_add_densification_stats(const dg_densify_stats* stats, const uint8_t* visible, uint32_t N, dg_stream_t stream) {
+    if (!stats) return fail("stats required%s%d");
+    return dg_adam_update_groups(nullptr, 0, visible, N, 0.9f, 0.999f, stats, stream);
+}
+
+namespace {
+struct DensifyState {  // DG_BUF_DENSIFY: selection of the N originals
+    uint32_t *clone_flag, *split_flag, *clone_pos, *split_pos, *clone_idx, *split_idx, *totals;
+    void* scan_tmp;
+    size_t bytes;
+};
+DensifyState carve_densify(void* base, uint32_t N) {
+    Carver c(base);
+    DensifyState d;
+    const size_t n = N ? N : 1;
+    d.clone_flag = c.take<uint32_t>(n); d.split_flag = c.take<uint32_t>(n);
+    d.clone_pos = c.take<uint32_t>(n); d.split_pos = c.take<uint32_t>(n);
+    d.clone_idx = c.take<uint32_t>(n); d.split_idx = c.take<uint32_t>(n);
+    d.totals = c.take<uint32_t>(4);
+    d.scan_tmp = c.take<char>(gs::scan_temp_bytes((uint32_t)n));
+    d.bytes = c.off;
+    return d;
+}
+struct KeepState {  // DG_BUF_DENSIFY2: the C candidate rows
+    uint32_t *keep, *keep_pos, *total;
+    void* scan_tmp;
+    size_t bytes;
+};
+KeepState carve_keep(void* base, uint64_t C) {
+    Carver c(base);
+    KeepState k;
+    const size_t n = C ? (size_t)C : 1;
+    k.keep = c.take<uint32_t>(n); k.keep_pos = c.take<uint32_t>(n); k.total = c.take<uint32_t>(4);
+    k.scan_tmp = c.take<char>(gs::scan_temp_bytes((uint32_t)n));
+    k.bytes = c.off;
+    return k;
+}
+int densify_check(const dg_densify_args* a) {
+    if (!a) return fail("null densify args%s%d");
+    const dg_gaussian_set& g = a->set;
+    for (int q = 0; q < 6; q++) {
+        if (g.N && !g.params[q]) return fail("parameter tensor %s%d is NULL", "", q);
+        if ((g.exp_avg[q] == nullptr) != (g.exp_avg_sq[q] == nullptr))
+            return fail("exp_avg / exp_avg_sq of tensor %s%d: both or neither", "", q);
+    }
+    if (g.width[0] != 3 || g.width[4] != 3 || g.width[5] != 4 || g.width[3] != 1)
+        return fail("widths must be xyz 3, opacity 1, scaling 3, quaternion 4%s%d");
+    if (g.N && (!g.grad_accum || !g.denom)) return fail("grad_accum and denom required%s%d");
+    return 0;
+}
+gs::DensifyArgs densify_args(const dg_densify_args* a, const DensifyState& st) {
+    gs::DensifyArgs d;
+    memset(&d, 0, sizeof(d));
+    const dg_gaussian_set& g = a->set;
+    d.N = g.N;
+    d.xyz = g.params[0]; d.f_dc = g.params[1]; d.f_rest = g.params[2]; d.opacity = g.params[3];
+    d.scaling = g.params[4]; d.rot = g.params[5];
+    for (int q = 0; q < 6; q++) { d.m[q] = g.exp_avg[q]; d.v[q] = g.exp_avg_sq[q]; d.width[q] = g.width[q]; }
+    d.grad_accum = g.grad_accum; d.denom = g.denom;
+    d.grad_threshold = a->max_grad; d.dense_extent = a->dense_extent;
+    d.clone_flag = st.clone_flag; d.split_flag = st.split_flag;
+    return d;
+}
+}  // namespace
+
+int dg_densify_select(dg_densify_args* a, dg_alloc_fn alloc, void* user, dg_stream_t stream) {
+    if (densify_check(a)) return 1;
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t N = a->set.N;
+    a->nc = a->ns = a->n_out = 0;
+    a->state = alloc(user, DG_BUF_DENSIFY, carve_densify(nullptr, N).bytes);
+    if (!a->state) return fail("densify state allocation failed%s%d");
+    a->state2 = nullptr;
+    if (N == 0) return 0;
+    DensifyState st = carve_densify(a->state, N);
+    gs::DensifyArgs d = densify_args(a, st);
+    gs::launch_densify_select(d, s);
+    gs::exclusive_scan(st.clone_flag, N, st.clone_pos, st.totals, st.scan_tmp, s);
+    gs::exclusive_scan(st.split_flag, N, st.split_pos, st.totals + 1, st.scan_tmp, s);
+    gs::launch_densify_lists(d, st.clone_pos, st.split_pos, st.clone_idx, st.split_idx, s);
+    uint32_t h[2];
+    HIP_OK(hipMemcpyAsync(h, st.totals, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    a->nc = h[0];
+    a->ns = h[1];
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+namespace {
+__global__ void k_split_stds(const uint32_t* __restrict__ split_idx, uint32_t ns, uint32_t replicas,
+                             const float* __restrict__ scaling, float* __restrict__ stds) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= 3u * ns * replicas) return;
+    const uint32_t row = t / 3u, c = t % 3u;
+    stds[t] = expf(scaling[3 * (size_t)split_idx[row % ns] + c]);
+}
+}  // namespace
+
+int dg_densify_split_stds(const dg_densify_args* a, float* stds, dg_stream_t stream) {
+    if (!a || !a->state) return fail("dg_densify_select first%s%d");
+    if (a->ns == 0) return 0;
+    const uint32_t r = a->replicas ? a->replicas : 2;
+    DensifyState st = carve_densify(a->state, a->set.N);
+    const uint32_t n = 3u * a->ns * r;
+    k_split_stds<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(st.split_idx, a->ns, r, a->set.params[4], stds);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+namespace {
+gs::RebuildArgs rebuild_args(const dg_densify_args* a, const DensifyState& st, const KeepState& ks) {
+    gs::RebuildArgs r;
+    memset(&r, 0, sizeof(r));
+    r.d = densify_args(a, st);
+    r.nc = a->nc; r.ns = a->ns; r.replicas = a->replicas ? a->replicas : 2;
+    r.clone_idx = st.clone_idx; r.split_idx = st.split_idx; r.samples = a->samples;
+    r.min_opacity = a->min_opacity; r.use_bbox = a->use_bbox; r.bbox_z = a->bbox_z;
+    r.use_screen = a->use_screen; r.max_screen = a->max_screen_size; r.big_extent = a->big_extent;
+    r.keep = ks.keep;
+    for (int q = 0; q < 6; q++) { r.out_p[q] = a->out_params[q]; r.out_m[q] = a->out_exp_avg[q]; r.out_v[q] = a->out_exp_avg_sq[q]; }
+    return r;
+}
+}  // namespace
+
+int dg_densify_count(dg_densify_args* a, dg_alloc_fn alloc, void* user, dg_stream_t stream) {
+    if (densify_check(a)) return 1;
+    if (!a->state) return fail("dg_densify_select first%s%d");
+    if (a->ns && !a->samples) return fail("samples [replicas*ns, 3] required%s%d");
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t r = a->replicas ? a->replicas : 2;
+    const uint64_t C = (uint64_t)a->set.N + a->nc + (uint64_t)r * a->ns;
+    uint64_t wsum = 0;
+    for (int q = 0; q < 6; q++) wsum += a->set.width[q];
+    if (C * wsum >= 0xfffff000ull) return fail("too many candidate rows x floats%s%d");
+    a->state2 = alloc(user, DG_BUF_DENSIFY2, carve_keep(nullptr, C).bytes);
+    if (!a->state2) return fail("densify candidate allocation failed%s%d");
+    a->n_out = 0;
+    if (C == 0) return 0;
+    DensifyState st = carve_densify(a->state, a->set.N);
+    KeepState ks = carve_keep(a->state2, C);
+    gs::RebuildArgs rb = rebuild_args(a, st, ks);
+    gs::launch_densify_keep(rb, s);
+    gs::exclusive_scan(ks.keep, (uint32_t)C, ks.keep_pos, ks.total, ks.scan_tmp, s);
+    uint32_t h = 0;
+    HIP_OK(hipMemcpyAsync(&h, ks.total, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    a->n_out = h;
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_densify_gather(const dg_densify_args* a, dg_stream_t stream) {
+    if (densify_check(a)) return 1;
+    if (!a->state || !a->state2) return fail("dg_densify_select and dg_densify_count first%s%d");
+    for (int q = 0; q < 6; q++) {
+        if (a->n_out && !a->out_params[q]) return fail("output tensor %s%d is NULL", "", q);
+        if ((a->out_exp_avg[q] == nullptr) != (a->out_exp_avg_sq[q] == nullptr))
+            return fail("output moments of tensor %s%d: both or neither", "", q);
+    }
+    if (a->n_out == 0) return 0;
+    const uint32_t r = a->replicas ? a->replicas : 2;
+    const uint64_t C = (uint64_t)a->set.N + a->nc + (uint64_t)r * a->ns;
+    DensifyState st = carve_densify(a->state, a->set.N);
+    KeepState ks = carve_keep(a->state2, C);
+    gs::RebuildArgs rb = rebuild_args(a, st, ks);
+    gs::launch_densify_gather(rb, ks.keep_pos, (hipStream_t)stream);
     HIP_OK(hipGetLastError());
     return 0;
 }

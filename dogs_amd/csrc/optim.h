@@ -1,0 +1,82 @@
+// optim.h -- the optimizer side of a training view:
+//   * SparseGaussianAdam over all parameter groups in one launch (adam.cu:10-38 per group), with the densification
+//     statistics of the same view (gaussian_trainer.py:433-438, gaussian_splat_model.py:533-541) folded in;
+//   * densify_and_prune (gaussian_splat_model.py:434-531) as GPU stream compaction: selection, one candidate pass
+//     over [originals not split | clones | split children], one gather of every parameter and Adam moment.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gs {
+
+constexpr int MAX_ADAM_GROUPS = 8;
+
+struct AdamGroup {
+    float* param;
+    const float* grad;
+    float* m;
+    float* v;
+    float lr, eps;
+    uint32_t M;       // floats per Gaussian
+    uint32_t vec;     // 1: param/grad/m/v 16-byte aligned (float4 path)
+};
+
+struct AdamMultiArgs {
+    AdamGroup g[MAX_ADAM_GROUPS];
+    uint32_t start[MAX_ADAM_GROUPS + 2];  // first work item of group k (items = 4-float chunks); start[n] = stats
+    int n;
+    const uint8_t* visible;  // [N]
+    uint32_t N;
+    float b1, b2;
+    // densification statistics (optional: radii == nullptr)
+    const int* radii;          // [N]
+    const float* dmeans2D;     // [N, stride] screen-space gradient (x, y used)
+    uint32_t dm_stride;
+    float* max_radii2D;        // [N]
+    float* grad_accum;         // [N]
+    float* denom;              // [N]
+};
+void launch_adam_multi(const AdamMultiArgs& a, hipStream_t s);
+
+// ---- densify_and_prune
+struct DensifyArgs {
+    uint32_t N;
+    // parameters (raw, as stored by the model) and their Adam moments (m/v may be null: no optimizer state)
+    const float *xyz, *f_dc, *f_rest, *opacity, *scaling, *rot;
+    const float *m[6], *v[6];
+    uint32_t width[6];         // floats per Gaussian: xyz 3, f_dc 3*, f_rest 3*(M), opacity 1, scaling 3, rot 4
+    const float* grad_accum;   // [N]
+    const float* denom;        // [N]
+    float grad_threshold, dense_extent;  // max_grad, percent_dense * extent
+    // selection outputs (device scratch, 0/1 per original)
+    uint32_t* clone_flag;      // [N]
+    uint32_t* split_flag;      // [N]
+};
+struct RebuildArgs {
+    DensifyArgs d;
+    uint32_t nc, ns, replicas;
+    const uint32_t* clone_idx;  // [nc]
+    const uint32_t* split_idx;  // [ns]
+    const float* samples;       // [replicas * ns, 3]
+    float min_opacity;
+    int use_bbox;
+    float bbox_z;
+    int use_screen;             // max_screen_size is not None
+    float max_screen, big_extent;  // max_screen_size, 0.1 * extent
+    uint32_t* keep;             // [C] 0/1 per candidate row
+    // outputs: [Nf, width] each
+    float* out_p[6];
+    float* out_m[6];
+    float* out_v[6];
+};
+// clone/split flags (0/1) of every original Gaussian
+void launch_densify_select(const DensifyArgs& a, hipStream_t s);
+// clone_idx / split_idx from the scanned flags
+void launch_densify_lists(const DensifyArgs& a, const uint32_t* clone_pos, const uint32_t* split_pos,
+                          uint32_t* clone_idx, uint32_t* split_idx, hipStream_t s);
+// keep flags of the candidates (C = N + nc + replicas * ns)
+void launch_densify_keep(const RebuildArgs& a, hipStream_t s);
+// gather of the kept candidates into out_* (positions = scanned keep)
+void launch_densify_gather(const RebuildArgs& a, const uint32_t* keep_pos, hipStream_t s);
+
+}  // namespace gs

@@ -1,0 +1,268 @@
+// optim.hip -- optimizer-side kernels of a training view (optim.h).
+//
+// k_adam_multi      SparseGaussianAdam.step (diff_gaussian_rasterization/__init__.py:303-332 -> adam.cu:10-38) for
+//                   every parameter group in one launch, plus the view's densification statistics
+//                   (gaussian_trainer.py:433-438 max_radii2D, gaussian_splat_model.py:533-541 add_densification_stats).
+//                   Blocks are assigned to groups in contiguous ranges (block-uniform group, scalar kernel-argument
+//                   loads); each lane updates 4 consecutive floats (float4 when the group is 16-byte aligned).
+//                   HBM-bound: 28 B per visible float (read param/grad/m/v, write param/m/v).
+// k_densify_*       densify_and_prune (gaussian_splat_model.py:434-531) as stream compaction: clone/split selection,
+//                   keep flags over the candidate rows [originals not split | clones | split children], one gather.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "optim.h"
+
+namespace gs {
+
+namespace {
+
+__device__ __forceinline__ float adam_one(float p, float gr, float& m, float& v, float lr, float b1, float b2, float eps) {
+    // adam.cu:21-28 (same expression shape as aux_kernels.hip k_adam)
+    const float em = fmaf(b1, m, (1.0f - b1) * gr);
+    const float ev = fmaf(b2, v, ((1.0f - b2) * gr) * gr);
+    m = em;
+    v = ev;
+    return p + (-lr * em / (sqrtf(ev) + eps));
+}
+
+__global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
+    const uint32_t blk = blockIdx.x;
+    if (blk >= a.start[a.n]) {  // densification statistics, one Gaussian per lane
+        const uint32_t i = (blk - a.start[a.n]) * 256u + threadIdx.x;
+        if (i >= a.N || !a.visible[i]) return;
+        // max_radii2D[vis] = max(max_radii2D[vis], radii[vis]) (float result: radii promote to float)
+        const float r = (float)a.radii[i];
+        const float mr = a.max_radii2D[i];
+        a.max_radii2D[i] = r > mr ? r : mr;
+        // xyz_gradient_accum[vis] += ||grad[vis, :2]||, denom[vis] += 1
+        const float gx = a.dmeans2D[(size_t)i * a.dm_stride], gy = a.dmeans2D[(size_t)i * a.dm_stride + 1];
+        a.grad_accum[i] += sqrtf(gx * gx + gy * gy);
+        a.denom[i] += 1.0f;
+        return;
+    }
+    int k = 0;
+    while (k + 1 < a.n && blk >= a.start[k + 1]) k++;  // block-uniform
+    const AdamGroup g = a.g[k];
+    // N * M < 2^32 (checked on the host): 32-bit index math, one division per lane
+    const uint32_t total = a.N * g.M;
+    const uint32_t e0 = 4u * ((blk - a.start[k]) * 256u + threadIdx.x);
+    if (e0 >= total) return;
+    const float b1 = a.b1, b2 = a.b2;
+    uint32_t gi = e0 / g.M, r = e0 - gi * g.M;
+    bool vis[4];
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        vis[j] = e0 + j < total && a.visible[gi] != 0;
+        any |= vis[j];
+        if (++r == g.M) { r = 0; gi++; }
+    }
+    if (!any) return;
+    if (g.vec && e0 + 4 <= total) {
+        float4 p = *reinterpret_cast<const float4*>(g.param + e0);
+        const float4 gr = *reinterpret_cast<const float4*>(g.grad + e0);
+        float4 m = *reinterpret_cast<const float4*>(g.m + e0);
+        float4 v = *reinterpret_cast<const float4*>(g.v + e0);
+        if (vis[0]) p.x = adam_one(p.x, gr.x, m.x, v.x, g.lr, b1, b2, g.eps);
+        if (vis[1]) p.y = adam_one(p.y, gr.y, m.y, v.y, g.lr, b1, b2, g.eps);
+        if (vis[2]) p.z = adam_one(p.z, gr.z, m.z, v.z, g.lr, b1, b2, g.eps);
+        if (vis[3]) p.w = adam_one(p.w, gr.w, m.w, v.w, g.lr, b1, b2, g.eps);
+        *reinterpret_cast<float4*>(g.param + e0) = p;
+        *reinterpret_cast<float4*>(g.m + e0) = m;
+        *reinterpret_cast<float4*>(g.v + e0) = v;
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        if (!vis[j]) continue;
+        const uint32_t e = e0 + j;
+        float m = g.m[e], v = g.v[e];
+        g.param[e] = adam_one(g.param[e], g.grad[e], m, v, g.lr, b1, b2, g.eps);
+        g.m[e] = m;
+        g.v[e] = v;
+    }
+}
+
+// ---- densify_and_prune
+
+__device__ __forceinline__ float max_scale(const float* s) {
+    // torch.max(get_scaling, dim=1).values, get_scaling = exp(_scaling)
+    const float a = expf(s[0]), b = expf(s[1]), c = expf(s[2]);
+    const float ab = a > b ? a : b;
+    return ab > c ? ab : c;
+}
+
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// densify_and_clone / densify_and_split selection (gaussian_splat_model.py:434-441, 464-469):
+// grads = accum / denom (NaN -> 0); clone: |grads| >= thr and max scale <= percent_dense * extent;
+// split: grads >= thr and max scale > percent_dense * extent (clones are appended with padded grad 0: never split).
+__global__ void __launch_bounds__(256) k_densify_select(DensifyArgs a) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= a.N) return;
+    float g = a.grad_accum[i] / a.denom[i];
+    if (g != g) g = 0.0f;
+    const float ms = max_scale(a.scaling + 3 * (size_t)i);
+    a.clone_flag[i] = (fabsf(g) >= a.grad_threshold && ms <= a.dense_extent) ? 1u : 0u;
+    a.split_flag[i] = (g >= a.grad_threshold && ms > a.dense_extent) ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(256) k_densify_lists(DensifyArgs a, const uint32_t* __restrict__ clone_pos,
+                                                       const uint32_t* __restrict__ split_pos,
+                                                       uint32_t* __restrict__ clone_idx, uint32_t* __restrict__ split_idx) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= a.N) return;
+    if (a.clone_flag[i]) clone_idx[clone_pos[i]] = i;
+    if (a.split_flag[i]) split_idx[split_pos[i]] = i;
+}
+
+// Candidate row r: r < N original r (dropped when split), then nc clones, then replicas x ns split children
+// (torch .repeat(replicas, 1): replica-major).  src = the original it comes from; child = replica index + 1 or 0.
+struct Cand { uint32_t src; int kind; };  // kind 0 original, 1 clone, 2 child
+__device__ __forceinline__ Cand cand_of(const RebuildArgs& a, uint32_t r) {
+    if (r < a.d.N) return {r, 0};
+    r -= a.d.N;
+    if (r < a.nc) return {a.clone_idx[r], 1};
+    r -= a.nc;
+    return {a.split_idx[r % a.ns], 2};
+}
+
+// normalize_quaternion + quaternion_to_rotation_mat (utils.py:20-67), one op at a time as torch evaluates them;
+// row c of R only (c may differ per lane: selects, no indexed local array)
+__device__ __forceinline__ void rot_row(const float* q, int c, float& a0, float& a1, float& a2) {
+    const float n = sqrtf(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]);
+    const float r = q[0] / n, x = q[1] / n, y = q[2] / n, z = q[3] / n;
+    if (c == 0) {
+        a0 = 1.0f - 2.0f * (y * y + z * z); a1 = 2.0f * (x * y - r * z); a2 = 2.0f * (x * z + r * y);
+    } else if (c == 1) {
+        a0 = 2.0f * (x * y + r * z); a1 = 1.0f - 2.0f * (x * x + z * z); a2 = 2.0f * (y * z - r * x);
+    } else {
+        a0 = 2.0f * (x * z - r * y); a1 = 2.0f * (y * z + r * x); a2 = 1.0f - 2.0f * (x * x + y * y);
+    }
+}
+
+// split child k (gaussian_splat_model.py:471-483): xyz = R(q) @ sample + xyz (bmm: k = 3 fma chain),
+// scaling = log(exp(s) / (0.8 * replicas))
+__device__ __forceinline__ float child_xyz(const RebuildArgs& a, uint32_t k, uint32_t src, int c) {
+    float r0, r1, r2;
+    rot_row(a.d.rot + 4 * (size_t)src, c, r0, r1, r2);
+    const float* smp = a.samples + 3 * (size_t)k;
+    const float dot = fmaf(r2, smp[2], fmaf(r1, smp[1], r0 * smp[0]));
+    return dot + a.d.xyz[3 * (size_t)src + c];
+}
+__device__ __forceinline__ float child_scaling(const RebuildArgs& a, uint32_t src, int c) {
+    // torch divides by a Python scalar on the GPU as a multiplication by its float reciprocal
+    const float inv = 1.0f / (float)(0.8 * (double)a.replicas);
+    return logf(expf(a.d.scaling[3 * (size_t)src + c]) * inv);
+}
+
+// prune mask (gaussian_splat_model.py:516-528) of a candidate row.  densification_postfix reset max_radii2D to zeros
+// before this test, so big_points_vs reduces to 0 > max_screen_size, as in the reference.
+__global__ void __launch_bounds__(256) k_densify_keep(RebuildArgs a) {
+    const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t C = a.d.N + a.nc + a.replicas * a.ns;
+    if (r >= C) return;
+    const Cand c = cand_of(a, r);
+    uint32_t keep = 1u;
+    if (c.kind == 0 && a.d.split_flag[c.src]) keep = 0u;
+    float z, s[3];
+    if (c.kind == 2) {
+        const uint32_t k = r - a.d.N - a.nc;
+        z = child_xyz(a, k, c.src, 2);
+        for (int j = 0; j < 3; j++) s[j] = child_scaling(a, c.src, j);
+    } else {
+        z = a.d.xyz[3 * (size_t)c.src + 2];
+        for (int j = 0; j < 3; j++) s[j] = a.d.scaling[3 * (size_t)c.src + j];
+    }
+    bool prune = sigmoid_f(a.d.opacity[c.src]) < a.min_opacity;
+    if (a.use_bbox) prune = prune || z < a.bbox_z;
+    if (a.use_screen) prune = prune || (0.0f > a.max_screen) || max_scale(s) > a.big_extent;
+    if (prune) keep = 0u;
+    a.keep[r] = keep;
+}
+
+// One lane per (candidate, float) of one group; blocks are assigned to the six groups in contiguous ranges
+// (gstart[q], block-uniform group), so every lane of a wave reads and writes one array, coalesced.  Params from the
+// source row (children: new xyz / scaling), Adam moments copied for originals, zero for appended rows
+// (cat_tensors_to_optimizer: zeros_like).
+template <int Q>
+__device__ __forceinline__ void gather_group(const RebuildArgs& a, const uint32_t* __restrict__ keep_pos, uint32_t t,
+                                             uint32_t C) {
+    const uint32_t w = a.d.width[Q];
+    const uint32_t r = t / w;
+    if (r >= C || !a.keep[r]) return;
+    const uint32_t e = t - r * w;
+    const Cand c = cand_of(a, r);
+    const float* src = Q == 0 ? a.d.xyz : Q == 1 ? a.d.f_dc : Q == 2 ? a.d.f_rest : Q == 3 ? a.d.opacity
+                     : Q == 4 ? a.d.scaling : a.d.rot;
+    float val;
+    if (Q == 0 && c.kind == 2) val = child_xyz(a, r - a.d.N - a.nc, c.src, (int)e);
+    else if (Q == 4 && c.kind == 2) val = child_scaling(a, c.src, (int)e);
+    else val = src[(size_t)c.src * w + e];
+    const size_t o = (size_t)keep_pos[r] * w + e;
+    a.out_p[Q][o] = val;
+    if (a.out_m[Q]) a.out_m[Q][o] = (c.kind == 0 && a.d.m[Q]) ? a.d.m[Q][(size_t)c.src * w + e] : 0.0f;
+    if (a.out_v[Q]) a.out_v[Q][o] = (c.kind == 0 && a.d.v[Q]) ? a.d.v[Q][(size_t)c.src * w + e] : 0.0f;
+}
+
+struct GatherGrid { uint32_t start[7]; };
+
+__global__ void __launch_bounds__(256) k_densify_gather(RebuildArgs a, const uint32_t* __restrict__ keep_pos,
+                                                        GatherGrid gg) {
+    const uint32_t blk = blockIdx.x;
+    const uint32_t C = a.d.N + a.nc + a.replicas * a.ns;
+    int q = 0;
+    while (q < 5 && blk >= gg.start[q + 1]) q++;  // block-uniform
+    const uint32_t t = (blk - gg.start[q]) * 256u + threadIdx.x;  // C * width < 2^32 (checked on the host)
+    switch (q) {
+        case 0: gather_group<0>(a, keep_pos, t, C); break;
+        case 1: gather_group<1>(a, keep_pos, t, C); break;
+        case 2: gather_group<2>(a, keep_pos, t, C); break;
+        case 3: gather_group<3>(a, keep_pos, t, C); break;
+        case 4: gather_group<4>(a, keep_pos, t, C); break;
+        default: gather_group<5>(a, keep_pos, t, C); break;
+    }
+}
+
+}  // namespace
+
+void launch_adam_multi(const AdamMultiArgs& a0, hipStream_t s) {
+    AdamMultiArgs a = a0;
+    // start[] in blocks: each group gets ceil(N*M / 4 / 256) blocks, the statistics ceil(N / 256)
+    uint32_t b = 0;
+    for (int k = 0; k < a.n; k++) {
+        a.start[k] = b;
+        const uint64_t items = ((uint64_t)a.N * a.g[k].M + 3) / 4;
+        b += (uint32_t)((items + 255) / 256);
+    }
+    a.start[a.n] = b;
+    if (a.radii) b += (a.N + 255) / 256;
+    if (b == 0) return;
+    k_adam_multi<<<b, 256, 0, s>>>(a);
+}
+
+void launch_densify_select(const DensifyArgs& a, hipStream_t s) {
+    if (a.N) k_densify_select<<<(a.N + 255) / 256, 256, 0, s>>>(a);
+}
+void launch_densify_lists(const DensifyArgs& a, const uint32_t* clone_pos, const uint32_t* split_pos,
+                          uint32_t* clone_idx, uint32_t* split_idx, hipStream_t s) {
+    if (a.N) k_densify_lists<<<(a.N + 255) / 256, 256, 0, s>>>(a, clone_pos, split_pos, clone_idx, split_idx);
+}
+void launch_densify_keep(const RebuildArgs& a, hipStream_t s) {
+    const uint32_t C = a.d.N + a.nc + a.replicas * a.ns;
+    if (C) k_densify_keep<<<(C + 255) / 256, 256, 0, s>>>(a);
+}
+void launch_densify_gather(const RebuildArgs& a, const uint32_t* keep_pos, hipStream_t s) {
+    const uint64_t C = (uint64_t)a.d.N + a.nc + (uint64_t)a.replicas * a.ns;
+    GatherGrid gg;
+    uint32_t b = 0;
+    for (int q = 0; q < 6; q++) {
+        gg.start[q] = b;
+        b += (uint32_t)((C * a.d.width[q] + 255) / 256);
+    }
+    gg.start[6] = b;
+    if (b) k_densify_gather<<<b, 256, 0, s>>>(a, keep_pos, gg);
+}
+
+}  // namespace gs

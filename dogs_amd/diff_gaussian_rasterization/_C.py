@@ -223,3 +223,47 @@ def fusedssim_backward(C1, C2, img1, img2, dL_dmap):
     a, b = img1.unsqueeze(0), img2.unsqueeze(0)
     _, d1, d2, d3 = _cuda.fusedssim(C1, C2, a, b, True)
     return _cuda.fusedssim_backward(C1, C2, a, b, dL_dmap.unsqueeze(0), d1, d2, d3)[0]
+
+
+def adam_update_groups(groups, visible, N, b1=0.9, b2=0.999, stats=None):
+    """SparseGaussianAdam over several groups in one launch (dg_adam_update_groups; each group as adamUpdate).
+    groups: iterable of (param, grad, exp_avg, exp_avg_sq, lr, eps); stats (optional): dict with radii [N] int32,
+    dmeans2D [N,>=2] (screen-space-point gradient), max_radii2D [N], grad_accum [N(,1)], denom [N(,1)] -- the view's
+    densification statistics (gaussian_trainer.py:433-438), updated in the same launch."""
+    groups = list(groups)
+    vis = visible.contiguous()
+    if vis.dtype != torch.bool:
+        vis = vis.bool()
+    dev = vis.device
+    keep = [vis]
+    arr = (_lib.DgAdamGroup * max(1, min(8, len(groups))))()
+    st = None
+    if stats is not None:
+        dm = stats["dmeans2D"]
+        if dm.dim() != 2 or dm.stride(1) != 1 or dm.size(1) < 2:
+            dm = dm.reshape(int(N), -1).contiguous()
+        for k in ("max_radii2D", "grad_accum", "denom"):
+            t = stats[k]
+            if not t.is_contiguous() or t.dtype != torch.float32:
+                raise RuntimeError(f"{k} must be a contiguous float32 tensor (updated in place)")
+        radii = stats["radii"].contiguous()
+        if radii.dtype != torch.int32:
+            radii = radii.int()
+        keep += [dm, radii]
+        st = _lib.DgDensifyStats(radii.data_ptr(), dm.data_ptr(), int(dm.stride(0)), stats["max_radii2D"].data_ptr(),
+                                 stats["grad_accum"].data_ptr(), stats["denom"].data_ptr())
+    L = _lib.load()
+    with torch.cuda.device(dev):
+        for c0 in range(0, max(1, len(groups)), 8):
+            chunk = groups[c0:c0 + 8]
+            for i, (param, grad, m, v, lr, eps) in enumerate(chunk):
+                for t, n in ((param, "param"), (grad, "grad"), (m, "exp_avg"), (v, "exp_avg_sq")):
+                    _lib.require_device(t, n)
+                    if not t.is_contiguous() or t.dtype != torch.float32:
+                        raise RuntimeError(f"{n} must be a contiguous float32 tensor")
+                arr[i] = _lib.DgAdamGroup(param.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(), float(lr),
+                                          float(eps), int(param.numel() // N) if N else 0)
+            _lib.check(L.dg_adam_update_groups(arr, len(chunk), vis.data_ptr(), int(N), float(b1), float(b2),
+                                               C.byref(st) if (st is not None and c0 == 0) else None,
+                                               _lib.stream_of(dev)))
+    del keep

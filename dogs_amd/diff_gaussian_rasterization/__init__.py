@@ -172,13 +172,16 @@ class GaussianRasterizer(nn.Module):
 
 
 class SparseGaussianAdam(torch.optim.Adam):
-    """Adam restricted to visible Gaussians (adam.cu): b1/b2 fixed at 0.9/0.999, no bias correction."""
+    """Adam restricted to visible Gaussians (__init__.py:303-332, adam.cu): b1/b2 fixed at 0.9/0.999, no bias
+    correction.  All groups are updated by one launch (dg_adam_update_groups) instead of one adamUpdate per group;
+    `stats` (optional, see _C.adam_update_groups) folds the view's densification statistics into the same launch."""
 
     def __init__(self, params, lr, eps):
         super().__init__(params=params, lr=lr, eps=eps)
 
     @torch.no_grad()
-    def step(self, visibility, N):
+    def step(self, visibility, N, stats=None):
+        groups = []
         for group in self.param_groups:
             lr = group["lr"]
             eps = group["eps"]
@@ -191,6 +194,7 @@ class SparseGaussianAdam(torch.optim.Adam):
                 state["step"] = torch.tensor(0.0, dtype=torch.float32)
                 state["exp_avg"] = torch.zeros_like(param, memory_format=torch.preserve_format)
                 state["exp_avg_sq"] = torch.zeros_like(param, memory_format=torch.preserve_format)
-            M = param.numel() // N
             grad = param.grad if param.grad.is_contiguous() else param.grad.contiguous()
-            _C.adamUpdate(param, grad, state["exp_avg"], state["exp_avg_sq"], visibility, lr, 0.9, 0.999, eps, N, M)
+            groups.append((param, grad, state["exp_avg"], state["exp_avg_sq"], lr, eps))
+        if groups or stats is not None:
+            _C.adam_update_groups(groups, visibility, N, 0.9, 0.999, stats)

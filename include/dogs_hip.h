@@ -102,6 +102,85 @@ int dg_rasterize_filter(const dg_raster_args* a, int* radii, dg_stream_t stream)
 int dg_adam_update(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const uint8_t* visible,
                    float lr, float b1, float b2, float eps, uint32_t N, uint32_t M, dg_stream_t stream);
 
+/* ---- the optimizer side of a training view ---- */
+
+/* One parameter group of SparseGaussianAdam (diff_gaussian_rasterization/__init__.py:303-332): M floats per Gaussian. */
+typedef struct {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    float lr, eps;
+    uint32_t M;
+} dg_adam_group;
+
+/* The view's densification statistics (gaussian_trainer.py:433-438, gaussian_splat_model.py:533-541), for the
+ * Gaussians with visible[i]: max_radii2D = max(max_radii2D, radii); grad_accum += ||dmeans2D[i, :2]||; denom += 1.
+ * dmeans2D is the screen-space-point gradient [N, stride] (stride 3 for the [N,3] tensor of the reference). */
+typedef struct {
+    const int* radii;
+    const float* dmeans2D;
+    uint32_t dmeans2D_stride;
+    float* max_radii2D;
+    float* grad_accum;
+    float* denom;
+} dg_densify_stats;
+
+/* SparseGaussianAdam.step(visible, N) over up to 8 groups in one launch (each group as dg_adam_update), plus the
+ * densification statistics of the same view when stats != NULL (they read nothing Adam writes). */
+int dg_adam_update_groups(const dg_adam_group* groups, int n_groups, const uint8_t* visible, uint32_t N, float b1,
+                          float b2, const dg_densify_stats* stats, dg_stream_t stream);
+/* The statistics alone (replaces the max_radii2D update + add_densification_stats of gaussian_trainer.py:433-438). */
+int dg_add_densification_stats(const dg_densify_stats* stats, const uint8_t* visible, uint32_t N, dg_stream_t stream);
+
+/* The six optimised tensors of a GaussianSplatModel, in the order xyz [N,3], f_dc [N,1,3], f_rest [N,M,3],
+ * opacity [N,1] (raw), scaling [N,3] (raw, log), quaternion [N,4] (raw), with their Adam moments (NULL pair: the
+ * optimizer holds no state for that tensor) and the densification statistics. */
+typedef struct {
+    uint32_t N;
+    const float* params[6];
+    const float* exp_avg[6];
+    const float* exp_avg_sq[6];
+    uint32_t width[6];      /* floats per Gaussian: 3, 3, 3*M, 1, 3, 4 */
+    const float* grad_accum; /* [N] xyz_gradient_accum */
+    const float* denom;      /* [N] */
+} dg_gaussian_set;
+
+/* densify_and_prune (gaussian_splat_model.py:434-531) as GPU stream compaction, in four calls sharing this struct:
+ *   1. dg_densify_select      clone / split selection -> nc, ns (one sync);
+ *   2. dg_densify_split_stds  stds [replicas*ns, 3] = get_scaling of the split Gaussians, repeated replica-major: the
+ *                             caller draws samples = torch.normal(mean=0, std=stds) exactly as the reference does;
+ *   3. dg_densify_count       prune test over the candidate rows [originals not split | clones | children] ->
+ *                             n_out (one sync);
+ *   4. dg_densify_gather      every kept row of every tensor and its Adam moments (originals keep theirs, appended
+ *                             rows get zeros) into out_* [n_out, width].
+ * The statistics are zeros of n_out afterwards (densification_postfix); the caller allocates them. */
+typedef struct {
+    dg_gaussian_set set;
+    float max_grad;          /* densify_grad_threshold */
+    float dense_extent;      /* percent_dense * extent */
+    uint32_t replicas;       /* num_replica of densify_and_split (0 -> 2) */
+    float min_opacity;
+    int use_bbox;            /* bounding_box is not None */
+    float bbox_z;            /* bounding_box[2] */
+    int use_screen;          /* max_screen_size is not None */
+    float max_screen_size;
+    float big_extent;        /* 0.1 * extent */
+    const float* samples;    /* [replicas*ns, 3] */
+    float* out_params[6];
+    float* out_exp_avg[6];
+    float* out_exp_avg_sq[6];
+    /* filled by the library */
+    void* state;
+    void* state2;
+    uint32_t nc, ns, n_out;
+} dg_densify_args;
+enum { DG_BUF_DENSIFY = 6, DG_BUF_DENSIFY2 = 7 };
+int dg_densify_select(dg_densify_args* a, dg_alloc_fn alloc, void* user, dg_stream_t stream);
+int dg_densify_split_stds(const dg_densify_args* a, float* stds, dg_stream_t stream);
+int dg_densify_count(dg_densify_args* a, dg_alloc_fn alloc, void* user, dg_stream_t stream);
+int dg_densify_gather(const dg_densify_args* a, dg_stream_t stream);
+
 /* Replaces fusedssim (fused-ssim/ssim.cu:368-404) / fused_ssim_cuda.fusedssim: img [B,CH,H,W];
  * dm_dmu1/dm_dsigma1_sq/dm_dsigma12 NULL <=> train == false. */
 int dg_fused_ssim_forward(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,

@@ -97,3 +97,36 @@ def test_no_cpu_fallback():
         _C.rasterize_gaussians(torch.zeros(3), torch.zeros(4, 3), e, torch.ones(4, 1), torch.ones(4, 3),
                                torch.ones(4, 4), 1.0, e, torch.eye(4), torch.eye(4), 0.5, 0.4, 48, 64,
                                torch.zeros(4, 1, 3), torch.zeros(4, 15, 3), 3, torch.zeros(3), False, False, False)
+
+
+def test_ctypes_structs_match_the_header(tmp_path):
+    """sizeof/offsetof of the C structs (gcc on include/dogs_hip.h) equal the ctypes mirrors in dogs_amd/_lib.py."""
+    import shutil
+    import subprocess
+    from dogs_amd import _lib
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    checks = {
+        "dg_raster_args": (_lib.DgRasterArgs, ["P", "prefix_per_tile", "scale_modifier", "bg", "campos"]),
+        "dg_adam_group": (_lib.DgAdamGroup, ["param", "lr", "eps", "M"]),
+        "dg_densify_stats": (_lib.DgDensifyStats, ["radii", "dmeans2D_stride", "max_radii2D", "denom"]),
+        "dg_gaussian_set": (_lib.DgGaussianSet, ["N", "params", "exp_avg_sq", "width", "grad_accum", "denom"]),
+        "dg_densify_args": (_lib.DgDensifyArgs, ["set", "max_grad", "replicas", "big_extent", "samples",
+                                                 "out_params", "out_exp_avg_sq", "state", "state2", "nc", "n_out"]),
+    }
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
+    for s, (_, fields) in checks.items():
+        lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
+        for f in fields:
+            lines.append(f'printf("{s}.{f} %zu\\n", offsetof({s}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
+    got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                       check=True).stdout.split("\n") if l)
+    for s, (cls, fields) in checks.items():
+        assert int(got[s]) == C.sizeof(cls), s
+        for f in fields:
+            assert int(got[f"{s}.{f}"]) == getattr(cls, f).offset, f"{s}.{f}"
