@@ -262,7 +262,7 @@ void note_unfinished(const dg_raster_args* a, const uint32_t* counters, hipStrea
 struct BwdScratch {
     uint8_t* flag;
     float* rec;
-    uint32_t *live_idx, *live_cnt;  // compacted contributing Gaussians (k_gauss_prep -> k_gauss_live)
+    uint32_t* live_idx;  // compacted contributing Gaussians (k_gauss_prep -> k_gauss_live)
     float* live_acc;
     uint32_t* invd_flag;
     uint32_t* order;  // [T] replay order of the tiles
@@ -277,7 +277,6 @@ BwdScratch carve_bwd(void* base, int64_t K, int P, int T) {
     const size_t np = (size_t)(P > 0 ? P : 1);
     s.live_idx = c.take<uint32_t>(np);
     s.live_acc = c.take<float>(10 * np);
-    s.live_cnt = c.take<uint32_t>((np + 255) / 256);
     s.invd_flag = c.take<uint32_t>(4);
     s.order = c.take<uint32_t>((size_t)(T > 0 ? T : 1));
     s.bytes = c.off;
@@ -623,7 +622,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     q.radii = radii; q.dkey = g.dkey; q.cnt = g.rcnt; q.first_e = g.first_e; q.sp = g.sp; q.rec = sc.rec; q.flag = sc.flag;
     q.dmeans2D = dmeans2D; q.dcolors = dcolors; q.dopacity = dopacity; q.dmeans3D = dmeans3D; q.dcov3D = dcov3D;
     q.ddc = ddc; q.dsh = dsh; q.dscales = dscales; q.drot = drot; q.depth = depth;
-    q.live_idx = sc.live_idx; q.live_acc = sc.live_acc; q.live_cnt = sc.live_cnt;
+    q.live_idx = sc.live_idx; q.live_acc = sc.live_acc; q.live_total = g.counters + gs::CNT_LIVE;
     q.outputs_zeroed = zero_count != 0;
     { PROF("gauss_bwd"); gs::launch_gauss_bwd(q, s); }
     DBG_SYNC(a->debug, s);

@@ -43,6 +43,7 @@ enum {
     CNT_INVD = 9,       // backward: any(dL/dinvdepth != 0) (zeroed with the block by the forward)
     CNT_LONG = 11,      // phase-1 tiles queued for the long-list depth sort
     CNT_LONG2 = 12,     // phase-2 tiles queued for the long-list depth sort
+    CNT_LIVE = 13,      // backward: contributing Gaussians compacted by k_gauss_prep (zeroed by k_bwd_prologue)
 };
 
 // Depth histogram of the prefix cut: bins of 2^DH_SHIFT key ulps (1/64 of a binade) from the near plane up;
@@ -114,10 +115,11 @@ struct GaussBwdArgs {
     const uint8_t* flag;
     float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *ddc, *dsh, *dscales, *drot, *depth;
     int outputs_zeroed;      // the nine gradient outputs were zero-filled by k_render_bwd
-    // k_gauss_prep -> k_gauss_live: per block of 256 Gaussians, the contributing ones (slots [256 b, 256 b + cnt))
+    // k_gauss_prep -> k_gauss_live: the contributing Gaussians, compacted into one list (a block's run is allocated
+    // with one atomic: the list order varies run to run, each Gaussian's outputs do not)
     uint32_t* live_idx;      // [P]
     float* live_acc;         // [P][10] record sums
-    uint32_t* live_cnt;      // [ceil(P / 256)]
+    uint32_t* live_total;    // counters + CNT_LIVE
 };
 
 void launch_preprocess(const PreArgs& a, hipStream_t s);

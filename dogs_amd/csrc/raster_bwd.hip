@@ -293,6 +293,7 @@ __global__ void __launch_bounds__(256) BWD_WPE_ATTR k_render_bwd(RenderBwdArgs a
 __global__ void __launch_bounds__(256) k_bwd_prologue(uint32_t* __restrict__ counters, uint8_t* __restrict__ flag,
                                                       uint32_t Kcap, const float* __restrict__ dinvd, uint32_t npix) {
     const uint32_t nflags = min(counters[CNT_E1] + counters[CNT_K2], Kcap);
+    if (blockIdx.x == 0 && threadIdx.x == 0) counters[CNT_LIVE] = 0u;
     const uint32_t stride = gridDim.x * blockDim.x;
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t* f4 = reinterpret_cast<uint32_t*>(flag);  // the flag block is 256-B aligned
@@ -400,7 +401,7 @@ __device__ __forceinline__ void record_sum(const GaussBwdArgs& a, int idx, RecSu
 //               (record_sum, a wave per 64) and compacts the contributing ones -- any record sum nonzero -- into the
 //               block's slot list (index + the 10 sums).  A Gaussian without contribution has exactly zero
 //               gradients, as in the reference.
-// k_gauss_live  one wave per prep block: the per-Gaussian backward of its compacted Gaussians.
+// k_gauss_live  one lane per compacted Gaussian (grid-stride): its per-Gaussian backward.
 __device__ __forceinline__ void zero_slice(float* out, size_t first, size_t count) {
     float* p = out + first;
     size_t i = threadIdx.x;
@@ -446,7 +447,8 @@ __global__ void __launch_bounds__(256) k_gauss_prep(GaussBwdArgs a) {
         for (int v = 0; v < 10; v++) live |= acc[v] != 0.0f;
         live = live && rad > 0;
     }
-    // block-local compaction of the contributing Gaussians, in index order
+    // compaction of the contributing Gaussians: one atomic per block allocates the block's run of the global list
+    __shared__ uint32_t s_base;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t lm = __ballot(live);
     if (lane == 0) s_wcnt[w] = (uint32_t)__popcll(lm);
@@ -454,23 +456,24 @@ __global__ void __launch_bounds__(256) k_gauss_prep(GaussBwdArgs a) {
     uint32_t off = 0, tot = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) { if (q < w) off += s_wcnt[q]; tot += s_wcnt[q]; }
+    if (threadIdx.x == 0) s_base = tot ? atomicAdd(a.live_total, tot) : 0u;
+    __syncthreads();
     if (live) {
-        const uint32_t j = (uint32_t)base + off + (uint32_t)__popcll(lm & (lane ? (~0ull >> (64 - lane)) : 0ull));
+        const uint32_t j = s_base + off + (uint32_t)__popcll(lm & (lane ? (~0ull >> (64 - lane)) : 0ull));
         a.live_idx[j] = (uint32_t)idx;
 #pragma unroll
         for (int v = 0; v < 10; v++) a.live_acc[(size_t)j * 10 + v] = acc[v];
     }
-    if (threadIdx.x == 0) a.live_cnt[blockIdx.x] = tot;
 }
 
-__global__ void __launch_bounds__(64) k_gauss_live(GaussBwdArgs a) {
-    const uint32_t n = a.live_cnt[blockIdx.x];
-    const uint32_t base = blockIdx.x * 256u;
-    for (uint32_t j = threadIdx.x; j < n; j += 64) {
-        const uint32_t idx = a.live_idx[base + j];
+// grid-stride over the compacted list (its length is device-side): one lane per contributing Gaussian
+__global__ void __launch_bounds__(256) k_gauss_live(GaussBwdArgs a) {
+    const uint32_t n = *a.live_total;
+    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < n; j += gridDim.x * 256u) {
+        const uint32_t idx = a.live_idx[j];
         float acc[10];
 #pragma unroll
-        for (int v = 0; v < 10; v++) acc[v] = a.live_acc[(size_t)(base + j) * 10 + v];
+        for (int v = 0; v < 10; v++) acc[v] = a.live_acc[(size_t)j * 10 + v];
         gauss_bwd_one(a, (int)idx, acc);
     }
 }
@@ -732,7 +735,7 @@ void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
     const int blocks = (a.P + 255) / 256;
     k_gauss_prep<<<blocks, 256, 0, s>>>(a);
-    k_gauss_live<<<blocks, 64, 0, s>>>(a);
+    k_gauss_live<<<blocks < 2048 ? blocks : 2048, 256, 0, s>>>(a);
 }
 
 }  // namespace gs
