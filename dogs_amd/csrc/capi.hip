@@ -262,7 +262,7 @@ void note_unfinished(const dg_raster_args* a, const uint32_t* counters, hipStrea
 struct BwdScratch {
     uint8_t* flag;
     float* rec;
-    uint32_t* live_idx;  // compacted contributing Gaussians (k_gauss_prep -> k_gauss_live)
+    uint32_t *live_idx, *live_cnt;  // compacted contributing Gaussians (k_gauss_prep -> k_gauss_live)
     float* live_acc;
     uint32_t* invd_flag;
     uint32_t* order;  // [T] replay order of the tiles
@@ -277,6 +277,7 @@ BwdScratch carve_bwd(void* base, int64_t K, int P, int T) {
     const size_t np = (size_t)(P > 0 ? P : 1);
     s.live_idx = c.take<uint32_t>(np);
     s.live_acc = c.take<float>(10 * np);
+    s.live_cnt = c.take<uint32_t>((np + 255) / 256);
     s.invd_flag = c.take<uint32_t>(4);
     s.order = c.take<uint32_t>((size_t)(T > 0 ? T : 1));
     s.bytes = c.off;
@@ -413,7 +414,9 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     fill_pre(pre, a);
     pre.radii = radii; pre.sp = g.sp; pre.depthkey = g.dkey; pre.cnt = g.cnt; pre.rcnt = g.rcnt;
     pre.hist = g.hist;
-    pre.rect_sum = (unsigned long long*)(g.counters + gs::CNT_RECT_LO); pre.err = g.counters + gs::CNT_ERR;
+    // per-block rect sums land in the wave-total array (ceil(P/64) u32 >= ceil(P/256) u64), free until the binning
+    pre.rect_part = reinterpret_cast<unsigned long long*>(g.wtot); pre.err = g.counters + gs::CNT_ERR;
+    const uint32_t nparts = (uint32_t)((P + 255) / 256);
     { PROF("preprocess"); gs::launch_preprocess(pre, s); }
     DBG_SYNC(a->debug, s);
 
@@ -425,9 +428,11 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
         gs::launch_depth_hist(P, g.dkey, g.cnt, g.hist, s);
         if (prefix_enabled(a)) {
             C1 = phase1_cap(a, T);
-            gs::launch_depth_cut(g.hist, (uint32_t)C1, g.counters, im.tile_cnt, im.tile_cnt2, (uint32_t)T, s);
+            gs::launch_depth_cut(g.hist, (uint32_t)C1, g.counters, im.tile_cnt, im.tile_cnt2, (uint32_t)T,
+                                 pre.rect_part, nparts, s);
         } else {  // everything in one phase: the capacity is the total rect area itself (one early sync)
-            gs::launch_depth_cut(g.hist, 0xffffffffu, g.counters, im.tile_cnt, im.tile_cnt2, (uint32_t)T, s);
+            gs::launch_depth_cut(g.hist, 0xffffffffu, g.counters, im.tile_cnt, im.tile_cnt2, (uint32_t)T,
+                                 pre.rect_part, nparts, s);
             uint32_t k = 0;
             HIP_OK(hipMemcpyAsync(&k, g.counters + gs::CNT_K, 4, hipMemcpyDeviceToHost, s));
             HIP_OK(hipStreamSynchronize(s));
@@ -622,7 +627,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     q.radii = radii; q.dkey = g.dkey; q.cnt = g.rcnt; q.first_e = g.first_e; q.sp = g.sp; q.rec = sc.rec; q.flag = sc.flag;
     q.dmeans2D = dmeans2D; q.dcolors = dcolors; q.dopacity = dopacity; q.dmeans3D = dmeans3D; q.dcov3D = dcov3D;
     q.ddc = ddc; q.dsh = dsh; q.dscales = dscales; q.drot = drot; q.depth = depth;
-    q.live_idx = sc.live_idx; q.live_acc = sc.live_acc; q.live_total = g.counters + gs::CNT_LIVE;
+    q.live_idx = sc.live_idx; q.live_acc = sc.live_acc; q.live_cnt = sc.live_cnt;
     q.outputs_zeroed = zero_count != 0;
     { PROF("gauss_bwd"); gs::launch_gauss_bwd(q, s); }
     DBG_SYNC(a->debug, s);

@@ -26,7 +26,7 @@ struct PreArgs {
     uint32_t* hist;     // [DH_BINS] depth histogram, zeroed here
     uint32_t* cnt;      // tile-rect area (0 when culled)
     uint32_t* rcnt;     // records per Gaussian, zeroed here (written by the emission kernels)
-    unsigned long long* rect_sum;  // num_rendered of the reference (sum of rect areas)
+    unsigned long long* rect_part;  // [blocks] per-block sums of rect areas (k_depth_cut totals them: num_rendered)
     uint32_t* err;
 };
 
@@ -43,7 +43,6 @@ enum {
     CNT_INVD = 9,       // backward: any(dL/dinvdepth != 0) (zeroed with the block by the forward)
     CNT_LONG = 11,      // phase-1 tiles queued for the long-list depth sort
     CNT_LONG2 = 12,     // phase-2 tiles queued for the long-list depth sort
-    CNT_LIVE = 13,      // backward: contributing Gaussians compacted by k_gauss_prep (zeroed by k_bwd_prologue)
 };
 
 // Depth histogram of the prefix cut: bins of 2^DH_SHIFT key ulps (1/64 of a binade) from the near plane up;
@@ -115,11 +114,10 @@ struct GaussBwdArgs {
     const uint8_t* flag;
     float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *ddc, *dsh, *dscales, *drot, *depth;
     int outputs_zeroed;      // the nine gradient outputs were zero-filled by k_render_bwd
-    // k_gauss_prep -> k_gauss_live: the contributing Gaussians, compacted into one list (a block's run is allocated
-    // with one atomic: the list order varies run to run, each Gaussian's outputs do not)
+    // k_gauss_prep -> k_gauss_live: per block of 256 Gaussians, the contributing ones (slots [256 b, 256 b + cnt))
     uint32_t* live_idx;      // [P]
     float* live_acc;         // [P][10] record sums
-    uint32_t* live_total;    // counters + CNT_LIVE
+    uint32_t* live_cnt;      // [ceil(P / 256)]
 };
 
 void launch_preprocess(const PreArgs& a, hipStream_t s);
@@ -127,8 +125,10 @@ void launch_preprocess(const PreArgs& a, hipStream_t s);
 void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_t* hist, hipStream_t s);
 // counters[K, THR, E1, CUT] from the histogram (phase-1 capacity cap); resets the per-view counters and zeroes
 // the per-tile counters of both binning phases (tile_cnt, tile_cnt2 [num_tiles])
+// It also totals the preprocess's per-block rect-area sums into counters[CNT_RECT_LO..+1] (num_rendered): one
+// atomic per block on a single address costs ~10 us per 1e6 Gaussians (cross-XCD serialization).
 void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, uint32_t* tile_cnt, uint32_t* tile_cnt2,
-                      uint32_t num_tiles, hipStream_t s);
+                      uint32_t num_tiles, const unsigned long long* rect_part, uint32_t nparts, hipStream_t s);
 // Binning walk of one phase (phase 1: Gaussians with key < counters[CNT_THR]; phase 2: those past it, only instances
 // in tiles phase 1 left unfinished): k_bin_count (precise cull walk -> rcnt, per-wave totals, per-tile counts),
 // exclusive scan of the wave totals (*total = the phase's instance count), per-tile ranges, k_bin_emit (first_e;

@@ -293,16 +293,16 @@ __global__ void __launch_bounds__(256) BWD_WPE_ATTR k_render_bwd(RenderBwdArgs a
 __global__ void __launch_bounds__(256) k_bwd_prologue(uint32_t* __restrict__ counters, uint8_t* __restrict__ flag,
                                                       uint32_t Kcap, const float* __restrict__ dinvd, uint32_t npix) {
     const uint32_t nflags = min(counters[CNT_E1] + counters[CNT_K2], Kcap);
-    if (blockIdx.x == 0 && threadIdx.x == 0) counters[CNT_LIVE] = 0u;
     const uint32_t stride = gridDim.x * blockDim.x;
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t* f4 = reinterpret_cast<uint32_t*>(flag);  // the flag block is 256-B aligned
     for (uint32_t i = i0; i < nflags / 4; i += stride) f4[i] = 0u;
     for (uint32_t i = (nflags & ~3u) + i0; i < nflags; i += stride) flag[i] = 0;
-    if (dinvd) {
+    if (dinvd) {  // one atomic per block at most, skipped once the flag is set (single-address atomics serialize)
         bool nz = false;
         for (uint32_t i = i0; i < npix; i += stride) nz |= (dinvd[i] != 0.0f);
-        if (__any(nz) && (threadIdx.x & 63) == 0) atomicOr(counters + CNT_INVD, 1u);
+        if (__syncthreads_or(nz) && threadIdx.x == 0 && !static_cast<volatile uint32_t*>(counters)[CNT_INVD])
+            atomicOr(counters + CNT_INVD, 1u);
     }
 }
 
@@ -401,7 +401,7 @@ __device__ __forceinline__ void record_sum(const GaussBwdArgs& a, int idx, RecSu
 //               (record_sum, a wave per 64) and compacts the contributing ones -- any record sum nonzero -- into the
 //               block's slot list (index + the 10 sums).  A Gaussian without contribution has exactly zero
 //               gradients, as in the reference.
-// k_gauss_live  one lane per compacted Gaussian (grid-stride): its per-Gaussian backward.
+// k_gauss_live  one block per 4 prep blocks, one lane per compacted Gaussian: its per-Gaussian backward.
 __device__ __forceinline__ void zero_slice(float* out, size_t first, size_t count) {
     float* p = out + first;
     size_t i = threadIdx.x;
@@ -447,8 +447,8 @@ __global__ void __launch_bounds__(256) k_gauss_prep(GaussBwdArgs a) {
         for (int v = 0; v < 10; v++) live |= acc[v] != 0.0f;
         live = live && rad > 0;
     }
-    // compaction of the contributing Gaussians: one atomic per block allocates the block's run of the global list
-    __shared__ uint32_t s_base;
+    // block-local compaction of the contributing Gaussians, in index order (no atomics: one per block on a single
+    // address serializes across the XCDs)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t lm = __ballot(live);
     if (lane == 0) s_wcnt[w] = (uint32_t)__popcll(lm);
@@ -456,24 +456,33 @@ __global__ void __launch_bounds__(256) k_gauss_prep(GaussBwdArgs a) {
     uint32_t off = 0, tot = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) { if (q < w) off += s_wcnt[q]; tot += s_wcnt[q]; }
-    if (threadIdx.x == 0) s_base = tot ? atomicAdd(a.live_total, tot) : 0u;
-    __syncthreads();
     if (live) {
-        const uint32_t j = s_base + off + (uint32_t)__popcll(lm & (lane ? (~0ull >> (64 - lane)) : 0ull));
+        const uint32_t j = (uint32_t)base + off + (uint32_t)__popcll(lm & (lane ? (~0ull >> (64 - lane)) : 0ull));
         a.live_idx[j] = (uint32_t)idx;
 #pragma unroll
         for (int v = 0; v < 10; v++) a.live_acc[(size_t)j * 10 + v] = acc[v];
     }
+    if (threadIdx.x == 0) a.live_cnt[blockIdx.x] = tot;
 }
 
-// grid-stride over the compacted list (its length is device-side): one lane per contributing Gaussian
-__global__ void __launch_bounds__(256) k_gauss_live(GaussBwdArgs a) {
-    const uint32_t n = *a.live_total;
-    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < n; j += gridDim.x * 256u) {
-        const uint32_t idx = a.live_idx[j];
+// one block per LIVE_GROUP prep blocks (~25% of Gaussians contribute: about one Gaussian per lane), one lane per
+// compacted Gaussian of their lists
+constexpr int LIVE_GROUP = 4;
+__global__ void __launch_bounds__(256) k_gauss_live(GaussBwdArgs a, uint32_t nblocks) {
+    const uint32_t b0 = blockIdx.x * LIVE_GROUP;
+    uint32_t pre[LIVE_GROUP + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int k = 0; k < LIVE_GROUP; k++) pre[k + 1] = pre[k] + (b0 + k < nblocks ? a.live_cnt[b0 + k] : 0u);
+    for (uint32_t j = threadIdx.x; j < pre[LIVE_GROUP]; j += 256) {
+        uint32_t slot = 0;
+#pragma unroll
+        for (int k = 0; k < LIVE_GROUP; k++)
+            if (j >= pre[k] && j < pre[k + 1]) slot = (b0 + k) * 256u + (j - pre[k]);
+        const uint32_t idx = a.live_idx[slot];
         float acc[10];
 #pragma unroll
-        for (int v = 0; v < 10; v++) acc[v] = a.live_acc[(size_t)j * 10 + v];
+        for (int v = 0; v < 10; v++) acc[v] = a.live_acc[(size_t)slot * 10 + v];
         gauss_bwd_one(a, (int)idx, acc);
     }
 }
@@ -735,7 +744,7 @@ void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
     const int blocks = (a.P + 255) / 256;
     k_gauss_prep<<<blocks, 256, 0, s>>>(a);
-    k_gauss_live<<<blocks < 2048 ? blocks : 2048, 256, 0, s>>>(a);
+    k_gauss_live<<<(blocks + LIVE_GROUP - 1) / LIVE_GROUP, 256, 0, s>>>(a, (uint32_t)blocks);
 }
 
 }  // namespace gs

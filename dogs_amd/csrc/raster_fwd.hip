@@ -227,10 +227,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = v;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned long long s = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
-        if (s) atomicAdd(a.rect_sum, s);
-    }
+    if (threadIdx.x == 0) a.rect_part[blockIdx.x] = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -278,11 +275,21 @@ __global__ void __launch_bounds__(DH_THREADS) k_depth_hist(int P, const uint32_t
 // counters and the per-tile counters of both binning phases.
 __global__ void __launch_bounds__(1024) k_depth_cut(const uint32_t* __restrict__ hist, uint32_t cap,
                                                     uint32_t* __restrict__ counters, uint32_t* __restrict__ tile_cnt,
-                                                    uint32_t* __restrict__ tile_cnt2, uint32_t num_tiles) {
+                                                    uint32_t* __restrict__ tile_cnt2, uint32_t num_tiles,
+                                                    const unsigned long long* __restrict__ rect_part,
+                                                    uint32_t nparts) {
     __shared__ uint32_t s_w[16];
     __shared__ int s_best;
+    __shared__ unsigned long long s_rect[16];
     constexpr int PER = DH_BINS / 1024;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    {  // num_rendered = sum of the preprocess's per-block rect areas
+        unsigned long long r = 0;
+        for (uint32_t i = t; i < nparts; i += 1024) r += rect_part[i];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
+        if (lane == 0) s_rect[w] = r;
+    }
     for (uint32_t i = t; i < num_tiles; i += 1024) { tile_cnt[i] = 0u; tile_cnt2[i] = 0u; }
     if (t == 0) s_best = -1;
     uint32_t v[PER], loc = 0;
@@ -309,6 +316,13 @@ __global__ void __launch_bounds__(1024) k_depth_cut(const uint32_t* __restrict__
     }
     if (best >= 0) atomicMax(&s_best, best);
     __syncthreads();
+    if (t == 0) {
+        unsigned long long r = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) r += s_rect[k];
+        counters[CNT_RECT_LO] = (uint32_t)r;
+        counters[CNT_RECT_LO + 1] = (uint32_t)(r >> 32);
+    }
     const bool cut = K > cap;
     if (t == 0 && s_best < 0) {  // not even bin 0 fits: phase 1 bins nothing, phase 2 everything
         counters[CNT_K] = K;
@@ -750,8 +764,8 @@ void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_
     if (P > 0) k_depth_hist<<<(P + per - 1) / per, DH_THREADS, 0, s>>>(P, dkey, cnt, hist);
 }
 void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, uint32_t* tile_cnt, uint32_t* tile_cnt2,
-                      uint32_t num_tiles, hipStream_t s) {
-    k_depth_cut<<<1, 1024, 0, s>>>(hist, cap, counters, tile_cnt, tile_cnt2, num_tiles);
+                      uint32_t num_tiles, const unsigned long long* rect_part, uint32_t nparts, hipStream_t s) {
+    k_depth_cut<<<1, 1024, 0, s>>>(hist, cap, counters, tile_cnt, tile_cnt2, num_tiles, rect_part, nparts);
 }
 void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s) {
     if (a.P <= 0) return;
