@@ -246,11 +246,8 @@ __device__ __forceinline__ uint32_t replay_len(const RenderBwdArgs& a, int tile)
     return n < mc ? n : mc;
 }
 
-// Longest-first launch order for the replay (tile_order_sort); the key is the exact replay length.  Per tile,
-// not per 4-tile block: ordering whole blocks by their longest tile measured 6% slower.
-__global__ void __launch_bounds__(1024) k_tile_order(RenderBwdArgs a) {
-    tile_order_sort(a.num_tiles, a.order, [&](int tile) { return replay_len(a, tile); });
-}
+// Longest-first launch order for the replay (tile_order_sort in k_bwd_prologue); the key is the exact replay
+// length.  Per tile, not per 4-tile block: ordering whole blocks by their longest tile measured 6% slower.
 
 #ifdef DG_BWD_WPE  // occupancy experiment: cap VGPRs so that DG_BWD_WPE waves fit per SIMD
 #define BWD_WPE_ATTR __attribute__((amdgpu_waves_per_eu(DG_BWD_WPE)))
@@ -288,19 +285,27 @@ __global__ void __launch_bounds__(256) BWD_WPE_ATTR k_render_bwd(RenderBwdArgs a
     }
 }
 
-// Backward prologue, one launch: zero the record flags of the E1 + K2 binned instances (device-side count) and
-// set counters[CNT_INVD] = any(dL/dinvdepth != 0), which lets the replay drop the inverse-depth terms.
-__global__ void __launch_bounds__(256) k_bwd_prologue(uint32_t* __restrict__ counters, uint8_t* __restrict__ flag,
-                                                      uint32_t Kcap, const float* __restrict__ dinvd, uint32_t npix) {
-    const uint32_t nflags = min(counters[CNT_E1] + counters[CNT_K2], Kcap);
-    const uint32_t stride = gridDim.x * blockDim.x;
+// Backward prologue, one launch: blocks [0, PRO_BLOCKS) zero the record flags of the E1 + K2 binned instances
+// (device-side count) and set counters[CNT_INVD] = any(dL/dinvdepth != 0), which lets the replay drop the
+// inverse-depth terms; the extra last block (when tile ordering is on) computes the longest-first replay order
+// (tile_order_sort) concurrently, instead of a one-block launch of its own on the critical path.
+constexpr uint32_t PRO_BLOCKS = 128;
+__global__ void __launch_bounds__(1024) k_bwd_prologue(RenderBwdArgs a, uint32_t* __restrict__ counters) {
+    if (blockIdx.x == PRO_BLOCKS) {
+        tile_order_sort(a.num_tiles, a.order, [&](int tile) { return replay_len(a, tile); });
+        return;
+    }
+    uint8_t* flag = a.flag;
+    const uint32_t nflags = min(counters[CNT_E1] + counters[CNT_K2], a.K);
+    const uint32_t stride = PRO_BLOCKS * blockDim.x;
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t* f4 = reinterpret_cast<uint32_t*>(flag);  // the flag block is 256-B aligned
     for (uint32_t i = i0; i < nflags / 4; i += stride) f4[i] = 0u;
     for (uint32_t i = (nflags & ~3u) + i0; i < nflags; i += stride) flag[i] = 0;
-    if (dinvd) {  // one atomic per block at most, skipped once the flag is set (single-address atomics serialize)
+    if (a.dL_dinvd) {  // one atomic per block at most, skipped once the flag is set (single-address atomics serialize)
+        const uint32_t npix = (uint32_t)a.W * a.H;
         bool nz = false;
-        for (uint32_t i = i0; i < npix; i += stride) nz |= (dinvd[i] != 0.0f);
+        for (uint32_t i = i0; i < npix; i += stride) nz |= (a.dL_dinvd[i] != 0.0f);
         if (__syncthreads_or(nz) && threadIdx.x == 0 && !static_cast<volatile uint32_t*>(counters)[CNT_INVD])
             atomicOr(counters + CNT_INVD, 1u);
     }
@@ -734,11 +739,9 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, co
 }
 
 void launch_render_bwd(const RenderBwdArgs& a, uint32_t* counters, hipStream_t s) {
-    k_bwd_prologue<<<512, 256, 0, s>>>(counters, a.flag, a.K, a.dL_dinvd, (uint32_t)a.W * a.H);
-    if (a.num_tiles > 0) {
-        if (a.order) k_tile_order<<<1, 1024, 0, s>>>(a);
-        k_render_bwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
-    }
+    const bool order = a.order && a.num_tiles > 0;
+    k_bwd_prologue<<<PRO_BLOCKS + (order ? 1 : 0), 1024, 0, s>>>(a, counters);
+    if (a.num_tiles > 0) k_render_bwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
 }
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
