@@ -64,7 +64,7 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count"
            "dg_debug_geometry", "dg_debug_image_state", "dg_sort_pairs_u32", "dg_exclusive_scan_u32",
            "dg_profile_enable", "dg_profile_collect", "dg_binned_instances", "dg_adam_update_groups",
            "dg_add_densification_stats", "dg_densify_select", "dg_densify_split_stds", "dg_densify_count",
-           "dg_densify_gather",
+           "dg_densify_gather", "dg_splat_pack", "dg_ply_pack",
            "dg_last_error", "dg_version")
 
 _lib = None
@@ -145,6 +145,11 @@ def load(path: str | None = None):
             L.dg_densify_count.argtypes = [dp, ALLOC_FN, vp, vp]
             L.dg_densify_gather.restype = C.c_int
             L.dg_densify_gather.argtypes = [dp, vp]
+        if hasattr(L, "dg_splat_pack"):
+            L.dg_splat_pack.restype = C.c_int
+            L.dg_splat_pack.argtypes = [C.c_uint32, vp, vp, vp, vp, vp, vp, ALLOC_FN, vp, vp]
+            L.dg_ply_pack.restype = C.c_int
+            L.dg_ply_pack.argtypes = [C.c_uint32, vp, vp, vp, vp]
         L.dg_last_error.restype = C.c_char_p
         L.dg_last_error.argtypes = []
         L.dg_version.restype = C.c_int

@@ -12,6 +12,7 @@
 #include "../../include/dogs_hip.h"
 #include "aux_kernels.h"
 #include "optim.h"
+#include "export.h"
 #include "raster.h"
 #include "sortscan.h"
 
@@ -866,6 +867,37 @@ int dg_densify_gather(const dg_densify_args* a, dg_stream_t stream) {
     KeepState ks = carve_keep(a->state2, C);
     gs::RebuildArgs rb = rebuild_args(a, st, ks);
     gs::launch_densify_gather(rb, ks.keep_pos, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_splat_pack(uint32_t N, const float* xyz, const float* scaling, const float* opacity, const float* rotation,
+                  const float* f_dc, uint8_t* out, dg_alloc_fn alloc, void* user, dg_stream_t stream) {
+    if (N == 0) return 0;
+    if (!xyz || !scaling || !opacity || !rotation || !f_dc || !out) return fail("splat pack: NULL tensor%s%d");
+    hipStream_t s = (hipStream_t)stream;
+    Carver c(nullptr);
+    c.take<uint32_t>(N); c.take<uint32_t>(N); c.take<uint32_t>(N); c.take<uint32_t>(N);
+    c.take<char>(gs::radix_sort_temp_bytes(N));
+    void* base = alloc(user, DG_BUF_TEMP, c.off);
+    if (!base) return fail("splat pack scratch allocation failed%s%d");
+    Carver d(base);
+    uint32_t* k0 = d.take<uint32_t>(N);
+    uint32_t* v0 = d.take<uint32_t>(N);
+    uint32_t* k1 = d.take<uint32_t>(N);
+    uint32_t* v1 = d.take<uint32_t>(N);
+    void* tmp = d.take<char>(gs::radix_sort_temp_bytes(N));
+    gs::launch_splat_keys(N, scaling, opacity, k0, v0, s);
+    const int which = gs::radix_sort_pairs(k0, v0, k1, v1, nullptr, N, 0, 32, tmp, s);  // stable: ties by index
+    gs::launch_splat_pack(N, which ? v1 : v0, xyz, scaling, opacity, rotation, f_dc, out, s);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_ply_pack(uint32_t N, const float* xyz, const float* f_dc, uint8_t* out, dg_stream_t stream) {
+    if (N == 0) return 0;
+    if (!xyz || !f_dc || !out) return fail("ply pack: NULL tensor%s%d");
+    gs::launch_ply_pack(N, xyz, f_dc, out, (hipStream_t)stream);
     HIP_OK(hipGetLastError());
     return 0;
 }

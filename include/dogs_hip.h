@@ -181,6 +181,18 @@ int dg_densify_split_stds(const dg_densify_args* a, float* stds, dg_stream_t str
 int dg_densify_count(dg_densify_args* a, dg_alloc_fn alloc, void* user, dg_stream_t stream);
 int dg_densify_gather(const dg_densify_args* a, dg_stream_t stream);
 
+/* ---- export formats of the trained / fused Gaussians ---- */
+
+/* GaussianSplatModel.save_splat (gaussian_splat_model.py:666-708): out [N * 32] device bytes, the .splat records
+ * (position f32x3, exp(scale) f32x3, RGBA u8x4, normalised quaternion u8x4) in ascending order of
+ * -exp(s0 + s1 + s2) / (1 + exp(opacity)) (stable: equal keys keep index order).  Raw (pre-activation) tensors:
+ * xyz [N,3], scaling [N,3], opacity [N,1], rotation [N,4], f_dc [N,1,3].  Allocates DG_BUF_TEMP. */
+int dg_splat_pack(uint32_t N, const float* xyz, const float* scaling, const float* opacity, const float* rotation,
+                  const float* f_dc, uint8_t* out, dg_alloc_fn alloc, void* user, dg_stream_t stream);
+/* GaussianSplatModel.save_ply (gaussian_splat_model.py:616-640): out [N * 27] device bytes, the binary vertex
+ * records (x y z f32, nx ny nz = 0, red green blue u8 = the degree-0 SH colour x 255). */
+int dg_ply_pack(uint32_t N, const float* xyz, const float* f_dc, uint8_t* out, dg_stream_t stream);
+
 /* Replaces fusedssim (fused-ssim/ssim.cu:368-404) / fused_ssim_cuda.fusedssim: img [B,CH,H,W];
  * dm_dmu1/dm_dsigma1_sq/dm_dsigma12 NULL <=> train == false. */
 int dg_fused_ssim_forward(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,
