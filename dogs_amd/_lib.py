@@ -64,7 +64,8 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count"
            "dg_debug_geometry", "dg_debug_image_state", "dg_sort_pairs_u32", "dg_exclusive_scan_u32",
            "dg_profile_enable", "dg_profile_collect", "dg_binned_instances", "dg_adam_update_groups",
            "dg_add_densification_stats", "dg_densify_select", "dg_densify_split_stds", "dg_densify_count",
-           "dg_densify_gather", "dg_splat_pack", "dg_ply_pack",
+           "dg_densify_gather", "dg_splat_pack", "dg_ply_pack", "dg_ring_create", "dg_ring_submit", "dg_ring_next",
+           "dg_ring_upload", "dg_ring_pending", "dg_ring_destroy", "dg_image_u8_to_chw",
            "dg_last_error", "dg_version")
 
 _lib = None
@@ -150,6 +151,22 @@ def load(path: str | None = None):
             L.dg_splat_pack.argtypes = [C.c_uint32, vp, vp, vp, vp, vp, vp, ALLOC_FN, vp, vp]
             L.dg_ply_pack.restype = C.c_int
             L.dg_ply_pack.argtypes = [C.c_uint32, vp, vp, vp, vp]
+        if hasattr(L, "dg_ring_create"):
+            ip = C.POINTER(C.c_int)
+            L.dg_ring_create.restype = vp
+            L.dg_ring_create.argtypes = [C.c_int, C.c_uint64, C.c_int]
+            L.dg_ring_submit.restype = C.c_int
+            L.dg_ring_submit.argtypes = [vp, C.c_char_p, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int]
+            L.dg_ring_next.restype = C.c_int
+            L.dg_ring_next.argtypes = [vp, ip, ip, ip, ip, ip]
+            L.dg_ring_upload.restype = C.c_int
+            L.dg_ring_upload.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp]
+            L.dg_ring_pending.restype = C.c_int
+            L.dg_ring_pending.argtypes = [vp]
+            L.dg_ring_destroy.restype = None
+            L.dg_ring_destroy.argtypes = [vp]
+            L.dg_image_u8_to_chw.restype = C.c_int
+            L.dg_image_u8_to_chw.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp]
         L.dg_last_error.restype = C.c_char_p
         L.dg_last_error.argtypes = []
         L.dg_version.restype = C.c_int

@@ -193,6 +193,28 @@ int dg_splat_pack(uint32_t N, const float* xyz, const float* scaling, const floa
  * records (x y z f32, nx ny nz = 0, red green blue u8 = the degree-0 SH colour x 255). */
 int dg_ply_pack(uint32_t N, const float* xyz, const float* f_dc, uint8_t* out, dg_stream_t stream);
 
+/* ---- the training image path (ImageReader, conerf/base/task_queue.py:89-152) ---- */
+
+/* A ring of `slots` pinned host buffers (max_bytes each) filled by `threads` reader threads with raw u8 HWC images
+ * (a decoded cache, e.g. the data section of a .npy file at `offset`).  Completion order, like the reference's
+ * image queue.  NULL on failure. */
+typedef struct dg_image_ring dg_image_ring;
+dg_image_ring* dg_ring_create(int slots, uint64_t max_bytes, int threads);
+/* Queue one image: h x w x c bytes (c = 1, 3 or 4) read from `path` at `offset`, tagged `index`. */
+int dg_ring_submit(dg_image_ring* ring, const char* path, uint64_t offset, int index, int h, int w, int c);
+/* Block until an image is ready: its tag, shape and slot (return 3: the read failed, the slot is released). */
+int dg_ring_next(dg_image_ring* ring, int* index, int* h, int* w, int* c, int* slot);
+/* Copy the slot's bytes to dev_staging [h*w*c] on `stream` and convert them into out_chw [c', h, w] float
+ * (read_image: x / 255; with rgba_composite (its num_channels == 4) an RGBA image is composited over black ->
+ * c' = 3, else c' = c).  The slot is reused once the copy completed. */
+int dg_ring_upload(dg_image_ring* ring, int slot, int h, int w, int c, int rgba_composite, uint8_t* dev_staging,
+                   float* out_chw, dg_stream_t stream);
+int dg_ring_pending(dg_image_ring* ring);   /* submitted images not yet taken by dg_ring_next */
+void dg_ring_destroy(dg_image_ring* ring);
+/* The conversion alone, device to device. */
+int dg_image_u8_to_chw(const uint8_t* dev_hwc, int h, int w, int c, int rgba_composite, float* out_chw,
+                       dg_stream_t stream);
+
 /* Replaces fusedssim (fused-ssim/ssim.cu:368-404) / fused_ssim_cuda.fusedssim: img [B,CH,H,W];
  * dm_dmu1/dm_dsigma1_sq/dm_dsigma12 NULL <=> train == false. */
 int dg_fused_ssim_forward(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,
