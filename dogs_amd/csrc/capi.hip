@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 #include <map>
+#include <tuple>
 
 #include "../../include/dogs_hip.h"
 #include "aux_kernels.h"
@@ -217,47 +218,38 @@ int64_t clamp_cap(int64_t per, int T) {
     return c < 1 ? 1 : (c > 0xffffff00ll ? 0xffffff00ll : c);
 }
 
-// Adaptive phase-1 capacity (prefix_per_tile == 0).  Phase 2 costs 100-400 us whenever it runs (a full walk of the
-// Gaussians past the threshold), so a scene whose views keep leaving tiles unfinished wants a deeper prefix.  Per
-// image size on this thread: after each view the unfinished-tile count lands in pinned memory behind an event; the
-// next forward of that size reads it without waiting (hipEventQuery) and grows the per-tile capacity x1.5 when any
-// tile needed phase 2 (its cost is mostly per view, not per tile: the walk over the Gaussians past the threshold and
-// the block sort of the few, very long, phase-2 lists).  Grow-only: a capacity that was once needed stays, and a
-// too-deep prefix costs only proportionally more phase-1 work.  The capacity a view used travels to its backward as
-// the num_instances token, so later growth never desynchronises a forward/backward pair.
+// Adaptive phase-1 capacity (prefix_per_tile == 0).  Phase 2 costs 100-400 us whenever it runs, almost independently
+// of how many tiles need it (a walk over every Gaussian past the threshold, and the block sort of the few, very long,
+// phase-2 lists), so a scene whose views keep leaving tiles unfinished wants a deeper prefix.  Per device and image
+// size on this thread: the phase-2 launch leaves its unfinished-tile count in a device probe (k_sat_rows), the next
+// forward's k_depth_cut moves it into counters[CNT_PREV_UNF] (cleared after reading), the host sees it in the
+// counter copy it makes anyway, and the capacity grows x1.5 (up to MAX_PREFIX_PER_TILE) when it is nonzero -- no
+// extra copy, event or wait.  Grow-only: a capacity that was once needed stays, and a too-deep prefix costs only
+// proportionally more phase-1 work.  The capacity a view used travels to its backward as the num_instances token, so
+// later growth never desynchronises a forward/backward pair.
 struct AdaptiveCap {
     int per_tile = DEFAULT_PREFIX_PER_TILE;
-    uint32_t* unfinished = nullptr;  // pinned landing slot
-    hipEvent_t ev = nullptr;
-    bool pending = false;
+    uint32_t* probe = nullptr;  // device
 };
-AdaptiveCap& adaptive_cap(int W, int H) {
-    thread_local std::map<std::pair<int, int>, AdaptiveCap> caps;
-    AdaptiveCap& c = caps[{W, H}];
-    if (!c.unfinished) {
-        (void)hipHostMalloc((void**)&c.unfinished, 64, hipHostMallocDefault);
-        (void)hipEventCreateWithFlags(&c.ev, hipEventDisableTiming);
+AdaptiveCap* adaptive_cap(const dg_raster_args* a) {
+    if (a->prefix_per_tile != 0) return nullptr;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    thread_local std::map<std::tuple<int, int, int>, AdaptiveCap> caps;
+    AdaptiveCap& c = caps[std::make_tuple(dev, a->W, a->H)];
+    if (!c.probe) {
+        if (hipMalloc((void**)&c.probe, sizeof(uint32_t)) != hipSuccess) { c.probe = nullptr; return nullptr; }
+        (void)hipMemset(c.probe, 0, sizeof(uint32_t));
     }
-    return c;
+    return &c;
 }
-int64_t phase1_cap(const dg_raster_args* a, int T) {
+int64_t phase1_cap(const dg_raster_args* a, int T, AdaptiveCap* ac) {
     if (a->prefix_per_tile > 0) return clamp_cap(a->prefix_per_tile, T);
-    AdaptiveCap& c = adaptive_cap(a->W, a->H);
-    if (c.pending && hipEventQuery(c.ev) == hipSuccess) {
-        c.pending = false;
-        if (*c.unfinished > 0u && c.per_tile < MAX_PREFIX_PER_TILE)
-            c.per_tile = c.per_tile * 3 / 2 < MAX_PREFIX_PER_TILE ? c.per_tile * 3 / 2 : MAX_PREFIX_PER_TILE;
-    }
-    return clamp_cap(c.per_tile, T);
+    return clamp_cap(ac ? ac->per_tile : DEFAULT_PREFIX_PER_TILE, T);
 }
-// after the phase-1 render of an adaptive view: queue the unfinished count for the next forward of this size
-void note_unfinished(const dg_raster_args* a, const uint32_t* counters, hipStream_t s) {
-    if (a->prefix_per_tile != 0) return;
-    AdaptiveCap& c = adaptive_cap(a->W, a->H);
-    if (c.pending) return;  // one outstanding probe per size
-    (void)hipMemcpyAsync(c.unfinished, counters + gs::CNT_UNFINISHED, 4, hipMemcpyDeviceToHost, s);
-    (void)hipEventRecord(c.ev, s);
-    c.pending = true;
+void adapt(AdaptiveCap* ac, uint32_t prev_unfinished) {
+    if (ac && prev_unfinished > 0u && ac->per_tile < MAX_PREFIX_PER_TILE)
+        ac->per_tile = ac->per_tile * 3 / 2 < MAX_PREFIX_PER_TILE ? ac->per_tile * 3 / 2 : MAX_PREFIX_PER_TILE;
 }
 
 struct BwdScratch {
@@ -399,6 +391,7 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     *binning_out = nullptr;
     *binning2_out = nullptr;
 
+    AdaptiveCap* const ac = adaptive_cap(a);
     const size_t gbytes = carve_geom(nullptr, P).bytes;
     void* gbase = alloc(user, DG_BUF_GEOM, gbytes);
     if (!gbase) return fail("geometry allocation failed%s%d");
@@ -410,7 +403,8 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     *geom_out = gbase;
     *image_out = ibase;
 
-    HIP_OK(hipMemsetAsync(g.counters, 0, 64, s));
+    // no memset of the counters: k_depth_cut writes every slot (the preprocess's sums and error bits go through
+    // its per-block parts)
     gs::PreArgs pre;
     fill_pre(pre, a);
     pre.radii = radii; pre.sp = g.sp; pre.depthkey = g.dkey; pre.cnt = g.cnt; pre.rcnt = g.rcnt;
@@ -428,12 +422,12 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
         PROF("prefix_cut");
         gs::launch_depth_hist(P, g.dkey, g.cnt, g.hist, s);
         if (prefix_enabled(a)) {
-            C1 = phase1_cap(a, T);
+            C1 = phase1_cap(a, T, ac);
             gs::launch_depth_cut(g.hist, (uint32_t)C1, g.counters, im.tile_cnt, im.tile_cnt2, (uint32_t)T,
-                                 pre.rect_part, nparts, s);
+                                 pre.rect_part, nparts, ac ? ac->probe : nullptr, s);
         } else {  // everything in one phase: the capacity is the total rect area itself (one early sync)
             gs::launch_depth_cut(g.hist, 0xffffffffu, g.counters, im.tile_cnt, im.tile_cnt2, (uint32_t)T,
-                                 pre.rect_part, nparts, s);
+                                 pre.rect_part, nparts, nullptr, s);
             uint32_t k = 0;
             HIP_OK(hipMemcpyAsync(&k, g.counters + gs::CNT_K, 4, hipMemcpyDeviceToHost, s));
             HIP_OK(hipStreamSynchronize(s));
@@ -477,10 +471,10 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     if (gcount && P > 0) HIP_OK(hipMemsetAsync(gcount, 0, sizeof(uint32_t) * (size_t)P, s));
     { PROF("render_fwd"); gs::launch_render_fwd(r, s); }
     DBG_SYNC(a->debug, s);
-    if (prefix_enabled(a) && C1 > 0 && P > 0) note_unfinished(a, g.counters, s);
 
     HIP_OK(hipEventSynchronize(hcs.ev));
     const uint32_t* hc = hcs.buf;
+    adapt(ac, hc[gs::CNT_PREV_UNF]);
     if (hc[gs::CNT_ERR]) return fail("a Gaussian was filtered although prefiltered is set%s%d");
     const uint64_t rect = (uint64_t)hc[gs::CNT_RECT_LO] | ((uint64_t)hc[gs::CNT_RECT_LO + 1] << 32);
     *num_rendered = (int64_t)rect;
@@ -504,7 +498,7 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     const uint32_t* gate = g.counters + gs::CNT_UNFINISHED;
     {
         PROF("phase2");
-        gs::launch_unfinished_sat(g.counters, im.unfinished, tx, ty, im.sat, s);
+        gs::launch_unfinished_sat(g.counters, im.unfinished, tx, ty, im.sat, s, ac ? ac->probe : nullptr);
         gs::BinArgs ba = bin_args(a, g, im, T, (uint32_t)K, b2, im.tile_cnt2, im.ranges2);
         gs::launch_bin(2, ba, g.counters + gs::CNT_K2, g.scan_tmp, s);
         tile_sort(b2, K, T, im.ranges2, im.unfinished, gate, im.long_tiles, g.counters + gs::CNT_LONG2, s);

@@ -26,7 +26,8 @@ struct PreArgs {
     uint32_t* hist;     // [DH_BINS] depth histogram, zeroed here
     uint32_t* cnt;      // tile-rect area (0 when culled)
     uint32_t* rcnt;     // records per Gaussian, zeroed here (written by the emission kernels)
-    unsigned long long* rect_part;  // [blocks] per-block sums of rect areas (k_depth_cut totals them: num_rendered)
+    unsigned long long* rect_part;  // [blocks] per-block sums of rect areas (k_depth_cut totals them: num_rendered);
+                                    // bit 63 = a prefiltered violation in the block (-> counters[CNT_ERR])
     uint32_t* err;
 };
 
@@ -43,6 +44,7 @@ enum {
     CNT_INVD = 9,       // backward: any(dL/dinvdepth != 0) (zeroed with the block by the forward)
     CNT_LONG = 11,      // phase-1 tiles queued for the long-list depth sort
     CNT_LONG2 = 12,     // phase-2 tiles queued for the long-list depth sort
+    CNT_PREV_UNF = 14,  // unfinished tiles of the previous phase-2 launch at this image size (adaptive capacity)
 };
 
 // Depth histogram of the prefix cut: bins of 2^DH_SHIFT key ulps (1/64 of a binade) from the near plane up;
@@ -125,10 +127,13 @@ void launch_preprocess(const PreArgs& a, hipStream_t s);
 void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_t* hist, hipStream_t s);
 // counters[K, THR, E1, CUT] from the histogram (phase-1 capacity cap); resets the per-view counters and zeroes
 // the per-tile counters of both binning phases (tile_cnt, tile_cnt2 [num_tiles])
-// It also totals the preprocess's per-block rect-area sums into counters[CNT_RECT_LO..+1] (num_rendered): one
-// atomic per block on a single address costs ~10 us per 1e6 Gaussians (cross-XCD serialization).
+// It also totals the preprocess's per-block rect-area sums into counters[CNT_RECT_LO..+1] (num_rendered) and their
+// error bits into counters[CNT_ERR] (one atomic per block on a single address costs ~10 us per 1e6 Gaussians:
+// cross-XCD serialization), and writes every other counter slot, so the block needs no memset per view.  probe
+// (optional, device, per image size): moved into counters[CNT_PREV_UNF] and cleared.
 void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, uint32_t* tile_cnt, uint32_t* tile_cnt2,
-                      uint32_t num_tiles, const unsigned long long* rect_part, uint32_t nparts, hipStream_t s);
+                      uint32_t num_tiles, const unsigned long long* rect_part, uint32_t nparts, uint32_t* probe,
+                      hipStream_t s);
 // Binning walk of one phase (phase 1: Gaussians with key < counters[CNT_THR]; phase 2: those past it, only instances
 // in tiles phase 1 left unfinished): k_bin_count (precise cull walk -> rcnt, per-wave totals, per-tile counts),
 // exclusive scan of the wave totals (*total = the phase's instance count), per-tile ranges, k_bin_emit (first_e;
@@ -156,8 +161,9 @@ struct BinArgs {
 void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s);
 size_t bin_scan_temp_bytes(int P);
 int bin_waves(int P);
+// probe (optional, device): receives counters[CNT_UNFINISHED] (read back by the next view's k_depth_cut)
 void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, int tiles_x, int tiles_y,
-                           uint32_t* sat, hipStream_t s);
+                           uint32_t* sat, hipStream_t s, uint32_t* probe = nullptr);
 void launch_render_fwd(const RenderArgs& a, hipStream_t s);
 // count mode: score[i] = gcount[i] x the (AA-scaled) opacity of splat record i (0 when culled)
 void launch_count_score(int P, const int* radii, const float4* sp, const uint32_t* gcount, float* score,

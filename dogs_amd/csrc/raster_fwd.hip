@@ -216,10 +216,14 @@ __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx) {
 // Gaussians need them, and the binning walk (k_bin_count / k_bin_emit) computes them for those.
 __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     __shared__ unsigned long long s_sum[4];
+    __shared__ uint32_t s_err;
     const int t = threadIdx.x;
     const int base = blockIdx.x * 256;
     const int idx = base + t;
     for (int i = base + t; i < DH_BINS; i += gridDim.x * 256) a.hist[i] = 0u;  // for k_depth_hist
+    if (t == 0) s_err = 0u;
+    __syncthreads();
+    a.err = &s_err;  // a prefiltered violation flags the block (bit 63 of its part)
     uint32_t area = 0;
     if (idx < a.P) area = preprocess_one(a, idx);
     unsigned long long v = area;
@@ -227,7 +231,8 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = v;
     __syncthreads();
-    if (threadIdx.x == 0) a.rect_part[blockIdx.x] = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+    if (threadIdx.x == 0)
+        a.rect_part[blockIdx.x] = (s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3]) | (s_err ? (1ull << 63) : 0ull);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -277,15 +282,24 @@ __global__ void __launch_bounds__(1024) k_depth_cut(const uint32_t* __restrict__
                                                     uint32_t* __restrict__ counters, uint32_t* __restrict__ tile_cnt,
                                                     uint32_t* __restrict__ tile_cnt2, uint32_t num_tiles,
                                                     const unsigned long long* __restrict__ rect_part,
-                                                    uint32_t nparts) {
+                                                    uint32_t nparts, uint32_t* __restrict__ probe) {
     __shared__ uint32_t s_w[16];
     __shared__ int s_best;
     __shared__ unsigned long long s_rect[16];
+    __shared__ uint32_t s_err;
     constexpr int PER = DH_BINS / 1024;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (t == 0) s_err = 0u;
+    __syncthreads();
     {  // num_rendered = sum of the preprocess's per-block rect areas
         unsigned long long r = 0;
-        for (uint32_t i = t; i < nparts; i += 1024) r += rect_part[i];
+        bool e = false;
+        for (uint32_t i = t; i < nparts; i += 1024) {
+            const unsigned long long v = rect_part[i];
+            r += v & ~(1ull << 63);
+            e |= (v >> 63) != 0ull;
+        }
+        if (__any(e) && lane == 0) s_err = 1u;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
         if (lane == 0) s_rect[w] = r;
@@ -322,6 +336,10 @@ __global__ void __launch_bounds__(1024) k_depth_cut(const uint32_t* __restrict__
         for (int k = 0; k < 16; k++) r += s_rect[k];
         counters[CNT_RECT_LO] = (uint32_t)r;
         counters[CNT_RECT_LO + 1] = (uint32_t)(r >> 32);
+        counters[CNT_ERR] = s_err;
+        counters[CNT_INVD] = 0u; counters[10] = 0u; counters[13] = 0u; counters[15] = 0u;
+        counters[CNT_PREV_UNF] = probe ? *probe : 0u;
+        if (probe) *probe = 0u;
     }
     const bool cut = K > cap;
     if (t == 0 && s_best < 0) {  // not even bin 0 fits: phase 1 bins nothing, phase 2 everything
@@ -502,7 +520,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
 }
 __global__ void __launch_bounds__(256) k_sat_rows(const uint32_t* __restrict__ counters,
                                                   const uint8_t* __restrict__ unf, int tx, int ty,
-                                                  uint32_t* __restrict__ sat) {
+                                                  uint32_t* __restrict__ sat, uint32_t* __restrict__ probe) {
+    if (probe && blockIdx.x == 0 && threadIdx.x == 0) *probe = counters[CNT_UNFINISHED];
     if (counters[CNT_UNFINISHED] == 0u) return;
     const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);  // sat row r = tile row r - 1
     if (r > ty) return;
@@ -764,8 +783,9 @@ void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_
     if (P > 0) k_depth_hist<<<(P + per - 1) / per, DH_THREADS, 0, s>>>(P, dkey, cnt, hist);
 }
 void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, uint32_t* tile_cnt, uint32_t* tile_cnt2,
-                      uint32_t num_tiles, const unsigned long long* rect_part, uint32_t nparts, hipStream_t s) {
-    k_depth_cut<<<1, 1024, 0, s>>>(hist, cap, counters, tile_cnt, tile_cnt2, num_tiles, rect_part, nparts);
+                      uint32_t num_tiles, const unsigned long long* rect_part, uint32_t nparts, uint32_t* probe,
+                      hipStream_t s) {
+    k_depth_cut<<<1, 1024, 0, s>>>(hist, cap, counters, tile_cnt, tile_cnt2, num_tiles, rect_part, nparts, probe);
 }
 void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s) {
     if (a.P <= 0) return;
@@ -786,8 +806,8 @@ void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hi
 size_t bin_scan_temp_bytes(int P) { return scan_temp_bytes((uint32_t)((P + EMIT_RANKS - 1) / EMIT_RANKS)); }
 int bin_waves(int P) { return (P + EMIT_RANKS - 1) / EMIT_RANKS; }
 void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, int tiles_x, int tiles_y,
-                           uint32_t* sat, hipStream_t s) {
-    k_sat_rows<<<(tiles_y + 1 + 3) / 4, 256, 0, s>>>(counters, unfinished, tiles_x, tiles_y, sat);
+                           uint32_t* sat, hipStream_t s, uint32_t* probe) {
+    k_sat_rows<<<(tiles_y + 1 + 3) / 4, 256, 0, s>>>(counters, unfinished, tiles_x, tiles_y, sat, probe);
     k_sat_cols<<<(tiles_x + 3) / 4, 256, 0, s>>>(counters, tiles_x, tiles_y, sat);
 }
 void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
