@@ -182,14 +182,23 @@ gs::BinArgs bin_args(const dg_raster_args* r, const Geom& g, const Image& im, in
     return a;
 }
 // per-tile (depth, index) order of a phase's binned lists
-void tile_sort(const Binning& b, int64_t cap, int T, uint2* ranges, const uint8_t* only, const uint32_t* gate,
-               uint32_t* long_list, uint32_t* long_cnt, hipStream_t s) {
+gs::DSortArgs dsort_args(const Binning& b, int64_t cap, int T, uint2* ranges, const uint8_t* only,
+                         const uint32_t* gate, uint32_t* long_list, uint32_t* long_cnt) {
     gs::DSortArgs d;
     d.num_tiles = T; d.ranges = ranges; d.s_e = b.se; d.s_tmp = b.se_tmp; d.k_a = b.dk; d.k_b = b.dk2;
     d.ikey = b.ik; d.eg = b.eg; d.n_inst = (uint32_t)(cap > 0 ? cap : 1); d.only = only; d.gate = gate;
     d.long_list = long_list; d.long_cnt = long_cnt;
-    gs::tile_depth_sort(d, s);
+    return d;
 }
+void tile_sort(const Binning& b, int64_t cap, int T, uint2* ranges, const uint8_t* only, const uint32_t* gate,
+               uint32_t* long_list, uint32_t* long_cnt, hipStream_t s) {
+    gs::tile_depth_sort(dsort_args(b, cap, T, ranges, only, gate, long_list, long_cnt), s);
+}
+#ifdef DG_NO_FUSED_SORT  // A/B switch: the phase-1 depth sort as its own launches
+constexpr bool FUSED_SORT = false;
+#else
+constexpr bool FUSED_SORT = true;
+#endif
 
 // Pinned per-thread landing buffer + event for the forward's early counter read.
 struct HostCounters {
@@ -451,8 +460,12 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     HostCounters& hcs = host_counters();
     HIP_OK(hipMemcpyAsync(hcs.buf, g.counters, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_OK(hipEventRecord(hcs.ev, s));
+    const gs::DSortArgs ds1 = dsort_args(b, C1, T, im.ranges, nullptr, nullptr, im.long_tiles,
+                                         g.counters + gs::CNT_LONG);
+    const bool fuse = FUSED_SORT && C1 > 0 && P > 0;
     if (C1 > 0 && P > 0) {
-        { PROF("tile_bin"); tile_sort(b, C1, T, im.ranges, nullptr, nullptr, im.long_tiles, g.counters + gs::CNT_LONG, s); }
+        // the lists longer than a wave's capacity here; the render sorts the others tile by tile (fused)
+        { PROF("tile_bin"); if (fuse) gs::tile_depth_sort_long_only(ds1, s); else gs::tile_depth_sort(ds1, s); }
         DBG_SYNC(a->debug, s);
     } else {
         HIP_OK(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * (size_t)T, s));
@@ -468,6 +481,8 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     r.phase = 1; r.counters = g.counters; r.unfinished = im.unfinished; r.resume = im.resume;
     r.ranges2_zero = im.ranges2;
     r.gcount = gcount;
+    r.fuse_sort = fuse ? 1 : 0;
+    r.ds = ds1;
     if (gcount && P > 0) HIP_OK(hipMemsetAsync(gcount, 0, sizeof(uint32_t) * (size_t)P, s));
     { PROF("render_fwd"); gs::launch_render_fwd(r, s); }
     DBG_SYNC(a->debug, s);

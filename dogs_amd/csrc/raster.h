@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sortscan.h"
+
 namespace gs {
 
 // Splat record: everything binning and compositing read per Gaussian, in ONE 32-B record so a
@@ -73,6 +75,11 @@ struct RenderArgs {
     float *out_color, *out_invd, *final_T, *img_color, *img_invd;
     uint32_t *n_contrib, *max_contrib;
     uint32_t* gcount;           // optional (count mode): contributing pixels per Gaussian, accumulated
+    // phase 1: each wave first sorts its tile's list (<= DS_WAVE_MAX; longer ones were sorted beforehand by
+    // tile_depth_sort_long_only) into the reference order, writes it back for the backward and composites it from
+    // wave-private LDS -- the latency-bound sort overlaps the VALU-bound compositing of other waves
+    int fuse_sort;
+    DSortArgs ds;
 };
 
 struct RenderBwdArgs {

@@ -16,6 +16,7 @@
 #include "gs_common.h"
 #include "raster.h"
 #include "sortscan.h"
+#include "wave_sort.h"
 
 namespace gs {
 
@@ -586,12 +587,21 @@ constexpr int FWD_GROUP = DG_FWD_GROUP;  // splats per branch-free group of the 
 #endif
 template <int PHASE, bool COUNT>
 __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
-    __shared__ float4 s_b[4][65][3];  // 64 staged splats + a null splat (opacity 0: no pixel accepts it)
+    // per wave: the sort's scratch (cnt 256 + keys 512 + values 512 u32), then 64 staged splats + a null splat
+    // (opacity 0: no pixel accepts it) = 780 u32 and the sorted list (512 u32)
+    constexpr int WAVE_LDS = 780 + DS_WAVE_MAX;
+    __shared__ __attribute__((aligned(16))) uint32_t s_raw[4][WAVE_LDS];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tile = blockIdx.x * 4 + w;
     if (tile >= a.num_tiles) return;
     if (PHASE == 2 && !a.unfinished[tile]) return;  // finished in phase 1: outputs already final
-    float4* sb = &s_b[w][0][0];
+    float4* sb = reinterpret_cast<float4*>(&s_raw[w][0]);
+    uint32_t* ids = &s_raw[w][780];
+    bool lds_ids = false;
+    if (PHASE == 1 && a.fuse_sort) {
+        const int ns = wave_sort_tile(a.ds, tile, lane, &s_raw[w][0], &s_raw[w][256], &s_raw[w][768], ids);
+        lds_ids = ns > 1 && ns <= DS_WAVE_MAX;  // 0/1 need no sort, longer lists were sorted by the pre-pass
+    }
     if (lane < 3) sb[64 * 3 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
     const int tx0 = tx * GS_TILE_X, ty0 = ty * GS_TILE_Y;
@@ -624,7 +634,7 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
         const int j = base + lane;
         bool touch = false;
         if (j < n) {
-            const uint32_t e = min(a.s_e[rg.x + j], a.K - 1);
+            const uint32_t e = min(lds_ids ? ids[j] : a.s_e[rg.x + j], a.K - 1);
             const uint32_t g = min(a.eg[e], a.P - 1);
             const float4 s0 = a.sp[2 * g], s1 = a.sp[2 * g + 1];
             const float4 q = a.rgbi[g];
@@ -644,7 +654,7 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
           for (int u = 0; u < FWD_GROUP; u++) {
             const int jj = mask ? (int)__builtin_ctzll(mask) : 64;
             mask &= mask - 1;
-            const float4 Sa = s_b[w][jj][0], Sb = s_b[w][jj][1], Sc = s_b[w][jj][2];
+            const float4 Sa = sb[jj * 3 + 0], Sb = sb[jj * 3 + 1], Sc = sb[jj * 3 + 2];
             const uint32_t c = cbase + (uint32_t)(base + jj + 1);
             const v4f p2 = splat_power4(Sa.z, Sa.w, Sb.x, Sa.x, Sa.y, pxv, pyv);
             v4f al = bc4(Sb.y) * (v4f){__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y),

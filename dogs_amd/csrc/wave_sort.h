@@ -1,0 +1,228 @@
+// wave_sort.h -- per-tile depth sort of an instance list by one wave64 (in registers + wave-private LDS), shared by
+// k_tile_dsort (sortscan.hip) and the phase-1 render, which sorts its own tile before compositing it
+// (raster_fwd.hip).  See sortscan.hip "binning by tile" for the design.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sortscan.h"
+
+namespace gs {
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const int lane = __lane_id();
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// lanes of this wave (among active ones) whose 8-bit digit equals mine
+__device__ __forceinline__ uint64_t peer_mask(uint32_t digit, bool active) {
+    uint64_t m = __ballot(active);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+        const bool bit = (digit >> b) & 1u;
+        const uint64_t bal = __ballot(bit && active);
+        m &= bit ? bal : ~bal;
+    }
+    return active ? m : 0ull;
+}
+
+constexpr int DS_WAVE_MAX = 512;
+constexpr int DS_ROWS = DS_WAVE_MAX / 64;
+
+__device__ __forceinline__ uint32_t ds_key(const DSortArgs& a, uint32_t v) {
+    return a.ikey[v < a.n_inst ? v : a.n_inst - 1];
+}
+__device__ __forceinline__ uint32_t ds_gid(const DSortArgs& a, uint32_t v) {
+    return a.eg[v < a.n_inst ? v : a.n_inst - 1];
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { const uint32_t y = __shfl_xor(x, o); x = y < x ? y : x; }
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { const uint32_t y = __shfl_xor(x, o); x = y > x ? y : x; }
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+}
+__device__ __forceinline__ int passes_for(uint32_t range) { return range ? (32 - __clz((int)range) + 7) >> 3 : 0; }
+
+// Stable in-wave LSD radix sort of (k, v) over the R = ceil(n/64) register rows, digits of k below 8*passes.
+// Items i >= n must carry k = 0xffffffff (they stay last).
+__device__ __forceinline__ void wave_radix(uint32_t (&k)[DS_ROWS], uint32_t (&v)[DS_ROWS], int R, int passes,
+                                           uint32_t* cnt, uint32_t* lk, uint32_t* lv, int lane) {
+    uint32_t rank[DS_ROWS];
+    const uint64_t lt = lanemask_lt();
+    for (int p = 0; p < passes; p++) {
+        const int shift = 8 * p;
+#pragma unroll
+        for (int q = 0; q < 4; q++) cnt[q * 64 + lane] = 0u;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < DS_ROWS; r++) {
+            if (r < R) {
+                const uint32_t d = (k[r] >> shift) & 0xffu;
+                const uint64_t m = peer_mask(d, true);
+                const uint32_t before = (uint32_t)__popcll(m & lt);
+                const uint32_t cur = cnt[d];
+                rank[r] = cur + before;
+                if (before == 0) cnt[d] = cur + (uint32_t)__popcll(m);  // LDS ops of one wave complete in order
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        {  // exclusive scan of the 256 digit counts, 4 per lane
+            const uint32_t c0 = cnt[4 * lane], c1 = cnt[4 * lane + 1], c2 = cnt[4 * lane + 2], c3 = cnt[4 * lane + 3];
+            const uint32_t loc = c0 + c1 + c2 + c3;
+            uint32_t x = loc;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o);
+                if (lane >= o) x += y;
+            }
+            const uint32_t ex = x - loc;
+            __builtin_amdgcn_wave_barrier();
+            cnt[4 * lane] = ex; cnt[4 * lane + 1] = ex + c0; cnt[4 * lane + 2] = ex + c0 + c1;
+            cnt[4 * lane + 3] = ex + c0 + c1 + c2;
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < DS_ROWS; r++) {
+            if (r < R) {
+                const uint32_t pos = cnt[(k[r] >> shift) & 0xffu] + rank[r];
+                lk[pos] = k[r];
+                lv[pos] = v[r];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < DS_ROWS; r++) {
+            if (r < R) { k[r] = lk[r * 64 + lane]; v[r] = lv[r * 64 + lane]; }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Relative sort keys of the wave's items (key(v) - min over the list; 0xffffffff padding); returns the range.
+template <typename KeyFn>
+__device__ __forceinline__ uint32_t wave_rel_keys(uint32_t (&k)[DS_ROWS], const uint32_t (&v)[DS_ROWS], int R, int n,
+                                                  int lane, KeyFn&& key) {
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        const int i = r * 64 + lane;
+        k[r] = (r < R && i < n) ? key(v[r]) : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        const int i = r * 64 + lane;
+        if (r < R && i < n) {
+            kmin = k[r] < kmin ? k[r] : kmin;
+            kmax = k[r] > kmax ? k[r] : kmax;
+        }
+    }
+    kmin = wave_min_u32(kmin);
+    kmax = wave_max_u32(kmax);
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        const int i = r * 64 + lane;
+        k[r] = (i < n) ? k[r] - kmin : 0xffffffffu;
+    }
+    return kmax - kmin;
+}
+
+// Sort tile `tile`'s list (n <= DS_WAVE_MAX) into (depth key, Gaussian index) order and write it back to s_e (and,
+// when ids_out is given, to ids_out[0..n), e.g. wave-private LDS).  cnt [256], lk/lv [DS_WAVE_MAX]: wave-private LDS
+// scratch.  Returns n; a longer list is left alone (returns n too: the caller handles it).
+__device__ __forceinline__ int wave_sort_tile(const DSortArgs& a, int tile, int lane, uint32_t* cnt, uint32_t* lk,
+                                              uint32_t* lv, uint32_t* ids_out) {
+    const uint2 rg = a.ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    if (n <= 1 || n > DS_WAVE_MAX) return n;
+    uint32_t* se = a.s_e + rg.x;
+    const int R = (n + 63) >> 6;
+    uint32_t k[DS_ROWS], v[DS_ROWS];
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        const int i = r * 64 + lane;
+        v[r] = (r < R && i < n) ? se[i] : 0u;
+    }
+    const uint32_t range = wave_rel_keys(k, v, R, n, lane, [&](uint32_t x) { return ds_key(a, x); });
+#ifndef DG_DSORT_NOSORT
+    wave_radix(k, v, R, passes_for(range), cnt, lk, lv, lane);
+#endif
+    // Equal depth keys (i >= n carry 0xffffffff and never match a real relative key) must end up in Gaussian
+    // index order; the counting sort left them in arrival order.  They sit next to each other after the sort, so
+    // odd-even transposition between equal-key neighbours fixes them (one round per element of the longest run).
+    bool tie = false;
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        if (r < R) {
+            uint32_t prev = __shfl_up(k[r], 1);
+            if (lane == 0) prev = r > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)k[r > 0 ? r - 1 : 0], 63) : ~k[r];
+            const int i = r * 64 + lane;
+            tie |= (i < n) && prev == k[r];
+        }
+    }
+    if (__any(tie)) {
+        uint32_t gid[DS_ROWS];
+#pragma unroll
+        for (int r = 0; r < DS_ROWS; r++) {
+            const int i = r * 64 + lane;
+            gid[r] = (r < R && i < n) ? ds_gid(a, v[r]) : 0xffffffffu;
+        }
+        for (int round = 0; round < DS_WAVE_MAX; round++) {
+            bool changed = false;
+#pragma unroll
+            for (int par = 0; par < 2; par++) {
+                uint32_t nv[DS_ROWS], ng[DS_ROWS];
+#pragma unroll
+                for (int r = 0; r < DS_ROWS; r++) {
+                    nv[r] = v[r]; ng[r] = gid[r];
+                    if (r >= R) continue;
+                    const int i = r * 64 + lane;
+                    // right neighbour (i + 1) and left neighbour (i - 1)
+                    uint32_t kr = __shfl_down(k[r], 1), vr = __shfl_down(v[r], 1), gr = __shfl_down(gid[r], 1);
+                    uint32_t kl = __shfl_up(k[r], 1), vl = __shfl_up(v[r], 1), gl = __shfl_up(gid[r], 1);
+                    if (r + 1 < DS_ROWS) {
+                        const int rn = r + 1 < DS_ROWS ? r + 1 : r;
+                        const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)k[rn], 0);
+                        const uint32_t v0 = (uint32_t)__builtin_amdgcn_readlane((int)v[rn], 0);
+                        const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)gid[rn], 0);
+                        if (lane == 63) { kr = k0; vr = v0; gr = g0; }
+                    }
+                    if (r > 0) {
+                        const int rp = r > 0 ? r - 1 : 0;
+                        const uint32_t k63 = (uint32_t)__builtin_amdgcn_readlane((int)k[rp], 63);
+                        const uint32_t v63 = (uint32_t)__builtin_amdgcn_readlane((int)v[rp], 63);
+                        const uint32_t g63 = (uint32_t)__builtin_amdgcn_readlane((int)gid[rp], 63);
+                        if (lane == 0) { kl = k63; vl = v63; gl = g63; }
+                    }
+                    if (i < n) {
+                        if ((i & 1) == par) {  // left element of the pair (i, i + 1)
+                            if (i + 1 < n && kr == k[r] && gr < gid[r]) { nv[r] = vr; ng[r] = gr; changed = true; }
+                        } else if (i > 0) {    // right element of the pair (i - 1, i)
+                            if (kl == k[r] && gid[r] < gl) { nv[r] = vl; ng[r] = gl; changed = true; }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < DS_ROWS; r++) { v[r] = nv[r]; gid[r] = ng[r]; }
+            }
+            if (!__any(changed)) break;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < DS_ROWS; r++) {
+        const int i = r * 64 + lane;
+        if (r < R && i < n) {
+            se[i] = v[r];
+            if (ids_out) ids_out[i] = v[r];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    return n;
+}
+
+}  // namespace gs
