@@ -599,8 +599,8 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
     uint32_t* ids = &s_raw[w][780];
     bool lds_ids = false;
     if (PHASE == 1 && a.fuse_sort) {
-        const int ns = wave_sort_tile(a.ds, tile, lane, &s_raw[w][0], &s_raw[w][256], &s_raw[w][768], ids);
-        lds_ids = ns > 1 && ns <= DS_WAVE_MAX;  // 0/1 need no sort, longer lists were sorted by the pre-pass
+        const int ns = wave_sort_tile<DS_ROWS>(a.ds, tile, lane, &s_raw[w][0], &s_raw[w][256], &s_raw[w][768], ids);
+        lds_ids = ns > 1 && ns <= DS_WAVE_MAX;  // 0/1 need no sort, longer lists were sorted before the render
     }
     if (lane < 3) sb[64 * 3 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;

@@ -51,7 +51,7 @@ struct DSortArgs {
     uint32_t* long_cnt;         // device queue length, zeroed beforehand
 };
 void tile_depth_sort(const DSortArgs& a, hipStream_t stream);
-// Only the lists longer than one wave's capacity (DS_WAVE_MAX), found by scanning the ranges; the phase-1 render
-// sorts the others itself (wave_sort.h).
+// Only the lists longer than the render's per-wave capacity (DS_WAVE_MAX): a wave per list up to DS_WAVE_MAX2, a block
+// per longer one; the phase-1 render sorts the others itself (wave_sort.h).
 void tile_depth_sort_long_only(const DSortArgs& a, hipStream_t stream);
 }  // namespace gs

@@ -454,17 +454,20 @@ void bin_offsets(uint32_t* wtot, uint32_t n, uint32_t* total, uint32_t* tile_cnt
     k_bin_offsets<<<2, 1024, 0, stream>>>(wtot, n, total, tile_cnt, num_tiles, ranges, gate);
 }
 
+// One wave per tile, lists up to DS_WAVE_MAX2 (16 items per lane); min_n: only lists longer than that (the phase-1
+// render sorts the shorter ones itself).  Longer lists are queued for k_tile_dsort_long.
+template <int MIN_N>
 __global__ void __launch_bounds__(256) k_tile_dsort(DSortArgs a) {
     __shared__ uint32_t s_cnt[4][RS_RADIX];
-    __shared__ uint32_t s_k[4][DS_WAVE_MAX];
-    __shared__ uint32_t s_v[4][DS_WAVE_MAX];
+    __shared__ uint32_t s_k[4][DS_WAVE_MAX2];
+    __shared__ uint32_t s_v[4][DS_WAVE_MAX2];
     if (a.gate && *a.gate == 0u) return;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tile = blockIdx.x * 4 + w;
     if (tile >= a.num_tiles) return;
     if (a.only && !a.only[tile]) return;
-    const int n = wave_sort_tile(a, tile, lane, s_cnt[w], s_k[w], s_v[w], nullptr);
-    if (n > DS_WAVE_MAX && lane == 0) a.long_list[atomicAdd(a.long_cnt, 1u)] = (uint32_t)tile;
+    const int n = wave_sort_tile<DS_ROWS2>(a, tile, lane, s_cnt[w], s_k[w], s_v[w], nullptr, MIN_N);
+    if (n > DS_WAVE_MAX2 && lane == 0) a.long_list[atomicAdd(a.long_cnt, 1u)] = (uint32_t)tile;
 }
 
 // One stable LSD step of the long-list sort by the 256-thread block: (key(v) - kmin) digits, (keys, vals) ping-pong
@@ -580,35 +583,15 @@ __global__ void __launch_bounds__(256) k_tile_dsort_long(DSortArgs a) {
         block_sort_long(a, (int)a.long_list[li], s_base, s_wh, s_red, &s_tie);
 }
 
-// The long lists alone, found by scanning the ranges (each block checks 256 tiles): the phase-1 render sorts the
-// short ones itself, wave by wave, before compositing them.
-__global__ void __launch_bounds__(256) k_tile_dsort_long_scan(DSortArgs a) {
-    __shared__ uint32_t s_base[RS_RADIX];
-    __shared__ uint32_t s_wh[RS_WAVES][RS_RADIX];
-    __shared__ uint32_t s_red[2][RS_WAVES];
-    __shared__ int s_tie;
-    __shared__ uint32_t s_n;
-    __shared__ uint32_t s_list[256];
-    const int t = threadIdx.x;
-    if (t == 0) s_n = 0u;
-    __syncthreads();
-    const int tile = blockIdx.x * 256 + t;
-    if (tile < a.num_tiles) {
-        const uint2 rg = a.ranges[tile];
-        if (rg.y - rg.x > (uint32_t)DS_WAVE_MAX) s_list[atomicAdd(&s_n, 1u)] = (uint32_t)tile;
-    }
-    __syncthreads();
-    const uint32_t nl = s_n;
-    for (uint32_t li = 0; li < nl; li++) block_sort_long(a, (int)s_list[li], s_base, s_wh, s_red, &s_tie);
-}
-
 void tile_depth_sort_long_only(const DSortArgs& a, hipStream_t stream) {
-    if (a.num_tiles > 0) k_tile_dsort_long_scan<<<(a.num_tiles + 255) / 256, 256, 0, stream>>>(a);
+    if (a.num_tiles <= 0) return;
+    k_tile_dsort<DS_WAVE_MAX><<<(a.num_tiles + 3) / 4, 256, 0, stream>>>(a);
+    k_tile_dsort_long<<<256, 256, 0, stream>>>(a);
 }
 
 void tile_depth_sort(const DSortArgs& a, hipStream_t stream) {
     if (a.num_tiles <= 0) return;
-    k_tile_dsort<<<(a.num_tiles + 3) / 4, 256, 0, stream>>>(a);
+    k_tile_dsort<1><<<(a.num_tiles + 3) / 4, 256, 0, stream>>>(a);
     k_tile_dsort_long<<<256, 256, 0, stream>>>(a);
 }
 

@@ -26,8 +26,10 @@ __device__ __forceinline__ uint64_t peer_mask(uint32_t digit, bool active) {
     return active ? m : 0ull;
 }
 
-constexpr int DS_WAVE_MAX = 512;
+constexpr int DS_WAVE_MAX = 512;           // per-wave capacity inside the render (8 items per lane)
 constexpr int DS_ROWS = DS_WAVE_MAX / 64;
+constexpr int DS_WAVE_MAX2 = 1024;         // per-wave capacity of the standalone sort kernels (16 per lane)
+constexpr int DS_ROWS2 = DS_WAVE_MAX2 / 64;
 
 __device__ __forceinline__ uint32_t ds_key(const DSortArgs& a, uint32_t v) {
     return a.ikey[v < a.n_inst ? v : a.n_inst - 1];
@@ -50,9 +52,10 @@ __device__ __forceinline__ int passes_for(uint32_t range) { return range ? (32 -
 
 // Stable in-wave LSD radix sort of (k, v) over the R = ceil(n/64) register rows, digits of k below 8*passes.
 // Items i >= n must carry k = 0xffffffff (they stay last).
-__device__ __forceinline__ void wave_radix(uint32_t (&k)[DS_ROWS], uint32_t (&v)[DS_ROWS], int R, int passes,
+template <int ROWS>
+__device__ __forceinline__ void wave_radix(uint32_t (&k)[ROWS], uint32_t (&v)[ROWS], int R, int passes,
                                            uint32_t* cnt, uint32_t* lk, uint32_t* lv, int lane) {
-    uint32_t rank[DS_ROWS];
+    uint32_t rank[ROWS];
     const uint64_t lt = lanemask_lt();
     for (int p = 0; p < passes; p++) {
         const int shift = 8 * p;
@@ -60,7 +63,7 @@ __device__ __forceinline__ void wave_radix(uint32_t (&k)[DS_ROWS], uint32_t (&v)
         for (int q = 0; q < 4; q++) cnt[q * 64 + lane] = 0u;
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int r = 0; r < DS_ROWS; r++) {
+        for (int r = 0; r < ROWS; r++) {
             if (r < R) {
                 const uint32_t d = (k[r] >> shift) & 0xffu;
                 const uint64_t m = peer_mask(d, true);
@@ -87,7 +90,7 @@ __device__ __forceinline__ void wave_radix(uint32_t (&k)[DS_ROWS], uint32_t (&v)
         }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int r = 0; r < DS_ROWS; r++) {
+        for (int r = 0; r < ROWS; r++) {
             if (r < R) {
                 const uint32_t pos = cnt[(k[r] >> shift) & 0xffu] + rank[r];
                 lk[pos] = k[r];
@@ -96,7 +99,7 @@ __device__ __forceinline__ void wave_radix(uint32_t (&k)[DS_ROWS], uint32_t (&v)
         }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int r = 0; r < DS_ROWS; r++) {
+        for (int r = 0; r < ROWS; r++) {
             if (r < R) { k[r] = lk[r * 64 + lane]; v[r] = lv[r * 64 + lane]; }
         }
         __builtin_amdgcn_wave_barrier();
@@ -104,17 +107,17 @@ __device__ __forceinline__ void wave_radix(uint32_t (&k)[DS_ROWS], uint32_t (&v)
 }
 
 // Relative sort keys of the wave's items (key(v) - min over the list; 0xffffffff padding); returns the range.
-template <typename KeyFn>
-__device__ __forceinline__ uint32_t wave_rel_keys(uint32_t (&k)[DS_ROWS], const uint32_t (&v)[DS_ROWS], int R, int n,
+template <int ROWS, typename KeyFn>
+__device__ __forceinline__ uint32_t wave_rel_keys(uint32_t (&k)[ROWS], const uint32_t (&v)[ROWS], int R, int n,
                                                   int lane, KeyFn&& key) {
     uint32_t kmin = 0xffffffffu, kmax = 0u;
 #pragma unroll
-    for (int r = 0; r < DS_ROWS; r++) {
+    for (int r = 0; r < ROWS; r++) {
         const int i = r * 64 + lane;
         k[r] = (r < R && i < n) ? key(v[r]) : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < DS_ROWS; r++) {
+    for (int r = 0; r < ROWS; r++) {
         const int i = r * 64 + lane;
         if (r < R && i < n) {
             kmin = k[r] < kmin ? k[r] : kmin;
@@ -124,39 +127,40 @@ __device__ __forceinline__ uint32_t wave_rel_keys(uint32_t (&k)[DS_ROWS], const 
     kmin = wave_min_u32(kmin);
     kmax = wave_max_u32(kmax);
 #pragma unroll
-    for (int r = 0; r < DS_ROWS; r++) {
+    for (int r = 0; r < ROWS; r++) {
         const int i = r * 64 + lane;
         k[r] = (i < n) ? k[r] - kmin : 0xffffffffu;
     }
     return kmax - kmin;
 }
 
-// Sort tile `tile`'s list (n <= DS_WAVE_MAX) into (depth key, Gaussian index) order and write it back to s_e (and,
-// when ids_out is given, to ids_out[0..n), e.g. wave-private LDS).  cnt [256], lk/lv [DS_WAVE_MAX]: wave-private LDS
-// scratch.  Returns n; a longer list is left alone (returns n too: the caller handles it).
+// Sort tile `tile`'s list (min_n < n <= 64 ROWS) into (depth key, Gaussian index) order and write it back to s_e
+// (and, when ids_out is given, to ids_out[0..n), e.g. wave-private LDS).  cnt [256], lk/lv [64 ROWS]: wave-private
+// LDS scratch.  Returns n; a list outside (min_n, 64 ROWS] is left alone (the caller handles it).
+template <int ROWS>
 __device__ __forceinline__ int wave_sort_tile(const DSortArgs& a, int tile, int lane, uint32_t* cnt, uint32_t* lk,
-                                              uint32_t* lv, uint32_t* ids_out) {
+                                              uint32_t* lv, uint32_t* ids_out, int min_n = 1) {
     const uint2 rg = a.ranges[tile];
     const int n = (int)(rg.y - rg.x);
-    if (n <= 1 || n > DS_WAVE_MAX) return n;
+    if (n <= min_n || n <= 1 || n > 64 * ROWS) return n;
     uint32_t* se = a.s_e + rg.x;
     const int R = (n + 63) >> 6;
-    uint32_t k[DS_ROWS], v[DS_ROWS];
+    uint32_t k[ROWS], v[ROWS];
 #pragma unroll
-    for (int r = 0; r < DS_ROWS; r++) {
+    for (int r = 0; r < ROWS; r++) {
         const int i = r * 64 + lane;
         v[r] = (r < R && i < n) ? se[i] : 0u;
     }
     const uint32_t range = wave_rel_keys(k, v, R, n, lane, [&](uint32_t x) { return ds_key(a, x); });
 #ifndef DG_DSORT_NOSORT
-    wave_radix(k, v, R, passes_for(range), cnt, lk, lv, lane);
+    wave_radix<ROWS>(k, v, R, passes_for(range), cnt, lk, lv, lane);
 #endif
     // Equal depth keys (i >= n carry 0xffffffff and never match a real relative key) must end up in Gaussian
     // index order; the counting sort left them in arrival order.  They sit next to each other after the sort, so
     // odd-even transposition between equal-key neighbours fixes them (one round per element of the longest run).
     bool tie = false;
 #pragma unroll
-    for (int r = 0; r < DS_ROWS; r++) {
+    for (int r = 0; r < ROWS; r++) {
         if (r < R) {
             uint32_t prev = __shfl_up(k[r], 1);
             if (lane == 0) prev = r > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)k[r > 0 ? r - 1 : 0], 63) : ~k[r];
@@ -165,27 +169,27 @@ __device__ __forceinline__ int wave_sort_tile(const DSortArgs& a, int tile, int 
         }
     }
     if (__any(tie)) {
-        uint32_t gid[DS_ROWS];
+        uint32_t gid[ROWS];
 #pragma unroll
-        for (int r = 0; r < DS_ROWS; r++) {
+        for (int r = 0; r < ROWS; r++) {
             const int i = r * 64 + lane;
             gid[r] = (r < R && i < n) ? ds_gid(a, v[r]) : 0xffffffffu;
         }
-        for (int round = 0; round < DS_WAVE_MAX; round++) {
+        for (int round = 0; round < 64 * ROWS; round++) {
             bool changed = false;
 #pragma unroll
             for (int par = 0; par < 2; par++) {
-                uint32_t nv[DS_ROWS], ng[DS_ROWS];
+                uint32_t nv[ROWS], ng[ROWS];
 #pragma unroll
-                for (int r = 0; r < DS_ROWS; r++) {
+                for (int r = 0; r < ROWS; r++) {
                     nv[r] = v[r]; ng[r] = gid[r];
                     if (r >= R) continue;
                     const int i = r * 64 + lane;
                     // right neighbour (i + 1) and left neighbour (i - 1)
                     uint32_t kr = __shfl_down(k[r], 1), vr = __shfl_down(v[r], 1), gr = __shfl_down(gid[r], 1);
                     uint32_t kl = __shfl_up(k[r], 1), vl = __shfl_up(v[r], 1), gl = __shfl_up(gid[r], 1);
-                    if (r + 1 < DS_ROWS) {
-                        const int rn = r + 1 < DS_ROWS ? r + 1 : r;
+                    if (r + 1 < ROWS) {
+                        const int rn = r + 1 < ROWS ? r + 1 : r;
                         const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)k[rn], 0);
                         const uint32_t v0 = (uint32_t)__builtin_amdgcn_readlane((int)v[rn], 0);
                         const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)gid[rn], 0);
@@ -207,14 +211,14 @@ __device__ __forceinline__ int wave_sort_tile(const DSortArgs& a, int tile, int 
                     }
                 }
 #pragma unroll
-                for (int r = 0; r < DS_ROWS; r++) { v[r] = nv[r]; gid[r] = ng[r]; }
+                for (int r = 0; r < ROWS; r++) { v[r] = nv[r]; gid[r] = ng[r]; }
             }
             if (!__any(changed)) break;
         }
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int r = 0; r < DS_ROWS; r++) {
+    for (int r = 0; r < ROWS; r++) {
         const int i = r * 64 + lane;
         if (r < R && i < n) {
             se[i] = v[r];
