@@ -219,6 +219,7 @@ __device__ __forceinline__ void tile_order_sort(int num_tiles, uint32_t* order, 
     if (t < NB) s_hist[t] = 0u;
     __syncthreads();
     const int chunk = (int)blockDim.x * PER;
+    uint32_t b0[PER];  // the keys of the first chunk, kept for the scatter (the only chunk up to 16384 tiles)
     for (int c0 = 0; c0 < num_tiles; c0 += chunk) {
         uint32_t b[PER];
 #pragma unroll
@@ -226,6 +227,7 @@ __device__ __forceinline__ void tile_order_sort(int num_tiles, uint32_t* order, 
             const int tile = c0 + k * (int)blockDim.x + t;
             const uint32_t l = tile < num_tiles ? len(tile) >> 2 : 0u;
             b[k] = NB - 1 - (l < NB - 1 ? l : NB - 1);
+            if (c0 == 0) b0[k] = b[k];
         }
 #pragma unroll
         for (int k = 0; k < PER; k++)
@@ -252,17 +254,18 @@ __device__ __forceinline__ void tile_order_sort(int num_tiles, uint32_t* order, 
     }
     __syncthreads();
     for (int c0 = 0; c0 < num_tiles; c0 += chunk) {
-        uint32_t b[PER];
+        if (c0 > 0 || num_tiles > chunk) {  // more than one chunk: the keys were not kept, recompute them
 #pragma unroll
-        for (int k = 0; k < PER; k++) {
-            const int tile = c0 + k * (int)blockDim.x + t;
-            const uint32_t l = tile < num_tiles ? len(tile) >> 2 : 0u;
-            b[k] = NB - 1 - (l < NB - 1 ? l : NB - 1);
+            for (int k = 0; k < PER; k++) {
+                const int tile = c0 + k * (int)blockDim.x + t;
+                const uint32_t l = tile < num_tiles ? len(tile) >> 2 : 0u;
+                b0[k] = NB - 1 - (l < NB - 1 ? l : NB - 1);
+            }
         }
 #pragma unroll
         for (int k = 0; k < PER; k++) {
             const int tile = c0 + k * (int)blockDim.x + t;
-            if (tile < num_tiles) order[atomicAdd(&s_hist[b[k]], 1u)] = (uint32_t)tile;
+            if (tile < num_tiles) order[atomicAdd(&s_hist[b0[k]], 1u)] = (uint32_t)tile;
         }
     }
 }

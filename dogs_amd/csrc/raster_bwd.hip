@@ -235,19 +235,12 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
 }
 
 // Replay length of a tile: its list (phase 1 + phase 2) cut at the last contributor, as render_bwd_tile.
-__device__ __forceinline__ uint32_t replay_len(const RenderBwdArgs& a, int tile) {
-    const uint2 rg = a.ranges[tile];
-    uint32_t n = rg.y - rg.x;
-    if (a.ranges2 && a.unfinished[tile]) {
-        const uint2 rg2 = a.ranges2[tile];
-        n += rg2.y - rg2.x;
-    }
-    const uint32_t mc = a.max_contrib[tile];
-    return n < mc ? n : mc;
-}
+// Replay length of a tile for the launch order: its max contributor (the replay runs to it; the list is never
+// shorter), one load per tile.
+__device__ __forceinline__ uint32_t replay_len(const RenderBwdArgs& a, int tile) { return a.max_contrib[tile]; }
 
-// Longest-first launch order for the replay (tile_order_sort in k_bwd_prologue); the key is the exact replay
-// length.  Per tile, not per 4-tile block: ordering whole blocks by their longest tile measured 6% slower.
+// Longest-first launch order for the replay (tile_order_sort in k_bwd_prologue).  Per tile, not per 4-tile block:
+// ordering whole blocks by their longest tile measured 6% slower.
 
 #ifdef DG_BWD_WPE  // occupancy experiment: cap VGPRs so that DG_BWD_WPE waves fit per SIMD
 #define BWD_WPE_ATTR __attribute__((amdgpu_waves_per_eu(DG_BWD_WPE)))
