@@ -59,12 +59,14 @@ typedef struct {
  * Outputs out_color [3,H,W], out_invdepth [1,H,W], radii [P] (int32).
  * *num_rendered = the reference's num_rendered (sum of tile-rect areas);
  * *num_instances = the phase-1 binning capacity this view used (returned where the reference returns num_buckets;
- * both are opaque tokens handed back to the backward; dg_binned_instances gives the instance count).  Binning is depth-prefix (DESIGN.md "Binning"):
+ * both are opaque tokens handed back to the backward; dg_binned_instances gives the instance count).
+ * Binning is depth-prefix (DESIGN.md "Binning"):
  * phase 1 bins the first instances of the global depth order (a prefix of every tile's list), phase 2 bins
  * the rest only for tiles that phase 1 left unfinished -- same images and gradients, far fewer instances.
  * Allocates DG_BUF_GEOM, DG_BUF_IMAGE, DG_BUF_BINNING and, only when phase 2 runs, DG_BUF_BINNING2 through
  * `alloc`; the caller keeps the four pointers (*binning2 = NULL when absent; the reference's sampleBuffer
- * slot carries it) and passes them to dg_rasterize_backward.  One host sync (two when phase 2 runs). */
+ * slot carries it) and passes them to dg_rasterize_backward.  One host sync, after the binning is queued (two
+ * with prefix_per_tile < 0, which sizes the binning from the rect total first). */
 int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_invdepth, int* radii,
                          dg_alloc_fn alloc, void* user, void** geom, void** binning, void** image, void** binning2,
                          int64_t* num_rendered, int64_t* num_instances, dg_stream_t stream);
