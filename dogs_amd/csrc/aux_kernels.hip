@@ -11,143 +11,14 @@
 namespace gs {
 
 // ------------------------------------------------------------------------------------------------
-// fused SSIM.  One 256-thread workgroup per 32x32 tile of one (batch, channel) plane.  The reference
-// runs five separable convolutions back to back through one scratch buffer (15 barriers per channel);
-// here the x-pass of all five moments is done in one sweep over the 42x42 halo tile and the y-pass
-// reads them from LDS.  Accumulation order per moment is the reference's (tap 0..10, x then y).
-// ------------------------------------------------------------------------------------------------
-__constant__ float c_gw[11] = {0.001028380123898387f, 0.0075987582094967365f, 0.036000773310661316f,
-                               0.10936068743467331f, 0.21300552785396576f, 0.26601171493530273f,
-                               0.21300552785396576f, 0.10936068743467331f, 0.036000773310661316f,
-                               0.0075987582094967365f, 0.001028380123898387f};
-constexpr int SB = 32, SH = SB + 10;
-
-__device__ __forceinline__ float pix_at(const float* img, int y, int x, int H, int W) {
-    return (x >= W || y >= H || x < 0 || y < 0) ? 0.0f : img[(size_t)y * W + x];
-}
-
-template <bool TRAIN>
-__global__ void __launch_bounds__(256) k_ssim_fwd(int H, int W, float C1, float C2, const float* __restrict__ img1,
-                                                  const float* __restrict__ img2, float* __restrict__ map,
-                                                  float* __restrict__ dmu1, float* __restrict__ ds1,
-                                                  float* __restrict__ ds12) {
-    __shared__ float s1[SH][SH + 1];
-    __shared__ float s2[SH][SH + 1];
-    __shared__ float hx[5][SH][SB + 1];
-    const size_t plane = (size_t)blockIdx.z * H * W;
-    const float* a = img1 + plane;
-    const float* b = img2 + plane;
-    const int y0 = blockIdx.y * SB - 5, x0 = blockIdx.x * SB - 5;
-    for (int i = threadIdx.x; i < SH * SH; i += 256) {
-        const int ly = i / SH, lx = i % SH;
-        s1[ly][lx] = pix_at(a, y0 + ly, x0 + lx, H, W);
-        s2[ly][lx] = pix_at(b, y0 + ly, x0 + lx, H, W);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < SH * SB; i += 256) {
-        const int ly = i / SB, lx = i % SB;
-        float m1 = 0, m2 = 0, q1 = 0, q2 = 0, q12 = 0;
-#pragma unroll
-        for (int k = 0; k < 11; k++) {
-            const float g = c_gw[k];
-            const float u = s1[ly][lx + k], v = s2[ly][lx + k];
-            m1 = fmaf(g, u, m1);
-            q1 = fmaf(g, u * u, q1);
-            m2 = fmaf(g, v, m2);
-            q2 = fmaf(g, v * v, q2);
-            q12 = fmaf(g, u * v, q12);
-        }
-        hx[0][ly][lx] = m1; hx[1][ly][lx] = q1; hx[2][ly][lx] = m2; hx[3][ly][lx] = q2; hx[4][ly][lx] = q12;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < SB * SB; i += 256) {
-        const int ly = i / SB, lx = i % SB;
-        const int y = blockIdx.y * SB + ly, x = blockIdx.x * SB + lx;
-        float v[5] = {0, 0, 0, 0, 0};
-#pragma unroll
-        for (int k = 0; k < 11; k++) {
-            const float g = c_gw[k];
-#pragma unroll
-            for (int q = 0; q < 5; q++) v[q] = fmaf(g, hx[q][ly + k][lx], v[q]);
-        }
-        const float mu1 = v[0], mu2 = v[2];
-        const float sigma1_sq = fmaf(-mu1, mu1, v[1]);
-        const float sigma2_sq = fmaf(-mu2, mu2, v[3]);
-        const float sigma12 = fmaf(-mu1, mu2, v[4]);
-        const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu1_mu2 = mu1 * mu2;
-        const float Cc = fmaf(2.0f, mu1_mu2, C1);
-        const float D = fmaf(2.0f, sigma12, C2);
-        const float A = (mu1_sq + mu2_sq) + C1;
-        const float B = (sigma1_sq + sigma2_sq) + C2;
-        if (x < W && y < H) {
-            const size_t gi = plane + (size_t)y * W + x;
-            map[gi] = (Cc * D) / (A * B);
-            if (TRAIN) {
-                dmu1[gi] = ((mu2 * 2.0f * D) / (A * B) - (mu2 * 2.0f * Cc) / (A * B) - (mu1 * 2.0f * Cc * D) / (A * A * B) +
-                            (mu1 * 2.0f * Cc * D) / (A * B * B));
-                ds1[gi] = ((-Cc * D) / (A * B * B));
-                ds12[gi] = ((2 * Cc) / (A * B));
-            }
-        }
-    }
-}
-
-__global__ void __launch_bounds__(256) k_ssim_bwd(int H, int W, const float* __restrict__ img1,
-                                                  const float* __restrict__ img2, const float* __restrict__ dL,
-                                                  const float* __restrict__ dmu1, const float* __restrict__ ds1,
-                                                  const float* __restrict__ ds12, float* __restrict__ dimg1) {
-    __shared__ float s[3][SH][SH + 1];
-    __shared__ float hx[3][SH][SB + 1];
-    const size_t plane = (size_t)blockIdx.z * H * W;
-    const int y0 = blockIdx.y * SB - 5, x0 = blockIdx.x * SB - 5;
-    for (int i = threadIdx.x; i < SH * SH; i += 256) {
-        const int ly = i / SH, lx = i % SH;
-        const int y = y0 + ly, x = x0 + lx;
-        const float l = pix_at(dL + plane, y, x, H, W);
-        s[0][ly][lx] = pix_at(dmu1 + plane, y, x, H, W) * l;
-        s[1][ly][lx] = pix_at(ds1 + plane, y, x, H, W) * l;
-        s[2][ly][lx] = pix_at(ds12 + plane, y, x, H, W) * l;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < SH * SB; i += 256) {
-        const int ly = i / SB, lx = i % SB;
-        float h0 = 0, h1 = 0, h2 = 0;
-#pragma unroll
-        for (int k = 0; k < 11; k++) {
-            const float g = c_gw[k];
-            h0 = fmaf(g, s[0][ly][lx + k], h0);
-            h1 = fmaf(g, s[1][ly][lx + k], h1);
-            h2 = fmaf(g, s[2][ly][lx + k], h2);
-        }
-        hx[0][ly][lx] = h0; hx[1][ly][lx] = h1; hx[2][ly][lx] = h2;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < SB * SB; i += 256) {
-        const int ly = i / SB, lx = i % SB;
-        const int y = blockIdx.y * SB + ly, x = blockIdx.x * SB + lx;
-        if (x >= W || y >= H) continue;
-        float v0 = 0, v1 = 0, v2 = 0;
-#pragma unroll
-        for (int k = 0; k < 11; k++) {
-            const float g = c_gw[k];
-            v0 = fmaf(g, hx[0][ly + k][lx], v0);
-            v1 = fmaf(g, hx[1][ly + k][lx], v1);
-            v2 = fmaf(g, hx[2][ly + k][lx], v2);
-        }
-        const size_t gi = plane + (size_t)y * W + x;
-        float d = v0;
-        d += (img1[gi] * 2.0f) * v1;
-        d += img2[gi] * v2;
-        dimg1[gi] = d;
-    }
-}
-
-// ---- wave-strip variant (the one launched).  One wave per strip of 54 output columns x 32 output rows of one
+// fused SSIM (ssim.cu:187-444 semantics).  One wave per strip of 54 output columns x 32 output rows of one
 // plane: the 64 lanes hold 54 + 10 halo columns, so the horizontal 11-tap pass is a chain of DPP wave_shl:1 moves
 // (lane i <- lane i+1) with no LDS at all, and the vertical pass runs over a ring of the last 11 rows' horizontal
-// moments in registers (the 11-row loop is unrolled so every ring slot is a compile-time register).  Same products
-// and the same fma order per moment as k_ssim_fwd/k_ssim_bwd above (x taps 0..10, then y taps 0..10): identical
-// results.  Rows are read 2 ahead of use.
+// moments in registers (the 11-row loop is unrolled so every ring slot is a compile-time register).  Products and
+// fma order per moment are the reference's (x taps 0..10, then y taps 0..10).  Rows are read 2 ahead of use.
+// (The first version staged 42x42 halo tiles and the x-pass moments in LDS: forward 94-102 us, backward 80 us at
+// 1080p x 3; this one: 94 and 60.)
+// ------------------------------------------------------------------------------------------------
 constexpr int SSW_OUT = 54;   // output columns per wave
 #ifndef DG_SSW_ROWS
 #define DG_SSW_ROWS 32
@@ -162,7 +33,7 @@ constexpr float GW[11] = {0.001028380123898387f, 0.0075987582094967365f, 0.03600
 __device__ __forceinline__ float wave_shl1(float x) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x130, 0xf, 0xf, false));
 }
-// sum_k GW[k] * x(lane + k), k = 0..10, as the x-pass of k_ssim_fwd accumulates it
+// sum_k GW[k] * x(lane + k), k = 0..10, in the reference's tap order
 __device__ __forceinline__ float hconv11(float x) {
     float acc = fmaf(GW[0], x, 0.0f);
 #pragma unroll
@@ -240,6 +111,18 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
                         const float A = (mu1_sq + mu2_sq) + C1;
                         const float B = (sigma1_sq + sigma2_sq) + C2;
                         const size_t gi = plane + (size_t)y * W + ox;
+#ifndef DG_SSIM_IEEEDIV  // reciprocals of the three denominators instead of seven IEEE divisions: forward 97 -> 81 us
+                         // at 1080p x 3, within the 1e-5 parity bar (test_fused_ssim_matches_oracle)
+                        const float rAB = __builtin_amdgcn_rcpf(A * B), rAAB = __builtin_amdgcn_rcpf(A * A * B),
+                                    rABB = __builtin_amdgcn_rcpf(A * B * B);
+                        map[gi] = (Cc * D) * rAB;
+                        if (TRAIN) {
+                            dmu1[gi] = ((mu2 * 2.0f * D) * rAB - (mu2 * 2.0f * Cc) * rAB - (mu1 * 2.0f * Cc * D) * rAAB +
+                                        (mu1 * 2.0f * Cc * D) * rABB);
+                            ds1[gi] = ((-Cc * D) * rABB);
+                            ds12[gi] = ((2 * Cc) * rAB);
+                        }
+#else
                         map[gi] = (Cc * D) / (A * B);
                         if (TRAIN) {
                             dmu1[gi] = ((mu2 * 2.0f * D) / (A * B) - (mu2 * 2.0f * Cc) / (A * B) -
@@ -247,6 +130,7 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
                             ds1[gi] = ((-Cc * D) / (A * B * B));
                             ds12[gi] = ((2 * Cc) / (A * B));
                         }
+#endif
                     }
                 }
             }
