@@ -293,13 +293,19 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    step_t = []
     for i in range(args.steps):
+        ts = time.perf_counter()
         one(i)
+        step_t.append(time.perf_counter() - ts)
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0)
+    st = sorted(step_t)
+    print(f"[bench rank {rank}] host time per step (launch + forward sync): min {st[0] * 1e3:.3f} "
+          f"median {st[len(st) // 2] * 1e3:.3f} max {st[-1] * 1e3:.3f} ms", file=sys.stderr)
     # The consensus runs once per consensus_interval steps (urban3d_admm.yaml:44: 200).  It is timed on its own,
     # barrier-bracketed like the steps, and its cost is added in that proportion (a K-step window either misses it
     # or, holding one whole exchange, would overweight it K/interval-fold).

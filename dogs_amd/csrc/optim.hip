@@ -26,6 +26,21 @@ __device__ __forceinline__ float adam_one(float p, float gr, float& m, float& v,
     return p + (-lr * em / (sqrtf(ev) + eps));
 }
 
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 nt_load4(const float* p) {
+    const nt_f4 x = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(p));
+    return make_float4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ void nt_store4(float* p, float4 v) {
+    const nt_f4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<nt_f4*>(p));
+}
+
+#ifndef DG_ADAM_CHUNKS
+#define DG_ADAM_CHUNKS 1
+#endif
+constexpr int ADAM_CHUNKS = DG_ADAM_CHUNKS;  // float4 chunks per lane
+
 __global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
     const uint32_t blk = blockIdx.x;
     if (blk >= a.start[a.n]) {  // densification statistics, one Gaussian per lane
@@ -44,43 +59,64 @@ __global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
     int k = 0;
     while (k + 1 < a.n && blk >= a.start[k + 1]) k++;  // block-uniform
     const AdamGroup g = a.g[k];
-    // N * M < 2^32 (checked on the host): 32-bit index math, one division per lane
+    // N * M < 2^32 (checked on the host): 32-bit index math, one division per lane.  Each lane owns ADAM_CHUNKS
+    // float4 chunks, 256 * 4 floats apart (coalesced per chunk), all loads issued before any update.
     const uint32_t total = a.N * g.M;
-    const uint32_t e0 = 4u * ((blk - a.start[k]) * 256u + threadIdx.x);
-    if (e0 >= total) return;
     const float b1 = a.b1, b2 = a.b2;
-    uint32_t gi = e0 / g.M, r = e0 - gi * g.M;
-    bool vis[4];
-    bool any = false;
+    const uint32_t base = 4u * ((blk - a.start[k]) * 256u * ADAM_CHUNKS + threadIdx.x);
+    float4 p[ADAM_CHUNKS], gr[ADAM_CHUNKS], m[ADAM_CHUNKS], v[ADAM_CHUNKS];
+    bool vis[ADAM_CHUNKS][4], act[ADAM_CHUNKS];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        vis[j] = e0 + j < total && a.visible[gi] != 0;
-        any |= vis[j];
-        if (++r == g.M) { r = 0; gi++; }
-    }
-    if (!any) return;
-    if (g.vec && e0 + 4 <= total) {
-        float4 p = *reinterpret_cast<const float4*>(g.param + e0);
-        const float4 gr = *reinterpret_cast<const float4*>(g.grad + e0);
-        float4 m = *reinterpret_cast<const float4*>(g.m + e0);
-        float4 v = *reinterpret_cast<const float4*>(g.v + e0);
-        if (vis[0]) p.x = adam_one(p.x, gr.x, m.x, v.x, g.lr, b1, b2, g.eps);
-        if (vis[1]) p.y = adam_one(p.y, gr.y, m.y, v.y, g.lr, b1, b2, g.eps);
-        if (vis[2]) p.z = adam_one(p.z, gr.z, m.z, v.z, g.lr, b1, b2, g.eps);
-        if (vis[3]) p.w = adam_one(p.w, gr.w, m.w, v.w, g.lr, b1, b2, g.eps);
-        *reinterpret_cast<float4*>(g.param + e0) = p;
-        *reinterpret_cast<float4*>(g.m + e0) = m;
-        *reinterpret_cast<float4*>(g.v + e0) = v;
-        return;
+    for (int c = 0; c < ADAM_CHUNKS; c++) {
+        const uint32_t e0 = base + 1024u * c;
+        act[c] = false;
+        if (e0 >= total) continue;
+        uint32_t gi = e0 / g.M, r = e0 - gi * g.M;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            vis[c][j] = e0 + j < total && a.visible[gi] != 0;
+            act[c] |= vis[c][j];
+            if (++r == g.M) { r = 0; gi++; }
+        }
+        if (act[c] && g.vec && e0 + 4 <= total) {
+#ifndef DG_ADAM_CACHED
+            p[c] = nt_load4(g.param + e0); gr[c] = nt_load4(g.grad + e0);
+            m[c] = nt_load4(g.m + e0); v[c] = nt_load4(g.v + e0);
+#else
+            p[c] = *reinterpret_cast<const float4*>(g.param + e0);
+            gr[c] = *reinterpret_cast<const float4*>(g.grad + e0);
+            m[c] = *reinterpret_cast<const float4*>(g.m + e0);
+            v[c] = *reinterpret_cast<const float4*>(g.v + e0);
+#endif
+        }
     }
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        if (!vis[j]) continue;
-        const uint32_t e = e0 + j;
-        float m = g.m[e], v = g.v[e];
-        g.param[e] = adam_one(g.param[e], g.grad[e], m, v, g.lr, b1, b2, g.eps);
-        g.m[e] = m;
-        g.v[e] = v;
+    for (int c = 0; c < ADAM_CHUNKS; c++) {
+        const uint32_t e0 = base + 1024u * c;
+        if (!act[c]) continue;
+        if (g.vec && e0 + 4 <= total) {
+            if (vis[c][0]) p[c].x = adam_one(p[c].x, gr[c].x, m[c].x, v[c].x, g.lr, b1, b2, g.eps);
+            if (vis[c][1]) p[c].y = adam_one(p[c].y, gr[c].y, m[c].y, v[c].y, g.lr, b1, b2, g.eps);
+            if (vis[c][2]) p[c].z = adam_one(p[c].z, gr[c].z, m[c].z, v[c].z, g.lr, b1, b2, g.eps);
+            if (vis[c][3]) p[c].w = adam_one(p[c].w, gr[c].w, m[c].w, v[c].w, g.lr, b1, b2, g.eps);
+#ifndef DG_ADAM_CACHED  // streaming (non-temporal) loads and stores: every byte is touched once (327 -> 269 us)
+            nt_store4(g.param + e0, p[c]); nt_store4(g.m + e0, m[c]); nt_store4(g.v + e0, v[c]);
+#else
+            *reinterpret_cast<float4*>(g.param + e0) = p[c];
+            *reinterpret_cast<float4*>(g.m + e0) = m[c];
+            *reinterpret_cast<float4*>(g.v + e0) = v[c];
+#endif
+            continue;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (!vis[c][j]) continue;
+            const uint32_t e = e0 + j;
+            float mm = g.m[e], vv = g.v[e];
+            g.param[e] = adam_one(g.param[e], g.grad[e], mm, vv, g.lr, b1, b2, g.eps);
+            g.m[e] = mm;
+            g.v[e] = vv;
+        }
     }
 }
 
@@ -233,8 +269,8 @@ void launch_adam_multi(const AdamMultiArgs& a0, hipStream_t s) {
     uint32_t b = 0;
     for (int k = 0; k < a.n; k++) {
         a.start[k] = b;
-        const uint64_t items = ((uint64_t)a.N * a.g[k].M + 3) / 4;
-        b += (uint32_t)((items + 255) / 256);
+        const uint64_t items = ((uint64_t)a.N * a.g[k].M + 3) / 4;  // float4 chunks
+        b += (uint32_t)((items + 256 * ADAM_CHUNKS - 1) / (256 * ADAM_CHUNKS));
     }
     a.start[a.n] = b;
     if (a.radii) b += (a.N + 255) / 256;
