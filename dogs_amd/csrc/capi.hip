@@ -264,8 +264,7 @@ void adapt(AdaptiveCap* ac, uint32_t prev_unfinished) {
 struct BwdScratch {
     uint8_t* flag;
     float* rec;
-    uint32_t *live_idx, *live_cnt;  // compacted contributing Gaussians (k_gauss_prep -> k_gauss_live)
-    float* live_acc;
+    uint32_t *live_list, *live_cnt;  // contributing Gaussians per record-sum chunk (k_gauss_sum -> k_gauss_live)
     uint32_t* invd_flag;
     uint32_t* order;  // [T] replay order of the tiles
     size_t bytes;
@@ -276,10 +275,9 @@ BwdScratch carve_bwd(void* base, int64_t K, int P, int T) {
     const size_t n = (size_t)(K > 0 ? K : 1);
     s.flag = c.take<uint8_t>(n);
     s.rec = c.take<float>(12 * n);
-    const size_t np = (size_t)(P > 0 ? P : 1);
-    s.live_idx = c.take<uint32_t>(np);
-    s.live_acc = c.take<float>(10 * np);
-    s.live_cnt = c.take<uint32_t>((np + 255) / 256);
+    const size_t chunks = (n + gs::SUM_CHUNK - 1) / gs::SUM_CHUNK;  // every slot < K
+    s.live_list = c.take<uint32_t>(chunks * gs::SUM_CHUNK);
+    s.live_cnt = c.take<uint32_t>(chunks);
     s.invd_flag = c.take<uint32_t>(4);
     s.order = c.take<uint32_t>((size_t)(T > 0 ? T : 1));
     s.bytes = c.off;
@@ -594,7 +592,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     BwdScratch sc = carve_bwd(sbase, Kcap, P, T);
     if (a->M > 0 && !dsh) return fail("dsh output required when M > 0%s%d");
     // the nine gradient outputs back to back (the Python side allocates them as views of one buffer): the replay
-    // zero-fills them while it is VALU-bound; otherwise k_gauss_prep does
+    // zero-fills them while it is VALU-bound; otherwise the aux blocks of k_gauss_sum do
     size_t zero_count = 0;
     {
         const size_t Pz = (size_t)P, Mz = (size_t)(a->M > 0 ? a->M : 0);
@@ -634,10 +632,11 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     q.means3D = a->means3D; q.scales = a->scales; q.rotations = a->rotations; q.opacities = a->opacities;
     q.dc = a->dc; q.sh = (a->M > 0) ? a->sh : nullptr; q.cov3D_precomp = a->cov3D_precomp;
     q.view = a->viewmatrix; q.proj = a->projmatrix; q.campos = a->campos;
-    q.radii = radii; q.dkey = g.dkey; q.cnt = g.rcnt; q.first_e = g.first_e; q.sp = g.sp; q.rec = sc.rec; q.flag = sc.flag;
+    q.radii = radii; q.dkey = g.dkey; q.sp = g.sp; q.rec = sc.rec; q.flag = sc.flag;
+    q.eg = b.eg; q.eg2 = eg2; q.counters = g.counters; q.K1 = (uint32_t)C1;
     q.dmeans2D = dmeans2D; q.dcolors = dcolors; q.dopacity = dopacity; q.dmeans3D = dmeans3D; q.dcov3D = dcov3D;
     q.ddc = ddc; q.dsh = dsh; q.dscales = dscales; q.drot = drot; q.depth = depth;
-    q.live_idx = sc.live_idx; q.live_acc = sc.live_acc; q.live_cnt = sc.live_cnt;
+    q.live_list = sc.live_list; q.live_cnt = sc.live_cnt;
     q.outputs_zeroed = zero_count != 0;
     { PROF("gauss_bwd"); gs::launch_gauss_bwd(q, s); }
     DBG_SYNC(a->debug, s);

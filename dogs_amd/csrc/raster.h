@@ -116,18 +116,27 @@ struct GaussBwdArgs {
     const float *view, *proj, *campos;
     const int* radii;
     const uint32_t* dkey;    // forward depth keys (bits of the view z)
-    const uint32_t* cnt;
-    const uint32_t* first_e;
     const float4* sp;        // splat records (conic + AA-scaled opacity)
-    const float* rec;
+    float* rec;              // per-instance records; k_gauss_sum overwrites a contributing Gaussian's last one
     const uint8_t* flag;
     float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *ddc, *dsh, *dscales, *drot, *depth;
     int outputs_zeroed;      // the nine gradient outputs were zero-filled by k_render_bwd
-    // k_gauss_prep -> k_gauss_live: per block of 256 Gaussians, the contributing ones (slots [256 b, 256 b + cnt))
-    uint32_t* live_idx;      // [P]
-    float* live_acc;         // [P][10] record sums
-    uint32_t* live_cnt;      // [ceil(P / 256)]
+    // k_gauss_sum walks the instance slots [0, E1 + K2) in chunks of SUM_CHUNK; owner of slot e: eg[e] (phase 1,
+    // e < E1) or eg2[e - E1] (phase 2)
+    const uint32_t* eg;
+    const uint32_t* eg2;     // null: no phase-2 block
+    const uint32_t* counters;  // CNT_E1, CNT_K2
+    uint32_t K1;             // phase-1 capacity (the forward's num_instances token)
+    // k_gauss_sum -> k_gauss_live: per chunk, the contributing Gaussians' last instance slots
+    // (live_list[chunk * SUM_CHUNK + j], j < live_cnt[chunk]); their record sums + index overwrite that record
+    uint32_t* live_list;     // [chunks * SUM_CHUNK]
+    uint32_t* live_cnt;      // [chunks]
 };
+#ifndef DG_SUM_STEPS
+#define DG_SUM_STEPS 4
+#endif
+constexpr uint32_t SUM_STEPS = DG_SUM_STEPS;      // 64-instance steps per record-sum chunk
+constexpr uint32_t SUM_CHUNK = 64u * SUM_STEPS;
 
 void launch_preprocess(const PreArgs& a, hipStream_t s);
 // hist[DH_BINS] (zeroed by the preprocess) += precise counts by depth bin

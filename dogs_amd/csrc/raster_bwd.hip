@@ -8,8 +8,9 @@
 //                reduce-scatter (13 cross-lane exchanges instead of 60) and stored once as a 48-B record
 //                at the instance's emission slot -- no float atomics (the chip-wide atomic rate and the
 //                scattered-row penalty make per-instance atomicAdd the wrong tool on MI355X).
-// k_gauss_prep   a wave per 64 Gaussians sums their records (deterministic order), zero-fills the gradient
-//                outputs and compacts the contributing Gaussians;
+// k_gauss_sum    a wave per chunk of instance slots sums the records of the Gaussians beginning there
+//                (segmented scan, deterministic order) and lists the contributing ones; extra blocks write the
+//                view depth (and zero-fill the gradient outputs when the replay could not);
 // k_gauss_live   one thread per contributing Gaussian turns the summed moments into dL/d(mean2D, conic,
 //                opacity), then computeCov2DCUDA + preprocessCUDA backward (backward.cu:149-451) fused in one pass.
 #include <hip/hip_runtime.h>
@@ -311,95 +312,156 @@ __device__ __forceinline__ float sq(float x) { return x * x; }
 
 __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, const float (&acc)[10]);
 
-struct RecSumLDS {
-    uint32_t pre[4][64];
-    uint32_t e0[4][64];
-    float acc[4][64][11];  // per-Gaussian accumulators (odd stride: conflict-free per-lane rows)
-};
-
-// Sum each Gaussian's instance records (written by k_render_bwd at emission slots [first_e, first_e + cnt) whose
-// flag is set) into acc (registers).  A wave owns 64 consecutive Gaussians; their instances are walked flattened,
-// 64 per step (one per lane; the records of a step are contiguous, so the loads are coalesced, and the flag and
-// the record are loaded together -- an unflagged slot counts zero).  A segmented scan over the lanes (segments =
-// owners, contiguous) sums each owner's part of the step; the segment's last lane adds it to the owner's LDS
-// accumulator.  Fixed summation order: deterministic.
-__device__ __forceinline__ void record_sum(const GaussBwdArgs& a, int idx, RecSumLDS& L, float (&acc)[10]) {
-    uint32_t (&s_pre)[4][64] = L.pre;
-    uint32_t (&s_e0)[4][64] = L.e0;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float* my_acc = L.acc[w][lane];
-#pragma unroll
-    for (int v = 0; v < 10; v++) my_acc[v] = 0.f;
-    uint32_t c = 0, e0 = 0;
-    if (idx < a.P && a.radii[idx] > 0) {
-        c = a.cnt[idx];
-        e0 = c ? a.first_e[idx] : 0u;
-        if (e0 >= a.K || c > a.K - e0) c = 0;  // defensive: never read outside the record block
-    }
-    uint32_t incl = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    s_pre[w][lane] = incl - c;
-    s_e0[w][lane] = e0;
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t i0 = 0; i0 < total; i0 += 64) {
-        const uint32_t item = i0 + (uint32_t)lane;
-        const bool valid = item < total;
-        int owner = 64 + lane;  // invalid lanes: a segment of their own
-        float v[10];
-#pragma unroll
-        for (int k = 0; k < 10; k++) v[k] = 0.f;
-        if (valid) {
-            int lo = 0;
-#pragma unroll
-            for (int step = 32; step > 0; step >>= 1)
-                if (s_pre[w][lo + step] <= item) lo += step;
-            owner = lo;
-            const uint32_t e = s_e0[w][lo] + (item - s_pre[w][lo]);
-            const bool f = a.flag[e] != 0;
-            const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
-            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
-            if (f) {
-                v[0] = r0.x; v[1] = r0.y; v[2] = r0.z; v[3] = r0.w; v[4] = r1.x;
-                v[5] = r1.y; v[6] = r1.z; v[7] = r1.w; v[8] = r2.x; v[9] = r2.y;
-            }
-        }
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int up = __shfl_up(owner, d);  // every lane shuffles (a bpermute from an inactive lane reads 0)
-            const bool same = lane >= d && up == owner;
-#pragma unroll
-            for (int k = 0; k < 10; k++) {
-                const float t = __shfl_up(v[k], d);
-                v[k] += same ? t : 0.f;
-            }
-        }
-        const int next = __shfl_down(owner, 1);
-        if (valid && (lane == 63 || next != owner)) {  // the segment's last lane: one per owner and step
-            float* dst = L.acc[w][owner];
-#pragma unroll
-            for (int k = 0; k < 10; k++) dst[k] += v[k];
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-#pragma unroll
-    for (int k = 0; k < 10; k++) acc[k] = my_acc[k];
+// ---- record sum: instance-parallel segmented reduction over the record slots
+// The instances of a Gaussian are contiguous slots in Gaussian order (phase 1 in [0, E1), phase 2 after it), and only
+// ~5% of the Gaussians have any, so the sum walks the slots, not the Gaussians: a wave per chunk of SUM_CHUNK slots,
+// 64 per step (owner, flag and record loads coalesced).  A Gaussian belongs to the chunk holding its first slot; the
+// wave skips the slots of a Gaussian begun in the chunk before and follows its last one past the chunk end.  Sums:
+// a segmented scan over the lanes (segments = owners) per step, plus the open segment carried from the previous step
+// -- a fixed order, deterministic.  The segment's last lane writes the Gaussian's 10 sums and its index over its own
+// record (read by now, by this wave only) and appends the slot to the chunk's list if any sum is nonzero.
+__device__ __forceinline__ uint32_t inst_owner(const GaussBwdArgs& a, uint32_t e, uint32_t E1) {
+    return e < E1 ? a.eg[e] : a.eg2[e - E1];
+}
+struct SumRange { uint32_t E1, NR; };
+__device__ __forceinline__ SumRange sum_range(const GaussBwdArgs& a) {
+    SumRange r;
+    r.E1 = min(a.counters[CNT_E1], min(a.K1, a.K));
+    r.NR = a.eg2 ? min(r.E1 + a.counters[CNT_K2], a.K) : r.E1;
+    return r;
 }
 
-// Block of 256 Gaussians; the [256][M][3] SH slab is staged through LDS so both the coefficient loads
-// and the dL/dsh stores are coalesced (a per-thread 180-B stride touches 64 lines per wave instruction).
-// The per-Gaussian backward in two passes, so that only the contributing Gaussians pay for the heavy math:
-// k_gauss_prep  one block per 256 consecutive Gaussians: zero-fills the block's slices of the nine gradient
-//               outputs (coalesced 16-B stores; skipped when k_render_bwd already zero-filled them), writes the view
-//               depth, sums every Gaussian's instance records
-//               (record_sum, a wave per 64) and compacts the contributing ones -- any record sum nonzero -- into the
-//               block's slot list (index + the 10 sums).  A Gaussian without contribution has exactly zero
-//               gradients, as in the reference.
-// k_gauss_live  one block per 4 prep blocks, one lane per compacted Gaussian: its per-Gaussian backward.
+// One 64-slot step: o/f/r* are this lane's slot (owner, flag, record; loaded by the caller, unconditionally, so that
+// the loads of every step are in flight together), nxt63 the owner of the slot after lane 63's.
+struct SumStep {
+    float carry[10];
+    uint32_t carry_owner, nlive;
+};
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void seg_level(uint32_t own, float (&v)[10]) {
+    // rows the DPP does not write, and lanes without a source, keep `old`: owner ~0 (never a lane's owner), value 0
+    const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)own, CTRL, ROW_MASK, 0xf, false);
+    const bool same = up == own;
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+        const float t = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[k]), CTRL, ROW_MASK, 0xf, false));
+        v[k] += same ? t : 0.f;
+    }
+}
+__device__ __forceinline__ bool sum_step(const GaussBwdArgs& a, uint32_t i0, uint32_t lo, uint32_t hi, uint32_t skip,
+                                         uint32_t tail, const SumRange R, int lane, uint32_t o, bool f, float4 r0,
+                                         float4 r1, float4 r2, uint32_t nxt63, SumStep& st) {
+    const uint32_t e = i0 + (uint32_t)lane;
+    const bool valid = e < R.NR && o != skip && (e < hi || o == tail) && o < (uint32_t)a.P;
+    // invalid lanes: a segment of their own (Gaussian ids < 2^31; never equal to carry_owner's ~0)
+    const uint32_t own = valid ? o : (0x80000000u | (uint32_t)lane);
+    float v[10];
+    const bool use = valid && f;
+    v[0] = use ? r0.x : 0.f; v[1] = use ? r0.y : 0.f; v[2] = use ? r0.z : 0.f; v[3] = use ? r0.w : 0.f;
+    v[4] = use ? r1.x : 0.f; v[5] = use ? r1.y : 0.f; v[6] = use ? r1.z : 0.f; v[7] = use ? r1.w : 0.f;
+    v[8] = use ? r2.x : 0.f; v[9] = use ? r2.y : 0.f;
+    // segmented inclusive scan with DPP (no LDS): row_shr 1, 2, 4, 8 within each 16-lane row, then row_bcast:15
+    // and row_bcast:31 across rows; a lane adds its partner's partial only when both have the same owner (segments
+    // are contiguous, so everything between them does too)
+    seg_level<0x111, 0xf>(own, v);
+    seg_level<0x112, 0xf>(own, v);
+    seg_level<0x114, 0xf>(own, v);
+    seg_level<0x118, 0xf>(own, v);
+    seg_level<0x142, 0xa>(own, v);
+    seg_level<0x143, 0xc>(own, v);
+    if (own == st.carry_owner) {  // the step's first segment continues the open one
+#pragma unroll
+        for (int k = 0; k < 10; k++) v[k] += st.carry[k];
+    }
+    const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)own, 0x130, 0xf, 0xf, false);  // wave_shl:1
+    const bool last = valid && (lane == 63 ? nxt63 != own : dn != own);
+    bool live = false;
+#pragma unroll
+    for (int k = 0; k < 10; k++) live |= v[k] != 0.0f;
+    live = live && last;
+    const uint64_t lm = __ballot(live);
+    if (live) {
+        float* r = a.rec + (size_t)e * 12;
+        *reinterpret_cast<float4*>(r) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(r + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        *reinterpret_cast<float4*>(r + 8) = make_float4(v[8], v[9], __uint_as_float(own), 0.f);
+        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        a.live_list[(size_t)lo + st.nlive + (uint32_t)__popcll(lm & lt)] = e;
+    }
+    st.nlive += (uint32_t)__popcll(lm);
+    // lane 63's segment stays open when it continues into the next step
+    const bool open = __builtin_amdgcn_readlane((int)(valid && !last), 63) != 0;
+    st.carry_owner = open ? (uint32_t)__builtin_amdgcn_readlane((int)own, 63) : 0xffffffffu;
+#pragma unroll
+    for (int k = 0; k < 10; k++) st.carry[k] = bcastf(v[k], 63);
+    return open;
+}
+
+__device__ __forceinline__ void sum_chunk(const GaussBwdArgs& a, uint32_t ch, const SumRange R, int lane) {
+    const uint32_t lo = ch * SUM_CHUNK, hi = min(lo + SUM_CHUNK, R.NR);
+    // every load of the chunk's SUM_STEPS + 1 steps (the last one for the tail Gaussian running past hi) is issued
+    // before any is used: one HBM round trip per chunk instead of two per step
+    constexpr int PF = SUM_STEPS + 1;
+    const uint32_t skip = lo ? inst_owner(a, lo - 1, R.E1) : 0xffffffffu;  // begun in the chunk before
+    const uint32_t tail = inst_owner(a, hi - 1, R.E1);                      // may run past hi
+    uint32_t o[PF];
+    bool f[PF];
+    float4 r0[PF], r1[PF], r2[PF];
+#pragma unroll
+    for (int q = 0; q < PF; q++) {
+        const uint32_t e = lo + 64u * q + (uint32_t)lane;
+        o[q] = 0xffffffffu; f[q] = false;
+        r0[q] = r1[q] = r2[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < R.NR) {
+            o[q] = inst_owner(a, e, R.E1);
+            f[q] = a.flag[e] != 0;
+            const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
+            r0[q] = r[0]; r1[q] = r[1]; r2[q] = r[2];
+        }
+    }
+    const uint32_t after = lo + 64u * PF;
+    const uint32_t nxt_pf = (lane == 63 && after < R.NR) ? inst_owner(a, after, R.E1) : 0xffffffffu;
+    SumStep st;
+#pragma unroll
+    for (int k = 0; k < 10; k++) st.carry[k] = 0.f;
+    st.carry_owner = 0xffffffffu;
+    st.nlive = 0;
+    bool open = false;
+    if (skip != tail) {  // else one Gaussian covers the whole chunk and belongs to an earlier one
+        bool done = false;
+#pragma unroll
+        for (int q = 0; q < PF; q++) {
+            if (!done) {
+                const uint32_t i0 = lo + 64u * q;
+                const uint32_t n63 = q + 1 < PF ? (uint32_t)__builtin_amdgcn_readlane((int)o[q + 1 < PF ? q + 1 : q], 0)
+                                                : nxt_pf;
+                const uint32_t nx = i0 + 64u < R.NR ? n63 : 0xffffffffu;
+                open = sum_step(a, i0, lo, hi, skip, tail, R, lane, o[q], f[q], r0[q], r1[q], r2[q], nx, st);
+                done = i0 >= R.NR || (i0 + 64u >= hi && !open);
+            }
+        }
+        // a tail Gaussian still open after the prefetched steps: one step at a time
+        for (uint32_t i0 = after; open && i0 < R.NR; i0 += 64u) {
+            const uint32_t e = i0 + (uint32_t)lane;
+            uint32_t oo = 0xffffffffu, n63 = 0xffffffffu;
+            bool ff = false;
+            float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0, q2 = q0;
+            if (e < R.NR) {
+                oo = inst_owner(a, e, R.E1);
+                ff = a.flag[e] != 0;
+                const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
+                q0 = r[0]; q1 = r[1]; q2 = r[2];
+                if (lane == 63 && e + 1 < R.NR) n63 = inst_owner(a, e + 1, R.E1);
+            }
+            open = sum_step(a, i0, lo, hi, skip, tail, R, lane, oo, ff, q0, q1, q2, n63, st);
+        }
+    }
+    if (lane == 0) a.live_cnt[ch] = st.nlive;
+}
+
+// Gaussians' view depth (the forward's depth key for rendered ones, 0 otherwise) and, when k_render_bwd did not
+// zero-fill the nine gradient outputs (not contiguous), their zero fill: one block per AUX_SPAN Gaussians.
+constexpr int AUX_SPAN = 1024;
 __device__ __forceinline__ void zero_slice(float* out, size_t first, size_t count) {
     float* p = out + first;
     size_t i = threadIdx.x;
@@ -410,15 +472,11 @@ __device__ __forceinline__ void zero_slice(float* out, size_t first, size_t coun
     }
     for (; i < count; i += 256) p[i] = 0.f;
 }
-
-__global__ void __launch_bounds__(256) k_gauss_prep(GaussBwdArgs a) {
-    __shared__ RecSumLDS s_rs;
-    __shared__ uint32_t s_wcnt[4];
-    const int base = blockIdx.x * 256;
-    const int idx = base + threadIdx.x;
-    const size_t nloc = (size_t)((a.P - base) < 256 ? (a.P - base) : 256);
-    const size_t b0 = (size_t)base, M = (size_t)a.M;
-    if (!a.outputs_zeroed) {  // else k_render_bwd zero-filled them (contiguous outputs)
+__device__ __forceinline__ void gauss_aux(const GaussBwdArgs& a, uint32_t blk) {
+    const size_t b0 = (size_t)blk * AUX_SPAN;
+    const size_t nloc = (size_t)a.P - b0 < (size_t)AUX_SPAN ? (size_t)a.P - b0 : (size_t)AUX_SPAN;
+    const size_t M = (size_t)a.M;
+    if (!a.outputs_zeroed) {
         zero_slice(a.dmeans2D, 3 * b0, 3 * nloc);
         zero_slice(a.dcolors, 3 * b0, 3 * nloc);
         zero_slice(a.dopacity, b0, nloc);
@@ -429,59 +487,63 @@ __global__ void __launch_bounds__(256) k_gauss_prep(GaussBwdArgs a) {
         zero_slice(a.dscales, 3 * b0, 3 * nloc);
         zero_slice(a.drot, 4 * b0, 4 * nloc);
     }
-    float acc[10];
-#ifdef DG_ABLATE_RECSUM  // timing experiment only: no records summed (every Gaussian takes the zero path)
-    for (int v = 0; v < 10; v++) acc[v] = 0.f;
-#else
-    record_sum(a, idx, s_rs, acc);
-#endif
-    bool live = false;
-    if (idx < a.P) {
+    for (size_t i = threadIdx.x; i < nloc; i += 256) {
+        const size_t idx = b0 + i;
         const uint32_t key = a.dkey[idx];
-        const int rad = a.radii[idx];
-        // depth: the view z of the forward (its depth key) for rendered Gaussians, 0 otherwise
-        a.depth[idx] = (rad > 0 && key != 0xffffffffu) ? __uint_as_float(key) : 0.f;
-#pragma unroll
-        for (int v = 0; v < 10; v++) live |= acc[v] != 0.0f;
-        live = live && rad > 0;
+        a.depth[idx] = (a.radii[idx] > 0 && key != 0xffffffffu) ? __uint_as_float(key) : 0.f;
     }
-    // block-local compaction of the contributing Gaussians, in index order (no atomics: one per block on a single
-    // address serializes across the XCDs)
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint64_t lm = __ballot(live);
-    if (lane == 0) s_wcnt[w] = (uint32_t)__popcll(lm);
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-#pragma unroll
-    for (int q = 0; q < 4; q++) { if (q < w) off += s_wcnt[q]; tot += s_wcnt[q]; }
-    if (live) {
-        const uint32_t j = (uint32_t)base + off + (uint32_t)__popcll(lm & (lane ? (~0ull >> (64 - lane)) : 0ull));
-        a.live_idx[j] = (uint32_t)idx;
-#pragma unroll
-        for (int v = 0; v < 10; v++) a.live_acc[(size_t)j * 10 + v] = acc[v];
-    }
-    if (threadIdx.x == 0) a.live_cnt[blockIdx.x] = tot;
 }
 
-// one block per LIVE_GROUP prep blocks (~25% of Gaussians contribute: about one Gaussian per lane), one lane per
-// compacted Gaussian of their lists
-constexpr int LIVE_GROUP = 4;
-__global__ void __launch_bounds__(256) k_gauss_live(GaussBwdArgs a, uint32_t nblocks) {
-    const uint32_t b0 = blockIdx.x * LIVE_GROUP;
-    uint32_t pre[LIVE_GROUP + 1];
-    pre[0] = 0;
+// blocks [0, sum_blocks): record-sum waves (grid-stride over the chunks: phase 2 may add chunks past the phase-1
+// capacity the grid is sized for); the rest: gauss_aux.  The zero fill must precede k_gauss_live (next launch).
+__global__ void __launch_bounds__(256) k_gauss_sum(GaussBwdArgs a, uint32_t sum_blocks) {
+#ifdef DG_SUM_NOAUX  // timing experiment only
+    if (blockIdx.x >= sum_blocks) return;
+#endif
+    if (blockIdx.x >= sum_blocks) {
+        gauss_aux(a, blockIdx.x - sum_blocks);
+        return;
+    }
+    const int lane = threadIdx.x & 63;
+    const SumRange R = sum_range(a);
+    const uint32_t nchunks = (R.NR + SUM_CHUNK - 1) / SUM_CHUNK;
+    for (uint32_t ch = blockIdx.x * 4 + (threadIdx.x >> 6); ch < nchunks; ch += sum_blocks * 4)
+        sum_chunk(a, ch, R, lane);
+}
+
+// LIVE_CHUNKS chunk lists per block (grid-stride), one lane per listed Gaussian (~7 per chunk on the bench scene).
+constexpr int LIVE_CHUNKS = 16;
+__global__ void __launch_bounds__(256) k_gauss_live(GaussBwdArgs a) {
+    __shared__ uint32_t s_pre[LIVE_CHUNKS + 1];
+    const SumRange R = sum_range(a);
+    const uint32_t nchunks = (R.NR + SUM_CHUNK - 1) / SUM_CHUNK;
+    for (uint32_t c0 = blockIdx.x * LIVE_CHUNKS; c0 < nchunks; c0 += gridDim.x * LIVE_CHUNKS) {
+        if (threadIdx.x < 64) {
+            const uint32_t t = threadIdx.x;
+            uint32_t incl = (t < (uint32_t)LIVE_CHUNKS && c0 + t < nchunks) ? a.live_cnt[c0 + t] : 0u;
 #pragma unroll
-    for (int k = 0; k < LIVE_GROUP; k++) pre[k + 1] = pre[k] + (b0 + k < nblocks ? a.live_cnt[b0 + k] : 0u);
-    for (uint32_t j = threadIdx.x; j < pre[LIVE_GROUP]; j += 256) {
-        uint32_t slot = 0;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if ((int)t >= o) incl += y;
+            }
+            if (t < (uint32_t)LIVE_CHUNKS) s_pre[t + 1] = incl;
+            if (t == 0) s_pre[0] = 0u;
+        }
+        __syncthreads();
+        const uint32_t tot = s_pre[LIVE_CHUNKS];
+        for (uint32_t j = threadIdx.x; j < tot; j += 256) {
+            int k = 0;
 #pragma unroll
-        for (int k = 0; k < LIVE_GROUP; k++)
-            if (j >= pre[k] && j < pre[k + 1]) slot = (b0 + k) * 256u + (j - pre[k]);
-        const uint32_t idx = a.live_idx[slot];
-        float acc[10];
-#pragma unroll
-        for (int v = 0; v < 10; v++) acc[v] = a.live_acc[(size_t)slot * 10 + v];
-        gauss_bwd_one(a, (int)idx, acc);
+            for (int st = LIVE_CHUNKS / 2; st > 0; st >>= 1)
+                if (s_pre[k + st] <= j) k += st;
+            const uint32_t e = a.live_list[(size_t)(c0 + k) * SUM_CHUNK + (j - s_pre[k])];
+            const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
+            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+            const float acc[10] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y};
+            const int idx = (int)__float_as_uint(r2.z);
+            if (a.radii[idx] > 0) gauss_bwd_one(a, idx, acc);
+        }
+        __syncthreads();
     }
 }
 
@@ -738,9 +800,13 @@ void launch_render_bwd(const RenderBwdArgs& a, uint32_t* counters, hipStream_t s
 }
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
-    const int blocks = (a.P + 255) / 256;
-    k_gauss_prep<<<blocks, 256, 0, s>>>(a);
-    k_gauss_live<<<(blocks + LIVE_GROUP - 1) / LIVE_GROUP, 256, 0, s>>>(a, (uint32_t)blocks);
+    // sized for the phase-1 capacity (E1 <= K1); phase-2 chunks are picked up by the grid-stride loops
+    const uint32_t chunks = (a.K1 + SUM_CHUNK - 1) / SUM_CHUNK;
+    const uint32_t sum_blocks = chunks ? (chunks + 3) / 4 : 1u;
+    const uint32_t aux_blocks = ((uint32_t)a.P + AUX_SPAN - 1) / AUX_SPAN;
+    k_gauss_sum<<<sum_blocks + aux_blocks, 256, 0, s>>>(a, sum_blocks);
+    const uint32_t live_blocks = chunks ? (chunks + LIVE_CHUNKS - 1) / LIVE_CHUNKS : 1u;
+    k_gauss_live<<<live_blocks, 256, 0, s>>>(a);
 }
 
 }  // namespace gs

@@ -15,7 +15,7 @@ from pmc_summary import avg, load_counters  # noqa: E402
 # gated phase-2 path under the same name are left out)
 PHASE_KERNEL = {
     "preprocess": ["k_preprocess"], "emit": ["k_bin_count<1>", "k_bin_emit<1>"], "render_fwd": ["k_render_fwd<1>"],
-    "render_bwd": ["k_bwd_prologue", "k_render_bwd"], "gauss_bwd": ["k_gauss_prep", "k_gauss_live"],
+    "render_bwd": ["k_bwd_prologue", "k_render_bwd"], "gauss_bwd": ["k_gauss_sum", "k_gauss_live"],
 }
 
 
