@@ -57,6 +57,13 @@ class DgDensifyArgs(C.Structure):
 ALLOC_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int, C.c_uint64)
 DG_BUF_GEOM, DG_BUF_BINNING, DG_BUF_IMAGE, DG_BUF_BACKWARD, DG_BUF_TEMP, DG_BUF_BINNING2, DG_BUF_DENSIFY, \
     DG_BUF_DENSIFY2 = range(8)
+DG_BUF_MEMBERS = 8
+DG_MAX_BOXES = 64
+
+
+class DgBox2dSet(C.Structure):
+    _fields_ = [("C", C.c_uint32), ("has_T", C.c_int), ("T", C.c_double * 6),
+                ("box", (C.c_double * 4) * DG_MAX_BOXES)]
 
 EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count", "dg_mark_visible", "dg_rasterize_filter",
            "dg_adam_update", "dg_fused_ssim_forward", "dg_fused_ssim_backward", "dg_dist_cuda2",
@@ -65,7 +72,7 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count"
            "dg_profile_enable", "dg_profile_collect", "dg_binned_instances", "dg_adam_update_groups",
            "dg_add_densification_stats", "dg_densify_select", "dg_densify_split_stds", "dg_densify_count",
            "dg_densify_gather", "dg_splat_pack", "dg_ply_pack", "dg_ring_create", "dg_ring_submit", "dg_ring_next",
-           "dg_ring_upload", "dg_ring_pending", "dg_ring_destroy", "dg_image_u8_to_chw",
+           "dg_ring_upload", "dg_ring_pending", "dg_ring_destroy", "dg_image_u8_to_chw", "dg_points_in_boxes2d",
            "dg_last_error", "dg_version")
 
 _lib = None
@@ -151,6 +158,10 @@ def load(path: str | None = None):
             L.dg_splat_pack.argtypes = [C.c_uint32, vp, vp, vp, vp, vp, vp, ALLOC_FN, vp, vp]
             L.dg_ply_pack.restype = C.c_int
             L.dg_ply_pack.argtypes = [C.c_uint32, vp, vp, vp, vp]
+        if hasattr(L, "dg_points_in_boxes2d"):
+            L.dg_points_in_boxes2d.restype = C.c_int
+            L.dg_points_in_boxes2d.argtypes = [C.c_uint32, vp, C.c_uint32, C.POINTER(DgBox2dSet), vp, vp,
+                                               C.POINTER(C.c_uint32), C.c_int, ALLOC_FN, vp, vp]
         if hasattr(L, "dg_ring_create"):
             ip = C.POINTER(C.c_int)
             L.dg_ring_create.restype = vp

@@ -12,6 +12,7 @@
 
 #include "../../include/dogs_hip.h"
 #include "aux_kernels.h"
+#include "blocksplit.h"
 #include "optim.h"
 #include "export.h"
 #include "raster.h"
@@ -906,6 +907,54 @@ int dg_ply_pack(uint32_t N, const float* xyz, const float* f_dc, uint8_t* out, d
     if (N == 0) return 0;
     if (!xyz || !f_dc || !out) return fail("ply pack: NULL tensor%s%d");
     gs::launch_ply_pack(N, xyz, f_dc, out, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_points_in_boxes2d(uint32_t N, const double* points, uint32_t stride, const dg_box2d_set* boxes,
+                         uint8_t* labels, double* transformed, uint32_t* counts, int want_members, dg_alloc_fn alloc,
+                         void* user, dg_stream_t stream) {
+    static_assert(DG_MAX_BOXES == gs::BOX_MAX, "box capacity");
+    if (!boxes || boxes->C == 0 || boxes->C > DG_MAX_BOXES) return fail("points_in_boxes2d: 1..%s%d boxes", "", DG_MAX_BOXES);
+    if (!counts) return fail("points_in_boxes2d: NULL counts%s%d");
+    const uint32_t C = boxes->C;
+    for (uint32_t k = 0; k < C; k++) counts[k] = 0;
+    if (N == 0) return 0;
+    if (!points || stride < 2) return fail("points_in_boxes2d: NULL points or stride < 2%s%d");
+    if (!alloc) return fail("points_in_boxes2d: NULL allocator%s%d");
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t nb = gs::box_blocks(N);
+    Carver c(nullptr);
+    c.take<uint64_t>(N); c.take<uint32_t>((size_t)C * nb); c.take<uint32_t>(C);
+    void* base = alloc(user, DG_BUF_TEMP, c.off);
+    if (!base) return fail("points_in_boxes2d scratch allocation failed%s%d");
+    Carver d(base);
+    uint64_t* masks = d.take<uint64_t>(N);
+    uint32_t* cnt = d.take<uint32_t>((size_t)C * nb);
+    uint32_t* total = d.take<uint32_t>(C);
+    gs::BoxSet bs;
+    bs.C = C;
+    bs.has_T = boxes->has_T;
+    for (int q = 0; q < 6; q++) bs.T[q] = boxes->T[q];
+    for (uint32_t k = 0; k < gs::BOX_MAX; k++)
+        for (int q = 0; q < 4; q++) bs.box[k][q] = k < C ? boxes->box[k][q] : 0.0;
+    gs::launch_box_test(N, points, stride, bs, labels, transformed, masks, cnt, s);
+    gs::launch_box_scan(N, C, cnt, total, s);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(counts, total, C * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (!want_members) return 0;
+    gs::BoxOffsets off;
+    off.C = C;
+    uint64_t run = 0;
+    for (uint32_t k = 0; k < gs::BOX_MAX; k++) {
+        off.first[k] = (uint32_t)run;
+        if (k < C) run += counts[k];
+    }
+    if (run > 0xffffffffull) return fail("points_in_boxes2d: %s%d members exceed 2^32", "", 0);
+    uint32_t* members = (uint32_t*)alloc(user, DG_BUF_MEMBERS, run * sizeof(uint32_t));
+    if (!members) return fail("points_in_boxes2d member allocation failed%s%d");
+    gs::launch_box_scatter(N, masks, cnt, off, members, s);
     HIP_OK(hipGetLastError());
     return 0;
 }

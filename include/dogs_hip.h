@@ -251,6 +251,28 @@ int dg_debug_geometry(const void* geom, int P, float* means2D, float* conic_opac
 int dg_debug_image_state(const void* image, int W, int H, float* final_T, uint32_t* n_contrib,
                          uint32_t* max_contrib, uint32_t* ranges, dg_stream_t stream);
 
+/* ---- Grid2D block split (load_colmap.py:98-177, cluster.py:73-199) ---- */
+
+/* Axis-aligned 2D boxes [A0, A1, B0, B1] tested in an optional planar frame x' = (T0 x + T1 y) + T2,
+ * y' = (T3 x + T4 y) + T5 (trimesh.transform_points of a 3x3 world-to-OBB matrix, rows 0-1). */
+#define DG_MAX_BOXES 64
+typedef struct {
+    uint32_t C;                      /* number of boxes, 1..DG_MAX_BOXES */
+    int has_T;                       /* 0: points are tested as given */
+    double T[6];
+    double box[DG_MAX_BOXES][4];
+} dg_box2d_set;
+enum { DG_BUF_MEMBERS = 8 };
+/* points_in_bbox2D (conerf/datasets/utils.py:186-206) for every box at once, plus Grid2DClustering's labels
+ * (cluster.py:173-178: label = the LAST box containing the point, 0 when none).  points: device f64, point i at
+ * points[i * stride], points[i * stride + 1].  Optional outputs (NULL = skip): labels u8 [N], transformed f64 [N,2]
+ * (the points in the box frame).  counts: host u32 [C], points per box (synchronises once).  When want_members, the
+ * concatenated ascending member indices of box 0, 1, ... (u32, counts[k] each) are written to a DG_BUF_MEMBERS
+ * buffer.  Allocates DG_BUF_TEMP. */
+int dg_points_in_boxes2d(uint32_t N, const double* points, uint32_t stride, const dg_box2d_set* boxes,
+                         uint8_t* labels, double* transformed, uint32_t* counts, int want_members, dg_alloc_fn alloc,
+                         void* user, dg_stream_t stream);
+
 /* Device primitives used by the rasterizer, exported for tests: stable LSD radix sort of (key, value)
  * pairs over bits [begin_bit, end_bit) in place, and an exclusive scan (total -> *total, device). */
 int dg_sort_pairs_u32(uint32_t* keys, uint32_t* vals, uint32_t n, int begin_bit, int end_bit, dg_alloc_fn alloc,
