@@ -134,7 +134,9 @@ class TrainStep:
     def __init__(self, s, dev, seed):
         from dogs_amd.diff_gaussian_rasterization import (GaussianRasterizationSettings, GaussianRasterizer,
                                                           SparseGaussianAdam)
+        from dogs_amd.activations import activate
         from dogs_amd.fused_ssim import fused_ssim
+        self.activate = activate
         self.fused_ssim = fused_ssim
         self.s = s
         c = s.camera
@@ -162,9 +164,10 @@ class TrainStep:
     def step(self):
         p = self.params
         m2d = torch.zeros_like(p["xyz"], requires_grad=True)
-        img, radii, _ = self.rast(means3D=p["xyz"], means2D=m2d, opacities=torch.sigmoid(p["opacity"]),
-                                  dc=p["f_dc"], shs=p["f_rest"], scales=torch.exp(p["scaling"]),
-                                  rotations=torch.nn.functional.normalize(p["quaternion"]))
+        # get_opacity / get_scaling / get_quaternion (sigmoid, exp, normalize) fused in one launch each way
+        opac, scales, rots = self.activate(p["opacity"], p["scaling"], p["quaternion"])
+        img, radii, _ = self.rast(means3D=p["xyz"], means2D=m2d, opacities=opac, dc=p["f_dc"], shs=p["f_rest"],
+                                  scales=scales, rotations=rots)
         img = img.clamp(0, 1)
         l1 = (img - self.gt).abs().mean()
         ssim = self.fused_ssim(img.unsqueeze(0), self.gt.unsqueeze(0))

@@ -880,6 +880,33 @@ int dg_densify_gather(const dg_densify_args* a, dg_stream_t stream) {
     return 0;
 }
 
+int dg_activate_forward(uint32_t N, const float* raw_opacity, const float* raw_scaling, const float* raw_rotation,
+                        float* opacity, float* scaling, float* rotation, dg_stream_t stream) {
+    if (N == 0) return 0;
+    if (!raw_opacity || !raw_scaling || !raw_rotation || !opacity || !scaling || !rotation)
+        return fail("activate: NULL tensor%s%d");
+    if ((reinterpret_cast<uintptr_t>(raw_rotation) | reinterpret_cast<uintptr_t>(rotation)) & 15u)
+        return fail("activate: rotation rows must be 16-byte aligned%s%d");
+    gs::launch_activate_fwd(N, raw_opacity, raw_scaling, raw_rotation, opacity, scaling, rotation, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_activate_backward(uint32_t N, const float* opacity, const float* scaling, const float* raw_rotation,
+                         const float* d_opacity, const float* d_scaling, const float* d_rotation, float* d_raw_opacity,
+                         float* d_raw_scaling, float* d_raw_rotation, dg_stream_t stream) {
+    if (N == 0) return 0;
+    if (!opacity || !scaling || !raw_rotation || !d_raw_opacity || !d_raw_scaling || !d_raw_rotation)
+        return fail("activate backward: NULL tensor%s%d");
+    if ((reinterpret_cast<uintptr_t>(raw_rotation) | reinterpret_cast<uintptr_t>(d_raw_rotation) |
+         reinterpret_cast<uintptr_t>(d_rotation)) & 15u)
+        return fail("activate backward: rotation rows must be 16-byte aligned%s%d");
+    gs::launch_activate_bwd(N, opacity, scaling, raw_rotation, d_opacity, d_scaling, d_rotation, d_raw_opacity,
+                            d_raw_scaling, d_raw_rotation, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
 int dg_splat_pack(uint32_t N, const float* xyz, const float* scaling, const float* opacity, const float* rotation,
                   const float* f_dc, uint8_t* out, dg_alloc_fn alloc, void* user, dg_stream_t stream) {
     if (N == 0) return 0;

@@ -37,6 +37,10 @@ struct AdamMultiArgs {
     float* denom;              // [N]
 };
 void launch_adam_multi(const AdamMultiArgs& a, hipStream_t s);
+void launch_activate_fwd(uint32_t N, const float* ro, const float* rs, const float* rq, float* o, float* sc, float* q,
+                         hipStream_t s);
+void launch_activate_bwd(uint32_t N, const float* o, const float* sc, const float* rq, const float* go,
+                         const float* gsc, const float* gq, float* dro, float* drs, float* drq, hipStream_t s);
 
 // ---- densify_and_prune
 struct DensifyArgs {

@@ -261,6 +261,53 @@ __global__ void __launch_bounds__(256) k_densify_gather(RebuildArgs a, const uin
     }
 }
 
+// Parameter activations of GaussianSplatModel (gaussian_splat_model.py get_opacity / get_scaling / get_quaternion:
+// sigmoid, exp, F.normalize(eps 1e-12)) and their backward, one thread per Gaussian, one launch each way (torch
+// runs ~4 kernels forward and ~8 backward for the three).
+__global__ void __launch_bounds__(256) k_activate_fwd(uint32_t N, const float* __restrict__ ro,
+                                                      const float* __restrict__ rs, const float* __restrict__ rq,
+                                                      float* __restrict__ o, float* __restrict__ sc,
+                                                      float* __restrict__ q) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= N) return;
+    o[i] = 1.0f / (1.0f + expf(-ro[i]));
+    for (int k = 0; k < 3; k++) sc[3 * (size_t)i + k] = expf(rs[3 * (size_t)i + k]);
+    const float4 x = reinterpret_cast<const float4*>(rq)[i];
+    const float d = fmaxf(sqrtf(((x.x * x.x + x.y * x.y) + x.z * x.z) + x.w * x.w), 1e-12f);
+    reinterpret_cast<float4*>(q)[i] = make_float4(x.x / d, x.y / d, x.z / d, x.w / d);
+}
+__global__ void __launch_bounds__(256) k_activate_bwd(uint32_t N, const float* __restrict__ o,
+                                                      const float* __restrict__ sc, const float* __restrict__ rq,
+                                                      const float* __restrict__ go, const float* __restrict__ gs_,
+                                                      const float* __restrict__ gq, float* __restrict__ dro,
+                                                      float* __restrict__ drs, float* __restrict__ drq) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= N) return;
+    if (go) {
+        const float v = o[i];
+        dro[i] = go[i] * (v * (1.0f - v));
+    } else {
+        dro[i] = 0.0f;
+    }
+    for (int k = 0; k < 3; k++) drs[3 * (size_t)i + k] = gs_ ? gs_[3 * (size_t)i + k] * sc[3 * (size_t)i + k] : 0.0f;
+    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (gq) {
+        const float4 x = reinterpret_cast<const float4*>(rq)[i];
+        const float4 g = reinterpret_cast<const float4*>(gq)[i];
+        const float n = sqrtf(((x.x * x.x + x.y * x.y) + x.z * x.z) + x.w * x.w);
+        if (n > 1e-12f) {  // d(x / n) = (g - y (y . g)) / n
+            const float inv = 1.0f / n;
+            const float4 y = make_float4(x.x * inv, x.y * inv, x.z * inv, x.w * inv);
+            const float yg = ((y.x * g.x + y.y * g.y) + y.z * g.z) + y.w * g.w;
+            r = make_float4((g.x - y.x * yg) * inv, (g.y - y.y * yg) * inv, (g.z - y.z * yg) * inv,
+                            (g.w - y.w * yg) * inv);
+        } else {          // clamped denominator: x / eps
+            r = make_float4(g.x / 1e-12f, g.y / 1e-12f, g.z / 1e-12f, g.w / 1e-12f);
+        }
+    }
+    reinterpret_cast<float4*>(drq)[i] = r;
+}
+
 }  // namespace
 
 void launch_adam_multi(const AdamMultiArgs& a0, hipStream_t s) {
@@ -299,6 +346,15 @@ void launch_densify_gather(const RebuildArgs& a, const uint32_t* keep_pos, hipSt
     }
     gg.start[6] = b;
     if (b) k_densify_gather<<<b, 256, 0, s>>>(a, keep_pos, gg);
+}
+
+void launch_activate_fwd(uint32_t N, const float* ro, const float* rs, const float* rq, float* o, float* sc, float* q,
+                         hipStream_t s) {
+    if (N) k_activate_fwd<<<(N + 255) / 256, 256, 0, s>>>(N, ro, rs, rq, o, sc, q);
+}
+void launch_activate_bwd(uint32_t N, const float* o, const float* sc, const float* rq, const float* go,
+                         const float* gsc, const float* gq, float* dro, float* drs, float* drq, hipStream_t s) {
+    if (N) k_activate_bwd<<<(N + 255) / 256, 256, 0, s>>>(N, o, sc, rq, go, gsc, gq, dro, drs, drq);
 }
 
 }  // namespace gs

@@ -128,6 +128,16 @@ typedef struct {
     float* denom;
 } dg_densify_stats;
 
+/* GaussianSplatModel activations (gaussian_splat_model.py get_opacity / get_scaling / get_quaternion): opacity =
+ * sigmoid(raw_opacity) [N,1], scaling = exp(raw_scaling) [N,3], rotation = raw_rotation / max(|raw_rotation|, 1e-12)
+ * [N,4] (16-B aligned rows), one launch; and the backward from the activated values and raw rotation (a NULL
+ * incoming gradient counts as zeros). */
+int dg_activate_forward(uint32_t N, const float* raw_opacity, const float* raw_scaling, const float* raw_rotation,
+                        float* opacity, float* scaling, float* rotation, dg_stream_t stream);
+int dg_activate_backward(uint32_t N, const float* opacity, const float* scaling, const float* raw_rotation,
+                         const float* d_opacity, const float* d_scaling, const float* d_rotation, float* d_raw_opacity,
+                         float* d_raw_scaling, float* d_raw_rotation, dg_stream_t stream);
+
 /* SparseGaussianAdam.step(visible, N) over up to 8 groups in one launch (each group as dg_adam_update), plus the
  * densification statistics of the same view when stats != NULL (they read nothing Adam writes). */
 int dg_adam_update_groups(const dg_adam_group* groups, int n_groups, const uint8_t* visible, uint32_t N, float b1,

@@ -1,0 +1,33 @@
+"""Fused parameter activations (dogs_amd.activations, optim.hip k_activate_*) against the plain PyTorch fp32 ops the
+reference's GaussianSplatModel uses (sigmoid, exp, F.normalize): values and gradients within 2e-6 relative
+(fp32 rounding of expf / the reciprocal norm; the tolerance is written below), zero-norm rotations included."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_activations_match_torch(hip_device):
+    from dogs_amd.activations import activate
+    g = torch.Generator().manual_seed(0)
+    n = 100_003
+    ro = (torch.randn(n, 1, generator=g) * 3).to(hip_device)
+    rs = (torch.randn(n, 3, generator=g) - 4).to(hip_device)
+    rq = torch.randn(n, 4, generator=g).to(hip_device)
+    rq[7] = 0.0                                                  # clamped denominator
+    a = [t.clone().requires_grad_(True) for t in (ro, rs, rq)]
+    b = [t.clone().requires_grad_(True) for t in (ro, rs, rq)]
+    o, s, q = activate(*a)
+    o2, s2, q2 = torch.sigmoid(b[0]), torch.exp(b[1]), torch.nn.functional.normalize(b[2])
+    for x, y in ((o, o2), (s, s2), (q, q2)):
+        torch.testing.assert_close(x, y, rtol=2e-6, atol=1e-7)
+    w = [torch.randn(t.shape, generator=g).to(hip_device) for t in (o, s, q)]
+    sum((x * y).sum() for x, y in zip((o, s, q), w)).backward()
+    sum((x * y).sum() for x, y in zip((o2, s2, q2), w)).backward()
+    for x, y in zip(a, b):
+        torch.testing.assert_close(x.grad, y.grad, rtol=2e-6, atol=1e-6 * float(y.grad.abs().max()))
+    # a missing incoming gradient counts as zeros
+    c = [t.clone().requires_grad_(True) for t in (ro, rs, rq)]
+    activate(*c)[1].sum().backward()
+    assert float(c[0].grad.abs().max()) == 0.0 and float(c[2].grad.abs().max()) == 0.0
+    torch.testing.assert_close(c[1].grad, torch.exp(rs), rtol=2e-6, atol=0)
