@@ -136,7 +136,9 @@ class TrainStep:
                                                           SparseGaussianAdam)
         from dogs_amd.activations import activate
         from dogs_amd.fused_ssim import fused_ssim
+        from dogs_amd.loss import clamp_l1
         self.activate = activate
+        self.clamp_l1 = clamp_l1
         self.fused_ssim = fused_ssim
         self.s = s
         c = s.camera
@@ -168,8 +170,7 @@ class TrainStep:
         opac, scales, rots = self.activate(p["opacity"], p["scaling"], p["quaternion"])
         img, radii, _ = self.rast(means3D=p["xyz"], means2D=m2d, opacities=opac, dc=p["f_dc"], shs=p["f_rest"],
                                   scales=scales, rotations=rots)
-        img = img.clamp(0, 1)
-        l1 = (img - self.gt).abs().mean()
+        img, l1 = self.clamp_l1(img, self.gt)  # render()'s clamp + the L1 term, one launch each way
         ssim = self.fused_ssim(img.unsqueeze(0), self.gt.unsqueeze(0))
         loss = 0.8 * l1 + 0.2 * (1.0 - ssim)
         loss.backward()

@@ -72,7 +72,8 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count"
            "dg_profile_enable", "dg_profile_collect", "dg_binned_instances", "dg_adam_update_groups",
            "dg_add_densification_stats", "dg_densify_select", "dg_densify_split_stds", "dg_densify_count",
            "dg_densify_gather", "dg_splat_pack", "dg_ply_pack", "dg_ring_create", "dg_ring_submit", "dg_ring_next",
-           "dg_ring_upload", "dg_ring_pending", "dg_ring_destroy", "dg_image_u8_to_chw", "dg_points_in_boxes2d", "dg_activate_forward", "dg_activate_backward",
+           "dg_ring_upload", "dg_ring_pending", "dg_ring_destroy", "dg_image_u8_to_chw", "dg_points_in_boxes2d", "dg_activate_forward", "dg_activate_backward", "dg_clamp_l1_blocks",
+           "dg_clamp_l1_forward", "dg_clamp_l1_backward",
            "dg_last_error", "dg_version")
 
 _lib = None
@@ -158,6 +159,13 @@ def load(path: str | None = None):
             L.dg_splat_pack.argtypes = [C.c_uint32, vp, vp, vp, vp, vp, vp, ALLOC_FN, vp, vp]
             L.dg_ply_pack.restype = C.c_int
             L.dg_ply_pack.argtypes = [C.c_uint32, vp, vp, vp, vp]
+        if hasattr(L, "dg_clamp_l1_forward"):
+            L.dg_clamp_l1_blocks.restype = C.c_uint32
+            L.dg_clamp_l1_blocks.argtypes = [C.c_uint32]
+            L.dg_clamp_l1_forward.restype = C.c_int
+            L.dg_clamp_l1_forward.argtypes = [C.c_uint32] + [vp] * 4 + [vp]
+            L.dg_clamp_l1_backward.restype = C.c_int
+            L.dg_clamp_l1_backward.argtypes = [C.c_uint32] + [vp] * 6 + [vp]
         if hasattr(L, "dg_activate_forward"):
             L.dg_activate_forward.restype = C.c_int
             L.dg_activate_forward.argtypes = [C.c_uint32] + [vp] * 6 + [vp]

@@ -880,6 +880,28 @@ int dg_densify_gather(const dg_densify_args* a, dg_stream_t stream) {
     return 0;
 }
 
+uint32_t dg_clamp_l1_blocks(uint32_t n) { return gs::clamp_l1_blocks(n); }
+
+int dg_clamp_l1_forward(uint32_t n, const float* img, const float* gt, float* clamped, float* partial,
+                        dg_stream_t stream) {
+    if (n == 0) return 0;
+    if (!img || !gt || !clamped || !partial) return fail("clamp_l1: NULL tensor%s%d");
+    if ((reinterpret_cast<uintptr_t>(img) | reinterpret_cast<uintptr_t>(gt) | reinterpret_cast<uintptr_t>(clamped)) & 15u)
+        return fail("clamp_l1: tensors must be 16-byte aligned%s%d");
+    gs::launch_clamp_l1_fwd(n, img, gt, clamped, partial, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_clamp_l1_backward(uint32_t n, const float* img, const float* clamped, const float* gt, const float* g_clamped,
+                         const float* g_l1, float* d_img, dg_stream_t stream) {
+    if (n == 0) return 0;
+    if (!img || !clamped || !gt || !d_img) return fail("clamp_l1 backward: NULL tensor%s%d");
+    gs::launch_clamp_l1_bwd(n, img, clamped, gt, g_clamped, g_l1, d_img, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
 int dg_activate_forward(uint32_t N, const float* raw_opacity, const float* raw_scaling, const float* raw_rotation,
                         float* opacity, float* scaling, float* rotation, dg_stream_t stream) {
     if (N == 0) return 0;

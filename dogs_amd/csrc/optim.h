@@ -37,6 +37,10 @@ struct AdamMultiArgs {
     float* denom;              // [N]
 };
 void launch_adam_multi(const AdamMultiArgs& a, hipStream_t s);
+uint32_t clamp_l1_blocks(uint32_t n);
+void launch_clamp_l1_fwd(uint32_t n, const float* img, const float* gt, float* out, float* partial, hipStream_t s);
+void launch_clamp_l1_bwd(uint32_t n, const float* img, const float* clamped, const float* gt, const float* g_img,
+                         const float* g_l1, float* d_img, hipStream_t s);
 void launch_activate_fwd(uint32_t N, const float* ro, const float* rs, const float* rq, float* o, float* sc, float* q,
                          hipStream_t s);
 void launch_activate_bwd(uint32_t N, const float* o, const float* sc, const float* rq, const float* go,

@@ -308,6 +308,53 @@ __global__ void __launch_bounds__(256) k_activate_bwd(uint32_t N, const float* _
     reinterpret_cast<float4*>(drq)[i] = r;
 }
 
+// The photometric L1 term of a training view (gaussian_trainer.py: image = render(...).clamp(0, 1), l1_loss =
+// |image - gt|.mean()): the clamped image and per-block partial sums of |image - gt| in one pass (the caller sums
+// the partials, a fixed order); backward d_img = (g_image + g_l1 sgn(image - gt) / n) [0 <= img <= 1] in one pass
+// -- torch runs four kernels forward and five backward for it.
+constexpr int L1_PER_THREAD = 16;  // 4 float4 per thread, 4096 floats per block
+__global__ void __launch_bounds__(256) k_clamp_l1_fwd(uint32_t n, const float* __restrict__ img,
+                                                      const float* __restrict__ gt, float* __restrict__ out,
+                                                      float* __restrict__ partial) {
+    __shared__ float s_w[4];
+    const size_t base = (size_t)blockIdx.x * 256u * L1_PER_THREAD;
+    float acc = 0.0f;
+#pragma unroll
+    for (int r = 0; r < L1_PER_THREAD / 4; r++) {
+        const size_t i = base + ((size_t)r * 256u + threadIdx.x) * 4u;
+        if (i + 3 < n) {
+            const float4 x = *reinterpret_cast<const float4*>(img + i);
+            const float4 g = *reinterpret_cast<const float4*>(gt + i);
+            const float4 c = make_float4(fminf(fmaxf(x.x, 0.f), 1.f), fminf(fmaxf(x.y, 0.f), 1.f),
+                                         fminf(fmaxf(x.z, 0.f), 1.f), fminf(fmaxf(x.w, 0.f), 1.f));
+            *reinterpret_cast<float4*>(out + i) = c;
+            acc += (fabsf(c.x - g.x) + fabsf(c.y - g.y)) + (fabsf(c.z - g.z) + fabsf(c.w - g.w));
+        } else {
+            for (size_t j = i; j < n && j < i + 4; j++) {
+                const float c = fminf(fmaxf(img[j], 0.f), 1.f);
+                out[j] = c;
+                acc += fabsf(c - gt[j]);
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[blockIdx.x] = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);
+}
+__global__ void __launch_bounds__(256) k_clamp_l1_bwd(uint32_t n, const float* __restrict__ img,
+                                                      const float* __restrict__ clamped, const float* __restrict__ gt,
+                                                      const float* __restrict__ g_img, const float* __restrict__ g_l1,
+                                                      float* __restrict__ d_img) {
+    const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const float s = g_l1 ? g_l1[0] / (float)n : 0.0f;
+    const float x = img[i], d = clamped[i] - gt[i];
+    const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+    const float g = (g_img ? g_img[i] : 0.f) + s * sg;
+    d_img[i] = (x >= 0.f && x <= 1.f) ? g : 0.f;
+}
+
 }  // namespace
 
 void launch_adam_multi(const AdamMultiArgs& a0, hipStream_t s) {
@@ -355,6 +402,15 @@ void launch_activate_fwd(uint32_t N, const float* ro, const float* rs, const flo
 void launch_activate_bwd(uint32_t N, const float* o, const float* sc, const float* rq, const float* go,
                          const float* gsc, const float* gq, float* dro, float* drs, float* drq, hipStream_t s) {
     if (N) k_activate_bwd<<<(N + 255) / 256, 256, 0, s>>>(N, o, sc, rq, go, gsc, gq, dro, drs, drq);
+}
+
+uint32_t clamp_l1_blocks(uint32_t n) { return (n + 256u * L1_PER_THREAD - 1) / (256u * L1_PER_THREAD); }
+void launch_clamp_l1_fwd(uint32_t n, const float* img, const float* gt, float* out, float* partial, hipStream_t s) {
+    if (n) k_clamp_l1_fwd<<<clamp_l1_blocks(n), 256, 0, s>>>(n, img, gt, out, partial);
+}
+void launch_clamp_l1_bwd(uint32_t n, const float* img, const float* clamped, const float* gt, const float* g_img,
+                         const float* g_l1, float* d_img, hipStream_t s) {
+    if (n) k_clamp_l1_bwd<<<(n + 255) / 256, 256, 0, s>>>(n, img, clamped, gt, g_img, g_l1, d_img);
 }
 
 }  // namespace gs

@@ -1,0 +1,46 @@
+"""The photometric L1 term of a training view in one launch each way: `rendered_image.clamp(0, 1)` (the end of
+render(), gaussian_render.py:149) and `l1_loss(image, gt)` = mean |image - gt| (gaussian_trainer.py's loss), through
+dg_clamp_l1_forward / dg_clamp_l1_backward (optim.hip k_clamp_l1_*).  The clamped image is returned too, so the
+SSIM term reads it and its gradient joins the L1 gradient and the clamp mask in the same backward pass."""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+class _ClampL1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, gt):
+        x, g = img.detach().contiguous(), gt.detach().contiguous()
+        _lib.require_device(x, "image")
+        if x.shape != g.shape or x.dtype != torch.float32 or g.dtype != torch.float32:
+            raise RuntimeError(f"clamp_l1: image {tuple(x.shape)} {x.dtype} vs gt {tuple(g.shape)} {g.dtype}")
+        n = x.numel()
+        L = _lib.load()
+        out = torch.empty_like(x)
+        partial = torch.empty(max(int(L.dg_clamp_l1_blocks(n)), 1), dtype=torch.float32, device=x.device)
+        with torch.cuda.device(x.device):
+            _lib.check(L.dg_clamp_l1_forward(n, x.data_ptr(), g.data_ptr(), out.data_ptr(), partial.data_ptr(),
+                                             _lib.stream_of(x.device)))
+        l1 = partial.sum() / n
+        ctx.save_for_backward(x, out, g)
+        return out, l1
+
+    @staticmethod
+    def backward(ctx, g_out, g_l1):
+        x, out, g = ctx.saved_tensors
+        d = torch.empty_like(x)
+        go = None if g_out is None else g_out.contiguous()
+        gl = None if g_l1 is None else g_l1.reshape(1).to(torch.float32).contiguous()
+        with torch.cuda.device(x.device):
+            _lib.check(_lib.load().dg_clamp_l1_backward(x.numel(), x.data_ptr(), out.data_ptr(), g.data_ptr(),
+                                                        None if go is None else go.data_ptr(),
+                                                        None if gl is None else gl.data_ptr(), d.data_ptr(),
+                                                        _lib.stream_of(x.device)))
+        return d, None
+
+
+def clamp_l1(image: torch.Tensor, gt: torch.Tensor):
+    """(image.clamp(0, 1), mean |image.clamp(0, 1) - gt|), both differentiable w.r.t. image."""
+    return _ClampL1.apply(image, gt)

@@ -128,6 +128,16 @@ typedef struct {
     float* denom;
 } dg_densify_stats;
 
+/* The view's photometric L1 term (gaussian_trainer.py: rendered_image.clamp(0, 1), l1_loss(image, gt) = mean |image -
+ * gt|): clamped [n] and per-block partial sums of |clamped - gt| (partial [dg_clamp_l1_blocks(n)]; the caller sums
+ * them and divides by n).  Backward: d_img = (g_clamped + *g_l1 * sgn(clamped - gt) / n) where 0 <= img <= 1, else 0
+ * (g_clamped, g_l1: device, NULL = zero).  img, gt, clamped 16-byte aligned. */
+uint32_t dg_clamp_l1_blocks(uint32_t n);
+int dg_clamp_l1_forward(uint32_t n, const float* img, const float* gt, float* clamped, float* partial,
+                        dg_stream_t stream);
+int dg_clamp_l1_backward(uint32_t n, const float* img, const float* clamped, const float* gt, const float* g_clamped,
+                         const float* g_l1, float* d_img, dg_stream_t stream);
+
 /* GaussianSplatModel activations (gaussian_splat_model.py get_opacity / get_scaling / get_quaternion): opacity =
  * sigmoid(raw_opacity) [N,1], scaling = exp(raw_scaling) [N,3], rotation = raw_rotation / max(|raw_rotation|, 1e-12)
  * [N,4] (16-B aligned rows), one launch; and the backward from the activated values and raw rotation (a NULL

@@ -31,3 +31,26 @@ def test_activations_match_torch(hip_device):
     activate(*c)[1].sum().backward()
     assert float(c[0].grad.abs().max()) == 0.0 and float(c[2].grad.abs().max()) == 0.0
     torch.testing.assert_close(c[1].grad, torch.exp(rs), rtol=2e-6, atol=0)
+
+
+def test_clamp_l1_matches_torch(hip_device):
+    """dogs_amd.loss.clamp_l1 vs img.clamp(0, 1) and (img - gt).abs().mean() in torch fp32: the clamped image is
+    exact; the mean within 1e-6 relative (different summation order); the gradient, with an SSIM-like upstream
+    gradient on the clamped image, within 1e-6 relative (exact zeros at clamp boundaries and ties)."""
+    from dogs_amd.loss import clamp_l1
+    g = torch.Generator().manual_seed(1)
+    for shape in ((3, 1080, 1920), (3, 17, 29)):
+        img = (torch.rand(shape, generator=g) * 1.4 - 0.2).to(hip_device)
+        gt = torch.rand(shape, generator=g).to(hip_device)
+        img.view(-1)[:5] = torch.tensor([0.0, 1.0, -0.0, 0.5, 2.0])
+        gt.view(-1)[3] = 0.5                                     # a tie: sgn 0
+        up = torch.randn(shape, generator=g).to(hip_device)
+        a, b = img.clone().requires_grad_(True), img.clone().requires_grad_(True)
+        c1, l1 = clamp_l1(a, gt)
+        c2 = b.clamp(0, 1)
+        l2 = (c2 - gt).abs().mean()
+        assert torch.equal(c1, c2)
+        torch.testing.assert_close(l1, l2, rtol=1e-6, atol=0)
+        (0.8 * l1 + (c1 * up).sum() * 1e-3).backward()
+        (0.8 * l2 + (c2 * up).sum() * 1e-3).backward()
+        torch.testing.assert_close(a.grad, b.grad, rtol=1e-6, atol=1e-12)
