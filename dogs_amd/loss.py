@@ -19,7 +19,9 @@ class _ClampL1(torch.autograd.Function):
         n = x.numel()
         L = _lib.load()
         out = torch.empty_like(x)
-        partial = torch.empty(max(int(L.dg_clamp_l1_blocks(n)), 1), dtype=torch.float32, device=x.device)
+        nb = int(L.dg_clamp_l1_blocks(n))
+        partial = (torch.empty(nb, dtype=torch.float32, device=x.device) if nb else
+                   torch.zeros(1, dtype=torch.float32, device=x.device))   # empty image: 0 / 0 = nan, as torch's mean
         with torch.cuda.device(x.device):
             _lib.check(L.dg_clamp_l1_forward(n, x.data_ptr(), g.data_ptr(), out.data_ptr(), partial.data_ptr(),
                                              _lib.stream_of(x.device)))
