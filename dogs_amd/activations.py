@@ -10,7 +10,9 @@ from . import _lib
 
 
 def _c(t: torch.Tensor) -> torch.Tensor:
-    return t.detach().contiguous()
+    """Contiguous and 16-B aligned (rotation rows are read as float4; a contiguous slice may start mid-row)."""
+    t = t.detach().contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
 
 
 class _Activate(torch.autograd.Function):

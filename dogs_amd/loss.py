@@ -12,7 +12,9 @@ from . import _lib
 class _ClampL1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, img, gt):
-        x, g = img.detach().contiguous(), gt.detach().contiguous()
+        # contiguous and 16-B aligned (a contiguous slice can start mid-vector): the kernel reads float4
+        x, g = (t.detach().contiguous() for t in (img, gt))
+        x, g = (t if t.data_ptr() % 16 == 0 else t.clone() for t in (x, g))
         _lib.require_device(x, "image")
         if x.shape != g.shape or x.dtype != torch.float32 or g.dtype != torch.float32:
             raise RuntimeError(f"clamp_l1: image {tuple(x.shape)} {x.dtype} vs gt {tuple(g.shape)} {g.dtype}")

@@ -26,6 +26,9 @@ def test_activations_match_torch(hip_device):
     sum((x * y).sum() for x, y in zip((o2, s2, q2), w)).backward()
     for x, y in zip(a, b):
         torch.testing.assert_close(x.grad, y.grad, rtol=2e-6, atol=1e-6 * float(y.grad.abs().max()))
+    # a contiguous slice that starts mid-row (not 16-B aligned) is accepted
+    o3, s3, q3 = activate(ro[1:], rs[1:], rq[1:])
+    torch.testing.assert_close(q3, torch.nn.functional.normalize(rq[1:]), rtol=2e-6, atol=1e-7)
     # a missing incoming gradient counts as zeros
     c = [t.clone().requires_grad_(True) for t in (ro, rs, rq)]
     activate(*c)[1].sum().backward()
@@ -54,3 +57,6 @@ def test_clamp_l1_matches_torch(hip_device):
         (0.8 * l1 + (c1 * up).sum() * 1e-3).backward()
         (0.8 * l2 + (c2 * up).sum() * 1e-3).backward()
         torch.testing.assert_close(a.grad, b.grad, rtol=1e-6, atol=1e-12)
+    flat = img.reshape(-1)[1:]                                   # misaligned start
+    torch.testing.assert_close(clamp_l1(flat, gt.reshape(-1)[1:])[1], (flat.clamp(0, 1) - gt.reshape(-1)[1:]).abs().mean(),
+                               rtol=1e-6, atol=0)
