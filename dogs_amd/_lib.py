@@ -73,7 +73,7 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count"
            "dg_add_densification_stats", "dg_densify_select", "dg_densify_split_stds", "dg_densify_count",
            "dg_densify_gather", "dg_splat_pack", "dg_ply_pack", "dg_ring_create", "dg_ring_submit", "dg_ring_next",
            "dg_ring_upload", "dg_ring_pending", "dg_ring_destroy", "dg_image_u8_to_chw", "dg_points_in_boxes2d", "dg_activate_forward", "dg_activate_backward", "dg_clamp_l1_blocks",
-           "dg_clamp_l1_forward", "dg_clamp_l1_backward",
+           "dg_clamp_l1_forward", "dg_clamp_l1_backward", "dg_adaptive_capacity",
            "dg_last_error", "dg_version")
 
 _lib = None
@@ -127,6 +127,9 @@ def load(path: str | None = None):
         if hasattr(L, "dg_binned_instances"):  # introspection only; absent in older builds used for A/B runs
             L.dg_binned_instances.restype = C.c_int
             L.dg_binned_instances.argtypes = [vp, C.c_int, i64p, vp]
+        if hasattr(L, "dg_adaptive_capacity"):
+            L.dg_adaptive_capacity.restype = C.c_int
+            L.dg_adaptive_capacity.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
         L.dg_debug_geometry.restype = C.c_int
         L.dg_debug_geometry.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp]
         L.dg_debug_image_state.restype = C.c_int
@@ -217,6 +220,17 @@ def require_device(t: torch.Tensor, name: str) -> None:
         raise RuntimeError(f"{name} must be a HIP (cuda) tensor: libdogs_hip has no CPU path")
 
 
+def require_f32_on(device: torch.device, **tensors: torch.Tensor) -> None:
+    """Every tensor float32 and on `device` (a HIP device): the kernels read raw fp32 device pointers, so a host,
+    foreign-device or other-dtype tensor would be read as garbage or fault instead of raising like torch's ops."""
+    for name, t in tensors.items():
+        require_device(t, name)
+        if t.device != device:
+            raise RuntimeError(f"{name} is on {t.device}, expected {device}")
+        if t.dtype != torch.float32:
+            raise RuntimeError(f"{name} must be float32, got {t.dtype}")
+
+
 def stream_of(device: torch.device):
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
@@ -240,6 +254,14 @@ class TensorArena:
 
     def get(self, which: int) -> torch.Tensor:
         return self.buffers.get(which, torch.empty(0, dtype=torch.uint8, device=self.device))
+
+
+def adaptive_capacity(W: int, H: int, reset: bool = False) -> int:
+    """The adaptive phase-1 capacity (tile-rect units per tile) of a W x H image on the current device; reset=True
+    first returns it to its cold default."""
+    v = C.c_int(0)
+    check(load().dg_adaptive_capacity(int(W), int(H), 1 if reset else 0, C.byref(v)))
+    return int(v.value)
 
 
 def profile_enable(on: bool = True) -> None:

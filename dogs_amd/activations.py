@@ -18,8 +18,10 @@ def _c(t: torch.Tensor) -> torch.Tensor:
 class _Activate(torch.autograd.Function):
     @staticmethod
     def forward(ctx, raw_opacity, raw_scaling, raw_rotation):
+        _lib.require_device(raw_opacity, "raw_opacity")
+        _lib.require_f32_on(raw_opacity.device, raw_opacity=raw_opacity, raw_scaling=raw_scaling,
+                            raw_rotation=raw_rotation)
         ro, rs, rq = _c(raw_opacity), _c(raw_scaling), _c(raw_rotation)
-        _lib.require_device(ro, "raw_opacity")
         n = int(ro.shape[0])
         if rs.shape != (n, 3) or rq.shape != (n, 4) or ro.numel() != n:
             raise RuntimeError(f"activate: shapes {tuple(ro.shape)}, {tuple(rs.shape)}, {tuple(rq.shape)}")

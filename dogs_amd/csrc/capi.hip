@@ -9,6 +9,7 @@
 #include <vector>
 #include <map>
 #include <tuple>
+#include <mutex>
 
 #include "../../include/dogs_hip.h"
 #include "aux_kernels.h"
@@ -201,18 +202,39 @@ constexpr bool FUSED_SORT = false;
 constexpr bool FUSED_SORT = true;
 #endif
 
-// Pinned per-thread landing buffer + event for the forward's early counter read.
+// Pinned landing buffer + event for the forward's early counter read, one per calling thread while it lives: a
+// thread's slot goes back to a process-wide pool when the thread exits (ADMM worker and RPC threads come and go), so
+// the pinned buffers and events are bounded by the number of threads alive at once.
 struct HostCounters {
     uint32_t* buf = nullptr;
     hipEvent_t ev = nullptr;
 };
-HostCounters& host_counters() {
-    thread_local HostCounters h;
-    if (!h.buf) {
-        (void)hipHostMalloc((void**)&h.buf, 64 * sizeof(uint32_t), hipHostMallocDefault);
-        (void)hipEventCreateWithFlags(&h.ev, hipEventDisableTiming);
+std::mutex g_hc_mu;
+std::vector<HostCounters> g_hc_pool;
+struct HostCountersSlot {
+    HostCounters h;
+    ~HostCountersSlot() {
+        if (!h.buf) return;
+        std::lock_guard<std::mutex> lk(g_hc_mu);
+        g_hc_pool.push_back(h);
     }
-    return h;
+};
+HostCounters& host_counters() {
+    thread_local HostCountersSlot slot;
+    if (!slot.h.buf) {
+        {
+            std::lock_guard<std::mutex> lk(g_hc_mu);
+            if (!g_hc_pool.empty()) {
+                slot.h = g_hc_pool.back();
+                g_hc_pool.pop_back();
+            }
+        }
+        if (!slot.h.buf) {
+            (void)hipHostMalloc((void**)&slot.h.buf, 64 * sizeof(uint32_t), hipHostMallocDefault);
+            (void)hipEventCreateWithFlags(&slot.h.ev, hipEventDisableTiming);
+        }
+    }
+    return slot.h;
 }
 
 // Phase-1 binning capacity, in tile-rect area units (the depth cut bounds the precise instances by the rect areas):
@@ -237,15 +259,20 @@ int64_t clamp_cap(int64_t per, int T) {
 // extra copy, event or wait.  Grow-only: a capacity that was once needed stays, and a too-deep prefix costs only
 // proportionally more phase-1 work.  The capacity a view used travels to its backward as the num_instances token, so
 // later growth never desynchronises a forward/backward pair.
+// One state per (device, image size) for the whole process (not per thread), so the device probe is allocated once
+// per image size and shared by every thread that renders it.  Concurrent renders of one size may only lose or double a
+// growth signal (the capacity a view used always travels with that view), never affect results.
 struct AdaptiveCap {
     int per_tile = DEFAULT_PREFIX_PER_TILE;
     uint32_t* probe = nullptr;  // device
 };
+std::mutex g_cap_mu;
 AdaptiveCap* adaptive_cap(const dg_raster_args* a) {
     if (a->prefix_per_tile != 0) return nullptr;
     int dev = 0;
     (void)hipGetDevice(&dev);
-    thread_local std::map<std::tuple<int, int, int>, AdaptiveCap> caps;
+    static std::map<std::tuple<int, int, int>, AdaptiveCap> caps;  // node-based: entries never move
+    std::lock_guard<std::mutex> lk(g_cap_mu);
     AdaptiveCap& c = caps[std::make_tuple(dev, a->W, a->H)];
     if (!c.probe) {
         if (hipMalloc((void**)&c.probe, sizeof(uint32_t)) != hipSuccess) { c.probe = nullptr; return nullptr; }
@@ -255,10 +282,14 @@ AdaptiveCap* adaptive_cap(const dg_raster_args* a) {
 }
 int64_t phase1_cap(const dg_raster_args* a, int T, AdaptiveCap* ac) {
     if (a->prefix_per_tile > 0) return clamp_cap(a->prefix_per_tile, T);
-    return clamp_cap(ac ? ac->per_tile : DEFAULT_PREFIX_PER_TILE, T);
+    if (!ac) return clamp_cap(DEFAULT_PREFIX_PER_TILE, T);
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    return clamp_cap(ac->per_tile, T);
 }
 void adapt(AdaptiveCap* ac, uint32_t prev_unfinished) {
-    if (ac && prev_unfinished > 0u && ac->per_tile < MAX_PREFIX_PER_TILE)
+    if (!ac || prev_unfinished == 0u) return;
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    if (ac->per_tile < MAX_PREFIX_PER_TILE)
         ac->per_tile = ac->per_tile * 3 / 2 < MAX_PREFIX_PER_TILE ? ac->per_tile * 3 / 2 : MAX_PREFIX_PER_TILE;
 }
 
@@ -378,6 +409,21 @@ int dg_exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_
     return 0;
 }
 int dg_version(void) { return 1; }
+
+int dg_adaptive_capacity(int W, int H, int reset, int* per_tile_out) {
+    dg_raster_args a;
+    memset(&a, 0, sizeof(a));
+    a.W = W; a.H = H; a.prefix_per_tile = 0;
+    AdaptiveCap* ac = adaptive_cap(&a);
+    if (!ac) return fail("adaptive capacity probe allocation failed%s%d");
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    if (reset) {
+        ac->per_tile = DEFAULT_PREFIX_PER_TILE;
+        HIP_OK(hipMemset(ac->probe, 0, sizeof(uint32_t)));
+    }
+    if (per_tile_out) *per_tile_out = ac->per_tile;
+    return 0;
+}
 
 uint64_t dg_geom_bytes(int P) { return carve_geom(nullptr, P).bytes; }
 uint64_t dg_image_bytes(int W, int H) { return carve_image(nullptr, W, H).bytes; }

@@ -313,6 +313,8 @@ __global__ void __launch_bounds__(256) k_activate_bwd(uint32_t N, const float* _
 // the partials, a fixed order); backward d_img = (g_image + g_l1 sgn(image - gt) / n) [0 <= img <= 1] in one pass
 // -- torch runs four kernels forward and five backward for it.
 constexpr int L1_PER_THREAD = 16;  // 4 float4 per thread, 4096 floats per block
+// torch.clamp(x, 0, 1) keeps NaN (fminf/fmaxf alone would turn it into 0 and hide a diverged render from the loss)
+__device__ __forceinline__ float clamp01(float x) { return x != x ? x : fminf(fmaxf(x, 0.f), 1.f); }
 __global__ void __launch_bounds__(256) k_clamp_l1_fwd(uint32_t n, const float* __restrict__ img,
                                                       const float* __restrict__ gt, float* __restrict__ out,
                                                       float* __restrict__ partial) {
@@ -325,13 +327,12 @@ __global__ void __launch_bounds__(256) k_clamp_l1_fwd(uint32_t n, const float* _
         if (i + 3 < n) {
             const float4 x = *reinterpret_cast<const float4*>(img + i);
             const float4 g = *reinterpret_cast<const float4*>(gt + i);
-            const float4 c = make_float4(fminf(fmaxf(x.x, 0.f), 1.f), fminf(fmaxf(x.y, 0.f), 1.f),
-                                         fminf(fmaxf(x.z, 0.f), 1.f), fminf(fmaxf(x.w, 0.f), 1.f));
+            const float4 c = make_float4(clamp01(x.x), clamp01(x.y), clamp01(x.z), clamp01(x.w));
             *reinterpret_cast<float4*>(out + i) = c;
             acc += (fabsf(c.x - g.x) + fabsf(c.y - g.y)) + (fabsf(c.z - g.z) + fabsf(c.w - g.w));
         } else {
             for (size_t j = i; j < n && j < i + 4; j++) {
-                const float c = fminf(fmaxf(img[j], 0.f), 1.f);
+                const float c = clamp01(img[j]);
                 out[j] = c;
                 acc += fabsf(c - gt[j]);
             }

@@ -12,12 +12,13 @@ from . import _lib
 class _ClampL1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, img, gt):
+        _lib.require_device(img, "image")
+        _lib.require_f32_on(img.device, image=img, gt=gt)
         # contiguous and 16-B aligned (a contiguous slice can start mid-vector): the kernel reads float4
         x, g = (t.detach().contiguous() for t in (img, gt))
         x, g = (t if t.data_ptr() % 16 == 0 else t.clone() for t in (x, g))
-        _lib.require_device(x, "image")
-        if x.shape != g.shape or x.dtype != torch.float32 or g.dtype != torch.float32:
-            raise RuntimeError(f"clamp_l1: image {tuple(x.shape)} {x.dtype} vs gt {tuple(g.shape)} {g.dtype}")
+        if x.shape != g.shape:
+            raise RuntimeError(f"clamp_l1: image {tuple(x.shape)} vs gt {tuple(g.shape)}")
         n = x.numel()
         L = _lib.load()
         out = torch.empty_like(x)

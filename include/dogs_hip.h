@@ -266,6 +266,10 @@ int dg_debug_sorted_instances(const dg_raster_args* a, const void* geom, const v
                               uint32_t* gauss_out, int64_t* e1, dg_stream_t stream);
 /* Instances actually binned by the last forward on this geometry block: phase 1 + phase 2 (synchronises). */
 int dg_binned_instances(const void* geom, int P, int64_t* binned, dg_stream_t stream);
+/* The adaptive phase-1 capacity (prefix_per_tile == 0) of image size W x H on the current device, in tile-rect
+ * units per tile (*per_tile_out, may be NULL); reset != 0 sets it back to its cold default first.  Tests and the
+ * bench use it to start a scene cold and to report what the views settled on. */
+int dg_adaptive_capacity(int W, int H, int reset, int* per_tile_out);
 int dg_debug_geometry(const void* geom, int P, float* means2D, float* conic_opacity, float* rgb_invdepth,
                       uint32_t* tile_count, dg_stream_t stream);
 int dg_debug_image_state(const void* image, int W, int H, float* final_T, uint32_t* n_contrib,

@@ -22,6 +22,12 @@
  *     (auxiliary.h:40-43).
  * The one non-reproducible op is exp() in compositing (GPU v_exp_f32 vs libm
  * expf); it is the only source of forward image differences.
+ *
+ * Threads (OpenMP, gso_set_threads): every parallel loop writes disjoint
+ * outputs, and every floating-point sum that crosses a parallel loop's items is
+ * re-done afterwards in the sequential order (per-instance backward records
+ * summed in sorted-instance order, the count-mode score as repeated adds), so
+ * the results are bit-identical for any thread count.
  */
 #include <math.h>
 #include <stdint.h>
@@ -29,6 +35,7 @@
 #include <string.h>
 #include <float.h>
 #include <limits.h>
+#include <omp.h>
 
 #define BLOCK_X 16
 #define BLOCK_Y 16
@@ -74,6 +81,10 @@ float gs_logf(float a) {
     float lm = s * p;
     return fmaf((float)e, 0.693147182f, lm);
 }
+
+/* threads of the parallel loops (OpenMP); <= 0 -> all cores.  Results do not depend on it. */
+void gso_set_threads(int n) { omp_set_num_threads(n > 0 ? n : omp_get_num_procs()); }
+int gso_get_threads(void) { return omp_get_max_threads(); }
 
 /* saturating float -> int, NaN -> 0 (GPU cvt semantics) */
 static inline int sat_f2i(float f) {
@@ -418,8 +429,11 @@ gso_ctx* gso_forward(const gso_params* prm, float* out_color, float* out_invdept
     c->ranges = calloc(2 * (size_t)(c->num_tiles ? c->num_tiles : 1), 4);
     c->bucket_offsets = calloc(c->num_tiles ? c->num_tiles : 1, 4);
 
+    int pre_err = 0;
+#pragma omp parallel for schedule(static) reduction(| : pre_err)
     for (int i = 0; i < P; i++)
-        if (preprocess_one(c, i) < 0) { *err = 1; gso_free(c); return NULL; }
+        if (preprocess_one(c, i) < 0) pre_err |= 1;
+    if (pre_err) { *err = 1; gso_free(c); return NULL; }
 
     /* inclusive scan of tiles_touched -> num_rendered (rect bound) */
     int64_t total = 0;
@@ -427,36 +441,74 @@ gso_ctx* gso_forward(const gso_params* prm, float* out_color, float* out_invdept
     c->num_rendered = total;
 
     /* duplicateWithKeys (rasterizer_impl.cu:120-190): only valid instances are kept;
-       the reference's invalid padding sorts after every valid key and is never read. */
-    kv_t* kv = (kv_t*)malloc(sizeof(kv_t) * (size_t)(total ? total : 1));
-    int64_t nv = 0;
-    for (int idx = 0; idx < P; idx++) {
-        if (!(c->radii[idx] > 0)) continue;
-        uint32_t rmin[2], rmax[2];
-        float mx = c->means2D[2 * idx], my = c->means2D[2 * idx + 1];
-        get_rect(mx, my, c->radii[idx], rmin, rmax, c->tiles_x, c->tiles_y);
-        v4 co = {c->conic_opacity[4 * idx], c->conic_opacity[4 * idx + 1], c->conic_opacity[4 * idx + 2],
-                 c->conic_opacity[4 * idx + 3]};
-        const float thr = gs_logf(co.w / (1.0f / 255.0f));
-        uint32_t dbits; memcpy(&dbits, &c->depths[idx], 4);
-        for (uint32_t y = rmin[1]; y < rmax[1]; y++)
-            for (uint32_t x = rmin[0]; x < rmax[0]; x++) {
-                float p = max_contrib_power_rect(co, mx, my, (float)(x * BLOCK_X), (float)(y * BLOCK_Y),
-                                                 (float)((x + 1) * BLOCK_X - 1), (float)((y + 1) * BLOCK_Y - 1));
-                if (p <= thr) {
-                    uint64_t key = (uint64_t)(y * c->tiles_x + x);
-                    key = (key << 32) | dbits;
-                    kv[nv].key = key; kv[nv].val = (uint32_t)idx; nv++;
+       the reference's invalid padding sorts after every valid key and is never read.
+       Two passes over the Gaussians (precise count, then emit at the scanned offsets) keep the sequential
+       emission order (Gaussian-major, tile rows then columns) whatever the thread count. */
+    uint32_t* vcount = (uint32_t*)calloc(Pn, 4);
+    int64_t* voff = (int64_t*)malloc(8 * (Pn + 1));
+    for (int pass = 0; pass < 2; pass++) {
+        if (pass == 1) {
+            voff[0] = 0;
+            for (int i = 0; i < P; i++) voff[i + 1] = voff[i] + vcount[i];
+        }
+#pragma omp parallel for schedule(dynamic, 256)
+        for (int idx = 0; idx < P; idx++) {
+            if (!(c->radii[idx] > 0)) continue;
+            uint32_t rmin[2], rmax[2];
+            float mx = c->means2D[2 * idx], my = c->means2D[2 * idx + 1];
+            get_rect(mx, my, c->radii[idx], rmin, rmax, c->tiles_x, c->tiles_y);
+            v4 co = {c->conic_opacity[4 * idx], c->conic_opacity[4 * idx + 1], c->conic_opacity[4 * idx + 2],
+                     c->conic_opacity[4 * idx + 3]};
+            const float thr = gs_logf(co.w / (1.0f / 255.0f));
+            uint32_t dbits; memcpy(&dbits, &c->depths[idx], 4);
+            int64_t o = pass ? voff[idx] : 0;
+            uint32_t cnt = 0;
+            for (uint32_t y = rmin[1]; y < rmax[1]; y++)
+                for (uint32_t x = rmin[0]; x < rmax[0]; x++) {
+                    float p = max_contrib_power_rect(co, mx, my, (float)(x * BLOCK_X), (float)(y * BLOCK_Y),
+                                                     (float)((x + 1) * BLOCK_X - 1), (float)((y + 1) * BLOCK_Y - 1));
+                    if (p <= thr) {
+                        if (pass) {
+                            uint64_t key = (uint64_t)(y * c->tiles_x + x);
+                            c->keys[o] = (key << 32) | dbits;
+                            c->vals[o] = (uint32_t)idx;
+                            o++;
+                        }
+                        cnt++;
+                    }
                 }
-            }
+            if (!pass) vcount[idx] = cnt;
+        }
+        if (pass == 0) {
+            int64_t t = 0;
+            for (int i = 0; i < P; i++) t += vcount[i];
+            c->keys = (uint64_t*)malloc(8 * (size_t)(t ? t : 1));
+            c->vals = (uint32_t*)malloc(4 * (size_t)(t ? t : 1));
+            c->num_valid = t;
+        }
     }
-    /* stable LSD sort == lexicographic (tile, depth bits, idx) order */
-    qsort(kv, (size_t)nv, sizeof(kv_t), kv_cmp);
-    c->num_valid = nv;
-    c->keys = (uint64_t*)malloc(8 * (size_t)(nv ? nv : 1));
-    c->vals = (uint32_t*)malloc(4 * (size_t)(nv ? nv : 1));
-    for (int64_t i = 0; i < nv; i++) { c->keys[i] = kv[i].key; c->vals[i] = kv[i].val; }
-    free(kv);
+    free(vcount); free(voff);
+    const int64_t nv = c->num_valid;
+    /* stable LSD sort == lexicographic (tile, depth bits, idx) order: a stable counting sort by tile
+       (emission order within a tile is ascending idx), then each tile's run sorted by (depth bits, idx) */
+    {
+        const int NT = c->num_tiles;
+        int64_t* tstart = (int64_t*)calloc((size_t)NT + 1, 8);
+        for (int64_t i = 0; i < nv; i++) tstart[(c->keys[i] >> 32) + 1]++;
+        for (int t = 0; t < NT; t++) tstart[t + 1] += tstart[t];
+        int64_t* fill = (int64_t*)malloc(8 * (size_t)(NT ? NT : 1));
+        memcpy(fill, tstart, 8 * (size_t)NT);
+        kv_t* kv = (kv_t*)malloc(sizeof(kv_t) * (size_t)(nv ? nv : 1));
+        for (int64_t i = 0; i < nv; i++) {
+            const int64_t d = fill[c->keys[i] >> 32]++;
+            kv[d].key = c->keys[i]; kv[d].val = c->vals[i];
+        }
+#pragma omp parallel for schedule(dynamic, 16)
+        for (int t = 0; t < NT; t++)
+            qsort(kv + tstart[t], (size_t)(tstart[t + 1] - tstart[t]), sizeof(kv_t), kv_cmp);
+        for (int64_t i = 0; i < nv; i++) { c->keys[i] = kv[i].key; c->vals[i] = kv[i].val; }
+        free(kv); free(fill); free(tstart);
+    }
     /* identifyTileRanges (rasterizer_impl.cu:195-220), valid keys only */
     for (int64_t i = 0; i < nv; i++) {
         uint32_t t = (uint32_t)(c->keys[i] >> 32);
@@ -476,11 +528,12 @@ gso_ctx* gso_forward(const gso_params* prm, float* out_color, float* out_invdept
     c->sard = (float*)malloc(4 * (size_t)BLOCK_SIZE * (size_t)(bsum ? bsum : 1));
     if (!c->sT || !c->sar || !c->sard) { *err = 2; gso_free(c); return NULL; }
 
-    /* renderCUDA (forward.cu:349-501): one tile at a time, pixels in thread-rank order */
+    /* renderCUDA (forward.cu:349-501): tiles in parallel, pixels of a tile in thread-rank order */
     const float* feat = prm->colors ? prm->colors : c->rgb;
-    for (int ty = 0; ty < c->tiles_y; ty++)
-        for (int tx = 0; tx < c->tiles_x; tx++) {
-            const int tile = ty * c->tiles_x + tx;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int tile = 0; tile < c->num_tiles; tile++) {
+        {
+            const int ty = tile / c->tiles_x, tx = tile % c->tiles_x;
             const uint32_t r0 = c->ranges[2 * tile], r1 = c->ranges[2 * tile + 1];
             const uint32_t n = r1 - r0;
             const uint32_t bbm0 = tile == 0 ? 0 : c->bucket_offsets[tile - 1];
@@ -514,8 +567,8 @@ gso_ctx* gso_forward(const gso_params* prm, float* out_color, float* out_invdept
                     ed = fmaf((1.f / c->depths[g]) * alpha, T, ed);
                     T = test_T;
                     last = contributor;
+#pragma omp atomic
                     c->gcount[g]++;            /* gaussian_count[collected_id[j]]++ */
-                    c->gscore[g] += co[3];     /* important_score[collected_id[j]] += con_o.w */
                 }
                 const size_t pid = (size_t)W * py + px;
                 c->final_T[pid] = T;
@@ -531,6 +584,16 @@ gso_ctx* gso_forward(const gso_params* prm, float* out_color, float* out_invdept
             }
             c->max_contrib[tile] = tile_max;
         }
+    }
+    /* important_score[g] += con_o.w once per contributing pixel: every term of the sum is the same float, so repeated
+       adds give the sequential (tile, pixel) order's result exactly */
+#pragma omp parallel for schedule(static)
+    for (int g = 0; g < P; g++) {
+        float sc = 0.0f;
+        const float o = c->conic_opacity[4 * g + 3];
+        for (int32_t k = 0; k < c->gcount[g]; k++) sc += o;
+        c->gscore[g] = sc;
+    }
     if (radii_out) memcpy(radii_out, c->radii, 4 * (size_t)P);
     return c;
 }
@@ -556,12 +619,17 @@ typedef struct {
 
 /* PerGaussianRenderCUDA (backward.cu:455-658): buckets of 32 splats, per-pixel state from the
    forward samples; lanes visit pixels in order so the per-splat sums run over pixels 0..255. */
-static void render_bwd(gso_ctx* c, const gso_grads* g) {
+static int render_bwd(gso_ctx* c, const gso_grads* g) {
     const gso_params* p = &c->p;
     const int W = p->W, H = p->H;
     const size_t HW = (size_t)W * H;
     const float* colors = p->colors ? p->colors : c->rgb;
     const float ddelx_dx = (float)(0.5 * W), ddely_dy = (float)(0.5 * H);
+    /* the 10 sums of each (tile, splat) instance; added into the per-Gaussian gradients below in the sequential
+       (tile, bucket, splat) order */
+    float* rec = (float*)malloc(sizeof(float) * 10 * (size_t)(c->num_valid ? c->num_valid : 1));
+    if (!rec) return 2;
+#pragma omp parallel for schedule(dynamic, 4)
     for (int tile = 0; tile < c->num_tiles; tile++) {
         const uint32_t r0 = c->ranges[2 * tile], r1 = c->ranges[2 * tile + 1];
         const int n = (int)(r1 - r0);
@@ -632,18 +700,30 @@ static void render_bwd(gso_ctx* c, const gso_grads* g) {
             for (int k = 0; k < 32; k++) {
                 const int sidx = b * 32 + k;
                 if (sidx >= n) break;
-                const uint32_t gi = c->vals[r0 + sidx];
-                g->dmeans2D[3 * gi + 0] += acc[k][0];
-                g->dmeans2D[3 * gi + 1] += acc[k][1];
-                g->dconic[4 * gi + 0] += acc[k][2];
-                g->dconic[4 * gi + 1] += acc[k][3];
-                g->dconic[4 * gi + 3] += acc[k][4];
-                g->dopacity[gi] += acc[k][5];
-                for (int ch = 0; ch < 3; ch++) g->dcolors[3 * gi + ch] += acc[k][6 + ch];
-                g->dinvdepth[gi] += acc[k][9];
+                memcpy(rec + 10 * ((size_t)r0 + sidx), acc[k], sizeof(acc[k]));
             }
         }
     }
+    for (int tile = 0; tile < c->num_tiles; tile++) {
+        const uint32_t r0 = c->ranges[2 * tile], r1 = c->ranges[2 * tile + 1];
+        /* the buckets the loop above visited: up to the first that starts at or past the tile's max contributor */
+        const uint32_t nbv = (c->max_contrib[tile] + 31) / 32;
+        const uint32_t end = r0 + (nbv * 32 < r1 - r0 ? nbv * 32 : r1 - r0);
+        for (uint32_t i = r0; i < end; i++) {
+            const uint32_t gi = c->vals[i];
+            const float* a = rec + 10 * (size_t)i;
+            g->dmeans2D[3 * gi + 0] += a[0];
+            g->dmeans2D[3 * gi + 1] += a[1];
+            g->dconic[4 * gi + 0] += a[2];
+            g->dconic[4 * gi + 1] += a[3];
+            g->dconic[4 * gi + 3] += a[4];
+            g->dopacity[gi] += a[5];
+            for (int ch = 0; ch < 3; ch++) g->dcolors[3 * gi + ch] += a[6 + ch];
+            g->dinvdepth[gi] += a[9];
+        }
+    }
+    free(rec);
+    return 0;
 }
 
 static inline float sq(float x) { return x * x; }
@@ -832,11 +912,13 @@ int gso_backward(gso_ctx* c, const float* dL_dpix, const float* dL_dinvdepth, fl
                  float* dsh, float* dscales, float* drot, float* depth) {
     gso_grads g = {dL_dpix, dL_dinvdepth, dmeans2D, dconic, dopacity, dcolors, dinvdepth, dmeans3D,
                    dcov3D, ddc, dsh, dscales, drot, depth};
-    render_bwd(c, &g);
+    if (render_bwd(c, &g)) return 2;
+#pragma omp parallel for schedule(static)
     for (int i = 0; i < c->p.P; i++) {
         if (!(c->radii[i] > 0)) continue;
         cov2d_bwd(c, &g, i);
     }
+#pragma omp parallel for schedule(static)
     for (int i = 0; i < c->p.P; i++) {
         if (!(c->radii[i] > 0)) continue;
         mean2d_bwd(c, &g, i);
@@ -927,6 +1009,7 @@ void gso_filter_radii(const gso_params* p, int* radii) {
 /* adamUpdateCUDA (adam.cu:10-38) */
 void gso_adam(float* param, const float* grad, float* m, float* v, const uint8_t* visible, float lr, float b1, float b2,
               float eps, uint32_t N, uint32_t M) {
+#pragma omp parallel for schedule(static)
     for (uint64_t i = 0; i < (uint64_t)N * M; i++) {
         if (!visible[i / M]) continue;
         float gr = grad[i];

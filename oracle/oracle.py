@@ -68,6 +68,8 @@ def lib():
         L.gso_filter_radii.argtypes = [C.POINTER(GsoParams), i32p]
         L.gso_adam.argtypes = [f32p, f32p, f32p, f32p, u8p, C.c_float, C.c_float, C.c_float, C.c_float,
                                C.c_uint32, C.c_uint32]
+        L.gso_set_threads.argtypes = [C.c_int]
+        L.gso_get_threads.restype = C.c_int
         L.gs_logf.restype = C.c_float
         L.gs_logf.argtypes = [C.c_float]
         L.aux_ssim_fwd.argtypes = [C.c_int] * 4 + [C.c_float, C.c_float] + [f32p] * 6
@@ -207,6 +209,18 @@ def forward(means3D, opacities, viewmatrix, projmatrix, campos, tanfovx, tanfovy
     num_tiles = ((W + 15) // 16) * ((H + 15) // 16)
     st = OracleForward(ctx, keep, P, M, W, H, num_tiles)
     return color, radii, invd, st
+
+
+def set_threads(n: int) -> int:
+    """Threads of the oracle's OpenMP loops (<= 0: all cores); returns the previous count.  Results are
+    bit-identical for any count (gs_oracle.c header)."""
+    old = int(lib().gso_get_threads())
+    lib().gso_set_threads(int(n))
+    return old
+
+
+def get_threads() -> int:
+    return int(lib().gso_get_threads())
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

@@ -112,3 +112,37 @@ def rel_err(a, b):
     b = np.asarray(b, np.float64)
     n = np.linalg.norm(b)
     return float(np.linalg.norm(a - b) / (n if n > 0 else 1.0))
+
+
+def yaw_view(s, yaw_deg, fx=1600.0):
+    """The scene seen by a camera at the origin rotated about +y by yaw_deg (dogs_amd.camera.yaw_world_to_camera):
+    the seeded view batches of SURVEY.md §8(d)."""
+    import dataclasses
+    import math
+    from dogs_amd.camera import make_camera, yaw_world_to_camera
+    c = s.camera
+    cam = make_camera(c.width, c.height, fx, fx, world_to_camera=yaw_world_to_camera(math.radians(yaw_deg)))
+    return dataclasses.replace(s, camera=cam)
+
+
+def check_binned_prefix(t_h, i_h, e1, t_o, i_o, ranges_o, max_contrib):
+    """Vectorised form of the per-tile prefix check: every tile's binned list (its phase-1 entries, then its phase-2
+    entries) equals the first entries of the reference's (tile, depth bits, index) list, and reaches the tile's last
+    contributor.  Returns (max binned list length, number of tiles with a phase-2 list)."""
+    t_h = np.asarray(t_h, np.int64)
+    i_h = np.asarray(i_h, np.int64)
+    order = np.argsort(t_h, kind="stable")          # phase-1 entries stay ahead of phase-2 ones within a tile
+    ts, gs = t_h[order], i_h[order]
+    first = np.searchsorted(ts, ts, side="left")
+    rank = np.arange(len(ts)) - first
+    r0 = ranges_o[:, 0].astype(np.int64)
+    rlen = (ranges_o[:, 1].astype(np.int64) - r0)
+    assert (rank < rlen[ts]).all(), "a tile's binned list is longer than the reference list"
+    bad = np.nonzero(np.asarray(i_o, np.int64)[r0[ts] + rank] != gs)[0]
+    assert len(bad) == 0, f"{len(bad)} binned entries differ from the reference order (first tile {ts[bad[0]]})"
+    T = len(ranges_o)
+    cnt = np.bincount(ts, minlength=T)
+    short = np.nonzero(np.asarray(max_contrib, np.int64) > cnt)[0]
+    assert len(short) == 0, f"tile {short[:5]}: max contributor beyond the binned list"
+    p2 = np.unique(t_h[e1:]) if len(t_h) > e1 else np.zeros(0)
+    return int(cnt.max()) if T else 0, int(len(p2))

@@ -29,11 +29,38 @@ def test_activations_match_torch(hip_device):
     # a contiguous slice that starts mid-row (not 16-B aligned) is accepted
     o3, s3, q3 = activate(ro[1:], rs[1:], rq[1:])
     torch.testing.assert_close(q3, torch.nn.functional.normalize(rq[1:]), rtol=2e-6, atol=1e-7)
+    # a truly misaligned [N,4] rotation view (rows start 4 B past a 16-B boundary): the float4 path gets a copy
+    mis = torch.empty(4 * n + 1, device=hip_device)[1:].view(n, 4).copy_(rq)
+    assert mis.data_ptr() % 16 != 0
+    mq = mis.detach().requires_grad_(True)
+    assert mq.data_ptr() % 16 != 0
+    rq_ref = rq.clone().requires_grad_(True)
+    q4 = activate(ro, rs, mq)[2]
+    q5 = torch.nn.functional.normalize(rq_ref)
+    torch.testing.assert_close(q4, q5, rtol=2e-6, atol=1e-7)
+    wq = torch.randn(q4.shape, generator=g).to(hip_device)
+    (q4 * wq).sum().backward()
+    (q5 * wq).sum().backward()
+    torch.testing.assert_close(mq.grad, rq_ref.grad, rtol=2e-6, atol=1e-6 * float(rq_ref.grad.abs().max()))
     # a missing incoming gradient counts as zeros
     c = [t.clone().requires_grad_(True) for t in (ro, rs, rq)]
     activate(*c)[1].sum().backward()
     assert float(c[0].grad.abs().max()) == 0.0 and float(c[2].grad.abs().max()) == 0.0
     torch.testing.assert_close(c[1].grad, torch.exp(rs), rtol=2e-6, atol=0)
+
+
+def test_activations_reject_foreign_tensors(hip_device):
+    """A host tensor or a float64 parameter raises like torch's own ops instead of handing the kernel a host pointer
+    or doubles read as floats."""
+    from dogs_amd.activations import activate
+    n = 16
+    ro, rs, rq = torch.zeros(n, 1, device=hip_device), torch.zeros(n, 3, device=hip_device), torch.ones(n, 4, device=hip_device)
+    with pytest.raises(RuntimeError):
+        activate(ro, rs.cpu(), rq)
+    with pytest.raises(RuntimeError):
+        activate(ro, rs, rq.double())
+    with pytest.raises(RuntimeError):
+        activate(ro.cpu(), rs, rq)
 
 
 def test_clamp_l1_matches_torch(hip_device):
@@ -57,6 +84,21 @@ def test_clamp_l1_matches_torch(hip_device):
         (0.8 * l1 + (c1 * up).sum() * 1e-3).backward()
         (0.8 * l2 + (c2 * up).sum() * 1e-3).backward()
         torch.testing.assert_close(a.grad, b.grad, rtol=1e-6, atol=1e-12)
+    # NaN propagates as in torch.clamp (a diverged render must not read as a finite loss); its gradient is 0
+    x = torch.tensor([[0.5, float("nan"), 1.5, -1.0, 0.25]], device=hip_device).expand(3, 5).contiguous()
+    y = torch.full_like(x, 0.5)
+    a = x.clone().requires_grad_(True)
+    c1, l1 = clamp_l1(a, y)
+    c2 = x.clamp(0, 1)
+    assert torch.equal(torch.isnan(c1), torch.isnan(c2)) and bool(torch.isnan(l1))
+    torch.testing.assert_close(c1[~torch.isnan(c1)], c2[~torch.isnan(c2)], rtol=0, atol=0)
+    (c1 * 1.0).sum().backward()
+    assert float(a.grad[0, 1]) == 0.0
+    # foreign tensors raise
+    with pytest.raises(RuntimeError):
+        clamp_l1(img, gt.cpu())
+    with pytest.raises(RuntimeError):
+        clamp_l1(img, gt.double())
     flat = img.reshape(-1)[1:]                                   # misaligned start
     torch.testing.assert_close(clamp_l1(flat, gt.reshape(-1)[1:])[1], (flat.clamp(0, 1) - gt.reshape(-1)[1:]).abs().mean(),
                                rtol=1e-6, atol=0)
