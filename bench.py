@@ -1,25 +1,34 @@
 """bench.py -- train views/sec (fwd+bwd raster) @1080p, 1e6 Gaussians; 1/2/4/8-GPU ADMM scaling.
 
-One step = one view per rank: _C.rasterize_gaussians + _C.rasterize_gaussians_backward on the synthetic
-1080p scene of BASELINE.md §2 (SH degree 3, AA off, fixed random dL/dcolor, zero dL/dinvdepth), inputs
-resident in HBM.  With N > 1 ranks (torch.distributed.run, one GPU each, RCCL) every rank trains its own
-scene block and the ADMM consensus all_reduce of the shared Gaussians runs every --consensus-interval
-steps and at least once inside the timed region.  value = views of all ranks / max-over-ranks time.
+One step = one view per rank: _C.rasterize_gaussians + _C.rasterize_gaussians_backward on the synthetic 1080p scene of
+BASELINE.md §2 / SURVEY.md §8(d) (SH degree 3, AA off, fixed random dL/dcolor, zero dL/dinvdepth), inputs resident in
+HBM.  The steps cycle through --views seeded yaw views (camera at the origin rotated about +y, yaw ~ U[-10, 10] deg
+from seed 1234, view 0 = yaw 0; SURVEY.md §8(d) "vary the camera yaw to build view batches").  With N > 1 ranks
+(torch.distributed.run, one GPU each, RCCL) every rank renders its own scene block and the ADMM consensus all_reduce
+of the shared Gaussians is added in its 1-per-200-iterations proportion.  value = views of all ranks / max-over-ranks
+time.
 
 Also reported on the same JSON line:
-  roofline      per-phase hipEvent timing of one extra profiled step; algorithmic bytes per phase from
-                SURVEY.md §8(d) (B_view = 856 N + 172 K + 64 HW); `traffic` from the committed rocprofv3
-                PMC summary of the same command when present (profiles/), else null
-  cpu_baseline  the CPU oracle (oracle/gs_oracle.c restating the reference kernels) on one view of the
-                same scene, rank 0 at N = 1 only
-  train_step    secondary figure: fwd + L1 + fused-SSIM fwd/bwd + bwd + densification stats + SparseGaussianAdam
-                (6 groups, one launch), and one densify_and_prune timed on the trained state
+  views         per view: yaw, num_rendered, the reference's precise instance count K (its full per-tile lists, one
+                untimed forward with depth-prefix binning off), this build's binned instances (phase 1 E1 + phase 2
+                E2), visible / binned / gradient-carrying Gaussians
+  roofline      the dominant kernel (most time per view, hipEvent-timed on the launch stream over one extra pass of
+                the views) credited with the algorithmic bytes of the work it performs (phase_bytes: binned
+                instances, not the reference's K); the view total over the same model (view_frac); the reference-
+                equivalent figure of SURVEY.md §8(d) (B_view = 856 N + 172 K + 64 HW, the reference's work) kept
+                apart; HBM `traffic` and a VALU-issue roofline of the render kernels from the committed rocprofv3 PMC
+                passes of the same command (profiles/pmc_traffic.json), when present
+  cpu_baseline  the CPU oracle (oracle/gs_oracle.c, the reference kernels restated; OpenMP, results identical for
+                any thread count) on the same views: all host threads of this job, and one core
+  train_step    secondary figure: activations + fwd + L1 + fused-SSIM fwd/bwd + bwd + densification statistics +
+                SparseGaussianAdam (6 groups, one launch) over the same views, and one densify_and_prune
+  admm          N > 1 (or --admm): the ADMM block trainer (dogs_amd.admm_trainer) run for --admm-iters local
+                iterations per rank with a consensus every --admm-interval, and its sequential single-GPU equivalent
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -32,29 +41,43 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "train views/sec (fwd+bwd raster) @1080p, 1e6 Gaussians; 1/2/4/8-GPU ADMM scaling"
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+SIMDS, CLOCK_GHZ = 1024, 2.4   # 256 CUs x 4 SIMDs; a wave64 VALU instruction issues over 2 cycles (SIMD-32)
+VALU_PEAK_GINST = SIMDS * CLOCK_GHZ / 2.0   # 1228.8 G wave-instructions/s
 
 
-def phase_bytes(phase: str, N: int, K: int, HW: int) -> float:
-    """Algorithmic bytes per launch of each phase (DESIGN.md 'Roofline'), with K the reference's
-    precise instance count (its full per-tile lists), whatever this build bins."""
+def phase_bytes(phase: str, v: dict) -> float:
+    """Algorithmic bytes of the work each phase performs on one view (DESIGN.md §3 "Roofline"):
+    N Gaussians, Vis visible (radii > 0), Gb binned (>= 1 instance), Gl gradient-carrying, E1/E2 phase-1/phase-2
+    instances (E = E1 + E2), HW pixels.  Per unit: preprocess reads means/scales/rotation/opacity (44 B) and writes the
+    32-B splat record, depth key, rect count, instance count and radius (48 B); the depth histogram reads key + count;
+    the binning walk reads the splat record twice (count, emit) and, for the SH colour, means + dc + rest (204 B) and
+    writes rgb/inv-depth (16 B) per binned Gaussian, and writes Gaussian, depth key and tile slot (12 B) per instance;
+    the render gathers 44 B per instance (id, xy, conic/opacity, rgb, depth) and its fused sort reads key + id and
+    writes the sorted id (12 B), and writes colour, inverse depth, T and last contributor (24 B/px); the replay
+    re-gathers 44 B and writes one 40-B record per instance and reads 40 B/px; the per-Gaussian backward reads the
+    records (40 B/instance), 236 B of parameters + radius + 40-B sums per gradient-carrying Gaussian, and writes every
+    output element once (288 B per Gaussian: the dense gradient tensors, zeros included -- the zero fill itself is
+    issued by the replay's waves, in the shadow of its VALU work)."""
+    N, HW = v["N"], v["HW"]
+    E1, E2 = v["e1"], v["e2"]
+    E = E1 + E2
+    Gb, Gl = v["binned_gaussians"], v["live_gaussians"]
     return {
-        "preprocess": 284.0 * N,            # 236 B params read + 48 B geometry written
-        "prefix_cut": 8.0 * N,              # depth histogram: key + count per Gaussian
-        "count_scan": 8.0 * N,
-        "tile_dsort": 0.0,                  # implementation overhead: per-tile depth order of the binned lists
-        "emit": 36.0 * N + 12.0 * K,
-        "tile_sort": 24.0 * K,
-        "ranges": 8.0 * K,
-        "render_fwd": 44.0 * K + 24.0 * HW,
-        "flag_clear": 0.0,
-        "render_bwd": 84.0 * K + 40.0 * HW,
-        "record_sum": 0.0,                  # implementation overhead (per-instance records -> sums)
-        "phase2_count": 0.0,                # depth-prefix binning, phase 2 (only when tiles were left unfinished)
-        "phase2_bin": 0.0,
-        "render_fwd2": 0.0,
-        "gauss_bwd": 528.0 * N,
+        "preprocess": 92.0 * N,
+        "prefix_cut": 8.0 * N,
+        "emit": (64.0 + 220.0) * Gb + 12.0 * E1,
+        "tile_bin": 0.0,
+        "render_fwd": 56.0 * E1 + 24.0 * HW,
+        "phase2": 68.0 * E2,
+        "render_bwd": 84.0 * E + 40.0 * HW,
+        "gauss_bwd": 40.0 * E + 280.0 * Gl + 288.0 * N,
     }.get(phase, 0.0)
+
+
+def reference_view_bytes(N: int, K: int, HW: int) -> float:
+    """the reference's algorithmic bytes per view (its full lists, K precise instances)."""
+    return 856.0 * N + 172.0 * K + 64.0 * HW
 
 
 def dist_env():
@@ -64,88 +87,92 @@ def dist_env():
     return ws, rank, local
 
 
-def make_inputs(n, W, H, seed, dev):
-    from dogs_amd.synthetic import make_scene
-    s = make_scene(n, W, H, seed=seed).to(dev)
-    g = torch.Generator().manual_seed(seed + 99)
-    grad_color = torch.randn((3, H, W), generator=g).to(dev)
-    grad_inv = torch.zeros((1, H, W), device=dev)
-    return s, grad_color, grad_inv
+def view_yaws(views: int, seed: int = 1234):
+    """Seeded yaw batch (degrees): view 0 looks down +z, the others yaw ~ U[-10, 10]."""
+    return [0.0] + [float(x) for x in np.random.default_rng(seed).uniform(-10.0, 10.0, max(views - 1, 0))]
 
 
-class View:
-    """One fwd+bwd raster step through the drop-in `_C` table."""
+def make_cameras(W, H, yaws, dev, fx=1600.0):
+    import math
+    from dogs_amd.camera import make_camera, yaw_world_to_camera
+    return [make_camera(W, H, fx, fx, world_to_camera=yaw_world_to_camera(math.radians(y))).to(dev) for y in yaws]
 
-    def __init__(self, s, grad_color, grad_inv, dev):
+
+class Views:
+    """One fwd+bwd raster step per call through the drop-in `_C` table, cycling through the view cameras."""
+
+    def __init__(self, s, cams, grad_color, grad_inv, dev):
         from dogs_amd.diff_gaussian_rasterization import _C
         self._C = _C
-        self.s, self.gc, self.gi, self.dev = s, grad_color, grad_inv, dev
-        self.c = s.camera
+        self.s, self.cams, self.gc, self.gi, self.dev = s, cams, grad_color, grad_inv, dev
         self.bg = torch.zeros(3, device=dev)
         self.e = torch.empty(0, device=dev)
-        self.last = None
+        self.i = 0
 
-    def forward(self):
-        s, c, e = self.s, self.c, self.e
+    def forward(self, c):
+        s, e = self.s, self.e
         return self._C.rasterize_gaussians(self.bg, s.means3D, e, s.opacities, s.scales, s.rotations, 1.0, e,
                                            c.world_to_camera, c.projective_matrix, c.tanfovx, c.tanfovy, c.height,
                                            c.width, s.dc, s.sh, 3, c.camera_center, False, False, False)
 
-    def reference_instances(self):
-        """The reference's precise instance count (its full per-tile lists): one untimed forward with
-        depth-prefix binning off.  The §8(d) byte formula is written in terms of it."""
-        old = self._C.set_prefix_per_tile(-1)
-        try:
-            self.last_out = self.forward()
-            return self.binned_instances()
-        finally:
-            self._C.set_prefix_per_tile(old)
+    def backward(self, c, out):
+        s, e = self.s, self.e
+        return self._C.rasterize_gaussians_backward(self.bg, s.means3D, out[4], e, s.opacities, s.scales, s.rotations,
+                                                    1.0, e, c.world_to_camera, c.projective_matrix, c.tanfovx,
+                                                    c.tanfovy, self.gc, s.dc, s.sh, self.gi, 3, c.camera_center,
+                                                    out[5], out[0], out[6], out[7], out[1], out[8], False, False)
 
     def step(self):
-        s, c, e = self.s, self.c, self.e
-        out = self._C.rasterize_gaussians(self.bg, s.means3D, e, s.opacities, s.scales, s.rotations, 1.0, e,
-                                          c.world_to_camera, c.projective_matrix, c.tanfovx, c.tanfovy, c.height,
-                                          c.width, s.dc, s.sh, 3, c.camera_center, False, False, False)
-        g = self._C.rasterize_gaussians_backward(self.bg, s.means3D, out[4], e, s.opacities, s.scales, s.rotations,
-                                                 1.0, e, c.world_to_camera, c.projective_matrix, c.tanfovx,
-                                                 c.tanfovy, self.gc, s.dc, s.sh, self.gi, 3, c.camera_center,
-                                                 out[5], out[0], out[6], out[7], out[1], out[8], False, False)
-        self.last = (out[0], out[1])
-        self.last_out = out
-        return out, g
+        c = self.cams[self.i % len(self.cams)]
+        self.i += 1
+        out = self.forward(c)
+        return out, self.backward(c, out)
 
-    def binned_instances(self):
-        import ctypes as C
+    def stats(self, k, reference_k=True):
+        """Untimed per-view figures: counters of a normal forward, the gradient-carrying Gaussians of its backward,
+        and the reference's precise instance count K (one forward with depth-prefix binning off)."""
         import dogs_amd._lib as L
-        v = C.c_int64(-1)
-        if not hasattr(L.load(), "dg_binned_instances"):
-            return -1
-        L.check(L.load().dg_binned_instances(self.last_out[5].data_ptr(), int(self.s.means3D.shape[0]), C.byref(v),
-                                             L.stream_of(self.dev)))
-        return int(v.value)
+        c = self.cams[k]
+        out = self.forward(c)
+        g = self.backward(c, out)
+        n = int(self.s.means3D.shape[0])
+        cnt = L.forward_counters(out[5], n)
+        tile_count = torch.empty(n, dtype=torch.int32, device=self.dev)
+        L.check(L.load().dg_debug_geometry(out[5].data_ptr(), n, None, None, None, tile_count.data_ptr(),
+                                           L.stream_of(self.dev)))
+        rec = {"num_rendered": int(out[0]), "e1": cnt["e1"], "e2": cnt["e2"],
+               "unfinished_tiles": cnt["unfinished_tiles"] if cnt["cut"] else 0,
+               "visible_gaussians": int((out[4] > 0).sum()), "binned_gaussians": int((tile_count > 0).sum()),
+               "live_gaussians": int((g[2].reshape(-1) != 0).sum())}
+        if not reference_k:
+            rec["K"] = -1
+            return rec
+        old = self._C.set_prefix_per_tile(-1)
+        try:
+            ref = self.forward(c)
+            rec["K"] = L.forward_counters(ref[5], n)["e1"]
+        finally:
+            self._C.set_prefix_per_tile(old)
+        return rec
 
 
 class TrainStep:
     """Training iteration of GaussianSplatTrainer.train_iteration (gaussian_trainer.py:324-513) before
     densify_end_iter, without the periodic densify_and_prune: activations, raster, L1 + fused-SSIM, backward, the
     view's densification statistics (:433-438) and SparseGaussianAdam.step(visible, N) -- the last two in one
-    launch.  densify() times one densify_and_prune (dogs_amd.densify) on the trained state."""
+    launch -- cycling through the view cameras.  densify() times one densify_and_prune (dogs_amd.densify)."""
 
-    def __init__(self, s, dev, seed):
+    def __init__(self, s, cams, dev, seed):
         from dogs_amd.diff_gaussian_rasterization import (GaussianRasterizationSettings, GaussianRasterizer,
                                                           SparseGaussianAdam)
         from dogs_amd.activations import activate
         from dogs_amd.fused_ssim import fused_ssim
         from dogs_amd.loss import clamp_l1
-        self.activate = activate
-        self.clamp_l1 = clamp_l1
-        self.fused_ssim = fused_ssim
-        self.s = s
-        c = s.camera
-        self.rs = GaussianRasterizationSettings(c.height, c.width, c.tanfovx, c.tanfovy, torch.zeros(3, device=dev),
-                                                1.0, c.world_to_camera, c.projective_matrix, 3, c.camera_center,
-                                                False, False, False, 0.0)
-        self.rast = GaussianRasterizer(self.rs)
+        self.activate, self.clamp_l1, self.fused_ssim = activate, clamp_l1, fused_ssim
+        self.rasts = [GaussianRasterizer(GaussianRasterizationSettings(
+            c.height, c.width, c.tanfovx, c.tanfovy, torch.zeros(3, device=dev), 1.0, c.world_to_camera,
+            c.projective_matrix, 3, c.camera_center, False, False, False, 0.0)) for c in cams]
+        self.i = 0
         self.params = {
             "xyz": s.means3D.clone().requires_grad_(True),
             "f_dc": s.dc.clone().requires_grad_(True),
@@ -157,6 +184,7 @@ class TrainStep:
         lrs = {"xyz": 1.6e-4, "f_dc": 2.5e-3, "f_rest": 1.25e-4, "scaling": 5e-3, "quaternion": 1e-3, "opacity": 2.5e-2}
         self.opt = SparseGaussianAdam([{"params": [p], "lr": lrs[k], "name": k} for k, p in self.params.items()],
                                       lr=0.0, eps=1e-15)
+        c = cams[0]
         g = torch.Generator().manual_seed(seed + 7)
         self.gt = torch.rand((3, c.height, c.width), generator=g).to(dev)
         N = s.means3D.shape[0]
@@ -165,11 +193,13 @@ class TrainStep:
 
     def step(self):
         p = self.params
+        rast = self.rasts[self.i % len(self.rasts)]
+        self.i += 1
         m2d = torch.zeros_like(p["xyz"], requires_grad=True)
         # get_opacity / get_scaling / get_quaternion (sigmoid, exp, normalize) fused in one launch each way
         opac, scales, rots = self.activate(p["opacity"], p["scaling"], p["quaternion"])
-        img, radii, _ = self.rast(means3D=p["xyz"], means2D=m2d, opacities=opac, dc=p["f_dc"], shs=p["f_rest"],
-                                  scales=scales, rotations=rots)
+        img, radii, _ = rast(means3D=p["xyz"], means2D=m2d, opacities=opac, dc=p["f_dc"], shs=p["f_rest"],
+                             scales=scales, rotations=rots)
         img, l1 = self.clamp_l1(img, self.gt)  # render()'s clamp + the L1 term, one launch each way
         ssim = self.fused_ssim(img.unsqueeze(0), self.gt.unsqueeze(0))
         loss = 0.8 * l1 + 0.2 * (1.0 - ssim)
@@ -195,54 +225,93 @@ class TrainStep:
         return (time.perf_counter() - t0) * 1e3, n_out
 
 
-def cpu_baseline(n, W, H, seed):
-    """Oracle fwd+bwd of one view of the same scene on this host (1 core): the reference has no CPU
-    rasterizer, so this is the CPU restatement of its kernels."""
+def host_threads() -> int:
+    """Threads this job may use on the host: OMP_NUM_THREADS when the launcher sets it (the GPU box grants a share of
+    a bigger machine), else the CPUs this process may run on."""
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    if n > 0:
+        return n
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(n, W, H, seed, yaws, budget_s=12.0):
+    """The CPU oracle (the reference's kernels restated in C; the reference has no CPU rasterizer) on
+    the same views, fwd+bwd: all host threads of this job, then one core.  Each leg runs whole views in the bench's
+    view order until its time budget is spent (at least one view)."""
     from oracle import oracle as O
     from dogs_amd.synthetic import make_scene
     O.build()
     s = make_scene(n, W, H, seed=seed)
-    c = s.camera
+    cams = make_cameras(W, H, yaws, torch.device("cpu"))
     g = torch.Generator().manual_seed(seed + 99)
     gc = torch.randn((3, H, W), generator=g).numpy()
-    t0 = time.perf_counter()
-    _, _, _, st = O.forward(s.means3D.numpy(), s.opacities.numpy(), c.world_to_camera.numpy(),
-                            c.projective_matrix.numpy(), c.camera_center.numpy(), c.tanfovx, c.tanfovy, H, W,
-                            np.zeros(3, np.float32), dc=s.dc.numpy(), sh=s.sh.numpy(), scales=s.scales.numpy(),
-                            rotations=s.rotations.numpy())
-    st.backward(gc)
-    dt = time.perf_counter() - t0
+    prm = dict(dc=s.dc.numpy(), sh=s.sh.numpy(), scales=s.scales.numpy(), rotations=s.rotations.numpy())
+    means, opac = s.means3D.numpy(), s.opacities.numpy()
+
+    def leg(threads):
+        old = O.set_threads(threads)
+        try:
+            done, t0 = 0, time.perf_counter()
+            while True:
+                c = cams[done % len(cams)]
+                _, _, _, st = O.forward(means, opac, c.world_to_camera.numpy(), c.projective_matrix.numpy(),
+                                        c.camera_center.numpy(), c.tanfovx, c.tanfovy, H, W, np.zeros(3, np.float32),
+                                        **prm)
+                st.backward(gc)
+                del st
+                done += 1
+                dt = time.perf_counter() - t0
+                if dt >= budget_s or done >= 4 * len(cams):
+                    return done, dt, O.get_threads()
+        finally:
+            O.set_threads(old)
+
+    threads = host_threads()
+    nv_all, dt_all, used = leg(threads)
+    nv_one, dt_one, _ = leg(1)
     try:
         model = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":", 1)[1].strip()
     except Exception:  # noqa: BLE001
         model = "unknown"
-    return {"value": round(1.0 / dt, 5), "unit": "views/s", "cores": 1, "kind": "port",
-            "sample": f"1 view fwd+bwd of the same {W}x{H} / {n} Gaussian scene, 1 thread ({model})",
-            "seconds": round(dt, 3)}
+    return {"value": round(nv_all / dt_all, 4), "unit": "views/s", "cores": used, "kind": "port",
+            "sample": f"{nv_all} views fwd+bwd of the same {W}x{H} / {n}-Gaussian yaw batch, {used} OpenMP threads "
+                      f"({model}; os.cpu_count()={os.cpu_count()})",
+            "seconds": round(dt_all, 3),
+            "single_core": {"value": round(nv_one / dt_one, 4), "unit": "views/s", "cores": 1,
+                            "sample": f"{nv_one} views, 1 thread", "seconds": round(dt_one, 3)}}
 
 
-def load_traffic(phase: str, n: int, W: int, H: int):
+def load_pmc(n: int, W: int, H: int):
+    """Per-phase HBM bytes and VALU figures per launch from the committed PMC passes (tools/pmc_traffic.py)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        d = json.load(open(path))
-        e = d.get(f"{n}x{W}x{H}", {}).get(phase)
-        return None if e is None else float(e)
+        return json.load(open(path)).get(f"{n}x{W}x{H}", {})
     except Exception:  # noqa: BLE001
-        return None
+        return {}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--views", type=int, default=8)
     ap.add_argument("--consensus-interval", type=int, default=200)
     ap.add_argument("--shared-frac", type=float, default=0.2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train-step", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds per CPU-baseline leg")
+    ap.add_argument("--no-reference-k", action="store_true",
+                    help="skip the untimed depth-prefix-off forwards (profiling runs: keeps kernel averages clean)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -263,8 +332,16 @@ def main():
 
     n, W, H = args.n, args.width, args.height
     seed = 1234 + rank
-    s, gc, gi = make_inputs(n, W, H, seed, dev)
-    view = View(s, gc, gi, dev)
+    from dogs_amd.synthetic import make_scene
+    s = make_scene(n, W, H, seed=seed).to(dev)
+    yaws = view_yaws(args.views)
+    cams = make_cameras(W, H, yaws, dev)
+    g = torch.Generator().manual_seed(seed + 99)
+    grad_color = torch.randn((3, H, W), generator=g).to(dev)
+    grad_inv = torch.zeros((1, H, W), device=dev)
+    views = Views(s, cams, grad_color, grad_inv, dev)
+    with torch.cuda.device(dev):
+        L.adaptive_capacity(W, H, reset=True)   # every run starts cold; the warmup views let it settle
 
     cons = None
     if ws > 1:
@@ -276,11 +353,6 @@ def main():
         cons = BlockConsensus(gidx, num_global, device=dev)
         cparams = (s.means3D, s.dc, s.sh, s.raw_scales.to(dev), s.raw_rotations.to(dev), s.raw_opacities.to(dev))
 
-    def one(i):
-        view.step()
-        if cons is not None and ((i + 1) % args.consensus_interval == 0):
-            cons.consensus(cparams)
-
     def max_over_ranks(x):
         if ws == 1:
             return x
@@ -288,8 +360,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    for i in range(args.warmup):
-        one(i)
+    for _ in range(args.warmup):
+        views.step()
     if cons is not None:
         cons.consensus(cparams)  # untimed: the first exchange carries one-time buffer and communicator setup
     torch.cuda.synchronize()
@@ -298,9 +370,9 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     step_t = []
-    for i in range(args.steps):
+    for _ in range(args.steps):
         ts = time.perf_counter()
-        one(i)
+        views.step()
         step_t.append(time.perf_counter() - ts)
     torch.cuda.synchronize()
     if ws > 1:
@@ -324,34 +396,71 @@ def main():
         torch.cuda.synchronize()
         cons_s = max_over_ranks(time.perf_counter() - t1)
         elapsed += cons_s * args.steps / args.consensus_interval
-    num_rendered = view.last[0]
-    K_binned = view.binned_instances()
-    K = view.reference_instances()
+    view_ms = elapsed / args.steps * 1e3
+    with torch.cuda.device(dev):
+        cap = L.adaptive_capacity(W, H)
 
-    # ---- one profiled step: per-phase hipEvent durations on the stream the kernels run on
+    # ---- untimed per-view figures, then one profiled pass over the views: per-phase hipEvent durations on the stream
+    # the kernels run on
+    HW = W * H
+    vstats = []
+    for k, y in enumerate(yaws):
+        r = views.stats(k, reference_k=not args.no_reference_k)
+        r.update(view=k, yaw=round(y, 3), N=n, HW=HW)
+        vstats.append(r)
+    torch.cuda.synchronize()
+    views.i = 0
     L.profile_enable(True)
-    view.step()
+    for _ in range(len(yaws)):
+        views.step()
     torch.cuda.synchronize()
     prof = L.profile_collect()
     L.profile_enable(False)
-    HW = W * H
-    phases = {k: round(v[0], 4) for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}
-    dom = max(prof.items(), key=lambda kv: kv[1][0] if phase_bytes(kv[0], n, K, HW) > 0 else -1)[0]
-    dom_ms = prof[dom][0] / max(prof[dom][1], 1)
-    dom_bytes = phase_bytes(dom, n, K, HW)
+    nv = float(len(yaws))
+    phase_ms = {k: v[0] / nv for k, v in prof.items()}
+    phase_b = {k: float(np.mean([phase_bytes(k, r) for r in vstats])) for k in phase_ms}
+    dom = max(phase_ms, key=lambda k: phase_ms[k] if phase_b.get(k, 0) > 0 else -1.0)
+    dom_ms, dom_bytes = phase_ms[dom], phase_b[dom]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    b_view = 856.0 * n + 172.0 * K + 64.0 * HW
-    view_ms = elapsed / args.steps * 1e3
-    traffic = load_traffic(dom, n, W, H)
+    view_bytes = float(sum(phase_b.values()))
+    K_mean = float(np.mean([r["K"] for r in vstats])) if not args.no_reference_k else float("nan")
+    ref_bytes = reference_view_bytes(n, int(K_mean), HW) if K_mean == K_mean else float("nan")
+    pmc = load_pmc(n, W, H)
+
+    def valu(phase):
+        e = pmc.get(phase)
+        if not isinstance(e, dict) or "valu_insts" not in e:
+            return None
+        t = phase_ms[phase] * 1e-3
+        out = {"insts": e["valu_insts"], "achieved_ginst_s": round(e["valu_insts"] / t / 1e9, 1),
+               "peak_ginst_s": VALU_PEAK_GINST, "frac": round(e["valu_insts"] / t / 1e9 / VALU_PEAK_GINST, 4)}
+        if "valu_busy" in e:
+            out["busy"] = e["valu_busy"]
+        return out
+
+    traffic = pmc.get(dom, {}).get("hbm_bytes") if isinstance(pmc.get(dom), dict) else None
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
+            "kernel_ms": round(dom_ms, 4), "kernel_bytes": round(dom_bytes),
+            "view_bytes": round(view_bytes), "view_achieved_GBs": round(view_bytes / (view_ms * 1e-3) / 1e9, 1),
+            "view_frac": round(view_bytes / (view_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "phase_bytes": {k: round(v) for k, v in phase_b.items() if v > 0},
+            "valu": {k: valu(k) for k in ("render_bwd", "render_fwd") if k in phase_ms},
+            "reference_equivalent": {
+                "formula": "856 N + 172 K + 64 HW (SURVEY.md 8(d), the reference's full per-tile lists)",
+                "view_bytes": round(ref_bytes) if ref_bytes == ref_bytes else None,
+                "K_mean": round(K_mean) if K_mean == K_mean else None,
+                "view_frac": (round(ref_bytes / (view_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                              if ref_bytes == ref_bytes else None)}}
 
     train = None
     if not args.no_train_step and ws == 1:
-        ts = TrainStep(s, dev, seed)
-        for _ in range(3):
+        ts = TrainStep(s, cams, dev, seed)
+        for _ in range(len(cams)):
             ts.step()
         torch.cuda.synchronize()
         tt = time.perf_counter()
-        nts = max(5, args.steps // 2)
+        nts = max(2 * len(cams), args.steps // 2)
         for _ in range(nts):
             ts.step()
         torch.cuda.synchronize()
@@ -359,12 +468,12 @@ def main():
         dms, n_after = ts.densify()
         train = {"views_per_s": round(1e3 / tms, 2), "ms_per_step": round(tms, 3),
                  "includes": "activations + raster fwd/bwd + L1 + fused-SSIM fwd/bwd + densification stats + "
-                             "SparseGaussianAdam (one launch)",
+                             "SparseGaussianAdam (one launch), cycling the view batch",
                  "densify_and_prune_ms": round(dms, 3), "gaussians_after_densify": n_after}
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(n, W, H, seed)
+        cpu = cpu_baseline(n, W, H, seed, yaws, budget_s=args.cpu_budget)
 
     if rank == 0:
         line = {
@@ -379,21 +488,20 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (BASELINE.md §2 generator, seed 1234+rank; random dL/dcolor, zero dL/dinvdepth)",
-            "config": {"workload": f"synthetic {W}x{H}, {n} Gaussians/rank, SH3, raster fwd+bwd per view",
+            "data": f"synthetic (BASELINE.md §2 generator, seed 1234+rank; {len(yaws)} seeded yaw views; random "
+                    "dL/dcolor, zero dL/dinvdepth)",
+            "config": {"workload": f"synthetic {W}x{H}, {n} Gaussians/rank, SH3, raster fwd+bwd per view, "
+                                   f"{len(yaws)}-view yaw batch",
                        "width": W, "height": H, "gaussians_per_rank": n, "sh_degree": 3,
-                       "num_rendered": int(num_rendered), "instances_K": int(K),
-                       "instances_binned": int(K_binned),
+                       "adaptive_capacity_per_tile": cap,
                        "consensus_interval": args.consensus_interval if ws > 1 else None,
                        "consensus_ms": round(cons_s * 1e3, 3) if ws > 1 else None,
                        "shared_gaussians": (cons.num_shared if cons is not None else 0),
                        "parallelism": f"admm-blocks x{ws}" if ws > 1 else "single"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
-                         "kernel_ms": round(dom_ms, 4), "kernel_bytes": dom_bytes,
-                         "view_bytes": b_view, "view_achieved_GBs": round(b_view / (view_ms * 1e-3) / 1e9, 1),
-                         "view_frac": round(b_view / (view_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-            "phases_ms": phases,
+            "views": [{k: r[k] for k in ("view", "yaw", "num_rendered", "K", "e1", "e2", "unfinished_tiles",
+                                         "visible_gaussians", "binned_gaussians", "live_gaussians")} for r in vstats],
+            "roofline": roof,
+            "phases_ms": {k: round(v, 4) for k, v in sorted(phase_ms.items(), key=lambda kv: -kv[1])},
             "cpu_baseline": cpu,
             "train_step": train,
         }

@@ -73,7 +73,7 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count"
            "dg_add_densification_stats", "dg_densify_select", "dg_densify_split_stds", "dg_densify_count",
            "dg_densify_gather", "dg_splat_pack", "dg_ply_pack", "dg_ring_create", "dg_ring_submit", "dg_ring_next",
            "dg_ring_upload", "dg_ring_pending", "dg_ring_destroy", "dg_image_u8_to_chw", "dg_points_in_boxes2d", "dg_activate_forward", "dg_activate_backward", "dg_clamp_l1_blocks",
-           "dg_clamp_l1_forward", "dg_clamp_l1_backward", "dg_adaptive_capacity",
+           "dg_clamp_l1_forward", "dg_clamp_l1_backward", "dg_adaptive_capacity", "dg_debug_counters",
            "dg_last_error", "dg_version")
 
 _lib = None
@@ -127,6 +127,9 @@ def load(path: str | None = None):
         if hasattr(L, "dg_binned_instances"):  # introspection only; absent in older builds used for A/B runs
             L.dg_binned_instances.restype = C.c_int
             L.dg_binned_instances.argtypes = [vp, C.c_int, i64p, vp]
+        if hasattr(L, "dg_debug_counters"):
+            L.dg_debug_counters.restype = C.c_int
+            L.dg_debug_counters.argtypes = [vp, C.c_int, C.POINTER(C.c_uint32), vp]
         if hasattr(L, "dg_adaptive_capacity"):
             L.dg_adaptive_capacity.restype = C.c_int
             L.dg_adaptive_capacity.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
@@ -262,6 +265,14 @@ def adaptive_capacity(W: int, H: int, reset: bool = False) -> int:
     v = C.c_int(0)
     check(load().dg_adaptive_capacity(int(W), int(H), 1 if reset else 0, C.byref(v)))
     return int(v.value)
+
+
+def forward_counters(geom: torch.Tensor, P: int) -> dict:
+    """The per-view counters of the last forward on a geometry buffer (dg_debug_counters; synchronises)."""
+    a = (C.c_uint32 * 16)()
+    check(load().dg_debug_counters(geom.data_ptr(), int(P), a, stream_of(geom.device)))
+    return {"num_rendered": int(a[2]) | (int(a[3]) << 32), "e1": int(a[5]), "unfinished_tiles": int(a[6]),
+            "e2": int(a[7]), "cut": bool(a[8])}
 
 
 def profile_enable(on: bool = True) -> None:

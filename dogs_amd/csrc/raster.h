@@ -47,6 +47,7 @@ enum {
     CNT_LONG = 11,      // phase-1 tiles queued for the long-list depth sort
     CNT_LONG2 = 12,     // phase-2 tiles queued for the long-list depth sort
     CNT_PREV_UNF = 14,  // unfinished tiles of the previous phase-2 launch at this image size (adaptive capacity)
+    CNT_PREV_K2 = 15,   // phase-2 instances of that launch
 };
 
 // Depth histogram of the prefix cut: bins of 2^DH_SHIFT key ulps (1/64 of a binade) from the near plane up;
@@ -80,6 +81,7 @@ struct RenderArgs {
     // wave-private LDS -- the latency-bound sort overlaps the VALU-bound compositing of other waves
     int fuse_sort;
     DSortArgs ds;
+    uint32_t* probe;            // optional (phase 2, adaptive capacity): [1] <- counters[CNT_K2]
 };
 
 struct RenderBwdArgs {

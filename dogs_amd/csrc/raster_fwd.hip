@@ -338,9 +338,10 @@ __global__ void __launch_bounds__(1024) k_depth_cut(const uint32_t* __restrict__
         counters[CNT_RECT_LO] = (uint32_t)r;
         counters[CNT_RECT_LO + 1] = (uint32_t)(r >> 32);
         counters[CNT_ERR] = s_err;
-        counters[CNT_INVD] = 0u; counters[10] = 0u; counters[13] = 0u; counters[15] = 0u;
-        counters[CNT_PREV_UNF] = probe ? *probe : 0u;
-        if (probe) *probe = 0u;
+        counters[CNT_INVD] = 0u; counters[10] = 0u; counters[13] = 0u;
+        counters[CNT_PREV_UNF] = probe ? probe[0] : 0u;
+        counters[CNT_PREV_K2] = probe ? probe[1] : 0u;
+        if (probe) { probe[0] = 0u; probe[1] = 0u; }
     }
     const bool cut = K > cap;
     if (t == 0 && s_best < 0) {  // not even bin 0 fits: phase 1 bins nothing, phase 2 everything
@@ -594,6 +595,8 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tile = blockIdx.x * 4 + w;
     if (tile >= a.num_tiles) return;
+    // the adaptive capacity's probe gets this view's phase-2 instance count (the next view's k_depth_cut reads it)
+    if (PHASE == 2 && a.probe && blockIdx.x == 0 && threadIdx.x == 0) a.probe[1] = a.counters[CNT_K2];
     if (PHASE == 2 && !a.unfinished[tile]) return;  // finished in phase 1: outputs already final
     float4* sb = reinterpret_cast<float4*>(&s_raw[w][0]);
     uint32_t* ids = &s_raw[w][780];

@@ -266,6 +266,10 @@ int dg_debug_sorted_instances(const dg_raster_args* a, const void* geom, const v
                               uint32_t* gauss_out, int64_t* e1, dg_stream_t stream);
 /* Instances actually binned by the last forward on this geometry block: phase 1 + phase 2 (synchronises). */
 int dg_binned_instances(const void* geom, int P, int64_t* binned, dg_stream_t stream);
+/* The 16 per-view counters of the last forward on this geometry block (synchronises): [0] tile-rect area of the
+ * visible Gaussians (u32, saturating), [2..3] num_rendered (u64), [5] phase-1 instances E1, [6] tiles left unfinished
+ * by phase 1, [7] phase-2 instances, [8] nonzero when phase 1 was a cut prefix.  Introspection for the bench. */
+int dg_debug_counters(const void* geom, int P, uint32_t* counters16, dg_stream_t stream);
 /* The adaptive phase-1 capacity (prefix_per_tile == 0) of image size W x H on the current device, in tile-rect
  * units per tile (*per_tile_out, may be NULL); reset != 0 sets it back to its cold default first.  Tests and the
  * bench use it to start a scene cold and to report what the views settled on. */
