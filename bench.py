@@ -287,6 +287,64 @@ def cpu_baseline(n, W, H, seed, yaws, budget_s=12.0):
                             "sample": f"{nv_one} views, 1 thread", "seconds": round(dt_one, 3)}}
 
 
+def admm_leg(args, ws, rank, dev, n, W, H):
+    """The ADMM block trainer (dogs_amd.admm_trainer): every rank trains its block of a chain split (1e6 Gaussians,
+    20% shared with the next block, --views yaw cameras, random targets) for --admm-rounds rounds of --admm-interval
+    local iterations (activations, raster fwd/bwd, L1 + SSIM + scale regulariser, SparseGaussianAdam with the ADMM
+    penalty) each followed by the consensus round (RCCL all_reduce of the shared Gaussians, duals, residuals,
+    penalty adaptation).  Then rank 0 trains the same split sequentially on its one GPU (the single-GPU baseline of
+    the '>= 6x at 8 GPUs' target) for the same rounds; speedup = sequential / parallel wall time."""
+    import gc
+    from dogs_amd.admm import ADMMConfig
+    from dogs_amd.admm_trainer import barrier_time, distributed_trainer, sequential_trainer
+    cfg = ADMMConfig(consensus_interval=args.admm_interval)
+    tr, cons, run = distributed_trainer(rank, ws, n, W, H, args.views, args.shared_frac, dev, admm=cfg)
+    for _ in range(min(args.views, 8)):   # warm-up: allocator, adaptive capacity
+        tr.local_step()
+    ps = tuple(p.detach() for p in tr.param_tuple())
+    run.cons.residuals(ps, run.cons.consensus(ps), ps, tr.admm.rho)   # communicator / buffer setup
+    del ps
+    rounds = max(1, args.admm_rounds)
+    t_par = barrier_time(lambda: [run.round() for _ in range(rounds)], dev, ws)
+    steps = rounds * cfg.consensus_interval
+    out = {"views_per_s": round(ws * steps / t_par, 2), "ms_per_round": round(t_par / rounds * 1e3, 2),
+           "rounds": rounds, "interval": cfg.consensus_interval, "blocks": ws, "gaussians_per_block": n,
+           "shared_gaussians": cons.num_shared,
+           "consensus_ms": round(1e3 * max(lg.seconds["consensus"] for lg in run.logs), 3),
+           "last_round": {"primal": {k: float(f"{v:.4g}") for k, v in run.logs[-1].primal.items()},
+                          "dual": {k: float(f"{v:.4g}") for k, v in run.logs[-1].dual.items()},
+                          "loss": float(tr.last_loss), "penalty": float(tr.penalty())},
+           "includes": "per local step: activations + raster fwd/bwd + clamp/L1 + fused SSIM + scale regulariser + "
+                       "SparseGaussianAdam with the ADMM proximal gradient (one launch); per round: consensus "
+                       "all_reduce of the shared set, duals, residuals, rho adaptation"}
+    del tr, cons, run
+    gc.collect()
+    torch.cuda.empty_cache()
+    nseq = args.admm_seq if args.admm_seq >= 0 else (ws if ws > 1 else 0)
+    if nseq > 0:
+        if ws > 1:
+            dist.barrier()
+        if rank == 0:
+            blocks, seq = sequential_trainer(nseq, n, W, H, args.views, args.shared_frac, dev, admm=cfg)
+            for b in blocks:
+                for _ in range(min(args.views, 8)):
+                    b.local_step()
+            ps = [tuple(p.detach() for p in b.param_tuple()) for b in blocks]
+            seq.cons.residuals(ps, seq.cons.consensus(ps), ps, blocks[0].admm.rho)   # warm-up of the exchange
+            del ps
+            t_seq = barrier_time(lambda: [seq.round() for _ in range(rounds)], dev, 1)
+            out["sequential"] = {"blocks": nseq, "seconds": round(t_seq, 3),
+                                 "views_per_s": round(nseq * steps / t_seq, 2)}
+            if nseq == ws:
+                out["speedup_vs_sequential"] = round(t_seq / t_par, 3)
+            del blocks, seq
+            gc.collect()
+            torch.cuda.empty_cache()
+        if ws > 1:
+            dist.barrier()
+    return out
+
+
 def load_pmc(n: int, W: int, H: int):
     """Per-phase HBM bytes and VALU figures per launch from the committed PMC passes (tools/pmc_traffic.py)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -310,6 +368,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train-step", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds per CPU-baseline leg")
+    ap.add_argument("--no-admm", action="store_true", help="skip the ADMM block-trainer leg")
+    ap.add_argument("--admm-rounds", type=int, default=1, help="timed ADMM rounds (each: interval local steps)")
+    ap.add_argument("--admm-interval", type=int, default=200, help="local steps per round (urban3d_admm.yaml:44)")
+    ap.add_argument("--admm-seq", type=int, default=-1,
+                    help="blocks of the sequential single-GPU baseline on rank 0 (-1: the world size when > 1)")
     ap.add_argument("--no-reference-k", action="store_true",
                     help="skip the untimed depth-prefix-off forwards (profiling runs: keeps kernel averages clean)")
     args = ap.parse_args()
@@ -471,6 +534,12 @@ def main():
                              "SparseGaussianAdam (one launch), cycling the view batch",
                  "densify_and_prune_ms": round(dms, 3), "gaussians_after_densify": n_after}
 
+    admm = None
+    if not args.no_admm:
+        del views
+        torch.cuda.empty_cache()
+        admm = admm_leg(args, ws, rank, dev, n, W, H)
+
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(n, W, H, seed, yaws, budget_s=args.cpu_budget)
@@ -504,6 +573,7 @@ def main():
             "phases_ms": {k: round(v, 4) for k, v in sorted(phase_ms.items(), key=lambda kv: -kv[1])},
             "cpu_baseline": cpu,
             "train_step": train,
+            "admm": admm,
         }
         print(json.dumps(line))
     if ws > 1:

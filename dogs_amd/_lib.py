@@ -34,6 +34,10 @@ class DgAdamGroup(C.Structure):
                 ("lr", C.c_float), ("eps", C.c_float), ("M", C.c_uint32)]
 
 
+class DgAdamProx(C.Structure):
+    _fields_ = [("u", C.c_void_p), ("z", C.c_void_p), ("coef", C.c_float)]
+
+
 class DgDensifyStats(C.Structure):
     _fields_ = [("radii", C.c_void_p), ("dmeans2D", C.c_void_p), ("dmeans2D_stride", C.c_uint32),
                 ("max_radii2D", C.c_void_p), ("grad_accum", C.c_void_p), ("denom", C.c_void_p)]
@@ -73,7 +77,7 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count"
            "dg_add_densification_stats", "dg_densify_select", "dg_densify_split_stds", "dg_densify_count",
            "dg_densify_gather", "dg_splat_pack", "dg_ply_pack", "dg_ring_create", "dg_ring_submit", "dg_ring_next",
            "dg_ring_upload", "dg_ring_pending", "dg_ring_destroy", "dg_image_u8_to_chw", "dg_points_in_boxes2d", "dg_activate_forward", "dg_activate_backward", "dg_clamp_l1_blocks",
-           "dg_clamp_l1_forward", "dg_clamp_l1_backward", "dg_adaptive_capacity", "dg_debug_counters",
+           "dg_clamp_l1_forward", "dg_clamp_l1_backward", "dg_adaptive_capacity", "dg_debug_counters", "dg_adam_update_groups_prox",
            "dg_last_error", "dg_version")
 
 _lib = None
@@ -149,6 +153,11 @@ def load(path: str | None = None):
             L.dg_adam_update_groups.restype = C.c_int
             L.dg_adam_update_groups.argtypes = [C.POINTER(DgAdamGroup), C.c_int, vp, C.c_uint32, C.c_float,
                                                 C.c_float, C.POINTER(DgDensifyStats), vp]
+            if hasattr(L, "dg_adam_update_groups_prox"):
+                L.dg_adam_update_groups_prox.restype = C.c_int
+                L.dg_adam_update_groups_prox.argtypes = [C.POINTER(DgAdamGroup), C.POINTER(DgAdamProx), C.c_int, vp,
+                                                         C.c_uint32, C.c_float, C.c_float, C.POINTER(DgDensifyStats),
+                                                         vp]
             L.dg_add_densification_stats.restype = C.c_int
             L.dg_add_densification_stats.argtypes = [C.POINTER(DgDensifyStats), vp, C.c_uint32, vp]
             dp = C.POINTER(DgDensifyArgs)

@@ -88,6 +88,7 @@ class BlockConsensus:
         if self.num_shared:
             own[self.loc] = owner[self.sid] == self.rank
         self.owned = own
+        self._owned_f = None
         self.widths: tuple[int, ...] | None = None
 
     # ---------------------------------------------------------------------------------------------
@@ -125,20 +126,35 @@ class BlockConsensus:
                   z_prev: tuple[torch.Tensor, ...] | None, rho: dict[str, float]) -> tuple[dict, dict]:
         """Primal: sum over blocks of MSE(z[idx_k], x_k) (master_gaussian_trainer.py:396-433).
         Dual: rho * MSE(z_prev, z) over the global set (:435-456), each Gaussian counted once."""
-        part = torch.zeros(12, dtype=torch.float64, device=self.device)
-        for i, (x, zz) in enumerate(zip(params, z)):
-            part[i] = F.mse_loss(zz.float(), x.detach().float()).double()
-            if z_prev is not None:
-                d = (_flat(z_prev[i]) - _flat(zz))[self.owned]
-                part[6 + i] = (d.double() ** 2).sum()
+        if self._owned_f is None or self._owned_f.shape[0] != self.owned.shape[0]:
+            self._owned_f = self.owned.to(torch.float64).unsqueeze(-1)
+        part = residual_parts(params, z, z_prev, self._owned_f)
         if self.world > 1:
             dist.all_reduce(part, op=dist.ReduceOp.SUM, group=self.group)
-        primal = {n: float(part[i]) for i, n in enumerate(RHO_NAMES)}
-        dual = {}
-        for i, n in enumerate(RHO_NAMES):
-            per = int(_flat(params[i]).shape[1])
-            dual[n] = rho[n] * float(part[6 + i]) / float(self.num_global * per) if z_prev is not None else 0.0
-        return primal, dual
+        return residual_dicts(part.cpu(), params, z_prev is not None, self.num_global, rho)
+
+
+@torch.no_grad()
+def residual_parts(params, z, z_prev, owned_f: torch.Tensor) -> torch.Tensor:
+    """[12] float64 on the device, no host sync: MSE(z, x) per tensor, then the owned rows' sum of (z_prev - z)^2."""
+    part = torch.zeros(12, dtype=torch.float64, device=owned_f.device)
+    for i, (x, zz) in enumerate(zip(params, z)):
+        part[i] = F.mse_loss(zz.float(), x.detach().float()).double()
+        if z_prev is not None:
+            d = (_flat(z_prev[i]) - _flat(zz)).double() * owned_f
+            part[6 + i] = (d * d).sum()
+    return part
+
+
+def residual_dicts(part: torch.Tensor, params, have_prev: bool, num_global: int, rho: dict):
+    """(primal, dual) dicts from the summed parts (one host copy)."""
+    v = part.tolist()
+    primal = {n: float(v[i]) for i, n in enumerate(RHO_NAMES)}
+    dual = {}
+    for i, n in enumerate(RHO_NAMES):
+        per = int(_flat(params[i]).shape[1])
+        dual[n] = rho[n] * float(v[6 + i]) / float(num_global * per) if have_prev else 0.0
+    return primal, dual
 
 
 def initial_rho(cfg: ADMMConfig, num_gaussians: int) -> dict[str, float]:

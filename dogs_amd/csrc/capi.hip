@@ -741,6 +741,12 @@ static int fill_stats(gs::AdamMultiArgs& m, const dg_densify_stats* st) {
 
 int dg_adam_update_groups(const dg_adam_group* groups, int n_groups, const uint8_t* visible, uint32_t N, float b1,
                           float b2, const dg_densify_stats* stats, dg_stream_t stream) {
+    return dg_adam_update_groups_prox(groups, nullptr, n_groups, visible, N, b1, b2, stats, stream);
+}
+
+int dg_adam_update_groups_prox(const dg_adam_group* groups, const dg_adam_prox* prox, int n_groups,
+                               const uint8_t* visible, uint32_t N, float b1, float b2, const dg_densify_stats* stats,
+                               dg_stream_t stream) {
     if (n_groups < 0 || n_groups > gs::MAX_ADAM_GROUPS) return fail("n_groups must be 0..8%s (got %d)", "", n_groups);
     if (N && !visible) return fail("visible mask required%s%d");
     gs::AdamMultiArgs m;
@@ -756,7 +762,13 @@ int dg_adam_update_groups(const dg_adam_group* groups, int n_groups, const uint8
         d.param = g.param; d.grad = g.grad; d.m = g.exp_avg; d.v = g.exp_avg_sq; d.lr = g.lr; d.eps = g.eps; d.M = g.M;
         const uintptr_t al = reinterpret_cast<uintptr_t>(g.param) | reinterpret_cast<uintptr_t>(g.grad) |
                              reinterpret_cast<uintptr_t>(g.exp_avg) | reinterpret_cast<uintptr_t>(g.exp_avg_sq);
-        d.vec = (al & 15u) == 0u;
+        uintptr_t alp = 0;
+        if (prox && prox[k].u) {
+            if (!prox[k].z) return fail("adam group %s%d: prox u without z", "", k);
+            d.u = prox[k].u; d.z = prox[k].z; d.coef = prox[k].coef;
+            alp = reinterpret_cast<uintptr_t>(prox[k].u) | reinterpret_cast<uintptr_t>(prox[k].z);
+        }
+        d.vec = ((al | alp) & 15u) == 0u;
     }
     m.n = n;
     if (fill_stats(m, stats)) return 1;

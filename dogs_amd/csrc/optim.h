@@ -18,7 +18,11 @@ struct AdamGroup {
     float* v;
     float lr, eps;
     uint32_t M;       // floats per Gaussian
-    uint32_t vec;     // 1: param/grad/m/v 16-byte aligned (float4 path)
+    uint32_t vec;     // 1: param/grad/m/v (and u/z) 16-byte aligned (float4 path)
+    // optional ADMM proximal term 0.5 rho mse(x + u, z): gradient coef ((x + u) - z), coef = rho / numel
+    const float* u;
+    const float* z;
+    float coef;
 };
 
 struct AdamMultiArgs {

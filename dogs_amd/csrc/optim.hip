@@ -1,7 +1,9 @@
 // optim.hip -- optimizer-side kernels of a training view (optim.h).
 //
 // k_adam_multi      SparseGaussianAdam.step (diff_gaussian_rasterization/__init__.py:303-332 -> adam.cu:10-38) for
-//                   every parameter group in one launch, plus the view's densification statistics
+//                   every parameter group in one launch (optionally with the ADMM proximal gradient of a block
+//                   trainer, slave_gaussian_trainer.py:161-202, added to the visible rows' gradient), plus the view's
+//                   densification statistics
 //                   (gaussian_trainer.py:433-438 max_radii2D, gaussian_splat_model.py:533-541 add_densification_stats).
 //                   Blocks are assigned to groups in contiguous ranges (block-uniform group, scalar kernel-argument
 //                   loads); each lane updates 4 consecutive floats (float4 when the group is 16-byte aligned).
@@ -88,6 +90,11 @@ __global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
             m[c] = *reinterpret_cast<const float4*>(g.m + e0);
             v[c] = *reinterpret_cast<const float4*>(g.v + e0);
 #endif
+            if (g.u) {  // the ADMM proximal gradient joins the loss gradient before the moments see it
+                const float4 u = nt_load4(g.u + e0), z = nt_load4(g.z + e0);
+                gr[c].x += g.coef * ((p[c].x + u.x) - z.x); gr[c].y += g.coef * ((p[c].y + u.y) - z.y);
+                gr[c].z += g.coef * ((p[c].z + u.z) - z.z); gr[c].w += g.coef * ((p[c].w + u.w) - z.w);
+            }
         }
     }
 #pragma unroll
@@ -113,7 +120,9 @@ __global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
             if (!vis[c][j]) continue;
             const uint32_t e = e0 + j;
             float mm = g.m[e], vv = g.v[e];
-            g.param[e] = adam_one(g.param[e], g.grad[e], mm, vv, g.lr, b1, b2, g.eps);
+            const float pe = g.param[e];
+            const float ge = g.u ? g.grad[e] + g.coef * ((pe + g.u[e]) - g.z[e]) : g.grad[e];
+            g.param[e] = adam_one(pe, ge, mm, vv, g.lr, b1, b2, g.eps);
             g.m[e] = mm;
             g.v[e] = vv;
         }

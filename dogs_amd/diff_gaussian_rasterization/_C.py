@@ -225,12 +225,17 @@ def fusedssim_backward(C1, C2, img1, img2, dL_dmap):
     return _cuda.fusedssim_backward(C1, C2, a, b, dL_dmap.unsqueeze(0), d1, d2, d3)[0]
 
 
-def adam_update_groups(groups, visible, N, b1=0.9, b2=0.999, stats=None):
+def adam_update_groups(groups, visible, N, b1=0.9, b2=0.999, stats=None, prox=None):
     """SparseGaussianAdam over several groups in one launch (dg_adam_update_groups; each group as adamUpdate).
     groups: iterable of (param, grad, exp_avg, exp_avg_sq, lr, eps); stats (optional): dict with radii [N] int32,
     dmeans2D [N,>=2] (screen-space-point gradient), max_radii2D [N], grad_accum [N(,1)], denom [N(,1)] -- the view's
-    densification statistics (gaussian_trainer.py:433-438), updated in the same launch."""
+    densification statistics (gaussian_trainer.py:433-438), updated in the same launch.  prox (optional): one entry
+    per group, None or (u, z, coef) -- the ADMM penalty 0.5 rho mse(x + u, z) of a block trainer as its gradient
+    coef ((x + u) - z), coef = rho / numel(x), added for the rows Adam updates (dg_adam_update_groups_prox)."""
     groups = list(groups)
+    prox = list(prox) if prox is not None else None
+    if prox is not None and len(prox) != len(groups):
+        raise RuntimeError("prox needs one entry (or None) per group")
     vis = visible.contiguous()
     if vis.dtype != torch.bool:
         vis = vis.bool()
@@ -253,6 +258,7 @@ def adam_update_groups(groups, visible, N, b1=0.9, b2=0.999, stats=None):
         st = _lib.DgDensifyStats(radii.data_ptr(), dm.data_ptr(), int(dm.stride(0)), stats["max_radii2D"].data_ptr(),
                                  stats["grad_accum"].data_ptr(), stats["denom"].data_ptr())
     L = _lib.load()
+    parr = (_lib.DgAdamProx * max(1, min(8, len(groups))))() if prox is not None else None
     with torch.cuda.device(dev):
         for c0 in range(0, max(1, len(groups)), 8):
             chunk = groups[c0:c0 + 8]
@@ -263,7 +269,23 @@ def adam_update_groups(groups, visible, N, b1=0.9, b2=0.999, stats=None):
                         raise RuntimeError(f"{n} must be a contiguous float32 tensor")
                 arr[i] = _lib.DgAdamGroup(param.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(), float(lr),
                                           float(eps), int(param.numel() // N) if N else 0)
-            _lib.check(L.dg_adam_update_groups(arr, len(chunk), vis.data_ptr(), int(N), float(b1), float(b2),
-                                               C.byref(st) if (st is not None and c0 == 0) else None,
-                                               _lib.stream_of(dev)))
+                if parr is not None:
+                    pe = prox[c0 + i]
+                    if pe is None:
+                        parr[i] = _lib.DgAdamProx(None, None, 0.0)
+                    else:
+                        u, z, coef = pe
+                        for t, n in ((u, "dual"), (z, "global")):
+                            _lib.require_f32_on(param.device, **{n: t})
+                            if not t.is_contiguous() or t.shape != param.shape:
+                                raise RuntimeError(f"{n} must be a contiguous tensor shaped like the parameter")
+                        keep += [u, z]
+                        parr[i] = _lib.DgAdamProx(u.data_ptr(), z.data_ptr(), float(coef))
+            st_p = C.byref(st) if (st is not None and c0 == 0) else None
+            if parr is not None:
+                _lib.check(L.dg_adam_update_groups_prox(arr, parr, len(chunk), vis.data_ptr(), int(N), float(b1),
+                                                        float(b2), st_p, _lib.stream_of(dev)))
+            else:
+                _lib.check(L.dg_adam_update_groups(arr, len(chunk), vis.data_ptr(), int(N), float(b1), float(b2),
+                                                   st_p, _lib.stream_of(dev)))
     del keep

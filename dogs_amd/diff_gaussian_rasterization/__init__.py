@@ -180,8 +180,11 @@ class SparseGaussianAdam(torch.optim.Adam):
         super().__init__(params=params, lr=lr, eps=eps)
 
     @torch.no_grad()
-    def step(self, visibility, N, stats=None):
+    def step(self, visibility, N, stats=None, prox=None):
+        """prox (optional): {group name: (u, z, coef)} -- an ADMM block trainer's penalty gradient folded into the
+        same launch (_C.adam_update_groups)."""
         groups = []
+        proxes = []
         for group in self.param_groups:
             lr = group["lr"]
             eps = group["eps"]
@@ -196,5 +199,7 @@ class SparseGaussianAdam(torch.optim.Adam):
                 state["exp_avg_sq"] = torch.zeros_like(param, memory_format=torch.preserve_format)
             grad = param.grad if param.grad.is_contiguous() else param.grad.contiguous()
             groups.append((param, grad, state["exp_avg"], state["exp_avg_sq"], lr, eps))
+            proxes.append(None if prox is None else prox.get(group.get("name")))
         if groups or stats is not None:
-            _C.adam_update_groups(groups, visibility, N, 0.9, 0.999, stats)
+            _C.adam_update_groups(groups, visibility, N, 0.9, 0.999, stats,
+                                  prox=proxes if prox is not None else None)

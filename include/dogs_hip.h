@@ -152,6 +152,20 @@ int dg_activate_backward(uint32_t N, const float* opacity, const float* scaling,
  * densification statistics of the same view when stats != NULL (they read nothing Adam writes). */
 int dg_adam_update_groups(const dg_adam_group* groups, int n_groups, const uint8_t* visible, uint32_t N, float b1,
                           float b2, const dg_densify_stats* stats, dg_stream_t stream);
+/* The ADMM penalty of a block trainer's loss, 0.5 * rho_p * F.mse_loss(x_p + u_p, z_p) per parameter tensor
+ * (SlaveGaussianSplatTrainer.add_admm_penalties, slave_gaussian_trainer.py:161-202), as its gradient
+ * coef * ((x + u) - z) with coef = rho_p / numel(x_p), added to the loss gradient of the rows Adam updates (the
+ * visible ones; SparseGaussianAdam ignores every other row's gradient, penalty included).  u (duals) and z (global
+ * values) have the parameter's shape; u == NULL: no term for that group. */
+typedef struct {
+    const float* u;
+    const float* z;
+    float coef;
+} dg_adam_prox;
+/* dg_adam_update_groups with one dg_adam_prox per group (prox may be NULL). */
+int dg_adam_update_groups_prox(const dg_adam_group* groups, const dg_adam_prox* prox, int n_groups,
+                               const uint8_t* visible, uint32_t N, float b1, float b2, const dg_densify_stats* stats,
+                               dg_stream_t stream);
 /* The statistics alone (replaces the max_radii2D update + add_densification_stats of gaussian_trainer.py:433-438). */
 int dg_add_densification_stats(const dg_densify_stats* stats, const uint8_t* visible, uint32_t N, dg_stream_t stream);
 

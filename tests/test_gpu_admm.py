@@ -1,0 +1,116 @@
+"""The ADMM block trainer on the GPU (dogs_amd.admm_trainer):
+
+* the penalty folded into SparseGaussianAdam (dg_adam_update_groups_prox) gives the same Adam moments as the
+  reference's route -- 0.5 rho mse(x + u, z) added to the loss (slave_gaussian_trainer.py:161-202), differentiated by
+  torch autograd, then the plain sparse Adam step -- within 1e-5 relative (fp32 rounding of the two gradient sums);
+* consensus, dual update, residuals and the penalty value on device tensors equal the same code on the host (1e-6);
+* a short sequential ADMM run (2 blocks, 2 rounds) on one GPU stays finite and moves the penalty parameters.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _small_block(dev, k=0, blocks=2, n=4000, W=192, H=128):
+    from dogs_amd.admm import ADMMConfig
+    from dogs_amd.admm_trainer import TrainConfig, make_block
+    return make_block(k, blocks, n, W, H, 1, 0.25, dev, seed=77, admm=ADMMConfig(consensus_interval=3),
+                      cfg=TrainConfig())
+
+
+def _perturb_state(tr, seed):
+    g = torch.Generator().manual_seed(seed)
+    st = tr.admm
+    st.u = tuple((0.01 * torch.randn(p.shape, generator=g)).to(p.device) for p in tr.param_tuple())
+    st.z = tuple((p.detach().cpu() + 0.02 * torch.randn(p.shape, generator=g)).to(p.device)
+                 for p in tr.param_tuple())
+    st.rho = {k: v * 1e3 for k, v in st.rho.items()}   # make the penalty matter against the image terms
+
+
+def test_prox_adam_matches_autograd_penalty(hip_device):
+    from dogs_amd.admm import PARAM_NAMES, admm_penalty
+    a, _, _ = _small_block(hip_device)
+    b, _, _ = _small_block(hip_device)
+    _perturb_state(a, 3)
+    _perturb_state(b, 3)
+    a.local_step()                      # penalty as the proximal gradient inside the Adam launch
+    # reference route on b: the same iteration with the penalty in the loss, then the plain sparse Adam step
+    b.iteration += 1
+    for g in b.opt.param_groups:
+        if g["name"] == "xyz":
+            g["lr"] = b.xyz_lr(b.iteration)
+    p = b.params
+    k = b._next_view()
+    gt = b.images[k]
+    m2d = torch.zeros_like(p["xyz"], requires_grad=True)
+    opac, scales, rots = b.activate(p["opacity"], p["scaling"], p["quaternion"])
+    img, radii, _ = b.rasts[k](means3D=p["xyz"], means2D=m2d, opacities=opac, dc=p["features_dc"],
+                               shs=p["features_rest"], scales=scales, rotations=rots)
+    img, l1 = b.clamp_l1(img, gt)
+    ssim = b.fused_ssim(img.unsqueeze(0), gt.unsqueeze(0))
+    c = b.cfg
+    loss = (1.0 - c.lambda_dssim) * l1 + c.lambda_dssim * (1.0 - ssim) + c.lambda_scale * scales.prod(dim=1).mean()
+    loss = loss + admm_penalty(b.param_tuple(), list(b.admm.u), b.admm.z, b.admm.rho)
+    loss.backward()
+    vis = radii > 0
+    b.opt.step(vis, radii.shape[0])
+    assert int(vis.sum()) > 100
+    for n in PARAM_NAMES:
+        ma = a.opt.state[a.params[n]]["exp_avg"]
+        mb = b.opt.state[b.params[n]]["exp_avg"]
+        err = float((ma - mb).norm() / mb.norm())
+        assert err < 1e-5, (n, err)
+        # rows outside the view: untouched by either route (SparseGaussianAdam ignores their gradient)
+        assert float(ma[~vis].abs().max()) == 0.0
+        torch.testing.assert_close(a.params[n].detach(), b.params[n].detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_device_consensus_residuals_penalty_match_host(hip_device):
+    from dogs_amd.admm import RHO_NAMES, ADMMConfig, initial_rho
+    from dogs_amd.admm_trainer import ADMMBlockState, InProcessConsensus, chain_block_indices
+    cfg = ADMMConfig()
+    g = torch.Generator().manual_seed(11)
+    n, f = 500, 0.3
+    idx = [chain_block_indices(k, n, f)[0] for k in range(3)]
+    ng = int(idx[-1][-1]) + 1
+    widths = (3, 3, 45, 3, 4, 1)
+    host = [tuple(torch.randn((n, w), generator=g) for w in widths) for _ in range(3)]
+    out = {}
+    for dev in (torch.device("cpu"), hip_device):
+        ps = [tuple(t.to(dev) for t in b) for b in host]
+        cons = InProcessConsensus([i.to(dev) for i in idx], ng, dev)
+        sts = [ADMMBlockState(p, ng, cfg) for p in ps]
+        moved = [tuple(t + 0.05 * (j + 1) for j, t in enumerate(p)) for p in ps]
+        zs = cons.consensus(moved)
+        for st, p, z in zip(sts, moved, zs):
+            st.update_duals(p, z)
+        rho = initial_rho(cfg, ng)
+        primal, dual = cons.residuals(moved, [s.z for s in sts], [s.z_prev for s in sts], rho)
+        pen = [float(s.penalty(p)) for s, p in zip(sts, moved)]
+        out[dev.type] = (zs, [s.u for s in sts], primal, dual, pen)
+    zc, uc, pc, dc, penc = out["cpu"]
+    zg, ug, pg, dg, peng = out["cuda"]
+    for a, b in zip(zc + uc, zg + ug):
+        for x, y in zip(a, b):
+            torch.testing.assert_close(x, y.cpu(), rtol=1e-6, atol=1e-6)
+    for k in RHO_NAMES:
+        assert abs(pc[k] - pg[k]) <= 1e-6 * max(abs(pc[k]), 1e-12)
+        assert abs(dc[k] - dg[k]) <= 1e-6 * max(abs(dc[k]), 1e-12)
+        assert pc[k] > 0.0 and dc[k] > 0.0
+    np.testing.assert_allclose(penc, peng, rtol=1e-5)
+
+
+def test_sequential_admm_two_blocks_gpu(hip_device):
+    from dogs_amd.admm import ADMMConfig
+    from dogs_amd.admm_trainer import sequential_trainer
+    cfg = ADMMConfig(consensus_interval=3, stop_adapt_iter=30003)
+    blocks, seq = sequential_trainer(2, 3000, 128, 96, 1, 0.25, hip_device, admm=cfg, seed=5)
+    logs = [seq.round() for _ in range(2)]
+    assert [lg.adapted for lg in logs] == [True, False]
+    for b in blocks:
+        assert torch.isfinite(b.last_loss)
+        assert all(torch.isfinite(p).all() for p in b.param_tuple())
+        assert torch.isfinite(b.penalty())
+    assert logs[0].primal["xyz"] > 0.0
