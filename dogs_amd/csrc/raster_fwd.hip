@@ -744,6 +744,122 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
     }
 }
 
+// Phase 2 of renderCUDA (forward.cu:441-591 over the rest of the list) for the tiles phase 1 left unfinished: one
+// 256-thread block per tile, one pixel per lane (wave w owns rows 4w..4w+3 of the tile).  These few tiles carry the
+// view's longest phase-2 lists (typically tiles that see only splats past the depth threshold) and run nearly alone
+// on the chip, so their latency is the cost: the block gathers the list in chunks of FWD2_CHUNK splats into LDS
+// with every thread's loads in flight at once (one dependent-load chain per chunk instead of one per 64 splats of a
+// lone wave), and each wave walks the chunk in branch-free groups of four splats (null-splat padding, as
+// k_render_fwd) with one pixel per lane.  The per-pixel arithmetic is k_render_fwd's (splat_exp_coeffs, the
+// splat_power4 operation order, the same accept / stop / update sequence), so the backward's replay reproduces
+// every decision.  Every splat of the list is evaluated (the quadrant test only skips splats no pixel accepts).
+constexpr int FWD2_CHUNK = 1024;
+template <bool COUNT>
+__global__ void __launch_bounds__(256) k_render_fwd2(RenderArgs a) {
+    __shared__ __attribute__((aligned(16))) float4 s_sb[(FWD2_CHUNK + 4) * 3];
+    __shared__ uint32_t s_mx[4];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tile = blockIdx.x;
+    // the adaptive capacity's probe gets this view's phase-2 instance count (the next view's k_depth_cut reads it)
+    if (a.probe && blockIdx.x == 0 && threadIdx.x == 0) a.probe[1] = a.counters[CNT_K2];
+    if (tile >= a.num_tiles || !a.unfinished[tile]) return;  // block-uniform: finished in phase 1
+    const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
+    const int px = tx * GS_TILE_X + (lane & 15), py = ty * GS_TILE_Y + 4 * w + (lane >> 4);
+    const bool inside = px < a.W && py < a.H;
+    const float pxf = (float)px, pyf = (float)py;
+    float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f, D = 0.0f, thr = 2.0f;
+    uint32_t last = 0;
+    const size_t pid = inside ? (size_t)py * a.W + px : 0;
+    if (inside) {  // resume the phase-1 state of this pixel
+        const float4 rs = a.resume[pid];
+        T = a.final_T[pid];
+        D = a.img_invd[pid];
+        last = a.n_contrib[pid];
+        C0 = rs.x; C1 = rs.y; C2 = rs.z; thr = rs.w;
+    }
+    const uint32_t cbase = a.ranges1[tile].y - a.ranges1[tile].x;
+    const uint2 rg = a.ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    for (int base = 0; base < n; base += FWD2_CHUNK) {
+        const int cnt = n - base < FWD2_CHUNK ? n - base : FWD2_CHUNK;
+        // the previous chunk is consumed by every wave; stop when every pixel of the tile has saturated
+        if (!__syncthreads_or(thr < 1.0f ? 1 : 0)) break;
+        for (int j = threadIdx.x; j < cnt + 4; j += 256) {
+            float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;  // past the end: the null splat (opacity 0)
+            if (j < cnt) {
+                const uint32_t e = min(a.s_e[rg.x + base + j], a.K - 1);
+                const uint32_t g = min(a.eg[e], a.P - 1);
+                const float4 s0 = a.sp[2 * g], s1 = a.sp[2 * g + 1];
+                const float4 q = a.rgbi[g];
+                const SplatExp k = splat_exp_coeffs(s0.z, s0.w, s1.x);
+                r0 = make_float4(s0.x, s0.y, k.A, k.B);
+                r1 = make_float4(k.C, s1.y, q.x, q.y);
+                r2 = make_float4(q.z, q.w, __uint_as_float(g), 0.0f);
+            }
+            s_sb[j * 3 + 0] = r0; s_sb[j * 3 + 1] = r1; s_sb[j * 3 + 2] = r2;
+        }
+        __syncthreads();
+        for (int j0 = 0; j0 < cnt; j0 += 4) {
+            if (!__any(thr < 1.0f)) break;  // every pixel of the wave saturated (or outside)
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int jj = j0 + u;
+                const float4 Sa = s_sb[jj * 3 + 0], Sb = s_sb[jj * 3 + 1], Sc = s_sb[jj * 3 + 2];
+                const float dy = Sa.y - pyf;
+                const float bdy = Sa.w * dy, cdy2 = (Sb.x * dy) * dy;
+                const float dx = Sa.x - pxf;
+                const float p2 = fmaf(dx, fmaf(Sa.z, dx, bdy), cdy2);
+                float al = Sb.y * __builtin_amdgcn_exp2f(p2);
+                // forward.cu:451-475: skip power > 0 and alpha < 1/255, stop once T would fall below 1e-4
+                const float ak = fminf(0.99f, al);
+                const bool acc = !(p2 > 0.0f || ak < thr);
+                al = acc ? ak : 0.0f;
+                const float test_T = T * (1.0f - al);
+                const bool term = test_T < 0.0001f;
+                thr = term ? 2.0f : thr;
+                al = term ? 0.0f : al;
+                const float Tn = term ? T : test_T;
+                last = (acc && !term) ? cbase + (uint32_t)(base + jj + 1) : last;
+                if (COUNT) {  // LightGaussian count mode: pixels the splat contributes to (old forward.cu:481-487)
+                    const uint32_t c = (uint32_t)__popcll(__ballot(acc && al != 0.0f));
+                    if (c && lane == 0) atomicAdd(a.gcount + __float_as_uint(Sc.z), c);
+                }
+                const float wt = al * T;
+                C0 = fmaf(Sb.z, wt, C0);
+                C1 = fmaf(Sb.w, wt, C1);
+                C2 = fmaf(Sc.x, wt, C2);
+                D = fmaf(Sc.y, wt, D);
+                T = Tn;
+            }
+        }
+    }
+    uint32_t mx = 0;
+    if (inside) {
+        const size_t HW = (size_t)a.W * a.H;
+        a.final_T[pid] = T;
+        a.n_contrib[pid] = last;
+        const float o0 = fmaf(T, a.bg[0], C0);
+        const float o1 = fmaf(T, a.bg[1], C1);
+        const float o2 = fmaf(T, a.bg[2], C2);
+        a.out_color[pid] = o0; a.out_color[HW + pid] = o1; a.out_color[2 * HW + pid] = o2;
+        a.img_color[pid] = o0; a.img_color[HW + pid] = o1; a.img_color[2 * HW + pid] = o2;
+        a.out_invd[pid] = D;
+        a.img_invd[pid] = D;
+        mx = last;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t y = __shfl_xor(mx, o);
+        mx = y > mx ? y : mx;
+    }
+    if (lane == 0) s_mx[w] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t m01 = s_mx[0] > s_mx[1] ? s_mx[0] : s_mx[1], m23 = s_mx[2] > s_mx[3] ? s_mx[2] : s_mx[3];
+        a.max_contrib[tile] = m01 > m23 ? m01 : m23;
+    }
+}
+
 // checkFrustum (rasterizer_impl.cu:104-116)
 __global__ void __launch_bounds__(256) k_mark_visible(int P, const float* __restrict__ means3D,
                                                       const float* __restrict__ view, bool* __restrict__ present) {
@@ -826,6 +942,13 @@ void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, 
 void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
     if (a.num_tiles <= 0) return;
     const int blocks = (a.num_tiles + 3) / 4;
+#ifndef DG_PHASE2_WAVE_PER_TILE  // A/B switch: phase 2 with k_render_fwd's one wave per tile
+    if (a.phase == 2) {
+        if (a.gcount) k_render_fwd2<true><<<a.num_tiles, 256, 0, s>>>(a);
+        else k_render_fwd2<false><<<a.num_tiles, 256, 0, s>>>(a);
+        return;
+    }
+#endif
     if (a.gcount) {
         if (a.phase == 2) k_render_fwd<2, true><<<blocks, 256, 0, s>>>(a);
         else k_render_fwd<1, true><<<blocks, 256, 0, s>>>(a);

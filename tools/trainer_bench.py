@@ -1,0 +1,64 @@
+"""Local-step time of the ADMM block trainer (dogs_amd.admm_trainer.BlockTrainer) on one GPU, with the host time per
+step, for kernel-trace profiling: python tools/trainer_bench.py [--n 1000000] [--steps 100]"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--views", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--cprofile", action="store_true", help="print the host profile of the timed steps")
+    ap.add_argument("--raster-only", action="store_true", help="time bench.py's raster view step instead")
+    args = ap.parse_args()
+    from dogs_amd.admm import ADMMConfig
+    from dogs_amd.admm_trainer import make_block
+    dev = torch.device("cuda", 0)
+    if args.raster_only:
+        import bench
+        from dogs_amd.synthetic import make_scene
+        s = make_scene(args.n, args.width, args.height, seed=1234).to(dev)
+        cams = bench.make_cameras(args.width, args.height, bench.view_yaws(args.views), dev)
+        g = torch.Generator().manual_seed(1234 + 99)
+        gc = torch.randn((3, args.height, args.width), generator=g).to(dev)
+        v = bench.Views(s, cams, gc, torch.zeros((1, args.height, args.width), device=dev), dev)
+        step = v.step
+    else:
+        tr, _, _ = make_block(0, 1, args.n, args.width, args.height, args.views, 0.0, dev, admm=ADMMConfig())
+        step = tr.local_step
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize()
+    host = []
+    prof = None
+    if args.cprofile:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        h = time.perf_counter()
+        step()
+        host.append(time.perf_counter() - h)
+    torch.cuda.synchronize()
+    if prof is not None:
+        prof.disable()
+        import pstats
+        pstats.Stats(prof).sort_stats("tottime").print_stats(30)
+    dt = (time.perf_counter() - t0) / args.steps
+    host.sort()
+    print(f"local step {dt * 1e3:.3f} ms ({1.0 / dt:.1f} views/s); host per step median {host[len(host) // 2] * 1e3:.3f}"
+          f" ms, min {host[0] * 1e3:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()
