@@ -169,6 +169,7 @@ class TrainStep:
         from dogs_amd.fused_ssim import fused_ssim
         from dogs_amd.loss import clamp_l1
         self.activate, self.clamp_l1, self.fused_ssim = activate, clamp_l1, fused_ssim
+        self.cams = cams
         self.rasts = [GaussianRasterizer(GaussianRasterizationSettings(
             c.height, c.width, c.tanfovx, c.tanfovy, torch.zeros(3, device=dev), 1.0, c.world_to_camera,
             c.projective_matrix, 3, c.camera_center, False, False, False, 0.0)) for c in cams]
@@ -202,11 +203,27 @@ class TrainStep:
                              scales=scales, rotations=rots)
         img, l1 = self.clamp_l1(img, self.gt)  # render()'s clamp + the L1 term, one launch each way
         ssim = self.fused_ssim(img.unsqueeze(0), self.gt.unsqueeze(0))
-        loss = 0.8 * l1 + 0.2 * (1.0 - ssim)
+        # gaussian_trainer.py:387-408: lambda_dssim 0.2, lambda_scale 0.05 (urban3d_admm.yaml loss block)
+        loss = 0.8 * l1 + 0.2 * (1.0 - ssim) + 0.05 * scales.prod(dim=1).mean()
         loss.backward()
         vis = radii > 0
         self.opt.step(vis, radii.shape[0], stats=dict(self.stats, radii=radii, dmeans2D=m2d.grad))
         self.opt.zero_grad(set_to_none=True)
+
+    def native(self):
+        """The same iteration through dg_train_step (dogs_amd.train_step): one C call per view."""
+        from dogs_amd.train_step import NativeTrainStep
+        p = self.params
+        params = {"xyz": p["xyz"], "features_dc": p["f_dc"], "features_rest": p["f_rest"], "opacity": p["opacity"],
+                  "scaling": p["scaling"], "quaternion": p["quaternion"]}
+        nts = NativeTrainStep(params, self.opt, self.cams, [self.gt] * len(self.cams), 3, 0.2, 0.05,
+                              torch.zeros(3, device=self.gt.device), self.gt.device, stats=self.stats)
+        state = {"i": 0}
+
+        def step():
+            nts.step(state["i"] % len(self.cams))
+            state["i"] += 1
+        return step
 
     def densify(self):
         """One densify_and_prune (urban3d.yaml thresholds: grad 2e-4, percent_dense 0.01, min opacity 0.005,
@@ -528,10 +545,22 @@ def main():
             ts.step()
         torch.cuda.synchronize()
         tms = (time.perf_counter() - tt) / nts * 1e3
+        nstep = ts.native()
+        for _ in range(len(cams)):
+            nstep()
+        torch.cuda.synchronize()
+        tt = time.perf_counter()
+        for _ in range(nts):
+            nstep()
+        torch.cuda.synchronize()
+        nms = (time.perf_counter() - tt) / nts * 1e3
         dms, n_after = ts.densify()
         train = {"views_per_s": round(1e3 / tms, 2), "ms_per_step": round(tms, 3),
-                 "includes": "activations + raster fwd/bwd + L1 + fused-SSIM fwd/bwd + densification stats + "
-                             "SparseGaussianAdam (one launch), cycling the view batch",
+                 "includes": "activations + raster fwd/bwd + L1 + fused-SSIM fwd/bwd + scale regulariser + "
+                             "densification stats + SparseGaussianAdam (one launch), cycling the view batch; "
+                             "autograd route (the drop-in API)",
+                 "native": {"views_per_s": round(1e3 / nms, 2), "ms_per_step": round(nms, 3),
+                            "route": "dg_train_step (dogs_amd.train_step): the same iteration in one C call"},
                  "densify_and_prune_ms": round(dms, 3), "gaussians_after_densify": n_after}
 
     admm = None

@@ -43,6 +43,12 @@ class DgDensifyStats(C.Structure):
                 ("max_radii2D", C.c_void_p), ("grad_accum", C.c_void_p), ("denom", C.c_void_p)]
 
 
+class DgTrainStepArgs(C.Structure):
+    _fields_ = [("view", DgRasterArgs), ("gt", C.c_void_p), ("lambda_dssim", C.c_float), ("lambda_scale", C.c_float),
+                ("groups", DgAdamGroup * 6), ("prox", DgAdamProx * 6), ("stats", C.c_void_p), ("radii", C.c_void_p),
+                ("image", C.c_void_p), ("loss", C.c_void_p)]
+
+
 class DgGaussianSet(C.Structure):
     _fields_ = [("N", C.c_uint32), ("params", C.c_void_p * 6), ("exp_avg", C.c_void_p * 6),
                 ("exp_avg_sq", C.c_void_p * 6), ("width", C.c_uint32 * 6), ("grad_accum", C.c_void_p),
@@ -77,7 +83,7 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count"
            "dg_add_densification_stats", "dg_densify_select", "dg_densify_split_stds", "dg_densify_count",
            "dg_densify_gather", "dg_splat_pack", "dg_ply_pack", "dg_ring_create", "dg_ring_submit", "dg_ring_next",
            "dg_ring_upload", "dg_ring_pending", "dg_ring_destroy", "dg_image_u8_to_chw", "dg_points_in_boxes2d", "dg_activate_forward", "dg_activate_backward", "dg_clamp_l1_blocks",
-           "dg_clamp_l1_forward", "dg_clamp_l1_backward", "dg_adaptive_capacity", "dg_debug_counters", "dg_adam_update_groups_prox",
+           "dg_clamp_l1_forward", "dg_clamp_l1_backward", "dg_adaptive_capacity", "dg_debug_counters", "dg_adam_update_groups_prox", "dg_train_step",
            "dg_last_error", "dg_version")
 
 _lib = None
@@ -131,6 +137,9 @@ def load(path: str | None = None):
         if hasattr(L, "dg_binned_instances"):  # introspection only; absent in older builds used for A/B runs
             L.dg_binned_instances.restype = C.c_int
             L.dg_binned_instances.argtypes = [vp, C.c_int, i64p, vp]
+        if hasattr(L, "dg_train_step"):
+            L.dg_train_step.restype = C.c_int
+            L.dg_train_step.argtypes = [C.POINTER(DgTrainStepArgs), ALLOC_FN, vp, vp]
         if hasattr(L, "dg_debug_counters"):
             L.dg_debug_counters.restype = C.c_int
             L.dg_debug_counters.argtypes = [vp, C.c_int, C.POINTER(C.c_uint32), vp]
@@ -266,6 +275,29 @@ class TensorArena:
 
     def get(self, which: int) -> torch.Tensor:
         return self.buffers.get(which, torch.empty(0, dtype=torch.uint8, device=self.device))
+
+
+class ReuseArena:
+    """dg_alloc_fn for a loop of same-shaped calls on one stream (the native training step): one grow-only uint8
+    tensor per buffer kind, handed out again while it is large enough.  Stream order makes the reuse safe: the next
+    call's kernels run after this call's on the same stream."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.buffers: dict[int, torch.Tensor] = {}
+
+        def _alloc(user, which, nbytes):  # noqa: ARG001
+            which, nbytes = int(which), max(int(nbytes), 1)
+            t = self.buffers.get(which)
+            if t is None or t.numel() < nbytes:
+                try:
+                    t = torch.empty(nbytes + nbytes // 4, dtype=torch.uint8, device=self.device)
+                except Exception:  # noqa: BLE001 - reported to C as NULL, surfaces as RuntimeError
+                    return None
+                self.buffers[which] = t
+            return t.data_ptr()
+
+        self.fn = ALLOC_FN(_alloc)
 
 
 def adaptive_capacity(W: int, H: int, reset: bool = False) -> int:

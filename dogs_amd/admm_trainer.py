@@ -127,7 +127,8 @@ class BlockTrainer:
     dogs_amd.camera.RasterCamera on the device; images: list of [3,H,W] float targets (same order)."""
 
     def __init__(self, raw: dict, cameras: list, images: list, num_global: int, admm: ADMMConfig,
-                 cfg: TrainConfig | None = None, device: torch.device | None = None, seed: int = 0):
+                 cfg: TrainConfig | None = None, device: torch.device | None = None, seed: int = 0,
+                 native: bool = True):
         from .diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer, SparseGaussianAdam
         from .activations import activate
         from .fused_ssim import fused_ssim
@@ -153,7 +154,24 @@ class BlockTrainer:
         self.order: list[int] = []
         self.iteration = c.start_iteration
         self.admm = ADMMBlockState(self.param_tuple(), num_global, admm)
-        self.last_loss = None
+        self._last_loss = None
+        self.cameras = cameras
+        self.native = native
+        if native:
+            from .train_step import NativeTrainStep
+            self._nts = NativeTrainStep({n: self.params[n] for n in PARAM_NAMES}, self.opt, cameras, images,
+                                        c.sh_degree, c.lambda_dssim, c.lambda_scale, bg, self.device)
+
+    @property
+    def last_loss(self):
+        """The last iteration's loss without the ADMM penalty (a device scalar)."""
+        if self.native and self._last_loss is None:
+            self._last_loss = self._nts.loss()
+        return self._last_loss
+
+    @property
+    def last_radii(self) -> torch.Tensor:
+        return self._nts.radii if self.native else self._last_radii
 
     def param_tuple(self) -> tuple:
         return tuple(self.params[n] for n in PARAM_NAMES)
@@ -164,8 +182,23 @@ class BlockTrainer:
             self.order = list(self.rng.permutation(len(self.rasts)))
         return int(self.order.pop())
 
-    def local_step(self) -> torch.Tensor:
-        """One training iteration; returns the loss without the penalty (a device scalar, no sync)."""
+    def local_step(self) -> None:
+        """One training iteration (native: one dg_train_step call; else the autograd route)."""
+        if not self.native:
+            self.local_step_autograd()
+            return
+        self.iteration += 1
+        lr = self.xyz_lr(self.iteration)
+        for g in self.opt.param_groups:
+            if g["name"] == "xyz":
+                g["lr"] = lr
+        self._nts.step(self._next_view(), lr, prox=self.admm.prox(self.param_tuple()))
+        self._last_loss = None
+
+    def local_step_autograd(self) -> torch.Tensor:
+        """One training iteration through the drop-in autograd API (the reference's route: rasterizer, clamp/L1 and
+        SSIM autograd functions, torch for the loss sum and the scale regulariser, SparseGaussianAdam with the
+        penalty's proximal gradient); returns the loss without the penalty (a device scalar, no sync)."""
         self.iteration += 1
         for g in self.opt.param_groups:
             if g["name"] == "xyz":
@@ -184,8 +217,9 @@ class BlockTrainer:
         loss.backward()
         self.opt.step(radii > 0, radii.shape[0], prox=self.admm.prox(self.param_tuple()))
         self.opt.zero_grad(set_to_none=True)
-        self.last_loss = loss.detach()
-        return self.last_loss
+        self._last_radii = radii
+        self._last_loss = loss.detach()
+        return self._last_loss
 
     def penalty(self) -> torch.Tensor:
         return self.admm.penalty(self.param_tuple())
@@ -349,7 +383,7 @@ def chain_block_indices(k: int, n: int, shared_frac: float) -> tuple[torch.Tenso
 
 
 def make_block(k: int, num_blocks: int, n: int, W: int, H: int, views: int, shared_frac: float, device,
-               seed: int = 1234, admm: ADMMConfig | None = None, cfg: TrainConfig | None = None):
+               seed: int = 1234, admm: ADMMConfig | None = None, cfg: TrainConfig | None = None, native: bool = True):
     """Block k of a synthetic chain split: the BASELINE generator's scene (one global scene, seed `seed`, of
     num_global Gaussians; block k takes its rows), `views` seeded yaw cameras and random target images."""
     from .camera import make_camera, yaw_world_to_camera
@@ -371,7 +405,7 @@ def make_block(k: int, num_blocks: int, n: int, W: int, H: int, views: int, shar
             for y in yaws]
     g = torch.Generator().manual_seed(seed + 7 + k)
     images = [torch.rand((3, H, W), generator=g).to(device) for _ in yaws]
-    tr = BlockTrainer(raw, cams, images, num_global, admm or ADMMConfig(), cfg, device, seed=seed + k)
+    tr = BlockTrainer(raw, cams, images, num_global, admm or ADMMConfig(), cfg, device, seed=seed + k, native=native)
     return tr, gidx, num_global
 
 

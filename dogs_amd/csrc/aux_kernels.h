@@ -8,7 +8,8 @@ namespace gs {
 void launch_ssim_fwd(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2, float* map,
                      float* dmu1, float* ds1, float* ds12, hipStream_t s);
 void launch_ssim_bwd(int B, int CH, int H, int W, const float* img1, const float* img2, const float* dL,
-                     const float* dmu1, const float* ds1, const float* ds12, float* dimg1, hipStream_t s);
+                     const float* dmu1, const float* ds1, const float* ds12, float* dimg1, hipStream_t s,
+                     float dl_value = 0.0f);
 void launch_adam(float* param, const float* grad, float* m, float* v, const bool* visible, float lr, float b1, float b2,
                  float eps, uint32_t N, uint32_t M, hipStream_t s);
 size_t knn_temp_bytes(int P);

@@ -140,8 +140,9 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
 
 __global__ void __launch_bounds__(256) k_ssim_bwd_strip(int H, int W, int planes, const float* __restrict__ img1,
                                                         const float* __restrict__ img2, const float* __restrict__ dL,
-                                                        const float* __restrict__ dmu1, const float* __restrict__ ds1,
-                                                        const float* __restrict__ ds12, float* __restrict__ dimg1) {
+                                                        float dl_value, const float* __restrict__ dmu1,
+                                                        const float* __restrict__ ds1, const float* __restrict__ ds12,
+                                                        float* __restrict__ dimg1) {
     const StripPos sp = strip_of(H, W, planes);
     if (!sp.valid) return;
     const int lane = threadIdx.x & 63;
@@ -152,7 +153,7 @@ __global__ void __launch_bounds__(256) k_ssim_bwd_strip(int H, int W, int planes
     auto ld3 = [&](int row, float& s0, float& s1, float& s2) {
         if (colok && row >= 0 && row < H) {
             const size_t gi = plane + (size_t)row * W + sp.x;
-            const float l = dL[gi];
+            const float l = dL ? dL[gi] : dl_value;  // dL == NULL: a uniform dL/dmap (the mean's backward)
             s0 = dmu1[gi] * l; s1 = ds1[gi] * l; s2 = ds12[gi] * l;
         } else {
             s0 = s1 = s2 = 0.0f;
@@ -212,10 +213,11 @@ void launch_ssim_fwd(int B, int CH, int H, int W, float C1, float C2, const floa
                                                         nullptr);
 }
 void launch_ssim_bwd(int B, int CH, int H, int W, const float* img1, const float* img2, const float* dL,
-                     const float* dmu1, const float* ds1, const float* ds12, float* dimg1, hipStream_t s) {
+                     const float* dmu1, const float* ds1, const float* ds12, float* dimg1, hipStream_t s,
+                     float dl_value) {
     if ((size_t)B * CH * H * W == 0) return;
-    k_ssim_bwd_strip<<<ssim_strip_blocks(B * CH, H, W), 256, 0, s>>>(H, W, B * CH, img1, img2, dL, dmu1, ds1, ds12,
-                                                                      dimg1);
+    k_ssim_bwd_strip<<<ssim_strip_blocks(B * CH, H, W), 256, 0, s>>>(H, W, B * CH, img1, img2, dL, dl_value, dmu1, ds1,
+                                                                      ds12, dimg1);
 }
 
 // ------------------------------------------------------------------------------------------------

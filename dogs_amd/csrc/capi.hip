@@ -777,6 +777,121 @@ int dg_adam_update_groups_prox(const dg_adam_group* groups, const dg_adam_prox* 
     return 0;
 }
 
+int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg_stream_t stream) {
+    if (!a || !a->gt || !a->radii || !a->image) return fail("train step: args, gt, radii and image are required%s%d");
+    hipStream_t s = (hipStream_t)stream;
+    const int P = a->view.P, W = a->view.W, H = a->view.H, M = a->view.M;
+    if (P <= 0 || W <= 0 || H <= 0) return fail("train step: empty model or image%s (P=%d)", "", P);
+    for (int k = 0; k < 6; k++)
+        if (!a->groups[k].param || !a->groups[k].exp_avg || !a->groups[k].exp_avg_sq)
+            return fail("train step: group %s%d lacks param or moments", "", k);
+    const size_t Pz = (size_t)P, Mz = (size_t)(M > 0 ? M : 0), n_img = 3 * (size_t)W * H, HW = (size_t)W * H;
+    if (n_img >= 0xffffff00ull) return fail("train step: image too large%s%d");
+    const uint32_t nb_l1 = gs::clamp_l1_blocks((uint32_t)n_img);
+    const uint32_t nb_map = gs::block_sum_blocks((uint32_t)n_img), nb_sc = gs::block_sum_blocks((uint32_t)P);
+    // ---- the step's scratch (DG_BUF_TRAIN); the nine rasterizer gradients back to back (the replay zero-fills them)
+    const size_t n9 = (3 + 3 + 1 + 3 + 6 + 3 + 3 * Mz + 3 + 4) * Pz;
+    auto carve = [&](void* base, float** f) {
+        Carver c(base);
+        f[0] = c.take<float>(Pz);          // opacity (activated)
+        f[1] = c.take<float>(3 * Pz);      // scaling
+        f[2] = c.take<float>(4 * Pz);      // rotation
+        f[3] = c.take<float>(n_img);       // raw render
+        f[4] = c.take<float>(HW);          // inverse depth
+        f[5] = c.take<float>(nb_l1 + nb_map + nb_sc);  // partial sums
+        f[6] = c.take<float>(n_img);       // SSIM map
+        f[7] = c.take<float>(n_img);       // dm/dmu1
+        f[8] = c.take<float>(n_img);       // dm/dsigma1_sq
+        f[9] = c.take<float>(n_img);       // dm/dsigma12
+        f[10] = c.take<float>(n_img);      // dL/dimage
+        f[11] = c.take<float>(n9);         // dmeans2D | dcolors | dopacity | dmeans3D | dcov3D | ddc | dsh | dscales | drot
+        f[12] = c.take<float>(Pz);         // depth
+        f[13] = c.take<float>(Pz);         // raw opacity grad
+        f[14] = c.take<float>(3 * Pz);     // raw scaling grad
+        f[15] = c.take<float>(4 * Pz);     // raw quaternion grad
+        return c.off;
+    };
+    float* f[16];
+    const size_t tbytes = carve(nullptr, f);
+    void* tbase = alloc(user, DG_BUF_TRAIN, tbytes);
+    if (!tbase) return fail("train step scratch allocation failed%s%d");
+    carve(tbase, f);
+    float *act_o = f[0], *act_s = f[1], *act_q = f[2], *color = f[3], *invd = f[4], *part = f[5];
+    float *map = f[6], *dmu1 = f[7], *ds1 = f[8], *ds12 = f[9], *dimg = f[10];
+    float* g9 = f[11];
+    float *dmeans2D = g9, *dcolors = dmeans2D + 3 * Pz, *dopac = dcolors + 3 * Pz, *dmeans3D = dopac + Pz;
+    float *dcov3D = dmeans3D + 3 * Pz, *ddc = dcov3D + 6 * Pz, *dsh = ddc + 3 * Pz, *dscales = dsh + 3 * Mz * Pz;
+    float* drot = dscales + 3 * Pz;
+    float *depth = f[12], *g_o = f[13], *g_s = f[14], *g_q = f[15];
+    const dg_adam_group* G = a->groups;  // xyz, f_dc, f_rest, opacity, scaling, quaternion
+    // ---- forward: activations, rasterizer, clamp + L1, SSIM
+    gs::launch_activate_fwd((uint32_t)P, G[3].param, G[4].param, G[5].param, act_o, act_s, act_q, s);
+    dg_raster_args r = a->view;
+    r.means3D = G[0].param; r.dc = G[1].param; r.sh = M > 0 ? G[2].param : nullptr;
+    r.opacities = act_o; r.scales = act_s; r.rotations = act_q; r.colors = nullptr; r.cov3D_precomp = nullptr;
+    void *geom = nullptr, *binning = nullptr, *image = nullptr, *binning2 = nullptr;
+    int64_t num_rendered = 0, num_instances = 0;
+    if (dg_rasterize_forward(&r, color, invd, a->radii, alloc, user, &geom, &binning, &image, &binning2,
+                             &num_rendered, &num_instances, stream))
+        return 1;
+    gs::launch_clamp_l1_fwd((uint32_t)n_img, color, a->gt, a->image, part, s);
+    const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;   // fused_ssim's constants
+    gs::launch_ssim_fwd(1, 3, H, W, C1, C2, a->image, a->gt, map, dmu1, ds1, ds12, s);
+    if (a->loss) {
+        gs::launch_block_sum(map, (uint32_t)n_img, 0, part + nb_l1, s);
+        gs::launch_block_sum(act_s, (uint32_t)P, 1, part + nb_l1 + nb_map, s);
+        gs::launch_loss_final(part, nb_l1, part + nb_l1, nb_map, part + nb_l1 + nb_map, nb_sc, (uint32_t)n_img,
+                              (uint32_t)P, a->loss, s);
+    }
+    // ---- backward of (1 - ld) L1 + ld (1 - SSIM) + ls mean(prod(scaling)): d/dmap = -ld / n (the mean's backward)
+    const float ld = a->lambda_dssim;
+    gs::launch_ssim_bwd(1, 3, H, W, a->image, a->gt, nullptr, dmu1, ds1, ds12, map, s, (-ld) / (float)n_img);
+    gs::launch_clamp_l1_bwd((uint32_t)n_img, color, a->image, a->gt, map, nullptr, dimg, s,
+                            (float)(1.0 - (double)ld));
+    if (dg_rasterize_backward(&r, a->radii, geom, binning, image, binning2, num_rendered, num_instances, dimg, nullptr,
+                              dmeans2D, dcolors, dopac, dmeans3D, dcov3D, ddc, dsh, dscales, drot, depth, alloc, user,
+                              stream))
+        return 1;
+    gs::launch_activate_bwd((uint32_t)P, act_o, act_s, G[5].param, dopac, dscales, drot, g_o, g_s, g_q, s,
+                            a->lambda_scale / (float)P);
+    // ---- SparseGaussianAdam.step(radii > 0) over the six groups, ADMM proximal gradient, densification statistics
+    dg_adam_group groups[6];
+    const float* grads[6] = {dmeans3D, ddc, dsh, g_o, g_s, g_q};
+    for (int k = 0; k < 6; k++) {
+        groups[k] = G[k];
+        groups[k].grad = grads[k];
+    }
+    if (M <= 0) groups[2].M = 0;  // no rest coefficients: nothing to update
+    gs::AdamMultiArgs m;
+    memset(&m, 0, sizeof(m));
+    m.visible = nullptr; m.vis_radii = a->radii; m.N = (uint32_t)P; m.b1 = 0.9f; m.b2 = 0.999f;
+    int n = 0;
+    for (int k = 0; k < 6; k++) {
+        const dg_adam_group& g = groups[k];
+        if (g.M == 0) continue;
+        if ((uint64_t)P * g.M >= 0xfffff000ull) return fail("train step: group %s%d has N * M >= 2^32", "", k);
+        gs::AdamGroup& d = m.g[n++];
+        d.param = g.param; d.grad = g.grad; d.m = g.exp_avg; d.v = g.exp_avg_sq; d.lr = g.lr; d.eps = g.eps; d.M = g.M;
+        uintptr_t al = reinterpret_cast<uintptr_t>(g.param) | reinterpret_cast<uintptr_t>(g.grad) |
+                       reinterpret_cast<uintptr_t>(g.exp_avg) | reinterpret_cast<uintptr_t>(g.exp_avg_sq);
+        if (a->prox[k].u) {
+            if (!a->prox[k].z) return fail("train step: group %s%d has prox u without z", "", k);
+            d.u = a->prox[k].u; d.z = a->prox[k].z; d.coef = a->prox[k].coef;
+            al |= reinterpret_cast<uintptr_t>(a->prox[k].u) | reinterpret_cast<uintptr_t>(a->prox[k].z);
+        }
+        d.vec = (al & 15u) == 0u;
+    }
+    m.n = n;
+    if (a->stats) {
+        dg_densify_stats st = *a->stats;
+        st.radii = a->radii; st.dmeans2D = dmeans2D; st.dmeans2D_stride = 3;
+        if (fill_stats(m, &st)) return 1;
+    }
+    gs::launch_adam_multi(m, s);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
 int dg_add_densification_stats(const dg_densify_stats* stats, const uint8_t* visible, uint32_t N, dg_stream_t stream) {
     if (!stats) return fail("stats required%s%d");
     return dg_adam_update_groups(nullptr, 0, visible, N, 0.9f, 0.999f, stats, stream);

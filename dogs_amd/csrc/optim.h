@@ -29,7 +29,8 @@ struct AdamMultiArgs {
     AdamGroup g[MAX_ADAM_GROUPS];
     uint32_t start[MAX_ADAM_GROUPS + 2];  // first work item of group k (items = 4-float chunks); start[n] = stats
     int n;
-    const uint8_t* visible;  // [N]
+    const uint8_t* visible;  // [N]; NULL: visible = vis_radii > 0
+    const int* vis_radii;    // [N]
     uint32_t N;
     float b1, b2;
     // densification statistics (optional: radii == nullptr)
@@ -44,11 +45,16 @@ void launch_adam_multi(const AdamMultiArgs& a, hipStream_t s);
 uint32_t clamp_l1_blocks(uint32_t n);
 void launch_clamp_l1_fwd(uint32_t n, const float* img, const float* gt, float* out, float* partial, hipStream_t s);
 void launch_clamp_l1_bwd(uint32_t n, const float* img, const float* clamped, const float* gt, const float* g_img,
-                         const float* g_l1, float* d_img, hipStream_t s);
+                         const float* g_l1, float* d_img, hipStream_t s, float g_l1_value = 0.0f);
+uint32_t block_sum_blocks(uint32_t n);
+void launch_block_sum(const float* x, uint32_t n, int mode, float* partial, hipStream_t s);
+void launch_loss_final(const float* p_l1, uint32_t n_l1, const float* p_ssim, uint32_t n_ssim, const float* p_sc,
+                       uint32_t n_sc, uint32_t n_img, uint32_t P, float* loss, hipStream_t s);
 void launch_activate_fwd(uint32_t N, const float* ro, const float* rs, const float* rq, float* o, float* sc, float* q,
                          hipStream_t s);
 void launch_activate_bwd(uint32_t N, const float* o, const float* sc, const float* rq, const float* go,
-                         const float* gsc, const float* gq, float* dro, float* drs, float* drq, hipStream_t s);
+                         const float* gsc, const float* gq, float* dro, float* drs, float* drq, hipStream_t s,
+                         float scale_reg = 0.0f);
 
 // ---- densify_and_prune
 struct DensifyArgs {

@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
     const uint32_t blk = blockIdx.x;
     if (blk >= a.start[a.n]) {  // densification statistics, one Gaussian per lane
         const uint32_t i = (blk - a.start[a.n]) * 256u + threadIdx.x;
-        if (i >= a.N || !a.visible[i]) return;
+        if (i >= a.N || !(a.visible ? a.visible[i] != 0 : a.vis_radii[i] > 0)) return;
         // max_radii2D[vis] = max(max_radii2D[vis], radii[vis]) (float result: radii promote to float)
         const float r = (float)a.radii[i];
         const float mr = a.max_radii2D[i];
@@ -76,7 +76,7 @@ __global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
         uint32_t gi = e0 / g.M, r = e0 - gi * g.M;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            vis[c][j] = e0 + j < total && a.visible[gi] != 0;
+            vis[c][j] = e0 + j < total && (a.visible ? a.visible[gi] != 0 : a.vis_radii[gi] > 0);
             act[c] |= vis[c][j];
             if (++r == g.M) { r = 0; gi++; }
         }
@@ -289,7 +289,8 @@ __global__ void __launch_bounds__(256) k_activate_bwd(uint32_t N, const float* _
                                                       const float* __restrict__ sc, const float* __restrict__ rq,
                                                       const float* __restrict__ go, const float* __restrict__ gs_,
                                                       const float* __restrict__ gq, float* __restrict__ dro,
-                                                      float* __restrict__ drs, float* __restrict__ drq) {
+                                                      float* __restrict__ drs, float* __restrict__ drq,
+                                                      float scale_reg) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= N) return;
     if (go) {
@@ -298,7 +299,19 @@ __global__ void __launch_bounds__(256) k_activate_bwd(uint32_t N, const float* _
     } else {
         dro[i] = 0.0f;
     }
-    for (int k = 0; k < 3; k++) drs[3 * (size_t)i + k] = gs_ ? gs_[3 * (size_t)i + k] * sc[3 * (size_t)i + k] : 0.0f;
+    if (scale_reg != 0.0f) {
+        // the native step's scale regulariser lambda_scale mean(prod(scaling, 1)) (gaussian_trainer.py:407-408):
+        // its gradient on scaling j, scale_reg prod / s_j (scale_reg = lambda_scale / N), joins the rasterizer's
+        // before exp's backward
+        const float* sv = sc + 3 * (size_t)i;
+        const float prod = (sv[0] * sv[1]) * sv[2];
+        for (int k = 0; k < 3; k++) {
+            const float g = (gs_ ? gs_[3 * (size_t)i + k] : 0.0f) + scale_reg * (prod / sv[k]);
+            drs[3 * (size_t)i + k] = g * sv[k];
+        }
+    } else {
+        for (int k = 0; k < 3; k++) drs[3 * (size_t)i + k] = gs_ ? gs_[3 * (size_t)i + k] * sc[3 * (size_t)i + k] : 0.0f;
+    }
     float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
     if (gq) {
         const float4 x = reinterpret_cast<const float4*>(rq)[i];
@@ -355,10 +368,11 @@ __global__ void __launch_bounds__(256) k_clamp_l1_fwd(uint32_t n, const float* _
 __global__ void __launch_bounds__(256) k_clamp_l1_bwd(uint32_t n, const float* __restrict__ img,
                                                       const float* __restrict__ clamped, const float* __restrict__ gt,
                                                       const float* __restrict__ g_img, const float* __restrict__ g_l1,
-                                                      float* __restrict__ d_img) {
+                                                      float g_l1_value, float* __restrict__ d_img) {
     const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
-    const float s = g_l1 ? g_l1[0] / (float)n : 0.0f;
+    // the L1 term's incoming gradient: a device scalar (autograd) or a value (the native step; 0 = no L1 term)
+    const float s = (g_l1 ? g_l1[0] : g_l1_value) / (float)n;
     const float x = img[i], d = clamped[i] - gt[i];
     const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
     const float g = (g_img ? g_img[i] : 0.f) + s * sg;
@@ -410,8 +424,9 @@ void launch_activate_fwd(uint32_t N, const float* ro, const float* rs, const flo
     if (N) k_activate_fwd<<<(N + 255) / 256, 256, 0, s>>>(N, ro, rs, rq, o, sc, q);
 }
 void launch_activate_bwd(uint32_t N, const float* o, const float* sc, const float* rq, const float* go,
-                         const float* gsc, const float* gq, float* dro, float* drs, float* drq, hipStream_t s) {
-    if (N) k_activate_bwd<<<(N + 255) / 256, 256, 0, s>>>(N, o, sc, rq, go, gsc, gq, dro, drs, drq);
+                         const float* gsc, const float* gq, float* dro, float* drs, float* drq, hipStream_t s,
+                         float scale_reg) {
+    if (N) k_activate_bwd<<<(N + 255) / 256, 256, 0, s>>>(N, o, sc, rq, go, gsc, gq, dro, drs, drq, scale_reg);
 }
 
 uint32_t clamp_l1_blocks(uint32_t n) { return (n + 256u * L1_PER_THREAD - 1) / (256u * L1_PER_THREAD); }
@@ -419,8 +434,47 @@ void launch_clamp_l1_fwd(uint32_t n, const float* img, const float* gt, float* o
     if (n) k_clamp_l1_fwd<<<clamp_l1_blocks(n), 256, 0, s>>>(n, img, gt, out, partial);
 }
 void launch_clamp_l1_bwd(uint32_t n, const float* img, const float* clamped, const float* gt, const float* g_img,
-                         const float* g_l1, float* d_img, hipStream_t s) {
-    if (n) k_clamp_l1_bwd<<<(n + 255) / 256, 256, 0, s>>>(n, img, clamped, gt, g_img, g_l1, d_img);
+                         const float* g_l1, float* d_img, hipStream_t s, float g_l1_value) {
+    if (n) k_clamp_l1_bwd<<<(n + 255) / 256, 256, 0, s>>>(n, img, clamped, gt, g_img, g_l1, g_l1_value, d_img);
+}
+
+// Sum of x[0..n) (mode 0) or of the row products x[3i] x[3i+1] x[3i+2] over n rows (mode 1: the scale
+// regulariser's prod(scaling, 1)) into one partial per 256-thread block; k_loss_final totals the partials in order.
+__global__ void __launch_bounds__(256) k_block_sum(const float* __restrict__ x, uint32_t n, int mode,
+                                                   float* __restrict__ partial) {
+    __shared__ float s_w[4];
+    float acc = 0.0f;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u)
+        acc += mode ? (x[3 * (size_t)i] * x[3 * (size_t)i + 1]) * x[3 * (size_t)i + 2] : x[i];
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[blockIdx.x] = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);
+}
+// loss[0] = L1 (mean |clamped - gt|), loss[1] = SSIM (mean of the map), loss[2] = mean prod(scaling, 1)
+__global__ void __launch_bounds__(64) k_loss_final(const float* __restrict__ p_l1, uint32_t n_l1,
+                                                   const float* __restrict__ p_ssim, uint32_t n_ssim,
+                                                   const float* __restrict__ p_sc, uint32_t n_sc, uint32_t n_img,
+                                                   uint32_t P, float* __restrict__ loss) {
+    const float* ps[3] = {p_l1, p_ssim, p_sc};
+    const uint32_t ns[3] = {n_l1, n_ssim, n_sc};
+    for (int k = 0; k < 3; k++) {
+        float acc = 0.0f;
+        for (uint32_t i = threadIdx.x; i < ns[k]; i += 64) acc += ps[k][i];
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if (threadIdx.x == 0) loss[k] = acc / (float)(k == 2 ? P : n_img);
+    }
+}
+uint32_t block_sum_blocks(uint32_t n) {
+    const uint32_t b = (n + 255) / 256;
+    return b < 1024u ? (b ? b : 1u) : 1024u;
+}
+void launch_block_sum(const float* x, uint32_t n, int mode, float* partial, hipStream_t s) {
+    k_block_sum<<<block_sum_blocks(n), 256, 0, s>>>(x, n, mode, partial);
+}
+void launch_loss_final(const float* p_l1, uint32_t n_l1, const float* p_ssim, uint32_t n_ssim, const float* p_sc,
+                       uint32_t n_sc, uint32_t n_img, uint32_t P, float* loss, hipStream_t s) {
+    k_loss_final<<<1, 64, 0, s>>>(p_l1, n_l1, p_ssim, n_ssim, p_sc, n_sc, n_img, P, loss);
 }
 
 }  // namespace gs

@@ -1,0 +1,119 @@
+"""The native training step (dg_train_step): one GaussianSplatTrainer.train_iteration after densify_end_iter
+(gaussian_trainer.py:324-476) -- activations, rasterizer forward, render()'s clamp + L1, fused SSIM, the loss
+gradient, rasterizer backward, the scale regulariser, activation backward and SparseGaussianAdam (with an ADMM block
+trainer's proximal gradient and the densification statistics when given) -- as one C call.
+
+It runs the kernels of the autograd route with the same arithmetic (tests/test_gpu_admm.py compares the two), but
+the host issues ~15 launches after the forward's one wait instead of ~100 Python-level operations, so the GPU does
+not wait for the host between views.  The per-view argument blocks are built once; a step rewrites only the view's
+learning rate, the proximal pointers and the depth-prefix policy."""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+
+# setup_optimizer's group order (gaussian_trainer.py:205-230), which dg_train_step_args.groups follows
+C_ORDER = ("xyz", "features_dc", "features_rest", "opacity", "scaling", "quaternion")
+GROUP_NAME = {"xyz": "xyz", "features_dc": "f_dc", "features_rest": "f_rest", "opacity": "opacity",
+              "scaling": "scaling", "quaternion": "quaternion"}
+
+
+class NativeTrainStep:
+    """params: {name: leaf tensor} for the six raw tensors (C_ORDER names); opt: the SparseGaussianAdam holding them
+    (its exp_avg / exp_avg_sq state is created here when absent, the tensors the autograd route would create);
+    cameras / images: the views (dogs_amd.camera.RasterCamera on the device, [3,H,W] targets); stats (optional):
+    {max_radii2D, grad_accum, denom} updated each step (gaussian_trainer.py:433-438)."""
+
+    def __init__(self, params: dict, opt, cameras: list, images: list, sh_degree: int, lambda_dssim: float,
+                 lambda_scale: float, bg: torch.Tensor, device: torch.device, stats: dict | None = None):
+        self.L = _lib.load()
+        self.device = device
+        self.params = params
+        self.arena = _lib.ReuseArena(device)
+        P = int(params["xyz"].shape[0])
+        rest = params["features_rest"]
+        M = int(rest.shape[1]) if rest.dim() == 3 else 0
+        self.lambdas = (float(lambda_dssim), float(lambda_scale))
+        self.radii = torch.zeros(P, dtype=torch.int32, device=device)
+        self.loss_buf = torch.zeros(3, dtype=torch.float32, device=device)
+        self.bg = bg.to(device=device, dtype=torch.float32).contiguous()
+        self.images_out = {}
+        self.keep = [self.bg, cameras, images]
+        for n in C_ORDER:
+            p = params[n]
+            if not (p.is_contiguous() and p.dtype == torch.float32 and p.device == device):
+                raise RuntimeError(f"native step: {n} must be a contiguous float32 tensor on {device}")
+            st = opt.state[p]
+            if len(st) == 0:
+                st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        groups = {g["name"]: g for g in opt.param_groups}
+        self.stats = None
+        if stats is not None:
+            for k in ("max_radii2D", "grad_accum", "denom"):
+                t = stats[k]
+                if not (t.is_contiguous() and t.dtype == torch.float32 and t.device == device):
+                    raise RuntimeError(f"native step: {k} must be a contiguous float32 tensor on {device}")
+            self.stats = _lib.DgDensifyStats(None, None, 3, stats["max_radii2D"].data_ptr(),
+                                             stats["grad_accum"].data_ptr(), stats["denom"].data_ptr())
+            self.keep.append(stats)
+        self.args = []
+        for cam, gt in zip(cameras, images):
+            for t in (cam.world_to_camera, cam.projective_matrix, cam.camera_center, gt):
+                if not (t.is_contiguous() and t.dtype == torch.float32 and t.device == device):
+                    raise RuntimeError("native step: cameras and targets must be contiguous float32 on the device")
+            a = _lib.DgTrainStepArgs()
+            v = a.view
+            v.P, v.D, v.M, v.W, v.H = P, int(sh_degree), M, int(cam.width), int(cam.height)
+            v.prefiltered, v.antialiasing, v.debug = 0, 0, 0
+            v.scale_modifier, v.tanfovx, v.tanfovy = 1.0, float(cam.tanfovx), float(cam.tanfovy)
+            v.bg, v.viewmatrix = self.bg.data_ptr(), cam.world_to_camera.data_ptr()
+            v.projmatrix, v.campos = cam.projective_matrix.data_ptr(), cam.camera_center.data_ptr()
+            a.gt = gt.data_ptr()
+            a.lambda_dssim, a.lambda_scale = self.lambdas
+            for i, n in enumerate(C_ORDER):
+                p = params[n]
+                st = opt.state[p]
+                g = groups[GROUP_NAME[n]]
+                a.groups[i] = _lib.DgAdamGroup(p.data_ptr(), None, st["exp_avg"].data_ptr(),
+                                               st["exp_avg_sq"].data_ptr(), float(g["lr"]), float(g["eps"]),
+                                               int(p.numel() // P))
+            key = (int(cam.height), int(cam.width))
+            if key not in self.images_out:
+                self.images_out[key] = torch.empty((3, key[0], key[1]), dtype=torch.float32, device=device)
+            a.radii, a.image, a.loss = self.radii.data_ptr(), self.images_out[key].data_ptr(), self.loss_buf.data_ptr()
+            a.stats = C.addressof(self.stats) if self.stats is not None else None
+            self.args.append(a)
+        self.stream = _lib.stream_of(device)
+        self.last_view = None
+
+    def step(self, k: int, xyz_lr: float | None = None, prox: dict | None = None) -> None:
+        """One iteration on view k; prox: {group name: (u, z, coef)} (ADMMBlockState.prox) or None."""
+        from .diff_gaussian_rasterization import _C
+        a = self.args[k]
+        a.view.prefix_per_tile = int(_C.PREFIX_PER_TILE)
+        if xyz_lr is not None:
+            a.groups[0].lr = float(xyz_lr)
+        for i, n in enumerate(C_ORDER):
+            if prox is None:
+                a.prox[i].u = a.prox[i].z = None
+                continue
+            u, z, coef = prox[GROUP_NAME[n]]
+            a.prox[i].u, a.prox[i].z, a.prox[i].coef = u.data_ptr(), z.data_ptr(), float(coef)
+        _lib.check(self.L.dg_train_step(C.byref(a), self.arena.fn, None, self.stream))
+        self.last_view = k
+
+    def image(self, k: int | None = None) -> torch.Tensor:
+        """The clamped render of the last step (shared buffer per image size)."""
+        c = self.keep[1][self.last_view if k is None else k]
+        return self.images_out[(int(c.height), int(c.width))]
+
+    def loss(self) -> torch.Tensor:
+        """(1 - ld) L1 + ld (1 - SSIM) + ls mean(prod(scaling)) of the last step, a device scalar."""
+        ld, ls = self.lambdas
+        L1, ssim, sc = self.loss_buf[0], self.loss_buf[1], self.loss_buf[2]
+        return (1.0 - ld) * L1 + ld * (1.0 - ssim) + ls * sc

@@ -166,6 +166,31 @@ typedef struct {
 int dg_adam_update_groups_prox(const dg_adam_group* groups, const dg_adam_prox* prox, int n_groups,
                                const uint8_t* visible, uint32_t N, float b1, float b2, const dg_densify_stats* stats,
                                dg_stream_t stream);
+/* ---- the native training step of a block trainer (dogs_amd.admm_trainer.BlockTrainer's fast path) ----
+ * One GaussianSplatTrainer.train_iteration after densify_end_iter (gaussian_trainer.py:324-476) with the ADMM
+ * penalty of SlaveGaussianSplatTrainer.add_admm_penalties (slave_gaussian_trainer.py:161-202), as one call:
+ *   activations (get_opacity / get_scaling / get_quaternion) -> dg_rasterize_forward -> clamp(0, 1) + L1
+ *   -> fused SSIM -> dL/dimage of (1 - lambda_dssim) L1 + lambda_dssim (1 - SSIM) -> dg_rasterize_backward
+ *   -> lambda_scale mean(prod(scaling, 1)) + activation backward -> SparseGaussianAdam.step(radii > 0) with the ADMM
+ *   proximal gradient and the densification statistics, one launch.
+ * The kernels and arithmetic of the autograd path (the drop-in API), issued from C: after the forward's one wait the
+ * host enqueues ~15 launches instead of ~100 Python-level operations, so the GPU does not wait on the host.
+ * Allocates DG_BUF_GEOM/IMAGE/BINNING(2)/BACKWARD as the rasterizer does, and DG_BUF_TRAIN (the step's scratch). */
+enum { DG_BUF_TRAIN = 9 };
+typedef struct {
+    dg_raster_args view;        /* camera, image size and settings; its Gaussian pointers are ignored */
+    const float* gt;            /* [3,H,W] target image */
+    float lambda_dssim, lambda_scale;
+    /* the model's six raw tensors, in place, in setup_optimizer's order: xyz [P,3], f_dc [P,1,3], f_rest [P,M,3],
+     * opacity [P,1] (logit), scaling [P,3] (log), quaternion [P,4]; with Adam moments, lr and eps (grad ignored) */
+    dg_adam_group groups[6];
+    dg_adam_prox prox[6];       /* ADMM penalty per tensor; u == NULL: none */
+    const dg_densify_stats* stats;  /* optional; only max_radii2D / grad_accum / denom are read */
+    int* radii;                 /* [P] out */
+    float* image;               /* [3,H,W] out: the clamped render */
+    float* loss;                /* optional, device [3] out: L1, SSIM, mean prod(scaling) of this view */
+} dg_train_step_args;
+int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg_stream_t stream);
 /* The statistics alone (replaces the max_radii2D update + add_densification_stats of gaussian_trainer.py:433-438). */
 int dg_add_densification_stats(const dg_densify_stats* stats, const uint8_t* visible, uint32_t N, dg_stream_t stream);
 
