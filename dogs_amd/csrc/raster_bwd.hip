@@ -64,6 +64,82 @@ __device__ __forceinline__ float wave_reduce10(const float (&p)[10], int lane, i
     return u;
 }
 
+// One splat of the replay for the lane's four pixels: exponent, acceptance, the regrouped dL/dalpha terms, the 10
+// moments and their wave reduction into the instance's record.  PER_SPLAT_LAST: test "splat index < last contributor"
+// per pixel; otherwise athr already holds it (1/255 alive, 2 dead).
+template <bool HAS_INVD, bool HAS_BG, bool PER_SPLAT_LAST>
+__device__ __forceinline__ void replay_splat(const RenderBwdArgs& a, const float4* sb, int jj, int sidx, const v4f pxv,
+                                             const v2f pyv, const int (&last)[4], const v4f athr, const v4f g0,
+                                             const v4f g1, const v4f g2, const v4f gd, const v4f ntb, v4f& T, v4f& S,
+                                             int lane) {
+    const float4 Sa = sb[jj * 3 + 0], Sb = sb[jj * 3 + 1], Sc = sb[jj * 3 + 2];
+    const float sx = Sa.x, sy = Sa.y, so = Sb.y, sr = Sb.z, sg = Sb.w, sbl = Sc.x, si = Sc.y;
+    // exponent, identical to the forward's splat_power4
+    const v2f dy = bc2(sy) - pyv;
+    const v4f dx = bc4(sx) - pxv;
+    const v2f bdy = bc2(Sa.w) * dy, cdy2 = (bc2(Sb.x) * dy) * dy;
+    const v4f p2 = fma4(dx, fma4(bc4(Sa.z), dx, cat4(bdy, bdy)), cat4(cdy2, cdy2));
+    const v4f G = {__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y), __builtin_amdgcn_exp2f(p2.z),
+                   __builtin_amdgcn_exp2f(p2.w)};
+    v4f al = bc4(so) * G;
+    bool ok[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const float ak = fminf(0.99f, al[k]);
+        ok[k] = PER_SPLAT_LAST ? (sidx < last[k]) && !(p2[k] > 0.0f) && !(ak < athr[k])
+                               : !(p2[k] > 0.0f) && !(ak < athr[k]);
+        al[k] = ok[k] ? ak : 0.0f;
+    }
+    const v4f wgt = al * T;
+    const v4f oma = bc4(1.0f) - al;
+    const v4f inv = {__builtin_amdgcn_rcpf(oma.x), __builtin_amdgcn_rcpf(oma.y), __builtin_amdgcn_rcpf(oma.z),
+                     __builtin_amdgcn_rcpf(oma.w)};
+    v4f cg = fma4(bc4(sbl), g2, fma4(bc4(sg), g1, bc4(sr) * g0));
+    if (HAS_INVD) cg = fma4(bc4(si), gd, cg);
+    S = fma4(wgt, cg, S);
+    v4f dLda = fma4(cg, T, inv * S);
+    if (HAS_BG) dLda = fma4(ntb, inv, dLda);
+#pragma unroll
+    for (int k = 0; k < 4; k++) dLda[k] = ok[k] ? dLda[k] : 0.0f;
+    T = T * oma;
+    // per-splat moments over the lane's 4 pixels; lo + hi of a v4 = the two row sums {row A, row B}
+    const v4f t4 = G * dLda;
+    const v4f tdx = t4 * dx;
+    const v4f tdx2 = tdx * dx;
+    const v2f rt = (v2f){t4.x, t4.y} + (v2f){t4.z, t4.w};
+    const v2f rtx = (v2f){tdx.x, tdx.y} + (v2f){tdx.z, tdx.w};
+    const v2f rtxx = (v2f){tdx2.x, tdx2.y} + (v2f){tdx2.z, tdx2.w};
+    const v4f w0 = wgt * g0, w1 = wgt * g1, w2 = wgt * g2;
+    const v2f rc0 = (v2f){w0.x, w0.y} + (v2f){w0.z, w0.w};
+    const v2f rc1 = (v2f){w1.x, w1.y} + (v2f){w1.z, w1.w};
+    const v2f rc2 = (v2f){w2.x, w2.y} + (v2f){w2.z, w2.w};
+    const v2f u = rt * dy;  // {tA dyA, tB dyB}
+    float p[10];
+    p[0] = rtx.x + rtx.y;                            // SGx
+    p[1] = u.x + u.y;                                // SGy
+    p[2] = rtxx.x + rtxx.y;                          // SGxx
+    p[3] = fmaf(rtx.x, dy.x, rtx.y * dy.y);          // SGxy
+    p[4] = fmaf(u.x, dy.x, u.y * dy.y);              // SGyy
+    p[5] = rt.x + rt.y;                              // SG
+    p[6] = rc0.x + rc0.y;
+    p[7] = rc1.x + rc1.y;
+    p[8] = rc2.x + rc2.y;
+    if (HAS_INVD) {
+        const v4f wd = wgt * gd;
+        const v2f rcd = (v2f){wd.x, wd.y} + (v2f){wd.z, wd.w};
+        p[9] = rcd.x + rcd.y;
+    } else {
+        p[9] = 0.0f;
+    }
+    if (__any(ok[0] || ok[1] || ok[2] || ok[3])) {
+        int slot;
+        const float tot = wave_reduce10(p, lane, slot);
+        const uint32_t e = __builtin_amdgcn_readfirstlane(__float_as_uint(Sc.z));
+        if (slot >= 0) a.rec[(size_t)e * 12 + slot] = tot;
+        if (lane == 0) a.flag[e] = 1;
+    }
+}
+
 // Front-to-back replay.  Lane l owns pixels (l&7, l>>3) and (l&7 + 8, l>>3) of the tile's top half
 // (pair A = quadrants 0,1) and the same two of the bottom half (pair B = quadrants 2,3); each pair is
 // one row, evaluated with packed fp32.  Per 64-splat batch each lane stages its splat in wave-private
@@ -161,75 +237,32 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
         }
         __builtin_amdgcn_wave_barrier();
         uint64_t smask = __ballot(qm != 0u);
+#ifndef DG_BWD_NO_BATCH_ALIVE
+        // A pixel's last contributor lies inside this batch for few pixels: when it lies outside for every pixel of
+        // the wave, "splat index < last" is constant over the batch and folds into the acceptance threshold (2 > any
+        // alpha: dead), as the forward's; otherwise the per-splat test.
+        bool straddle = false;
+#pragma unroll
+        for (int k = 0; k < 4; k++) straddle |= last[k] > base && last[k] < base + 64;
+        if (!__any(straddle)) {
+            v4f athr;
+#pragma unroll
+            for (int k = 0; k < 4; k++) athr[k] = last[k] > base ? (1.0f / 255.0f) : 2.0f;
+            while (smask) {
+                const int jj = (int)__builtin_ctzll(smask);
+                smask &= smask - 1;
+                replay_splat<HAS_INVD, HAS_BG, false>(a, sb, jj, base + jj, pxv, pyv, last, athr, g0, g1, g2, gd, ntb, T, S,
+                                                       lane);
+            }
+            __builtin_amdgcn_wave_barrier();
+            continue;
+        }
+#endif
         while (smask) {
             const int jj = (int)__builtin_ctzll(smask);
             smask &= smask - 1;
-            const float4 Sa = sb[jj * 3 + 0], Sb = sb[jj * 3 + 1], Sc = sb[jj * 3 + 2];
-            const int sidx = base + jj;
-            const float sx = Sa.x, sy = Sa.y, so = Sb.y, sr = Sb.z, sg = Sb.w, sbl = Sc.x, si = Sc.y;
-            // exponent, identical to the forward's splat_power4
-            const v2f dy = bc2(sy) - pyv;
-            const v4f dx = bc4(sx) - pxv;
-            const v2f bdy = bc2(Sa.w) * dy, cdy2 = (bc2(Sb.x) * dy) * dy;
-            const v4f p2 = fma4(dx, fma4(bc4(Sa.z), dx, cat4(bdy, bdy)), cat4(cdy2, cdy2));
-            const v4f G = {__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y), __builtin_amdgcn_exp2f(p2.z),
-                           __builtin_amdgcn_exp2f(p2.w)};
-            v4f al = bc4(so) * G;
-            bool ok[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const float ak = fminf(0.99f, al[k]);
-                ok[k] = (sidx < last[k]) && !(p2[k] > 0.0f) && !(ak < (1.0f / 255.0f));
-                al[k] = ok[k] ? ak : 0.0f;
-            }
-            const v4f wgt = al * T;
-            const v4f oma = bc4(1.0f) - al;
-            const v4f inv = {__builtin_amdgcn_rcpf(oma.x), __builtin_amdgcn_rcpf(oma.y), __builtin_amdgcn_rcpf(oma.z),
-                             __builtin_amdgcn_rcpf(oma.w)};
-            v4f cg = fma4(bc4(sbl), g2, fma4(bc4(sg), g1, bc4(sr) * g0));
-            if (HAS_INVD) cg = fma4(bc4(si), gd, cg);
-            S = fma4(wgt, cg, S);
-            v4f dLda = fma4(cg, T, inv * S);
-            if (HAS_BG) dLda = fma4(ntb, inv, dLda);
-#pragma unroll
-            for (int k = 0; k < 4; k++) dLda[k] = ok[k] ? dLda[k] : 0.0f;
-            T = T * oma;
-            // per-splat moments over the lane's 4 pixels; lo + hi of a v4 = the two row sums {row A, row B}
-            const v4f t4 = G * dLda;
-            const v4f tdx = t4 * dx;
-            const v4f tdx2 = tdx * dx;
-            const v2f rt = (v2f){t4.x, t4.y} + (v2f){t4.z, t4.w};
-            const v2f rtx = (v2f){tdx.x, tdx.y} + (v2f){tdx.z, tdx.w};
-            const v2f rtxx = (v2f){tdx2.x, tdx2.y} + (v2f){tdx2.z, tdx2.w};
-            const v4f w0 = wgt * g0, w1 = wgt * g1, w2 = wgt * g2;
-            const v2f rc0 = (v2f){w0.x, w0.y} + (v2f){w0.z, w0.w};
-            const v2f rc1 = (v2f){w1.x, w1.y} + (v2f){w1.z, w1.w};
-            const v2f rc2 = (v2f){w2.x, w2.y} + (v2f){w2.z, w2.w};
-            const v2f u = rt * dy;  // {tA dyA, tB dyB}
-            float p[10];
-            p[0] = rtx.x + rtx.y;                            // SGx
-            p[1] = u.x + u.y;                                // SGy
-            p[2] = rtxx.x + rtxx.y;                          // SGxx
-            p[3] = fmaf(rtx.x, dy.x, rtx.y * dy.y);          // SGxy
-            p[4] = fmaf(u.x, dy.x, u.y * dy.y);              // SGyy
-            p[5] = rt.x + rt.y;                              // SG
-            p[6] = rc0.x + rc0.y;
-            p[7] = rc1.x + rc1.y;
-            p[8] = rc2.x + rc2.y;
-            if (HAS_INVD) {
-                const v4f wd = wgt * gd;
-                const v2f rcd = (v2f){wd.x, wd.y} + (v2f){wd.z, wd.w};
-                p[9] = rcd.x + rcd.y;
-            } else {
-                p[9] = 0.0f;
-            }
-            if (__any(ok[0] || ok[1] || ok[2] || ok[3])) {
-                int slot;
-                const float tot = wave_reduce10(p, lane, slot);
-                const uint32_t e = __builtin_amdgcn_readfirstlane(__float_as_uint(Sc.z));
-                if (slot >= 0) a.rec[(size_t)e * 12 + slot] = tot;
-                if (lane == 0) a.flag[e] = 1;
-            }
+            replay_splat<HAS_INVD, HAS_BG, true>(a, sb, jj, base + jj, pxv, pyv, last, bc4(1.0f / 255.0f), g0, g1, g2, gd,
+                                                 ntb, T, S, lane);
         }
         __builtin_amdgcn_wave_barrier();
     }
