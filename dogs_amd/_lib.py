@@ -84,6 +84,7 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count"
            "dg_densify_gather", "dg_splat_pack", "dg_ply_pack", "dg_ring_create", "dg_ring_submit", "dg_ring_next",
            "dg_ring_upload", "dg_ring_pending", "dg_ring_destroy", "dg_image_u8_to_chw", "dg_points_in_boxes2d", "dg_activate_forward", "dg_activate_backward", "dg_clamp_l1_blocks",
            "dg_clamp_l1_forward", "dg_clamp_l1_backward", "dg_adaptive_capacity", "dg_debug_counters", "dg_adam_update_groups_prox", "dg_train_step",
+           "dg_colmap_cameras", "dg_colmap_images", "dg_colmap_points3d",
            "dg_last_error", "dg_version")
 
 _lib = None
@@ -137,6 +138,14 @@ def load(path: str | None = None):
         if hasattr(L, "dg_binned_instances"):  # introspection only; absent in older builds used for A/B runs
             L.dg_binned_instances.restype = C.c_int
             L.dg_binned_instances.argtypes = [vp, C.c_int, i64p, vp]
+        if hasattr(L, "dg_colmap_points3d"):
+            u64p = C.POINTER(C.c_uint64)
+            L.dg_colmap_cameras.restype = C.c_int
+            L.dg_colmap_cameras.argtypes = [C.c_char_p, u64p, vp, vp, vp, vp]
+            L.dg_colmap_images.restype = C.c_int
+            L.dg_colmap_images.argtypes = [C.c_char_p, u64p, u64p, u64p, vp, vp, vp, vp, vp, vp, vp, vp]
+            L.dg_colmap_points3d.restype = C.c_int
+            L.dg_colmap_points3d.argtypes = [C.c_char_p, C.c_int, u64p, u64p, vp, vp, vp, vp, vp, vp]
         if hasattr(L, "dg_train_step"):
             L.dg_train_step.restype = C.c_int
             L.dg_train_step.argtypes = [C.POINTER(DgTrainStepArgs), ALLOC_FN, vp, vp]

@@ -352,6 +352,23 @@ int dg_exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_
 void dg_profile_enable(int on);
 int dg_profile_collect(char* buf, int buflen);
 
+/* ---- COLMAP binary model readers (host code; the block split's input) ----
+ * Replace SceneManager._load_cameras_bin / _load_images_bin / _load_points3D_bin
+ * (conerf/pycolmap/pycolmap/scene_manager.py:137-310), called by load_colmap (load_colmap.py:221-226).  Each call
+ * maps the file and walks it: with the output arrays NULL it only counts (sizes for the caller), otherwise it fills
+ * them.  Return 0, or 1 (cannot open), 2 (truncated), 3 (unknown camera model).
+ * cameras: ids [n] u32, models [n] i32, wh [n,2] u64, params8 [n,8] f64 (zero-padded past the model's count). */
+int dg_colmap_cameras(const char* path, uint64_t* n, uint32_t* ids, int32_t* models, uint64_t* wh, double* params8);
+/* images: ids [n], qt7 [n,7] (qvec w,x,y,z then tvec), camera_ids [n], name_offsets [n+1] into names (no NUL),
+ * p2d_offsets [n+1] into xy [m,2] / point3d_ids [m] -- points2D without a 3D point (id -1) dropped as the reference. */
+int dg_colmap_images(const char* path, uint64_t* n, uint64_t* name_bytes, uint64_t* n_points2d, uint32_t* ids,
+                     double* qt7, uint32_t* camera_ids, uint64_t* name_offsets, char* names, uint64_t* p2d_offsets,
+                     double* xy, int64_t* point3d_ids);
+/* points3D with track_len >= min_track_length (the reference's default 3): ids [n] u64, xyz [n,3] f64, rgb [n,3] u8,
+ * err [n] f64, track_offsets [n+1] into tracks [t,2] u32 (image_id, point2D_idx). */
+int dg_colmap_points3d(const char* path, int min_track_length, uint64_t* n, uint64_t* n_track, uint64_t* ids,
+                       double* xyz, uint8_t* rgb, double* err, uint64_t* track_offsets, uint32_t* tracks);
+
 const char* dg_last_error(void);
 int dg_version(void);
 

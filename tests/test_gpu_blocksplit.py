@@ -102,3 +102,28 @@ def test_cluster_points_and_images(hip_device, tmp_path):
     assert lines[:200] == [f"{1000 + i} {lab_o[i]}" for i in range(200)]
     for k in range(4):
         np.testing.assert_array_equal(blocks[k][0], 2 * O.points_in_bbox2D(c2w[:, :3, 3], exp_o[k], T_o))
+
+
+def test_colmap_to_block_folders(hip_device, tmp_path):
+    """The whole block-preprocessing path on the golden COLMAP model: native binary readers -> sorted views
+    (load_colmap.py:226-273) -> Grid2D split of cameras and points on the GPU (:412-425) -> per-block folders in
+    MiniDataset's format (:459-487, dataset_base.py:111-124), read back."""
+    import os
+    from dogs_amd import blocksplit
+    from dogs_amd.blockio import MiniDataset, colmap_views, export_blocks
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "colmap")
+    v = colmap_views(gold)
+    n = len(v["image_names"])
+    bids, cb, ecb, T = blocksplit.cluster_image_in_grid(v["camtoworlds"], str(tmp_path), np.arange(n),
+                                                        [1.0, 1.0, 1.0], v["image_index_to_image_id"], 2, 2, 1)
+    pb, epb, _ = blocksplit.cluster_points_in_grid(v["points3d"], v["colors"], str(tmp_path), [1.0, 1.0, 1.0], 2, 2, 1,
+                                                   False, T)
+    assert len(bids) == 2 and os.path.exists(tmp_path / "cluster.txt") and os.path.exists(tmp_path / "points3D_0.ply")
+    covered = set()
+    for ids in bids.values():
+        covered |= set(np.concatenate(ids).tolist())
+    assert covered == set(range(n))                   # every camera centre lands in some expanded cell
+    out = export_blocks(str(tmp_path / "blocks"), v, bids)
+    for b, d in enumerate(out):
+        back = MiniDataset().read(str(tmp_path / "blocks" / f"block_{b}"), block_id=b)
+        assert sorted(c.image_index for c in back.cameras) == sorted(np.concatenate(bids[b]).tolist())

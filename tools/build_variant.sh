@@ -7,7 +7,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 TMP=$(mktemp -d)
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result -munsafe-fp-atomics"
 pids=()
-for s in sortscan raster_fwd raster_bwd aux_kernels optim export loader blocksplit capi; do
+for s in sortscan raster_fwd raster_bwd aux_kernels optim export loader blocksplit colmap capi; do
   hipcc $FLAGS "$@" -c "$ROOT/dogs_amd/csrc/$s.hip" -o "$TMP/$s.o" &
   pids+=($!)
 done
