@@ -546,21 +546,33 @@ def main():
         torch.cuda.synchronize()
         tms = (time.perf_counter() - tt) / nts * 1e3
         nstep = ts.native()
-        for _ in range(len(cams)):
-            nstep()
-        torch.cuda.synchronize()
-        tt = time.perf_counter()
-        for _ in range(nts):
-            nstep()
-        torch.cuda.synchronize()
-        nms = (time.perf_counter() - tt) / nts * 1e3
+        route_ms = {}
+        # the default route (activation backward folded into the update) last; before it the unfused one
+        for route, env in (("unfused", "DG_TRAIN_UNFUSED"), ("folded", None)):
+            if env:
+                os.environ[env] = "1"
+            try:
+                for _ in range(len(cams)):
+                    nstep()
+                torch.cuda.synchronize()
+                tt = time.perf_counter()
+                for _ in range(nts):
+                    nstep()
+                torch.cuda.synchronize()
+                route_ms[route] = round((time.perf_counter() - tt) / nts * 1e3, 4)
+            finally:
+                if env:
+                    del os.environ[env]
+        nms = route_ms["folded"]
         dms, n_after = ts.densify()
         train = {"views_per_s": round(1e3 / tms, 2), "ms_per_step": round(tms, 3),
                  "includes": "activations + raster fwd/bwd + L1 + fused-SSIM fwd/bwd + scale regulariser + "
                              "densification stats + SparseGaussianAdam (one launch), cycling the view batch; "
                              "autograd route (the drop-in API)",
                  "native": {"views_per_s": round(1e3 / nms, 2), "ms_per_step": round(nms, 3),
-                            "route": "dg_train_step (dogs_amd.train_step): the same iteration in one C call"},
+                            "route": "dg_train_step (dogs_amd.train_step): the same iteration in one C call, the "
+                                     "activation backward folded into the optimizer update",
+                            "routes_ms": route_ms},
                  "densify_and_prune_ms": round(dms, 3), "gaussians_after_densify": n_after}
 
     admm = None

@@ -10,6 +10,15 @@ void launch_ssim_fwd(int B, int CH, int H, int W, float C1, float C2, const floa
 void launch_ssim_bwd(int B, int CH, int H, int W, const float* img1, const float* img2, const float* dL,
                      const float* dmu1, const float* ds1, const float* ds12, float* dimg1, hipStream_t s,
                      float dl_value = 0.0f);
+// the native training step's variants: clamp(0, 1) of the raw render, the L1 term and the SSIM mean folded into the
+// forward (part: ssim_waves() L1 partials, then as many map partials; no map written), and the clamp / L1 backward
+// folded into the backward (d_raw: dL/d raw render; l1_scale = dL/dL1 / n)
+uint32_t ssim_waves(int planes, int H, int W);
+void launch_ssim_fwd_fused(int H, int W, float C1, float C2, const float* raw, const float* gt, float* clamped,
+                           float* dmu1, float* ds1, float* ds12, float* part, hipStream_t s);
+void launch_ssim_bwd_fused(int H, int W, const float* clamped, const float* gt, const float* raw, float dl_value,
+                           float l1_scale, const float* dmu1, const float* ds1, const float* ds12, float* d_raw,
+                           hipStream_t s);
 void launch_adam(float* param, const float* grad, float* m, float* v, const bool* visible, float lr, float b1, float b2,
                  float eps, uint32_t N, uint32_t M, hipStream_t s);
 size_t knn_temp_bytes(int P);

@@ -57,11 +57,19 @@ __device__ __forceinline__ StripPos strip_of(int H, int W, int planes) {
     return p;
 }
 
-template <bool TRAIN>
+// torch.clamp(x, 0, 1), NaN kept (optim.hip clamp01)
+__device__ __forceinline__ float clamp01f(float x) { return x != x ? x : fminf(fmaxf(x, 0.f), 1.f); }
+
+// FUSED (the native training step): img1 is the raw render, read through clamp(0, 1); the clamped image goes to
+// out_img, and each wave writes its partial sums of |clamped - gt| and of the map (part[wave], part[nwaves + wave])
+// instead of the map itself -- render()'s clamp, the L1 term and the SSIM mean in the same pass.
+template <bool TRAIN, bool FUSED = false>
 __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes, float C1, float C2,
                                                         const float* __restrict__ img1, const float* __restrict__ img2,
                                                         float* __restrict__ map, float* __restrict__ dmu1,
-                                                        float* __restrict__ ds1, float* __restrict__ ds12) {
+                                                        float* __restrict__ ds1, float* __restrict__ ds12,
+                                                        float* __restrict__ out_img = nullptr,
+                                                        float* __restrict__ part = nullptr) {
     const StripPos sp = strip_of(H, W, planes);
     if (!sp.valid) return;  // wave-uniform
     const int lane = threadIdx.x & 63;
@@ -72,12 +80,18 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
     // the lane's window covers columns x .. x+10: its output is column x+5
     const int ox = sp.x + 5;
     const bool out_col = lane < SSW_OUT && ox < W;
-    auto ld = [&](const float* img, int row) -> float {
-        return (colok && row >= 0 && row < H) ? img[(size_t)row * W + sp.x] : 0.0f;
+    auto lda = [&](int row) -> float {
+        if (!(colok && row >= 0 && row < H)) return 0.0f;
+        const float x = a[(size_t)row * W + sp.x];
+        return FUSED ? clamp01f(x) : x;
     };
+    auto ldb = [&](int row) -> float {
+        return (colok && row >= 0 && row < H) ? b[(size_t)row * W + sp.x] : 0.0f;
+    };
+    float acc_l1 = 0.0f, acc_map = 0.0f;
     float ring[11][5];
-    float ua = ld(a, sp.y0 - 5), va = ld(b, sp.y0 - 5);
-    float ub = ld(a, sp.y0 - 4), vb = ld(b, sp.y0 - 4);
+    float ua = lda(sp.y0 - 5), va = ldb(sp.y0 - 5);
+    float ub = lda(sp.y0 - 4), vb = ldb(sp.y0 - 4);
     for (int base = 0; base < SSW_IN; base += 11) {
 #pragma unroll
         for (int j = 0; j < 11; j++) {
@@ -85,8 +99,8 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
             if (rr < SSW_IN) {
                 const float u = ua, v = va;
                 ua = ub; va = vb;
-                ub = ld(a, sp.y0 - 5 + rr + 2);
-                vb = ld(b, sp.y0 - 5 + rr + 2);
+                ub = lda(sp.y0 - 5 + rr + 2);
+                vb = ldb(sp.y0 - 5 + rr + 2);
                 ring[j][0] = hconv11(u);
                 ring[j][1] = hconv11(u * u);
                 ring[j][2] = hconv11(v);
@@ -115,7 +129,14 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
                          // at 1080p x 3, within the 1e-5 parity bar (test_fused_ssim_matches_oracle)
                         const float rAB = __builtin_amdgcn_rcpf(A * B), rAAB = __builtin_amdgcn_rcpf(A * A * B),
                                     rABB = __builtin_amdgcn_rcpf(A * B * B);
-                        map[gi] = (Cc * D) * rAB;
+                        if (FUSED) {
+                            const float c = clamp01f(img1[gi]), g = img2[gi];
+                            out_img[gi] = c;
+                            acc_l1 += fabsf(c - g);
+                            acc_map += (Cc * D) * rAB;
+                        } else {
+                            map[gi] = (Cc * D) * rAB;
+                        }
                         if (TRAIN) {
                             dmu1[gi] = ((mu2 * 2.0f * D) * rAB - (mu2 * 2.0f * Cc) * rAB - (mu1 * 2.0f * Cc * D) * rAAB +
                                         (mu1 * 2.0f * Cc * D) * rABB);
@@ -136,13 +157,31 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
             }
         }
     }
+    if (FUSED) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            acc_l1 += __shfl_xor(acc_l1, o);
+            acc_map += __shfl_xor(acc_map, o);
+        }
+        if (lane == 0) {
+            const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+            const int nw = ((W + SSW_OUT - 1) / SSW_OUT) * ((H + SSW_ROWS - 1) / SSW_ROWS) * planes;
+            part[wid] = acc_l1;
+            part[nw + wid] = acc_map;
+        }
+    }
 }
 
+// FUSED (the native training step): img1 is the clamped image, raw the render before the clamp, and the output is
+// the gradient w.r.t. the raw render of (1 - ld) L1 + ld (1 - SSIM): (dSSIM + g_l1 sgn(img1 - img2) / n) where the
+// render lies in [0, 1], else 0 -- k_clamp_l1_bwd's expression in the same pass.
+template <bool FUSED = false>
 __global__ void __launch_bounds__(256) k_ssim_bwd_strip(int H, int W, int planes, const float* __restrict__ img1,
                                                         const float* __restrict__ img2, const float* __restrict__ dL,
                                                         float dl_value, const float* __restrict__ dmu1,
                                                         const float* __restrict__ ds1, const float* __restrict__ ds12,
-                                                        float* __restrict__ dimg1) {
+                                                        float* __restrict__ dimg1, const float* __restrict__ raw = nullptr,
+                                                        float l1_scale = 0.0f) {
     const StripPos sp = strip_of(H, W, planes);
     if (!sp.valid) return;
     const int lane = threadIdx.x & 63;
@@ -186,9 +225,16 @@ __global__ void __launch_bounds__(256) k_ssim_bwd_strip(int H, int W, int planes
                     }
                     if (out_col) {
                         const size_t gi = plane + (size_t)y * W + ox;
+                        const float i1 = img1[gi], i2 = img2[gi];
                         float d = v0;
-                        d += (img1[gi] * 2.0f) * v1;
-                        d += img2[gi] * v2;
+                        d += (i1 * 2.0f) * v1;
+                        d += i2 * v2;
+                        if (FUSED) {
+                            const float x = raw[gi], e = i1 - i2;
+                            const float sg = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
+                            const float gsum = d + l1_scale * sg;
+                            d = (x >= 0.f && x <= 1.f) ? gsum : 0.f;
+                        }
                         dimg1[gi] = d;
                     }
                 }
@@ -216,8 +262,24 @@ void launch_ssim_bwd(int B, int CH, int H, int W, const float* img1, const float
                      const float* dmu1, const float* ds1, const float* ds12, float* dimg1, hipStream_t s,
                      float dl_value) {
     if ((size_t)B * CH * H * W == 0) return;
-    k_ssim_bwd_strip<<<ssim_strip_blocks(B * CH, H, W), 256, 0, s>>>(H, W, B * CH, img1, img2, dL, dl_value, dmu1, ds1,
-                                                                      ds12, dimg1);
+    k_ssim_bwd_strip<false><<<ssim_strip_blocks(B * CH, H, W), 256, 0, s>>>(H, W, B * CH, img1, img2, dL, dl_value,
+                                                                             dmu1, ds1, ds12, dimg1);
+}
+uint32_t ssim_waves(int planes, int H, int W) {
+    return (uint32_t)(((W + SSW_OUT - 1) / SSW_OUT) * ((H + SSW_ROWS - 1) / SSW_ROWS) * planes);
+}
+void launch_ssim_fwd_fused(int H, int W, float C1, float C2, const float* raw, const float* gt, float* clamped,
+                           float* dmu1, float* ds1, float* ds12, float* part, hipStream_t s) {
+    if ((size_t)H * W == 0) return;
+    k_ssim_fwd_strip<true, true><<<ssim_strip_blocks(3, H, W), 256, 0, s>>>(H, W, 3, C1, C2, raw, gt, nullptr, dmu1,
+                                                                             ds1, ds12, clamped, part);
+}
+void launch_ssim_bwd_fused(int H, int W, const float* clamped, const float* gt, const float* raw, float dl_value,
+                           float l1_scale, const float* dmu1, const float* ds1, const float* ds12, float* d_raw,
+                           hipStream_t s) {
+    if ((size_t)H * W == 0) return;
+    k_ssim_bwd_strip<true><<<ssim_strip_blocks(3, H, W), 256, 0, s>>>(H, W, 3, clamped, gt, nullptr, dl_value, dmu1,
+                                                                       ds1, ds12, d_raw, raw, l1_scale);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -4,6 +4,7 @@
 // carving of the private state blocks, the single host sync (instance count), launch order.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <string>
 #include <vector>
@@ -789,6 +790,8 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     if (n_img >= 0xffffff00ull) return fail("train step: image too large%s%d");
     const uint32_t nb_l1 = gs::clamp_l1_blocks((uint32_t)n_img);
     const uint32_t nb_map = gs::block_sum_blocks((uint32_t)n_img), nb_sc = gs::block_sum_blocks((uint32_t)P);
+    const uint32_t nw_ssim = gs::ssim_waves(3, H, W);  // the fused SSIM's partials: nw L1, then nw map
+    const uint32_t n_part = (nb_l1 + nb_map > 2 * nw_ssim ? nb_l1 + nb_map : 2 * nw_ssim) + nb_sc;
     // ---- the step's scratch (DG_BUF_TRAIN); the nine rasterizer gradients back to back (the replay zero-fills them)
     const size_t n9 = (3 + 3 + 1 + 3 + 6 + 3 + 3 * Mz + 3 + 4) * Pz;
     auto carve = [&](void* base, float** f) {
@@ -798,7 +801,7 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
         f[2] = c.take<float>(4 * Pz);      // rotation
         f[3] = c.take<float>(n_img);       // raw render
         f[4] = c.take<float>(HW);          // inverse depth
-        f[5] = c.take<float>(nb_l1 + nb_map + nb_sc);  // partial sums
+        f[5] = c.take<float>(n_part);      // partial sums
         f[6] = c.take<float>(n_img);       // SSIM map
         f[7] = c.take<float>(n_img);       // dm/dmu1
         f[8] = c.take<float>(n_img);       // dm/dsigma1_sq
@@ -834,29 +837,15 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     if (dg_rasterize_forward(&r, color, invd, a->radii, alloc, user, &geom, &binning, &image, &binning2,
                              &num_rendered, &num_instances, stream))
         return 1;
-    gs::launch_clamp_l1_fwd((uint32_t)n_img, color, a->gt, a->image, part, s);
-    const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;   // fused_ssim's constants
-    gs::launch_ssim_fwd(1, 3, H, W, C1, C2, a->image, a->gt, map, dmu1, ds1, ds12, s);
-    if (a->loss) {
-        gs::launch_block_sum(map, (uint32_t)n_img, 0, part + nb_l1, s);
-        gs::launch_block_sum(act_s, (uint32_t)P, 1, part + nb_l1 + nb_map, s);
-        gs::launch_loss_final(part, nb_l1, part + nb_l1, nb_map, part + nb_l1 + nb_map, nb_sc, (uint32_t)n_img,
-                              (uint32_t)P, a->loss, s);
-    }
-    // ---- backward of (1 - ld) L1 + ld (1 - SSIM) + ls mean(prod(scaling)): d/dmap = -ld / n (the mean's backward)
-    const float ld = a->lambda_dssim;
-    gs::launch_ssim_bwd(1, 3, H, W, a->image, a->gt, nullptr, dmu1, ds1, ds12, map, s, (-ld) / (float)n_img);
-    gs::launch_clamp_l1_bwd((uint32_t)n_img, color, a->image, a->gt, map, nullptr, dimg, s,
-                            (float)(1.0 - (double)ld));
-    if (dg_rasterize_backward(&r, a->radii, geom, binning, image, binning2, num_rendered, num_instances, dimg, nullptr,
-                              dmeans2D, dcolors, dopac, dmeans3D, dcov3D, ddc, dsh, dscales, drot, depth, alloc, user,
-                              stream))
-        return 1;
-    gs::launch_activate_bwd((uint32_t)P, act_o, act_s, G[5].param, dopac, dscales, drot, g_o, g_s, g_q, s,
-                            a->lambda_scale / (float)P);
-    // ---- SparseGaussianAdam.step(radii > 0) over the six groups, ADMM proximal gradient, densification statistics
+    // ---- SparseGaussianAdam.step(radii > 0) over the six groups, ADMM proximal gradient, densification statistics.
+    // Default route: the activations' backward is folded into the update (gmode), and the 4-float chunks that touch
+    // no binned row (rcnt == 0: rasterizer gradient exactly zero) skip reading the gradient buffers.  Same arithmetic
+    // per element as the unfused route (DG_TRAIN_UNFUSED=1: k_activate_bwd, then the plain update).  (Running the
+    // update of those rows on a side stream, overlapping the backward, was measured and dropped: DESIGN.md §8.)
+    const bool unfused = getenv("DG_TRAIN_UNFUSED") != nullptr;
     dg_adam_group groups[6];
-    const float* grads[6] = {dmeans3D, ddc, dsh, g_o, g_s, g_q};
+    const float* grads[6] = {dmeans3D, ddc, dsh, unfused ? g_o : dopac, unfused ? g_s : dscales,
+                             unfused ? g_q : drot};
     for (int k = 0; k < 6; k++) {
         groups[k] = G[k];
         groups[k].grad = grads[k];
@@ -880,6 +869,11 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
             al |= reinterpret_cast<uintptr_t>(a->prox[k].u) | reinterpret_cast<uintptr_t>(a->prox[k].z);
         }
         d.vec = (al & 15u) == 0u;
+        if (!unfused && k >= 3) {
+            d.gmode = k - 2;  // opacity: sigmoid, scaling: exp + regulariser, quaternion: normalize
+            d.act = k == 3 ? act_o : (k == 4 ? act_s : nullptr);
+            d.reg = k == 4 ? a->lambda_scale / (float)P : 0.0f;
+        }
     }
     m.n = n;
     if (a->stats) {
@@ -887,6 +881,40 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
         st.radii = a->radii; st.dmeans2D = dmeans2D; st.dmeans2D_stride = 3;
         if (fill_stats(m, &st)) return 1;
     }
+    if (!unfused) m.hot = carve_geom(geom, P).rcnt;
+    const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;   // fused_ssim's constants
+    const float ld = a->lambda_dssim;
+    const float g_l1 = (float)(1.0 - (double)ld);
+    // loss backward of (1 - ld) L1 + ld (1 - SSIM) + ls mean(prod(scaling)): d/dmap = -ld / n (the mean's backward)
+    if (!unfused) {  // render()'s clamp, L1 and the SSIM mean inside the SSIM passes (same values per pixel)
+        float* const p_sc = part + 2 * nw_ssim;
+        gs::launch_ssim_fwd_fused(H, W, C1, C2, color, a->gt, a->image, dmu1, ds1, ds12, part, s);
+        if (a->loss) {
+            gs::launch_block_sum(act_s, (uint32_t)P, 1, p_sc, s);
+            gs::launch_loss_final(part, nw_ssim, part + nw_ssim, nw_ssim, p_sc, nb_sc, (uint32_t)n_img, (uint32_t)P,
+                                  a->loss, s);
+        }
+        gs::launch_ssim_bwd_fused(H, W, a->image, a->gt, color, (-ld) / (float)n_img, g_l1 / (float)n_img, dmu1, ds1,
+                                  ds12, dimg, s);
+    } else {
+        gs::launch_clamp_l1_fwd((uint32_t)n_img, color, a->gt, a->image, part, s);
+        gs::launch_ssim_fwd(1, 3, H, W, C1, C2, a->image, a->gt, map, dmu1, ds1, ds12, s);
+        if (a->loss) {
+            gs::launch_block_sum(map, (uint32_t)n_img, 0, part + nb_l1, s);
+            gs::launch_block_sum(act_s, (uint32_t)P, 1, part + nb_l1 + nb_map, s);
+            gs::launch_loss_final(part, nb_l1, part + nb_l1, nb_map, part + nb_l1 + nb_map, nb_sc, (uint32_t)n_img,
+                                  (uint32_t)P, a->loss, s);
+        }
+        gs::launch_ssim_bwd(1, 3, H, W, a->image, a->gt, nullptr, dmu1, ds1, ds12, map, s, (-ld) / (float)n_img);
+        gs::launch_clamp_l1_bwd((uint32_t)n_img, color, a->image, a->gt, map, nullptr, dimg, s, g_l1);
+    }
+    if (dg_rasterize_backward(&r, a->radii, geom, binning, image, binning2, num_rendered, num_instances, dimg, nullptr,
+                              dmeans2D, dcolors, dopac, dmeans3D, dcov3D, ddc, dsh, dscales, drot, depth, alloc, user,
+                              stream))
+        return 1;
+    if (unfused)
+        gs::launch_activate_bwd((uint32_t)P, act_o, act_s, G[5].param, dopac, dscales, drot, g_o, g_s, g_q, s,
+                                a->lambda_scale / (float)P);
     gs::launch_adam_multi(m, s);
     HIP_OK(hipGetLastError());
     return 0;

@@ -23,6 +23,12 @@ struct AdamGroup {
     const float* u;
     const float* z;
     float coef;
+    // optional activation backward folded in (the native training step): grad is dL/d(activated parameter) and the
+    // update sees dL/d(raw parameter) -- 0: grad as given; 1: sigmoid (act = sigmoid(raw), M = 1); 2: exp plus the
+    // scale regulariser reg * prod(scaling) (act = exp(raw), M = 3); 3: F.normalize (the raw quaternion is param, M = 4)
+    int gmode;
+    const float* act;
+    float reg;
 };
 
 struct AdamMultiArgs {
@@ -40,6 +46,10 @@ struct AdamMultiArgs {
     float* max_radii2D;        // [N]
     float* grad_accum;         // [N]
     float* denom;              // [N]
+    // optional: hot[i] != 0 marks the rows that may carry a rasterizer gradient (the binned Gaussians, rcnt > 0);
+    // a 4-float chunk touching no hot row takes its incoming gradient as zero without reading it (the native step,
+    // where the activation fold supplies the regulariser's gradient of every row)
+    const uint32_t* hot;
 };
 void launch_adam_multi(const AdamMultiArgs& a, hipStream_t s);
 uint32_t clamp_l1_blocks(uint32_t n);

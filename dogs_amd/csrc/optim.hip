@@ -43,6 +43,36 @@ __device__ __forceinline__ void nt_store4(float* p, float4 v) {
 #endif
 constexpr int ADAM_CHUNKS = DG_ADAM_CHUNKS;  // float4 chunks per lane
 
+// Backward of the parameter activations (gaussian_splat_model.py get_opacity / get_scaling / get_quaternion), shared
+// by k_activate_bwd and the activation-folded Adam so both routes evaluate the same expressions.
+__device__ __forceinline__ float sigmoid_bwd(float g, float v) { return g * (v * (1.0f - v)); }
+// exp's backward of scaling column r, with the scale regulariser lambda_scale mean(prod(scaling, 1))
+// (gaussian_trainer.py:407-408): its gradient reg prod / s_r joins the rasterizer's before exp's backward
+__device__ __forceinline__ float exp_bwd(float g, const float* __restrict__ s3, int r, float reg) {
+    if (reg != 0.0f) {
+        const float prod = (s3[0] * s3[1]) * s3[2];
+        return (g + reg * (prod / s3[r])) * s3[r];
+    }
+    return g * s3[r];
+}
+// F.normalize(x, eps 1e-12): d(x / n) = (g - y (y . g)) / n, or g / eps on the clamped denominator
+__device__ __forceinline__ float4 normalize_bwd(float4 x, float4 g) {
+    const float n = sqrtf(((x.x * x.x + x.y * x.y) + x.z * x.z) + x.w * x.w);
+    if (n > 1e-12f) {
+        const float inv = 1.0f / n;
+        const float4 y = make_float4(x.x * inv, x.y * inv, x.z * inv, x.w * inv);
+        const float yg = ((y.x * g.x + y.y * g.y) + y.z * g.z) + y.w * g.w;
+        return make_float4((g.x - y.x * yg) * inv, (g.y - y.y * yg) * inv, (g.z - y.z * yg) * inv,
+                           (g.w - y.w * yg) * inv);
+    }
+    return make_float4(g.x / 1e-12f, g.y / 1e-12f, g.z / 1e-12f, g.w / 1e-12f);
+}
+
+__device__ __forceinline__ float f4get(const float4& v, int j) { return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w; }
+__device__ __forceinline__ void f4set(float4& v, int j, float x) {
+    if (j == 0) v.x = x; else if (j == 1) v.y = x; else if (j == 2) v.z = x; else v.w = x;
+}
+
 __global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
     const uint32_t blk = blockIdx.x;
     if (blk >= a.start[a.n]) {  // densification statistics, one Gaussian per lane
@@ -52,8 +82,12 @@ __global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
         const float r = (float)a.radii[i];
         const float mr = a.max_radii2D[i];
         a.max_radii2D[i] = r > mr ? r : mr;
-        // xyz_gradient_accum[vis] += ||grad[vis, :2]||, denom[vis] += 1
-        const float gx = a.dmeans2D[(size_t)i * a.dm_stride], gy = a.dmeans2D[(size_t)i * a.dm_stride + 1];
+        // xyz_gradient_accum[vis] += ||grad[vis, :2]||, denom[vis] += 1 (a row no tile binned has none)
+        float gx = 0.0f, gy = 0.0f;
+        if (!a.hot || a.hot[i] != 0u) {
+            gx = a.dmeans2D[(size_t)i * a.dm_stride];
+            gy = a.dmeans2D[(size_t)i * a.dm_stride + 1];
+        }
         a.grad_accum[i] += sqrtf(gx * gx + gy * gy);
         a.denom[i] += 1.0f;
         return;
@@ -67,45 +101,88 @@ __global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
     const float b1 = a.b1, b2 = a.b2;
     const uint32_t base = 4u * ((blk - a.start[k]) * 256u * ADAM_CHUNKS + threadIdx.x);
     float4 p[ADAM_CHUNKS], gr[ADAM_CHUNKS], m[ADAM_CHUNKS], v[ADAM_CHUNKS];
-    bool vis[ADAM_CHUNKS][4], act[ADAM_CHUNKS];
+    bool vis[ADAM_CHUNKS][4], act[ADAM_CHUNKS], full[ADAM_CHUNKS];
 #pragma unroll
     for (int c = 0; c < ADAM_CHUNKS; c++) {
         const uint32_t e0 = base + 1024u * c;
         act[c] = false;
+        full[c] = false;
         if (e0 >= total) continue;
-        uint32_t gi = e0 / g.M, r = e0 - gi * g.M;
+        const uint32_t gi0 = e0 / g.M, r0 = e0 - gi0 * g.M;
+        uint32_t gi = gi0, r = r0;
+        bool hot = false;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            vis[c][j] = e0 + j < total && (a.visible ? a.visible[gi] != 0 : a.vis_radii[gi] > 0);
+            const bool in = e0 + j < total;
+            vis[c][j] = in && (a.visible ? a.visible[gi] != 0 : a.vis_radii[gi] > 0);
             act[c] |= vis[c][j];
+            if (a.hot && in) hot |= a.hot[gi] != 0u;
             if (++r == g.M) { r = 0; gi++; }
         }
-        if (act[c] && g.vec && e0 + 4 <= total) {
+        if (!act[c]) continue;
+        const bool zero_grad = a.hot && !hot;  // no binned row in the chunk: its rasterizer gradient is zero
+        full[c] = g.vec && e0 + 4 <= total;
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (full[c]) {
 #ifndef DG_ADAM_CACHED
-            p[c] = nt_load4(g.param + e0); gr[c] = nt_load4(g.grad + e0);
+            p[c] = nt_load4(g.param + e0);
+            gr[c] = zero_grad ? z4 : nt_load4(g.grad + e0);
             m[c] = nt_load4(g.m + e0); v[c] = nt_load4(g.v + e0);
 #else
             p[c] = *reinterpret_cast<const float4*>(g.param + e0);
-            gr[c] = *reinterpret_cast<const float4*>(g.grad + e0);
+            gr[c] = zero_grad ? z4 : *reinterpret_cast<const float4*>(g.grad + e0);
             m[c] = *reinterpret_cast<const float4*>(g.m + e0);
             v[c] = *reinterpret_cast<const float4*>(g.v + e0);
 #endif
-            if (g.u) {  // the ADMM proximal gradient joins the loss gradient before the moments see it
-                const float4 u = nt_load4(g.u + e0), z = nt_load4(g.z + e0);
-                gr[c].x += g.coef * ((p[c].x + u.x) - z.x); gr[c].y += g.coef * ((p[c].y + u.y) - z.y);
-                gr[c].z += g.coef * ((p[c].z + u.z) - z.z); gr[c].w += g.coef * ((p[c].w + u.w) - z.w);
+        } else {
+            p[c] = gr[c] = m[c] = v[c] = z4;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (e0 + j >= total) continue;
+                f4set(p[c], j, g.param[e0 + j]);
+                f4set(m[c], j, g.m[e0 + j]);
+                f4set(v[c], j, g.v[e0 + j]);
+                if (!zero_grad) f4set(gr[c], j, g.grad[e0 + j]);
             }
+        }
+        // the activation's backward (dL/d activated -> dL/d raw), before the proximal term and the moments
+        if (g.gmode == 1) {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (e0 + j < total) f4set(gr[c], j, sigmoid_bwd(f4get(gr[c], j), g.act[gi0 + j]));
+        } else if (g.gmode == 2) {
+            uint32_t gj = gi0, rj = r0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (e0 + j < total) f4set(gr[c], j, exp_bwd(f4get(gr[c], j), g.act + 3 * (size_t)gj, (int)rj, g.reg));
+                if (++rj == 3u) { rj = 0; gj++; }
+            }
+        } else if (g.gmode == 3) {
+            gr[c] = normalize_bwd(p[c], gr[c]);  // M = 4: the chunk is the row
+        }
+        if (g.u) {  // the ADMM proximal gradient joins the loss gradient before the moments see it
+            float4 u, z;
+            if (full[c]) {
+                u = nt_load4(g.u + e0); z = nt_load4(g.z + e0);
+            } else {
+                u = z = z4;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (e0 + j < total) { f4set(u, j, g.u[e0 + j]); f4set(z, j, g.z[e0 + j]); }
+            }
+            gr[c].x += g.coef * ((p[c].x + u.x) - z.x); gr[c].y += g.coef * ((p[c].y + u.y) - z.y);
+            gr[c].z += g.coef * ((p[c].z + u.z) - z.z); gr[c].w += g.coef * ((p[c].w + u.w) - z.w);
         }
     }
 #pragma unroll
     for (int c = 0; c < ADAM_CHUNKS; c++) {
         const uint32_t e0 = base + 1024u * c;
         if (!act[c]) continue;
-        if (g.vec && e0 + 4 <= total) {
-            if (vis[c][0]) p[c].x = adam_one(p[c].x, gr[c].x, m[c].x, v[c].x, g.lr, b1, b2, g.eps);
-            if (vis[c][1]) p[c].y = adam_one(p[c].y, gr[c].y, m[c].y, v[c].y, g.lr, b1, b2, g.eps);
-            if (vis[c][2]) p[c].z = adam_one(p[c].z, gr[c].z, m[c].z, v[c].z, g.lr, b1, b2, g.eps);
-            if (vis[c][3]) p[c].w = adam_one(p[c].w, gr[c].w, m[c].w, v[c].w, g.lr, b1, b2, g.eps);
+        if (vis[c][0]) p[c].x = adam_one(p[c].x, gr[c].x, m[c].x, v[c].x, g.lr, b1, b2, g.eps);
+        if (vis[c][1]) p[c].y = adam_one(p[c].y, gr[c].y, m[c].y, v[c].y, g.lr, b1, b2, g.eps);
+        if (vis[c][2]) p[c].z = adam_one(p[c].z, gr[c].z, m[c].z, v[c].z, g.lr, b1, b2, g.eps);
+        if (vis[c][3]) p[c].w = adam_one(p[c].w, gr[c].w, m[c].w, v[c].w, g.lr, b1, b2, g.eps);
+        if (full[c]) {
 #ifndef DG_ADAM_CACHED  // streaming (non-temporal) loads and stores: every byte is touched once (327 -> 269 us)
             nt_store4(g.param + e0, p[c]); nt_store4(g.m + e0, m[c]); nt_store4(g.v + e0, v[c]);
 #else
@@ -118,13 +195,9 @@ __global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             if (!vis[c][j]) continue;
-            const uint32_t e = e0 + j;
-            float mm = g.m[e], vv = g.v[e];
-            const float pe = g.param[e];
-            const float ge = g.u ? g.grad[e] + g.coef * ((pe + g.u[e]) - g.z[e]) : g.grad[e];
-            g.param[e] = adam_one(pe, ge, mm, vv, g.lr, b1, b2, g.eps);
-            g.m[e] = mm;
-            g.v[e] = vv;
+            g.param[e0 + j] = f4get(p[c], j);
+            g.m[e0 + j] = f4get(m[c], j);
+            g.v[e0 + j] = f4get(v[c], j);
         }
     }
 }
@@ -293,40 +366,14 @@ __global__ void __launch_bounds__(256) k_activate_bwd(uint32_t N, const float* _
                                                       float scale_reg) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= N) return;
-    if (go) {
-        const float v = o[i];
-        dro[i] = go[i] * (v * (1.0f - v));
-    } else {
-        dro[i] = 0.0f;
-    }
-    if (scale_reg != 0.0f) {
-        // the native step's scale regulariser lambda_scale mean(prod(scaling, 1)) (gaussian_trainer.py:407-408):
-        // its gradient on scaling j, scale_reg prod / s_j (scale_reg = lambda_scale / N), joins the rasterizer's
-        // before exp's backward
-        const float* sv = sc + 3 * (size_t)i;
-        const float prod = (sv[0] * sv[1]) * sv[2];
-        for (int k = 0; k < 3; k++) {
-            const float g = (gs_ ? gs_[3 * (size_t)i + k] : 0.0f) + scale_reg * (prod / sv[k]);
-            drs[3 * (size_t)i + k] = g * sv[k];
-        }
-    } else {
-        for (int k = 0; k < 3; k++) drs[3 * (size_t)i + k] = gs_ ? gs_[3 * (size_t)i + k] * sc[3 * (size_t)i + k] : 0.0f;
-    }
+    dro[i] = go ? sigmoid_bwd(go[i], o[i]) : 0.0f;
+    const float* sv = sc + 3 * (size_t)i;
+    for (int k = 0; k < 3; k++)
+        drs[3 * (size_t)i + k] = (gs_ || scale_reg != 0.0f) ? exp_bwd(gs_ ? gs_[3 * (size_t)i + k] : 0.0f, sv, k,
+                                                                         scale_reg)
+                                                              : 0.0f;
     float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (gq) {
-        const float4 x = reinterpret_cast<const float4*>(rq)[i];
-        const float4 g = reinterpret_cast<const float4*>(gq)[i];
-        const float n = sqrtf(((x.x * x.x + x.y * x.y) + x.z * x.z) + x.w * x.w);
-        if (n > 1e-12f) {  // d(x / n) = (g - y (y . g)) / n
-            const float inv = 1.0f / n;
-            const float4 y = make_float4(x.x * inv, x.y * inv, x.z * inv, x.w * inv);
-            const float yg = ((y.x * g.x + y.y * g.y) + y.z * g.z) + y.w * g.w;
-            r = make_float4((g.x - y.x * yg) * inv, (g.y - y.y * yg) * inv, (g.z - y.z * yg) * inv,
-                            (g.w - y.w * yg) * inv);
-        } else {          // clamped denominator: x / eps
-            r = make_float4(g.x / 1e-12f, g.y / 1e-12f, g.z / 1e-12f, g.w / 1e-12f);
-        }
-    }
+    if (gq) r = normalize_bwd(reinterpret_cast<const float4*>(rq)[i], reinterpret_cast<const float4*>(gq)[i]);
     reinterpret_cast<float4*>(drq)[i] = r;
 }
 
@@ -451,18 +498,28 @@ __global__ void __launch_bounds__(256) k_block_sum(const float* __restrict__ x, 
     __syncthreads();
     if (threadIdx.x == 0) partial[blockIdx.x] = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);
 }
-// loss[0] = L1 (mean |clamped - gt|), loss[1] = SSIM (mean of the map), loss[2] = mean prod(scaling, 1)
-__global__ void __launch_bounds__(64) k_loss_final(const float* __restrict__ p_l1, uint32_t n_l1,
-                                                   const float* __restrict__ p_ssim, uint32_t n_ssim,
-                                                   const float* __restrict__ p_sc, uint32_t n_sc, uint32_t n_img,
-                                                   uint32_t P, float* __restrict__ loss) {
+// loss[0] = L1 (mean |clamped - gt|), loss[1] = SSIM (mean of the map), loss[2] = mean prod(scaling, 1); one
+// 1024-thread block, fixed summation order (strided per thread, then the waves, then the 16 wave sums in order)
+__global__ void __launch_bounds__(1024) k_loss_final(const float* __restrict__ p_l1, uint32_t n_l1,
+                                                     const float* __restrict__ p_ssim, uint32_t n_ssim,
+                                                     const float* __restrict__ p_sc, uint32_t n_sc, uint32_t n_img,
+                                                     uint32_t P, float* __restrict__ loss) {
+    __shared__ float s_w[3][16];
     const float* ps[3] = {p_l1, p_ssim, p_sc};
     const uint32_t ns[3] = {n_l1, n_ssim, n_sc};
+#pragma unroll
     for (int k = 0; k < 3; k++) {
         float acc = 0.0f;
-        for (uint32_t i = threadIdx.x; i < ns[k]; i += 64) acc += ps[k][i];
+        for (uint32_t i = threadIdx.x; i < ns[k]; i += 1024) acc += ps[k][i];
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-        if (threadIdx.x == 0) loss[k] = acc / (float)(k == 2 ? P : n_img);
+        if ((threadIdx.x & 63) == 0) s_w[k][threadIdx.x >> 6] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const int k = threadIdx.x;
+        float acc = 0.0f;
+        for (int w = 0; w < 16; w++) acc += s_w[k][w];
+        loss[k] = acc / (float)(k == 2 ? P : n_img);
     }
 }
 uint32_t block_sum_blocks(uint32_t n) {
@@ -474,7 +531,7 @@ void launch_block_sum(const float* x, uint32_t n, int mode, float* partial, hipS
 }
 void launch_loss_final(const float* p_l1, uint32_t n_l1, const float* p_ssim, uint32_t n_ssim, const float* p_sc,
                        uint32_t n_sc, uint32_t n_img, uint32_t P, float* loss, hipStream_t s) {
-    k_loss_final<<<1, 64, 0, s>>>(p_l1, n_l1, p_ssim, n_ssim, p_sc, n_sc, n_img, P, loss);
+    k_loss_final<<<1, 1024, 0, s>>>(p_l1, n_l1, p_ssim, n_ssim, p_sc, n_sc, n_img, P, loss);
 }
 
 }  // namespace gs

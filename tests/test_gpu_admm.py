@@ -140,3 +140,47 @@ def test_sequential_admm_two_blocks_gpu(hip_device):
         assert all(torch.isfinite(p).all() for p in b.param_tuple())
         assert torch.isfinite(b.penalty())
     assert logs[0].primal["xyz"] > 0.0
+
+
+@pytest.mark.parametrize("n,W,H", [(4000, 192, 128), (20000, 400, 304)])
+def test_native_step_folded_update_bitwise(hip_device, monkeypatch, n, W, H):
+    """dg_train_step's default route -- the activations' backward folded into the update, and the chunks touching no
+    binned row skipping the (zero) gradient reads -- gives bit-identical parameters, moments and densification
+    statistics to the unfused route (k_activate_bwd, then the plain update: DG_TRAIN_UNFUSED=1), three iterations with
+    a perturbed ADMM state (proximal gradient on)."""
+    from dogs_amd.admm import PARAM_NAMES
+    from dogs_amd.train_step import NativeTrainStep
+    routes = {"folded": None, "unfused": "DG_TRAIN_UNFUSED"}
+    tr, stats = {}, {}
+    for name in routes:
+        t, _, _ = _small_block(hip_device, n=n, W=W, H=H, native=True)
+        _perturb_state(t, 9)
+        rows = int(t.params["xyz"].shape[0])
+        stats[name] = {k: torch.zeros(rows, dtype=torch.float32, device=hip_device)
+                       for k in ("max_radii2D", "grad_accum", "denom")}
+        c = t.cfg
+        t._nts = NativeTrainStep({nm: t.params[nm] for nm in PARAM_NAMES}, t.opt, t.cameras, t.images, c.sh_degree,
+                                 c.lambda_dssim, c.lambda_scale, torch.tensor(c.background, dtype=torch.float32),
+                                 hip_device, stats=stats[name])
+        tr[name] = t
+    for _ in range(3):
+        for name, env in routes.items():
+            monkeypatch.delenv("DG_TRAIN_UNFUSED", raising=False)
+            if env:
+                monkeypatch.setenv(env, "1")
+            tr[name].local_step()
+        torch.cuda.synchronize()
+    monkeypatch.delenv("DG_TRAIN_UNFUSED", raising=False)
+    ref = tr["unfused"]
+    vis = ref.last_radii > 0
+    assert int(vis.sum()) > 100 and int((~vis).sum()) > 0
+    for name in ("folded",):
+        t = tr[name]
+        assert torch.equal(t.last_radii, ref.last_radii)
+        for nm in PARAM_NAMES:
+            assert torch.equal(t.params[nm].detach(), ref.params[nm].detach()), (name, nm)
+            for key in ("exp_avg", "exp_avg_sq"):
+                assert torch.equal(t.opt.state[t.params[nm]][key], ref.opt.state[ref.params[nm]][key]), (name, nm, key)
+        for key, v in stats["unfused"].items():
+            assert torch.equal(stats[name][key], v), (name, key)
+        assert float(stats[name]["denom"].max()) >= 1.0 and float(stats[name]["grad_accum"].max()) > 0.0

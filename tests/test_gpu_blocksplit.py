@@ -119,10 +119,11 @@ def test_colmap_to_block_folders(hip_device, tmp_path):
     pb, epb, _ = blocksplit.cluster_points_in_grid(v["points3d"], v["colors"], str(tmp_path), [1.0, 1.0, 1.0], 2, 2, 1,
                                                    False, T)
     assert len(bids) == 2 and os.path.exists(tmp_path / "cluster.txt") and os.path.exists(tmp_path / "points3D_0.ply")
-    covered = set()
-    for ids in bids.values():
-        covered |= set(np.concatenate(ids).tolist())
-    assert covered == set(range(n))                   # every camera centre lands in some expanded cell
+    # the image sets are the oracle's (strict box test: a camera on an expanded cell's edge belongs to no block)
+    c = v["camtoworlds"][:, :3, -1]
+    _, _, exp_cells, To = O.Grid2DClustering(c, scale_factor=(1.0, 1.0), p0=0, p1=1, mx=2, my=1, num_blocks=2)
+    for k, e in enumerate(exp_cells):
+        assert np.concatenate(bids[k]).tolist() == list(O.points_in_bbox2D(c[:, :2], e, To))
     out = export_blocks(str(tmp_path / "blocks"), v, bids)
     for b, d in enumerate(out):
         back = MiniDataset().read(str(tmp_path / "blocks" / f"block_{b}"), block_id=b)

@@ -19,11 +19,19 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--cprofile", action="store_true", help="print the host profile of the timed steps")
     ap.add_argument("--raster-only", action="store_true", help="time bench.py's raster view step instead")
+    ap.add_argument("--bench-native", action="store_true",
+                    help="time bench.py's native train step (no ADMM penalty, densification statistics on)")
     args = ap.parse_args()
     from dogs_amd.admm import ADMMConfig
     from dogs_amd.admm_trainer import make_block
     dev = torch.device("cuda", 0)
-    if args.raster_only:
+    if args.bench_native:
+        import bench
+        from dogs_amd.synthetic import make_scene
+        s = make_scene(args.n, args.width, args.height, seed=1234).to(dev)
+        cams = bench.make_cameras(args.width, args.height, bench.view_yaws(args.views), dev)
+        step = bench.TrainStep(s, cams, dev, 1234).native()
+    elif args.raster_only:
         import bench
         from dogs_amd.synthetic import make_scene
         s = make_scene(args.n, args.width, args.height, seed=1234).to(dev)
