@@ -90,6 +90,7 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
     };
     float acc_l1 = 0.0f, acc_map = 0.0f;
     float ring[11][5];
+    float rawc[FUSED ? 11 : 1], rawg[FUSED ? 11 : 1];  // FUSED: the last 11 rows' clamped / target values
     float ua = lda(sp.y0 - 5), va = ldb(sp.y0 - 5);
     float ub = lda(sp.y0 - 4), vb = ldb(sp.y0 - 4);
     for (int base = 0; base < SSW_IN; base += 11) {
@@ -101,6 +102,7 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
                 ua = ub; va = vb;
                 ub = lda(sp.y0 - 5 + rr + 2);
                 vb = ldb(sp.y0 - 5 + rr + 2);
+                if (FUSED) { rawc[j] = u; rawg[j] = v; }
                 ring[j][0] = hconv11(u);
                 ring[j][1] = hconv11(u * u);
                 ring[j][2] = hconv11(v);
@@ -130,7 +132,8 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
                         const float rAB = __builtin_amdgcn_rcpf(A * B), rAAB = __builtin_amdgcn_rcpf(A * A * B),
                                     rABB = __builtin_amdgcn_rcpf(A * B * B);
                         if (FUSED) {
-                            const float c = clamp01f(img1[gi]), g = img2[gi];
+                            // output row y is input row rr - 5 (ring slot (j + 6) % 11) of column ox, lane + 5's
+                            const float c = __shfl_down(rawc[(j + 6) % 11], 5), g = __shfl_down(rawg[(j + 6) % 11], 5);
                             out_img[gi] = c;
                             acc_l1 += fabsf(c - g);
                             acc_map += (Cc * D) * rAB;

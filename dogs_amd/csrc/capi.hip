@@ -193,10 +193,6 @@ gs::DSortArgs dsort_args(const Binning& b, int64_t cap, int T, uint2* ranges, co
     d.long_list = long_list; d.long_cnt = long_cnt;
     return d;
 }
-void tile_sort(const Binning& b, int64_t cap, int T, uint2* ranges, const uint8_t* only, const uint32_t* gate,
-               uint32_t* long_list, uint32_t* long_cnt, hipStream_t s) {
-    gs::tile_depth_sort(dsort_args(b, cap, T, ranges, only, gate, long_list, long_cnt), s);
-}
 #ifdef DG_NO_FUSED_SORT  // A/B switch: the phase-1 depth sort as its own launches
 constexpr bool FUSED_SORT = false;
 #else
@@ -571,8 +567,16 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
         gs::launch_unfinished_sat(g.counters, im.unfinished, tx, ty, im.sat, s, ac ? ac->probe : nullptr);
         gs::BinArgs ba = bin_args(a, g, im, T, (uint32_t)K, b2, im.tile_cnt2, im.ranges2);
         gs::launch_bin(2, ba, g.counters + gs::CNT_K2, g.scan_tmp, s);
-        tile_sort(b2, K, T, im.ranges2, im.unfinished, gate, im.long_tiles, g.counters + gs::CNT_LONG2, s);
-    gs::RenderArgs r2 = r;
+        const gs::DSortArgs ds2 = dsort_args(b2, K, T, im.ranges2, im.unfinished, gate, im.long_tiles,
+                                             g.counters + gs::CNT_LONG2);
+        gs::RenderArgs r2 = r;
+#if defined(DG_PHASE2_WAVE_PER_TILE) || defined(DG_PHASE2_STANDALONE_SORT)
+        gs::tile_depth_sort(ds2, s);
+        r2.fuse_sort = 0;
+#else
+        r2.fuse_sort = 1;  // k_render_fwd2 sorts its tile's list itself
+#endif
+        r2.ds = ds2;
         r2.phase = 2;
         r2.K = (uint32_t)K;
         r2.ranges = im.ranges2; r2.ranges1 = im.ranges; r2.s_e = b2.se; r2.eg = b2.eg;

@@ -88,6 +88,7 @@ __device__ __forceinline__ f3 sh_to_rgb(f3 pos, const float* campos, int deg, f3
 // per step for every lane; `kept` is the precise per-tile cull (max_contrib_power <= log(255 o)).
 struct CandLDS {
     uint32_t pre[64];     // exclusive prefix of rect areas
+    int slot[64];         // per step: the lane whose rect starts at this item of the step (-1: none)
     int w[64], area[64];
     float4 co[64];        // conic.xyz, opacity
     float4 geo[64];       // mean2D.xy, log threshold, 1/rect width
@@ -113,19 +114,28 @@ __device__ __forceinline__ void wave_candidates(CandLDS& L, int lane, int x0, in
     L.geo[lane] = make_float4(mx, my, thr, area ? __builtin_amdgcn_rcpf((float)(x1 - x0)) : 0.f);
     L.rc[lane] = make_float4(rcp.x, rcp.y, __int_as_float(x0), __int_as_float(y0));
     __builtin_amdgcn_wave_barrier();
+    const uint32_t my_pre = incl - area;
+    int carry = 0;  // owner of the item just before the step
     for (uint32_t i0 = 0; i0 < total; i0 += 64) {
         const uint32_t item = i0 + (uint32_t)lane;
         const bool valid = item < total;
-        int owner = 0;
+        // owner of each item: the rects starting inside this step mark their start slot with their lane, and an
+        // item belongs to the last start at or before it (or to the owner carried over from the previous step).
+        // Zero-area lanes start nothing.  Two dependent LDS round trips instead of a 6-level binary search.
+        L.slot[lane] = -1;
+        if (area && my_pre >= i0 && my_pre - i0 < 64u) L.slot[my_pre - i0] = lane;
+        __builtin_amdgcn_wave_barrier();
+        const int sv = L.slot[lane];
+        const uint64_t starts = __ballot(sv >= 0);
+        const uint64_t upto = starts & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+        const int pos = upto ? 63 - __clzll((long long)upto) : -1;
+        const int from = __shfl(sv, pos < 0 ? 0 : pos);
+        int owner = pos >= 0 ? from : carry;
+        carry = __builtin_amdgcn_readlane(owner, 63);
         bool kept = false;
         int tx = 0, ty = 0;
+        if (!valid) owner = 0;
         if (valid) {
-            // largest lane with pre <= item (zero-area lanes share the next lane's prefix)
-            int lo = 0;
-#pragma unroll
-            for (int step = 32; step > 0; step >>= 1)
-                if (L.pre[lo + step] <= item) lo += step;
-            owner = lo;
             const int r = (int)(item - L.pre[owner]);
             const int ww = L.w[owner];
             const float4 g = L.geo[owner];
@@ -756,8 +766,9 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
 constexpr int FWD2_CHUNK = 1024;
 template <bool COUNT>
 __global__ void __launch_bounds__(256) k_render_fwd2(RenderArgs a) {
-    __shared__ __attribute__((aligned(16))) float4 s_sb[(FWD2_CHUNK + 4) * 3];
+    __shared__ __attribute__((aligned(16))) float4 s_sb[(FWD2_CHUNK + 4) * 3];  // (also the sort's scratch)
     __shared__ uint32_t s_mx[4];
+    __shared__ uint32_t s_ids[DS_WAVE_MAX2];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tile = blockIdx.x;
     // the adaptive capacity's probe gets this view's phase-2 instance count (the next view's k_depth_cut reads it)
@@ -780,6 +791,22 @@ __global__ void __launch_bounds__(256) k_render_fwd2(RenderArgs a) {
     const uint32_t cbase = a.ranges1[tile].y - a.ranges1[tile].x;
     const uint2 rg = a.ranges[tile];
     const int n = (int)(rg.y - rg.x);
+    // fused sort (no standalone phase-2 sort launches): wave 0 sorts a list of up to DS_WAVE_MAX2 into s_ids (and
+    // back to s_e for the backward), the block sorts a longer one in place through the global scratch -- the same
+    // two routines, so the same order, as k_tile_dsort / k_tile_dsort_long
+    bool lds_ids = false;
+    if (a.fuse_sort && n > 1) {
+        uint32_t* scr = reinterpret_cast<uint32_t*>(s_sb);
+        if (n <= DS_WAVE_MAX2) {
+            if (w == 0) wave_sort_tile<DS_ROWS2>(a.ds, tile, lane, scr, scr + 256, scr + 256 + DS_WAVE_MAX2, s_ids, 1);
+            lds_ids = true;
+        } else {
+            block_sort_long(a.ds, tile, scr, reinterpret_cast<uint32_t(*)[BS_RADIX]>(scr + BS_RADIX),
+                            reinterpret_cast<uint32_t(*)[BS_WAVES]>(scr + BS_RADIX * (1 + BS_WAVES)),
+                            reinterpret_cast<int*>(scr + BS_RADIX * (1 + BS_WAVES) + 2 * BS_WAVES));
+        }
+        __syncthreads();
+    }
     for (int base = 0; base < n; base += FWD2_CHUNK) {
         const int cnt = n - base < FWD2_CHUNK ? n - base : FWD2_CHUNK;
         // the previous chunk is consumed by every wave; stop when every pixel of the tile has saturated
@@ -787,7 +814,7 @@ __global__ void __launch_bounds__(256) k_render_fwd2(RenderArgs a) {
         for (int j = threadIdx.x; j < cnt + 4; j += 256) {
             float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;  // past the end: the null splat (opacity 0)
             if (j < cnt) {
-                const uint32_t e = min(a.s_e[rg.x + base + j], a.K - 1);
+                const uint32_t e = min(lds_ids ? s_ids[base + j] : a.s_e[rg.x + base + j], a.K - 1);
                 const uint32_t g = min(a.eg[e], a.P - 1);
                 const float4 s0 = a.sp[2 * g], s1 = a.sp[2 * g + 1];
                 const float4 q = a.rgbi[g];

@@ -229,4 +229,109 @@ __device__ __forceinline__ int wave_sort_tile(const DSortArgs& a, int tile, int 
     return n;
 }
 
+// ---- long lists (n > a wave's capacity): one 256-thread block, LSD radix through global scratch (k_a, k_b, s_tmp)
+constexpr int BS_RADIX = 256;
+constexpr int BS_WAVES = 4;
+
+// One stable LSD step of the long-list sort by the 256-thread block: (key(v) - kmin) digits, (keys, vals) ping-pong
+// through global scratch in 256-item chunks.  `key` maps a value to its sort key.  Result in va.
+template <typename KeyFn>
+__device__ __forceinline__ void block_radix_global(uint32_t*& va, uint32_t*& vb, uint32_t* ka, uint32_t* kb, uint32_t n,
+                                   KeyFn&& key, uint32_t* s_base, uint32_t (*s_wh)[BS_RADIX], uint32_t (*s_red)[BS_WAVES]) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint64_t lt = lanemask_lt();
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+    for (uint32_t i = t; i < n; i += 256) {
+        const uint32_t kk = key(va[i]);
+        ka[i] = kk;
+        kmin = kk < kmin ? kk : kmin;
+        kmax = kk > kmax ? kk : kmax;
+    }
+    kmin = wave_min_u32(kmin);
+    kmax = wave_max_u32(kmax);
+    __syncthreads();
+    if (lane == 0) { s_red[0][w] = kmin; s_red[1][w] = kmax; }
+    __syncthreads();
+    kmin = s_red[0][0]; kmax = s_red[1][0];
+    for (int q = 1; q < BS_WAVES; q++) {
+        kmin = s_red[0][q] < kmin ? s_red[0][q] : kmin;
+        kmax = s_red[1][q] > kmax ? s_red[1][q] : kmax;
+    }
+    const int passes = passes_for(kmax - kmin);
+    for (int p = 0; p < passes; p++) {
+        const int shift = 8 * p;
+        __syncthreads();
+        s_base[t] = 0u;
+        __syncthreads();
+        for (uint32_t i = t; i < n; i += 256) atomicAdd(&s_base[((ka[i] - kmin) >> shift) & 0xffu], 1u);
+        __syncthreads();
+        {  // exclusive scan of the digit counts (thread t = digit t)
+            const uint32_t c = s_base[t];
+            uint32_t x = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o);
+                if (lane >= o) x += y;
+            }
+            if (lane == 63) s_red[0][w] = x;
+            __syncthreads();
+            uint32_t off = 0;
+            for (int q = 0; q < w; q++) off += s_red[0][q];
+            s_base[t] = off + x - c;
+        }
+        __syncthreads();
+        for (uint32_t c0 = 0; c0 < n; c0 += 256) {
+            const uint32_t i = c0 + t;
+            const bool act = i < n;
+            const uint32_t kk = act ? ka[i] : 0u;
+            const uint32_t val = act ? va[i] : 0u;
+            const uint32_t d = ((kk - kmin) >> shift) & 0xffu;
+            const uint64_t m = peer_mask(d, act);
+            const uint32_t before = (uint32_t)__popcll(m & lt);
+#pragma unroll
+            for (int q = 0; q < BS_WAVES; q++) s_wh[q][t] = 0u;
+            __syncthreads();
+            if (act && before == 0) s_wh[w][d] = (uint32_t)__popcll(m);
+            __syncthreads();
+            if (act) {
+                uint32_t pos = s_base[d] + before;
+                for (int q = 0; q < w; q++) pos += s_wh[q][d];
+                kb[pos] = kk;
+                vb[pos] = val;
+            }
+            __syncthreads();
+            s_base[t] += s_wh[0][t] + s_wh[1][t] + s_wh[2][t] + s_wh[3][t];
+            __syncthreads();
+        }
+        uint32_t* tk = ka; ka = kb; kb = tk;
+        uint32_t* tv = va; va = vb; vb = tv;
+    }
+    __syncthreads();
+}
+
+// Block-level sort of one long list (n > DS_WAVE_MAX): LSD radix through global scratch; with equal keys it sorts by
+// Gaussian index first and then, stably, by key.
+__device__ __forceinline__ void block_sort_long(const DSortArgs& a, int tile, uint32_t* s_base, uint32_t (*s_wh)[BS_RADIX],
+                                uint32_t (*s_red)[BS_WAVES], int* s_tie) {
+    const int t = threadIdx.x;
+    const uint2 rg = a.ranges[tile];
+    const uint32_t n = rg.y - rg.x;
+    uint32_t *va = a.s_e + rg.x, *vb = a.s_tmp + rg.x;
+    auto dkey = [&](uint32_t x) { return ds_key(a, x); };
+    block_radix_global(va, vb, a.k_a + rg.x, a.k_b + rg.x, n, dkey, s_base, s_wh, s_red);
+    if (t == 0) *s_tie = 0;
+    __syncthreads();
+    for (uint32_t i = t + 1; i < n; i += 256)
+        if (ds_key(a, va[i]) == ds_key(a, va[i - 1])) *s_tie = 1;
+    __syncthreads();
+    if (*s_tie) {  // rare: order by Gaussian index first, then stably by key
+        block_radix_global(va, vb, a.k_a + rg.x, a.k_b + rg.x, n, [&](uint32_t x) { return ds_gid(a, x); }, s_base,
+                           s_wh, s_red);
+        block_radix_global(va, vb, a.k_a + rg.x, a.k_b + rg.x, n, dkey, s_base, s_wh, s_red);
+    }
+    if (va != a.s_e + rg.x)  // result in the scratch values: copy back into s_e
+        for (uint32_t i = t; i < n; i += 256) a.s_e[rg.x + i] = va[i];
+    __syncthreads();
+}
+
 }  // namespace gs
