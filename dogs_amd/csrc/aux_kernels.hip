@@ -110,6 +110,13 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
                 ring[j][4] = hconv11(u * v);
                 const int y = sp.y0 + rr - 10;
                 if (rr >= 10 && y < H) {
+                    // FUSED: output row y is input row rr - 5 (ring slot (j + 6) % 11) of column ox, which lane + 5
+                    // holds (shuffled by the whole wave, outside the output-column branch)
+                    float oc = 0.0f, og = 0.0f;
+                    if (FUSED) {
+                        oc = __shfl_down(rawc[(j + 6) % 11], 5);
+                        og = __shfl_down(rawg[(j + 6) % 11], 5);
+                    }
                     float m[5] = {0, 0, 0, 0, 0};
 #pragma unroll
                     for (int k = 0; k < 11; k++) {
@@ -132,8 +139,7 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
                         const float rAB = __builtin_amdgcn_rcpf(A * B), rAAB = __builtin_amdgcn_rcpf(A * A * B),
                                     rABB = __builtin_amdgcn_rcpf(A * B * B);
                         if (FUSED) {
-                            // output row y is input row rr - 5 (ring slot (j + 6) % 11) of column ox, lane + 5's
-                            const float c = __shfl_down(rawc[(j + 6) % 11], 5), g = __shfl_down(rawg[(j + 6) % 11], 5);
+                            const float c = oc, g = og;
                             out_img[gi] = c;
                             acc_l1 += fabsf(c - g);
                             acc_map += (Cc * D) * rAB;
