@@ -410,17 +410,20 @@ struct BinLane {
     float4 co;
     bool member;
 };
+// known: membership from the count pass's wave mask (0 / 1: no key test, no SAT test), -1: test here
 template <int PHASE>
-__device__ __forceinline__ BinLane bin_lane(const BinArgs& a, int g, int lane, uint32_t thr, uint32_t* s_key) {
+__device__ __forceinline__ BinLane bin_lane(const BinArgs& a, int g, int lane, uint32_t thr, uint32_t* s_key,
+                                            int known = -1) {
     BinLane b = {0, 0, 0, 0, 0.f, 0.f, 0.f, make_float4(0.f, 0.f, 0.f, 0.f), false};
-    if (lane < EMIT_RANKS && g < a.P) {
+    if (lane < EMIT_RANKS && g < a.P && known != 0) {
         const uint32_t key = a.dkey[g];
         s_key[lane] = key;
-        bool m = key != 0xffffffffu && (PHASE == 1 ? key < thr : key >= thr);
+        bool m = known == 1 || (key != 0xffffffffu && (PHASE == 1 ? key < thr : key >= thr));
         if (m) {
             const float4 s0 = a.sp[2 * g], s1 = a.sp[2 * g + 1];
             sp_rect(s1, b.x0, b.y0, b.x1, b.y1);
-            if (PHASE == 2) m = b.x1 > b.x0 && b.y1 > b.y0 && sat_rect(a.sat, a.tiles_x, b.x0, b.y0, b.x1, b.y1) != 0u;
+            if (PHASE == 2 && known < 0)
+                m = b.x1 > b.x0 && b.y1 > b.y0 && sat_rect(a.sat, a.tiles_x, b.x0, b.y0, b.x1, b.y1) != 0u;
             if (m) {
                 b.co = make_float4(s0.z, s0.w, s1.x, s1.y);
                 b.mx = s0.x; b.my = s0.y;
@@ -447,8 +450,10 @@ __global__ void __launch_bounds__(256) k_bin_count(BinArgs a) {
     if (g0 >= a.P) return;  // whole wave (past the last one the scan reads)
     const int g = g0 + lane;
     const BinLane b = bin_lane<PHASE>(a, g, lane, a.counters[CNT_THR], s_key[w]);
+    const uint64_t members = __ballot(b.member);
+    if (lane == 0) a.wmask[wave] = members;  // the emission pass skips the membership tests
     uint32_t c = 0;
-    if (__any(b.member)) {
+    if (members) {
         wave_count(s_cand[w], s_cnt[w], lane, b.x0, b.y0, b.x1, b.y1, b.mx, b.my, b.co, b.lthr,
                    [&](int tx, int ty) { return PHASE == 1 || a.unf[ty * a.tiles_x + tx] != 0; },
                    [&](int tx, int ty) { atomicAdd(&a.tile_cnt[ty * a.tiles_x + tx], 1u); });
@@ -475,9 +480,10 @@ __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
     const int wave = blockIdx.x * 4 + w;
     const int g0 = wave * EMIT_RANKS;
     if (g0 >= a.P) return;
+    const uint64_t members = a.wmask[wave];
+    if (!members) return;  // no member in this wave (no key, record or SAT loads)
     const int g = g0 + lane;
-    const BinLane b = bin_lane<PHASE>(a, g, lane, a.counters[CNT_THR], s_key[w]);
-    if (!__any(b.member)) return;
+    const BinLane b = bin_lane<PHASE>(a, g, lane, a.counters[CNT_THR], s_key[w], (int)((members >> lane) & 1ull));
     const uint32_t base = a.wtot[wave];
     const uint32_t c = b.member ? a.rcnt[g] : 0u;
     uint32_t incl = c;
