@@ -320,6 +320,8 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ v4f bc4(float x) { return (v4f){x, x, x, x}; }
 __device__ __forceinline__ v4f fma4(v4f a, v4f b, v4f c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ v4f cat4(v2f lo, v2f hi) { return (v4f){lo.x, lo.y, hi.x, hi.y}; }
+__device__ __forceinline__ v2f lo2(v4f v) { return (v2f){v.x, v.y}; }
+__device__ __forceinline__ v2f hi2(v4f v) { return (v2f){v.z, v.w}; }
 // p = dx (A dx + B dy) + C dy^2 for the 4 pixels; identical per-pixel arithmetic to splat_power2
 __device__ __forceinline__ v4f splat_power4(float A, float B, float C, float sx, float sy, v4f pxv, v2f pyv) {
     const v2f dy = bc2(sy) - pyv;

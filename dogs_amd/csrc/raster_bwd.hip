@@ -102,17 +102,16 @@ __device__ __forceinline__ void replay_splat(const RenderBwdArgs& a, const float
 #pragma unroll
     for (int k = 0; k < 4; k++) dLda[k] = ok[k] ? dLda[k] : 0.0f;
     T = T * oma;
-    // per-splat moments over the lane's 4 pixels; lo + hi of a v4 = the two row sums {row A, row B}
+    // per-splat moments over the lane's 4 pixels; lo + hi of a v4 = the two row sums {row A, row B}.  A sum of
+    // products folds its hi half in with an fma (one packed op fewer per moment than product, product, add).
     const v4f t4 = G * dLda;
     const v4f tdx = t4 * dx;
-    const v4f tdx2 = tdx * dx;
-    const v2f rt = (v2f){t4.x, t4.y} + (v2f){t4.z, t4.w};
-    const v2f rtx = (v2f){tdx.x, tdx.y} + (v2f){tdx.z, tdx.w};
-    const v2f rtxx = (v2f){tdx2.x, tdx2.y} + (v2f){tdx2.z, tdx2.w};
-    const v4f w0 = wgt * g0, w1 = wgt * g1, w2 = wgt * g2;
-    const v2f rc0 = (v2f){w0.x, w0.y} + (v2f){w0.z, w0.w};
-    const v2f rc1 = (v2f){w1.x, w1.y} + (v2f){w1.z, w1.w};
-    const v2f rc2 = (v2f){w2.x, w2.y} + (v2f){w2.z, w2.w};
+    const v2f rt = lo2(t4) + hi2(t4);
+    const v2f rtx = lo2(tdx) + hi2(tdx);
+    const v2f rtxx = fma2(hi2(tdx), hi2(dx), lo2(tdx) * lo2(dx));
+    const v2f rc0 = fma2(hi2(wgt), hi2(g0), lo2(wgt) * lo2(g0));
+    const v2f rc1 = fma2(hi2(wgt), hi2(g1), lo2(wgt) * lo2(g1));
+    const v2f rc2 = fma2(hi2(wgt), hi2(g2), lo2(wgt) * lo2(g2));
     const v2f u = rt * dy;  // {tA dyA, tB dyB}
     float p[10];
     p[0] = rtx.x + rtx.y;                            // SGx
@@ -125,8 +124,7 @@ __device__ __forceinline__ void replay_splat(const RenderBwdArgs& a, const float
     p[7] = rc1.x + rc1.y;
     p[8] = rc2.x + rc2.y;
     if (HAS_INVD) {
-        const v4f wd = wgt * gd;
-        const v2f rcd = (v2f){wd.x, wd.y} + (v2f){wd.z, wd.w};
+        const v2f rcd = fma2(hi2(wgt), hi2(gd), lo2(wgt) * lo2(gd));
         p[9] = rcd.x + rcd.y;
     } else {
         p[9] = 0.0f;
