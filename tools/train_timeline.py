@@ -12,7 +12,28 @@ def load(path):
     return rows
 
 
+def by_kind(out):
+    """One trace holding both routes (trainer_bench.py --alternate): steps classified by their kernels."""
+    f = glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True)
+    rows = load(f[0])
+    idx = [i for i, r in enumerate(rows) if "k_activate_fwd" in r["Kernel_Name"]]
+    spans = {"unfused": [], "folded": []}
+    ksum = {"unfused": [], "folded": []}
+    for a, b in zip(idx, idx[1:]):
+        names = " ".join(r["Kernel_Name"] for r in rows[a:b])
+        kind = "unfused" if "k_activate_bwd" in names else "folded"
+        spans[kind].append((int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1000)
+        ksum[kind].append(sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[a:b]) / 1000)
+    for k in spans:
+        sp, ks = sorted(spans[k]), sorted(ksum[k])
+        if sp:
+            print(f"{k}: {len(sp)} steps, span median {sp[len(sp) // 2]:.1f} us, kernel sum median {ks[len(ks) // 2]:.1f} us")
+
+
 def main(out):
+    if os.environ.get("BY_KIND"):
+        by_kind(out)
+        return
     for route in ("unfused", "folded"):
         f = glob.glob(os.path.join(out, route, "**", "*kernel_trace.csv"), recursive=True)
         if not f:

@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--cprofile", action="store_true", help="print the host profile of the timed steps")
     ap.add_argument("--raster-only", action="store_true", help="time bench.py's raster view step instead")
+    ap.add_argument("--alternate", action="store_true",
+                    help="alternate the native step's routes (DG_TRAIN_UNFUSED on/off) every 10 steps")
     ap.add_argument("--bench-native", action="store_true",
                     help="time bench.py's native train step (no ADMM penalty, densification statistics on)")
     args = ap.parse_args()
@@ -53,7 +55,12 @@ def main():
         prof = cProfile.Profile()
         prof.enable()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if args.alternate and i % 10 == 0:
+            if (i // 10) % 2 == 0:
+                os.environ["DG_TRAIN_UNFUSED"] = "1"
+            else:
+                os.environ.pop("DG_TRAIN_UNFUSED", None)
         h = time.perf_counter()
         step()
         host.append(time.perf_counter() - h)
