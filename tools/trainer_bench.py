@@ -54,9 +54,16 @@ def main():
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
+    blocks = {"unfused": [], "folded": []}
     t0 = time.perf_counter()
+    tb = t0
     for i in range(args.steps):
         if args.alternate and i % 10 == 0:
+            torch.cuda.synchronize()
+            now = time.perf_counter()
+            if i:
+                blocks["unfused" if ((i // 10) - 1) % 2 == 0 else "folded"].append((now - tb) / 10)
+            tb = now
             if (i // 10) % 2 == 0:
                 os.environ["DG_TRAIN_UNFUSED"] = "1"
             else:
@@ -64,6 +71,13 @@ def main():
         h = time.perf_counter()
         step()
         host.append(time.perf_counter() - h)
+    if args.alternate:
+        torch.cuda.synchronize()
+        blocks["unfused" if ((args.steps // 10) - 1) % 2 == 0 else "folded"].append((time.perf_counter() - tb) / 10)
+        for k, v in blocks.items():
+            if v:
+                v = sorted(v)
+                print(f"{k}: 10-step blocks {len(v)}, ms per step min {v[0] * 1e3:.4f} median {v[len(v) // 2] * 1e3:.4f}")
     torch.cuda.synchronize()
     if prof is not None:
         prof.disable()
