@@ -578,22 +578,149 @@ __global__ void __launch_bounds__(256) k_gauss_live(GaussBwdArgs a) {
     }
 }
 
+// computeColorFromSH backward (backward.cu:23-144) of one Gaussian; clamped flags recomputed from the forward rgb.
+// VEC: degree 3 with 15 rest rows (the bench / training layout), the row read and dL/dsh written with dword-aligned
+// dwordx4 accesses (45 dword accesses per lane, each touching its own cache line, made the per-Gaussian pass bound by
+// the address units); SHV(k, ch) reads coefficient (k, ch) from registers (VEC) or memory.
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+// a 3-float row as one dwordx2 + one dword access (rows are only 4-B aligned)
+__device__ __forceinline__ f3 ld3(const float* p) {
+    const f2u v = *reinterpret_cast<const f2u*>(p);
+    return {v.x, v.y, p[2]};
+}
+__device__ __forceinline__ void st3(float* p, float x, float y, float z) {
+    *reinterpret_cast<f2u*>(p) = f2u{x, y};
+    p[2] = z;
+}
+template <bool VEC, typename Get>
+__device__ __forceinline__ void sh_bwd(const GaussBwdArgs& a, int idx, f3 mean, f3 dcv, const float (&acc)[10],
+                                       Get&& SHV, float* dsh_row, f3& dmean) {
+    {
+        const float d0p[3] = {dcv.x, dcv.y, dcv.z};
+        const int deg = VEC ? 3 : a.D;
+        const f3 dir_orig = {mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]};
+        const float len = sqrtf(fmaf(dir_orig.z, dir_orig.z, fmaf(dir_orig.y, dir_orig.y, dir_orig.x * dir_orig.x)));
+        const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+        // forward colour (same expression as raster_fwd.hip sh_to_rgb) for the clamp mask
+        float basis[15];
+        int nb = 0;
+        float xx = 0, yy = 0, zz = 0, xy = 0, yz = 0, xz = 0;
+        if (deg > 0) {
+            basis[0] = -SH_C1 * y; basis[1] = SH_C1 * z; basis[2] = -SH_C1 * x; nb = 3;
+            if (deg > 1) {
+                xx = x * x; yy = y * y; zz = z * z; xy = x * y; yz = y * z; xz = x * z;
+                basis[3] = SH_C2[0] * xy;
+                basis[4] = SH_C2[1] * yz;
+                basis[5] = SH_C2[2] * (2.0f * zz - xx - yy);
+                basis[6] = SH_C2[3] * xz;
+                basis[7] = SH_C2[4] * (xx - yy);
+                nb = 8;
+                if (deg > 2) {
+                    basis[8] = SH_C3[0] * y * (3.0f * xx - yy);
+                    basis[9] = SH_C3[1] * xy * z;
+                    basis[10] = SH_C3[2] * y * (4.0f * zz - xx - yy);
+                    basis[11] = SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
+                    basis[12] = SH_C3[4] * x * (4.0f * zz - xx - yy);
+                    basis[13] = SH_C3[5] * z * (xx - yy);
+                    basis[14] = SH_C3[6] * x * (xx - 3.0f * yy);
+                    nb = 15;
+                }
+            }
+        }
+        float dRGB[3];
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) {
+            float r = SH_C0 * d0p[ch];
+#pragma unroll
+            for (int k = 0; k < 15; k++)
+                if (k < nb) r = fmaf(basis[k], SHV(k, ch), r);
+            r += 0.5f;
+            dRGB[ch] = (r < 0) ? 0.0f : acc[6 + ch];
+        }
+        st3(a.ddc + 3 * idx, SH_C0 * dRGB[0], SH_C0 * dRGB[1], SH_C0 * dRGB[2]);
+        float dx[3] = {0, 0, 0}, dy[3] = {0, 0, 0}, dz[3] = {0, 0, 0};
+        if (deg > 0) {
+            for (int ch = 0; ch < 3; ch++) {
+                dx[ch] = -SH_C1 * SHV(2, ch); dy[ch] = -SH_C1 * SHV(0, ch); dz[ch] = SH_C1 * SHV(1, ch);
+            }
+            if (deg > 1) {
+                for (int ch = 0; ch < 3; ch++) {
+                    dx[ch] += SH_C2[0] * y * SHV(3, ch) + SH_C2[2] * 2.f * -x * SHV(5, ch) + SH_C2[3] * z * SHV(6, ch) + SH_C2[4] * 2.f * x * SHV(7, ch);
+                    dy[ch] += SH_C2[0] * x * SHV(3, ch) + SH_C2[1] * z * SHV(4, ch) + SH_C2[2] * 2.f * -y * SHV(5, ch) + SH_C2[4] * 2.f * -y * SHV(7, ch);
+                    dz[ch] += SH_C2[1] * y * SHV(4, ch) + SH_C2[2] * 2.f * 2.f * z * SHV(5, ch) + SH_C2[3] * x * SHV(6, ch);
+                }
+                if (deg > 2) {
+                    for (int ch = 0; ch < 3; ch++) {
+                        dx[ch] += (SH_C3[0] * SHV(8, ch) * 3.f * 2.f * xy + SH_C3[1] * SHV(9, ch) * yz + SH_C3[2] * SHV(10, ch) * -2.f * xy +
+                                   SH_C3[3] * SHV(11, ch) * -3.f * 2.f * xz + SH_C3[4] * SHV(12, ch) * (-3.f * xx + 4.f * zz - yy) +
+                                   SH_C3[5] * SHV(13, ch) * 2.f * xz + SH_C3[6] * SHV(14, ch) * 3.f * (xx - yy));
+                        dy[ch] += (SH_C3[0] * SHV(8, ch) * 3.f * (xx - yy) + SH_C3[1] * SHV(9, ch) * xz +
+                                   SH_C3[2] * SHV(10, ch) * (-3.f * yy + 4.f * zz - xx) + SH_C3[3] * SHV(11, ch) * -3.f * 2.f * yz +
+                                   SH_C3[4] * SHV(12, ch) * -2.f * xy + SH_C3[5] * SHV(13, ch) * -2.f * yz + SH_C3[6] * SHV(14, ch) * -3.f * 2.f * xy);
+                        dz[ch] += (SH_C3[1] * SHV(9, ch) * xy + SH_C3[2] * SHV(10, ch) * 4.f * 2.f * yz +
+                                   SH_C3[3] * SHV(11, ch) * 3.f * (2.f * zz - xx - yy) + SH_C3[4] * SHV(12, ch) * 4.f * 2.f * xz +
+                                   SH_C3[5] * SHV(13, ch) * (xx - yy));
+                    }
+                }
+            }
+        }
+        // dL/dsh of the active rows (the rest stays zero); VEC: 11 dwordx4 stores + 1 instead of 45 dword stores
+        if (VEC) {
+            float o[45];
+#pragma unroll
+            for (int k = 0; k < 15; k++)
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) o[3 * k + ch] = basis[k] * dRGB[ch];
+#pragma unroll
+            for (int i = 0; i < 11; i++)
+                *reinterpret_cast<f4u*>(dsh_row + 4 * i) = f4u{o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]};
+            dsh_row[44] = o[44];
+        } else {
+            for (int k = 0; k < nb; k++)
+                for (int ch = 0; ch < 3; ch++) dsh_row[3 * k + ch] = basis[k] * dRGB[ch];
+        }
+        const f3 ddir = {dx[0] * dRGB[0] + dx[1] * dRGB[1] + dx[2] * dRGB[2], dy[0] * dRGB[0] + dy[1] * dRGB[1] + dy[2] * dRGB[2],
+                         dz[0] * dRGB[0] + dz[1] * dRGB[1] + dz[2] * dRGB[2]};
+        // dnormvdv (auxiliary.h:118-128)
+        const f3 v = dir_orig;
+        const float sum2 = fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
+        const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+        dmean.x += ((sum2 - v.x * v.x) * ddir.x - v.y * v.x * ddir.y - v.z * v.x * ddir.z) * invsum32;
+        dmean.y += (-v.x * v.y * ddir.x + (sum2 - v.y * v.y) * ddir.y - v.z * v.y * ddir.z) * invsum32;
+        dmean.z += (-v.x * v.z * ddir.x - v.y * v.z * ddir.y + (sum2 - v.z * v.z) * ddir.z) * invsum32;
+    }
+}
+
 // One contributing Gaussian: every gradient output of it (dL/dsh row included) is written here.
 __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, const float (&sums)[10]) {
     const int M = a.M;
     float* dsh_row = a.dsh ? a.dsh + (size_t)idx * M * 3 : nullptr;
     // every per-Gaussian input is loaded up front: one HBM round trip instead of dependent ones
     const float4 sp0 = a.sp[2 * (size_t)idx], sp1 = a.sp[2 * (size_t)idx + 1];
-    const f3 mean = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+    const f3 mean = ld3(a.means3D + 3 * idx);
     f3 scl = {0.f, 0.f, 0.f};
     f4 rot = {0.f, 0.f, 0.f, 0.f};
     if (a.scales) {
-        scl = {a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
-        rot = {a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]};
+        scl = ld3(a.scales + 3 * idx);
+        const f4u q = *reinterpret_cast<const f4u*>(a.rotations + 4 * idx);
+        rot = {q.x, q.y, q.z, q.w};
     }
     const float opac = a.antialiasing ? a.opacities[idx] : 0.f;
     f3 dcv = {0.f, 0.f, 0.f};
-    if (a.sh) dcv = {a.dc[3 * idx], a.dc[3 * idx + 1], a.dc[3 * idx + 2]};
+    if (a.sh) dcv = ld3(a.dc + 3 * idx);
+    // degree 3, 15 rest rows: the SH row in registers, loaded here with the other inputs (11 dwordx4 + 1)
+    const bool shvec = a.sh && a.D >= 3 && M == 15;
+    float shv[45];
+    if (shvec) {
+        const float* shp = a.sh + (size_t)idx * 45;
+#pragma unroll
+        for (int i = 0; i < 11; i++) {
+            const f4u v = *reinterpret_cast<const f4u*>(shp + 4 * i);
+            shv[4 * i] = v.x; shv[4 * i + 1] = v.y; shv[4 * i + 2] = v.z; shv[4 * i + 3] = v.w;
+        }
+        shv[44] = shp[44];
+    }
     // ---- records -> dL/d(mean2D, conic, opacity, color, invdepth): summed by the wave (see below)
     float acc[10];
 #pragma unroll
@@ -609,12 +736,8 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, co
         acc[3] = (-0.5f * so) * SGxy;
         acc[4] = (-0.5f * so) * SGyy;
     }
-    a.dmeans2D[3 * idx + 0] = acc[0];
-    a.dmeans2D[3 * idx + 1] = acc[1];
-    a.dmeans2D[3 * idx + 2] = 0.f;
-    a.dcolors[3 * idx + 0] = acc[6];
-    a.dcolors[3 * idx + 1] = acc[7];
-    a.dcolors[3 * idx + 2] = acc[8];
+    st3(a.dmeans2D + 3 * idx, acc[0], acc[1], 0.f);
+    st3(a.dcolors + 3 * idx, acc[6], acc[7], acc[8]);
     float dLo = acc[5];
     const float dL_dinvd = acc[9];
 
@@ -673,7 +796,9 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, co
     } else {
         for (int i = 0; i < 6; i++) dcov[i] = 0.f;
     }
-    for (int i = 0; i < 6; i++) a.dcov3D[6 * idx + i] = dcov[i];
+    *reinterpret_cast<f2u*>(a.dcov3D + 6 * idx) = f2u{dcov[0], dcov[1]};  // 8-B aligned rows: three dwordx2
+    *reinterpret_cast<f2u*>(a.dcov3D + 6 * idx + 2) = f2u{dcov[2], dcov[3]};
+    *reinterpret_cast<f2u*>(a.dcov3D + 6 * idx + 4) = f2u{dcov[4], dcov[5]};
     const m3& V = st.V;
     const float dT00 = 2 * (T00 * V.m[0][0] + T01 * V.m[0][1] + T02 * V.m[0][2]) * dcxx + (T10 * V.m[0][0] + T11 * V.m[0][1] + T12 * V.m[0][2]) * dcxy;
     const float dT01 = 2 * (T00 * V.m[1][0] + T01 * V.m[1][1] + T02 * V.m[1][2]) * dcxx + (T10 * V.m[1][0] + T11 * V.m[1][1] + T12 * V.m[1][2]) * dcxy;
@@ -707,94 +832,16 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, co
         dmean.z += (proj[8] * m_w - proj[11] * mul1) * gx + (proj[9] * m_w - proj[11] * mul2) * gy;
     }
 
-    // ---- computeColorFromSH backward (backward.cu:23-144); clamped flags recomputed from the forward rgb
-    if (a.sh) {
+    // ---- computeColorFromSH backward
+    if (shvec) {
+        sh_bwd<true>(a, idx, mean, dcv, acc, [&](int k, int ch) { return shv[3 * k + ch]; }, dsh_row, dmean);
+    } else if (a.sh) {
         const float* __restrict__ sh = a.sh + (size_t)idx * M * 3;
-        const float d0p[3] = {dcv.x, dcv.y, dcv.z};
-        const int deg = a.D;
-        const f3 dir_orig = {mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]};
-        const float len = sqrtf(fmaf(dir_orig.z, dir_orig.z, fmaf(dir_orig.y, dir_orig.y, dir_orig.x * dir_orig.x)));
-        const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
-        // forward colour (same expression as raster_fwd.hip sh_to_rgb) for the clamp mask
-        float basis[15];
-        int nb = 0;
-        float xx = 0, yy = 0, zz = 0, xy = 0, yz = 0, xz = 0;
-        if (deg > 0) {
-            basis[0] = -SH_C1 * y; basis[1] = SH_C1 * z; basis[2] = -SH_C1 * x; nb = 3;
-            if (deg > 1) {
-                xx = x * x; yy = y * y; zz = z * z; xy = x * y; yz = y * z; xz = x * z;
-                basis[3] = SH_C2[0] * xy;
-                basis[4] = SH_C2[1] * yz;
-                basis[5] = SH_C2[2] * (2.0f * zz - xx - yy);
-                basis[6] = SH_C2[3] * xz;
-                basis[7] = SH_C2[4] * (xx - yy);
-                nb = 8;
-                if (deg > 2) {
-                    basis[8] = SH_C3[0] * y * (3.0f * xx - yy);
-                    basis[9] = SH_C3[1] * xy * z;
-                    basis[10] = SH_C3[2] * y * (4.0f * zz - xx - yy);
-                    basis[11] = SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
-                    basis[12] = SH_C3[4] * x * (4.0f * zz - xx - yy);
-                    basis[13] = SH_C3[5] * z * (xx - yy);
-                    basis[14] = SH_C3[6] * x * (xx - 3.0f * yy);
-                    nb = 15;
-                }
-            }
-        }
-        float dRGB[3];
-        for (int ch = 0; ch < 3; ch++) {
-            float r = SH_C0 * d0p[ch];
-            for (int k = 0; k < nb; k++) r = fmaf(basis[k], sh[3 * k + ch], r);
-            r += 0.5f;
-            dRGB[ch] = (r < 0) ? 0.0f : acc[6 + ch];
-        }
-        for (int ch = 0; ch < 3; ch++) a.ddc[3 * idx + ch] = SH_C0 * dRGB[ch];
-        float dx[3] = {0, 0, 0}, dy[3] = {0, 0, 0}, dz[3] = {0, 0, 0};
-#define SHV(k, ch) sh[3 * (k) + (ch)]
-        if (deg > 0) {
-            for (int ch = 0; ch < 3; ch++) {
-                dx[ch] = -SH_C1 * SHV(2, ch); dy[ch] = -SH_C1 * SHV(0, ch); dz[ch] = SH_C1 * SHV(1, ch);
-            }
-            if (deg > 1) {
-                for (int ch = 0; ch < 3; ch++) {
-                    dx[ch] += SH_C2[0] * y * SHV(3, ch) + SH_C2[2] * 2.f * -x * SHV(5, ch) + SH_C2[3] * z * SHV(6, ch) + SH_C2[4] * 2.f * x * SHV(7, ch);
-                    dy[ch] += SH_C2[0] * x * SHV(3, ch) + SH_C2[1] * z * SHV(4, ch) + SH_C2[2] * 2.f * -y * SHV(5, ch) + SH_C2[4] * 2.f * -y * SHV(7, ch);
-                    dz[ch] += SH_C2[1] * y * SHV(4, ch) + SH_C2[2] * 2.f * 2.f * z * SHV(5, ch) + SH_C2[3] * x * SHV(6, ch);
-                }
-                if (deg > 2) {
-                    for (int ch = 0; ch < 3; ch++) {
-                        dx[ch] += (SH_C3[0] * SHV(8, ch) * 3.f * 2.f * xy + SH_C3[1] * SHV(9, ch) * yz + SH_C3[2] * SHV(10, ch) * -2.f * xy +
-                                   SH_C3[3] * SHV(11, ch) * -3.f * 2.f * xz + SH_C3[4] * SHV(12, ch) * (-3.f * xx + 4.f * zz - yy) +
-                                   SH_C3[5] * SHV(13, ch) * 2.f * xz + SH_C3[6] * SHV(14, ch) * 3.f * (xx - yy));
-                        dy[ch] += (SH_C3[0] * SHV(8, ch) * 3.f * (xx - yy) + SH_C3[1] * SHV(9, ch) * xz +
-                                   SH_C3[2] * SHV(10, ch) * (-3.f * yy + 4.f * zz - xx) + SH_C3[3] * SHV(11, ch) * -3.f * 2.f * yz +
-                                   SH_C3[4] * SHV(12, ch) * -2.f * xy + SH_C3[5] * SHV(13, ch) * -2.f * yz + SH_C3[6] * SHV(14, ch) * -3.f * 2.f * xy);
-                        dz[ch] += (SH_C3[1] * SHV(9, ch) * xy + SH_C3[2] * SHV(10, ch) * 4.f * 2.f * yz +
-                                   SH_C3[3] * SHV(11, ch) * 3.f * (2.f * zz - xx - yy) + SH_C3[4] * SHV(12, ch) * 4.f * 2.f * xz +
-                                   SH_C3[5] * SHV(13, ch) * (xx - yy));
-                    }
-                }
-            }
-        }
-#undef SHV
-        // dL/dsh overwrites the staged coefficients in place (all reads of them are above)
-        for (int k = 0; k < nb; k++)
-            for (int ch = 0; ch < 3; ch++) dsh_row[3 * k + ch] = basis[k] * dRGB[ch];  // the rest stays zero
-        const f3 ddir = {dx[0] * dRGB[0] + dx[1] * dRGB[1] + dx[2] * dRGB[2], dy[0] * dRGB[0] + dy[1] * dRGB[1] + dy[2] * dRGB[2],
-                         dz[0] * dRGB[0] + dz[1] * dRGB[1] + dz[2] * dRGB[2]};
-        // dnormvdv (auxiliary.h:118-128)
-        const f3 v = dir_orig;
-        const float sum2 = fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
-        const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
-        dmean.x += ((sum2 - v.x * v.x) * ddir.x - v.y * v.x * ddir.y - v.z * v.x * ddir.z) * invsum32;
-        dmean.y += (-v.x * v.y * ddir.x + (sum2 - v.y * v.y) * ddir.y - v.z * v.y * ddir.z) * invsum32;
-        dmean.z += (-v.x * v.z * ddir.x - v.y * v.z * ddir.y + (sum2 - v.z * v.z) * ddir.z) * invsum32;
+        sh_bwd<false>(a, idx, mean, dcv, acc, [&](int k, int ch) { return sh[3 * k + ch]; }, dsh_row, dmean);
     } else {
         for (int ch = 0; ch < 3; ch++) a.ddc[3 * idx + ch] = 0.f;
     }
-    a.dmeans3D[3 * idx + 0] = dmean.x;
-    a.dmeans3D[3 * idx + 1] = dmean.y;
-    a.dmeans3D[3 * idx + 2] = dmean.z;
+    st3(a.dmeans3D + 3 * idx, dmean.x, dmean.y, dmean.z);
 
     // ---- computeCov3D backward (backward.cu:330-393)
     if (a.scales) {
@@ -810,14 +857,16 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, co
         for (int i = 0; i < 3; i++) for (int jx = 0; jx < 3; jx++) dM.m[i][jx] *= 2.0f;
         const m3 Rt = m3_T(R);
         m3 D = m3_T(dM);
-        for (int k = 0; k < 3; k++)
-            a.dscales[3 * idx + k] = fmaf(Rt.m[k][2], D.m[k][2], fmaf(Rt.m[k][1], D.m[k][1], Rt.m[k][0] * D.m[k][0]));
+        float dsc[3];
+        for (int k = 0; k < 3; k++) dsc[k] = fmaf(Rt.m[k][2], D.m[k][2], fmaf(Rt.m[k][1], D.m[k][1], Rt.m[k][0] * D.m[k][0]));
+        st3(a.dscales + 3 * idx, dsc[0], dsc[1], dsc[2]);
         for (int jx = 0; jx < 3; jx++) { D.m[0][jx] *= s.x; D.m[1][jx] *= s.y; D.m[2][jx] *= s.z; }
-        float* dq = a.drot + 4 * idx;
+        float dq[4];
         dq[0] = 2 * z * (D.m[0][1] - D.m[1][0]) + 2 * y * (D.m[2][0] - D.m[0][2]) + 2 * x * (D.m[1][2] - D.m[2][1]);
         dq[1] = 2 * y * (D.m[1][0] + D.m[0][1]) + 2 * z * (D.m[2][0] + D.m[0][2]) + 2 * r * (D.m[1][2] - D.m[2][1]) - 4 * x * (D.m[2][2] + D.m[1][1]);
         dq[2] = 2 * x * (D.m[1][0] + D.m[0][1]) + 2 * r * (D.m[2][0] - D.m[0][2]) + 2 * z * (D.m[1][2] + D.m[2][1]) - 4 * y * (D.m[2][2] + D.m[0][0]);
         dq[3] = 2 * r * (D.m[0][1] - D.m[1][0]) + 2 * x * (D.m[2][0] + D.m[0][2]) + 2 * y * (D.m[1][2] + D.m[2][1]) - 4 * z * (D.m[1][1] + D.m[0][0]);
+        *reinterpret_cast<f4u*>(a.drot + 4 * idx) = f4u{dq[0], dq[1], dq[2], dq[3]};
     } else {
         for (int k = 0; k < 3; k++) a.dscales[3 * idx + k] = 0.f;
         for (int k = 0; k < 4; k++) a.drot[4 * idx + k] = 0.f;
