@@ -317,6 +317,21 @@ __device__ __forceinline__ v2f splat_power2(float A, float B, float C, v2f dx, f
 // Four pixels per lane as {(c0, rA), (c0, rB), (c1, rA), (c1, rB)}: two columns c0, c0 + 8 of two rows
 // rA, rA + 8.  Each packed op's halves are independent rows, and lo + hi gives the two row sums.
 typedef float v4f __attribute__((ext_vector_type(4)));
+// Per-lane rows of a few floats (Gaussian parameters and gradients) are only 4-B aligned; one dwordx2/x3/x4 access per
+// row instead of one dword access per float: a wave's dword access touches up to 64 cache lines, and 45 of them per SH
+// row made the per-Gaussian passes bound by the address units.
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+// a 3-float row as one dwordx2 + one dword access (rows are only 4-B aligned)
+__device__ __forceinline__ f3 ld3(const float* p) {
+    const f2u v = *reinterpret_cast<const f2u*>(p);
+    return {v.x, v.y, p[2]};
+}
+__device__ __forceinline__ void st3(float* p, float x, float y, float z) {
+    *reinterpret_cast<f2u*>(p) = f2u{x, y};
+    p[2] = z;
+}
+
 __device__ __forceinline__ v4f bc4(float x) { return (v4f){x, x, x, x}; }
 __device__ __forceinline__ v4f fma4(v4f a, v4f b, v4f c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ v4f cat4(v2f lo, v2f hi) { return (v4f){lo.x, lo.y, hi.x, hi.y}; }

@@ -582,17 +582,6 @@ __global__ void __launch_bounds__(256) k_gauss_live(GaussBwdArgs a) {
 // VEC: degree 3 with 15 rest rows (the bench / training layout), the row read and dL/dsh written with dword-aligned
 // dwordx4 accesses (45 dword accesses per lane, each touching its own cache line, made the per-Gaussian pass bound by
 // the address units); SHV(k, ch) reads coefficient (k, ch) from registers (VEC) or memory.
-typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
-typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
-// a 3-float row as one dwordx2 + one dword access (rows are only 4-B aligned)
-__device__ __forceinline__ f3 ld3(const float* p) {
-    const f2u v = *reinterpret_cast<const f2u*>(p);
-    return {v.x, v.y, p[2]};
-}
-__device__ __forceinline__ void st3(float* p, float x, float y, float z) {
-    *reinterpret_cast<f2u*>(p) = f2u{x, y};
-    p[2] = z;
-}
 template <bool VEC, typename Get>
 __device__ __forceinline__ void sh_bwd(const GaussBwdArgs& a, int idx, f3 mean, f3 dcv, const float (&acc)[10],
                                        Get&& SHV, float* dsh_row, f3& dmean) {
