@@ -373,10 +373,12 @@ __device__ __forceinline__ void seg_level(uint32_t own, float (&v)[10]) {
     // rows the DPP does not write, and lanes without a source, keep `old`: owner ~0 (never a lane's owner), value 0
     const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)own, CTRL, ROW_MASK, 0xf, false);
     const bool same = up == own;
+    // sum, then select: the DPP move folds into the add (v_add_f32_dpp), two VALU per value instead of three
 #pragma unroll
     for (int k = 0; k < 10; k++) {
         const float t = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[k]), CTRL, ROW_MASK, 0xf, false));
-        v[k] += same ? t : 0.f;
+        const float s = v[k] + t;
+        v[k] = same ? s : v[k];
     }
 }
 __device__ __forceinline__ bool sum_step(const GaussBwdArgs& a, uint32_t i0, uint32_t lo, uint32_t hi, uint32_t skip,
