@@ -207,10 +207,36 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
         }
         qlast[2 * (k & 1) + (k >> 1)] = __builtin_amdgcn_readfirstlane(m);
     }
+#ifndef DG_BWD_NO_PREFETCH
+    // The batch gather is a dependent chain (list slot -> emission index -> Gaussian -> splat record).  The first two
+    // links of batch b + 1 (and the first of b + 2) are loaded while batch b replays, so a batch start waits on one
+    // HBM round trip instead of three.
+    auto slot_of = [&](int j) -> uint32_t {  // emission index of list position j (phase-2 entries: local index)
+        if (j >= n) return 0u;
+        return j < n1 ? min(a.s_e[rg.x + j], a.K1 - 1) : min(a.s_e2[rg2.x + (uint32_t)(j - n1)], a.K - 1 - E1);
+    };
+    auto gauss_of = [&](int j, uint32_t e) -> uint32_t {
+        if (j >= n) return 0u;
+        return j < n1 ? min(a.eg[e], a.P - 1) : min(a.eg2[e], a.P - 1);
+    };
+    uint32_t e_cur = slot_of(lane), e_nxt = slot_of(64 + lane);
+    uint32_t g_cur = gauss_of(lane, e_cur);
+#endif
     for (int base = 0; base < n; base += 64) {
         const int j = base + lane;
         uint32_t qm = 0;
+#ifndef DG_BWD_NO_PREFETCH
+        const uint32_t ee_b = j < n1 ? e_cur : E1 + e_cur, g_b = g_cur;
+        if (base + 64 < n) {
+            g_cur = gauss_of(j + 64, e_nxt);
+            e_cur = e_nxt;
+            e_nxt = slot_of(j + 128);
+        }
+#endif
         if (j < n) {
+#ifndef DG_BWD_NO_PREFETCH
+            const uint32_t ee = ee_b, g = g_b;
+#else
             uint32_t ee, g;
             if (j < n1) {
                 ee = min(a.s_e[rg.x + j], a.K1 - 1);
@@ -220,6 +246,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
                 ee = E1 + el;
                 g = min(a.eg2[el], a.P - 1);
             }
+#endif
             const float4 s0 = a.sp[2 * g], s1 = a.sp[2 * g + 1];
             const float2 m = make_float2(s0.x, s0.y);
             const float4 c4 = make_float4(s0.z, s0.w, s1.x, s1.y);
