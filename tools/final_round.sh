@@ -13,4 +13,7 @@ bash tools/profile.sh "$OUT/prof" pmc
 python3 tools/pmc_traffic.py "$OUT/prof" 1000000 1920 1080 > "$OUT/pmc_traffic.log" 2>&1
 cp profiles/pmc_traffic.json "$OUT/pmc_traffic.json"
 python3 tools/pmc_summary.py "$OUT/prof" > "$OUT/pmc_summary.txt" 2>&1
+# the raw per-dispatch counter dumps exceed gpurun's copy-back limit: keep the summaries and the trace statistics
+cp "$OUT"/prof/trace/*kernel_stats.csv "$OUT/" 2>/dev/null || true
+rm -rf "$OUT"/prof/pmc* "$OUT"/prof/trace/*kernel_trace.csv
 timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
