@@ -135,7 +135,7 @@ struct GaussBwdArgs {
     uint32_t* live_cnt;      // [chunks]
 };
 #ifndef DG_SUM_STEPS
-#define DG_SUM_STEPS 4
+#define DG_SUM_STEPS 2
 #endif
 constexpr uint32_t SUM_STEPS = DG_SUM_STEPS;      // 64-instance steps per record-sum chunk
 constexpr uint32_t SUM_CHUNK = 64u * SUM_STEPS;

@@ -572,7 +572,10 @@ __global__ void __launch_bounds__(256) k_gauss_sum(GaussBwdArgs a, uint32_t sum_
 }
 
 // LIVE_CHUNKS chunk lists per block (grid-stride), one lane per listed Gaussian (~7 per chunk on the bench scene).
-constexpr int LIVE_CHUNKS = 16;
+#ifndef DG_LIVE_CHUNKS
+#define DG_LIVE_CHUNKS 16
+#endif
+constexpr int LIVE_CHUNKS = DG_LIVE_CHUNKS;
 __global__ void __launch_bounds__(256) k_gauss_live(GaussBwdArgs a) {
     __shared__ uint32_t s_pre[LIVE_CHUNKS + 1];
     const SumRange R = sum_range(a);
