@@ -87,6 +87,12 @@ struct Carver {
 
 inline int tiles_x_of(int W) { return (W + 15) / 16; }
 inline int tiles_y_of(int H) { return (H + 15) / 16; }
+inline int unf_rw_of(int tiles_x) { return (tiles_x + 63) / 64; }  // bitmask words per tile row
+#ifdef DG_PHASE2_SAT  // A/B switch: phase-2 membership from a summed-area table (two launches per view)
+constexpr bool UNF_ROWS = false;
+#else
+constexpr bool UNF_ROWS = true;
+#endif
 
 struct Geom {
     uint32_t* counters;  // CNT_* (raster.h)
@@ -145,7 +151,11 @@ Image carve_image(void* base, int W, int H) {
     im.ranges2 = c.take<uint2>(T);
     im.unfinished = c.take<uint8_t>(T);
     im.resume = c.take<float4>(HW);
-    im.sat = c.take<uint32_t>((size_t)(tiles_x_of(W) + 1) * (tiles_y_of(H) + 1));
+    {  // the SAT of the A/B build, or the phase-2 row bitmasks (u64: rows, column OR, row summary)
+        const size_t txs = (size_t)tiles_x_of(W), tys = (size_t)tiles_y_of(H);
+        const size_t sat_n = (txs + 1) * (tys + 1), rows_n = 2 * ((tys + 1) * ((txs + 63) / 64) + (tys + 63) / 64);
+        im.sat = c.take<uint32_t>(sat_n > rows_n ? sat_n : rows_n);
+    }
     im.long_tiles = c.take<uint32_t>(T);
     im.tile_cnt = c.take<uint32_t>(T);
     im.tile_cnt2 = c.take<uint32_t>(T);
@@ -184,6 +194,7 @@ gs::BinArgs bin_args(const dg_raster_args* r, const Geom& g, const Image& im, in
     a.P = P; a.tiles_x = tx; a.num_tiles = T; a.dkey = g.dkey; a.sp = g.sp; a.counters = g.counters;
     a.unf = im.unfinished; a.sat = im.sat; a.wtot = g.wtot; a.wmask = g.wmask; a.cap = cap; a.first_e = g.first_e; a.rcnt = g.rcnt;
     a.eg = b.eg; a.ikey = b.ik; a.tile_cnt = tile_cnt; a.ranges = ranges; a.s_e = b.se;
+    a.unf_rows = nullptr; a.unf_rw = 0; a.unf_th = 0; a.probe = nullptr;
     return a;
 }
 // per-tile (depth, index) order of a phase's binned lists
@@ -471,6 +482,8 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     fill_pre(pre, a);
     pre.radii = radii; pre.sp = g.sp; pre.depthkey = g.dkey; pre.cnt = g.cnt; pre.rcnt = g.rcnt;
     pre.hist = g.hist;
+    pre.unf_rows = UNF_ROWS ? reinterpret_cast<unsigned long long*>(im.sat) : nullptr;  // (the SAT block is larger)
+    pre.unf_words = UNF_ROWS ? (ty + 1) * unf_rw_of(tx) + (ty + 63) / 64 : 0;  // rows, column OR, row summary
     // per-block rect sums land in the wave-total array (ceil(P/64) u32 >= ceil(P/256) u64), free until the binning
     pre.rect_part = reinterpret_cast<unsigned long long*>(g.wtot); pre.err = g.counters + gs::CNT_ERR;
     const uint32_t nparts = (uint32_t)((P + 255) / 256);
@@ -533,6 +546,7 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     r.img_invd = im.img_invd; r.n_contrib = im.n_contrib; r.max_contrib = im.max_contrib;
     r.phase = 1; r.counters = g.counters; r.unfinished = im.unfinished; r.resume = im.resume;
     r.ranges2_zero = im.ranges2;
+    r.unf_rows = pre.unf_rows; r.unf_rw = unf_rw_of(tx);
     r.gcount = gcount;
     r.fuse_sort = fuse ? 1 : 0;
     r.ds = ds1;
@@ -566,8 +580,11 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     const uint32_t* gate = g.counters + gs::CNT_UNFINISHED;
     {
         PROF("phase2");
-        gs::launch_unfinished_sat(g.counters, im.unfinished, tx, ty, im.sat, s, ac ? ac->probe : nullptr);
+        if (!UNF_ROWS) gs::launch_unfinished_sat(g.counters, im.unfinished, tx, ty, im.sat, s, ac ? ac->probe : nullptr);
         gs::BinArgs ba = bin_args(a, g, im, T, (uint32_t)K, b2, im.tile_cnt2, im.ranges2);
+        ba.unf_rows = UNF_ROWS ? reinterpret_cast<const unsigned long long*>(im.sat) : nullptr;
+        ba.unf_rw = unf_rw_of(tx); ba.unf_th = ty;
+        ba.probe = UNF_ROWS && ac ? ac->probe : nullptr;
         gs::launch_bin(2, ba, g.counters + gs::CNT_K2, g.scan_tmp, s);
         const gs::DSortArgs ds2 = dsort_args(b2, K, T, im.ranges2, im.unfinished, gate, im.long_tiles,
                                              g.counters + gs::CNT_LONG2);

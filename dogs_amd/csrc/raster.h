@@ -31,6 +31,8 @@ struct PreArgs {
     unsigned long long* rect_part;  // [blocks] per-block sums of rect areas (k_depth_cut totals them: num_rendered);
                                     // bit 63 = a prefiltered violation in the block (-> counters[CNT_ERR])
     uint32_t* err;
+    unsigned long long* unf_rows;  // [unf_words] per-tile-row bitmasks of unfinished tiles, zeroed here (set by the render)
+    int unf_words;
 };
 
 // Counters block at the head of the geometry state (device, uint32 slots).
@@ -82,6 +84,8 @@ struct RenderArgs {
     int fuse_sort;
     DSortArgs ds;
     uint32_t* probe;            // optional (phase 2, adaptive capacity): [1] <- counters[CNT_K2]
+    unsigned long long* unf_rows;  // phase 1: bit tx % 64 of word ty * unf_rw + tx / 64 set for each unfinished tile
+    int unf_rw;
 };
 
 struct RenderBwdArgs {
@@ -176,6 +180,10 @@ struct BinArgs {
     uint32_t* tile_cnt;          // [num_tiles] zero on entry: counts, then arrival cursors
     uint2* ranges;               // [num_tiles] per-tile [start, end) of s_e
     uint32_t* s_e;               // instances grouped by tile
+    const unsigned long long* unf_rows;  // phase 2: per-row bitmasks of the unfinished tiles (RenderArgs::unf_rows)
+    int unf_rw;                  // words per tile row
+    int unf_th;                  // tile rows
+    uint32_t* probe;             // optional (phase 2, adaptive capacity): [0] <- counters[CNT_UNFINISHED]
 };
 void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s);
 size_t bin_scan_temp_bytes(int P);

@@ -232,6 +232,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     const int base = blockIdx.x * 256;
     const int idx = base + t;
     for (int i = base + t; i < DH_BINS; i += gridDim.x * 256) a.hist[i] = 0u;  // for k_depth_hist
+    for (int i = base + t; i < a.unf_words; i += gridDim.x * 256) a.unf_rows[i] = 0ull;  // for the phase-1 render
     if (t == 0) s_err = 0u;
     __syncthreads();
     a.err = &s_err;  // a prefiltered violation flags the block (bit 63 of its part)
@@ -400,6 +401,35 @@ __device__ __forceinline__ void wave_count(CandLDS& L, uint32_t* cnt, int lane, 
 constexpr int EMIT_RANKS = DG_EMIT_RANKS;  // Gaussians per wave of the binning walks
 
 __device__ __forceinline__ uint32_t sat_rect(const uint32_t* sat, int tx, int x0, int y0, int x1, int y1);
+// does the tile rect [x0,x1) x [y0,y1) hold an unfinished tile.  Layout of unf_rows (rw = words per tile row, th =
+// tile rows): [th * rw] per-row bitmasks, [rw] their OR over all rows (columns holding an unfinished tile), [(th + 63)
+// / 64] rows holding one.  The two summaries reject most rects with a load or two (every lane of a wave reads the same
+// few words); the rows are walked four at a time only for rects that pass both.
+__device__ __forceinline__ unsigned long long bits_range(int lo, int hi, int w) {  // bits [lo, hi) within word w
+    const int a = lo - 64 * w > 0 ? lo - 64 * w : 0, b = hi - 64 * w < 64 ? hi - 64 * w : 64;
+    if (b <= a) return 0ull;
+    return (b == 64 ? ~0ull : ((1ull << b) - 1ull)) & ~((1ull << a) - 1ull);
+}
+__device__ __forceinline__ bool rows_touch(const BinArgs& a, int x0, int y0, int x1, int y1) {
+    const int w0 = x0 >> 6, w1 = (x1 - 1) >> 6;
+    const unsigned long long* cols = a.unf_rows + (size_t)a.unf_th * a.unf_rw;
+    const unsigned long long* rany = cols + a.unf_rw;
+    bool c = false, r = false;
+    for (int w = w0; w <= w1; w++) c |= (cols[w] & bits_range(x0, x1, w)) != 0ull;
+    for (int w = y0 >> 6; w <= (y1 - 1) >> 6; w++) r |= (rany[w] & bits_range(y0, y1, w)) != 0ull;
+    if (!(c && r)) return false;
+    for (int w = w0; w <= w1; w++) {
+        const unsigned long long m = bits_range(x0, x1, w);
+        for (int y = y0; y < y1; y += 4) {
+            unsigned long long v = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (y + k < y1) v |= a.unf_rows[(size_t)(y + k) * a.unf_rw + w];
+            if (v & m) return true;
+        }
+    }
+    return false;
+}
 
 // The binned Gaussians of a wave (EMIT_RANKS consecutive indices) and their walk inputs.
 //   phase 1: the prefix Gaussians (key < thr);
@@ -422,8 +452,12 @@ __device__ __forceinline__ BinLane bin_lane(const BinArgs& a, int g, int lane, u
         if (m) {
             const float4 s0 = a.sp[2 * g], s1 = a.sp[2 * g + 1];
             sp_rect(s1, b.x0, b.y0, b.x1, b.y1);
+#ifdef DG_PHASE2_SAT
             if (PHASE == 2 && known < 0)
                 m = b.x1 > b.x0 && b.y1 > b.y0 && sat_rect(a.sat, a.tiles_x, b.x0, b.y0, b.x1, b.y1) != 0u;
+#else
+            if (PHASE == 2 && known < 0) m = b.x1 > b.x0 && b.y1 > b.y0 && rows_touch(a, b.x0, b.y0, b.x1, b.y1);
+#endif
             if (m) {
                 b.co = make_float4(s0.z, s0.w, s1.x, s1.y);
                 b.mx = s0.x; b.my = s0.y;
@@ -443,6 +477,7 @@ __global__ void __launch_bounds__(256) k_bin_count(BinArgs a) {
     __shared__ CandLDS s_cand[4];
     __shared__ uint32_t s_key[4][64];
     __shared__ uint32_t s_cnt[4][64];
+    if (PHASE == 2 && a.probe && blockIdx.x == 0 && threadIdx.x == 0) a.probe[0] = a.counters[CNT_UNFINISHED];
     if (PHASE == 2 && a.counters[CNT_UNFINISHED] == 0u) return;  // phase 1 finished every tile
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wave = blockIdx.x * 4 + w;
@@ -748,6 +783,12 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
             if (unf) {
                 atomicAdd(a.counters + CNT_UNFINISHED, 1u);
                 a.ranges2_zero[tile] = make_uint2(0u, 0u);  // empty unless phase 2 bins instances for it
+                if (a.unf_rows) {  // row word, column summary, row summary (rows_touch's layout)
+                    const int th = (a.num_tiles + a.tiles_x - 1) / a.tiles_x;
+                    atomicOr(a.unf_rows + (size_t)ty * a.unf_rw + (tx >> 6), 1ull << (tx & 63));
+                    atomicOr(a.unf_rows + (size_t)th * a.unf_rw + (tx >> 6), 1ull << (tx & 63));
+                    atomicOr(a.unf_rows + (size_t)(th + 1) * a.unf_rw + (ty >> 6), 1ull << (ty & 63));
+                }
             }
         }
         if (unf) {
