@@ -704,6 +704,83 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
         // Splats go in groups of FWD_GROUP with no branch between them (a group's missing tail is the null splat), and the
         // saturation exit is tested once per group: per-splat control flow costs more than the null splats do.
         while (mask) {
+#ifdef DG_FWD_FAST
+          // Two passes over the group: alphas first, then a wave-uniform test of whether any pixel's T can fall below
+          // 1e-4 inside the group (T only falls, and the chained product is exactly the per-splat test_T sequence).
+          // When none can, the group commits without the termination selects; otherwise the per-splat sequence runs.
+          int jg[FWD_GROUP];
+          v4f alg[FWD_GROUP];
+          uint32_t accb[FWD_GROUP];
+          v4f Tt = T;
+#pragma unroll
+          for (int u = 0; u < FWD_GROUP; u++) {
+            const int jj = mask ? (int)__builtin_ctzll(mask) : 64;
+            mask &= mask - 1;
+            jg[u] = jj;
+            const float4 Sa = sb[jj * 3 + 0], Sb = sb[jj * 3 + 1];
+            const v4f p2 = splat_power4(Sa.z, Sa.w, Sb.x, Sa.x, Sa.y, pxv, pyv);
+            v4f al = bc4(Sb.y) * (v4f){__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y),
+                                       __builtin_amdgcn_exp2f(p2.z), __builtin_amdgcn_exp2f(p2.w)};
+            uint32_t ab = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float ak = fminf(0.99f, al[k]);
+                const bool ok = !(p2[k] > 0.0f || ak < thr[k]);
+                al[k] = ok ? ak : 0.0f;
+                ab |= ok ? (1u << k) : 0u;
+            }
+            alg[u] = al;
+            accb[u] = ab;
+            Tt = Tt * (bc4(1.0f) - al);
+          }
+          const bool safe = !COUNT && !__any(fminf(fminf(Tt.x, Tt.y), fminf(Tt.z, Tt.w)) < 0.0001f);
+          if (safe) {
+#pragma unroll
+            for (int u = 0; u < FWD_GROUP; u++) {
+              const float4 Sb = sb[jg[u] * 3 + 1], Sc = sb[jg[u] * 3 + 2];
+              const uint32_t c = cbase + (uint32_t)(base + jg[u] + 1);
+              const v4f wt = alg[u] * T;
+              C0 = fma4(bc4(Sb.z), wt, C0);
+              C1 = fma4(bc4(Sb.w), wt, C1);
+              C2 = fma4(bc4(Sc.x), wt, C2);
+              D = fma4(bc4(Sc.y), wt, D);
+              T = T * (bc4(1.0f) - alg[u]);
+#pragma unroll
+              for (int k = 0; k < 4; k++) last[k] = (accb[u] >> k) & 1u ? c : last[k];
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < FWD_GROUP; u++) {
+              const float4 Sb = sb[jg[u] * 3 + 1], Sc = sb[jg[u] * 3 + 2];
+              const uint32_t c = cbase + (uint32_t)(base + jg[u] + 1);
+              v4f al = alg[u];
+              const v4f test_T = T * (bc4(1.0f) - al);
+              v4f Tn;
+              bool acc[4];
+#pragma unroll
+              for (int k = 0; k < 4; k++) {
+                  acc[k] = (accb[u] >> k) & 1u;
+                  const bool term = test_T[k] < 0.0001f;
+                  thr[k] = term ? 2.0f : thr[k];
+                  al[k] = term ? 0.0f : al[k];
+                  Tn[k] = term ? T[k] : test_T[k];
+                  last[k] = (acc[k] && !term) ? c : last[k];
+              }
+              if (COUNT) {
+                  uint32_t n = 0;
+#pragma unroll
+                  for (int k = 0; k < 4; k++) n += (uint32_t)__popcll(__ballot(acc[k] && al[k] != 0.0f));
+                  if (n && lane == 0) atomicAdd(a.gcount + __float_as_uint(Sc.z), n);
+              }
+              const v4f wt = al * T;
+              C0 = fma4(bc4(Sb.z), wt, C0);
+              C1 = fma4(bc4(Sb.w), wt, C1);
+              C2 = fma4(bc4(Sc.x), wt, C2);
+              D = fma4(bc4(Sc.y), wt, D);
+              T = Tn;
+            }
+          }
+#else
 #pragma unroll
           for (int u = 0; u < FWD_GROUP; u++) {
             const int jj = mask ? (int)__builtin_ctzll(mask) : 64;
@@ -744,6 +821,7 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
             D = fma4(bc4(Sc.y), wt, D);
             T = Tn;
           }
+#endif
             // early exit, checked every 8 splats (splats after saturation leave every pixel unchanged)
             if (!__any(fminf(fminf(thr.x, thr.y), fminf(thr.z, thr.w)) < 1.0f)) break;
         }
