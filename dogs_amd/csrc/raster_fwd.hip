@@ -12,6 +12,7 @@
 //   k_render_fwd   one wave per 16x16 tile, 4 pixels per lane as two row pairs evaluated with packed fp32
 //                  (v_pk_*_f32); a 64-splat batch is staged in wave-private LDS and read back with broadcast
 //                  ds_read_b128; splats that cannot reach a quadrant pair skip it; wave-uniform early exit.
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include "gs_common.h"
 #include "raster.h"
@@ -781,6 +782,9 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
             }
           }
 #else
+          // TERM = false: the group cannot take any pixel's T below 1e-4, so the termination selects are dropped
+          auto group = [&](auto term_c) {
+          constexpr bool TERM = decltype(term_c)::value;
 #pragma unroll
           for (int u = 0; u < FWD_GROUP; u++) {
             const int jj = mask ? (int)__builtin_ctzll(mask) : 64;
@@ -802,7 +806,7 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
             v4f Tn;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const bool term = test_T[k] < 0.0001f;
+                const bool term = TERM && test_T[k] < 0.0001f;
                 thr[k] = term ? 2.0f : thr[k];
                 al[k] = term ? 0.0f : al[k];
                 Tn[k] = term ? T[k] : test_T[k];
@@ -821,6 +825,29 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
             D = fma4(bc4(Sc.y), wt, D);
             T = Tn;
           }
+          };
+#ifdef DG_FWD_BOUND
+          // Exact, wave-uniform bound: a splat's alpha is at most min(0.99, opacity), and rounded products and
+          // differences are monotone, so the chain min_live(T) * prod(1 - min(0.99, opacity)) bounds every live
+          // pixel's T after the group from below (margin 1.001 for the exp2 approximation at 0).  Finished pixels
+          // (threshold 2) accept nothing and do not count.
+          float tb = 1.0f;
+#pragma unroll
+          for (int k = 0; k < 4; k++) tb = fminf(tb, thr[k] < 1.0f ? T[k] : 1.0f);
+          {
+            uint64_t m2 = mask;
+#pragma unroll
+            for (int u = 0; u < FWD_GROUP; u++) {
+              const int jj = m2 ? (int)__builtin_ctzll(m2) : 64;
+              m2 &= m2 - 1;
+              tb = tb * (1.0f - fminf(0.99f, sb[jj * 3 + 1].y));
+            }
+          }
+          if (!COUNT && !__any(tb < 1.001e-4f)) group(std::false_type{});
+          else group(std::true_type{});
+#else
+          group(std::true_type{});
+#endif
 #endif
             // early exit, checked every 8 splats (splats after saturation leave every pixel unchanged)
             if (!__any(fminf(fminf(thr.x, thr.y), fminf(thr.z, thr.w)) < 1.0f)) break;
