@@ -80,6 +80,28 @@ def reference_view_bytes(N: int, K: int, HW: int) -> float:
     return 856.0 * N + 172.0 * K + 64.0 * HW
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return int(sk.getsockname()[1])
+
+
+def relaunch_command(gpus: int | None, argv: list, environ) -> list | None:
+    """`bench.py --gpus N` (N > 1) outside a launcher: the torch.distributed.run command that runs it as N ranks, one
+    per GPU (the reference launches its trainer the same way, scripts/train/train_admm_master.sh:34-42); None when
+    this process is already a rank or N <= 1."""
+    if gpus is None or gpus <= 1 or "WORLD_SIZE" in environ:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *argv]
+
+
+def check_world(gpus: int | None, ws: int) -> None:
+    if gpus is not None and gpus != ws:
+        raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started {ws} rank(s) (WORLD_SIZE)")
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -373,7 +395,8 @@ def load_pmc(n: int, W: int, H: int):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); > 1 without a launcher relaunches under torch.distributed.run")
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--n", type=int, default=1_000_000)
@@ -390,11 +413,32 @@ def main():
     ap.add_argument("--admm-interval", type=int, default=200, help="local steps per round (urban3d_admm.yaml:44)")
     ap.add_argument("--admm-seq", type=int, default=-1,
                     help="blocks of the sequential single-GPU baseline on rank 0 (-1: the world size when > 1)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="plumbing check, no GPU: every rank joins a gloo group, all_reduces its rank and rank 0 "
+                         "prints the world it saw (tests/test_bench_launch.py)")
     ap.add_argument("--no-reference-k", action="store_true",
                     help="skip the untimed depth-prefix-off forwards (profiling runs: keeps kernel averages clean)")
     args = ap.parse_args()
+    # nothing has touched the GPU yet: the launcher runs as a child process (never an exec from this process)
+    cmd = relaunch_command(args.gpus, sys.argv[1:], os.environ)
+    if cmd is not None:
+        import subprocess
+        print("[bench] launching " + " ".join(cmd), file=sys.stderr)
+        sys.exit(subprocess.call(cmd))
 
     ws, rank, local = dist_env()
+    check_world(args.gpus, ws)
+    if args.launch_check:
+        if ws > 1:
+            dist.init_process_group("gloo")
+        t = torch.tensor([rank], dtype=torch.int64)
+        if ws > 1:
+            dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"n_gpus": ws, "rank_sum": int(t.item()), "gpus_arg": args.gpus}))
+        if ws > 1:
+            dist.destroy_process_group()
+        return
     # one rank per GPU over RCCL ("nccl" on ROCm).  DOGS_DIST_BACKEND=gloo + DOGS_BENCH_SHARE_DEVICE=1 rehearse the
     # multi-rank control flow with several ranks on one GPU (RCCL needs distinct devices).
     backend = os.environ.get("DOGS_DIST_BACKEND", "nccl")

@@ -84,7 +84,7 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count"
            "dg_densify_gather", "dg_splat_pack", "dg_ply_pack", "dg_ring_create", "dg_ring_submit", "dg_ring_next",
            "dg_ring_upload", "dg_ring_pending", "dg_ring_destroy", "dg_image_u8_to_chw", "dg_points_in_boxes2d", "dg_activate_forward", "dg_activate_backward", "dg_clamp_l1_blocks",
            "dg_clamp_l1_forward", "dg_clamp_l1_backward", "dg_adaptive_capacity", "dg_debug_counters", "dg_adam_update_groups_prox", "dg_train_step",
-           "dg_colmap_cameras", "dg_colmap_images", "dg_colmap_points3d",
+           "dg_colmap_cameras", "dg_colmap_images", "dg_colmap_points3d", "dg_prune_select", "dg_prune_gather_stats",
            "dg_last_error", "dg_version")
 
 _lib = None
@@ -187,6 +187,11 @@ def load(path: str | None = None):
             L.dg_densify_count.argtypes = [dp, ALLOC_FN, vp, vp]
             L.dg_densify_gather.restype = C.c_int
             L.dg_densify_gather.argtypes = [dp, vp]
+            if hasattr(L, "dg_prune_select"):
+                L.dg_prune_select.restype = C.c_int
+                L.dg_prune_select.argtypes = [dp, vp, ALLOC_FN, vp, vp]
+                L.dg_prune_gather_stats.restype = C.c_int
+                L.dg_prune_gather_stats.argtypes = [dp, vp, vp, vp, vp, vp]
         if hasattr(L, "dg_splat_pack"):
             L.dg_splat_pack.restype = C.c_int
             L.dg_splat_pack.argtypes = [C.c_uint32, vp, vp, vp, vp, vp, vp, ALLOC_FN, vp, vp]

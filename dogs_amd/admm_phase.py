@@ -1,0 +1,240 @@
+"""The ADMM phase entry: from per-block models trained independently up to densify_end_iter to the consensus phase's
+block split (MasterGaussianSplatTrainer.fuse_local_gaussians, conerf/trainers/master_gaussian_trainer.py:557-618),
+without the RPC master.
+
+Reference order (rank 0's master, once, at the first round with iteration >= densify_end_iter):
+    1. fuse_block_gaussians (:37-100): every block's model clipped to its ORIGINAL point box in the oriented-bbox frame
+       (points_in_bbox2D of x, y), then concatenated in block order;
+    2. prune_gaussians_after_merge (:103-121): prune_list over every block's cameras (LightGaussian count renders of
+       the fused model) -> calculate_v_imp_score -> prune_gaussians(0.4 * prune_percent);
+    3. num_gaussians = the pruned count, the denominator of the initial penalties (setup_penalty_parameters, :326-335);
+    4. select_gaussians_in_each_block (:124-172): the Gaussians inside no EXPANDED box are dropped, then each block
+       takes the Gaussians inside its expanded box (overlaps belong to several blocks), visibility_count = bincount;
+    5. new block trainers from the sub-models, penalties set, duals set up, ADMM enabled.
+
+Here every rank runs the entry for its own block ("one block per GPU"):
+    * the blocks' tensors are all-gathered (variable row counts: one all_gather of the sizes, one of the padded
+      [N_max, 59] rows), so every rank fuses the same global model -- clipping, concatenation, the box tests and the
+      prune compaction are deterministic, so the ranks agree bit for bit without further exchange;
+    * the count renders are split across ranks: rank r renders its own block's cameras only, and the per-block
+      importance sums are all-gathered and added in block order (the cameras' work is parallel, the sum order fixed);
+    * the expanded-box split, visibility_count and the rank's sub-model follow locally.
+The importance of a Gaussian is therefore sum_b (sum over block b's cameras, last camera first) instead of one sum
+over the concatenated camera list (prune_list pops the whole list from the end): the same terms, associated per block,
+a float rounding difference only (the counts are integers and exact).  `SequentialPhase` (tests) restates it in one
+process with the same association.
+
+The device work goes through `PhaseKernels` (HIP: dg_rasterize_count, dg_points_in_boxes2d, dg_prune_select +
+dg_densify_gather); the CPU tests substitute restatements of the same three operations to check the distributed
+plumbing with gloo.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .admm import PARAM_NAMES
+from .gaussian_model import GaussianSplatModel, percentile_mask
+
+
+@dataclass
+class PhaseConfig:
+    """prune block of the config (urban3d_admm.yaml / mill19: prune.prune_percent, prune.v_pow)."""
+    prune_percent: float = 0.5
+    v_pow: float = 0.1
+    merge_prune_factor: float = 0.4    # prune_gaussians_after_merge: 0.4 * prune_percent (:119)
+
+
+class PhaseKernels:
+    """The phase entry's device operations (HIP)."""
+
+    def importance(self, model: GaussianSplatModel, cameras: list, bg: torch.Tensor) -> torch.Tensor:
+        """prune_list's important_score summed over `cameras` (last camera first), float32 [N]."""
+        from .prune import prune_list
+        n = model.num_gaussians
+        if not cameras:
+            return torch.zeros(n, dtype=torch.float32, device=model.get_xyz.device)
+        return prune_list(model, cameras, None, bg)[1]
+
+    def members(self, xy: torch.Tensor, boxes: list, transform) -> list:
+        """[ascending int64 indices of the points inside each closed box (in the OBB frame)]."""
+        from .blocksplit import points_in_boxes2d
+        out = []
+        for i in range(0, len(boxes), 64):
+            out += points_in_boxes2d(xy, [np.asarray(b, dtype=np.float64).reshape(2, 3)[:, :2]
+                                          for b in boxes[i:i + 64]], transform, device=xy.device)["members"]
+        return out
+
+    def prune(self, model: GaussianSplatModel, mask: torch.Tensor) -> None:
+        model.prune_points(mask, None)
+
+
+def _flat(model: GaussianSplatModel) -> torch.Tensor:
+    """[N, 59] rows (xyz, f_dc, f_rest, scaling, quaternion, opacity: get_all_properties order)."""
+    ts = model.get_all_properties()
+    n = ts[0].shape[0]
+    return torch.cat([t.detach().reshape(n, -1).float() for t in ts], dim=1).contiguous()
+
+
+def _split_rows(rows: torch.Tensor, like: GaussianSplatModel) -> tuple:
+    shapes = [tuple(t.shape[1:]) for t in like.get_all_properties()]
+    out, o = [], 0
+    n = rows.shape[0]
+    for s in shapes:
+        w = int(np.prod(s)) if s else 1
+        out.append(rows[:, o:o + w].reshape((n,) + s).contiguous())
+        o += w
+    return tuple(out)
+
+
+def _gather_device(group) -> torch.device | None:
+    """gloo's all_gather takes host tensors; RCCL device tensors."""
+    return torch.device("cpu") if dist.get_backend(group) == "gloo" else None
+
+
+def all_gather_rows(rows: torch.Tensor, group=None) -> list:
+    """Every rank's [n_r, D] rows (n_r may differ), in rank order: one all_gather of the sizes, one of the padded
+    rows."""
+    world = dist.get_world_size(group)
+    host = _gather_device(group)
+    dev = rows.device
+    src = rows.to(host) if host is not None else rows
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=src.device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    sizes = [int(x.item()) for x in ns]
+    nmax = max(sizes) if sizes else 0
+    pad = torch.zeros((nmax, rows.shape[1]), dtype=rows.dtype, device=src.device)
+    pad[:rows.shape[0]] = src
+    outs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad, group=group)
+    return [o[:s].to(dev) for o, s in zip(outs, sizes)]
+
+
+def fuse_blocks(block_models: list, ori_point_bboxes, world_to_obb_transform, kernels: PhaseKernels):
+    """fuse_block_gaussians (master_gaussian_trainer.py:37-100) without its PLY side outputs: each block clipped to
+    its original box (OBB frame), concatenated in block order.  Returns the fused (non-optimisable) model."""
+    parts = []
+    for b, m in enumerate(block_models):
+        rows = _flat(m)
+        if ori_point_bboxes is not None:
+            keep = kernels.members(m.get_xyz.detach()[:, :2], [ori_point_bboxes[b]], world_to_obb_transform)[0]
+            rows = rows[keep.to(rows.device)]
+        parts.append(rows)
+    like = block_models[0]
+    fused = GaussianSplatModel(like.max_sh_degree, like.percent_dense, like.get_xyz.device)
+    fused.init_from_external_properties(*_split_rows(torch.cat(parts, 0), like), optimizable=False)
+    fused.active_sh_degree = like.active_sh_degree
+    return fused
+
+
+def v_imp_prune(model: GaussianSplatModel, imp: torch.Tensor, cfg: PhaseConfig, kernels: PhaseKernels) -> None:
+    """calculate_v_imp_score + prune_gaussians(0.4 * prune_percent) (master :117-119, prune.py:14-32,
+    gaussian_splat_model.py:420-432)."""
+    from .prune import calculate_v_imp_score
+    v = calculate_v_imp_score(model, imp, cfg.v_pow)
+    kernels.prune(model, percentile_mask(v, cfg.merge_prune_factor * cfg.prune_percent))
+
+
+def select_gaussians_in_each_block(bboxes: list, model: GaussianSplatModel, world_to_obb_transform,
+                                   kernels: PhaseKernels, blocks=None):
+    """master_gaussian_trainer.py:124-172: drop the Gaussians inside no expanded box, then (visibility_count [N],
+    global_indices [per block, ascending int64], sub-models of `blocks` (default: every block))."""
+    xy = model.get_xyz.detach()[:, :2]
+    mem = kernels.members(xy, bboxes, world_to_obb_transform)
+    n = model.num_gaussians
+    cnt = torch.zeros(n, dtype=torch.int64, device=xy.device)
+    for m in mem:
+        cnt.index_add_(0, m.to(xy.device), torch.ones_like(m, device=xy.device))
+    valid = torch.nonzero(cnt).squeeze(-1)
+    if valid.numel() != n:
+        model.extract_sub_gaussians(valid)
+        xy = model.get_xyz.detach()[:, :2]
+        mem = kernels.members(xy, bboxes, world_to_obb_transform)
+    n = model.num_gaussians
+    vis = torch.zeros(n, dtype=torch.int64, device=xy.device)
+    for m in mem:
+        vis.index_add_(0, m.to(xy.device), torch.ones_like(m, device=xy.device))
+    assert bool((vis != 0).all()), "visibility count has zero elements!"
+    want = range(len(bboxes)) if blocks is None else blocks
+    subs = {b: model.get_sub_gaussians(mem[b]) for b in want}
+    return vis, [m.to(torch.int64) for m in mem], subs
+
+
+@dataclass
+class PhaseEntry:
+    """What a rank needs to start the ADMM phase: its block's optimisable sub-model, its global indices, the
+    visibility count of the global set, the global count and the penalty denominator (the pruned count)."""
+    model: GaussianSplatModel
+    global_indices: torch.Tensor
+    visibility_count: torch.Tensor
+    num_global: int
+    rho_gaussians: int
+    fused: GaussianSplatModel
+
+    def raw(self) -> dict:
+        """The sub-model as BlockTrainer's raw dict (dogs_amd.admm.PARAM_NAMES)."""
+        m = self.model
+        return dict(zip(PARAM_NAMES, (m._xyz, m._features_dc, m._features_rest, m._scaling, m._quaternion,
+                                      m._opacity)))
+
+
+def enter_admm_phase(block_model: GaussianSplatModel, camera_blocks: list, ori_point_bboxes: list,
+                     exp_point_bboxes: list, world_to_obb_transform=None, cfg: PhaseConfig | None = None,
+                     kernels: PhaseKernels | None = None, group=None, bg: torch.Tensor | None = None) -> PhaseEntry:
+    """This rank's part of fuse_local_gaussians (master_gaussian_trainer.py:557-618) over the process group: rank r
+    holds block r's model (trained up to densify_end_iter) and camera_blocks[b] lists block b's cameras (every rank
+    knows the split, as every reference worker reads the block folders)."""
+    cfg = cfg or PhaseConfig()
+    kernels = kernels or PhaseKernels()
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    if len(camera_blocks) != world:
+        raise RuntimeError(f"{len(camera_blocks)} camera blocks for {world} ranks (one block per rank)")
+    dev = block_model.get_xyz.device
+    bg = torch.zeros(3, dtype=torch.float32, device=dev) if bg is None else bg
+    # 1. every block's model on every rank, fused identically
+    rows = all_gather_rows(_flat(block_model), group)
+    blocks = []
+    for r in rows:
+        m = GaussianSplatModel(block_model.max_sh_degree, block_model.percent_dense, dev)
+        m.init_from_external_properties(*_split_rows(r, block_model))
+        m.active_sh_degree = block_model.active_sh_degree
+        blocks.append(m)
+    fused = fuse_blocks(blocks, ori_point_bboxes, world_to_obb_transform, kernels)
+    del blocks, rows
+    # 2. importance: this rank's cameras only, then the per-block partial sums added in block order
+    part = kernels.importance(fused, camera_blocks[rank], bg).float().reshape(-1, 1)
+    parts = all_gather_rows(part, group)
+    imp = parts[0].reshape(-1).clone()
+    for p in parts[1:]:
+        imp += p.reshape(-1)
+    v_imp_prune(fused, imp, cfg, kernels)
+    rho_gaussians = fused.num_gaussians
+    # 4. the expanded-box split
+    vis, gidx, subs = select_gaussians_in_each_block(exp_point_bboxes, fused, world_to_obb_transform, kernels,
+                                                     blocks=[rank])
+    return PhaseEntry(subs[rank], gidx[rank], vis, int(vis.shape[0]), rho_gaussians, fused)
+
+
+def enter_admm_phase_sequential(block_models: list, camera_blocks: list, ori_point_bboxes: list,
+                                exp_point_bboxes: list, world_to_obb_transform=None, cfg: PhaseConfig | None = None,
+                                kernels: PhaseKernels | None = None, bg: torch.Tensor | None = None) -> list:
+    """The same entry for every block in one process (the single-GPU baseline, and the restatement the distributed
+    entry is tested against): [PhaseEntry per block]."""
+    cfg = cfg or PhaseConfig()
+    kernels = kernels or PhaseKernels()
+    dev = block_models[0].get_xyz.device
+    bg = torch.zeros(3, dtype=torch.float32, device=dev) if bg is None else bg
+    fused = fuse_blocks(block_models, ori_point_bboxes, world_to_obb_transform, kernels)
+    imp = None
+    for cams in camera_blocks:
+        p = kernels.importance(fused, cams, bg).float().reshape(-1)
+        imp = p.clone() if imp is None else imp + p
+    v_imp_prune(fused, imp, cfg, kernels)
+    rho_gaussians = fused.num_gaussians
+    vis, gidx, subs = select_gaussians_in_each_block(exp_point_bboxes, fused, world_to_obb_transform, kernels)
+    return [PhaseEntry(subs[b], gidx[b], vis, int(vis.shape[0]), rho_gaussians, fused)
+            for b in range(len(exp_point_bboxes))]

@@ -90,11 +90,13 @@ class ExponentialLR:
 class ADMMBlockState:
     """One block's ADMM variables: z (the global values of its rows), u (duals), rho, the previous z."""
 
-    def __init__(self, params: tuple, num_global: int, cfg: ADMMConfig):
+    def __init__(self, params: tuple, num_global: int, cfg: ADMMConfig, rho_gaussians: int | None = None):
+        """rho_gaussians: the denominator of the initial penalties (setup_penalty_parameters, master :326-335: the
+        pruned global count before the expanded-box selection); default num_global."""
         self.z = tuple(p.detach().clone() for p in params)
         self.z_prev = self.z
         self.u = tuple(torch.zeros_like(p) for p in params)
-        self.rho = initial_rho(cfg, num_global)
+        self.rho = initial_rho(cfg, rho_gaussians or num_global)
         self.cfg = cfg
 
     def prox(self, params: tuple) -> dict:
@@ -128,7 +130,7 @@ class BlockTrainer:
 
     def __init__(self, raw: dict, cameras: list, images: list, num_global: int, admm: ADMMConfig,
                  cfg: TrainConfig | None = None, device: torch.device | None = None, seed: int = 0,
-                 native: bool = True):
+                 native: bool = True, rho_gaussians: int | None = None):
         from .diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer, SparseGaussianAdam
         from .activations import activate
         from .fused_ssim import fused_ssim
@@ -153,7 +155,7 @@ class BlockTrainer:
         self.rng = np.random.default_rng(seed)
         self.order: list[int] = []
         self.iteration = c.start_iteration
-        self.admm = ADMMBlockState(self.param_tuple(), num_global, admm)
+        self.admm = ADMMBlockState(self.param_tuple(), num_global, admm, rho_gaussians)
         self._last_loss = None
         self.cameras = cameras
         self.native = native

@@ -219,24 +219,27 @@ struct HostCounters {
     uint32_t* buf = nullptr;
     hipEvent_t ev = nullptr;
 };
-std::mutex g_hc_mu;
-std::vector<HostCounters> g_hc_pool;
+// The pool and its mutex are allocated once and never freed: a thread that exits during interpreter teardown (after
+// the static destructors ran) still finds them alive.
+std::mutex& hc_mu() { static auto* m = new std::mutex; return *m; }
+std::vector<HostCounters>& hc_pool() { static auto* v = new std::vector<HostCounters>; return *v; }
 struct HostCountersSlot {
     HostCounters h;
     ~HostCountersSlot() {
         if (!h.buf) return;
-        std::lock_guard<std::mutex> lk(g_hc_mu);
-        g_hc_pool.push_back(h);
+        std::lock_guard<std::mutex> lk(hc_mu());
+        hc_pool().push_back(h);
     }
 };
 HostCounters& host_counters() {
     thread_local HostCountersSlot slot;
     if (!slot.h.buf) {
         {
-            std::lock_guard<std::mutex> lk(g_hc_mu);
-            if (!g_hc_pool.empty()) {
-                slot.h = g_hc_pool.back();
-                g_hc_pool.pop_back();
+            std::lock_guard<std::mutex> lk(hc_mu());
+            auto& pool = hc_pool();
+            if (!pool.empty()) {
+                slot.h = pool.back();
+                pool.pop_back();
             }
         }
         if (!slot.h.buf) {
@@ -269,46 +272,56 @@ int64_t clamp_cap(int64_t per, int T) {
 // extra copy, event or wait.  Grow-only: a capacity that was once needed stays, and a too-deep prefix costs only
 // proportionally more phase-1 work.  The capacity a view used travels to its backward as the num_instances token, so
 // later growth never desynchronises a forward/backward pair.
-// One state per (device, image size) for the whole process (not per thread), so the device probe is allocated once
-// per image size and shared by every thread that renders it.  Concurrent renders of one size may only lose or double a
-// growth signal (the capacity a view used always travels with that view), never affect results.
+// The capacity is one state per (device, image size) for the whole process (not per thread), so every thread and
+// stream rendering that size shares the growth.  The device probe and the phase-1 count it is judged against are per
+// (device, size, stream): a probe is written by one stream's phase 2 and read by that stream's next depth cut, so
+// concurrent renders on different streams never read each other's probe (stream order is what makes the pair valid).
 struct AdaptiveCap {
     int per_tile = DEFAULT_PREFIX_PER_TILE;
+};
+struct CapProbe {
+    AdaptiveCap* shared = nullptr;
     uint32_t* probe = nullptr;  // device: [0] unfinished tiles, [1] phase-2 instances of the last phase-2 launch
-    uint32_t last_e1 = 0;       // phase-1 instances of the last forward at this size
+    uint32_t last_e1 = 0;       // phase-1 instances of the last forward at this size on this stream
 };
 std::mutex g_cap_mu;
-AdaptiveCap* adaptive_cap(const dg_raster_args* a) {
+using CapKey = std::tuple<int, int, int>;
+std::map<CapKey, AdaptiveCap>& cap_states() { static auto* m = new std::map<CapKey, AdaptiveCap>; return *m; }
+std::map<std::tuple<int, int, int, hipStream_t>, CapProbe>& cap_probes() {
+    static auto* m = new std::map<std::tuple<int, int, int, hipStream_t>, CapProbe>;  // node-based: entries never move
+    return *m;
+}
+CapProbe* adaptive_cap(const dg_raster_args* a, hipStream_t s) {
     if (a->prefix_per_tile != 0) return nullptr;
     int dev = 0;
     (void)hipGetDevice(&dev);
-    static std::map<std::tuple<int, int, int>, AdaptiveCap> caps;  // node-based: entries never move
     std::lock_guard<std::mutex> lk(g_cap_mu);
-    AdaptiveCap& c = caps[std::make_tuple(dev, a->W, a->H)];
+    CapProbe& c = cap_probes()[std::make_tuple(dev, a->W, a->H, s)];
     if (!c.probe) {
+        c.shared = &cap_states()[std::make_tuple(dev, a->W, a->H)];
         if (hipMalloc((void**)&c.probe, 2 * sizeof(uint32_t)) != hipSuccess) { c.probe = nullptr; return nullptr; }
         (void)hipMemset(c.probe, 0, 2 * sizeof(uint32_t));
     }
     return &c;
 }
-int64_t phase1_cap(const dg_raster_args* a, int T, AdaptiveCap* ac) {
+int64_t phase1_cap(const dg_raster_args* a, int T, CapProbe* ac) {
     if (a->prefix_per_tile > 0) return clamp_cap(a->prefix_per_tile, T);
     if (!ac) return clamp_cap(DEFAULT_PREFIX_PER_TILE, T);
     std::lock_guard<std::mutex> lk(g_cap_mu);
-    return clamp_cap(ac->per_tile, T);
+    return clamp_cap(ac->shared->per_tile, T);
 }
 // Grow only when the last phase 2 did real work: more than an eighth of phase 1's instances.  Tiles that never
 // saturate (sparse regions, the scene's edge seen from a turned camera) stay unfinished at any prefix short of the
 // whole list, and phase 2 serves them with a few instances each; growing for them would bin everything
 // (measured on the 8-view yaw batch at 1e6: 448 -> 3402 per tile, 1190 -> 843 views/s).
-void adapt(AdaptiveCap* ac, uint32_t prev_unfinished, uint32_t prev_k2, uint32_t e1) {
+void adapt(CapProbe* ac, uint32_t prev_unfinished, uint32_t prev_k2, uint32_t e1) {
     if (!ac) return;
     std::lock_guard<std::mutex> lk(g_cap_mu);
     const uint32_t prev_e1 = ac->last_e1;
     ac->last_e1 = e1;
     if (prev_unfinished == 0u || (uint64_t)prev_k2 * 8u <= (uint64_t)prev_e1) return;
-    if (ac->per_tile < MAX_PREFIX_PER_TILE)
-        ac->per_tile = ac->per_tile * 3 / 2 < MAX_PREFIX_PER_TILE ? ac->per_tile * 3 / 2 : MAX_PREFIX_PER_TILE;
+    int& pt = ac->shared->per_tile;
+    if (pt < MAX_PREFIX_PER_TILE) pt = pt * 3 / 2 < MAX_PREFIX_PER_TILE ? pt * 3 / 2 : MAX_PREFIX_PER_TILE;
 }
 
 struct BwdScratch {
@@ -429,18 +442,19 @@ int dg_exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_
 int dg_version(void) { return 1; }
 
 int dg_adaptive_capacity(int W, int H, int reset, int* per_tile_out) {
-    dg_raster_args a;
-    memset(&a, 0, sizeof(a));
-    a.W = W; a.H = H; a.prefix_per_tile = 0;
-    AdaptiveCap* ac = adaptive_cap(&a);
-    if (!ac) return fail("adaptive capacity probe allocation failed%s%d");
+    int dev = 0;
+    HIP_OK(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(g_cap_mu);
+    AdaptiveCap& c = cap_states()[std::make_tuple(dev, W, H)];
     if (reset) {
-        ac->per_tile = DEFAULT_PREFIX_PER_TILE;
-        ac->last_e1 = 0;
-        HIP_OK(hipMemset(ac->probe, 0, 2 * sizeof(uint32_t)));
+        c.per_tile = DEFAULT_PREFIX_PER_TILE;
+        for (auto& kv : cap_probes()) {
+            if (std::get<0>(kv.first) != dev || std::get<1>(kv.first) != W || std::get<2>(kv.first) != H) continue;
+            kv.second.last_e1 = 0;
+            if (kv.second.probe) HIP_OK(hipMemset(kv.second.probe, 0, 2 * sizeof(uint32_t)));
+        }
     }
-    if (per_tile_out) *per_tile_out = ac->per_tile;
+    if (per_tile_out) *per_tile_out = c.per_tile;
     return 0;
 }
 
@@ -464,7 +478,7 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     *binning_out = nullptr;
     *binning2_out = nullptr;
 
-    AdaptiveCap* const ac = adaptive_cap(a);
+    CapProbe* const ac = adaptive_cap(a, s);
     const size_t gbytes = carve_geom(nullptr, P).bytes;
     void* gbase = alloc(user, DG_BUF_GEOM, gbytes);
     if (!gbase) return fail("geometry allocation failed%s%d");
@@ -980,7 +994,7 @@ KeepState carve_keep(void* base, uint64_t C) {
     k.bytes = c.off;
     return k;
 }
-int densify_check(const dg_densify_args* a) {
+int densify_check(const dg_densify_args* a, bool need_stats = true) {
     if (!a) return fail("null densify args%s%d");
     const dg_gaussian_set& g = a->set;
     for (int q = 0; q < 6; q++) {
@@ -990,7 +1004,7 @@ int densify_check(const dg_densify_args* a) {
     }
     if (g.width[0] != 3 || g.width[4] != 3 || g.width[5] != 4 || g.width[3] != 1)
         return fail("widths must be xyz 3, opacity 1, scaling 3, quaternion 4%s%d");
-    if (g.N && (!g.grad_accum || !g.denom)) return fail("grad_accum and denom required%s%d");
+    if (need_stats && g.N && (!g.grad_accum || !g.denom)) return fail("grad_accum and denom required%s%d");
     return 0;
 }
 gs::DensifyArgs densify_args(const dg_densify_args* a, const DensifyState& st) {
@@ -1096,7 +1110,7 @@ int dg_densify_count(dg_densify_args* a, dg_alloc_fn alloc, void* user, dg_strea
 }
 
 int dg_densify_gather(const dg_densify_args* a, dg_stream_t stream) {
-    if (densify_check(a)) return 1;
+    if (densify_check(a, false)) return 1;
     if (!a->state || !a->state2) return fail("dg_densify_select and dg_densify_count first%s%d");
     for (int q = 0; q < 6; q++) {
         if (a->n_out && !a->out_params[q]) return fail("output tensor %s%d is NULL", "", q);
@@ -1110,6 +1124,76 @@ int dg_densify_gather(const dg_densify_args* a, dg_stream_t stream) {
     KeepState ks = carve_keep(a->state2, C);
     gs::RebuildArgs rb = rebuild_args(a, st, ks);
     gs::launch_densify_gather(rb, ks.keep_pos, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+namespace {
+__global__ void __launch_bounds__(256) k_keep_from_mask(const uint8_t* __restrict__ prune, uint32_t N,
+                                                        uint32_t* __restrict__ keep) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < N) keep[i] = prune[i] ? 0u : 1u;
+}
+__global__ void __launch_bounds__(256) k_gather_stats(const uint32_t* __restrict__ keep,
+                                                      const uint32_t* __restrict__ keep_pos, uint32_t N,
+                                                      const float* __restrict__ ga, const float* __restrict__ dn,
+                                                      const float* __restrict__ mr, float* __restrict__ oga,
+                                                      float* __restrict__ odn, float* __restrict__ omr) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= N || !keep[i]) return;
+    const uint32_t o = keep_pos[i];
+    if (oga) oga[o] = ga[i];
+    if (odn) odn[o] = dn[i];
+    if (omr) omr[o] = mr[i];
+}
+}  // namespace
+
+int dg_prune_select(dg_densify_args* a, const uint8_t* prune_mask, dg_alloc_fn alloc, void* user,
+                    dg_stream_t stream) {
+    if (!a) return fail("null densify args%s%d");
+    const dg_gaussian_set& g = a->set;
+    for (int q = 0; q < 6; q++) {
+        if (g.N && !g.params[q]) return fail("parameter tensor %s%d is NULL", "", q);
+        if ((g.exp_avg[q] == nullptr) != (g.exp_avg_sq[q] == nullptr))
+            return fail("exp_avg / exp_avg_sq of tensor %s%d: both or neither", "", q);
+    }
+    if (g.width[0] != 3 || g.width[4] != 3 || g.width[5] != 4 || g.width[3] != 1)
+        return fail("widths must be xyz 3, opacity 1, scaling 3, quaternion 4%s%d");
+    if (g.N && !prune_mask) return fail("prune mask required%s%d");
+    uint64_t wsum = 0;
+    for (int q = 0; q < 6; q++) wsum += g.width[q];
+    if ((uint64_t)g.N * wsum >= 0xfffff000ull) return fail("too many rows x floats%s%d");
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t N = g.N;
+    a->nc = a->ns = a->n_out = 0;
+    a->samples = nullptr;
+    a->state = alloc(user, DG_BUF_DENSIFY, carve_densify(nullptr, N).bytes);
+    a->state2 = alloc(user, DG_BUF_DENSIFY2, carve_keep(nullptr, N).bytes);
+    if (!a->state || !a->state2) return fail("prune state allocation failed%s%d");
+    if (N == 0) return 0;
+    KeepState ks = carve_keep(a->state2, N);
+    k_keep_from_mask<<<(N + 255) / 256, 256, 0, s>>>(prune_mask, N, ks.keep);
+    gs::exclusive_scan(ks.keep, N, ks.keep_pos, ks.total, ks.scan_tmp, s);
+    uint32_t h = 0;
+    HIP_OK(hipMemcpyAsync(&h, ks.total, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    a->n_out = h;
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_prune_gather_stats(const dg_densify_args* a, const float* max_radii2D, float* out_grad_accum,
+                          float* out_denom, float* out_max_radii2D, dg_stream_t stream) {
+    if (!a || !a->state2) return fail("dg_prune_select first%s%d");
+    if (a->nc || a->ns) return fail("statistics are gathered for a pure prune only%s%d");
+    const uint32_t N = a->set.N;
+    if (N == 0 || a->n_out == 0) return 0;
+    if ((out_grad_accum && !a->set.grad_accum) || (out_denom && !a->set.denom) || (out_max_radii2D && !max_radii2D))
+        return fail("a statistics source is NULL%s%d");
+    KeepState ks = carve_keep(a->state2, N);
+    k_gather_stats<<<(N + 255) / 256, 256, 0, (hipStream_t)stream>>>(ks.keep, ks.keep_pos, N, a->set.grad_accum,
+                                                                    a->set.denom, max_radii2D, out_grad_accum,
+                                                                    out_denom, out_max_radii2D);
     HIP_OK(hipGetLastError());
     return 0;
 }

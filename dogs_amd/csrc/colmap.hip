@@ -135,7 +135,7 @@ int dg_colmap_images(const char* path, uint64_t* n_out, uint64_t* name_bytes, ui
         nb += len;
         c.skip(len + 1);
         const uint64_t k2 = c.get<uint64_t>();
-        if (c.bad || c.off + 24 * k2 > m.n) return 2;
+        if (c.bad || c.off > m.n || k2 > (m.n - c.off) / 24) return 2;   // no wrap-around on a hostile count
         for (uint64_t j = 0; j < k2; j++) {
             double x, y;
             int64_t pid;
@@ -167,7 +167,7 @@ int dg_colmap_points3d(const char* path, int min_track_length, uint64_t* n_out, 
         uint64_t tl;
         memcpy(&tl, r + 43, 8);
         c.off += REC;
-        if (c.off + 8 * tl > m.n) return 2;
+        if (c.off > m.n || tl > (m.n - c.off) / 8) return 2;
         if ((int64_t)tl >= (int64_t)min_track_length) {
             if (fill) {
                 memcpy(ids + kept, r, 8);

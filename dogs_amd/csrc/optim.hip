@@ -47,11 +47,18 @@ constexpr int ADAM_CHUNKS = DG_ADAM_CHUNKS;  // float4 chunks per lane
 // by k_activate_bwd and the activation-folded Adam so both routes evaluate the same expressions.
 __device__ __forceinline__ float sigmoid_bwd(float g, float v) { return g * (v * (1.0f - v)); }
 // exp's backward of scaling column r, with the scale regulariser lambda_scale mean(prod(scaling, 1))
-// (gaussian_trainer.py:407-408): its gradient reg prod / s_r joins the rasterizer's before exp's backward
+// (gaussian_trainer.py:407-408): its gradient reg prod / s_r joins the rasterizer's before exp's backward.  torch's
+// prod backward is result / input when the input holds no zero and the product of the other columns otherwise
+// (prod_safe_zeros_backward); the same here per row, so an underflowed scale (exp of a raw value below ~-87) gives a
+// finite gradient instead of 0/0.
 __device__ __forceinline__ float exp_bwd(float g, const float* __restrict__ s3, int r, float reg) {
     if (reg != 0.0f) {
-        const float prod = (s3[0] * s3[1]) * s3[2];
-        return (g + reg * (prod / s3[r])) * s3[r];
+        float d;
+        if (s3[0] == 0.0f || s3[1] == 0.0f || s3[2] == 0.0f)
+            d = r == 0 ? s3[2] * s3[1] : r == 1 ? s3[0] * s3[2] : s3[0] * s3[1];
+        else
+            d = ((s3[0] * s3[1]) * s3[2]) / s3[r];
+        return (g + reg * d) * s3[r];
     }
     return g * s3[r];
 }

@@ -31,44 +31,65 @@ class NativeTrainStep:
                  lambda_scale: float, bg: torch.Tensor, device: torch.device, stats: dict | None = None):
         self.L = _lib.load()
         self.device = device
-        self.params = params
         self.arena = _lib.ReuseArena(device)
+        self.lambdas = (float(lambda_dssim), float(lambda_scale))
+        self.sh_degree = int(sh_degree)
+        self.loss_buf = torch.zeros(3, dtype=torch.float32, device=device)
+        self.bg = bg.to(device=device, dtype=torch.float32).contiguous()
+        self.cameras, self.gt_images = cameras, images
+        for cam, gt in zip(cameras, images):
+            for t in (cam.world_to_camera, cam.projective_matrix, cam.camera_center, gt):
+                if not (t.is_contiguous() and t.dtype == torch.float32 and t.device == device):
+                    raise RuntimeError("native step: cameras and targets must be contiguous float32 on the device")
+        self.images_out = {}
+        self.opt = opt
+        self.stream = _lib.stream_of(device)
+        self.last_view = None
+        self.rebind(params, stats)
+
+    def rebind(self, params: dict | None = None, stats: dict | None = None) -> None:
+        """(Re)build the argument blocks from the current tensors: after densify_and_prune, reset_opacity, a prune or
+        optimizer.load_state_dict replaced the parameters or their Adam moments.  params: {C_ORDER name: tensor}
+        (None: the optimizer's current group tensors); stats: the densification statistics (None: none)."""
+        opt, device = self.opt, self.device
+        groups = {g["name"]: g for g in opt.param_groups}
+        if params is None:
+            params = {n: groups[GROUP_NAME[n]]["params"][0] for n in C_ORDER}
         P = int(params["xyz"].shape[0])
         rest = params["features_rest"]
         M = int(rest.shape[1]) if rest.dim() == 3 else 0
-        self.lambdas = (float(lambda_dssim), float(lambda_scale))
+        self.params = params
         self.radii = torch.zeros(P, dtype=torch.int32, device=device)
-        self.loss_buf = torch.zeros(3, dtype=torch.float32, device=device)
-        self.bg = bg.to(device=device, dtype=torch.float32).contiguous()
-        self.images_out = {}
-        self.keep = [self.bg, cameras, images]
         for n in C_ORDER:
             p = params[n]
             if not (p.is_contiguous() and p.dtype == torch.float32 and p.device == device):
                 raise RuntimeError(f"native step: {n} must be a contiguous float32 tensor on {device}")
+            if int(p.shape[0]) != P:
+                raise RuntimeError(f"native step: {n} has {int(p.shape[0])} rows, xyz {P}")
+            if groups[GROUP_NAME[n]]["params"][0] is not p:
+                raise RuntimeError(f"native step: {n} is not the tensor the optimizer's '{GROUP_NAME[n]}' group holds")
             st = opt.state[p]
             if len(st) == 0:
                 st["step"] = torch.tensor(0.0, dtype=torch.float32)
                 st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-        groups = {g["name"]: g for g in opt.param_groups}
         self.stats = None
+        self.keep = [self.bg, self.cameras, self.gt_images]
         if stats is not None:
             for k in ("max_radii2D", "grad_accum", "denom"):
                 t = stats[k]
-                if not (t.is_contiguous() and t.dtype == torch.float32 and t.device == device):
-                    raise RuntimeError(f"native step: {k} must be a contiguous float32 tensor on {device}")
+                if not (t.is_contiguous() and t.dtype == torch.float32 and t.device == device and t.numel() == P):
+                    raise RuntimeError(f"native step: {k} must be a contiguous float32 tensor of {P} on {device}")
             self.stats = _lib.DgDensifyStats(None, None, 3, stats["max_radii2D"].data_ptr(),
                                              stats["grad_accum"].data_ptr(), stats["denom"].data_ptr())
             self.keep.append(stats)
+        # what the argument blocks point at: checked by every step (a replaced tensor would be a use-after-free)
+        self._bound = self._pointers()
         self.args = []
-        for cam, gt in zip(cameras, images):
-            for t in (cam.world_to_camera, cam.projective_matrix, cam.camera_center, gt):
-                if not (t.is_contiguous() and t.dtype == torch.float32 and t.device == device):
-                    raise RuntimeError("native step: cameras and targets must be contiguous float32 on the device")
+        for cam, gt in zip(self.cameras, self.gt_images):
             a = _lib.DgTrainStepArgs()
             v = a.view
-            v.P, v.D, v.M, v.W, v.H = P, int(sh_degree), M, int(cam.width), int(cam.height)
+            v.P, v.D, v.M, v.W, v.H = P, self.sh_degree, M, int(cam.width), int(cam.height)
             v.prefiltered, v.antialiasing, v.debug = 0, 0, 0
             v.scale_modifier, v.tanfovx, v.tanfovy = 1.0, float(cam.tanfovx), float(cam.tanfovy)
             v.bg, v.viewmatrix = self.bg.data_ptr(), cam.world_to_camera.data_ptr()
@@ -81,23 +102,45 @@ class NativeTrainStep:
                 g = groups[GROUP_NAME[n]]
                 a.groups[i] = _lib.DgAdamGroup(p.data_ptr(), None, st["exp_avg"].data_ptr(),
                                                st["exp_avg_sq"].data_ptr(), float(g["lr"]), float(g["eps"]),
-                                               int(p.numel() // P))
+                                               int(p.numel() // P) if P else 1)
             key = (int(cam.height), int(cam.width))
             if key not in self.images_out:
                 self.images_out[key] = torch.empty((3, key[0], key[1]), dtype=torch.float32, device=device)
             a.radii, a.image, a.loss = self.radii.data_ptr(), self.images_out[key].data_ptr(), self.loss_buf.data_ptr()
             a.stats = C.addressof(self.stats) if self.stats is not None else None
             self.args.append(a)
-        self.stream = _lib.stream_of(device)
-        self.last_view = None
 
-    def step(self, k: int, xyz_lr: float | None = None, prox: dict | None = None) -> None:
-        """One iteration on view k; prox: {group name: (u, z, coef)} (ADMMBlockState.prox) or None."""
+    def _pointers(self) -> tuple:
+        """(param, exp_avg, exp_avg_sq) data pointers of the optimizer's current group tensors, C_ORDER."""
+        groups = {g["name"]: g for g in self.opt.param_groups}
+        out = []
+        for n in C_ORDER:
+            p = groups[GROUP_NAME[n]]["params"][0]
+            st = self.opt.state.get(p, {})
+            m, v = st.get("exp_avg"), st.get("exp_avg_sq")
+            out.append((p.data_ptr(), m.data_ptr() if m is not None else 0, v.data_ptr() if v is not None else 0,
+                        int(p.shape[0])))
+        return tuple(out)
+
+    def step(self, k: int, xyz_lr: float | None = None, prox: dict | None = None, sh_degree: int | None = None,
+             lrs: dict | None = None) -> None:
+        """One iteration on view k; prox: {group name: (u, z, coef)} (ADMMBlockState.prox) or None; sh_degree: the
+        model's active SH degree (increase_SH_degree), default the constructor's; lrs: {group name: lr} overrides.
+        Raises when the optimizer's tensors are no longer the ones the argument blocks point at (call rebind())."""
         from .diff_gaussian_rasterization import _C
+        if self._pointers() != self._bound:
+            raise RuntimeError("native step: the parameters or their Adam moments were replaced (densify, prune, "
+                               "reset_opacity, load_state_dict); call rebind() first")
         a = self.args[k]
         a.view.prefix_per_tile = int(_C.PREFIX_PER_TILE)
+        if sh_degree is not None:
+            a.view.D = int(sh_degree)
         if xyz_lr is not None:
             a.groups[0].lr = float(xyz_lr)
+        if lrs:
+            for i, n in enumerate(C_ORDER):
+                if GROUP_NAME[n] in lrs:
+                    a.groups[i].lr = float(lrs[GROUP_NAME[n]])
         for i, n in enumerate(C_ORDER):
             if prox is None:
                 a.prox[i].u = a.prox[i].z = None

@@ -242,6 +242,17 @@ int dg_densify_split_stds(const dg_densify_args* a, float* stds, dg_stream_t str
 int dg_densify_count(dg_densify_args* a, dg_alloc_fn alloc, void* user, dg_stream_t stream);
 int dg_densify_gather(const dg_densify_args* a, dg_stream_t stream);
 
+/* prune_points (gaussian_splat_model.py:396-410; prune_optimizer :86-108), used by prune_gaussians_with_opt (:412-418)
+ * and prune_gaussians (:420-432): drop the rows with prune_mask[i] != 0 from every tensor and its Adam moments (kept
+ * rows keep theirs), in row order.  dg_prune_select fills the keep list and n_out (one sync); then
+ * dg_densify_gather writes the out_* tensors (nc = ns = 0: every candidate is an original), and
+ * dg_prune_gather_stats the kept rows of xyz_gradient_accum / denom (set.grad_accum / set.denom) and max_radii2D
+ * (any output may be NULL).  set.grad_accum / denom may be NULL when not gathered. */
+int dg_prune_select(dg_densify_args* a, const uint8_t* prune_mask, dg_alloc_fn alloc, void* user,
+                    dg_stream_t stream);
+int dg_prune_gather_stats(const dg_densify_args* a, const float* max_radii2D, float* out_grad_accum,
+                          float* out_denom, float* out_max_radii2D, dg_stream_t stream);
+
 /* ---- export formats of the trained / fused Gaussians ---- */
 
 /* GaussianSplatModel.save_splat (gaussian_splat_model.py:666-708): out [N * 32] device bytes, the .splat records

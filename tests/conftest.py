@@ -12,6 +12,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
 
 
+# The hot-path parity files run first, so that `pytest -x` cannot hide the rasterizer's results behind an unrelated
+# early failure (the default order is alphabetical).
+FIRST = ("test_gpu_raster.py", "test_gpu_fullsize.py", "test_gpu_aux.py", "test_gpu_boundary.py")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    def rank(item):
+        name = os.path.basename(str(item.fspath))
+        return FIRST.index(name) if name in FIRST else len(FIRST)
+    items.sort(key=rank)   # stable: the order inside each file is kept
+
+
 @pytest.fixture(scope="session")
 def oracle():
     from oracle import oracle as O

@@ -89,6 +89,20 @@ def test_errors(tmp_path):
             p.write_bytes(raw[:cut])
             with pytest.raises(IOError):
                 reader(str(p))
+    # hostile lengths: a count whose byte size wraps around 2^64 must fail cleanly, not read past the mapping
+    raw = bytearray(open(os.path.join(GOLD, "images.bin"), "rb").read())
+    z = raw.index(0, 72)                                      # end of the first image's name
+    for huge in (2 ** 62, 2 ** 64 // 24 + 1, 2 ** 64 - 1):
+        raw[z + 1:z + 9] = np.array([huge], np.uint64).tobytes()
+        (tmp_path / "images.bin").write_bytes(bytes(raw))
+        with pytest.raises(IOError):
+            read_images_binary(str(tmp_path / "images.bin"))
+    raw = bytearray(open(os.path.join(GOLD, "points3D.bin"), "rb").read())
+    for huge in (2 ** 61, 2 ** 64 // 8 + 1, 2 ** 64 - 1):
+        raw[8 + 43:8 + 51] = np.array([huge], np.uint64).tobytes()
+        (tmp_path / "points3D.bin").write_bytes(bytes(raw))
+        with pytest.raises(IOError):
+            read_points3D_binary(str(tmp_path / "points3D.bin"))
     bad = tmp_path / "cameras.bin"
     bad.write_bytes(np.array([1], np.uint64).tobytes() + np.array([1, 6], np.int32).tobytes() + b"\0" * 16)
     from dogs_amd.colmap import read_cameras_binary
