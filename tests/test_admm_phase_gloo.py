@@ -1,0 +1,174 @@
+"""The ADMM phase entry (dogs_amd.admm_phase: fuse_local_gaussians without the RPC master,
+master_gaussian_trainer.py:37-172, 557-618) over torch.distributed (gloo, world size 2, CPU).
+
+The device operations (count renders, box membership, prune compaction) are replaced by CPU restatements
+(`CPUKernels`), so this checks the distributed plumbing and the lifecycle order:
+  * every rank's entry equals the single-process entry (enter_admm_phase_sequential) bit for bit -- the gathered and
+    fused model, the importance sums (per-block partials added in block order), the pruned set, the expanded-box
+    split, visibility_count and the penalty denominator;
+  * the single-process entry equals a plain restatement of the reference's own steps written here from its source
+    (clip to the original boxes, concatenate, prune_list, calculate_v_imp_score, prune_gaussians(0.4 p),
+    select_gaussians_in_each_block), with the importance summed with the same per-block association.
+The HIP versions of the three operations are checked on the GPU (tests/test_gpu_admm_phase.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N_BLOCK = (300, 260)
+T = np.array([[0.8, -0.6, 0.3], [0.6, 0.8, -0.2], [0.0, 0.0, 1.0]])   # world -> OBB (a rotation + shift)
+ORI = [np.array([-5.0, -5.0, -1.0, 0.0, 5.0, 1.0]), np.array([0.0, -5.0, -1.0, 5.0, 5.0, 1.0])]
+EXP = [np.array([-6.0, -6.0, -1.0, 1.0, 6.0, 1.0]), np.array([-1.0, -6.0, -1.0, 6.0, 6.0, 1.0])]
+
+
+def _cameras():
+    g = torch.Generator().manual_seed(3)
+    return [[torch.randn(3, generator=g) * 3.0 for _ in range(4)], [torch.randn(3, generator=g) * 3.0 for _ in range(3)]]
+
+
+def _block_model(b):
+    from dogs_amd.gaussian_model import GaussianSplatModel
+    g = torch.Generator().manual_seed(11 + b)
+    n = N_BLOCK[b]
+    m = GaussianSplatModel(3, 0.01, "cpu")
+    xyz = torch.randn(n, 3, generator=g) * 3.0
+    xyz[:, 0] += -2.0 if b == 0 else 2.0
+    m.init_from_external_properties(xyz, torch.randn(n, 1, 3, generator=g), torch.randn(n, 15, 3, generator=g) * 0.1,
+                                    torch.randn(n, 3, generator=g) - 3.0, torch.randn(n, 4, generator=g),
+                                    torch.randn(n, 1, generator=g), optimizable=True)
+    m.active_sh_degree = 3
+    return m
+
+
+def _cpu_kernels():
+    from dogs_amd.admm_phase import PhaseKernels
+    from oracle.blocksplit_oracle import points_in_bbox2D
+
+    class CPUKernels(PhaseKernels):
+        def importance(self, model, cameras, bg):
+            xyz = model.get_xyz.detach()
+            op = torch.sigmoid(model.get_raw_opacity.detach()).reshape(-1)
+            imp = torch.zeros(xyz.shape[0])
+            for c in reversed(list(cameras)):        # prune_list pops from the end
+                d = ((xyz - c) ** 2).sum(1)
+                cnt = (d < 40.0).to(torch.int32) * (1 + (d.to(torch.int32) % 7))   # integer pixel counts
+                imp += cnt.float() * op
+            return imp
+
+        def members(self, xy, boxes, transform):
+            return [torch.from_numpy(points_in_bbox2D(xy.numpy(), np.asarray(b).reshape(2, 3), transform))
+                    for b in boxes]
+
+        def prune(self, model, mask):
+            model.extract_sub_gaussians(torch.nonzero(~mask).squeeze(-1))
+    return CPUKernels()
+
+
+def _restated(cfg):
+    """The reference's steps, from its source text, on the same blocks and kernels."""
+    from oracle.blocksplit_oracle import points_in_bbox2D
+    K = _cpu_kernels()
+    models = [_block_model(b) for b in range(2)]
+    rows = []
+    for b, m in enumerate(models):              # fuse_block_gaussians :55-83
+        keep = torch.from_numpy(points_in_bbox2D(m.get_xyz.detach().numpy()[:, :2], ORI[b].reshape(2, 3), T))
+        rows.append([t.detach()[keep] for t in (m._xyz, m._features_dc, m._features_rest, m._scaling,
+                                                m._quaternion, m._opacity)])
+    fused = [torch.cat([r[i] for r in rows], 0) for i in range(6)]
+    from dogs_amd.gaussian_model import GaussianSplatModel
+    F = GaussianSplatModel(3, 0.01, "cpu")
+    F.init_from_external_properties(*fused)
+    F.active_sh_degree = 3
+    cams = _cameras()
+    imp = K.importance(F, cams[0], None) + K.importance(F, cams[1], None)   # per-block association
+    volume = torch.prod(torch.exp(F._scaling), dim=1)                       # calculate_v_imp_score
+    sv, _ = torch.sort(volume, descending=True)
+    v = torch.pow(volume / sv[int(len(volume) * 0.9)], cfg.v_pow) * imp
+    s, _ = torch.sort(v, dim=0)                                             # prune_gaussians
+    prune = (v <= s[int(0.4 * cfg.prune_percent * (s.shape[0] - 1))]).squeeze()
+    kept = [t[~prune] for t in fused]
+    n_rho = kept[0].shape[0]
+    gi = [torch.from_numpy(points_in_bbox2D(kept[0].numpy()[:, :2], e.reshape(2, 3), T)) for e in EXP]
+    cnt = torch.bincount(torch.cat(gi))                                     # select_gaussians_in_each_block
+    valid = torch.argwhere(cnt).squeeze(-1)
+    kept = [t[valid] for t in kept]
+    gi = [torch.from_numpy(points_in_bbox2D(kept[0].numpy()[:, :2], e.reshape(2, 3), T)) for e in EXP]
+    vis = torch.bincount(torch.cat(gi))
+    return kept, gi, vis, n_rho
+
+
+def _sequential(cfg):
+    from dogs_amd.admm_phase import enter_admm_phase_sequential
+    return enter_admm_phase_sequential([_block_model(b) for b in range(2)], _cameras(), ORI, EXP, T, cfg,
+                                       _cpu_kernels())
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dogs_amd.admm_phase import PhaseConfig, enter_admm_phase
+        cfg = PhaseConfig(prune_percent=0.5, v_pow=0.1)
+        e = enter_admm_phase(_block_model(rank), _cameras(), ORI, EXP, T, cfg, _cpu_kernels())
+        ref = _sequential(cfg)[rank]
+        assert torch.equal(e.global_indices, ref.global_indices)
+        assert torch.equal(e.visibility_count, ref.visibility_count)
+        assert (e.num_global, e.rho_gaussians) == (ref.num_global, ref.rho_gaussians)
+        for a, b in zip(e.model.get_all_properties(), ref.model.get_all_properties()):
+            assert torch.equal(a.detach(), b.detach())
+        for a, b in zip(e.fused.get_all_properties(), ref.fused.get_all_properties()):
+            assert torch.equal(a, b)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_phase_entry_gloo_matches_single_process():
+    mp.spawn(_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def test_single_process_entry_matches_reference_steps():
+    from dogs_amd.admm_phase import PhaseConfig
+    cfg = PhaseConfig(prune_percent=0.5, v_pow=0.1)
+    entries = _sequential(cfg)
+    kept, gi, vis, n_rho = _restated(cfg)
+    assert entries[0].rho_gaussians == n_rho
+    assert torch.equal(entries[0].visibility_count, vis)
+    assert 0 < n_rho < sum(N_BLOCK)
+    assert int((vis >= 2).sum()) > 0, "the expanded boxes must overlap"
+    for b in range(2):
+        assert torch.equal(entries[b].global_indices, gi[b])
+        for a, k in zip(entries[b].model.get_all_properties(), kept):
+            assert torch.equal(a.detach(), k[gi[b]])
+        assert isinstance(entries[b].model._xyz, torch.nn.Parameter)
+        assert entries[b].model.xyz_gradient_accum.shape == (len(gi[b]), 1)
+    # fused model = the clipped blocks, pruned
+    assert entries[0].fused.num_gaussians == kept[0].shape[0]
+
+
+def test_all_gather_rows_variable_sizes():
+    mp.spawn(_gather_worker, args=(3, _free_port()), nprocs=3, join=True)
+
+
+def _gather_worker(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dogs_amd.admm_phase import all_gather_rows
+        rows = torch.arange(rank * 5 * 4, dtype=torch.float32).reshape(rank * 5, 4) + 100 * rank
+        got = all_gather_rows(rows)
+        assert [g.shape[0] for g in got] == [0, 5, 10]
+        for r, g in enumerate(got):
+            assert torch.equal(g, torch.arange(r * 5 * 4, dtype=torch.float32).reshape(r * 5, 4) + 100 * r)
+    finally:
+        dist.destroy_process_group()

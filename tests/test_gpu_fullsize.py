@@ -29,6 +29,8 @@ WORKLOADS = [
     pytest.param(1_000_000, 1920, 1080, 3, id="1e6-1080p"),
     pytest.param(5_000_000, 1920, 1080, 3, id="5e6-1080p"),
     pytest.param(1_000_000, 3840, 2160, 3, id="1e6-4K"),
+    # config 5's per-block workload: >= 5e6 Gaussians at 4K, one cold-capacity view (phase 2 and the long-list sorts)
+    pytest.param(5_000_000, 3840, 2160, 1, id="5e6-4K"),
     # 31250 binning waves: the one-launch wave-total scan (k_bin_offsets) runs two super-rounds of prefetched loads
     # (1e6 fits one, 5e6 takes the multi-kernel scan)
     pytest.param(2_000_000, 1280, 720, 3, id="2e6-720p"),
