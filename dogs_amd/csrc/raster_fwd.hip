@@ -451,7 +451,11 @@ __device__ __forceinline__ BinLane bin_lane(const BinArgs& a, int g, int lane, u
         s_key[lane] = key;
         bool m = known == 1 || (key != 0xffffffffu && (PHASE == 1 ? key < thr : key >= thr));
         if (m) {
-            const float4 s0 = a.sp[2 * g], s1 = a.sp[2 * g + 1];
+            // phase 2 tests membership on the rect half of the record first: most past-threshold Gaussians touch no
+            // unfinished tile, so only the members load the other 16 bytes
+            const bool rect_first = PHASE == 2 && known < 0;
+            float4 s0 = rect_first ? make_float4(0.f, 0.f, 0.f, 0.f) : a.sp[2 * g];
+            const float4 s1 = a.sp[2 * g + 1];
             sp_rect(s1, b.x0, b.y0, b.x1, b.y1);
 #ifdef DG_PHASE2_SAT
             if (PHASE == 2 && known < 0)
@@ -459,6 +463,7 @@ __device__ __forceinline__ BinLane bin_lane(const BinArgs& a, int g, int lane, u
 #else
             if (PHASE == 2 && known < 0) m = b.x1 > b.x0 && b.y1 > b.y0 && rows_touch(a, b.x0, b.y0, b.x1, b.y1);
 #endif
+            if (m && rect_first) s0 = a.sp[2 * g];
             if (m) {
                 b.co = make_float4(s0.z, s0.w, s1.x, s1.y);
                 b.mx = s0.x; b.my = s0.y;
