@@ -952,7 +952,11 @@ __global__ void __launch_bounds__(256) k_render_fwd2(RenderArgs a) {
     // back to s_e for the backward), the block sorts a longer one in place through the global scratch -- the same
     // two routines, so the same order, as k_tile_dsort / k_tile_dsort_long
     bool lds_ids = false;
+#ifdef DG_DIAG_FWD2_NOSORT  // timing diagnostic only (wrong order)
+    if (false) {
+#else
     if (a.fuse_sort && n > 1) {
+#endif
         uint32_t* scr = reinterpret_cast<uint32_t*>(s_sb);
         if (n <= DS_WAVE_MAX2) {
             if (w == 0) wave_sort_tile<DS_ROWS2>(a.ds, tile, lane, scr, scr + 256, scr + 256 + DS_WAVE_MAX2, s_ids, 1);
@@ -983,6 +987,9 @@ __global__ void __launch_bounds__(256) k_render_fwd2(RenderArgs a) {
             s_sb[j * 3 + 0] = r0; s_sb[j * 3 + 1] = r1; s_sb[j * 3 + 2] = r2;
         }
         __syncthreads();
+#ifdef DG_DIAG_FWD2_NOCOMP  // timing diagnostic only (no compositing)
+        if (cnt > 0) continue;
+#endif
         for (int j0 = 0; j0 < cnt; j0 += 4) {
             if (!__any(thr < 1.0f)) break;  // every pixel of the wave saturated (or outside)
 #pragma unroll
@@ -1037,6 +1044,162 @@ __global__ void __launch_bounds__(256) k_render_fwd2(RenderArgs a) {
         mx = y > mx ? y : mx;
     }
     if (lane == 0) s_mx[w] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t m01 = s_mx[0] > s_mx[1] ? s_mx[0] : s_mx[1], m23 = s_mx[2] > s_mx[3] ? s_mx[2] : s_mx[3];
+        a.max_contrib[tile] = m01 > m23 ? m01 : m23;
+    }
+}
+
+// Phase 2 with the alphas and the compositing chain split (DG_FWD2_SPLIT; k_render_fwd2's arithmetic, bit for bit).
+// k_render_fwd2 runs nearly alone on the chip with one wave per SIMD, so its time is one wave's instruction stream
+// per splat.  Here a 1024-thread block per tile: all 16 waves compute the alphas of a sub-chunk of F2X_SUB splats
+// for the tile's 256 pixels (4 pixels per splat-lane team, 16 waves sharing the SIMDs) into LDS, then the four
+// pixel waves run only the transmittance / colour chain over them.  The stored value is min(0.99, o exp2(power)), or
+// -1 when power > 0 (then `ak < thr` rejects it exactly as `power > 0 ||` does).
+#ifndef DG_FWD2X_CHUNK
+#define DG_FWD2X_CHUNK 512
+#endif
+#ifndef DG_FWD2X_SUB
+#define DG_FWD2X_SUB 32
+#endif
+constexpr int F2X_CHUNK = DG_FWD2X_CHUNK, F2X_SUB = DG_FWD2X_SUB;
+template <bool COUNT>
+__global__ void __launch_bounds__(1024) k_render_fwd2x(RenderArgs a) {
+    __shared__ __attribute__((aligned(16))) float4 s_sb[(F2X_CHUNK + 4) * 3];  // (also the sort's scratch)
+    __shared__ float s_al[F2X_SUB * 256];
+    __shared__ uint32_t s_mx[4];
+    __shared__ uint32_t s_ids[DS_WAVE_MAX2];
+    static_assert((F2X_CHUNK + 4) * 12 >= BS_RADIX * (1 + BS_WAVES) + 2 * BS_WAVES + 1, "sort scratch");
+    static_assert(F2X_CHUNK % F2X_SUB == 0 && F2X_SUB % 4 == 0, "sub-chunks");
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const bool pix = t < 256;  // the four pixel waves (k_render_fwd2's mapping)
+    const int tile = blockIdx.x;
+    if (a.probe && blockIdx.x == 0 && threadIdx.x == 0) a.probe[1] = a.counters[CNT_K2];
+    if (tile >= a.num_tiles || !a.unfinished[tile]) return;  // block-uniform: finished in phase 1
+    const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
+    const int p = t & 255;                                  // pixel of this thread in the alpha pass (= t for pix)
+    const int px = tx * GS_TILE_X + (p & 15), py = ty * GS_TILE_Y + (p >> 4);
+    const bool inside = px < a.W && py < a.H;
+    const float pxf = (float)px, pyf = (float)py;
+    float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f, D = 0.0f, thr = 2.0f;
+    uint32_t last = 0;
+    const size_t pid = inside ? (size_t)py * a.W + px : 0;
+    if (pix && inside) {
+        const float4 rs = a.resume[pid];
+        T = a.final_T[pid];
+        D = a.img_invd[pid];
+        last = a.n_contrib[pid];
+        C0 = rs.x; C1 = rs.y; C2 = rs.z; thr = rs.w;
+    }
+    const uint32_t cbase = a.ranges1[tile].y - a.ranges1[tile].x;
+    const uint2 rg = a.ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    bool lds_ids = false;
+    if (a.fuse_sort && n > 1) {
+        uint32_t* scr = reinterpret_cast<uint32_t*>(s_sb);
+        if (n <= DS_WAVE_MAX2) {
+            if (w == 0) wave_sort_tile<DS_ROWS2>(a.ds, tile, lane, scr, scr + 256, scr + 256 + DS_WAVE_MAX2, s_ids, 1);
+            lds_ids = true;
+        } else {
+            block_sort_long(a.ds, tile, scr, reinterpret_cast<uint32_t(*)[BS_RADIX]>(scr + BS_RADIX),
+                            reinterpret_cast<uint32_t(*)[BS_WAVES]>(scr + BS_RADIX * (1 + BS_WAVES)),
+                            reinterpret_cast<int*>(scr + BS_RADIX * (1 + BS_WAVES) + 2 * BS_WAVES));
+        }
+        __syncthreads();
+    }
+    const int team = t >> 8;  // alpha pass: splat lanes team, team + 4, ...
+    for (int base = 0; base < n; base += F2X_CHUNK) {
+        const int cnt = n - base < F2X_CHUNK ? n - base : F2X_CHUNK;
+        if (!__syncthreads_or((pix && thr < 1.0f) ? 1 : 0)) break;
+        for (int j = t; j < cnt + 4; j += 1024) {
+            float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+            if (j < cnt) {
+                const uint32_t e = min(lds_ids ? s_ids[base + j] : a.s_e[rg.x + base + j], a.K - 1);
+                const uint32_t g = min(a.eg[e], a.P - 1);
+                const float4 s0 = a.sp[2 * g], s1 = a.sp[2 * g + 1];
+                const float4 q = a.rgbi[g];
+                const SplatExp k = splat_exp_coeffs(s0.z, s0.w, s1.x);
+                r0 = make_float4(s0.x, s0.y, k.A, k.B);
+                r1 = make_float4(k.C, s1.y, q.x, q.y);
+                r2 = make_float4(q.z, q.w, __uint_as_float(g), 0.0f);
+            }
+            s_sb[j * 3 + 0] = r0; s_sb[j * 3 + 1] = r1; s_sb[j * 3 + 2] = r2;
+        }
+        __syncthreads();
+        for (int sub = 0; sub < cnt; sub += F2X_SUB) {
+            if (!__syncthreads_or((pix && thr < 1.0f) ? 1 : 0)) break;  // (also: the last chain is done with s_al)
+#pragma unroll 4
+            for (int jj = team; jj < F2X_SUB; jj += 4) {
+                const int j = sub + jj;
+                float v = -1.0f;
+                if (j < cnt) {
+                    const float4 Sa = s_sb[j * 3 + 0], Sb = s_sb[j * 3 + 1];
+                    const float dy = Sa.y - pyf;
+                    const float bdy = Sa.w * dy, cdy2 = (Sb.x * dy) * dy;
+                    const float dx = Sa.x - pxf;
+                    const float p2 = fmaf(dx, fmaf(Sa.z, dx, bdy), cdy2);
+                    const float ak = fminf(0.99f, Sb.y * __builtin_amdgcn_exp2f(p2));
+                    v = p2 > 0.0f ? -1.0f : ak;
+                }
+                s_al[jj * 256 + p] = v;
+            }
+            __syncthreads();
+            if (pix) {
+                const int m = cnt - sub < F2X_SUB ? cnt - sub : F2X_SUB;
+                for (int j0 = 0; j0 < m; j0 += 4) {
+                    if (!__any(thr < 1.0f)) break;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int jj = j0 + u;
+                        if (jj >= m) break;  // wave-uniform
+                        const int j = sub + jj;
+                        const float4 Sb = s_sb[j * 3 + 1], Sc = s_sb[j * 3 + 2];
+                        const float ak = s_al[jj * 256 + p];
+                        const bool acc = !(ak < thr);
+                        float al = acc ? ak : 0.0f;
+                        const float test_T = T * (1.0f - al);
+                        const bool term = test_T < 0.0001f;
+                        thr = term ? 2.0f : thr;
+                        al = term ? 0.0f : al;
+                        const float Tn = term ? T : test_T;
+                        last = (acc && !term) ? cbase + (uint32_t)(base + j + 1) : last;
+                        if (COUNT) {
+                            const uint32_t c = (uint32_t)__popcll(__ballot(acc && al != 0.0f));
+                            if (c && lane == 0) atomicAdd(a.gcount + __float_as_uint(Sc.z), c);
+                        }
+                        const float wt = al * T;
+                        C0 = fmaf(Sb.z, wt, C0);
+                        C1 = fmaf(Sb.w, wt, C1);
+                        C2 = fmaf(Sc.x, wt, C2);
+                        D = fmaf(Sc.y, wt, D);
+                        T = Tn;
+                    }
+                }
+            }
+        }
+        __syncthreads();  // the next chunk's gather overwrites s_sb
+    }
+    uint32_t mx = 0;
+    if (pix && inside) {
+        const size_t HW = (size_t)a.W * a.H;
+        a.final_T[pid] = T;
+        a.n_contrib[pid] = last;
+        const float o0 = fmaf(T, a.bg[0], C0);
+        const float o1 = fmaf(T, a.bg[1], C1);
+        const float o2 = fmaf(T, a.bg[2], C2);
+        a.out_color[pid] = o0; a.out_color[HW + pid] = o1; a.out_color[2 * HW + pid] = o2;
+        a.img_color[pid] = o0; a.img_color[HW + pid] = o1; a.img_color[2 * HW + pid] = o2;
+        a.out_invd[pid] = D;
+        a.img_invd[pid] = D;
+        mx = last;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t y = __shfl_xor(mx, o);
+        mx = y > mx ? y : mx;
+    }
+    if (pix && lane == 0) s_mx[w] = mx;
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t m01 = s_mx[0] > s_mx[1] ? s_mx[0] : s_mx[1], m23 = s_mx[2] > s_mx[3] ? s_mx[2] : s_mx[3];
@@ -1128,8 +1291,13 @@ void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
     const int blocks = (a.num_tiles + 3) / 4;
 #ifndef DG_PHASE2_WAVE_PER_TILE  // A/B switch: phase 2 with k_render_fwd's one wave per tile
     if (a.phase == 2) {
+#ifdef DG_FWD2_SPLIT
+        if (a.gcount) k_render_fwd2x<true><<<a.num_tiles, 1024, 0, s>>>(a);
+        else k_render_fwd2x<false><<<a.num_tiles, 1024, 0, s>>>(a);
+#else
         if (a.gcount) k_render_fwd2<true><<<a.num_tiles, 256, 0, s>>>(a);
         else k_render_fwd2<false><<<a.num_tiles, 256, 0, s>>>(a);
+#endif
         return;
     }
 #endif

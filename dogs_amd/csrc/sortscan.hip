@@ -399,11 +399,10 @@ void tile_offsets(uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges, hipStre
 }
 
 // Block 0: exclusive scan of the wave totals in place (+ total); block 1: the per-tile ranges (tile_offsets).
-// One round covers 1024 x BO_ITEMS items: every thread loads its BO_ITEMS consecutive items at once (one HBM round
-// trip), sums them serially, and one wave shuffle scan + one LDS exchange of the 16 wave sums gives every thread its
-// exclusive base -- one barrier pair per round (a 1e6-Gaussian view has 15625 wave totals and 8160 tiles at 1080p:
-// a single round each).
-constexpr int BO_ITEMS = 16;
+// 4 items per thread per 4096-item round, wave shuffle scan + 16 wave sums in LDS, running carry.  The loads of
+// BO_ROUNDS rounds are issued before the first scan (one HBM round trip per 16384 items instead of one per round:
+// a 1e6-Gaussian view has 15625 wave totals, so the whole scan waits on memory once).
+constexpr int BO_ROUNDS = 4;
 __global__ void __launch_bounds__(1024) k_bin_offsets(uint32_t* __restrict__ wtot, uint32_t n,
                                                       uint32_t* __restrict__ total, uint32_t* __restrict__ tile_cnt,
                                                       uint32_t num_tiles, uint2* __restrict__ ranges,
@@ -420,14 +419,21 @@ __global__ void __launch_bounds__(1024) k_bin_offsets(uint32_t* __restrict__ wto
     uint32_t* src = tiles ? tile_cnt : wtot;
     if (t == 0) s_carry = 0u;
     __syncthreads();
-    for (uint32_t b = 0; b < N; b += 1024u * BO_ITEMS) {
-        const uint32_t i0 = b + (uint32_t)BO_ITEMS * (uint32_t)t;
-        uint32_t v[BO_ITEMS];
+    for (uint32_t sb = 0; sb < N; sb += 4096u * BO_ROUNDS) {
+      uint32_t pv[BO_ROUNDS][4];
 #pragma unroll
-        for (int k = 0; k < BO_ITEMS; k++) v[k] = i0 + k < N ? src[i0 + k] : 0u;
-        uint32_t loc = 0;
+      for (int r = 0; r < BO_ROUNDS; r++) {
+          const uint32_t i0 = sb + 4096u * r + 4u * (uint32_t)t;
 #pragma unroll
-        for (int k = 0; k < BO_ITEMS; k++) loc += v[k];
+          for (int k = 0; k < 4; k++) pv[r][k] = i0 + k < N ? src[i0 + k] : 0u;
+      }
+#pragma unroll
+      for (int r = 0; r < BO_ROUNDS; r++) {
+        const uint32_t b = sb + 4096u * r;
+        if (b >= N) break;  // block-uniform
+        const uint32_t i0 = b + 4u * (uint32_t)t;
+        const uint32_t* v = pv[r];
+        const uint32_t loc = v[0] + v[1] + v[2] + v[3];
         uint32_t x = loc;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -441,7 +447,7 @@ __global__ void __launch_bounds__(1024) k_bin_offsets(uint32_t* __restrict__ wto
         for (int k = 0; k < 16; k++) { if (k < w) off += s_w[k]; tot += s_w[k]; }
         uint32_t ex = off + x - loc;
 #pragma unroll
-        for (int k = 0; k < BO_ITEMS; k++) {
+        for (int k = 0; k < 4; k++) {
             if (i0 + k < N) {
                 if (tiles) { ranges[i0 + k] = make_uint2(ex, ex + v[k]); tile_cnt[i0 + k] = 0u; }
                 else wtot[i0 + k] = ex;
@@ -451,6 +457,7 @@ __global__ void __launch_bounds__(1024) k_bin_offsets(uint32_t* __restrict__ wto
         __syncthreads();
         if (t == 0) s_carry += tot;
         __syncthreads();
+      }
     }
     if (!tiles && t == 0) *total = s_carry;
 }

@@ -233,15 +233,17 @@ __device__ __forceinline__ int wave_sort_tile(const DSortArgs& a, int tile, int 
 constexpr int BS_RADIX = 256;
 constexpr int BS_WAVES = 4;
 
-// One stable LSD step of the long-list sort by the 256-thread block: (key(v) - kmin) digits, (keys, vals) ping-pong
-// through global scratch in 256-item chunks.  `key` maps a value to its sort key.  Result in va.
+// One stable LSD step of the long-list sort by a 256-thread team: (key(v) - kmin) digits, (keys, vals) ping-pong
+// through global scratch in 256-item chunks.  `key` maps a value to its sort key.  Result in va.  The team is threads
+// 0..255 of the block; a larger block's other threads only take part in the barriers (k_render_fwd2x's 1024).
 template <typename KeyFn>
 __device__ __forceinline__ void block_radix_global(uint32_t*& va, uint32_t*& vb, uint32_t* ka, uint32_t* kb, uint32_t n,
                                    KeyFn&& key, uint32_t* s_base, uint32_t (*s_wh)[BS_RADIX], uint32_t (*s_red)[BS_WAVES]) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const bool on = t < 256;
     const uint64_t lt = lanemask_lt();
     uint32_t kmin = 0xffffffffu, kmax = 0u;
-    for (uint32_t i = t; i < n; i += 256) {
+    for (uint32_t i = t; on && i < n; i += 256) {
         const uint32_t kk = key(va[i]);
         ka[i] = kk;
         kmin = kk < kmin ? kk : kmin;
@@ -250,7 +252,7 @@ __device__ __forceinline__ void block_radix_global(uint32_t*& va, uint32_t*& vb,
     kmin = wave_min_u32(kmin);
     kmax = wave_max_u32(kmax);
     __syncthreads();
-    if (lane == 0) { s_red[0][w] = kmin; s_red[1][w] = kmax; }
+    if (on && lane == 0) { s_red[0][w] = kmin; s_red[1][w] = kmax; }
     __syncthreads();
     kmin = s_red[0][0]; kmax = s_red[1][0];
     for (int q = 1; q < BS_WAVES; q++) {
@@ -261,35 +263,37 @@ __device__ __forceinline__ void block_radix_global(uint32_t*& va, uint32_t*& vb,
     for (int p = 0; p < passes; p++) {
         const int shift = 8 * p;
         __syncthreads();
-        s_base[t] = 0u;
+        if (on) s_base[t] = 0u;
         __syncthreads();
-        for (uint32_t i = t; i < n; i += 256) atomicAdd(&s_base[((ka[i] - kmin) >> shift) & 0xffu], 1u);
+        for (uint32_t i = t; on && i < n; i += 256) atomicAdd(&s_base[((ka[i] - kmin) >> shift) & 0xffu], 1u);
         __syncthreads();
         {  // exclusive scan of the digit counts (thread t = digit t)
-            const uint32_t c = s_base[t];
+            const uint32_t c = on ? s_base[t] : 0u;
             uint32_t x = c;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
                 const uint32_t y = __shfl_up(x, o);
                 if (lane >= o) x += y;
             }
-            if (lane == 63) s_red[0][w] = x;
+            if (on && lane == 63) s_red[0][w] = x;
             __syncthreads();
             uint32_t off = 0;
-            for (int q = 0; q < w; q++) off += s_red[0][q];
-            s_base[t] = off + x - c;
+            for (int q = 0; q < w && q < BS_WAVES; q++) off += s_red[0][q];
+            if (on) s_base[t] = off + x - c;
         }
         __syncthreads();
         for (uint32_t c0 = 0; c0 < n; c0 += 256) {
             const uint32_t i = c0 + t;
-            const bool act = i < n;
+            const bool act = on && i < n;
             const uint32_t kk = act ? ka[i] : 0u;
             const uint32_t val = act ? va[i] : 0u;
             const uint32_t d = ((kk - kmin) >> shift) & 0xffu;
             const uint64_t m = peer_mask(d, act);
             const uint32_t before = (uint32_t)__popcll(m & lt);
+            if (on) {
 #pragma unroll
-            for (int q = 0; q < BS_WAVES; q++) s_wh[q][t] = 0u;
+                for (int q = 0; q < BS_WAVES; q++) s_wh[q][t] = 0u;
+            }
             __syncthreads();
             if (act && before == 0) s_wh[w][d] = (uint32_t)__popcll(m);
             __syncthreads();
@@ -300,7 +304,7 @@ __device__ __forceinline__ void block_radix_global(uint32_t*& va, uint32_t*& vb,
                 vb[pos] = val;
             }
             __syncthreads();
-            s_base[t] += s_wh[0][t] + s_wh[1][t] + s_wh[2][t] + s_wh[3][t];
+            if (on) s_base[t] += s_wh[0][t] + s_wh[1][t] + s_wh[2][t] + s_wh[3][t];
             __syncthreads();
         }
         uint32_t* tk = ka; ka = kb; kb = tk;
@@ -310,10 +314,11 @@ __device__ __forceinline__ void block_radix_global(uint32_t*& va, uint32_t*& vb,
 }
 
 // Block-level sort of one long list (n > DS_WAVE_MAX): LSD radix through global scratch; with equal keys it sorts by
-// Gaussian index first and then, stably, by key.
+// Gaussian index first and then, stably, by key.  Threads 0..255 work; any others only join the barriers.
 __device__ __forceinline__ void block_sort_long(const DSortArgs& a, int tile, uint32_t* s_base, uint32_t (*s_wh)[BS_RADIX],
                                 uint32_t (*s_red)[BS_WAVES], int* s_tie) {
     const int t = threadIdx.x;
+    const bool on = t < 256;
     const uint2 rg = a.ranges[tile];
     const uint32_t n = rg.y - rg.x;
     uint32_t *va = a.s_e + rg.x, *vb = a.s_tmp + rg.x;
@@ -321,7 +326,7 @@ __device__ __forceinline__ void block_sort_long(const DSortArgs& a, int tile, ui
     block_radix_global(va, vb, a.k_a + rg.x, a.k_b + rg.x, n, dkey, s_base, s_wh, s_red);
     if (t == 0) *s_tie = 0;
     __syncthreads();
-    for (uint32_t i = t + 1; i < n; i += 256)
+    for (uint32_t i = t + 1; on && i < n; i += 256)
         if (ds_key(a, va[i]) == ds_key(a, va[i - 1])) *s_tie = 1;
     __syncthreads();
     if (*s_tie) {  // rare: order by Gaussian index first, then stably by key
@@ -330,7 +335,7 @@ __device__ __forceinline__ void block_sort_long(const DSortArgs& a, int tile, ui
         block_radix_global(va, vb, a.k_a + rg.x, a.k_b + rg.x, n, dkey, s_base, s_wh, s_red);
     }
     if (va != a.s_e + rg.x)  // result in the scratch values: copy back into s_e
-        for (uint32_t i = t; i < n; i += 256) a.s_e[rg.x + i] = va[i];
+        for (uint32_t i = t; on && i < n; i += 256) a.s_e[rg.x + i] = va[i];
     __syncthreads();
 }
 
