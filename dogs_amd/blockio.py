@@ -1,11 +1,11 @@
 """Block export around the Grid2D split: COLMAP model -> sorted views -> per-block view sets ->
 the on-disk block folders the ADMM block trainers read.
 
-* `colmap_views` restates load_colmap.py:226-273: load the binary model through the native readers
+* `colmap_views` restates load_colmap.py:226-313: load the binary model through the native readers
   (dogs_amd/colmap.py), build per image K = [[fx/f, 0, cx/f], [0, fy/f, cy/f], [0, 0, 1]] and w2c = [R | t; 0 0 0 1],
-  invert to camera-to-world, sort by image name, map sorted index -> COLMAP image id.  The scene normalisation that
-  follows in the reference (similarity_from_cameras / normalize_poses, :294-313) and image/normal file discovery are
-  dataset plumbing outside the hot path and not restated.
+  invert to camera-to-world, sort by image name, map sorted index -> COLMAP image id, then (scale / rotate, the
+  reference's defaults) the scene normalisation (dogs_amd.normalize: similarity_from_cameras + normalize_poses), so
+  the Grid2D split runs in the reference's frame.  Image/normal file discovery is dataset plumbing, not restated.
 * `block_views` restates the per-block selection of load_colmap.py:459-487 (block members in image order, validation
   indices removed, poses/intrinsics as float32 tensors).
 * `MiniDataset` writes/reads the reference's block folder format (dataset_base.py:96-150): cameras/camera_{i}.pt, one
@@ -25,9 +25,11 @@ from .camera import RasterCamera, make_camera
 from .colmap import SceneManager
 
 
-def colmap_views(colmap_dir: str, factor: int = 1, train_image_names=None) -> dict:
+def colmap_views(colmap_dir: str, factor: int = 1, train_image_names=None, scale: bool = True,
+                 rotate: bool = True) -> dict:
     """{'image_names', 'camtoworlds' [N,4,4] f64, 'intrinsics' [N,3,3] f64, 'image_index_to_image_id', 'points3d',
-    'colors', 'sizes' [N,2] (w,h of each image's camera / factor)} of a COLMAP binary model."""
+    'colors', 'sizes' [N,2] (w,h of each image's camera / factor)} of a COLMAP binary model; scale / rotate:
+    load_colmap's normalisation flags (its defaults, True)."""
     if factor not in (1, 2, 4, 8):
         raise ValueError(f"factor must be 1, 2, 4 or 8, got {factor}")
     m = SceneManager(colmap_dir, load_points=True)
@@ -47,10 +49,15 @@ def colmap_views(colmap_dir: str, factor: int = 1, train_image_names=None) -> di
     c2w = np.linalg.inv(np.stack(w2c))
     order = np.argsort(names)
     names = [names[i] for i in order]
-    return {"image_names": names, "camtoworlds": c2w[order], "intrinsics": np.stack(K)[order],
+    c2w, pts = c2w[order], m.points3D
+    if scale:
+        from .normalize import normalize_scene
+        c2w, pts = normalize_scene(c2w, pts, scale=True, rotate=rotate)
+        c2w, pts = np.asarray(c2w, dtype=np.float64), np.asarray(pts, dtype=np.float64)
+    return {"image_names": names, "camtoworlds": c2w, "intrinsics": np.stack(K)[order],
             "sizes": np.asarray(wh, dtype=np.int64)[order],
             "image_index_to_image_id": {i: m.name_to_image_id[n] for i, n in enumerate(names)},
-            "points3d": m.points3D, "colors": m.point3D_colors}
+            "points3d": pts, "colors": m.point3D_colors}
 
 
 def block_views(block_image_ids: dict, camtoworlds, intrinsics, image_paths, val_indices=()) -> dict:

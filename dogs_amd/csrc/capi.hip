@@ -103,6 +103,7 @@ struct Geom {
     uint32_t* hist;                  // [DH_BINS] depth histogram of the prefix cut
     uint32_t* wtot;                  // [bin_waves(P)] per-wave instance totals of the binning walk
     uint64_t* wmask;                 // [bin_waves(P)] per-wave member ballot of the binning walk
+    uint32_t* mlist;                 // [P] member lists of the fat binning waves
     void* scan_tmp;
     size_t bytes;
 };
@@ -120,6 +121,7 @@ Geom carve_geom(void* base, int P) {
     g.hist = c.take<uint32_t>(gs::DH_BINS);
     g.wtot = c.take<uint32_t>((size_t)gs::bin_waves(P > 0 ? P : 1));
     g.wmask = c.take<uint64_t>((size_t)gs::bin_waves(P > 0 ? P : 1));
+    g.mlist = c.take<uint32_t>(n);
     g.scan_tmp = c.take<char>(gs::bin_scan_temp_bytes(P > 0 ? P : 1));
     g.bytes = c.off;
     return g;
@@ -192,7 +194,7 @@ gs::BinArgs bin_args(const dg_raster_args* r, const Geom& g, const Image& im, in
     a.D = (r->sh && r->M > 0) ? r->D : 0; a.M = r->M; a.means3D = r->means3D; a.campos = r->campos; a.dc = r->dc;
     a.sh = (r->sh && r->M > 0) ? r->sh : nullptr; a.colors = r->colors; a.rgbi = g.rgbi;
     a.P = P; a.tiles_x = tx; a.num_tiles = T; a.dkey = g.dkey; a.sp = g.sp; a.counters = g.counters;
-    a.unf = im.unfinished; a.sat = im.sat; a.wtot = g.wtot; a.wmask = g.wmask; a.cap = cap; a.first_e = g.first_e; a.rcnt = g.rcnt;
+    a.unf = im.unfinished; a.sat = im.sat; a.wtot = g.wtot; a.wmask = g.wmask; a.mlist = g.mlist; a.cap = cap; a.first_e = g.first_e; a.rcnt = g.rcnt;
     a.eg = b.eg; a.ikey = b.ik; a.tile_cnt = tile_cnt; a.ranges = ranges; a.s_e = b.se;
     a.unf_rows = nullptr; a.unf_rw = 0; a.unf_th = 0; a.probe = nullptr;
     return a;

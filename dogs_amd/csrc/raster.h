@@ -170,6 +170,8 @@ struct BinArgs {
     const uint32_t* sat;         // phase 2: summed-area table of unf
     uint32_t* wtot;              // [bin_waves(P)] per-wave totals, scanned in place
     uint64_t* wmask;             // [bin_waves(P)] per-wave member ballot of the count pass, read by the emission
+                                 // (fat waves: the member count)
+    uint32_t* mlist;             // [P] fat waves: wave w's members (offsets from its first Gaussian), count pass
     uint32_t cap;                // capacity of the instance arrays
     uint32_t *first_e, *rcnt;
     uint32_t *eg, *ikey;         // per instance: Gaussian, depth key

@@ -566,6 +566,179 @@ __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
                     });
 }
 
+// ---- Fat binning waves (R x 64 consecutive Gaussians per wave; DG_BIN_FAT1 / DG_BIN_FAT2 = R of phase 1 / 2).
+// Most Gaussians of a wave are not members (phase 1: ~5% are in front of the threshold; phase 2: only those whose
+// rect touches an unfinished tile), so a 64-Gaussian wave mostly tests and exits, and its memory round trips are the
+// cost.  A fat wave loads the keys (and, in phase 2, the rect halves) of all R x 64 Gaussians at once, compacts its
+// members in LDS (index order), walks them 64 at a time and hands the member list to the emission pass, which then
+// skips every membership test.  The members stay in index order, so the emission numbering -- and every output -- is
+// the one of the 64-Gaussian waves.
+#ifndef DG_BIN_FAT1
+#define DG_BIN_FAT1 1
+#endif
+#ifndef DG_BIN_FAT2
+#define DG_BIN_FAT2 1
+#endif
+template <int PHASE> struct FatR { static constexpr int R = PHASE == 1 ? DG_BIN_FAT1 : DG_BIN_FAT2; };
+template <int PHASE> __host__ __device__ constexpr int fat_span() { return 64 * FatR<PHASE>::R; }
+
+// walk inputs of a known member g (BinLane with the membership already decided)
+__device__ __forceinline__ BinLane member_lane(const BinArgs& a, int g, bool member) {
+    BinLane b = {0, 0, 0, 0, 0.f, 0.f, 0.f, make_float4(0.f, 0.f, 0.f, 0.f), false};
+    if (member) {
+        const float4 s0 = a.sp[2 * g], s1 = a.sp[2 * g + 1];
+        sp_rect(s1, b.x0, b.y0, b.x1, b.y1);
+        b.co = make_float4(s0.z, s0.w, s1.x, s1.y);
+        b.mx = s0.x; b.my = s0.y;
+        b.lthr = gs_logf(b.co.w / (1.0f / 255.0f));
+        b.member = true;
+    }
+    if (!b.member) { b.x1 = b.x0; b.y1 = b.y0; }
+    return b;
+}
+
+template <int PHASE>
+__global__ void __launch_bounds__(256) k_bin_count_fat(BinArgs a) {
+    constexpr int R = FatR<PHASE>::R, S = 64 * R;
+    __shared__ CandLDS s_cand[4];
+    __shared__ uint32_t s_cnt[4][64];
+    __shared__ uint32_t s_mem[4][S];
+    if (PHASE == 2 && a.probe && blockIdx.x == 0 && threadIdx.x == 0) a.probe[0] = a.counters[CNT_UNFINISHED];
+    if (PHASE == 2 && a.counters[CNT_UNFINISHED] == 0u) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wave = blockIdx.x * 4 + w;
+    const int g0 = wave * S;
+    if (g0 >= a.P) return;
+    const uint32_t thr = a.counters[CNT_THR];
+    uint32_t key[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {  // every key load in flight at once
+        const int g = g0 + 64 * r + lane;
+        key[r] = g < a.P ? a.dkey[g] : 0xffffffffu;
+    }
+    bool mem[R];
+    if (PHASE == 1) {
+#pragma unroll
+        for (int r = 0; r < R; r++) mem[r] = key[r] != 0xffffffffu && key[r] < thr;
+    } else {
+        float4 s1[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {  // the rect halves of the past-threshold Gaussians, all at once
+            const bool c = key[r] != 0xffffffffu && key[r] >= thr;
+            s1[r] = c ? a.sp[2 * (g0 + 64 * r + lane) + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+            mem[r] = c;
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            if (!mem[r]) continue;
+            int x0, y0, x1, y1;
+            sp_rect(s1[r], x0, y0, x1, y1);
+            mem[r] = x1 > x0 && y1 > y0 && rows_touch(a, x0, y0, x1, y1);
+        }
+    }
+    // compact the members (index order) into LDS and the wave's slice of the global member list
+    uint32_t nm = 0;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint64_t bm = __ballot(mem[r]);
+        if (mem[r]) {
+            const uint32_t slot = nm + (uint32_t)__popcll(bm & lt);
+            s_mem[w][slot] = (uint32_t)(64 * r + lane);
+            a.mlist[g0 + slot] = (uint32_t)(64 * r + lane);
+        }
+        nm += (uint32_t)__popcll(bm);
+    }
+    if (lane == 0) a.wmask[wave] = nm;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t tot = 0;
+    for (uint32_t mb = 0; mb < nm; mb += 64) {
+        const uint32_t i = mb + (uint32_t)lane;
+        const bool member = i < nm;
+        const int g = member ? g0 + (int)s_mem[w][i] : 0;
+        const BinLane b = member_lane(a, g, member);
+        wave_count(s_cand[w], s_cnt[w], lane, b.x0, b.y0, b.x1, b.y1, b.mx, b.my, b.co, b.lthr,
+                   [&](int tx, int ty) { return PHASE == 1 || a.unf[ty * a.tiles_x + tx] != 0; },
+                   [&](int tx, int ty) { atomicAdd(&a.tile_cnt[ty * a.tiles_x + tx], 1u); });
+        const uint32_t c = member ? s_cnt[w][lane] : 0u;
+        if (member) a.rcnt[g] = c;
+        uint32_t sc = c;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sc += __shfl_xor(sc, o);
+        tot += sc;
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) a.wtot[wave] = tot;
+}
+
+template <int PHASE>
+__global__ void __launch_bounds__(256) k_bin_emit_fat(BinArgs a) {
+    constexpr int S = fat_span<PHASE>();
+    __shared__ CandLDS s_cand[4];
+    __shared__ uint32_t s_key[4][64];
+    __shared__ uint32_t s_g[4][64];
+    if (PHASE == 2 && a.counters[CNT_UNFINISHED] == 0u) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wave = blockIdx.x * 4 + w;
+    const int g0 = wave * S;
+    if (g0 >= a.P) return;
+    const uint32_t nm = (uint32_t)a.wmask[wave];
+    if (!nm) return;
+    const uint32_t base = a.wtot[wave];
+    const uint32_t e_off = PHASE == 2 ? a.counters[CNT_E1] : 0u;
+    uint32_t running = 0;
+    for (uint32_t mb = 0; mb < nm; mb += 64) {
+        const uint32_t i = mb + (uint32_t)lane;
+        const bool member = i < nm;
+        const int g = member ? g0 + (int)a.mlist[g0 + i] : 0;
+        const uint32_t key = member ? a.dkey[g] : 0u;
+        s_key[w][lane] = key;
+        s_g[w][lane] = (uint32_t)g;
+        const BinLane b = member_lane(a, g, member);
+        const uint32_t c = member ? a.rcnt[g] : 0u;
+        uint32_t incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const uint32_t wt = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        if (base + running + wt > a.cap) return;  // (capacity: never with consistent inputs)
+        if (member && c) {
+            a.first_e[g] = e_off + base + running + incl - c;
+            f3 col;
+            if (a.colors) {
+                col = {a.colors[3 * g], a.colors[3 * g + 1], a.colors[3 * g + 2]};
+            } else {
+                const f3 po = {a.means3D[3 * g], a.means3D[3 * g + 1], a.means3D[3 * g + 2]};
+                const f3 d0 = {a.dc[3 * g], a.dc[3 * g + 1], a.dc[3 * g + 2]};
+                col = sh_to_rgb(po, a.campos, a.sh ? a.D : 0, d0, a.sh ? a.sh + (size_t)g * a.M * 3 : nullptr, nullptr);
+            }
+            a.rgbi[g] = make_float4(col.x, col.y, col.z, 1.f / __uint_as_float(key));
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (wt) {
+            uint32_t run = running;
+            wave_candidates(s_cand[w], lane, b.x0, b.y0, b.x1, b.y1, b.mx, b.my, b.co, b.lthr,
+                            [&](int owner, int tx, int ty, bool kept, bool, uint32_t) {
+                                kept = kept && (PHASE == 1 || a.unf[ty * a.tiles_x + tx] != 0);
+                                const uint64_t km = __ballot(kept);
+                                const uint64_t ltm = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+                                if (kept) {
+                                    const uint32_t e = base + run + (uint32_t)__popcll(km & ltm);
+                                    const int t = ty * a.tiles_x + tx;
+                                    a.eg[e] = s_g[w][owner];
+                                    a.ikey[e] = s_key[w][owner];
+                                    a.s_e[a.ranges[t].x + atomicAdd(&a.tile_cnt[t], 1u)] = e;
+                                }
+                                run += (uint32_t)__popcll(km);
+                            });
+        }
+        running += wt;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // Exclusive summed-area table of the unfinished-tile flags, [(tiles_y+1) x (tiles_x+1)]: O(1) "does this
 // rect touch an unfinished tile" for the phase-2 kernels.  Two wave-parallel passes (one wave per row, then one
 // per column, 64-wide shuffle scans), so no lane walks a dependent chain of global accesses.
@@ -1265,10 +1438,15 @@ void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, ui
 }
 void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s) {
     if (a.P <= 0) return;
-    const int waves = (a.P + EMIT_RANKS - 1) / EMIT_RANKS;
+    const bool fat = phase == 1 ? DG_BIN_FAT1 > 1 : DG_BIN_FAT2 > 1;
+    const int span = fat ? (phase == 1 ? fat_span<1>() : fat_span<2>()) : EMIT_RANKS;
+    const int waves = (a.P + span - 1) / span;
     const int blocks = (waves + 3) / 4;
     const uint32_t* gate = phase == 2 ? a.counters + CNT_UNFINISHED : nullptr;
-    if (phase == 2) k_bin_count<2><<<blocks, 256, 0, s>>>(a);
+    if (fat) {
+        if (phase == 2) k_bin_count_fat<2><<<blocks, 256, 0, s>>>(a);
+        else k_bin_count_fat<1><<<blocks, 256, 0, s>>>(a);
+    } else if (phase == 2) k_bin_count<2><<<blocks, 256, 0, s>>>(a);
     else k_bin_count<1><<<blocks, 256, 0, s>>>(a);
     if ((uint32_t)waves <= BIN_OFFSETS_MAX_N) {  // one launch: wave offsets + tile ranges, tile_cnt -> 0 (cursors)
         bin_offsets(a.wtot, (uint32_t)waves, total, a.tile_cnt, (uint32_t)a.num_tiles, a.ranges, s, gate);
@@ -1276,7 +1454,10 @@ void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hi
         exclusive_scan(a.wtot, (uint32_t)waves, a.wtot, total, scan_tmp, s, gate);
         tile_offsets(a.tile_cnt, (uint32_t)a.num_tiles, a.ranges, s, gate);
     }
-    if (phase == 2) k_bin_emit<2><<<blocks, 256, 0, s>>>(a);
+    if (fat) {
+        if (phase == 2) k_bin_emit_fat<2><<<blocks, 256, 0, s>>>(a);
+        else k_bin_emit_fat<1><<<blocks, 256, 0, s>>>(a);
+    } else if (phase == 2) k_bin_emit<2><<<blocks, 256, 0, s>>>(a);
     else k_bin_emit<1><<<blocks, 256, 0, s>>>(a);
 }
 size_t bin_scan_temp_bytes(int P) { return scan_temp_bytes((uint32_t)((P + EMIT_RANKS - 1) / EMIT_RANKS)); }

@@ -116,7 +116,7 @@ def test_colmap_views_and_block_export(tmp_path, exp):
     written and read back in the reference's format."""
     import torch
     from dogs_amd.blockio import MiniDataset, colmap_views, export_blocks
-    v = colmap_views(GOLD, factor=2)
+    v = colmap_views(GOLD, factor=2, scale=False)
     order = np.argsort(exp["image_names"])
     assert v["image_names"] == [exp["image_names"][i] for i in order]
     w2c = np.linalg.inv(v["camtoworlds"])
@@ -128,6 +128,12 @@ def test_colmap_views_and_block_export(tmp_path, exp):
         np.testing.assert_array_equal(v["intrinsics"][i], [[fx / 2, 0, cx / 2], [0, fy / 2, cy / 2], [0, 0, 1]])
         assert v["image_index_to_image_id"][i] == int(exp["image_ids"][j])
     np.testing.assert_array_equal(v["points3d"], exp["points3D"])
+    # with load_colmap's defaults the scene is normalised (dogs_amd.normalize, pinned in tests/test_normalize.py)
+    from dogs_amd.normalize import normalize_scene
+    vn = colmap_views(GOLD, factor=2)
+    c_ref, p_ref = normalize_scene(v["camtoworlds"], v["points3d"])
+    np.testing.assert_allclose(vn["camtoworlds"], np.asarray(c_ref, dtype=np.float64), rtol=0, atol=0)
+    np.testing.assert_allclose(vn["points3d"], np.asarray(p_ref, dtype=np.float64), rtol=0, atol=0)
     blocks = {0: [np.array([0, 1, 2, 3])], 1: [np.array([2, 3, 4, 5])]}   # overlapping blocks, image 3 is validation
     out = export_blocks(str(tmp_path), v, blocks, val_indices=[3])
     assert [len(d) for d in out] == [3, 3]

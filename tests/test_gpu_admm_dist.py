@@ -83,7 +83,7 @@ def _split(tmp):
     block point sets)."""
     from dogs_amd.blockio import colmap_views, export_blocks
     from dogs_amd.blocksplit import cluster_image_in_grid, cluster_points_in_grid
-    v = colmap_views(GOLD, factor=8)
+    v = colmap_views(GOLD, factor=8, scale=False)
     n_img = len(v["image_names"])
     ids, _, _, _ = cluster_image_in_grid(v["camtoworlds"], tmp, list(range(n_img)), [1.4, 1.4, 1.4],
                                          v["image_index_to_image_id"], num_blocks=2, mx=2, my=1)

@@ -112,7 +112,7 @@ def test_colmap_to_block_folders(hip_device, tmp_path):
     from dogs_amd import blocksplit
     from dogs_amd.blockio import MiniDataset, colmap_views, export_blocks
     gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "colmap")
-    v = colmap_views(gold)
+    v = colmap_views(gold, scale=False)
     n = len(v["image_names"])
     bids, cb, ecb, T = blocksplit.cluster_image_in_grid(v["camtoworlds"], str(tmp_path), np.arange(n),
                                                         [1.0, 1.0, 1.0], v["image_index_to_image_id"], 2, 2, 1)
