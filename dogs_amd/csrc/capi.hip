@@ -137,6 +137,8 @@ struct Image {
     uint32_t* sat;          // [(ty+1)*(tx+1)] summed-area table of `unfinished`
     uint32_t* long_tiles;   // [T] queue of the long-list tile depth sort
     uint32_t *tile_cnt, *tile_cnt2;  // [T] per-tile instance counters of the phase-1 / phase-2 binning
+    uint32_t* order;        // [T] the backward's replay order (written by the phase-2 emission when phase 2 ran)
+    uint32_t* unf_list;     // [T] the unfinished tiles, in the order phase 1 found them
     size_t bytes;
 };
 Image carve_image(void* base, int W, int H) {
@@ -161,6 +163,8 @@ Image carve_image(void* base, int W, int H) {
     im.long_tiles = c.take<uint32_t>(T);
     im.tile_cnt = c.take<uint32_t>(T);
     im.tile_cnt2 = c.take<uint32_t>(T);
+    im.order = c.take<uint32_t>(T);
+    im.unf_list = c.take<uint32_t>(T);
     im.bytes = c.off;
     return im;
 }
@@ -172,6 +176,7 @@ struct Binning {
     uint32_t* eg;      // Gaussian of each instance
     uint32_t* ik;      // depth key of each instance
     uint32_t *dk, *dk2;  // scratch keys of the long-list depth sort
+    uint8_t* flag;     // the backward's record-written flag of each instance (zeroed by the emission)
     size_t bytes;
 };
 Binning carve_binning(void* base, int64_t K) {
@@ -184,6 +189,7 @@ Binning carve_binning(void* base, int64_t K) {
     b.ik = c.take<uint32_t>(n);
     b.dk = c.take<uint32_t>(n);
     b.dk2 = c.take<uint32_t>(n);
+    b.flag = c.take<uint8_t>(n);
     b.bytes = c.off;
     return b;
 }
@@ -195,7 +201,8 @@ gs::BinArgs bin_args(const dg_raster_args* r, const Geom& g, const Image& im, in
     a.sh = (r->sh && r->M > 0) ? r->sh : nullptr; a.colors = r->colors; a.rgbi = g.rgbi;
     a.P = P; a.tiles_x = tx; a.num_tiles = T; a.dkey = g.dkey; a.sp = g.sp; a.counters = g.counters;
     a.unf = im.unfinished; a.sat = im.sat; a.wtot = g.wtot; a.wmask = g.wmask; a.mlist = g.mlist; a.cap = cap; a.first_e = g.first_e; a.rcnt = g.rcnt;
-    a.eg = b.eg; a.ikey = b.ik; a.tile_cnt = tile_cnt; a.ranges = ranges; a.s_e = b.se;
+    a.eg = b.eg; a.ikey = b.ik; a.flag = b.flag; a.tile_cnt = tile_cnt; a.ranges = ranges; a.s_e = b.se;
+    a.order = nullptr; a.max_contrib = nullptr; a.ranges1 = nullptr;
     a.unf_rows = nullptr; a.unf_rw = 0; a.unf_th = 0; a.probe = nullptr;
     return a;
 }
@@ -327,24 +334,21 @@ void adapt(CapProbe* ac, uint32_t prev_unfinished, uint32_t prev_k2, uint32_t e1
 }
 
 struct BwdScratch {
-    uint8_t* flag;
     float* rec;
     uint32_t *live_list, *live_cnt;  // contributing Gaussians per record-sum chunk (k_gauss_sum -> k_gauss_live)
     uint32_t* invd_flag;
-    uint32_t* order;  // [T] replay order of the tiles
     size_t bytes;
 };
 BwdScratch carve_bwd(void* base, int64_t K, int P, int T) {
     Carver c(base);
     BwdScratch s;
     const size_t n = (size_t)(K > 0 ? K : 1);
-    s.flag = c.take<uint8_t>(n);
     s.rec = c.take<float>(12 * n);
     const size_t chunks = (n + gs::SUM_CHUNK - 1) / gs::SUM_CHUNK;  // every slot < K
     s.live_list = c.take<uint32_t>(chunks * gs::SUM_CHUNK);
     s.live_cnt = c.take<uint32_t>(chunks);
     s.invd_flag = c.take<uint32_t>(4);
-    s.order = c.take<uint32_t>((size_t)(T > 0 ? T : 1));
+    (void)T;
     s.bytes = c.off;
     return s;
 }
@@ -561,6 +565,7 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     r.out_color = out_color; r.out_invd = out_invdepth; r.final_T = im.final_T; r.img_color = im.img_color;
     r.img_invd = im.img_invd; r.n_contrib = im.n_contrib; r.max_contrib = im.max_contrib;
     r.phase = 1; r.counters = g.counters; r.unfinished = im.unfinished; r.resume = im.resume;
+    r.unf_list = im.unf_list;
     r.ranges2_zero = im.ranges2;
     r.unf_rows = pre.unf_rows; r.unf_rw = unf_rw_of(tx);
     r.gcount = gcount;
@@ -601,6 +606,7 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
         ba.unf_rows = UNF_ROWS ? reinterpret_cast<const unsigned long long*>(im.sat) : nullptr;
         ba.unf_rw = unf_rw_of(tx); ba.unf_th = ty;
         ba.probe = UNF_ROWS && ac ? ac->probe : nullptr;
+        ba.order = im.order; ba.max_contrib = im.max_contrib; ba.ranges1 = im.ranges;
         gs::launch_bin(2, ba, g.counters + gs::CNT_K2, g.scan_tmp, s);
         const gs::DSortArgs ds2 = dsort_args(b2, K, T, im.ranges2, im.unfinished, gate, im.long_tiles,
                                              g.counters + gs::CNT_LONG2);
@@ -677,10 +683,12 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     const uint32_t* s_e = b.se;
     const uint32_t* s_e2 = nullptr;
     const uint32_t* eg2 = nullptr;
+    uint8_t* flag2 = nullptr;
     if (binning2) {
         Binning b2 = carve_binning((void*)binning2, Kcap);
         s_e2 = b2.se;
         eg2 = b2.eg;
+        flag2 = b2.flag;
     }
 
     const size_t sbytes = carve_bwd(nullptr, Kcap, P, T).bytes;
@@ -713,9 +721,9 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
         r.unfinished = im.unfinished;
         r.sp = g.sp; r.rgbi = g.rgbi; r.bg = a->bg;
         r.final_T = im.final_T; r.img_color = im.img_color; r.img_invd = im.img_invd; r.n_contrib = im.n_contrib;
-        r.dL_dpix = dL_dout_color; r.dL_dinvd = dL_dout_invdepth; r.rec = sc.rec; r.flag = sc.flag;
-        r.order = sc.order;
-        { PROF("render_bwd"); gs::launch_render_bwd(r, g.counters, s); }
+        r.dL_dpix = dL_dout_color; r.dL_dinvd = dL_dout_invdepth; r.rec = sc.rec; r.flag = b.flag; r.flag2 = flag2;
+        r.order = im.order;
+        { PROF("render_bwd"); gs::launch_render_bwd(r, g.counters, s, binning2 != nullptr); }
         DBG_SYNC(a->debug, s);
     }
     gs::GaussBwdArgs q;
@@ -729,7 +737,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     q.means3D = a->means3D; q.scales = a->scales; q.rotations = a->rotations; q.opacities = a->opacities;
     q.dc = a->dc; q.sh = (a->M > 0) ? a->sh : nullptr; q.cov3D_precomp = a->cov3D_precomp;
     q.view = a->viewmatrix; q.proj = a->projmatrix; q.campos = a->campos;
-    q.radii = radii; q.dkey = g.dkey; q.sp = g.sp; q.rec = sc.rec; q.flag = sc.flag;
+    q.radii = radii; q.dkey = g.dkey; q.sp = g.sp; q.rec = sc.rec; q.flag = b.flag; q.flag2 = flag2;
     q.eg = b.eg; q.eg2 = eg2; q.counters = g.counters; q.K1 = (uint32_t)C1;
     q.dmeans2D = dmeans2D; q.dcolors = dcolors; q.dopacity = dopacity; q.dmeans3D = dmeans3D; q.dcov3D = dcov3D;
     q.ddc = ddc; q.dsh = dsh; q.dscales = dscales; q.drot = drot; q.depth = depth;

@@ -70,6 +70,8 @@ struct RenderArgs {
     const uint2* ranges1;       // phase 2: the phase-1 ranges (contributor numbering continues after them)
     uint32_t* counters;         // CNT_* (phase 1 reads CNT_CUT, counts CNT_UNFINISHED)
     uint8_t* unfinished;        // [num_tiles]
+    uint32_t* unf_list;         // [num_tiles] phase 1 appends each unfinished tile (counters[CNT_UNFINISHED] slots);
+                                // phase 2 walks this list with a small grid instead of a block per tile
     float4* resume;             // [H*W] raw colour + live flag of unfinished tiles' pixels
     uint2* ranges2_zero;        // phase 1: phase-2 range of each tile it marks unfinished, reset to empty
     const float4* sp;
@@ -108,7 +110,8 @@ struct RenderBwdArgs {
     const float* dL_dpix;
     const float* dL_dinvd;   // may be null
     float* rec;              // [K][12] per-instance gradient record
-    uint8_t* flag;           // [K] record written
+    uint8_t* flag;           // [K1] record written, phase-1 instances (binning block; zeroed by the emission)
+    uint8_t* flag2;          // phase-2 instances (binning2 block), local index: flag2[e - E1]; null without phase 2
     uint32_t* order;         // [num_tiles] scratch: tiles in descending replay length (launch order)
     float* zero_base;        // optional: [zero_count] floats zero-filled by the replay waves (gradient outputs)
     size_t zero_count;
@@ -124,7 +127,8 @@ struct GaussBwdArgs {
     const uint32_t* dkey;    // forward depth keys (bits of the view z)
     const float4* sp;        // splat records (conic + AA-scaled opacity)
     float* rec;              // per-instance records; k_gauss_sum overwrites a contributing Gaussian's last one
-    const uint8_t* flag;
+    const uint8_t* flag;     // record written: phase 1 (binning block)
+    const uint8_t* flag2;    // phase 2, local index (binning2 block)
     float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *ddc, *dsh, *dscales, *drot, *depth;
     int outputs_zeroed;      // the nine gradient outputs were zero-filled by k_render_bwd
     // k_gauss_sum walks the instance slots [0, E1 + K2) in chunks of SUM_CHUNK; owner of slot e: eg[e] (phase 1,
@@ -175,6 +179,12 @@ struct BinArgs {
     uint32_t cap;                // capacity of the instance arrays
     uint32_t *first_e, *rcnt;
     uint32_t *eg, *ikey;         // per instance: Gaussian, depth key
+    uint8_t* flag;               // per instance: the backward's record-written flag, zeroed here
+    // phase 2 only: an extra block of the emission launch computes the backward's longest-first replay order (on the
+    // otherwise latency-bound phase-2 tail, instead of a backward prologue launch)
+    uint32_t* order;             // [num_tiles] out (null: not here)
+    const uint32_t* max_contrib; // phase-1 max contributors (final for finished tiles)
+    const uint2* ranges1;        // phase-1 ranges (unfinished tiles: phase-1 + phase-2 list length bounds the replay)
     // colour of the binned Gaussians (computeColorFromSH), written by k_bin_emit
     int D, M;
     const float *means3D, *campos, *dc, *sh, *colors;
@@ -199,8 +209,8 @@ void launch_count_score(int P, const int* radii, const float4* sp, const uint32_
                         hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);
 void launch_filter(const PreArgs& a, hipStream_t s);
-// clears the record flags of the E1 + K2 binned instances and sets counters[CNT_INVD], then replays
-void launch_render_bwd(const RenderBwdArgs& a, uint32_t* counters, hipStream_t s);
+// the replay; order_ready: the forward's phase-2 emission already wrote the replay order, else one block sorts it
+void launch_render_bwd(const RenderBwdArgs& a, uint32_t* counters, hipStream_t s, bool order_ready);
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s);
 
 }  // namespace gs

@@ -71,7 +71,7 @@ template <bool HAS_INVD, bool HAS_BG, bool PER_SPLAT_LAST>
 __device__ __forceinline__ void replay_splat(const RenderBwdArgs& a, const float4* sb, int jj, int sidx, const v4f pxv,
                                              const v2f pyv, const int (&last)[4], const v4f athr, const v4f g0,
                                              const v4f g1, const v4f g2, const v4f gd, const v4f ntb, v4f& T, v4f& S,
-                                             int lane) {
+                                             int lane, uint32_t E1, uint8_t* flag2m) {
     const float4 Sa = sb[jj * 3 + 0], Sb = sb[jj * 3 + 1], Sc = sb[jj * 3 + 2];
     const float sx = Sa.x, sy = Sa.y, so = Sb.y, sr = Sb.z, sg = Sb.w, sbl = Sc.x, si = Sc.y;
     // exponent, identical to the forward's splat_power4
@@ -134,7 +134,7 @@ __device__ __forceinline__ void replay_splat(const RenderBwdArgs& a, const float
         const float tot = wave_reduce10(p, lane, slot);
         const uint32_t e = __builtin_amdgcn_readfirstlane(__float_as_uint(Sc.z));
         if (slot >= 0) a.rec[(size_t)e * 12 + slot] = tot;
-        if (lane == 0) a.flag[e] = 1;
+        if (lane == 0) (e < E1 ? a.flag : flag2m)[e] = 1;  // phase-2 flags: flag2[e - E1]
     }
 }
 
@@ -164,6 +164,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
     if (a.ranges2 && a.unfinished[tile]) rg2 = a.ranges2[tile];
     const int nall = n1 + (int)(rg2.y - rg2.x);
     const uint32_t E1 = a.counters[CNT_E1];
+    uint8_t* const flag2m = a.flag2 ? a.flag2 - E1 : a.flag;
     const int mc = (int)a.max_contrib[tile];
     const int n = nall < mc ? nall : mc;
     if (n <= 0) return;
@@ -277,7 +278,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
                 const int jj = (int)__builtin_ctzll(smask);
                 smask &= smask - 1;
                 replay_splat<HAS_INVD, HAS_BG, false>(a, sb, jj, base + jj, pxv, pyv, last, athr, g0, g1, g2, gd, ntb, T, S,
-                                                       lane);
+                                                       lane, E1, flag2m);
             }
             __builtin_amdgcn_wave_barrier();
             continue;
@@ -287,7 +288,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
             const int jj = (int)__builtin_ctzll(smask);
             smask &= smask - 1;
             replay_splat<HAS_INVD, HAS_BG, true>(a, sb, jj, base + jj, pxv, pyv, last, bc4(1.0f / 255.0f), g0, g1, g2, gd,
-                                                 ntb, T, S, lane);
+                                                 ntb, T, S, lane, E1, flag2m);
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -298,7 +299,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
 // shorter), one load per tile.
 __device__ __forceinline__ uint32_t replay_len(const RenderBwdArgs& a, int tile) { return a.max_contrib[tile]; }
 
-// Longest-first launch order for the replay (tile_order_sort in k_bwd_prologue).  Per tile, not per 4-tile block:
+// Longest-first launch order for the replay (tile_order_sort: the phase-2 emission's extra block, else k_bwd_order).  Per tile, not per 4-tile block:
 // ordering whole blocks by their longest tile measured 6% slower.
 
 #ifdef DG_BWD_WPE  // occupancy experiment: cap VGPRs so that DG_BWD_WPE waves fit per SIMD
@@ -327,7 +328,17 @@ __global__ void __launch_bounds__(256) BWD_WPE_ATTR k_render_bwd(RenderBwdArgs a
     const int tile = a.order ? (int)a.order[slot] : slot;
     float4* sb = &s_b[threadIdx.x >> 6][0][0];
     const bool has_bg = a.bg[0] != 0.0f || a.bg[1] != 0.0f || a.bg[2] != 0.0f;
-    const bool has_invd = a.dL_dinvd != nullptr && a.counters[CNT_INVD] != 0u;
+    // the inverse-depth terms only where this tile has a nonzero dL/dinvdepth: elsewhere they add exact zeros
+    bool invd_nz = false;
+    if (a.dL_dinvd) {
+        const int tx0 = (tile % a.tiles_x) * GS_TILE_X, ty0 = (tile / a.tiles_x) * GS_TILE_Y;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int px = tx0 + (lane & 7) + (k >> 1) * 8, py = ty0 + (lane >> 3) + (k & 1) * 8;
+            if (px < a.W && py < a.H) invd_nz |= a.dL_dinvd[(size_t)py * a.W + px] != 0.0f;
+        }
+    }
+    const bool has_invd = __any(invd_nz);
     if (has_invd) {
         if (has_bg) render_bwd_tile<true, true>(a, tile, lane, sb);
         else render_bwd_tile<true, false>(a, tile, lane, sb);
@@ -337,30 +348,11 @@ __global__ void __launch_bounds__(256) BWD_WPE_ATTR k_render_bwd(RenderBwdArgs a
     }
 }
 
-// Backward prologue, one launch: blocks [0, PRO_BLOCKS) zero the record flags of the E1 + K2 binned instances
-// (device-side count) and set counters[CNT_INVD] = any(dL/dinvdepth != 0), which lets the replay drop the
-// inverse-depth terms; the extra last block (when tile ordering is on) computes the longest-first replay order
-// (tile_order_sort) concurrently, instead of a one-block launch of its own on the critical path.
-constexpr uint32_t PRO_BLOCKS = 128;
-__global__ void __launch_bounds__(1024) k_bwd_prologue(RenderBwdArgs a, uint32_t* __restrict__ counters) {
-    if (blockIdx.x == PRO_BLOCKS) {
-        tile_order_sort(a.num_tiles, a.order, [&](int tile) { return replay_len(a, tile); });
-        return;
-    }
-    uint8_t* flag = a.flag;
-    const uint32_t nflags = min(counters[CNT_E1] + counters[CNT_K2], a.K);
-    const uint32_t stride = PRO_BLOCKS * blockDim.x;
-    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t* f4 = reinterpret_cast<uint32_t*>(flag);  // the flag block is 256-B aligned
-    for (uint32_t i = i0; i < nflags / 4; i += stride) f4[i] = 0u;
-    for (uint32_t i = (nflags & ~3u) + i0; i < nflags; i += stride) flag[i] = 0;
-    if (a.dL_dinvd) {  // one atomic per block at most, skipped once the flag is set (single-address atomics serialize)
-        const uint32_t npix = (uint32_t)a.W * a.H;
-        bool nz = false;
-        for (uint32_t i = i0; i < npix; i += stride) nz |= (a.dL_dinvd[i] != 0.0f);
-        if (__syncthreads_or(nz) && threadIdx.x == 0 && !static_cast<volatile uint32_t*>(counters)[CNT_INVD])
-            atomicOr(counters + CNT_INVD, 1u);
-    }
+// The replay order when the forward did not compute it (no phase 2: its emission launch carries the order block):
+// one 1024-thread block, longest first.  The record flags are zeroed by the forward's emission, and the inverse-depth
+// terms are decided per tile by the replay, so nothing else precedes the replay.
+__global__ void __launch_bounds__(1024) k_bwd_order(RenderBwdArgs a) {
+    tile_order_sort(a.num_tiles, a.order, [&](int tile) { return replay_len(a, tile); });
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -474,7 +466,7 @@ __device__ __forceinline__ void sum_chunk(const GaussBwdArgs& a, uint32_t ch, co
         r0[q] = r1[q] = r2[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (e < R.NR) {
             o[q] = inst_owner(a, e, R.E1);
-            f[q] = a.flag[e] != 0;
+            f[q] = (e < R.E1 ? a.flag[e] : a.flag2[e - R.E1]) != 0;
             const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
             r0[q] = r[0]; r1[q] = r[1]; r2[q] = r[2];
         }
@@ -508,7 +500,7 @@ __device__ __forceinline__ void sum_chunk(const GaussBwdArgs& a, uint32_t ch, co
             float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0, q2 = q0;
             if (e < R.NR) {
                 oo = inst_owner(a, e, R.E1);
-                ff = a.flag[e] != 0;
+                ff = (e < R.E1 ? a.flag[e] : a.flag2[e - R.E1]) != 0;
                 const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
                 q0 = r[0]; q1 = r[1]; q2 = r[2];
                 if (lane == 63 && e + 1 < R.NR) n63 = inst_owner(a, e + 1, R.E1);
@@ -894,10 +886,11 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, co
     }
 }
 
-void launch_render_bwd(const RenderBwdArgs& a, uint32_t* counters, hipStream_t s) {
-    const bool order = a.order && a.num_tiles > 0;
-    k_bwd_prologue<<<PRO_BLOCKS + (order ? 1 : 0), 1024, 0, s>>>(a, counters);
-    if (a.num_tiles > 0) k_render_bwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
+void launch_render_bwd(const RenderBwdArgs& a, uint32_t* counters, hipStream_t s, bool order_ready) {
+    (void)counters;
+    if (a.num_tiles <= 0) return;
+    if (a.order && !order_ready) k_bwd_order<<<1, 1024, 0, s>>>(a);
+    k_render_bwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
 }
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s) {
     if (a.P <= 0) return;

@@ -512,10 +512,21 @@ __global__ void __launch_bounds__(256) k_bin_count(BinArgs a) {
 // order, so every Gaussian's instances are contiguous: [first_e, first_e + rcnt); each instance index is also
 // placed in its tile's list, s_e[ranges[t].x + atomic arrival slot] (counting sort; the order inside a tile is
 // fixed afterwards by k_tile_dsort).
+// The backward's replay order (longest first) from the emission launch of phase 2: the phase-1 max contributor of a
+// finished tile is final; an unfinished tile's replay is bounded by its phase-1 + phase-2 list lengths.
+__device__ __forceinline__ void emit_order_block(const BinArgs& a) {
+    tile_order_sort(a.num_tiles, a.order, [&](int tile) {
+        if (!a.unf[tile]) return a.max_contrib[tile];
+        const uint2 r1 = a.ranges1[tile], r2 = a.ranges[tile];
+        return (r1.y - r1.x) + (r2.y - r2.x);
+    });
+}
+
 template <int PHASE>
 __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
     __shared__ CandLDS s_cand[4];
     __shared__ uint32_t s_key[4][64];
+    if (PHASE == 2 && a.order && blockIdx.x == gridDim.x - 1) { emit_order_block(a); return; }
     if (PHASE == 2 && a.counters[CNT_UNFINISHED] == 0u) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wave = blockIdx.x * 4 + w;
@@ -560,6 +571,7 @@ __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
                             const int t = ty * a.tiles_x + tx;
                             a.eg[e] = (uint32_t)(g0 + owner);
                             a.ikey[e] = s_key[w][owner];
+                            a.flag[e] = 0;
                             a.s_e[a.ranges[t].x + atomicAdd(&a.tile_cnt[t], 1u)] = e;
                         }
                         running += (uint32_t)__popcll(km);
@@ -677,6 +689,7 @@ __global__ void __launch_bounds__(256) k_bin_emit_fat(BinArgs a) {
     __shared__ CandLDS s_cand[4];
     __shared__ uint32_t s_key[4][64];
     __shared__ uint32_t s_g[4][64];
+    if (PHASE == 2 && a.order && blockIdx.x == gridDim.x - 1) { emit_order_block(a); return; }
     if (PHASE == 2 && a.counters[CNT_UNFINISHED] == 0u) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wave = blockIdx.x * 4 + w;
@@ -729,6 +742,7 @@ __global__ void __launch_bounds__(256) k_bin_emit_fat(BinArgs a) {
                                     const int t = ty * a.tiles_x + tx;
                                     a.eg[e] = s_g[w][owner];
                                     a.ikey[e] = s_key[w][owner];
+                                    a.flag[e] = 0;
                                     a.s_e[a.ranges[t].x + atomicAdd(&a.tile_cnt[t], 1u)] = e;
                                 }
                                 run += (uint32_t)__popcll(km);
@@ -1064,7 +1078,8 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
         if (lane == 0) {
             a.unfinished[tile] = unf ? 1 : 0;
             if (unf) {
-                atomicAdd(a.counters + CNT_UNFINISHED, 1u);
+                const uint32_t slot = atomicAdd(a.counters + CNT_UNFINISHED, 1u);
+                if (a.unf_list) a.unf_list[slot] = (uint32_t)tile;
                 a.ranges2_zero[tile] = make_uint2(0u, 0u);  // empty unless phase 2 bins instances for it
                 if (a.unf_rows) {  // row word, column summary, row summary (rows_touch's layout)
                     const int th = (a.num_tiles + a.tiles_x - 1) / a.tiles_x;
@@ -1095,15 +1110,32 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
 // every decision.  Every splat of the list is evaluated (the quadrant test only skips splats no pixel accepts).
 constexpr int FWD2_CHUNK = 1024;
 template <bool COUNT>
+__device__ __forceinline__ void render_fwd2_tile(const RenderArgs& a, int tile, float4* s_sb, uint32_t* s_mx,
+                                                 uint32_t* s_ids);
+constexpr int FWD2_GRID = 1024;  // blocks of the list-walking launch (a 1080p view has 0 to ~1100 unfinished tiles)
+template <bool COUNT>
 __global__ void __launch_bounds__(256) k_render_fwd2(RenderArgs a) {
     __shared__ __attribute__((aligned(16))) float4 s_sb[(FWD2_CHUNK + 4) * 3];  // (also the sort's scratch)
     __shared__ uint32_t s_mx[4];
     __shared__ uint32_t s_ids[DS_WAVE_MAX2];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = blockIdx.x;
     // the adaptive capacity's probe gets this view's phase-2 instance count (the next view's k_depth_cut reads it)
     if (a.probe && blockIdx.x == 0 && threadIdx.x == 0) a.probe[1] = a.counters[CNT_K2];
+    if (a.unf_list) {  // the unfinished tiles phase 1 listed, a block each, grid-stride
+        const uint32_t nu = a.counters[CNT_UNFINISHED];
+        for (uint32_t i = blockIdx.x; i < nu; i += gridDim.x) {
+            render_fwd2_tile<COUNT>(a, (int)a.unf_list[i], s_sb, s_mx, s_ids);
+            __syncthreads();  // s_sb / s_ids are reused by the next tile
+        }
+        return;
+    }
+    const int tile = blockIdx.x;
     if (tile >= a.num_tiles || !a.unfinished[tile]) return;  // block-uniform: finished in phase 1
+    render_fwd2_tile<COUNT>(a, tile, s_sb, s_mx, s_ids);
+}
+template <bool COUNT>
+__device__ __forceinline__ void render_fwd2_tile(const RenderArgs& a, int tile, float4* s_sb, uint32_t* s_mx,
+                                                 uint32_t* s_ids) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
     const int px = tx * GS_TILE_X + (lane & 15), py = ty * GS_TILE_Y + 4 * w + (lane >> 4);
     const bool inside = px < a.W && py < a.H;
@@ -1454,10 +1486,11 @@ void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hi
         exclusive_scan(a.wtot, (uint32_t)waves, a.wtot, total, scan_tmp, s, gate);
         tile_offsets(a.tile_cnt, (uint32_t)a.num_tiles, a.ranges, s, gate);
     }
+    const int eblocks = blocks + (phase == 2 && a.order ? 1 : 0);  // + the replay-order block
     if (fat) {
-        if (phase == 2) k_bin_emit_fat<2><<<blocks, 256, 0, s>>>(a);
+        if (phase == 2) k_bin_emit_fat<2><<<eblocks, 256, 0, s>>>(a);
         else k_bin_emit_fat<1><<<blocks, 256, 0, s>>>(a);
-    } else if (phase == 2) k_bin_emit<2><<<blocks, 256, 0, s>>>(a);
+    } else if (phase == 2) k_bin_emit<2><<<eblocks, 256, 0, s>>>(a);
     else k_bin_emit<1><<<blocks, 256, 0, s>>>(a);
 }
 size_t bin_scan_temp_bytes(int P) { return scan_temp_bytes((uint32_t)((P + EMIT_RANKS - 1) / EMIT_RANKS)); }
@@ -1476,8 +1509,9 @@ void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
         if (a.gcount) k_render_fwd2x<true><<<a.num_tiles, 1024, 0, s>>>(a);
         else k_render_fwd2x<false><<<a.num_tiles, 1024, 0, s>>>(a);
 #else
-        if (a.gcount) k_render_fwd2<true><<<a.num_tiles, 256, 0, s>>>(a);
-        else k_render_fwd2<false><<<a.num_tiles, 256, 0, s>>>(a);
+        const int g2 = a.unf_list ? (a.num_tiles < FWD2_GRID ? a.num_tiles : FWD2_GRID) : a.num_tiles;
+        if (a.gcount) k_render_fwd2<true><<<g2, 256, 0, s>>>(a);
+        else k_render_fwd2<false><<<g2, 256, 0, s>>>(a);
 #endif
         return;
     }

@@ -495,10 +495,46 @@ __global__ void __launch_bounds__(256) k_tile_dsort_long(DSortArgs a) {
         block_sort_long(a, (int)a.long_list[li], s_base, s_wh, s_red, &s_tie);
 }
 
+// The lists longer than the render's fused sort (n > DS_WAVE_MAX) in ONE launch of few blocks: block b scans the
+// ranges of tiles [64 b, 64 b + 64) (16 per wave), each wave sorts the lists it finds up to DS_WAVE_MAX2 itself
+// and queues longer ones in the block's LDS; after a barrier the block sorts its queue (block_sort_long).  A 1080p
+// view has a handful of such lists, so this replaces a 2040-block launch that mostly exits plus a 256-block
+// grid-stride launch: the same two sort routines, so the same order.
+constexpr int DSM_TILES = 64;
+__global__ void __launch_bounds__(256) k_tile_dsort_merged(DSortArgs a) {
+    __shared__ uint32_t s_cnt[4][RS_RADIX];
+    __shared__ uint32_t s_k[4][DS_WAVE_MAX2];
+    __shared__ uint32_t s_v[4][DS_WAVE_MAX2];
+    __shared__ uint32_t s_q[DSM_TILES];
+    __shared__ uint32_t s_nq;
+    __shared__ int s_tie;
+    if (a.gate && *a.gate == 0u) return;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (threadIdx.x == 0) s_nq = 0u;
+    __syncthreads();
+    const int t0 = blockIdx.x * DSM_TILES + w * (DSM_TILES / 4);
+    for (int i = 0; i < DSM_TILES / 4; i++) {
+        const int tile = t0 + i;
+        if (tile >= a.num_tiles) break;
+        const int n = wave_sort_tile<DS_ROWS2>(a, tile, lane, s_cnt[w], s_k[w], s_v[w], nullptr, DS_WAVE_MAX);
+        if (n > DS_WAVE_MAX2 && lane == 0) s_q[atomicAdd(&s_nq, 1u)] = (uint32_t)tile;
+    }
+    __syncthreads();
+    const uint32_t nq = s_nq;
+    uint32_t* scr = &s_k[0][0];  // the wave sorts are done: their scratch serves the block sort
+    for (uint32_t q = 0; q < nq; q++)
+        block_sort_long(a, (int)s_q[q], scr, reinterpret_cast<uint32_t(*)[BS_RADIX]>(scr + BS_RADIX),
+                        reinterpret_cast<uint32_t(*)[BS_WAVES]>(scr + BS_RADIX * (1 + BS_WAVES)), &s_tie);
+}
+
 void tile_depth_sort_long_only(const DSortArgs& a, hipStream_t stream) {
     if (a.num_tiles <= 0) return;
+#ifdef DG_DSORT_TWO_LAUNCHES
     k_tile_dsort<DS_WAVE_MAX><<<(a.num_tiles + 3) / 4, 256, 0, stream>>>(a);
     k_tile_dsort_long<<<256, 256, 0, stream>>>(a);
+#else
+    k_tile_dsort_merged<<<(a.num_tiles + DSM_TILES - 1) / DSM_TILES, 256, 0, stream>>>(a);
+#endif
 }
 
 void tile_depth_sort(const DSortArgs& a, hipStream_t stream) {
