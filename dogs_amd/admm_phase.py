@@ -21,8 +21,8 @@ Here every rank runs the entry for its own block ("one block per GPU"):
     * the expanded-box split, visibility_count and the rank's sub-model follow locally.
 The importance of a Gaussian is therefore sum_b (sum over block b's cameras, last camera first) instead of one sum
 over the concatenated camera list (prune_list pops the whole list from the end): the same terms, associated per block,
-a float rounding difference only (the counts are integers and exact).  `SequentialPhase` (tests) restates it in one
-process with the same association.
+a float rounding difference only (the counts are integers and exact).  `enter_admm_phase_sequential` restates it in one
+process with the same association (the reference's single-process order per block; the tests compare the two).
 
 The device work goes through `PhaseKernels` (HIP: dg_rasterize_count, dg_points_in_boxes2d, dg_prune_select +
 dg_densify_gather); the CPU tests substitute restatements of the same three operations to check the distributed

@@ -45,9 +45,9 @@ __device__ __forceinline__ float hconv11(float x) {
 }
 
 struct StripPos { int x, y0, plane; bool valid; };
-__device__ __forceinline__ StripPos strip_of(int H, int W, int planes) {
+__device__ __forceinline__ StripPos strip_of(int H, int W, int planes, uint32_t skip_blocks = 0) {
     const int sxn = (W + SSW_OUT - 1) / SSW_OUT, syn = (H + SSW_ROWS - 1) / SSW_ROWS;
-    const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int wid = (int)(blockIdx.x - skip_blocks) * 4 + (threadIdx.x >> 6);
     StripPos p;
     p.valid = wid < sxn * syn * planes;
     const int sx = wid % sxn, sy = (wid / sxn) % syn;
@@ -181,6 +181,26 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
     }
 }
 
+// The step's loss (k_loss_final's arithmetic, 256 threads): each total strided per thread, then the 4 wave sums in order.
+__device__ __forceinline__ void loss_final_block(const LossFinal& f) {
+    __shared__ float s_w[3][4];
+    const float* ps[3] = {f.p_l1, f.p_ssim, f.p_sc};
+    const uint32_t ns[3] = {f.n_l1, f.n_ssim, f.n_sc};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        float acc = 0.0f;
+        for (uint32_t i = threadIdx.x; i < ns[k]; i += 256) acc += ps[k][i];
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if ((threadIdx.x & 63) == 0) s_w[k][threadIdx.x >> 6] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const int k = threadIdx.x;
+        const float acc = (s_w[k][0] + s_w[k][1]) + (s_w[k][2] + s_w[k][3]);
+        f.loss[k] = acc / (float)(k == 2 ? f.P : f.n_img);
+    }
+}
+
 // FUSED (the native training step): img1 is the clamped image, raw the render before the clamp, and the output is
 // the gradient w.r.t. the raw render of (1 - ld) L1 + ld (1 - SSIM): (dSSIM + g_l1 sgn(img1 - img2) / n) where the
 // render lies in [0, 1], else 0 -- k_clamp_l1_bwd's expression in the same pass.
@@ -190,8 +210,10 @@ __global__ void __launch_bounds__(256) k_ssim_bwd_strip(int H, int W, int planes
                                                         float dl_value, const float* __restrict__ dmu1,
                                                         const float* __restrict__ ds1, const float* __restrict__ ds12,
                                                         float* __restrict__ dimg1, const float* __restrict__ raw = nullptr,
-                                                        float l1_scale = 0.0f) {
-    const StripPos sp = strip_of(H, W, planes);
+                                                        float l1_scale = 0.0f, LossFinal lf = {}, uint32_t lblk = 0) {
+    // lblk = 1: block 0 computes the step's loss (dispatched first, beside the strips), the strips follow
+    if (lblk && blockIdx.x == 0) { loss_final_block(lf); return; }
+    const StripPos sp = strip_of(H, W, planes, lblk);
     if (!sp.valid) return;
     const int lane = threadIdx.x & 63;
     const size_t plane = (size_t)sp.plane * H * W;
@@ -256,6 +278,9 @@ static unsigned ssim_strip_blocks(int planes, int H, int W) {
     const long waves = (long)((W + SSW_OUT - 1) / SSW_OUT) * ((H + SSW_ROWS - 1) / SSW_ROWS) * planes;
     return (unsigned)((waves + 3) / 4);
 }
+uint32_t ssim_waves(int planes, int H, int W) {
+    return (uint32_t)(((W + SSW_OUT - 1) / SSW_OUT) * ((H + SSW_ROWS - 1) / SSW_ROWS) * planes);
+}
 
 void launch_ssim_fwd(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2, float* map,
                      float* dmu1, float* ds1, float* ds12, hipStream_t s) {
@@ -264,31 +289,29 @@ void launch_ssim_fwd(int B, int CH, int H, int W, float C1, float C2, const floa
     if (dmu1)
         k_ssim_fwd_strip<true><<<blocks, 256, 0, s>>>(H, W, B * CH, C1, C2, img1, img2, map, dmu1, ds1, ds12);
     else
-        k_ssim_fwd_strip<false><<<blocks, 256, 0, s>>>(H, W, B * CH, C1, C2, img1, img2, map, nullptr, nullptr,
-                                                        nullptr);
+        k_ssim_fwd_strip<false><<<blocks, 256, 0, s>>>(H, W, B * CH, C1, C2, img1, img2, map, nullptr, nullptr, nullptr);
 }
 void launch_ssim_bwd(int B, int CH, int H, int W, const float* img1, const float* img2, const float* dL,
                      const float* dmu1, const float* ds1, const float* ds12, float* dimg1, hipStream_t s,
                      float dl_value) {
     if ((size_t)B * CH * H * W == 0) return;
-    k_ssim_bwd_strip<false><<<ssim_strip_blocks(B * CH, H, W), 256, 0, s>>>(H, W, B * CH, img1, img2, dL, dl_value,
-                                                                             dmu1, ds1, ds12, dimg1);
-}
-uint32_t ssim_waves(int planes, int H, int W) {
-    return (uint32_t)(((W + SSW_OUT - 1) / SSW_OUT) * ((H + SSW_ROWS - 1) / SSW_ROWS) * planes);
+    k_ssim_bwd_strip<false><<<ssim_strip_blocks(B * CH, H, W), 256, 0, s>>>(H, W, B * CH, img1, img2, dL, dl_value, dmu1,
+                                                                        ds1, ds12, dimg1);
 }
 void launch_ssim_fwd_fused(int H, int W, float C1, float C2, const float* raw, const float* gt, float* clamped,
                            float* dmu1, float* ds1, float* ds12, float* part, hipStream_t s) {
     if ((size_t)H * W == 0) return;
-    k_ssim_fwd_strip<true, true><<<ssim_strip_blocks(3, H, W), 256, 0, s>>>(H, W, 3, C1, C2, raw, gt, nullptr, dmu1,
-                                                                             ds1, ds12, clamped, part);
+    k_ssim_fwd_strip<true, true><<<ssim_strip_blocks(3, H, W), 256, 0, s>>>(H, W, 3, C1, C2, raw, gt, nullptr, dmu1, ds1,
+                                                                        ds12, clamped, part);
 }
 void launch_ssim_bwd_fused(int H, int W, const float* clamped, const float* gt, const float* raw, float dl_value,
                            float l1_scale, const float* dmu1, const float* ds1, const float* ds12, float* d_raw,
-                           hipStream_t s) {
+                           hipStream_t s, const LossFinal* lf) {
     if ((size_t)H * W == 0) return;
-    k_ssim_bwd_strip<true><<<ssim_strip_blocks(3, H, W), 256, 0, s>>>(H, W, 3, clamped, gt, nullptr, dl_value, dmu1,
-                                                                       ds1, ds12, d_raw, raw, l1_scale);
+    const uint32_t lb = lf ? 1u : 0u;
+    k_ssim_bwd_strip<true><<<ssim_strip_blocks(3, H, W) + lb, 256, 0, s>>>(H, W, 3, clamped, gt, nullptr, dl_value, dmu1,
+                                                                          ds1, ds12, d_raw, raw, l1_scale,
+                                                                          lf ? *lf : LossFinal{}, lb);
 }
 
 // ------------------------------------------------------------------------------------------------

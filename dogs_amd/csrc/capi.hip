@@ -10,6 +10,7 @@
 #include <vector>
 #include <map>
 #include <tuple>
+#include <chrono>
 #include <mutex>
 
 #include "../../include/dogs_hip.h"
@@ -202,7 +203,6 @@ gs::BinArgs bin_args(const dg_raster_args* r, const Geom& g, const Image& im, in
     a.P = P; a.tiles_x = tx; a.num_tiles = T; a.dkey = g.dkey; a.sp = g.sp; a.counters = g.counters;
     a.unf = im.unfinished; a.sat = im.sat; a.wtot = g.wtot; a.wmask = g.wmask; a.mlist = g.mlist; a.cap = cap; a.first_e = g.first_e; a.rcnt = g.rcnt;
     a.eg = b.eg; a.ikey = b.ik; a.flag = b.flag; a.tile_cnt = tile_cnt; a.ranges = ranges; a.s_e = b.se;
-    a.order = nullptr; a.max_contrib = nullptr; a.ranges1 = nullptr;
     a.unf_rows = nullptr; a.unf_rw = 0; a.unf_th = 0; a.probe = nullptr;
     return a;
 }
@@ -225,8 +225,10 @@ constexpr bool FUSED_SORT = true;
 // thread's slot goes back to a process-wide pool when the thread exits (ADMM worker and RPC threads come and go), so
 // the pinned buffers and events are bounded by the number of threads alive at once.
 struct HostCounters {
-    uint32_t* buf = nullptr;
+    uint32_t* buf = nullptr;  // [0, 16) the counters, [16] the sequence word of the polled path
+    uint32_t* dev = nullptr;  // buf as the device addresses it (null: copy with hipMemcpyAsync + event instead)
     hipEvent_t ev = nullptr;
+    uint32_t seq = 0;
 };
 // The pool and its mutex are allocated once and never freed: a thread that exits during interpreter teardown (after
 // the static destructors ran) still finds them alive.
@@ -252,11 +254,35 @@ HostCounters& host_counters() {
             }
         }
         if (!slot.h.buf) {
-            (void)hipHostMalloc((void**)&slot.h.buf, 64 * sizeof(uint32_t), hipHostMallocDefault);
+            // coherent (fine-grained): the device's system-scope stores reach host memory without a cache flush
+            if (hipHostMalloc((void**)&slot.h.buf, 64 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+                hipSuccess) {
+                slot.h.buf = nullptr;
+                (void)hipHostMalloc((void**)&slot.h.buf, 64 * sizeof(uint32_t), hipHostMallocDefault);
+                slot.h.dev = nullptr;
+            }
+            else if (hipHostGetDevicePointer((void**)&slot.h.dev, slot.h.buf, 0) != hipSuccess)
+                slot.h.dev = nullptr;
             (void)hipEventCreateWithFlags(&slot.h.ev, hipEventDisableTiming);
         }
     }
     return slot.h;
+}
+
+// Spin on the sequence word the long-list sort launch writes after the counters (no event: an event record is a
+// barrier packet, ~6 us of idle GPU per view).  A fault or a stall ends the spin after 2 s: the stream's error, if any,
+// is reported, else the word is re-read once the stream has drained.
+int wait_seq(HostCounters& h, hipStream_t s) {
+    volatile uint32_t* w = h.buf + 16;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t it = 0;; it++) {
+        if (__atomic_load_n(const_cast<uint32_t*>(w), __ATOMIC_ACQUIRE) == h.seq) return 0;
+        __builtin_ia32_pause();
+        if ((it & 4095u) == 4095u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+    }
+    HIP_OK(hipStreamSynchronize(s));
+    if (__atomic_load_n(const_cast<uint32_t*>(w), __ATOMIC_ACQUIRE) == h.seq) return 0;
+    return fail("forward: the counter read-back never arrived%s%d");
 }
 
 // Phase-1 binning capacity, in tile-rect area units (the depth cut bounds the precise instances by the rect areas):
@@ -515,14 +541,13 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     if (P == 0) HIP_OK(hipMemsetAsync(g.hist, 0, gs::DH_BINS * sizeof(uint32_t), s));  // no preprocess to zero it
     {
         PROF("prefix_cut");
-        gs::launch_depth_hist(P, g.dkey, g.cnt, g.hist, s);
         if (prefix_enabled(a)) {
             C1 = phase1_cap(a, T, ac);
-            gs::launch_depth_cut(g.hist, (uint32_t)C1, g.counters, im.tile_cnt, im.tile_cnt2, (uint32_t)T,
-                                 pre.rect_part, nparts, ac ? ac->probe : nullptr, s);
+            gs::launch_depth_hist_cut(P, g.dkey, g.cnt, g.hist, (uint32_t)C1, g.counters, im.tile_cnt, im.tile_cnt2,
+                                      (uint32_t)T, pre.rect_part, nparts, ac ? ac->probe : nullptr, s);
         } else {  // everything in one phase: the capacity is the total rect area itself (one early sync)
-            gs::launch_depth_cut(g.hist, 0xffffffffu, g.counters, im.tile_cnt, im.tile_cnt2, (uint32_t)T,
-                                 pre.rect_part, nparts, nullptr, s);
+            gs::launch_depth_hist_cut(P, g.dkey, g.cnt, g.hist, 0xffffffffu, g.counters, im.tile_cnt, im.tile_cnt2,
+                                      (uint32_t)T, pre.rect_part, nparts, nullptr, s);
             uint32_t k = 0;
             HIP_OK(hipMemcpyAsync(&k, g.counters + gs::CNT_K, 4, hipMemcpyDeviceToHost, s));
             HIP_OK(hipStreamSynchronize(s));
@@ -544,10 +569,19 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     // the host's only wait is on this early copy (num_rendered, E1, error flag, cut), and it happens after all of
     // phase 1 is queued, so the GPU never idles on it
     HostCounters& hcs = host_counters();
-    HIP_OK(hipMemcpyAsync(hcs.buf, g.counters, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_OK(hipEventRecord(hcs.ev, s));
     const gs::DSortArgs ds1 = dsort_args(b, C1, T, im.ranges, nullptr, nullptr, im.long_tiles,
                                          g.counters + gs::CNT_LONG);
+    // the phase-1 render lands the counters in the pinned buffer itself (no copy launch, no event: ~6-10 us of idle
+    // GPU per view); without a device-addressable buffer, a copy and an event
+#ifdef DG_HC_MEMCPY  // A/B switch: the copy launch
+    const bool kcopy = false;
+#else
+    const bool kcopy = hcs.dev != nullptr && T > 0;
+#endif
+    if (!kcopy) {
+        HIP_OK(hipMemcpyAsync(hcs.buf, g.counters, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIP_OK(hipEventRecord(hcs.ev, s));
+    }
     const bool fuse = FUSED_SORT && C1 > 0 && P > 0;
     if (C1 > 0 && P > 0) {
         // the lists longer than a wave's capacity here; the render sorts the others tile by tile (fused)
@@ -571,11 +605,16 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     r.gcount = gcount;
     r.fuse_sort = fuse ? 1 : 0;
     r.ds = ds1;
+    if (kcopy) { r.hc_src = g.counters; r.hc_dst = hcs.dev; r.hc_seq = ++hcs.seq; }
     if (gcount && P > 0) HIP_OK(hipMemsetAsync(gcount, 0, sizeof(uint32_t) * (size_t)P, s));
     { PROF("render_fwd"); gs::launch_render_fwd(r, s); }
     DBG_SYNC(a->debug, s);
 
-    HIP_OK(hipEventSynchronize(hcs.ev));
+    if (kcopy) {
+        if (wait_seq(hcs, s)) return 1;
+    } else {
+        HIP_OK(hipEventSynchronize(hcs.ev));
+    }
     const uint32_t* hc = hcs.buf;
     adapt(ac, hc[gs::CNT_PREV_UNF], hc[gs::CNT_PREV_K2], hc[gs::CNT_E1]);
     if (hc[gs::CNT_ERR]) return fail("a Gaussian was filtered although prefiltered is set%s%d");
@@ -606,7 +645,6 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
         ba.unf_rows = UNF_ROWS ? reinterpret_cast<const unsigned long long*>(im.sat) : nullptr;
         ba.unf_rw = unf_rw_of(tx); ba.unf_th = ty;
         ba.probe = UNF_ROWS && ac ? ac->probe : nullptr;
-        ba.order = im.order; ba.max_contrib = im.max_contrib; ba.ranges1 = im.ranges;
         gs::launch_bin(2, ba, g.counters + gs::CNT_K2, g.scan_tmp, s);
         const gs::DSortArgs ds2 = dsort_args(b2, K, T, im.ranges2, im.unfinished, gate, im.long_tiles,
                                              g.counters + gs::CNT_LONG2);
@@ -622,6 +660,7 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
         r2.K = (uint32_t)K;
         r2.ranges = im.ranges2; r2.ranges1 = im.ranges; r2.s_e = b2.se; r2.eg = b2.eg;
         r2.probe = ac ? ac->probe : nullptr;
+        r2.order = im.order;
         gs::launch_render_fwd(r2, s);
     }
     DBG_SYNC(a->debug, s);
@@ -723,7 +762,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
         r.final_T = im.final_T; r.img_color = im.img_color; r.img_invd = im.img_invd; r.n_contrib = im.n_contrib;
         r.dL_dpix = dL_dout_color; r.dL_dinvd = dL_dout_invdepth; r.rec = sc.rec; r.flag = b.flag; r.flag2 = flag2;
         r.order = im.order;
-        { PROF("render_bwd"); gs::launch_render_bwd(r, g.counters, s, binning2 != nullptr); }
+        { PROF("render_bwd"); gs::launch_render_bwd(r, g.counters, s, binning2 != nullptr && gs::render_fwd2_orders()); }
         DBG_SYNC(a->debug, s);
     }
     gs::GaussBwdArgs q;
@@ -838,7 +877,8 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     const uint32_t nb_l1 = gs::clamp_l1_blocks((uint32_t)n_img);
     const uint32_t nb_map = gs::block_sum_blocks((uint32_t)n_img), nb_sc = gs::block_sum_blocks((uint32_t)P);
     const uint32_t nw_ssim = gs::ssim_waves(3, H, W);  // the fused SSIM's partials: nw L1, then nw map
-    const uint32_t n_part = (nb_l1 + nb_map > 2 * nw_ssim ? nb_l1 + nb_map : 2 * nw_ssim) + nb_sc;
+    const uint32_t nb_act = gs::activate_blocks((uint32_t)P);  // the fused route's regulariser partials
+    const uint32_t n_part = (nb_l1 + nb_map > 2 * nw_ssim ? nb_l1 + nb_map : 2 * nw_ssim) + (nb_sc > nb_act ? nb_sc : nb_act);
     // ---- the step's scratch (DG_BUF_TRAIN); the nine rasterizer gradients back to back (the replay zero-fills them)
     const size_t n9 = (3 + 3 + 1 + 3 + 6 + 3 + 3 * Mz + 3 + 4) * Pz;
     auto carve = [&](void* base, float** f) {
@@ -874,8 +914,17 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     float* drot = dscales + 3 * Pz;
     float *depth = f[12], *g_o = f[13], *g_s = f[14], *g_q = f[15];
     const dg_adam_group* G = a->groups;  // xyz, f_dc, f_rest, opacity, scaling, quaternion
+    // Default route: the activations' backward is folded into the update (gmode), and the 4-float chunks that touch
+    // no binned row (rcnt == 0: rasterizer gradient exactly zero) skip reading the gradient buffers; the regulariser's
+    // partial sums come from the activation launch and the loss from block 0 of the SSIM backward.  Same arithmetic
+    // per element as the unfused route (DG_TRAIN_UNFUSED=1: k_activate_bwd, then the plain update; separate loss
+    // launches).  (Running the update of those rows on a side stream, overlapping the backward, was measured and
+    // dropped: DESIGN.md §8.)
+    const bool unfused = getenv("DG_TRAIN_UNFUSED") != nullptr;
+    float* const p_sc_fused = part + 2 * nw_ssim;
     // ---- forward: activations, rasterizer, clamp + L1, SSIM
-    gs::launch_activate_fwd((uint32_t)P, G[3].param, G[4].param, G[5].param, act_o, act_s, act_q, s);
+    gs::launch_activate_fwd((uint32_t)P, G[3].param, G[4].param, G[5].param, act_o, act_s, act_q, s,
+                            !unfused && a->loss ? p_sc_fused : nullptr);
     dg_raster_args r = a->view;
     r.means3D = G[0].param; r.dc = G[1].param; r.sh = M > 0 ? G[2].param : nullptr;
     r.opacities = act_o; r.scales = act_s; r.rotations = act_q; r.colors = nullptr; r.cov3D_precomp = nullptr;
@@ -885,11 +934,6 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
                              &num_rendered, &num_instances, stream))
         return 1;
     // ---- SparseGaussianAdam.step(radii > 0) over the six groups, ADMM proximal gradient, densification statistics.
-    // Default route: the activations' backward is folded into the update (gmode), and the 4-float chunks that touch
-    // no binned row (rcnt == 0: rasterizer gradient exactly zero) skip reading the gradient buffers.  Same arithmetic
-    // per element as the unfused route (DG_TRAIN_UNFUSED=1: k_activate_bwd, then the plain update).  (Running the
-    // update of those rows on a side stream, overlapping the backward, was measured and dropped: DESIGN.md §8.)
-    const bool unfused = getenv("DG_TRAIN_UNFUSED") != nullptr;
     dg_adam_group groups[6];
     const float* grads[6] = {dmeans3D, ddc, dsh, unfused ? g_o : dopac, unfused ? g_s : dscales,
                              unfused ? g_q : drot};
@@ -934,15 +978,11 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     const float g_l1 = (float)(1.0 - (double)ld);
     // loss backward of (1 - ld) L1 + ld (1 - SSIM) + ls mean(prod(scaling)): d/dmap = -ld / n (the mean's backward)
     if (!unfused) {  // render()'s clamp, L1 and the SSIM mean inside the SSIM passes (same values per pixel)
-        float* const p_sc = part + 2 * nw_ssim;
         gs::launch_ssim_fwd_fused(H, W, C1, C2, color, a->gt, a->image, dmu1, ds1, ds12, part, s);
-        if (a->loss) {
-            gs::launch_block_sum(act_s, (uint32_t)P, 1, p_sc, s);
-            gs::launch_loss_final(part, nw_ssim, part + nw_ssim, nw_ssim, p_sc, nb_sc, (uint32_t)n_img, (uint32_t)P,
-                                  a->loss, s);
-        }
+        const gs::LossFinal lf = {part, part + nw_ssim, p_sc_fused, nw_ssim, nw_ssim, nb_act, (uint32_t)n_img,
+                                  (uint32_t)P, a->loss};
         gs::launch_ssim_bwd_fused(H, W, a->image, a->gt, color, (-ld) / (float)n_img, g_l1 / (float)n_img, dmu1, ds1,
-                                  ds12, dimg, s);
+                                  ds12, dimg, s, a->loss ? &lf : nullptr);
     } else {
         gs::launch_clamp_l1_fwd((uint32_t)n_img, color, a->gt, a->image, part, s);
         gs::launch_ssim_fwd(1, 3, H, W, C1, C2, a->image, a->gt, map, dmu1, ds1, ds12, s);
@@ -962,7 +1002,9 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     if (unfused)
         gs::launch_activate_bwd((uint32_t)P, act_o, act_s, G[5].param, dopac, dscales, drot, g_o, g_s, g_q, s,
                                 a->lambda_scale / (float)P);
+#ifndef DG_DIAG_NO_ADAM  // timing diagnostic only (no parameter update): what the update costs the next step's forward
     gs::launch_adam_multi(m, s);
+#endif
     HIP_OK(hipGetLastError());
     return 0;
 }

@@ -88,6 +88,13 @@ struct RenderArgs {
     uint32_t* probe;            // optional (phase 2, adaptive capacity): [1] <- counters[CNT_K2]
     unsigned long long* unf_rows;  // phase 1: bit tx % 64 of word ty * unf_rw + tx / 64 set for each unfinished tile
     int unf_rw;
+    uint32_t* order;            // phase 2 (k_render_fwd2, optional): out, the backward's replay order (an extra block)
+    // phase 1 (optional): block 0 copies hc_src[0..16) to hc_dst[0..16), a coherent pinned host buffer, then sets
+    // hc_dst[16] = hc_seq; the host spins on that word (the forward's early counter read without a copy launch or an
+    // event; the PCIe round trip hides inside the render)
+    const uint32_t* hc_src;
+    uint32_t* hc_dst;
+    uint32_t hc_seq;
 };
 
 struct RenderBwdArgs {
@@ -160,6 +167,10 @@ void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_
 void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, uint32_t* tile_cnt, uint32_t* tile_cnt2,
                       uint32_t num_tiles, const unsigned long long* rect_part, uint32_t nparts, uint32_t* probe,
                       hipStream_t s);
+// launch_depth_hist + launch_depth_cut
+void launch_depth_hist_cut(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_t* hist, uint32_t cap,
+                           uint32_t* counters, uint32_t* tile_cnt, uint32_t* tile_cnt2, uint32_t num_tiles,
+                           const unsigned long long* rect_part, uint32_t nparts, uint32_t* probe, hipStream_t s);
 // Binning walk of one phase (phase 1: Gaussians with key < counters[CNT_THR]; phase 2: those past it, only instances
 // in tiles phase 1 left unfinished): k_bin_count (precise cull walk -> rcnt, per-wave totals, per-tile counts),
 // exclusive scan of the wave totals (*total = the phase's instance count), per-tile ranges, k_bin_emit (first_e;
@@ -182,9 +193,6 @@ struct BinArgs {
     uint8_t* flag;               // per instance: the backward's record-written flag, zeroed here
     // phase 2 only: an extra block of the emission launch computes the backward's longest-first replay order (on the
     // otherwise latency-bound phase-2 tail, instead of a backward prologue launch)
-    uint32_t* order;             // [num_tiles] out (null: not here)
-    const uint32_t* max_contrib; // phase-1 max contributors (final for finished tiles)
-    const uint2* ranges1;        // phase-1 ranges (unfinished tiles: phase-1 + phase-2 list length bounds the replay)
     // colour of the binned Gaussians (computeColorFromSH), written by k_bin_emit
     int D, M;
     const float *means3D, *campos, *dc, *sh, *colors;
@@ -204,6 +212,7 @@ int bin_waves(int P);
 void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, int tiles_x, int tiles_y,
                            uint32_t* sat, hipStream_t s, uint32_t* probe = nullptr);
 void launch_render_fwd(const RenderArgs& a, hipStream_t s);
+bool render_fwd2_orders();
 // count mode: score[i] = gcount[i] x the (AA-scaled) opacity of splat record i (0 when culled)
 void launch_count_score(int P, const int* radii, const float4* sp, const uint32_t* gcount, float* score,
                         hipStream_t s);

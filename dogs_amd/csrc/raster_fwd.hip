@@ -291,11 +291,24 @@ __global__ void __launch_bounds__(DH_THREADS) k_depth_hist(int P, const uint32_t
 // One block: K = total rect area, and the largest bin prefix [0, b] whose rect areas fit `cap`; thr = the first
 // key of bin b + 1 (S = {key < thr}).  No cut (thr = all visible) when K <= cap.  Also resets the per-view
 // counters and the per-tile counters of both binning phases.
+__device__ __forceinline__ void depth_cut_block(const uint32_t* __restrict__ hist, uint32_t cap,
+                                                uint32_t* __restrict__ counters, uint32_t* __restrict__ tile_cnt,
+                                                uint32_t* __restrict__ tile_cnt2, uint32_t num_tiles,
+                                                const unsigned long long* __restrict__ rect_part, uint32_t nparts,
+                                                uint32_t* __restrict__ probe);
 __global__ void __launch_bounds__(1024) k_depth_cut(const uint32_t* __restrict__ hist, uint32_t cap,
                                                     uint32_t* __restrict__ counters, uint32_t* __restrict__ tile_cnt,
                                                     uint32_t* __restrict__ tile_cnt2, uint32_t num_tiles,
                                                     const unsigned long long* __restrict__ rect_part,
                                                     uint32_t nparts, uint32_t* __restrict__ probe) {
+    depth_cut_block(hist, cap, counters, tile_cnt, tile_cnt2, num_tiles, rect_part, nparts, probe);
+}
+
+__device__ __forceinline__ void depth_cut_block(const uint32_t* __restrict__ hist, uint32_t cap,
+                                                uint32_t* __restrict__ counters, uint32_t* __restrict__ tile_cnt,
+                                                uint32_t* __restrict__ tile_cnt2, uint32_t num_tiles,
+                                                const unsigned long long* __restrict__ rect_part, uint32_t nparts,
+                                                uint32_t* __restrict__ probe) {
     __shared__ uint32_t s_w[16];
     __shared__ int s_best;
     __shared__ unsigned long long s_rect[16];
@@ -321,7 +334,10 @@ __global__ void __launch_bounds__(1024) k_depth_cut(const uint32_t* __restrict__
     if (t == 0) s_best = -1;
     uint32_t v[PER], loc = 0;
 #pragma unroll
-    for (int k = 0; k < PER; k++) { v[k] = hist[t * PER + k]; loc += v[k]; }
+    for (int k = 0; k < PER; k++) {
+        v[k] = hist[t * PER + k];
+        loc += v[k];
+    }
     uint32_t x = loc;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -512,21 +528,10 @@ __global__ void __launch_bounds__(256) k_bin_count(BinArgs a) {
 // order, so every Gaussian's instances are contiguous: [first_e, first_e + rcnt); each instance index is also
 // placed in its tile's list, s_e[ranges[t].x + atomic arrival slot] (counting sort; the order inside a tile is
 // fixed afterwards by k_tile_dsort).
-// The backward's replay order (longest first) from the emission launch of phase 2: the phase-1 max contributor of a
-// finished tile is final; an unfinished tile's replay is bounded by its phase-1 + phase-2 list lengths.
-__device__ __forceinline__ void emit_order_block(const BinArgs& a) {
-    tile_order_sort(a.num_tiles, a.order, [&](int tile) {
-        if (!a.unf[tile]) return a.max_contrib[tile];
-        const uint2 r1 = a.ranges1[tile], r2 = a.ranges[tile];
-        return (r1.y - r1.x) + (r2.y - r2.x);
-    });
-}
-
 template <int PHASE>
 __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
     __shared__ CandLDS s_cand[4];
     __shared__ uint32_t s_key[4][64];
-    if (PHASE == 2 && a.order && blockIdx.x == gridDim.x - 1) { emit_order_block(a); return; }
     if (PHASE == 2 && a.counters[CNT_UNFINISHED] == 0u) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wave = blockIdx.x * 4 + w;
@@ -689,7 +694,6 @@ __global__ void __launch_bounds__(256) k_bin_emit_fat(BinArgs a) {
     __shared__ CandLDS s_cand[4];
     __shared__ uint32_t s_key[4][64];
     __shared__ uint32_t s_g[4][64];
-    if (PHASE == 2 && a.order && blockIdx.x == gridDim.x - 1) { emit_order_block(a); return; }
     if (PHASE == 2 && a.counters[CNT_UNFINISHED] == 0u) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wave = blockIdx.x * 4 + w;
@@ -837,6 +841,13 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
     constexpr int WAVE_LDS = 780 + DS_WAVE_MAX;
     __shared__ __attribute__((aligned(16))) uint32_t s_raw[4][WAVE_LDS];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the counters the host waits for are final (written by the launches before this one): system-scope stores to the
+    // coherent pinned buffer, then the sequence word behind a system-scope release
+    if (PHASE == 1 && a.hc_dst && blockIdx.x == 0 && threadIdx.x == 0) {
+        for (int i = 0; i < 16; i++)
+            __hip_atomic_store(a.hc_dst + i, a.hc_src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.hc_dst + 16, a.hc_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     const int tile = blockIdx.x * 4 + w;
     if (tile >= a.num_tiles) return;
     // the adaptive capacity's probe gets this view's phase-2 instance count (the next view's k_depth_cut reads it)
@@ -1120,15 +1131,27 @@ __global__ void __launch_bounds__(256) k_render_fwd2(RenderArgs a) {
     __shared__ uint32_t s_ids[DS_WAVE_MAX2];
     // the adaptive capacity's probe gets this view's phase-2 instance count (the next view's k_depth_cut reads it)
     if (a.probe && blockIdx.x == 0 && threadIdx.x == 0) a.probe[1] = a.counters[CNT_K2];
+    // block 0 (dispatched first, so it overlaps the tiles' blocks): the backward's longest-first replay order -- a
+    // finished tile's phase-1 max contributor is final, an unfinished tile's replay is bounded by its phase-1 +
+    // phase-2 list lengths (it reads max_contrib only where the other blocks do not write it)
+    const uint32_t ob = a.order ? 1u : 0u;
+    if (ob && blockIdx.x == 0) {
+        tile_order_sort(a.num_tiles, a.order, [&](int tile) {
+            if (!a.unfinished[tile]) return a.max_contrib[tile];
+            const uint2 r1 = a.ranges1[tile], r2 = a.ranges[tile];
+            return (r1.y - r1.x) + (r2.y - r2.x);
+        });
+        return;
+    }
     if (a.unf_list) {  // the unfinished tiles phase 1 listed, a block each, grid-stride
         const uint32_t nu = a.counters[CNT_UNFINISHED];
-        for (uint32_t i = blockIdx.x; i < nu; i += gridDim.x) {
+        for (uint32_t i = blockIdx.x - ob; i < nu; i += gridDim.x - ob) {
             render_fwd2_tile<COUNT>(a, (int)a.unf_list[i], s_sb, s_mx, s_ids);
             __syncthreads();  // s_sb / s_ids are reused by the next tile
         }
         return;
     }
-    const int tile = blockIdx.x;
+    const int tile = (int)(blockIdx.x - ob);
     if (tile >= a.num_tiles || !a.unfinished[tile]) return;  // block-uniform: finished in phase 1
     render_fwd2_tile<COUNT>(a, tile, s_sb, s_mx, s_ids);
 }
@@ -1463,6 +1486,13 @@ void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_
     const int per = DH_THREADS * DH_ITEMS;
     if (P > 0) k_depth_hist<<<(P + per - 1) / per, DH_THREADS, 0, s>>>(P, dkey, cnt, hist);
 }
+void launch_depth_hist_cut(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_t* hist, uint32_t cap,
+                           uint32_t* counters, uint32_t* tile_cnt, uint32_t* tile_cnt2, uint32_t num_tiles,
+                           const unsigned long long* rect_part, uint32_t nparts, uint32_t* probe, hipStream_t s) {
+    // (one launch -- every block flushing, a ticket, the last block cutting -- measured 72 us against 8 + 7 here)
+    launch_depth_hist(P, dkey, cnt, hist, s);
+    launch_depth_cut(hist, cap, counters, tile_cnt, tile_cnt2, num_tiles, rect_part, nparts, probe, s);
+}
 void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, uint32_t* tile_cnt, uint32_t* tile_cnt2,
                       uint32_t num_tiles, const unsigned long long* rect_part, uint32_t nparts, uint32_t* probe,
                       hipStream_t s) {
@@ -1486,11 +1516,10 @@ void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hi
         exclusive_scan(a.wtot, (uint32_t)waves, a.wtot, total, scan_tmp, s, gate);
         tile_offsets(a.tile_cnt, (uint32_t)a.num_tiles, a.ranges, s, gate);
     }
-    const int eblocks = blocks + (phase == 2 && a.order ? 1 : 0);  // + the replay-order block
     if (fat) {
-        if (phase == 2) k_bin_emit_fat<2><<<eblocks, 256, 0, s>>>(a);
+        if (phase == 2) k_bin_emit_fat<2><<<blocks, 256, 0, s>>>(a);
         else k_bin_emit_fat<1><<<blocks, 256, 0, s>>>(a);
-    } else if (phase == 2) k_bin_emit<2><<<eblocks, 256, 0, s>>>(a);
+    } else if (phase == 2) k_bin_emit<2><<<blocks, 256, 0, s>>>(a);
     else k_bin_emit<1><<<blocks, 256, 0, s>>>(a);
 }
 size_t bin_scan_temp_bytes(int P) { return scan_temp_bytes((uint32_t)((P + EMIT_RANKS - 1) / EMIT_RANKS)); }
@@ -1499,6 +1528,13 @@ void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, 
                            uint32_t* sat, hipStream_t s, uint32_t* probe) {
     k_sat_rows<<<(tiles_y + 1 + 3) / 4, 256, 0, s>>>(counters, unfinished, tiles_x, tiles_y, sat, probe);
     k_sat_cols<<<(tiles_x + 3) / 4, 256, 0, s>>>(counters, tiles_x, tiles_y, sat);
+}
+bool render_fwd2_orders() {  // the phase-2 launch writes RenderArgs::order (the backward skips k_bwd_order)
+#if defined(DG_PHASE2_WAVE_PER_TILE) || defined(DG_FWD2_SPLIT)
+    return false;
+#else
+    return true;
+#endif
 }
 void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
     if (a.num_tiles <= 0) return;
@@ -1509,7 +1545,8 @@ void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
         if (a.gcount) k_render_fwd2x<true><<<a.num_tiles, 1024, 0, s>>>(a);
         else k_render_fwd2x<false><<<a.num_tiles, 1024, 0, s>>>(a);
 #else
-        const int g2 = a.unf_list ? (a.num_tiles < FWD2_GRID ? a.num_tiles : FWD2_GRID) : a.num_tiles;
+        const int g2 = (a.unf_list ? (a.num_tiles < FWD2_GRID ? a.num_tiles : FWD2_GRID) : a.num_tiles) +
+                       (a.order ? 1 : 0);
         if (a.gcount) k_render_fwd2<true><<<g2, 256, 0, s>>>(a);
         else k_render_fwd2<false><<<g2, 256, 0, s>>>(a);
 #endif

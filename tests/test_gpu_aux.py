@@ -14,7 +14,9 @@ from raster_util import oracle_forward, rel_err, small_scene
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("B,C,H,W", [(1, 3, 37, 53), (1, 3, 128, 96), (2, 1, 64, 64)])
+# several strips across (54 output columns per wave) with even and odd widths, ragged rows (32 per strip)
+@pytest.mark.parametrize("B,C,H,W", [(1, 3, 37, 53), (1, 3, 128, 96), (2, 1, 64, 64), (1, 3, 70, 250),
+                                     (1, 1, 33, 237), (1, 2, 5, 119)])
 def test_fused_ssim_matches_oracle(oracle, hip_device, B, C, H, W):
     from fused_ssim_cuda import fusedssim, fusedssim_backward
     g = torch.Generator().manual_seed(H * W)
