@@ -498,9 +498,17 @@ uint64_t dg_binning_bytes(int64_t K, int W, int H) { (void)W; (void)H; return ca
 
 namespace {
 // Rasterizer::forward (rasterizer_impl.cu:334-498); gcount (optional): count mode, contributing pixels per Gaussian
+// The native step's activation fold: the preprocess reads the raw parameters and writes the activated ones to
+// a->opacities / scales / rotations (PreArgs::raw_*), plus the regulariser's per-block partial sums.
+struct ActFold {
+    const float *raw_o, *raw_s, *raw_q;
+    float* part_sc;
+};
+
 int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth, int* radii, dg_alloc_fn alloc,
                  void* user, void** geom_out, void** binning_out, void** image_out, void** binning2_out,
-                 int64_t* num_rendered, int64_t* num_instances, dg_stream_t stream_, uint32_t* gcount) {
+                 int64_t* num_rendered, int64_t* num_instances, dg_stream_t stream_, uint32_t* gcount,
+                 const ActFold* fold = nullptr) {
     if (check_args(a)) return 1;
     hipStream_t s = (hipStream_t)stream_;
     const int P = a->P, W = a->W, H = a->H;
@@ -526,6 +534,7 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     // its per-block parts)
     gs::PreArgs pre;
     fill_pre(pre, a);
+    if (fold) { pre.raw_o = fold->raw_o; pre.raw_s = fold->raw_s; pre.raw_q = fold->raw_q; pre.part_sc = fold->part_sc; }
     pre.radii = radii; pre.sp = g.sp; pre.depthkey = g.dkey; pre.cnt = g.cnt; pre.rcnt = g.rcnt;
     pre.hist = g.hist;
     pre.unf_rows = UNF_ROWS ? reinterpret_cast<unsigned long long*>(im.sat) : nullptr;  // (the SAT block is larger)
@@ -877,7 +886,7 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     const uint32_t nb_l1 = gs::clamp_l1_blocks((uint32_t)n_img);
     const uint32_t nb_map = gs::block_sum_blocks((uint32_t)n_img), nb_sc = gs::block_sum_blocks((uint32_t)P);
     const uint32_t nw_ssim = gs::ssim_waves(3, H, W);  // the fused SSIM's partials: nw L1, then nw map
-    const uint32_t nb_act = gs::activate_blocks((uint32_t)P);  // the fused route's regulariser partials
+    const uint32_t nb_act = gs::preprocess_blocks(P);  // the fused route's regulariser partials (preprocess blocks)
     const uint32_t n_part = (nb_l1 + nb_map > 2 * nw_ssim ? nb_l1 + nb_map : 2 * nw_ssim) + (nb_sc > nb_act ? nb_sc : nb_act);
     // ---- the step's scratch (DG_BUF_TRAIN); the nine rasterizer gradients back to back (the replay zero-fills them)
     const size_t n9 = (3 + 3 + 1 + 3 + 6 + 3 + 3 * Mz + 3 + 4) * Pz;
@@ -922,16 +931,17 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     // dropped: DESIGN.md §8.)
     const bool unfused = getenv("DG_TRAIN_UNFUSED") != nullptr;
     float* const p_sc_fused = part + 2 * nw_ssim;
-    // ---- forward: activations, rasterizer, clamp + L1, SSIM
-    gs::launch_activate_fwd((uint32_t)P, G[3].param, G[4].param, G[5].param, act_o, act_s, act_q, s,
-                            !unfused && a->loss ? p_sc_fused : nullptr);
+    // ---- forward: activations, rasterizer, clamp + L1, SSIM.  Default route: the activations (and the regulariser's
+    // partial sums) inside the rasterizer's preprocess launch (ActFold); unfused: their own launch.
+    if (unfused) gs::launch_activate_fwd((uint32_t)P, G[3].param, G[4].param, G[5].param, act_o, act_s, act_q, s);
+    const ActFold fold = {G[3].param, G[4].param, G[5].param, a->loss ? p_sc_fused : nullptr};
     dg_raster_args r = a->view;
     r.means3D = G[0].param; r.dc = G[1].param; r.sh = M > 0 ? G[2].param : nullptr;
     r.opacities = act_o; r.scales = act_s; r.rotations = act_q; r.colors = nullptr; r.cov3D_precomp = nullptr;
     void *geom = nullptr, *binning = nullptr, *image = nullptr, *binning2 = nullptr;
     int64_t num_rendered = 0, num_instances = 0;
-    if (dg_rasterize_forward(&r, color, invd, a->radii, alloc, user, &geom, &binning, &image, &binning2,
-                             &num_rendered, &num_instances, stream))
+    if (forward_impl(&r, color, invd, a->radii, alloc, user, &geom, &binning, &image, &binning2, &num_rendered,
+                     &num_instances, stream, nullptr, unfused ? nullptr : &fold))
         return 1;
     // ---- SparseGaussianAdam.step(radii > 0) over the six groups, ADMM proximal gradient, densification statistics.
     dg_adam_group groups[6];

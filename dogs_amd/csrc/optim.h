@@ -57,14 +57,11 @@ void launch_clamp_l1_fwd(uint32_t n, const float* img, const float* gt, float* o
 void launch_clamp_l1_bwd(uint32_t n, const float* img, const float* clamped, const float* gt, const float* g_img,
                          const float* g_l1, float* d_img, hipStream_t s, float g_l1_value = 0.0f);
 uint32_t block_sum_blocks(uint32_t n);
-// partials launch_activate_fwd writes with part_sc (one per 256-row block)
-uint32_t activate_blocks(uint32_t N);
 void launch_block_sum(const float* x, uint32_t n, int mode, float* partial, hipStream_t s);
 void launch_loss_final(const float* p_l1, uint32_t n_l1, const float* p_ssim, uint32_t n_ssim, const float* p_sc,
                        uint32_t n_sc, uint32_t n_img, uint32_t P, float* loss, hipStream_t s);
 void launch_activate_fwd(uint32_t N, const float* ro, const float* rs, const float* rq, float* o, float* sc, float* q,
-                         hipStream_t s,
-                         float* part_sc = nullptr);
+                         hipStream_t s);
 void launch_activate_bwd(uint32_t N, const float* o, const float* sc, const float* rq, const float* go,
                          const float* gsc, const float* gq, float* dro, float* drs, float* drq, hipStream_t s,
                          float scale_reg = 0.0f);

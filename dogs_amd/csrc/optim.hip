@@ -353,29 +353,17 @@ __global__ void __launch_bounds__(256) k_densify_gather(RebuildArgs a, const uin
 // Parameter activations of GaussianSplatModel (gaussian_splat_model.py get_opacity / get_scaling / get_quaternion:
 // sigmoid, exp, F.normalize(eps 1e-12)) and their backward, one thread per Gaussian, one launch each way (torch
 // runs ~4 kernels forward and ~8 backward for the three).
-// part_sc (optional): the block's partial sum of the scale regulariser's row products prod(scaling, 1), the training
-// step's loss term (k_block_sum's mode 1, without its pass over the scaling)
 __global__ void __launch_bounds__(256) k_activate_fwd(uint32_t N, const float* __restrict__ ro,
                                                       const float* __restrict__ rs, const float* __restrict__ rq,
                                                       float* __restrict__ o, float* __restrict__ sc,
-                                                      float* __restrict__ q, float* __restrict__ part_sc) {
+                                                      float* __restrict__ q) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    float prod = 0.0f;
-    if (i < N) {
-        o[i] = 1.0f / (1.0f + expf(-ro[i]));
-        float e[3];
-        for (int k = 0; k < 3; k++) sc[3 * (size_t)i + k] = e[k] = expf(rs[3 * (size_t)i + k]);
-        prod = (e[0] * e[1]) * e[2];
-        const float4 x = reinterpret_cast<const float4*>(rq)[i];
-        const float d = fmaxf(sqrtf(((x.x * x.x + x.y * x.y) + x.z * x.z) + x.w * x.w), 1e-12f);
-        reinterpret_cast<float4*>(q)[i] = make_float4(x.x / d, x.y / d, x.z / d, x.w / d);
-    }
-    if (!part_sc) return;  // kernel-uniform
-    __shared__ float s_w[4];
-    for (int o2 = 32; o2 > 0; o2 >>= 1) prod += __shfl_xor(prod, o2);
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = prod;
-    __syncthreads();
-    if (threadIdx.x == 0) part_sc[blockIdx.x] = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);
+    if (i >= N) return;
+    o[i] = 1.0f / (1.0f + expf(-ro[i]));
+    for (int k = 0; k < 3; k++) sc[3 * (size_t)i + k] = expf(rs[3 * (size_t)i + k]);
+    const float4 x = reinterpret_cast<const float4*>(rq)[i];
+    const float d = fmaxf(sqrtf(((x.x * x.x + x.y * x.y) + x.z * x.z) + x.w * x.w), 1e-12f);
+    reinterpret_cast<float4*>(q)[i] = make_float4(x.x / d, x.y / d, x.z / d, x.w / d);
 }
 __global__ void __launch_bounds__(256) k_activate_bwd(uint32_t N, const float* __restrict__ o,
                                                       const float* __restrict__ sc, const float* __restrict__ rq,
@@ -485,10 +473,9 @@ void launch_densify_gather(const RebuildArgs& a, const uint32_t* keep_pos, hipSt
     if (b) k_densify_gather<<<b, 256, 0, s>>>(a, keep_pos, gg);
 }
 
-uint32_t activate_blocks(uint32_t N) { return (N + 255) / 256; }
 void launch_activate_fwd(uint32_t N, const float* ro, const float* rs, const float* rq, float* o, float* sc, float* q,
-                         hipStream_t s, float* part_sc) {
-    if (N) k_activate_fwd<<<activate_blocks(N), 256, 0, s>>>(N, ro, rs, rq, o, sc, q, part_sc);
+                         hipStream_t s) {
+    if (N) k_activate_fwd<<<(N + 255) / 256, 256, 0, s>>>(N, ro, rs, rq, o, sc, q);
 }
 void launch_activate_bwd(uint32_t N, const float* o, const float* sc, const float* rq, const float* go,
                          const float* gsc, const float* gq, float* dro, float* drs, float* drq, hipStream_t s,

@@ -33,6 +33,11 @@ struct PreArgs {
     uint32_t* err;
     unsigned long long* unf_rows;  // [unf_words] per-tile-row bitmasks of unfinished tiles, zeroed here (set by the render)
     int unf_words;
+    // optional (the native training step): the parameter activations of GaussianSplatModel done here -- opacity =
+    // sigmoid(raw_o), scaling = exp(raw_s), rotation = normalize(raw_q) written to opacities / scales / rotations
+    // (which then are outputs) for every Gaussian -- and part_sc[block] = the block's sum of prod(scaling, 1)
+    const float *raw_o, *raw_s, *raw_q;
+    float* part_sc;
 };
 
 // Counters block at the head of the geometry state (device, uint32 slots).
@@ -212,6 +217,7 @@ int bin_waves(int P);
 void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, int tiles_x, int tiles_y,
                            uint32_t* sat, hipStream_t s, uint32_t* probe = nullptr);
 void launch_render_fwd(const RenderArgs& a, hipStream_t s);
+uint32_t preprocess_blocks(int P);  // k_preprocess's grid (PreArgs::part_sc entries)
 bool render_fwd2_orders();
 // count mode: score[i] = gcount[i] x the (AA-scaled) opacity of splat record i (0 when culled)
 void launch_count_score(int P, const int* radii, const float4* sp, const uint32_t* gcount, float* score,

@@ -160,7 +160,25 @@ __device__ __forceinline__ void wave_candidates(CandLDS& L, int lane, int x0, in
 
 // Returns the tile-rect area (0 when culled); fills the geometry outputs of kept Gaussians.  The colour
 // (computeColorFromSH) is not evaluated here: only binned Gaussians need it, and k_bin_emit computes it for them.
-__device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx) {
+// GaussianSplatModel's activations (optim.hip k_activate_fwd's expressions), stored for the later consumers
+__device__ __forceinline__ void activate_one(const PreArgs& a, int idx, float& o, f3& s, f4& q, float& prod) {
+    const float ro = a.raw_o[idx];
+    const float rs0 = a.raw_s[3 * idx], rs1 = a.raw_s[3 * idx + 1], rs2 = a.raw_s[3 * idx + 2];
+    const float4 x = reinterpret_cast<const float4*>(a.raw_q)[idx];
+    o = 1.0f / (1.0f + expf(-ro));
+    s = {expf(rs0), expf(rs1), expf(rs2)};
+    prod = (s.x * s.y) * s.z;
+    const float d = fmaxf(sqrtf(((x.x * x.x + x.y * x.y) + x.z * x.z) + x.w * x.w), 1e-12f);
+    q = {x.x / d, x.y / d, x.z / d, x.w / d};
+    float* so = const_cast<float*>(a.opacities);
+    float* ss = const_cast<float*>(a.scales);
+    float* sq = const_cast<float*>(a.rotations);
+    so[idx] = o;
+    ss[3 * idx] = s.x; ss[3 * idx + 1] = s.y; ss[3 * idx + 2] = s.z;
+    reinterpret_cast<float4*>(sq)[idx] = make_float4(q.x, q.y, q.z, q.w);
+}
+
+__device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, float& prod) {
     a.radii[idx] = 0;
     a.depthkey[idx] = 0xffffffffu;
     a.cnt[idx] = 0u;
@@ -170,11 +188,16 @@ __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx) {
     // (issued after the frustum test they would cost a second, dependent, round trip per wave)
     f3 s = {0.f, 0.f, 0.f};
     f4 q = {0.f, 0.f, 0.f, 0.f};
-    if (!a.cov3D_precomp) {
-        s = {a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
-        q = {a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]};
+    float opac;
+    if (a.raw_o) {
+        activate_one(a, idx, opac, s, q, prod);
+    } else {
+        if (!a.cov3D_precomp) {
+            s = {a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
+            q = {a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]};
+        }
+        opac = a.opacities[idx];
     }
-    const float opac = a.opacities[idx];
     // in_frustum (auxiliary.h:150-175)
     const f3 pv = tp4x3(po, a.view);
     if (pv.z <= 0.2f) {
@@ -228,6 +251,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx) {
 // Gaussians need them, and the binning walk (k_bin_count / k_bin_emit) computes them for those.
 __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     __shared__ unsigned long long s_sum[4];
+    __shared__ float s_prod[4];
     __shared__ uint32_t s_err;
     const int t = threadIdx.x;
     const int base = blockIdx.x * 256;
@@ -238,14 +262,20 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     __syncthreads();
     a.err = &s_err;  // a prefiltered violation flags the block (bit 63 of its part)
     uint32_t area = 0;
-    if (idx < a.P) area = preprocess_one(a, idx);
+    float prod = 0.0f;
+    if (idx < a.P) area = preprocess_one(a, idx, prod);
     unsigned long long v = area;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = v;
+    for (int o = 32; o > 0; o >>= 1) {
+        v += __shfl_xor(v, o);
+        if (a.part_sc) prod += __shfl_xor(prod, o);
+    }
+    if ((threadIdx.x & 63) == 0) { s_sum[threadIdx.x >> 6] = v; s_prod[threadIdx.x >> 6] = prod; }
     __syncthreads();
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
         a.rect_part[blockIdx.x] = (s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3]) | (s_err ? (1ull << 63) : 0ull);
+        if (a.part_sc) a.part_sc[blockIdx.x] = (s_prod[0] + s_prod[1]) + (s_prod[2] + s_prod[3]);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -457,6 +487,33 @@ struct BinLane {
     float4 co;
     bool member;
 };
+// The walk's candidate tiles (DG_FULL_RECT_WALK: the whole rect): the rect's tiles that can meet the Gaussian's
+// contribution ellipse E = {d : 0.5 d^T C d <= lthr} (alpha >= 1/255 at d; C = conic).  max_contrib_power_rect's kept
+// test evaluates the power at a point of the tile's pixel rectangle, so a kept tile's rectangle holds a point of E and
+// meets E's bounding box, half-widths sqrt(2 lthr Sigma_xx) and sqrt(2 lthr Sigma_yy), Sigma = C^-1 (det in double:
+// no cancellation for thin conics; widened by 0.1% + 1 px against the test's float rounding).  The kept tiles, their
+// count and their (ty, tx) order are those of the full rect: the walk only skips candidates the test rejects (the
+// getRect radius is 3 sigma of the largest axis whatever the opacity and the orientation).
+__device__ __forceinline__ void tight_rect(BinLane& b) {
+#ifndef DG_FULL_RECT_WALK
+    const double a_ = b.co.x, bb = b.co.y, c_ = b.co.z;
+    const double det = a_ * c_ - bb * bb;
+    if (!(det > 0.0) || !(a_ > 0.0) || !(c_ > 0.0)) return;  // degenerate conic (or NaN): the full rect
+    const double L2 = 2.0 * (b.lthr > 0.0f ? (double)b.lthr : 0.0);
+    const float wx = (float)sqrt(L2 * (c_ / det)) * 1.001f + 1.0f;
+    const float wy = (float)sqrt(L2 * (a_ / det)) * 1.001f + 1.0f;
+    // tiles t with [16 t, 16 t + 15] meeting [m - w, m + w]; clamped to the rect (fmaxf / fminf drop a NaN bound)
+    const float fx0 = (float)b.x0, fx1 = (float)b.x1, fy0 = (float)b.y0, fy1 = (float)b.y1;
+    const float lx = fminf(fmaxf(ceilf((b.mx - wx - (float)(GS_TILE_X - 1)) / (float)GS_TILE_X), fx0), fx1);
+    const float hx = fminf(fmaxf(floorf((b.mx + wx) / (float)GS_TILE_X) + 1.0f, fx0), fx1);
+    const float ly = fminf(fmaxf(ceilf((b.my - wy - (float)(GS_TILE_Y - 1)) / (float)GS_TILE_Y), fy0), fy1);
+    const float hy = fminf(fmaxf(floorf((b.my + wy) / (float)GS_TILE_Y) + 1.0f, fy0), fy1);
+    b.x0 = (int)lx; b.x1 = (int)hx; b.y0 = (int)ly; b.y1 = (int)hy;
+    if (b.x1 < b.x0) b.x1 = b.x0;
+    if (b.y1 < b.y0) b.y1 = b.y0;
+#endif
+}
+
 // known: membership from the count pass's wave mask (0 / 1: no key test, no SAT test), -1: test here
 template <int PHASE>
 __device__ __forceinline__ BinLane bin_lane(const BinArgs& a, int g, int lane, uint32_t thr, uint32_t* s_key,
@@ -484,6 +541,7 @@ __device__ __forceinline__ BinLane bin_lane(const BinArgs& a, int g, int lane, u
                 b.co = make_float4(s0.z, s0.w, s1.x, s1.y);
                 b.mx = s0.x; b.my = s0.y;
                 b.lthr = gs_logf(b.co.w / (1.0f / 255.0f));
+                tight_rect(b);
             }
         }
         b.member = m;
@@ -608,6 +666,7 @@ __device__ __forceinline__ BinLane member_lane(const BinArgs& a, int g, bool mem
         b.co = make_float4(s0.z, s0.w, s1.x, s1.y);
         b.mx = s0.x; b.my = s0.y;
         b.lthr = gs_logf(b.co.w / (1.0f / 255.0f));
+        tight_rect(b);
         b.member = true;
     }
     if (!b.member) { b.x1 = b.x0; b.y1 = b.y0; }
@@ -1480,8 +1539,9 @@ __global__ void __launch_bounds__(256) k_filter(PreArgs a) {
 }
 
 void launch_preprocess(const PreArgs& a, hipStream_t s) {
-    if (a.P > 0) k_preprocess<<<(a.P + 255) / 256, 256, 0, s>>>(a);
+    if (a.P > 0) k_preprocess<<<preprocess_blocks(a.P), 256, 0, s>>>(a);
 }
+uint32_t preprocess_blocks(int P) { return (uint32_t)((P + 255) / 256); }
 void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_t* hist, hipStream_t s) {
     const int per = DH_THREADS * DH_ITEMS;
     if (P > 0) k_depth_hist<<<(P + per - 1) / per, DH_THREADS, 0, s>>>(P, dkey, cnt, hist);

@@ -1,0 +1,12 @@
+set -e
+OUT=gpurun_out/r3i; mkdir -p $OUT/ab $OUT/ts
+export TMPDIR=/tmp DOGS_TEST_LOG=$OUT/fullsize.jsonl
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { echo "gpu tests rc=$?" >> $OUT/gpu_tests.log; exit 0; }
+timeout -k 10 120 tools/bin/ubench_stream > $OUT/ubench_stream.txt 2>&1
+for lib in n7 n8 n7 n8; do DOGS_HIP_LIB=ab/$lib.so timeout -k 10 120 python tools/adam_bench.py >> $OUT/adam_bench.txt 2>&1; done
+for i in 1 2; do for lib in n7 n8; do
+  DOGS_HIP_LIB=ab/$lib.so timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-admm --no-reference-k > $OUT/ts/$lib.$i.log 2>&1
+done; done
+DOGS_HIP_LIB=ab/n8.so ROUTES=folded TB_ARGS=--bench-native bash tools/train_timeline.sh $OUT/tt
+python3 tools/train_timeline.py $OUT/tt > $OUT/train_timeline.txt 2>&1 || true
+find $OUT/tt -name '*kernel_trace.csv' -delete

@@ -1,4 +1,5 @@
-"""Per-step kernel timelines of the native training step from tools/train_timeline.sh traces.
+"""Per-step kernel timelines of the native training step from tools/train_timeline.sh traces (steps delimited by
+k_preprocess, the first launch of a step since the activations moved into it).
 usage: python tools/train_timeline.py OUTDIR"""
 import csv
 import glob
@@ -16,7 +17,7 @@ def by_kind(out):
     """One trace holding both routes (trainer_bench.py --alternate): steps classified by their kernels."""
     f = glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True)
     rows = load(f[0])
-    idx = [i for i, r in enumerate(rows) if "k_activate_fwd" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if "k_preprocess" in r["Kernel_Name"]]
     spans = {"unfused": [], "folded": []}
     ksum = {"unfused": [], "folded": []}
     for a, b in zip(idx, idx[1:]):
@@ -39,7 +40,7 @@ def main(out):
         if not f:
             continue
         rows = load(f[0])
-        idx = [i for i, r in enumerate(rows) if "k_activate_fwd" in r["Kernel_Name"]]
+        idx = [i for i, r in enumerate(rows) if "k_preprocess" in r["Kernel_Name"]]
         spans = [(int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1000 for a, b in zip(idx, idx[1:])]
         spans = spans[len(spans) // 2:]
         print(f"== {route}: step span median {sorted(spans)[len(spans) // 2]:.1f} us over {len(spans)} steps")
