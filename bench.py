@@ -238,8 +238,10 @@ class TrainStep:
         p = self.params
         params = {"xyz": p["xyz"], "features_dc": p["f_dc"], "features_rest": p["f_rest"], "opacity": p["opacity"],
                   "scaling": p["scaling"], "quaternion": p["quaternion"]}
+        # overlap: each step's f_dc / f_rest update runs beside the next step's forward up to its emission (the
+        # timed region's closing torch.cuda.synchronize() waits for it like for everything else)
         nts = NativeTrainStep(params, self.opt, self.cams, [self.gt] * len(self.cams), 3, 0.2, 0.05,
-                              torch.zeros(3, device=self.gt.device), self.gt.device, stats=self.stats)
+                              torch.zeros(3, device=self.gt.device), self.gt.device, stats=self.stats, overlap=True)
         state = {"i": 0}
 
         def step():

@@ -46,7 +46,7 @@ class DgDensifyStats(C.Structure):
 class DgTrainStepArgs(C.Structure):
     _fields_ = [("view", DgRasterArgs), ("gt", C.c_void_p), ("lambda_dssim", C.c_float), ("lambda_scale", C.c_float),
                 ("groups", DgAdamGroup * 6), ("prox", DgAdamProx * 6), ("stats", C.c_void_p), ("radii", C.c_void_p),
-                ("image", C.c_void_p), ("loss", C.c_void_p)]
+                ("image", C.c_void_p), ("loss", C.c_void_p), ("sh_status", C.c_void_p)]
 
 
 class DgGaussianSet(C.Structure):
@@ -83,7 +83,7 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count"
            "dg_add_densification_stats", "dg_densify_select", "dg_densify_split_stds", "dg_densify_count",
            "dg_densify_gather", "dg_splat_pack", "dg_ply_pack", "dg_ring_create", "dg_ring_submit", "dg_ring_next",
            "dg_ring_upload", "dg_ring_pending", "dg_ring_destroy", "dg_image_u8_to_chw", "dg_points_in_boxes2d", "dg_activate_forward", "dg_activate_backward", "dg_clamp_l1_blocks",
-           "dg_clamp_l1_forward", "dg_clamp_l1_backward", "dg_adaptive_capacity", "dg_debug_counters", "dg_adam_update_groups_prox", "dg_train_step",
+           "dg_clamp_l1_forward", "dg_clamp_l1_backward", "dg_adaptive_capacity", "dg_debug_counters", "dg_adam_update_groups_prox", "dg_train_step", "dg_train_sync",
            "dg_colmap_cameras", "dg_colmap_images", "dg_colmap_points3d", "dg_prune_select", "dg_prune_gather_stats",
            "dg_last_error", "dg_version")
 
@@ -149,6 +149,9 @@ def load(path: str | None = None):
         if hasattr(L, "dg_train_step"):
             L.dg_train_step.restype = C.c_int
             L.dg_train_step.argtypes = [C.POINTER(DgTrainStepArgs), ALLOC_FN, vp, vp]
+        if hasattr(L, "dg_train_sync"):
+            L.dg_train_sync.restype = C.c_int
+            L.dg_train_sync.argtypes = [vp]
         if hasattr(L, "dg_debug_counters"):
             L.dg_debug_counters.restype = C.c_int
             L.dg_debug_counters.argtypes = [vp, C.c_int, C.POINTER(C.c_uint32), vp]
@@ -296,22 +299,30 @@ class ReuseArena:
     tensor per buffer kind, handed out again while it is large enough.  Stream order makes the reuse safe: the next
     call's kernels run after this call's on the same stream."""
 
-    def __init__(self, device: torch.device):
+    def __init__(self, device: torch.device, keep_retired: bool = False):
         self.device = device
         self.buffers: dict[int, torch.Tensor] = {}
+        # keep_retired: outgrown buffers stay alive until release_retired() (work on a side stream may still read
+        # them: the native step's overlapped update)
+        self.keep_retired, self.retired = keep_retired, []
 
         def _alloc(user, which, nbytes):  # noqa: ARG001
             which, nbytes = int(which), max(int(nbytes), 1)
             t = self.buffers.get(which)
             if t is None or t.numel() < nbytes:
                 try:
-                    t = torch.empty(nbytes + nbytes // 4, dtype=torch.uint8, device=self.device)
+                    nt = torch.empty(nbytes + nbytes // 4, dtype=torch.uint8, device=self.device)
                 except Exception:  # noqa: BLE001 - reported to C as NULL, surfaces as RuntimeError
                     return None
-                self.buffers[which] = t
+                if t is not None and self.keep_retired:
+                    self.retired.append(t)
+                t = self.buffers[which] = nt
             return t.data_ptr()
 
         self.fn = ALLOC_FN(_alloc)
+
+    def release_retired(self) -> None:
+        self.retired.clear()
 
 
 def adaptive_capacity(W: int, H: int, reset: bool = False) -> int:

@@ -90,7 +90,8 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
     };
     float acc_l1 = 0.0f, acc_map = 0.0f;
     float ring[11][5];
-    float rawc[FUSED ? 11 : 1], rawg[FUSED ? 11 : 1];  // FUSED: the last 11 rows' clamped / target values
+    // FUSED: the clamped image and the L1 term as the input rows arrive -- lanes 5..58 hold the strip's output columns
+    const bool own_col = FUSED && lane >= 5 && lane < 5 + SSW_OUT && colok;
     float ua = lda(sp.y0 - 5), va = ldb(sp.y0 - 5);
     float ub = lda(sp.y0 - 4), vb = ldb(sp.y0 - 4);
     for (int base = 0; base < SSW_IN; base += 11) {
@@ -102,7 +103,13 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
                 ua = ub; va = vb;
                 ub = lda(sp.y0 - 5 + rr + 2);
                 vb = ldb(sp.y0 - 5 + rr + 2);
-                if (FUSED) { rawc[j] = u; rawg[j] = v; }
+                if (FUSED) {
+                    const int row = sp.y0 - 5 + rr;  // one of the strip's output rows
+                    if (own_col && row >= sp.y0 && row < sp.y0 + SSW_ROWS && row < H) {
+                        out_img[plane + (size_t)row * W + sp.x] = u;
+                        acc_l1 += fabsf(u - v);
+                    }
+                }
                 ring[j][0] = hconv11(u);
                 ring[j][1] = hconv11(u * u);
                 ring[j][2] = hconv11(v);
@@ -110,13 +117,6 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
                 ring[j][4] = hconv11(u * v);
                 const int y = sp.y0 + rr - 10;
                 if (rr >= 10 && y < H) {
-                    // FUSED: output row y is input row rr - 5 (ring slot (j + 6) % 11) of column ox, which lane + 5
-                    // holds (shuffled by the whole wave, outside the output-column branch)
-                    float oc = 0.0f, og = 0.0f;
-                    if (FUSED) {
-                        oc = __shfl_down(rawc[(j + 6) % 11], 5);
-                        og = __shfl_down(rawg[(j + 6) % 11], 5);
-                    }
                     float m[5] = {0, 0, 0, 0, 0};
 #pragma unroll
                     for (int k = 0; k < 11; k++) {
@@ -139,9 +139,6 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
                         const float rAB = __builtin_amdgcn_rcpf(A * B), rAAB = __builtin_amdgcn_rcpf(A * A * B),
                                     rABB = __builtin_amdgcn_rcpf(A * B * B);
                         if (FUSED) {
-                            const float c = oc, g = og;
-                            out_img[gi] = c;
-                            acc_l1 += fabsf(c - g);
                             acc_map += (Cc * D) * rAB;
                         } else {
                             map[gi] = (Cc * D) * rAB;

@@ -203,7 +203,7 @@ gs::BinArgs bin_args(const dg_raster_args* r, const Geom& g, const Image& im, in
     a.P = P; a.tiles_x = tx; a.num_tiles = T; a.dkey = g.dkey; a.sp = g.sp; a.counters = g.counters;
     a.unf = im.unfinished; a.sat = im.sat; a.wtot = g.wtot; a.wmask = g.wmask; a.mlist = g.mlist; a.cap = cap; a.first_e = g.first_e; a.rcnt = g.rcnt;
     a.eg = b.eg; a.ikey = b.ik; a.flag = b.flag; a.tile_cnt = tile_cnt; a.ranges = ranges; a.s_e = b.se;
-    a.unf_rows = nullptr; a.unf_rw = 0; a.unf_th = 0; a.probe = nullptr;
+    a.unf_rows = nullptr; a.unf_rw = 0; a.unf_th = 0; a.probe = nullptr; a.colors_later = 0;
     return a;
 }
 // per-tile (depth, index) order of a phase's binned lists
@@ -503,12 +503,14 @@ namespace {
 struct ActFold {
     const float *raw_o, *raw_s, *raw_q;
     float* part_sc;
+    hipEvent_t wait_before_emit;  // optional: the previous step's overlapped SH update (the emission reads the SH)
+    bool waited;                  // out: the wait was enqueued (a forward that binned nothing leaves it to the caller)
 };
 
 int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth, int* radii, dg_alloc_fn alloc,
                  void* user, void** geom_out, void** binning_out, void** image_out, void** binning2_out,
                  int64_t* num_rendered, int64_t* num_instances, dg_stream_t stream_, uint32_t* gcount,
-                 const ActFold* fold = nullptr) {
+                 ActFold* fold = nullptr) {
     if (check_args(a)) return 1;
     hipStream_t s = (hipStream_t)stream_;
     const int P = a->P, W = a->W, H = a->H;
@@ -570,9 +572,15 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     if (!bbase) return fail("binning allocation failed%s%d");
     *binning_out = bbase;
     Binning b = carve_binning(bbase, C1);
+    // the native step's overlapped SH update (fold->wait_before_emit): the phase-1 emission runs without the colours,
+    // and the colour pass waits for the update after the long-list sort (below)
+    hipEvent_t sh_wait = fold ? fold->wait_before_emit : nullptr;
+    gs::BinArgs ba1;
+    const bool colors_later = sh_wait && C1 > 0 && P > 0;
     if (C1 > 0 && P > 0) {
-        gs::BinArgs ba = bin_args(a, g, im, T, (uint32_t)C1, b, im.tile_cnt, im.ranges);
-        { PROF("emit"); gs::launch_bin(1, ba, g.counters + gs::CNT_E1, g.scan_tmp, s); }
+        ba1 = bin_args(a, g, im, T, (uint32_t)C1, b, im.tile_cnt, im.ranges);
+        ba1.colors_later = colors_later ? 1 : 0;
+        { PROF("emit"); gs::launch_bin(1, ba1, g.counters + gs::CNT_E1, g.scan_tmp, s); }
         DBG_SYNC(a->debug, s);
     }
     // the host's only wait is on this early copy (num_rendered, E1, error flag, cut), and it happens after all of
@@ -598,6 +606,12 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
         DBG_SYNC(a->debug, s);
     } else {
         HIP_OK(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * (size_t)T, s));
+    }
+    if (colors_later) {
+        HIP_OK(hipStreamWaitEvent(s, sh_wait, 0));
+        fold->waited = true;
+        sh_wait = nullptr;
+        gs::launch_binned_colors(ba1, s);
     }
 
     gs::RenderArgs r;
@@ -654,7 +668,9 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
         ba.unf_rows = UNF_ROWS ? reinterpret_cast<const unsigned long long*>(im.sat) : nullptr;
         ba.unf_rw = unf_rw_of(tx); ba.unf_th = ty;
         ba.probe = UNF_ROWS && ac ? ac->probe : nullptr;
-        gs::launch_bin(2, ba, g.counters + gs::CNT_K2, g.scan_tmp, s);
+        gs::launch_bin(2, ba, g.counters + gs::CNT_K2, g.scan_tmp, s, sh_wait);
+        if (sh_wait) fold->waited = true;
+        sh_wait = nullptr;
         const gs::DSortArgs ds2 = dsort_args(b2, K, T, im.ranges2, im.unfinished, gate, im.long_tiles,
                                              g.counters + gs::CNT_LONG2);
         gs::RenderArgs r2 = r;
@@ -825,6 +841,42 @@ int dg_rasterize_filter(const dg_raster_args* a, int* radii, dg_stream_t stream)
     return 0;
 }
 
+// The native step's overlapped SH update (dg_train_step_args::sh_status): per caller stream, a side stream and the
+// event its f_dc / f_rest update records; `pending` until a later step (or dg_train_sync) made the stream wait on it.
+// blocks of the side launch: few enough that the overlapped forward's kernels find free compute units
+uint32_t sh_grid_cap() {
+    static const uint32_t v = [] {
+        const char* e = getenv("DG_SH_ADAM_BLOCKS");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    return v;
+}
+struct ShOverlap {
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, done = nullptr;
+    bool pending = false;
+};
+std::mutex& sh_mu() { static auto* m = new std::mutex; return *m; }
+std::map<hipStream_t, ShOverlap>& sh_map() { static auto* m = new std::map<hipStream_t, ShOverlap>; return *m; }
+ShOverlap* sh_state(hipStream_t s, bool create) {
+    std::lock_guard<std::mutex> lk(sh_mu());
+    auto& mp = sh_map();
+    auto it = mp.find(s);
+    if (it != mp.end()) return &it->second;
+    if (!create) return nullptr;
+    ShOverlap o;
+    // the side stream at the lowest priority: the dispatcher then prefers the overlapped forward's work groups (at
+    // equal priority the update's many small groups kept a one-block launch of the forward waiting ~150 us)
+    int least = 0, greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (const char* e = getenv("DG_SH_PRIO")) least = atoi(e);
+    if (hipStreamCreateWithPriority(&o.side, hipStreamNonBlocking, least) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&o.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&o.done, hipEventDisableTiming) != hipSuccess)
+        return nullptr;
+    return &(mp[s] = o);
+}
+
 static int fill_stats(gs::AdamMultiArgs& m, const dg_densify_stats* st) {
     if (!st) return 0;
     if (!st->radii || !st->dmeans2D || !st->max_radii2D || !st->grad_accum || !st->denom)
@@ -934,7 +986,13 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     // ---- forward: activations, rasterizer, clamp + L1, SSIM.  Default route: the activations (and the regulariser's
     // partial sums) inside the rasterizer's preprocess launch (ActFold); unfused: their own launch.
     if (unfused) gs::launch_activate_fwd((uint32_t)P, G[3].param, G[4].param, G[5].param, act_o, act_s, act_q, s);
-    const ActFold fold = {G[3].param, G[4].param, G[5].param, a->loss ? p_sc_fused : nullptr};
+    // the previous step's overlapped SH update: the emission waits for it (the first launch that reads the SH rows)
+    ShOverlap* ov = sh_state(s, a->sh_status != nullptr);
+    if (a->sh_status && !ov) return fail("train step: no side stream for the overlapped update%s%d");
+    hipEvent_t prev = ov && ov->pending ? ov->done : nullptr;
+    if (prev && unfused) { HIP_OK(hipStreamWaitEvent(s, prev, 0)); prev = nullptr; }
+    if (ov) ov->pending = false;
+    ActFold fold = {G[3].param, G[4].param, G[5].param, a->loss ? p_sc_fused : nullptr, prev, false};
     dg_raster_args r = a->view;
     r.means3D = G[0].param; r.dc = G[1].param; r.sh = M > 0 ? G[2].param : nullptr;
     r.opacities = act_o; r.scales = act_s; r.rotations = act_q; r.colors = nullptr; r.cov3D_precomp = nullptr;
@@ -943,6 +1001,7 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     if (forward_impl(&r, color, invd, a->radii, alloc, user, &geom, &binning, &image, &binning2, &num_rendered,
                      &num_instances, stream, nullptr, unfused ? nullptr : &fold))
         return 1;
+    if (prev && !fold.waited) HIP_OK(hipStreamWaitEvent(s, prev, 0));  // nothing was binned: before the backward
     // ---- SparseGaussianAdam.step(radii > 0) over the six groups, ADMM proximal gradient, densification statistics.
     dg_adam_group groups[6];
     const float* grads[6] = {dmeans3D, ddc, dsh, unfused ? g_o : dopac, unfused ? g_s : dscales,
@@ -955,11 +1014,12 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     gs::AdamMultiArgs m;
     memset(&m, 0, sizeof(m));
     m.visible = nullptr; m.vis_radii = a->radii; m.N = (uint32_t)P; m.b1 = 0.9f; m.b2 = 0.999f;
-    int n = 0;
+    int n = 0, gk[6];
     for (int k = 0; k < 6; k++) {
         const dg_adam_group& g = groups[k];
         if (g.M == 0) continue;
         if ((uint64_t)P * g.M >= 0xfffff000ull) return fail("train step: group %s%d has N * M >= 2^32", "", k);
+        gk[n] = k;
         gs::AdamGroup& d = m.g[n++];
         d.param = g.param; d.grad = g.grad; d.m = g.exp_avg; d.v = g.exp_avg_sq; d.lr = g.lr; d.eps = g.eps; d.M = g.M;
         uintptr_t al = reinterpret_cast<uintptr_t>(g.param) | reinterpret_cast<uintptr_t>(g.grad) |
@@ -1013,9 +1073,40 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
         gs::launch_activate_bwd((uint32_t)P, act_o, act_s, G[5].param, dopac, dscales, drot, g_o, g_s, g_q, s,
                                 a->lambda_scale / (float)P);
 #ifndef DG_DIAG_NO_ADAM  // timing diagnostic only (no parameter update): what the update costs the next step's forward
-    gs::launch_adam_multi(m, s);
+    if (a->sh_status) {
+        // xyz / opacity / scaling / rotation + statistics + the rows' status snapshot here (the next forward's
+        // preprocess reads them); f_dc / f_rest (81% of the bytes) on the side stream from the snapshot, overlapping
+        // the next step's forward until its emission (the launches in between read neither them nor the snapshot)
+        gs::AdamMultiArgs mg = m, ms = m;
+        mg.n = ms.n = 0;
+        for (int i = 0; i < n; i++) {
+            if (gk[i] == 1 || gk[i] == 2) ms.g[ms.n++] = m.g[i];
+            else mg.g[mg.n++] = m.g[i];
+        }
+        mg.status_out = a->sh_status;
+        ms.status = a->sh_status;
+        ms.radii = nullptr;  // no statistics on the side
+        ms.grid_cap = sh_grid_cap();
+        gs::launch_adam_multi(mg, s);
+        HIP_OK(hipEventRecord(ov->fork, s));
+        HIP_OK(hipStreamWaitEvent(ov->side, ov->fork, 0));
+        if (ms.n) gs::launch_adam_multi(ms, ov->side);
+        HIP_OK(hipEventRecord(ov->done, ov->side));
+        ov->pending = true;
+    } else {
+        gs::launch_adam_multi(m, s);
+    }
 #endif
     HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_train_sync(dg_stream_t stream) {
+    ShOverlap* ov = sh_state((hipStream_t)stream, false);
+    if (ov && ov->pending) {
+        HIP_OK(hipStreamWaitEvent((hipStream_t)stream, ov->done, 0));
+        ov->pending = false;
+    }
     return 0;
 }
 

@@ -50,6 +50,13 @@ struct AdamMultiArgs {
     // a 4-float chunk touching no hot row takes its incoming gradient as zero without reading it (the native step,
     // where the activation fold supplies the regulariser's gradient of every row)
     const uint32_t* hot;
+    // optional (the native step's overlapped update, dg_train_step_args::sh_status): status_out[i] = visible | hot << 1
+    // written for every row by the row blocks; a launch given `status` reads its rows' visibility and hot flag there
+    // instead of visible / vis_radii / hot (the next step's forward overwrites those while the launch may still run)
+    uint8_t* status_out;
+    const uint8_t* status;
+    uint32_t grid_cap;   // optional: at most this many blocks, striding over the work (0: one block per work block)
+    uint32_t nblocks;    // set by launch_adam_multi
 };
 void launch_adam_multi(const AdamMultiArgs& a, hipStream_t s);
 uint32_t clamp_l1_blocks(uint32_t n);

@@ -80,11 +80,14 @@ __device__ __forceinline__ void f4set(float4& v, int j, float x) {
     if (j == 0) v.x = x; else if (j == 1) v.y = x; else if (j == 2) v.z = x; else v.w = x;
 }
 
-__global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
-    const uint32_t blk = blockIdx.x;
-    if (blk >= a.start[a.n]) {  // densification statistics, one Gaussian per lane
+// one 256-thread work block (group chunks, or the row blocks past start[n])
+__device__ __forceinline__ void adam_block(const AdamMultiArgs& a, const uint32_t blk) {
+    if (blk >= a.start[a.n]) {  // row blocks: the status snapshot and the densification statistics, a row per lane
         const uint32_t i = (blk - a.start[a.n]) * 256u + threadIdx.x;
-        if (i >= a.N || !(a.visible ? a.visible[i] != 0 : a.vis_radii[i] > 0)) return;
+        if (i >= a.N) return;
+        const bool vis = a.visible ? a.visible[i] != 0 : a.vis_radii[i] > 0;
+        if (a.status_out) a.status_out[i] = (uint8_t)((vis ? 1u : 0u) | (!a.hot || a.hot[i] != 0u ? 2u : 0u));
+        if (!a.radii || !vis) return;
         // max_radii2D[vis] = max(max_radii2D[vis], radii[vis]) (float result: radii promote to float)
         const float r = (float)a.radii[i];
         const float mr = a.max_radii2D[i];
@@ -121,13 +124,20 @@ __global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const bool in = e0 + j < total;
-            vis[c][j] = in && (a.visible ? a.visible[gi] != 0 : a.vis_radii[gi] > 0);
+            if (a.status) {
+                const uint32_t st = in ? a.status[gi] : 0u;
+                vis[c][j] = (st & 1u) != 0u;
+                hot |= (st & 2u) != 0u;
+            } else {
+                vis[c][j] = in && (a.visible ? a.visible[gi] != 0 : a.vis_radii[gi] > 0);
+                if (a.hot && in) hot |= a.hot[gi] != 0u;
+            }
             act[c] |= vis[c][j];
-            if (a.hot && in) hot |= a.hot[gi] != 0u;
             if (++r == g.M) { r = 0; gi++; }
         }
         if (!act[c]) continue;
-        const bool zero_grad = a.hot && !hot;  // no binned row in the chunk: its rasterizer gradient is zero
+        // no binned row in the chunk: its rasterizer gradient is zero
+        const bool zero_grad = a.status ? !hot : (a.hot && !hot);
         full[c] = g.vec && e0 + 4 <= total;
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
         if (full[c]) {
@@ -208,6 +218,14 @@ __global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
         }
     }
 }
+
+// A full grid (one work block per block), or -- grid_cap, the native step's overlapped SH update -- a capped grid that
+// strides over the work blocks, leaving compute units to the stream it overlaps (a full-grid update filled every CU
+// and held the next forward's one-block depth cut back ~150 us).
+__global__ void __launch_bounds__(256) k_adam_multi(AdamMultiArgs a) {
+    for (uint32_t blk = blockIdx.x; blk < a.nblocks; blk += gridDim.x) adam_block(a, blk);
+}
+
 
 // ---- densify_and_prune
 
@@ -445,9 +463,10 @@ void launch_adam_multi(const AdamMultiArgs& a0, hipStream_t s) {
         b += (uint32_t)((items + 256 * ADAM_CHUNKS - 1) / (256 * ADAM_CHUNKS));
     }
     a.start[a.n] = b;
-    if (a.radii) b += (a.N + 255) / 256;
+    if (a.radii || a.status_out) b += (a.N + 255) / 256;
     if (b == 0) return;
-    k_adam_multi<<<b, 256, 0, s>>>(a);
+    a.nblocks = b;
+    k_adam_multi<<<a.grid_cap && a.grid_cap < b ? a.grid_cap : b, 256, 0, s>>>(a);
 }
 
 void launch_densify_select(const DensifyArgs& a, hipStream_t s) {

@@ -196,9 +196,9 @@ struct BinArgs {
     uint32_t *first_e, *rcnt;
     uint32_t *eg, *ikey;         // per instance: Gaussian, depth key
     uint8_t* flag;               // per instance: the backward's record-written flag, zeroed here
-    // phase 2 only: an extra block of the emission launch computes the backward's longest-first replay order (on the
-    // otherwise latency-bound phase-2 tail, instead of a backward prologue launch)
-    // colour of the binned Gaussians (computeColorFromSH), written by k_bin_emit
+    // colour of the binned Gaussians (computeColorFromSH), written by k_bin_emit -- or, colors_later (phase 1, the
+    // native step's overlapped SH update), by launch_binned_colors after the emission
+    int colors_later;
     int D, M;
     const float *means3D, *campos, *dc, *sh, *colors;
     float4* rgbi;
@@ -210,7 +210,10 @@ struct BinArgs {
     int unf_th;                  // tile rows
     uint32_t* probe;             // optional (phase 2, adaptive capacity): [0] <- counters[CNT_UNFINISHED]
 };
-void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s);
+void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s,
+                hipEvent_t wait_before_emit = nullptr);
+// rgbi of the phase-1 Gaussians that got instances (rcnt > 0, key < thr), for an emission run with colors_later
+void launch_binned_colors(const BinArgs& a, hipStream_t s);
 size_t bin_scan_temp_bytes(int P);
 int bin_waves(int P);
 // probe (optional, device): receives counters[CNT_UNFINISHED] (read back by the next view's k_depth_cut)

@@ -581,6 +581,29 @@ __global__ void __launch_bounds__(256) k_bin_count(BinArgs a) {
     if (lane == 0) a.wtot[wave] = tot;
 }
 
+// colour + inverse depth of a binned Gaussian (computeColorFromSH, forward.cu:24-76; 1 / view z)
+__device__ __forceinline__ void binned_colour(const BinArgs& a, int g, uint32_t key) {
+    f3 col;
+    if (a.colors) {
+        col = {a.colors[3 * g], a.colors[3 * g + 1], a.colors[3 * g + 2]};
+    } else {
+        const f3 po = {a.means3D[3 * g], a.means3D[3 * g + 1], a.means3D[3 * g + 2]};
+        const f3 d0 = {a.dc[3 * g], a.dc[3 * g + 1], a.dc[3 * g + 2]};
+        col = sh_to_rgb(po, a.campos, a.sh ? a.D : 0, d0, a.sh ? a.sh + (size_t)g * a.M * 3 : nullptr, nullptr);
+    }
+    a.rgbi[g] = make_float4(col.x, col.y, col.z, 1.f / __uint_as_float(key));
+}
+
+// colors_later: the phase-1 members that got instances, a Gaussian per lane (the emission's colour, launched after
+// the overlapped SH update it reads)
+__global__ void __launch_bounds__(256) k_binned_colors(BinArgs a) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= a.P || a.rcnt[g] == 0u) return;
+    const uint32_t key = a.dkey[g];
+    if (key == 0xffffffffu || key >= a.counters[CNT_THR]) return;  // phase 2's members get theirs from emit<2>
+    binned_colour(a, g, key);
+}
+
 // Pass 2: wave base = exclusive scan of the wave totals (wtot, scanned in place); first_e of every binned
 // Gaussian, and a second walk writes its instances (Gaussian, depth key) at consecutive indices in (lane, ty, tx)
 // order, so every Gaussian's instances are contiguous: [first_e, first_e + rcnt); each instance index is also
@@ -611,17 +634,7 @@ __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
     if (wt == 0u || base + wt > a.cap) return;  // nothing kept; (capacity: never with consistent inputs)
     if (b.member && c) {
         a.first_e[g] = (PHASE == 2 ? a.counters[CNT_E1] : 0u) + base + incl - c;
-        // colour + inverse depth of a binned Gaussian (computeColorFromSH, forward.cu:24-76; 1 / view z)
-        const uint32_t key = s_key[w][lane];
-        f3 col;
-        if (a.colors) {
-            col = {a.colors[3 * g], a.colors[3 * g + 1], a.colors[3 * g + 2]};
-        } else {
-            const f3 po = {a.means3D[3 * g], a.means3D[3 * g + 1], a.means3D[3 * g + 2]};
-            const f3 d0 = {a.dc[3 * g], a.dc[3 * g + 1], a.dc[3 * g + 2]};
-            col = sh_to_rgb(po, a.campos, a.sh ? a.D : 0, d0, a.sh ? a.sh + (size_t)g * a.M * 3 : nullptr, nullptr);
-        }
-        a.rgbi[g] = make_float4(col.x, col.y, col.z, 1.f / __uint_as_float(key));
+        if (PHASE == 2 || !a.colors_later) binned_colour(a, g, s_key[w][lane]);
     }
     uint32_t running = 0;
     wave_candidates(s_cand[w], lane, b.x0, b.y0, b.x1, b.y1, b.mx, b.my, b.co, b.lthr,
@@ -782,15 +795,7 @@ __global__ void __launch_bounds__(256) k_bin_emit_fat(BinArgs a) {
         if (base + running + wt > a.cap) return;  // (capacity: never with consistent inputs)
         if (member && c) {
             a.first_e[g] = e_off + base + running + incl - c;
-            f3 col;
-            if (a.colors) {
-                col = {a.colors[3 * g], a.colors[3 * g + 1], a.colors[3 * g + 2]};
-            } else {
-                const f3 po = {a.means3D[3 * g], a.means3D[3 * g + 1], a.means3D[3 * g + 2]};
-                const f3 d0 = {a.dc[3 * g], a.dc[3 * g + 1], a.dc[3 * g + 2]};
-                col = sh_to_rgb(po, a.campos, a.sh ? a.D : 0, d0, a.sh ? a.sh + (size_t)g * a.M * 3 : nullptr, nullptr);
-            }
-            a.rgbi[g] = make_float4(col.x, col.y, col.z, 1.f / __uint_as_float(key));
+            if (PHASE == 2 || !a.colors_later) binned_colour(a, g, key);
         }
         __builtin_amdgcn_wave_barrier();
         if (wt) {
@@ -1558,7 +1563,7 @@ void launch_depth_cut(const uint32_t* hist, uint32_t cap, uint32_t* counters, ui
                       hipStream_t s) {
     k_depth_cut<<<1, 1024, 0, s>>>(hist, cap, counters, tile_cnt, tile_cnt2, num_tiles, rect_part, nparts, probe);
 }
-void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s) {
+void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s, hipEvent_t wait_before_emit) {
     if (a.P <= 0) return;
     const bool fat = phase == 1 ? DG_BIN_FAT1 > 1 : DG_BIN_FAT2 > 1;
     const int span = fat ? (phase == 1 ? fat_span<1>() : fat_span<2>()) : EMIT_RANKS;
@@ -1571,16 +1576,21 @@ void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hi
     } else if (phase == 2) k_bin_count<2><<<blocks, 256, 0, s>>>(a);
     else k_bin_count<1><<<blocks, 256, 0, s>>>(a);
     if ((uint32_t)waves <= BIN_OFFSETS_MAX_N) {  // one launch: wave offsets + tile ranges, tile_cnt -> 0 (cursors)
-        bin_offsets(a.wtot, (uint32_t)waves, total, a.tile_cnt, (uint32_t)a.num_tiles, a.ranges, s, gate);
+        bin_offsets(a.wtot, (uint32_t)waves, total, a.tile_cnt, (uint32_t)a.num_tiles, a.ranges, s, gate,
+                    a.colors_later != 0);
     } else {
         exclusive_scan(a.wtot, (uint32_t)waves, a.wtot, total, scan_tmp, s, gate);
         tile_offsets(a.tile_cnt, (uint32_t)a.num_tiles, a.ranges, s, gate);
     }
+    if (wait_before_emit) (void)hipStreamWaitEvent(s, wait_before_emit, 0);  // the emission reads the SH rows
     if (fat) {
         if (phase == 2) k_bin_emit_fat<2><<<blocks, 256, 0, s>>>(a);
         else k_bin_emit_fat<1><<<blocks, 256, 0, s>>>(a);
     } else if (phase == 2) k_bin_emit<2><<<blocks, 256, 0, s>>>(a);
     else k_bin_emit<1><<<blocks, 256, 0, s>>>(a);
+}
+void launch_binned_colors(const BinArgs& a, hipStream_t s) {
+    if (a.P > 0) k_binned_colors<<<(a.P + 255) / 256, 256, 0, s>>>(a);
 }
 size_t bin_scan_temp_bytes(int P) { return scan_temp_bytes((uint32_t)((P + EMIT_RANKS - 1) / EMIT_RANKS)); }
 int bin_waves(int P) { return (P + EMIT_RANKS - 1) / EMIT_RANKS; }

@@ -32,7 +32,7 @@ void tile_offsets(uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges, hipStre
 // exclusive_scan + tile_offsets).  gate as above (*total = 0 when gated).
 constexpr uint32_t BIN_OFFSETS_MAX_N = 65536;
 void bin_offsets(uint32_t* wtot, uint32_t n, uint32_t* total, uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges,
-                 hipStream_t stream, const uint32_t* gate = nullptr);
+                 hipStream_t stream, const uint32_t* gate = nullptr, bool small_blocks = false);
 
 // Per-tile sort of instance lists into (depth key, Gaussian index) order (sortscan.hip k_tile_dsort):
 // s_e[ranges[t].x .. ranges[t].y) is reordered in place by (ikey[v], eg[v]), whatever its input order.

@@ -403,11 +403,13 @@ void tile_offsets(uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges, hipStre
 // BO_ROUNDS rounds are issued before the first scan (one HBM round trip per 16384 items instead of one per round:
 // a 1e6-Gaussian view has 15625 wave totals, so the whole scan waits on memory once).
 constexpr int BO_ROUNDS = 4;
-__global__ void __launch_bounds__(1024) k_bin_offsets(uint32_t* __restrict__ wtot, uint32_t n,
+template <int NT>
+__global__ void __launch_bounds__(NT) k_bin_offsets(uint32_t* __restrict__ wtot, uint32_t n,
                                                       uint32_t* __restrict__ total, uint32_t* __restrict__ tile_cnt,
                                                       uint32_t num_tiles, uint2* __restrict__ ranges,
                                                       const uint32_t* __restrict__ gate) {
-    __shared__ uint32_t s_w[16];
+    constexpr int NW = NT / 64;
+    __shared__ uint32_t s_w[NW];
     __shared__ uint32_t s_carry;
     const bool tiles = blockIdx.x == 1;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -419,17 +421,17 @@ __global__ void __launch_bounds__(1024) k_bin_offsets(uint32_t* __restrict__ wto
     uint32_t* src = tiles ? tile_cnt : wtot;
     if (t == 0) s_carry = 0u;
     __syncthreads();
-    for (uint32_t sb = 0; sb < N; sb += 4096u * BO_ROUNDS) {
+    for (uint32_t sb = 0; sb < N; sb += (4u * NT) * BO_ROUNDS) {
       uint32_t pv[BO_ROUNDS][4];
 #pragma unroll
       for (int r = 0; r < BO_ROUNDS; r++) {
-          const uint32_t i0 = sb + 4096u * r + 4u * (uint32_t)t;
+          const uint32_t i0 = sb + (4u * NT) * r + 4u * (uint32_t)t;
 #pragma unroll
           for (int k = 0; k < 4; k++) pv[r][k] = i0 + k < N ? src[i0 + k] : 0u;
       }
 #pragma unroll
       for (int r = 0; r < BO_ROUNDS; r++) {
-        const uint32_t b = sb + 4096u * r;
+        const uint32_t b = sb + (4u * NT) * r;
         if (b >= N) break;  // block-uniform
         const uint32_t i0 = b + 4u * (uint32_t)t;
         const uint32_t* v = pv[r];
@@ -444,7 +446,7 @@ __global__ void __launch_bounds__(1024) k_bin_offsets(uint32_t* __restrict__ wto
         __syncthreads();
         uint32_t off = s_carry, tot = 0;
 #pragma unroll
-        for (int k = 0; k < 16; k++) { if (k < w) off += s_w[k]; tot += s_w[k]; }
+        for (int k = 0; k < NW; k++) { if (k < w) off += s_w[k]; tot += s_w[k]; }
         uint32_t ex = off + x - loc;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -463,8 +465,11 @@ __global__ void __launch_bounds__(1024) k_bin_offsets(uint32_t* __restrict__ wto
 }
 
 void bin_offsets(uint32_t* wtot, uint32_t n, uint32_t* total, uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges,
-                 hipStream_t stream, const uint32_t* gate) {
-    k_bin_offsets<<<2, 1024, 0, stream>>>(wtot, n, total, tile_cnt, num_tiles, ranges, gate);
+                 hipStream_t stream, const uint32_t* gate, bool small_blocks) {
+    // small_blocks: 256-thread blocks (more rounds), which find room beside another stream's kernel (the native step's
+    // overlapped update kept a 1024-thread block of this launch waiting until it ended)
+    if (small_blocks) k_bin_offsets<256><<<2, 256, 0, stream>>>(wtot, n, total, tile_cnt, num_tiles, ranges, gate);
+    else k_bin_offsets<1024><<<2, 1024, 0, stream>>>(wtot, n, total, tile_cnt, num_tiles, ranges, gate);
 }
 
 // One wave per tile, lists up to DS_WAVE_MAX2 (16 items per lane); min_n: only lists longer than that (the phase-1

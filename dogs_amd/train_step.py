@@ -28,10 +28,15 @@ class NativeTrainStep:
     {max_radii2D, grad_accum, denom} updated each step (gaussian_trainer.py:433-438)."""
 
     def __init__(self, params: dict, opt, cameras: list, images: list, sh_degree: int, lambda_dssim: float,
-                 lambda_scale: float, bg: torch.Tensor, device: torch.device, stats: dict | None = None):
+                 lambda_scale: float, bg: torch.Tensor, device: torch.device, stats: dict | None = None,
+                 overlap: bool = False):
         self.L = _lib.load()
         self.device = device
-        self.arena = _lib.ReuseArena(device)
+        # overlap: each step returns with its f_dc / f_rest update still running on a side stream; the next step waits
+        # for it before its binning emission (the first launch reading them) -- call sync() before anything else
+        # touches those tensors or their Adam moments (rebind() does)
+        self.overlap = bool(overlap) and hasattr(self.L, "dg_train_sync")
+        self.arena = _lib.ReuseArena(device, keep_retired=self.overlap)
         self.lambdas = (float(lambda_dssim), float(lambda_scale))
         self.sh_degree = int(sh_degree)
         self.loss_buf = torch.zeros(3, dtype=torch.float32, device=device)
@@ -51,6 +56,7 @@ class NativeTrainStep:
         """(Re)build the argument blocks from the current tensors: after densify_and_prune, reset_opacity, a prune or
         optimizer.load_state_dict replaced the parameters or their Adam moments.  params: {C_ORDER name: tensor}
         (None: the optimizer's current group tensors); stats: the densification statistics (None: none)."""
+        self.sync()
         opt, device = self.opt, self.device
         groups = {g["name"]: g for g in opt.param_groups}
         if params is None:
@@ -60,6 +66,7 @@ class NativeTrainStep:
         M = int(rest.shape[1]) if rest.dim() == 3 else 0
         self.params = params
         self.radii = torch.zeros(P, dtype=torch.int32, device=device)
+        self.sh_status = torch.zeros(P, dtype=torch.uint8, device=device) if self.overlap else None
         for n in C_ORDER:
             p = params[n]
             if not (p.is_contiguous() and p.dtype == torch.float32 and p.device == device):
@@ -108,6 +115,7 @@ class NativeTrainStep:
                 self.images_out[key] = torch.empty((3, key[0], key[1]), dtype=torch.float32, device=device)
             a.radii, a.image, a.loss = self.radii.data_ptr(), self.images_out[key].data_ptr(), self.loss_buf.data_ptr()
             a.stats = C.addressof(self.stats) if self.stats is not None else None
+            a.sh_status = self.sh_status.data_ptr() if self.sh_status is not None else None
             self.args.append(a)
 
     def _pointers(self) -> tuple:
@@ -149,6 +157,12 @@ class NativeTrainStep:
             a.prox[i].u, a.prox[i].z, a.prox[i].coef = u.data_ptr(), z.data_ptr(), float(coef)
         _lib.check(self.L.dg_train_step(C.byref(a), self.arena.fn, None, self.stream))
         self.last_view = k
+
+    def sync(self) -> None:
+        """Order the current stream after an overlapped f_dc / f_rest update (no-op without one)."""
+        if getattr(self, "overlap", False):
+            _lib.check(self.L.dg_train_sync(self.stream))
+            self.arena.release_retired()
 
     def image(self, k: int | None = None) -> torch.Tensor:
         """The clamped render of the last step (shared buffer per image size)."""

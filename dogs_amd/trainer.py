@@ -84,9 +84,14 @@ class GaussianSplatTrainer:
     on the device; images: [3,H,W] float targets (same order); bounding_box: the scene's [6] box or None."""
 
     def __init__(self, model: GaussianSplatModel, cameras: list, images: list, cfg: GSTrainConfig | None = None,
-                 device=None, seed: int = 0, native: bool = True, bounding_box=None, normal=torch.normal):
+                 device=None, seed: int = 0, native: bool = True, bounding_box=None, normal=torch.normal,
+                 overlap: bool = True):
         from .diff_gaussian_rasterization import SparseGaussianAdam
         self.cfg = c = cfg or GSTrainConfig()
+        # overlap: native steps return with their f_dc / f_rest update still running on a side stream (NativeTrainStep);
+        # the autograd-route iterations and train()'s end call sync() first -- call it before reading the model
+        # after train_iteration() yourself
+        self.overlap = overlap
         self.model = model
         self.device = torch.device(device) if device is not None else model.get_xyz.device
         self.cameras, self.images = cameras, images
@@ -129,7 +134,7 @@ class GaussianSplatTrainer:
             if self._nts is None:
                 self._nts = NativeTrainStep(params, self.optimizer, self.cameras, self.images, m.active_sh_degree,
                                             self.cfg.lambda_dssim, self.cfg.lambda_scale, self.bg, self.device,
-                                            stats=self._stats() if want_stats else None)
+                                            stats=self._stats() if want_stats else None, overlap=self.overlap)
             else:
                 self._nts.rebind(params, self._stats() if want_stats else None)
             self._nts_stats = want_stats
@@ -184,6 +189,7 @@ class GaussianSplatTrainer:
             self.last_loss = None
             log = IterationLog(self.iteration, "native", self.model.num_gaussians)
         else:
+            self.sync()
             self._autograd_iteration(k, ev)
             log = IterationLog(self.iteration, "autograd", self.model.num_gaussians, ev)
         self.logs.append(log)
@@ -234,8 +240,15 @@ class GaussianSplatTrainer:
             return self._nts.loss()
         return self.last_loss
 
+    def sync(self) -> None:
+        """Order the current stream after the native step's overlapped SH update (overlap=True), so that the model's
+        tensors and Adam moments can be read or replaced; train() ends with it."""
+        if self._nts is not None:
+            self._nts.sync()
+
     def train(self, iterations: int | None = None) -> None:
         """ImplicitReconTrainer.train's loop (checkpoints, validation and logging are not on the path)."""
         end = self.cfg.max_iterations if iterations is None else self.iteration + iterations
         while self.iteration < end:
             self.train_iteration()
+        self.sync()

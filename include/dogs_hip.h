@@ -189,8 +189,15 @@ typedef struct {
     int* radii;                 /* [P] out */
     float* image;               /* [3,H,W] out: the clamped render */
     float* loss;                /* optional, device [3] out: L1, SSIM, mean prod(scaling) of this view */
+    /* optional [P] device scratch: overlap the f_dc / f_rest part of the update (81% of its bytes) with the NEXT
+     * step's forward up to its binning emission, the first kernel that reads them.  The call returns with that part
+     * still running on a side stream; the next dg_train_step on the same stream waits for it before its emission, and
+     * any other use of the SH tensors or their moments needs dg_train_sync first. */
+    uint8_t* sh_status;
 } dg_train_step_args;
 int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg_stream_t stream);
+/* Make `stream` wait for an overlapped f_dc / f_rest update of the last dg_train_step on it (no-op when none). */
+int dg_train_sync(dg_stream_t stream);
 /* The statistics alone (replaces the max_radii2D update + add_densification_stats of gaussian_trainer.py:433-438). */
 int dg_add_densification_stats(const dg_densify_stats* stats, const uint8_t* visible, uint32_t N, dg_stream_t stream);
 

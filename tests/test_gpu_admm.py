@@ -147,10 +147,11 @@ def test_native_step_folded_update_bitwise(hip_device, monkeypatch, n, W, H):
     """dg_train_step's default route -- the activations' backward folded into the update, and the chunks touching no
     binned row skipping the (zero) gradient reads -- gives bit-identical parameters, moments and densification
     statistics to the unfused route (k_activate_bwd, then the plain update: DG_TRAIN_UNFUSED=1), three iterations with
-    a perturbed ADMM state (proximal gradient on)."""
+    a perturbed ADMM state (proximal gradient on).  So does the overlapped route (NativeTrainStep(overlap=True): the
+    f_dc / f_rest update of each step on a side stream, beside the next step's forward until its emission)."""
     from dogs_amd.admm import PARAM_NAMES
     from dogs_amd.train_step import NativeTrainStep
-    routes = {"folded": None, "unfused": "DG_TRAIN_UNFUSED"}
+    routes = {"folded": None, "unfused": "DG_TRAIN_UNFUSED", "overlap": None}
     tr, stats = {}, {}
     for name in routes:
         t, _, _ = _small_block(hip_device, n=n, W=W, H=H, native=True)
@@ -161,20 +162,24 @@ def test_native_step_folded_update_bitwise(hip_device, monkeypatch, n, W, H):
         c = t.cfg
         t._nts = NativeTrainStep({nm: t.params[nm] for nm in PARAM_NAMES}, t.opt, t.cameras, t.images, c.sh_degree,
                                  c.lambda_dssim, c.lambda_scale, torch.tensor(c.background, dtype=torch.float32),
-                                 hip_device, stats=stats[name])
+                                 hip_device, stats=stats[name], overlap=name == "overlap")
         tr[name] = t
-    for _ in range(3):
+    assert tr["overlap"]._nts.overlap
+    for it in range(4):
         for name, env in routes.items():
             monkeypatch.delenv("DG_TRAIN_UNFUSED", raising=False)
             if env:
                 monkeypatch.setenv(env, "1")
             tr[name].local_step()
-        torch.cuda.synchronize()
+        if it != 1:  # one round left pending across the next step's forward without a device sync in between
+            torch.cuda.synchronize()
+    tr["overlap"]._nts.sync()
+    torch.cuda.synchronize()
     monkeypatch.delenv("DG_TRAIN_UNFUSED", raising=False)
     ref = tr["unfused"]
     vis = ref.last_radii > 0
     assert int(vis.sum()) > 100 and int((~vis).sum()) > 0
-    for name in ("folded",):
+    for name in ("folded", "overlap"):
         t = tr[name]
         assert torch.equal(t.last_radii, ref.last_radii)
         for nm in PARAM_NAMES:

@@ -124,6 +124,40 @@ def test_backward_huge_splats(oracle, hip_device, prefix_policy):
     assert int(st.geom()["tiles_touched"].max()) > 256
 
 
+@pytest.mark.parametrize("seed", [3, 4])
+def test_tight_walk_thin_and_faint(oracle, hip_device, seed):
+    """The binning walks enumerate only the tiles of the contribution ellipse's bounding box (raster_fwd.hip
+    tight_rect): on needle-thin rotated splats (scales 30x and 0.03x of the scene's), faint ones around the alpha
+    1/255 cut (opacity 0.5/255 .. 4/255) and opaque ones, the binned instance list must still be the reference's,
+    instance for instance, with everything binned in one phase."""
+    from dogs_amd.diff_gaussian_rasterization import _C
+    n, W, H = 4000, 320, 240
+    s = small_scene(n, W, H, seed=seed)
+    g = torch.Generator().manual_seed(seed)
+    thin = torch.rand(n, generator=g) < 0.5
+    k = torch.ones((n, 3))
+    k[thin, 0] = 30.0
+    k[thin, 1] = 0.03
+    s.scales = (s.scales * k).contiguous()
+    faint = torch.rand(n, generator=g) < 0.3
+    op = s.opacities.clone()
+    op[faint, 0] = (0.5 + 3.5 * torch.rand(int(faint.sum()), generator=g)) / 255.0
+    s.opacities = op.contiguous()
+    old = _C.set_prefix_per_tile(-1)
+    try:
+        col_o, radii_o, inv_o, st = oracle_forward(oracle, s, (0, 0, 0), deg=3)
+        out = hip_forward(s, (0, 0, 0), hip_device, deg=3)
+        assert int(out[0]) == st.num_rendered
+        t_o, i_o, _ = st.sorted_list()
+        t_h, i_h, e1 = hip_sorted_instances(out, W, H, hip_device, n)
+        assert e1 == len(t_h) == st.num_valid
+        np.testing.assert_array_equal(t_h, t_o)
+        np.testing.assert_array_equal(i_h, i_o)
+        assert psnr(out[2].cpu().numpy(), col_o) > 80.0
+    finally:
+        _C.set_prefix_per_tile(old)
+
+
 @pytest.mark.parametrize("n,W,H,mode", [(3000, 256, 192, "clones"), (600, 64, 48, "planar"),
                                         (20000, 128, 96, "dense-clones")])
 @pytest.mark.parametrize("prefix", [0, 2, -1], ids=["prefix-default", "prefix-2-per-tile", "no-prefix"])
