@@ -339,9 +339,10 @@ def admm_leg(args, ws, rank, dev, n, W, H):
     from dogs_amd.admm import ADMMConfig
     from dogs_amd.admm_trainer import barrier_time, distributed_trainer, sequential_trainer
     cfg = ADMMConfig(consensus_interval=args.admm_interval)
-    tr, cons, run = distributed_trainer(rank, ws, n, W, H, args.views, args.shared_frac, dev, admm=cfg)
+    tr, cons, run = distributed_trainer(rank, ws, n, W, H, args.views, args.shared_frac, dev, admm=cfg, overlap=True)
     for _ in range(min(args.views, 8)):   # warm-up: allocator, adaptive capacity
         tr.local_step()
+    tr.sync()   # the overlapped update before the parameters are read
     ps = tuple(p.detach() for p in tr.param_tuple())
     run.cons.residuals(ps, run.cons.consensus(ps), ps, tr.admm.rho)   # communicator / buffer setup
     del ps
@@ -366,10 +367,12 @@ def admm_leg(args, ws, rank, dev, n, W, H):
         if ws > 1:
             dist.barrier()
         if rank == 0:
-            blocks, seq = sequential_trainer(nseq, n, W, H, args.views, args.shared_frac, dev, admm=cfg)
+            blocks, seq = sequential_trainer(nseq, n, W, H, args.views, args.shared_frac, dev, admm=cfg, overlap=True)
             for b in blocks:
                 for _ in range(min(args.views, 8)):
                     b.local_step()
+            for b in blocks:
+                b.sync()
             ps = [tuple(p.detach() for p in b.param_tuple()) for b in blocks]
             seq.cons.residuals(ps, seq.cons.consensus(ps), ps, blocks[0].admm.rho)   # warm-up of the exchange
             del ps

@@ -130,7 +130,7 @@ class BlockTrainer:
 
     def __init__(self, raw: dict, cameras: list, images: list, num_global: int, admm: ADMMConfig,
                  cfg: TrainConfig | None = None, device: torch.device | None = None, seed: int = 0,
-                 native: bool = True, rho_gaussians: int | None = None):
+                 native: bool = True, rho_gaussians: int | None = None, overlap: bool = False):
         from .diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer, SparseGaussianAdam
         from .activations import activate
         from .fused_ssim import fused_ssim
@@ -161,8 +161,12 @@ class BlockTrainer:
         self.native = native
         if native:
             from .train_step import NativeTrainStep
+            # overlap: the f_dc / f_rest update of each local step runs beside the next one's forward
+            # (NativeTrainStep); ADMMRunner / SequentialADMM synchronise the device before the consensus reads the
+            # parameters, and penalty() syncs
             self._nts = NativeTrainStep({n: self.params[n] for n in PARAM_NAMES}, self.opt, cameras, images,
-                                        c.sh_degree, c.lambda_dssim, c.lambda_scale, bg, self.device)
+                                        c.sh_degree, c.lambda_dssim, c.lambda_scale, bg, self.device,
+                                        overlap=overlap)
 
     @property
     def last_loss(self):
@@ -223,7 +227,13 @@ class BlockTrainer:
         self._last_loss = loss.detach()
         return self._last_loss
 
+    def sync(self) -> None:
+        """Order the current stream after an overlapped update (overlap=True) before reading the block's tensors."""
+        if self.native:
+            self._nts.sync()
+
     def penalty(self) -> torch.Tensor:
+        self.sync()
         return self.admm.penalty(self.param_tuple())
 
 
@@ -385,7 +395,8 @@ def chain_block_indices(k: int, n: int, shared_frac: float) -> tuple[torch.Tenso
 
 
 def make_block(k: int, num_blocks: int, n: int, W: int, H: int, views: int, shared_frac: float, device,
-               seed: int = 1234, admm: ADMMConfig | None = None, cfg: TrainConfig | None = None, native: bool = True):
+               seed: int = 1234, admm: ADMMConfig | None = None, cfg: TrainConfig | None = None, native: bool = True,
+               overlap: bool = False):
     """Block k of a synthetic chain split: the BASELINE generator's scene (one global scene, seed `seed`, of
     num_global Gaussians; block k takes its rows), `views` seeded yaw cameras and random target images."""
     from .camera import make_camera, yaw_world_to_camera
@@ -407,27 +418,29 @@ def make_block(k: int, num_blocks: int, n: int, W: int, H: int, views: int, shar
             for y in yaws]
     g = torch.Generator().manual_seed(seed + 7 + k)
     images = [torch.rand((3, H, W), generator=g).to(device) for _ in yaws]
-    tr = BlockTrainer(raw, cams, images, num_global, admm or ADMMConfig(), cfg, device, seed=seed + k, native=native)
+    tr = BlockTrainer(raw, cams, images, num_global, admm or ADMMConfig(), cfg, device, seed=seed + k, native=native,
+                      overlap=overlap)
     return tr, gidx, num_global
 
 
 def distributed_trainer(rank: int, world: int, n: int, W: int, H: int, views: int, shared_frac: float, device,
-                        admm: ADMMConfig | None = None, seed: int = 1234, group=None):
+                        admm: ADMMConfig | None = None, seed: int = 1234, group=None, overlap: bool = False):
     """This rank's block of a world-size chain split, its BlockConsensus and its ADMMRunner."""
     admm = admm or ADMMConfig()
-    tr, gidx, num_global = make_block(rank, world, n, W, H, views, shared_frac, device, seed, admm)
+    tr, gidx, num_global = make_block(rank, world, n, W, H, views, shared_frac, device, seed, admm, overlap=overlap)
     cons = BlockConsensus(gidx.to(device), num_global, group=group, device=device)
     run = ADMMRunner(tr.param_tuple, tr.admm, cons, tr.local_step, admm, tr.iteration)
     return tr, cons, run
 
 
 def sequential_trainer(num_blocks: int, n: int, W: int, H: int, views: int, shared_frac: float, device,
-                       admm: ADMMConfig | None = None, seed: int = 1234):
+                       admm: ADMMConfig | None = None, seed: int = 1234, overlap: bool = False):
     admm = admm or ADMMConfig()
     blocks, gidxs = [], []
     num_global = None
     for k in range(num_blocks):
-        tr, gidx, num_global = make_block(k, num_blocks, n, W, H, views, shared_frac, device, seed, admm)
+        tr, gidx, num_global = make_block(k, num_blocks, n, W, H, views, shared_frac, device, seed, admm,
+                                          overlap=overlap)
         blocks.append(tr)
         gidxs.append(gidx)
     seq = SequentialADMM([b.local_step for b in blocks], [b.admm for b in blocks], [b.param_tuple for b in blocks],

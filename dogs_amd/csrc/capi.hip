@@ -843,6 +843,9 @@ int dg_rasterize_filter(const dg_raster_args* a, int* radii, dg_stream_t stream)
 
 // The native step's overlapped SH update (dg_train_step_args::sh_status): per caller stream, a side stream and the
 // event its f_dc / f_rest update records; `pending` until a later step (or dg_train_sync) made the stream wait on it.
+}  // extern "C"
+
+namespace {
 // blocks of the side launch: few enough that the overlapped forward's kernels find free compute units
 uint32_t sh_grid_cap() {
     static const uint32_t v = [] {
@@ -876,6 +879,9 @@ ShOverlap* sh_state(hipStream_t s, bool create) {
         return nullptr;
     return &(mp[s] = o);
 }
+}  // namespace
+
+extern "C" {
 
 static int fill_stats(gs::AdamMultiArgs& m, const dg_densify_stats* st) {
     if (!st) return 0;
