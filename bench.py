@@ -664,6 +664,8 @@ def main():
                                          "visible_gaussians", "binned_gaussians", "live_gaussians")} for r in vstats],
             "roofline": roof,
             "phases_ms": {k: round(v, 4) for k, v in sorted(phase_ms.items(), key=lambda kv: -kv[1])},
+            "phases_note": "per-phase hipEvent times from a separate, untimed pass over the same views (event records "
+                           "between phases serialise the queue, so their sum exceeds ms_per_step)",
             "cpu_baseline": cpu,
             "train_step": train,
             "admm": admm,

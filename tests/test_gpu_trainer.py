@@ -237,3 +237,32 @@ def test_underflowed_scale_has_finite_regulariser_gradient(hip_device):
     a, b = (t.params["scaling"].detach() for t in trs)
     assert bool(torch.isfinite(a).all()) and bool(torch.isfinite(b).all())
     torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_overlapped_update_is_bitwise_the_serial_one(hip_device):
+    """GaussianSplatTrainer(overlap=True) -- each native step's f_dc / f_rest update on a side stream beside the next
+    step's forward -- ends with the same model, Adam state and statistics bit for bit as overlap=False, through a
+    densification and an opacity reset (autograd-route iterations in between sync first)."""
+    from dogs_amd.trainer import GaussianSplatTrainer
+    dev = hip_device
+    cfg = _cfg(max_iterations=90, densify_start_iter=30, densification_interval=40, opacity_reset_interval=60,
+               prune_iterations=(), sh_increase_interval=25)
+    out = []
+    for overlap in (False, True):
+        m, cams, gts = _problem(dev, n_true=20_000, n_init=4_000, W=320, H=240, views=4)
+        tr = GaussianSplatTrainer(m, cams, gts, cfg, device=dev, seed=3, native=True, normal=_normal(dev, 11),
+                                  overlap=overlap)
+        tr.train()
+        assert tr._nts.overlap == overlap
+        opt = {g["name"]: tr.optimizer.state[g["params"][0]] for g in tr.optimizer.param_groups}
+        out.append((_model_raw(m), {k: (v["exp_avg"].clone(), v["exp_avg_sq"].clone()) for k, v in opt.items()},
+                    (m.max_radii2D.clone(), m.xyz_gradient_accum.clone(), m.denom.clone()),
+                    [lg.route for lg in tr.logs]))
+    (r0, o0, s0, l0), (r1, o1, s1, l1) = out
+    assert l0 == l1 and l0.count("autograd") >= 2
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k
+    for k in o0:
+        assert torch.equal(o0[k][0], o1[k][0]) and torch.equal(o0[k][1], o1[k][1]), k
+    for a, b in zip(s0, s1):
+        assert torch.equal(a, b)
