@@ -543,7 +543,7 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     pre.unf_words = UNF_ROWS ? (ty + 1) * unf_rw_of(tx) + (ty + 63) / 64 : 0;  // rows, column OR, row summary
     // per-block rect sums land in the wave-total array (ceil(P/64) u32 >= ceil(P/256) u64), free until the binning
     pre.rect_part = reinterpret_cast<unsigned long long*>(g.wtot); pre.err = g.counters + gs::CNT_ERR;
-    const uint32_t nparts = (uint32_t)((P + 255) / 256);
+    const uint32_t nparts = gs::preprocess_blocks(P);
     { PROF("preprocess"); gs::launch_preprocess(pre, s); }
     DBG_SYNC(a->debug, s);
 

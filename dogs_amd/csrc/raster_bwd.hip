@@ -568,6 +568,9 @@ __global__ void __launch_bounds__(256) k_gauss_sum(GaussBwdArgs a, uint32_t sum_
 #define DG_LIVE_CHUNKS 16
 #endif
 constexpr int LIVE_CHUNKS = DG_LIVE_CHUNKS;
+// the chunk-count prefix below is one wave's scan (64 lanes) and the lookup a binary search over it
+static_assert(LIVE_CHUNKS >= 1 && LIVE_CHUNKS <= 64 && (LIVE_CHUNKS & (LIVE_CHUNKS - 1)) == 0,
+              "DG_LIVE_CHUNKS: a power of two up to 64");
 __global__ void __launch_bounds__(256) k_gauss_live(GaussBwdArgs a) {
     __shared__ uint32_t s_pre[LIVE_CHUNKS + 1];
     const SumRange R = sum_range(a);

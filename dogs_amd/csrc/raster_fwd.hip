@@ -160,44 +160,54 @@ __device__ __forceinline__ void wave_candidates(CandLDS& L, int lane, int x0, in
 
 // Returns the tile-rect area (0 when culled); fills the geometry outputs of kept Gaussians.  The colour
 // (computeColorFromSH) is not evaluated here: only binned Gaussians need it, and k_bin_emit computes it for them.
-// GaussianSplatModel's activations (optim.hip k_activate_fwd's expressions), stored for the later consumers
-__device__ __forceinline__ void activate_one(const PreArgs& a, int idx, float& o, f3& s, f4& q, float& prod) {
-    const float ro = a.raw_o[idx];
-    const float rs0 = a.raw_s[3 * idx], rs1 = a.raw_s[3 * idx + 1], rs2 = a.raw_s[3 * idx + 2];
-    const float4 x = reinterpret_cast<const float4*>(a.raw_q)[idx];
-    o = 1.0f / (1.0f + expf(-ro));
-    s = {expf(rs0), expf(rs1), expf(rs2)};
-    prod = (s.x * s.y) * s.z;
-    const float d = fmaxf(sqrtf(((x.x * x.x + x.y * x.y) + x.z * x.z) + x.w * x.w), 1e-12f);
-    q = {x.x / d, x.y / d, x.z / d, x.w / d};
-    float* so = const_cast<float*>(a.opacities);
-    float* ss = const_cast<float*>(a.scales);
-    float* sq = const_cast<float*>(a.rotations);
-    so[idx] = o;
-    ss[3 * idx] = s.x; ss[3 * idx + 1] = s.y; ss[3 * idx + 2] = s.z;
-    reinterpret_cast<float4*>(sq)[idx] = make_float4(q.x, q.y, q.z, q.w);
+// The per-Gaussian inputs of the preprocess, loaded before anything is stored (so a thread's several Gaussians have
+// all their loads in flight together).  With PreArgs::raw_* they are GaussianSplatModel's activations of the raw
+// parameters (optim.hip k_activate_fwd's expressions), stored by pre_compute for the later consumers.
+struct PreIn {
+    f3 po, s;
+    f4 q;
+    float opac, prod;
+};
+__device__ __forceinline__ PreIn pre_load(const PreArgs& a, int idx) {
+    PreIn in;
+    in.po = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+    in.s = {0.f, 0.f, 0.f};
+    in.q = {0.f, 0.f, 0.f, 0.f};
+    in.prod = 0.0f;
+    if (a.raw_o) {
+        const float ro = a.raw_o[idx];
+        const float rs0 = a.raw_s[3 * idx], rs1 = a.raw_s[3 * idx + 1], rs2 = a.raw_s[3 * idx + 2];
+        const float4 x = reinterpret_cast<const float4*>(a.raw_q)[idx];
+        in.opac = 1.0f / (1.0f + expf(-ro));
+        in.s = {expf(rs0), expf(rs1), expf(rs2)};
+        in.prod = (in.s.x * in.s.y) * in.s.z;
+        const float d = fmaxf(sqrtf(((x.x * x.x + x.y * x.y) + x.z * x.z) + x.w * x.w), 1e-12f);
+        in.q = {x.x / d, x.y / d, x.z / d, x.w / d};
+    } else {
+        if (!a.cov3D_precomp) {
+            in.s = {a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
+            in.q = {a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]};
+        }
+        in.opac = a.opacities[idx];
+    }
+    return in;
 }
 
-__device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, float& prod) {
+// Returns the tile-rect area (0 when culled); fills the geometry outputs of kept Gaussians.  The colour
+// (computeColorFromSH) is not evaluated here: only binned Gaussians need it, and k_bin_emit computes it for them.
+__device__ __forceinline__ uint32_t pre_compute(const PreArgs& a, int idx, const PreIn& in) {
     a.radii[idx] = 0;
     a.depthkey[idx] = 0xffffffffu;
     a.cnt[idx] = 0u;
     a.rcnt[idx] = 0u;
-    const f3 po = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
-    // every per-Gaussian input is loaded before the first use, so one HBM round trip covers them all
-    // (issued after the frustum test they would cost a second, dependent, round trip per wave)
-    f3 s = {0.f, 0.f, 0.f};
-    f4 q = {0.f, 0.f, 0.f, 0.f};
-    float opac;
-    if (a.raw_o) {
-        activate_one(a, idx, opac, s, q, prod);
-    } else {
-        if (!a.cov3D_precomp) {
-            s = {a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
-            q = {a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]};
-        }
-        opac = a.opacities[idx];
+    if (a.raw_o) {  // the activated parameters, for the later consumers (opacities / scales / rotations are outputs)
+        const_cast<float*>(a.opacities)[idx] = in.opac;
+        float* ss = const_cast<float*>(a.scales);
+        ss[3 * idx] = in.s.x; ss[3 * idx + 1] = in.s.y; ss[3 * idx + 2] = in.s.z;
+        reinterpret_cast<float4*>(const_cast<float*>(a.rotations))[idx] = make_float4(in.q.x, in.q.y, in.q.z, in.q.w);
     }
+    const f3 po = in.po;
+    const float opac = in.opac;
     // in_frustum (auxiliary.h:150-175)
     const f3 pv = tp4x3(po, a.view);
     if (pv.z <= 0.2f) {
@@ -213,7 +223,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, fl
 #pragma unroll
         for (int i = 0; i < 6; i++) cbuf[i] = a.cov3D_precomp[6 * idx + i];
     } else {
-        cov3d_fwd(s, a.scale_mod, q, cbuf);
+        cov3d_fwd(in.s, a.scale_mod, in.q, cbuf);
     }
     const float* cov3D = cbuf;
     f3 cov = cov2d_fwd(po, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy, cov3D, a.view, nullptr);
@@ -247,6 +257,12 @@ __device__ __forceinline__ uint32_t preprocess_one(const PreArgs& a, int idx, fl
     return area;
 }
 
+#ifndef DG_PRE_PER_THREAD
+#define DG_PRE_PER_THREAD 1
+#endif
+// Gaussians per thread of k_preprocess (their loads issued together); 2 or 4 measured slower (28 -> 32 us per view)
+constexpr int PRE_PT = DG_PRE_PER_THREAD;
+
 // One thread per Gaussian.  Neither the precise per-tile cull nor the colour is computed here: only the binned
 // Gaussians need them, and the binning walk (k_bin_count / k_bin_emit) computes them for those.
 __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
@@ -254,16 +270,28 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
     __shared__ float s_prod[4];
     __shared__ uint32_t s_err;
     const int t = threadIdx.x;
-    const int base = blockIdx.x * 256;
-    const int idx = base + t;
-    for (int i = base + t; i < DH_BINS; i += gridDim.x * 256) a.hist[i] = 0u;  // for k_depth_hist
-    for (int i = base + t; i < a.unf_words; i += gridDim.x * 256) a.unf_rows[i] = 0ull;  // for the phase-1 render
+    const int base = blockIdx.x * 256 * PRE_PT;
+    for (int i = blockIdx.x * 256 + t; i < DH_BINS; i += gridDim.x * 256) a.hist[i] = 0u;  // for k_depth_hist
+    for (int i = blockIdx.x * 256 + t; i < a.unf_words; i += gridDim.x * 256) a.unf_rows[i] = 0ull;  // phase-1 render
     if (t == 0) s_err = 0u;
     __syncthreads();
     a.err = &s_err;  // a prefiltered violation flags the block (bit 63 of its part)
+    PreIn in[PRE_PT];
+#pragma unroll
+    for (int k = 0; k < PRE_PT; k++) {
+        const int idx = base + k * 256 + t;
+        if (idx < a.P) in[k] = pre_load(a, idx);
+    }
     uint32_t area = 0;
     float prod = 0.0f;
-    if (idx < a.P) area = preprocess_one(a, idx, prod);
+#pragma unroll
+    for (int k = 0; k < PRE_PT; k++) {
+        const int idx = base + k * 256 + t;
+        if (idx < a.P) {
+            area += pre_compute(a, idx, in[k]);
+            prod += in[k].prod;
+        }
+    }
     unsigned long long v = area;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -1546,7 +1574,7 @@ __global__ void __launch_bounds__(256) k_filter(PreArgs a) {
 void launch_preprocess(const PreArgs& a, hipStream_t s) {
     if (a.P > 0) k_preprocess<<<preprocess_blocks(a.P), 256, 0, s>>>(a);
 }
-uint32_t preprocess_blocks(int P) { return (uint32_t)((P + 255) / 256); }
+uint32_t preprocess_blocks(int P) { return (uint32_t)((P + 256 * PRE_PT - 1) / (256 * PRE_PT)); }
 void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_t* hist, hipStream_t s) {
     const int per = DH_THREADS * DH_ITEMS;
     if (P > 0) k_depth_hist<<<(P + per - 1) / per, DH_THREADS, 0, s>>>(P, dkey, cnt, hist);
