@@ -138,6 +138,7 @@ struct Image {
     uint32_t* sat;          // [(ty+1)*(tx+1)] summed-area table of `unfinished`
     uint32_t* long_tiles;   // [T] queue of the long-list tile depth sort
     uint32_t *tile_cnt, *tile_cnt2;  // [T] per-tile instance counters of the phase-1 / phase-2 binning
+    uint32_t* ohist;        // [2 ORDER_NB] the phase-2 launches' replay-order buckets (after tile_cnt2)
     uint32_t* order;        // [T] the backward's replay order (written by the phase-2 emission when phase 2 ran)
     uint32_t* unf_list;     // [T] the unfinished tiles, in the order phase 1 found them
     size_t bytes;
@@ -163,7 +164,8 @@ Image carve_image(void* base, int W, int H) {
     }
     im.long_tiles = c.take<uint32_t>(T);
     im.tile_cnt = c.take<uint32_t>(T);
-    im.tile_cnt2 = c.take<uint32_t>(T);
+    im.tile_cnt2 = c.take<uint32_t>(T + 2 * gs::ORDER_NB);  // + the replay-order histogram (zeroed by k_depth_cut)
+    im.ohist = im.tile_cnt2 + T;
     im.order = c.take<uint32_t>(T);
     im.unf_list = c.take<uint32_t>(T);
     im.bytes = c.off;
@@ -204,6 +206,7 @@ gs::BinArgs bin_args(const dg_raster_args* r, const Geom& g, const Image& im, in
     a.unf = im.unfinished; a.sat = im.sat; a.wtot = g.wtot; a.wmask = g.wmask; a.mlist = g.mlist; a.cap = cap; a.first_e = g.first_e; a.rcnt = g.rcnt;
     a.eg = b.eg; a.ikey = b.ik; a.flag = b.flag; a.tile_cnt = tile_cnt; a.ranges = ranges; a.s_e = b.se;
     a.unf_rows = nullptr; a.unf_rw = 0; a.unf_th = 0; a.probe = nullptr; a.colors_later = 0;
+    a.ohist = nullptr; a.max_contrib = nullptr; a.ranges1 = nullptr;
     return a;
 }
 // per-tile (depth, index) order of a phase's binned lists
@@ -668,6 +671,8 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
         ba.unf_rows = UNF_ROWS ? reinterpret_cast<const unsigned long long*>(im.sat) : nullptr;
         ba.unf_rw = unf_rw_of(tx); ba.unf_th = ty;
         ba.probe = UNF_ROWS && ac ? ac->probe : nullptr;
+        const bool multi_order = gs::render_fwd2_orders() && gs::bin_emit_orders();
+        if (multi_order) { ba.ohist = im.ohist; ba.max_contrib = im.max_contrib; ba.ranges1 = im.ranges; }
         gs::launch_bin(2, ba, g.counters + gs::CNT_K2, g.scan_tmp, s, sh_wait);
         if (sh_wait) fold->waited = true;
         sh_wait = nullptr;
@@ -686,6 +691,7 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
         r2.ranges = im.ranges2; r2.ranges1 = im.ranges; r2.s_e = b2.se; r2.eg = b2.eg;
         r2.probe = ac ? ac->probe : nullptr;
         r2.order = im.order;
+        r2.ohist = multi_order ? im.ohist : nullptr;
         gs::launch_render_fwd(r2, s);
     }
     DBG_SYNC(a->debug, s);

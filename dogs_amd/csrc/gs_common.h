@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sortscan.h"
+
 #define GS_TILE_X 16
 #define GS_TILE_Y 16
 #define GS_TILE_PIX 256
@@ -268,6 +270,53 @@ __device__ __forceinline__ void tile_order_sort(int num_tiles, uint32_t* order, 
             if (tile < num_tiles) order[atomicAdd(&s_hist[b0[k]], 1u)] = (uint32_t)tile;
         }
     }
+}
+
+// The same order (same buckets) from two front pieces of two consecutive launches, ORDER_TILES tiles per block, so
+// that no single block walks every tile (the one-block sort's contended LDS atomics took ~25 us at 8160 tiles from a
+// 256-thread block, on the phase-2 critical path).  ohist[0, ORDER_NB) holds the bucket counts and
+// ohist[ORDER_NB, 2 ORDER_NB) the bucket cursors, both zero before the first piece.
+//   order_hist_piece:    the block's tiles' buckets into an LDS histogram, flushed with one atomic per nonempty bucket;
+//   order_scatter_piece: (a later launch) bucket starts = exclusive scan of the counts, the block's tiles ranked per
+//                        bucket in LDS, one global atomic per (block, bucket) reserves the run, then order[] is written.
+// Both need blockDim.x == ORDER_TILES == ORDER_NB and `len` returning the same value for a tile in both launches.
+// (ORDER_NB, ORDER_TILES, order_blocks: sortscan.h, shared with the host side)
+__device__ __forceinline__ uint32_t order_bucket(uint32_t len) {
+    const uint32_t l = len >> 2;
+    return (uint32_t)ORDER_NB - 1u - (l < (uint32_t)ORDER_NB - 1u ? l : (uint32_t)ORDER_NB - 1u);
+}
+template <typename LenFn>
+__device__ __forceinline__ void order_hist_piece(int num_tiles, int blk, uint32_t* ohist, uint32_t* s_h, LenFn&& len) {
+    const int t = threadIdx.x, tile = blk * ORDER_TILES + t;
+    s_h[t] = 0u;
+    __syncthreads();
+    if (tile < num_tiles) atomicAdd(&s_h[order_bucket(len(tile))], 1u);
+    __syncthreads();
+    if (s_h[t]) atomicAdd(&ohist[t], s_h[t]);
+}
+template <typename LenFn>
+__device__ __forceinline__ void order_scatter_piece(int num_tiles, int blk, uint32_t* ohist, uint32_t* order,
+                                                    uint32_t* s_start, uint32_t* s_cnt, uint32_t* s_w, LenFn&& len) {
+    const int t = threadIdx.x, lane = t & 63, tile = blk * ORDER_TILES + t;
+    const uint32_t b = tile < num_tiles ? order_bucket(len(tile)) : 0u;
+    const uint32_t v = ohist[t];
+    uint32_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_w[t >> 6] = incl;
+    s_cnt[t] = 0u;
+    __syncthreads();
+    uint32_t off = 0;
+    for (int w = 0; w < (t >> 6); w++) off += s_w[w];
+    s_start[t] = off + incl - v;
+    const uint32_t r = tile < num_tiles ? atomicAdd(&s_cnt[b], 1u) : 0u;
+    __syncthreads();
+    if (s_cnt[t]) s_start[t] += atomicAdd(&ohist[ORDER_NB + t], s_cnt[t]);
+    __syncthreads();
+    if (tile < num_tiles) order[s_start[b] + r] = (uint32_t)tile;
 }
 
 constexpr float LOG2E = 1.4426950408889634f;

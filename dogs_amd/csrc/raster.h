@@ -93,7 +93,8 @@ struct RenderArgs {
     uint32_t* probe;            // optional (phase 2, adaptive capacity): [1] <- counters[CNT_K2]
     unsigned long long* unf_rows;  // phase 1: bit tx % 64 of word ty * unf_rw + tx / 64 set for each unfinished tile
     int unf_rw;
-    uint32_t* order;            // phase 2 (k_render_fwd2, optional): out, the backward's replay order (an extra block)
+    uint32_t* order;            // phase 2 (k_render_fwd2, optional): out, the backward's replay order (front blocks)
+    uint32_t* ohist;            // phase 2 with order: the replay-order bucket counts / cursors (order_scatter_piece)
     // phase 1 (optional): block 0 copies hc_src[0..16) to hc_dst[0..16), a coherent pinned host buffer, then sets
     // hc_dst[16] = hc_seq; the host spins on that word (the forward's early counter read without a copy launch or an
     // event; the PCIe round trip hides inside the render)
@@ -164,7 +165,8 @@ void launch_preprocess(const PreArgs& a, hipStream_t s);
 // hist[DH_BINS] (zeroed by the preprocess) += precise counts by depth bin
 void launch_depth_hist(int P, const uint32_t* dkey, const uint32_t* cnt, uint32_t* hist, hipStream_t s);
 // counters[K, THR, E1, CUT] from the histogram (phase-1 capacity cap); resets the per-view counters and zeroes
-// the per-tile counters of both binning phases (tile_cnt, tile_cnt2 [num_tiles])
+// the per-tile counters of both binning phases (tile_cnt, tile_cnt2 [num_tiles]) and the replay-order histogram after
+// tile_cnt2 (tile_cnt2 + num_tiles, 2 * ORDER_NB words)
 // It also totals the preprocess's per-block rect-area sums into counters[CNT_RECT_LO..+1] (num_rendered) and their
 // error bits into counters[CNT_ERR] (one atomic per block on a single address costs ~10 us per 1e6 Gaussians:
 // cross-XCD serialization), and writes every other counter slot, so the block needs no memset per view.  probe
@@ -202,13 +204,19 @@ struct BinArgs {
     int D, M;
     const float *means3D, *campos, *dc, *sh, *colors;
     float4* rgbi;
-    uint32_t* tile_cnt;          // [num_tiles] zero on entry: counts, then arrival cursors
+    uint32_t* tile_cnt;          // [num_tiles] zero on entry: counts, then arrival cursors (from the range starts)
     uint2* ranges;               // [num_tiles] per-tile [start, end) of s_e
     uint32_t* s_e;               // instances grouped by tile
     const unsigned long long* unf_rows;  // phase 2: per-row bitmasks of the unfinished tiles (RenderArgs::unf_rows)
     int unf_rw;                  // words per tile row
     int unf_th;                  // tile rows
     uint32_t* probe;             // optional (phase 2, adaptive capacity): [0] <- counters[CNT_UNFINISHED]
+    // optional (phase 2): the emission's front blocks histogram the backward's replay-order buckets into ohist
+    // (order_hist_piece; k_render_fwd2 scatters the order): a finished tile's phase-1 max contributor, an unfinished
+    // tile's phase-1 + phase-2 list lengths
+    uint32_t* ohist;
+    const uint32_t* max_contrib;
+    const uint2* ranges1;
 };
 void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s,
                 hipEvent_t wait_before_emit = nullptr);
@@ -222,6 +230,7 @@ void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, 
 void launch_render_fwd(const RenderArgs& a, hipStream_t s);
 uint32_t preprocess_blocks(int P);  // k_preprocess's grid (PreArgs::part_sc entries)
 bool render_fwd2_orders();
+bool bin_emit_orders();
 // count mode: score[i] = gcount[i] x the (AA-scaled) opacity of splat record i (0 when culled)
 void launch_count_score(int P, const int* radii, const float4* sp, const uint32_t* gcount, float* score,
                         hipStream_t s);

@@ -389,6 +389,8 @@ __device__ __forceinline__ void depth_cut_block(const uint32_t* __restrict__ his
         if (lane == 0) s_rect[w] = r;
     }
     for (uint32_t i = t; i < num_tiles; i += 1024) { tile_cnt[i] = 0u; tile_cnt2[i] = 0u; }
+    // tile_cnt2 is followed by the replay-order histogram of the phase-2 launches (order_hist_piece: counts, cursors)
+    for (uint32_t i = t; i < 2u * ORDER_NB; i += 1024) tile_cnt2[num_tiles + i] = 0u;
     if (t == 0) s_best = -1;
     uint32_t v[PER], loc = 0;
 #pragma unroll
@@ -632,18 +634,38 @@ __global__ void __launch_bounds__(256) k_binned_colors(BinArgs a) {
     binned_colour(a, g, key);
 }
 
+// The backward's replay length of a tile as the phase-2 launches see it: a finished tile's phase-1 max contributor
+// (final), an unfinished tile's phase-1 + phase-2 list lengths (its max contributor is written by k_render_fwd2).
+__device__ __forceinline__ uint32_t fwd2_replay_len(const uint8_t* unf, const uint32_t* max_contrib, const uint2* ranges1,
+                                                    const uint2* ranges2, int tile) {
+    if (!unf[tile]) return max_contrib[tile];
+    const uint2 r1 = ranges1[tile], r2 = ranges2[tile];
+    return (r1.y - r1.x) + (r2.y - r2.x);
+}
+
 // Pass 2: wave base = exclusive scan of the wave totals (wtot, scanned in place); first_e of every binned
 // Gaussian, and a second walk writes its instances (Gaussian, depth key) at consecutive indices in (lane, ty, tx)
 // order, so every Gaussian's instances are contiguous: [first_e, first_e + rcnt); each instance index is also
-// placed in its tile's list, s_e[ranges[t].x + atomic arrival slot] (counting sort; the order inside a tile is
+// placed in its tile's list, s_e[atomic arrival cursor, from ranges[t].x] (counting sort; the order inside a tile is
 // fixed afterwards by k_tile_dsort).
 template <int PHASE>
 __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
     __shared__ CandLDS s_cand[4];
     __shared__ uint32_t s_key[4][64];
+    int bid = (int)blockIdx.x;
+    if (PHASE == 2 && a.ohist) {  // front blocks: the replay-order histogram (not gated: the backward needs the order)
+        const int ob = order_blocks(a.num_tiles);
+        if (bid < ob) {
+            order_hist_piece(a.num_tiles, bid, a.ohist, &s_key[0][0], [&](int tile) {
+                return fwd2_replay_len(a.unf, a.max_contrib, a.ranges1, a.ranges, tile);
+            });
+            return;
+        }
+        bid -= ob;
+    }
     if (PHASE == 2 && a.counters[CNT_UNFINISHED] == 0u) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int wave = blockIdx.x * 4 + w;
+    const int wave = bid * 4 + w;
     const int g0 = wave * EMIT_RANKS;
     if (g0 >= a.P) return;
     const uint64_t members = a.wmask[wave];
@@ -676,7 +698,7 @@ __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
                             a.eg[e] = (uint32_t)(g0 + owner);
                             a.ikey[e] = s_key[w][owner];
                             a.flag[e] = 0;
-                            a.s_e[a.ranges[t].x + atomicAdd(&a.tile_cnt[t], 1u)] = e;
+                            a.s_e[atomicAdd(&a.tile_cnt[t], 1u)] = e;
                         }
                         running += (uint32_t)__popcll(km);
                     });
@@ -839,7 +861,7 @@ __global__ void __launch_bounds__(256) k_bin_emit_fat(BinArgs a) {
                                     a.eg[e] = s_g[w][owner];
                                     a.ikey[e] = s_key[w][owner];
                                     a.flag[e] = 0;
-                                    a.s_e[a.ranges[t].x + atomicAdd(&a.tile_cnt[t], 1u)] = e;
+                                    a.s_e[atomicAdd(&a.tile_cnt[t], 1u)] = e;
                                 }
                                 run += (uint32_t)__popcll(km);
                             });
@@ -1211,7 +1233,11 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
 // k_render_fwd) with one pixel per lane.  The per-pixel arithmetic is k_render_fwd's (splat_exp_coeffs, the
 // splat_power4 operation order, the same accept / stop / update sequence), so the backward's replay reproduces
 // every decision.  Every splat of the list is evaluated (the quadrant test only skips splats no pixel accepts).
-constexpr int FWD2_CHUNK = 1024;
+#ifndef DG_FWD2_CHUNK
+#define DG_FWD2_CHUNK 1024
+#endif
+constexpr int FWD2_CHUNK = DG_FWD2_CHUNK;
+static_assert(FWD2_CHUNK >= 256 && FWD2_CHUNK % 64 == 0, "the chunk buffer is also the sorts' and the order's scratch");
 template <bool COUNT>
 __device__ __forceinline__ void render_fwd2_tile(const RenderArgs& a, int tile, float4* s_sb, uint32_t* s_mx,
                                                  uint32_t* s_ids);
@@ -1223,16 +1249,20 @@ __global__ void __launch_bounds__(256) k_render_fwd2(RenderArgs a) {
     __shared__ uint32_t s_ids[DS_WAVE_MAX2];
     // the adaptive capacity's probe gets this view's phase-2 instance count (the next view's k_depth_cut reads it)
     if (a.probe && blockIdx.x == 0 && threadIdx.x == 0) a.probe[1] = a.counters[CNT_K2];
-    // block 0 (dispatched first, so it overlaps the tiles' blocks): the backward's longest-first replay order -- a
-    // finished tile's phase-1 max contributor is final, an unfinished tile's replay is bounded by its phase-1 +
-    // phase-2 list lengths (it reads max_contrib only where the other blocks do not write it)
-    const uint32_t ob = a.order ? 1u : 0u;
-    if (ob && blockIdx.x == 0) {
-        tile_order_sort(a.num_tiles, a.order, [&](int tile) {
-            if (!a.unfinished[tile]) return a.max_contrib[tile];
-            const uint2 r1 = a.ranges1[tile], r2 = a.ranges[tile];
-            return (r1.y - r1.x) + (r2.y - r2.x);
-        });
+    // the front blocks (dispatched first, so they overlap the tiles' blocks): the backward's longest-first replay
+    // order, scattered from the buckets the phase-2 emission histogrammed (order_scatter_piece; one block sorting every
+    // tile without ohist) -- a finished tile's phase-1 max contributor is final, an unfinished tile's replay is bounded
+    // by its phase-1 + phase-2 list lengths (max_contrib is read only where the other blocks do not write it)
+    const uint32_t ob = a.order ? (a.ohist ? (uint32_t)order_blocks(a.num_tiles) : 1u) : 0u;
+    if (blockIdx.x < ob) {
+        const auto len = [&](int tile) { return fwd2_replay_len(a.unfinished, a.max_contrib, a.ranges1, a.ranges, tile); };
+        if (a.ohist) {  // the emission's front blocks histogrammed the buckets
+            uint32_t* scr = reinterpret_cast<uint32_t*>(s_sb);
+            order_scatter_piece(a.num_tiles, (int)blockIdx.x, a.ohist, a.order, scr, scr + ORDER_NB, scr + 2 * ORDER_NB,
+                                len);
+        } else {
+            tile_order_sort(a.num_tiles, a.order, len);
+        }
         return;
     }
     if (a.unf_list) {  // the unfinished tiles phase 1 listed, a block each, grid-stride
@@ -1603,7 +1633,7 @@ void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hi
         else k_bin_count_fat<1><<<blocks, 256, 0, s>>>(a);
     } else if (phase == 2) k_bin_count<2><<<blocks, 256, 0, s>>>(a);
     else k_bin_count<1><<<blocks, 256, 0, s>>>(a);
-    if ((uint32_t)waves <= BIN_OFFSETS_MAX_N) {  // one launch: wave offsets + tile ranges, tile_cnt -> 0 (cursors)
+    if ((uint32_t)waves <= BIN_OFFSETS_MAX_N) {  // one launch: wave offsets + tile ranges, tile_cnt -> range starts (cursors)
         bin_offsets(a.wtot, (uint32_t)waves, total, a.tile_cnt, (uint32_t)a.num_tiles, a.ranges, s, gate,
                     a.colors_later != 0);
     } else {
@@ -1614,7 +1644,7 @@ void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hi
     if (fat) {
         if (phase == 2) k_bin_emit_fat<2><<<blocks, 256, 0, s>>>(a);
         else k_bin_emit_fat<1><<<blocks, 256, 0, s>>>(a);
-    } else if (phase == 2) k_bin_emit<2><<<blocks, 256, 0, s>>>(a);
+    } else if (phase == 2) k_bin_emit<2><<<blocks + (a.ohist ? order_blocks(a.num_tiles) : 0), 256, 0, s>>>(a);
     else k_bin_emit<1><<<blocks, 256, 0, s>>>(a);
 }
 void launch_binned_colors(const BinArgs& a, hipStream_t s) {
@@ -1627,6 +1657,7 @@ void launch_unfinished_sat(const uint32_t* counters, const uint8_t* unfinished, 
     k_sat_rows<<<(tiles_y + 1 + 3) / 4, 256, 0, s>>>(counters, unfinished, tiles_x, tiles_y, sat, probe);
     k_sat_cols<<<(tiles_x + 3) / 4, 256, 0, s>>>(counters, tiles_x, tiles_y, sat);
 }
+bool bin_emit_orders() { return !(DG_BIN_FAT2 > 1); }  // k_bin_emit<2> runs order_hist_piece (BinArgs::ohist)
 bool render_fwd2_orders() {  // the phase-2 launch writes RenderArgs::order (the backward skips k_bwd_order)
 #if defined(DG_PHASE2_WAVE_PER_TILE) || defined(DG_FWD2_SPLIT)
     return false;
@@ -1644,7 +1675,7 @@ void launch_render_fwd(const RenderArgs& a, hipStream_t s) {
         else k_render_fwd2x<false><<<a.num_tiles, 1024, 0, s>>>(a);
 #else
         const int g2 = (a.unf_list ? (a.num_tiles < FWD2_GRID ? a.num_tiles : FWD2_GRID) : a.num_tiles) +
-                       (a.order ? 1 : 0);
+                       (a.order ? (a.ohist ? order_blocks(a.num_tiles) : 1) : 0);
         if (a.gcount) k_render_fwd2<true><<<g2, 256, 0, s>>>(a);
         else k_render_fwd2<false><<<g2, 256, 0, s>>>(a);
 #endif

@@ -5,6 +5,11 @@
 #include <stdint.h>
 
 namespace gs {
+
+// the multi-block replay order of the phase-2 launches (gs_common.h order_hist_piece / order_scatter_piece)
+constexpr int ORDER_NB = 256, ORDER_TILES = 256;
+__host__ __device__ constexpr int order_blocks(int num_tiles) { return (num_tiles + ORDER_TILES - 1) / ORDER_TILES; }
+
 // Stable LSD radix sort of (key, value) pairs over bits [begin_bit, end_bit), 8 bits per pass.
 // Pass 0 reads values from vals_first (nullptr -> value = input index).  Ping-pongs between the
 // (keys0, vals0) and (keys1, vals1) buffers; keys0 holds the input.  Returns 1 when the result is in
@@ -22,8 +27,8 @@ size_t scan_temp_bytes(uint32_t n);
 void exclusive_scan(const uint32_t* in, uint32_t n, uint32_t* out, uint32_t* total, void* temp, hipStream_t stream,
                     const uint32_t* gate = nullptr, const uint32_t* lt_keys = nullptr, const uint32_t* lt_thr = nullptr);
 
-// ranges[t] = [start, end) from the per-tile counts (exclusive scan, one block), and tile_cnt reset to 0 so that it
-// serves as the per-tile arrival cursor.  gate (optional, device): nothing when *gate == 0.
+// ranges[t] = [start, end) from the per-tile counts (exclusive scan, one block), and tile_cnt set to start so that it
+// serves as the per-tile arrival cursor (an atomic increment returns the instance's slot, no ranges load).  gate (optional, device): nothing when *gate == 0.
 void tile_offsets(uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges, hipStream_t stream,
                   const uint32_t* gate = nullptr);
 

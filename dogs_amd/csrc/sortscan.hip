@@ -387,7 +387,7 @@ __global__ void __launch_bounds__(1024) k_tile_offsets(uint32_t* __restrict__ ti
 #pragma unroll
         for (int k = 0; k < 16; k++) { if (k < w) off += s_w[k]; tot += s_w[k]; }
         const uint32_t ex = off + x - v;
-        if (i < num_tiles) { ranges[i] = make_uint2(ex, ex + v); tile_cnt[i] = 0u; }
+        if (i < num_tiles) { ranges[i] = make_uint2(ex, ex + v); tile_cnt[i] = ex; }
         __syncthreads();
         if (t == 0) s_carry += tot;
         __syncthreads();
@@ -451,7 +451,7 @@ __global__ void __launch_bounds__(NT) k_bin_offsets(uint32_t* __restrict__ wtot,
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             if (i0 + k < N) {
-                if (tiles) { ranges[i0 + k] = make_uint2(ex, ex + v[k]); tile_cnt[i0 + k] = 0u; }
+                if (tiles) { ranges[i0 + k] = make_uint2(ex, ex + v[k]); tile_cnt[i0 + k] = ex; }
                 else wtot[i0 + k] = ex;
             }
             ex += v[k];

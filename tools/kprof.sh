@@ -8,5 +8,5 @@ export TMPDIR=/tmp
 mkdir -p "$OUT"
 for lib in "$@"; do
   v=$(basename "$lib" .so)
-  DOGS_HIP_LIB=$ROOT/$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$v" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-train-step > "$OUT/$v.log" 2>&1
+  DOGS_HIP_LIB=$ROOT/$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$v" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-train-step --no-admm --no-reference-k > "$OUT/$v.log" 2>&1
 done
