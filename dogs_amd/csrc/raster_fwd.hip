@@ -1280,6 +1280,13 @@ __global__ void __launch_bounds__(256) k_render_fwd2(RenderArgs a) {
 template <bool COUNT>
 __device__ __forceinline__ void render_fwd2_tile(const RenderArgs& a, int tile, float4* s_sb, uint32_t* s_mx,
                                                  uint32_t* s_ids) {
+    const uint2 rg = a.ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    // No phase-2 instance (e.g. an image-edge tile whose list ended unsaturated in phase 1): phase 1 already wrote this
+    // tile's final outputs (colour with the background, T, inverse depth, last contributors, max contributor) -- the
+    // values this pass would rewrite -- so the block skips it.  Block-uniform.  (Two thirds of the unfinished tiles of
+    // some yaw views; with more unfinished tiles than blocks they made blocks composite two tiles in a row.)
+    if (n == 0) return;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
     const int px = tx * GS_TILE_X + (lane & 15), py = ty * GS_TILE_Y + 4 * w + (lane >> 4);
@@ -1296,8 +1303,6 @@ __device__ __forceinline__ void render_fwd2_tile(const RenderArgs& a, int tile, 
         C0 = rs.x; C1 = rs.y; C2 = rs.z; thr = rs.w;
     }
     const uint32_t cbase = a.ranges1[tile].y - a.ranges1[tile].x;
-    const uint2 rg = a.ranges[tile];
-    const int n = (int)(rg.y - rg.x);
     // fused sort (no standalone phase-2 sort launches): wave 0 sorts a list of up to DS_WAVE_MAX2 into s_ids (and
     // back to s_e for the backward), the block sorts a longer one in place through the global scratch -- the same
     // two routines, so the same order, as k_tile_dsort / k_tile_dsort_long
