@@ -141,6 +141,7 @@ struct Image {
     uint32_t* ohist;        // [2 ORDER_NB] the phase-2 launches' replay-order buckets (after tile_cnt2)
     uint32_t* order;        // [T] the backward's replay order (written by the phase-2 emission when phase 2 ran)
     uint32_t* unf_list;     // [T] the unfinished tiles, in the order phase 1 found them
+    uint32_t* unf_sorted;   // [T] those with phase-2 instances, longest list first (the phase-2 emission)
     size_t bytes;
 };
 Image carve_image(void* base, int W, int H) {
@@ -168,6 +169,7 @@ Image carve_image(void* base, int W, int H) {
     im.ohist = im.tile_cnt2 + T;
     im.order = c.take<uint32_t>(T);
     im.unf_list = c.take<uint32_t>(T);
+    im.unf_sorted = c.take<uint32_t>(T);
     im.bytes = c.off;
     return im;
 }
@@ -206,7 +208,7 @@ gs::BinArgs bin_args(const dg_raster_args* r, const Geom& g, const Image& im, in
     a.unf = im.unfinished; a.sat = im.sat; a.wtot = g.wtot; a.wmask = g.wmask; a.mlist = g.mlist; a.cap = cap; a.first_e = g.first_e; a.rcnt = g.rcnt;
     a.eg = b.eg; a.ikey = b.ik; a.flag = b.flag; a.tile_cnt = tile_cnt; a.ranges = ranges; a.s_e = b.se;
     a.unf_rows = nullptr; a.unf_rw = 0; a.unf_th = 0; a.probe = nullptr; a.colors_later = 0;
-    a.ohist = nullptr; a.max_contrib = nullptr; a.ranges1 = nullptr;
+    a.ohist = nullptr; a.max_contrib = nullptr; a.ranges1 = nullptr; a.unf_list = nullptr; a.unf_sorted = nullptr;
     return a;
 }
 // per-tile (depth, index) order of a phase's binned lists
@@ -672,7 +674,10 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
         ba.unf_rw = unf_rw_of(tx); ba.unf_th = ty;
         ba.probe = UNF_ROWS && ac ? ac->probe : nullptr;
         const bool multi_order = gs::render_fwd2_orders() && gs::bin_emit_orders();
-        if (multi_order) { ba.ohist = im.ohist; ba.max_contrib = im.max_contrib; ba.ranges1 = im.ranges; }
+        if (multi_order) {
+            ba.ohist = im.ohist; ba.max_contrib = im.max_contrib; ba.ranges1 = im.ranges;
+            ba.unf_list = im.unf_list; ba.unf_sorted = im.unf_sorted;
+        }
         gs::launch_bin(2, ba, g.counters + gs::CNT_K2, g.scan_tmp, s, sh_wait);
         if (sh_wait) fold->waited = true;
         sh_wait = nullptr;
@@ -692,6 +697,7 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
         r2.probe = ac ? ac->probe : nullptr;
         r2.order = im.order;
         r2.ohist = multi_order ? im.ohist : nullptr;
+        r2.unf_sorted = multi_order ? im.unf_sorted : nullptr;
         gs::launch_render_fwd(r2, s);
     }
     DBG_SYNC(a->debug, s);

@@ -53,6 +53,7 @@ enum {
     CNT_INVD = 9,       // backward: any(dL/dinvdepth != 0) (zeroed with the block by the forward)
     CNT_LONG = 11,      // phase-1 tiles queued for the long-list depth sort
     CNT_LONG2 = 12,     // phase-2 tiles queued for the long-list depth sort
+    CNT_UNF2 = 13,      // unfinished tiles with phase-2 instances (RenderArgs::unf_sorted entries)
     CNT_PREV_UNF = 14,  // unfinished tiles of the previous phase-2 launch at this image size (adaptive capacity)
     CNT_PREV_K2 = 15,   // phase-2 instances of that launch
 };
@@ -95,6 +96,8 @@ struct RenderArgs {
     int unf_rw;
     uint32_t* order;            // phase 2 (k_render_fwd2, optional): out, the backward's replay order (front blocks)
     uint32_t* ohist;            // phase 2 with order: the replay-order bucket counts / cursors (order_scatter_piece)
+    const uint32_t* unf_sorted; // phase 2 (optional): the unfinished tiles with phase-2 instances, longest list first
+                                // (counters[CNT_UNF2] entries; k_bin_emit<2>'s sort block), walked instead of unf_list
     // phase 1 (optional): block 0 copies hc_src[0..16) to hc_dst[0..16), a coherent pinned host buffer, then sets
     // hc_dst[16] = hc_seq; the host spins on that word (the forward's early counter read without a copy launch or an
     // event; the PCIe round trip hides inside the render)
@@ -217,6 +220,11 @@ struct BinArgs {
     uint32_t* ohist;
     const uint32_t* max_contrib;
     const uint2* ranges1;
+    // optional (phase 2): one more front block of the emission writes the unfinished tiles that got phase-2 instances,
+    // longest list first, to unf_sorted (counters[CNT_UNF2] of them): k_render_fwd2's first-dispatched blocks take the
+    // longest tiles, so those do not share a compute unit with another tile's block
+    const uint32_t* unf_list;
+    uint32_t* unf_sorted;
 };
 void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s,
                 hipEvent_t wait_before_emit = nullptr);

@@ -653,6 +653,32 @@ __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
     __shared__ CandLDS s_cand[4];
     __shared__ uint32_t s_key[4][64];
     int bid = (int)blockIdx.x;
+    if (PHASE == 2 && a.unf_sorted) {  // front block: the phase-2 tiles, longest list first (not gated)
+        if (bid == 0) {
+            const uint32_t nu = a.counters[CNT_UNFINISHED];
+            uint32_t* cnt = &s_key[0][0];  // 256 buckets of (list length / 4), longest first
+            if (threadIdx.x < 256) cnt[threadIdx.x] = 0u;
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < nu; i += 256) {
+                const uint2 r = a.ranges[a.unf_list[i]];
+                if (r.y > r.x) atomicAdd(&cnt[order_bucket(r.y - r.x)], 1u);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {  // exclusive prefix, one thread (256 buckets)
+                uint32_t run = 0;
+                for (int k = 0; k < 256; k++) { const uint32_t c = cnt[k]; cnt[k] = run; run += c; }
+                const_cast<uint32_t*>(a.counters)[CNT_UNF2] = run;
+            }
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < nu; i += 256) {
+                const uint32_t tile = a.unf_list[i];
+                const uint2 r = a.ranges[tile];
+                if (r.y > r.x) a.unf_sorted[atomicAdd(&cnt[order_bucket(r.y - r.x)], 1u)] = tile;
+            }
+            return;
+        }
+        bid -= 1;
+    }
     if (PHASE == 2 && a.ohist) {  // front blocks: the replay-order histogram (not gated: the backward needs the order)
         const int ob = order_blocks(a.num_tiles);
         if (bid < ob) {
@@ -1265,6 +1291,14 @@ __global__ void __launch_bounds__(256) k_render_fwd2(RenderArgs a) {
         }
         return;
     }
+    if (a.unf_sorted) {  // the tiles with phase-2 instances, longest first, a block each, grid-stride
+        const uint32_t nu = a.counters[CNT_UNF2];
+        for (uint32_t i = blockIdx.x - ob; i < nu; i += gridDim.x - ob) {
+            render_fwd2_tile<COUNT>(a, (int)a.unf_sorted[i], s_sb, s_mx, s_ids);
+            __syncthreads();  // s_sb / s_ids are reused by the next tile
+        }
+        return;
+    }
     if (a.unf_list) {  // the unfinished tiles phase 1 listed, a block each, grid-stride
         const uint32_t nu = a.counters[CNT_UNFINISHED];
         for (uint32_t i = blockIdx.x - ob; i < nu; i += gridDim.x - ob) {
@@ -1649,7 +1683,9 @@ void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hi
     if (fat) {
         if (phase == 2) k_bin_emit_fat<2><<<blocks, 256, 0, s>>>(a);
         else k_bin_emit_fat<1><<<blocks, 256, 0, s>>>(a);
-    } else if (phase == 2) k_bin_emit<2><<<blocks + (a.ohist ? order_blocks(a.num_tiles) : 0), 256, 0, s>>>(a);
+    } else if (phase == 2) {
+        k_bin_emit<2><<<blocks + (a.ohist ? order_blocks(a.num_tiles) : 0) + (a.unf_sorted ? 1 : 0), 256, 0, s>>>(a);
+    }
     else k_bin_emit<1><<<blocks, 256, 0, s>>>(a);
 }
 void launch_binned_colors(const BinArgs& a, hipStream_t s) {
