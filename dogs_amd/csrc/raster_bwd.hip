@@ -571,7 +571,14 @@ constexpr int LIVE_CHUNKS = DG_LIVE_CHUNKS;
 // the chunk-count prefix below is one wave's scan (64 lanes) and the lookup a binary search over it
 static_assert(LIVE_CHUNKS >= 1 && LIVE_CHUNKS <= 64 && (LIVE_CHUNKS & (LIVE_CHUNKS - 1)) == 0,
               "DG_LIVE_CHUNKS: a power of two up to 64");
-__global__ void __launch_bounds__(256) k_gauss_live(GaussBwdArgs a) {
+// threads per block: the listed Gaussians of a block (~2 per chunk) fill about one wave, and the per-Gaussian pass
+// needs ~220 VGPRs (2 waves per SIMD), so 256-thread blocks left idle waves holding residency slots.  gauss_bwd per
+// view (3 interleaved bench runs each, profiles/r03aa_live_threads_ab.txt): 256 threads 62-63 us, 128: 59, 64: 63-64
+#ifndef DG_LIVE_THREADS
+#define DG_LIVE_THREADS 128
+#endif
+constexpr int LIVE_THREADS = DG_LIVE_THREADS;
+__global__ void __launch_bounds__(LIVE_THREADS) k_gauss_live(GaussBwdArgs a) {
     __shared__ uint32_t s_pre[LIVE_CHUNKS + 1];
     const SumRange R = sum_range(a);
     const uint32_t nchunks = (R.NR + SUM_CHUNK - 1) / SUM_CHUNK;
@@ -589,7 +596,7 @@ __global__ void __launch_bounds__(256) k_gauss_live(GaussBwdArgs a) {
         }
         __syncthreads();
         const uint32_t tot = s_pre[LIVE_CHUNKS];
-        for (uint32_t j = threadIdx.x; j < tot; j += 256) {
+        for (uint32_t j = threadIdx.x; j < tot; j += LIVE_THREADS) {
             int k = 0;
 #pragma unroll
             for (int st = LIVE_CHUNKS / 2; st > 0; st >>= 1)
@@ -903,7 +910,7 @@ void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s) {
     const uint32_t aux_blocks = ((uint32_t)a.P + AUX_SPAN - 1) / AUX_SPAN;
     k_gauss_sum<<<sum_blocks + aux_blocks, 256, 0, s>>>(a, sum_blocks);
     const uint32_t live_blocks = chunks ? (chunks + LIVE_CHUNKS - 1) / LIVE_CHUNKS : 1u;
-    k_gauss_live<<<live_blocks, 256, 0, s>>>(a);
+    k_gauss_live<<<live_blocks, LIVE_THREADS, 0, s>>>(a);
 }
 
 }  // namespace gs

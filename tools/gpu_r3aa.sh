@@ -1,0 +1,6 @@
+set -e
+OUT=gpurun_out/r3aa; mkdir -p $OUT/ab
+export TMPDIR=/tmp
+DOGS_HIP_LIB=$(pwd)/ab/l64.so timeout -k 10 400 python -u -m pytest tests/test_gpu_raster.py tests/test_gpu_boundary.py tests/test_gpu_admm.py -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests_l64.log 2>&1 || { echo "gpu tests rc=$?" >> $OUT/gpu_tests_l64.log; exit 0; }
+bash tools/abn.sh $OUT/ab 3 ab/l256.so ab/l64.so ab/l64c32.so ab/l128.so
+bash tools/kprof.sh $OUT/kp ab/l64.so
