@@ -104,6 +104,7 @@ struct Geom {
     uint32_t* hist;                  // [DH_BINS] depth histogram of the prefix cut
     uint32_t* wtot;                  // [bin_waves(P)] per-wave instance totals of the binning walk
     uint64_t* wmask;                 // [bin_waves(P)] per-wave member ballot of the binning walk
+    uint64_t* kmask;                 // [bin_waves(P) * KM_STEPS] kept ballots of the phase-1 count walk's first steps
     uint32_t* mlist;                 // [P] member lists of the fat binning waves
     void* scan_tmp;
     size_t bytes;
@@ -122,6 +123,7 @@ Geom carve_geom(void* base, int P) {
     g.hist = c.take<uint32_t>(gs::DH_BINS);
     g.wtot = c.take<uint32_t>((size_t)gs::bin_waves(P > 0 ? P : 1));
     g.wmask = c.take<uint64_t>((size_t)gs::bin_waves(P > 0 ? P : 1));
+    g.kmask = c.take<uint64_t>((size_t)gs::bin_waves(P > 0 ? P : 1) * gs::KM_STEPS);
     g.mlist = c.take<uint32_t>(n);
     g.scan_tmp = c.take<char>(gs::bin_scan_temp_bytes(P > 0 ? P : 1));
     g.bytes = c.off;
@@ -209,6 +211,7 @@ gs::BinArgs bin_args(const dg_raster_args* r, const Geom& g, const Image& im, in
     a.eg = b.eg; a.ikey = b.ik; a.flag = b.flag; a.tile_cnt = tile_cnt; a.ranges = ranges; a.s_e = b.se;
     a.unf_rows = nullptr; a.unf_rw = 0; a.unf_th = 0; a.probe = nullptr; a.colors_later = 0;
     a.ohist = nullptr; a.max_contrib = nullptr; a.ranges1 = nullptr; a.unf_list = nullptr; a.unf_sorted = nullptr;
+    a.kmask = g.kmask;
     return a;
 }
 // per-tile (depth, index) order of a phase's binned lists

@@ -225,7 +225,14 @@ struct BinArgs {
     // longest tiles, so those do not share a compute unit with another tile's block
     const uint32_t* unf_list;
     uint32_t* unf_sorted;
+    // [bin_waves(P) * KM_STEPS] (phase 1): the count pass's kept ballot of each of a wave's first KM_STEPS walk steps;
+    // the emission walks the same candidates in the same steps and takes `kept` from here (no per-tile power test)
+    uint64_t* kmask;
 };
+#ifndef DG_KM_STEPS
+#define DG_KM_STEPS 8
+#endif
+constexpr int KM_STEPS = DG_KM_STEPS;  // 0: the emission recomputes every test
 void launch_bin(int phase, const BinArgs& a, uint32_t* total, void* scan_tmp, hipStream_t s,
                 hipEvent_t wait_before_emit = nullptr);
 // rgbi of the phase-1 Gaussians that got instances (rcnt > 0, key < thr), for an emission run with colors_later

@@ -96,9 +96,15 @@ struct CandLDS {
     float4 rc[64];        // max_contrib_power reciprocals (mcp_recips), rect x0, y0 (int bits)
 };
 
-template <typename Visit>
+// `known`: the kept ballots a previous walk of the same candidates recorded -- known.have(step) (wave-uniform) says
+// whether step `step` has one, known.mask(step) is it; such steps skip the per-tile power test.
+struct NoKnownKept {
+    __device__ __forceinline__ bool have(uint32_t) const { return false; }
+    __device__ __forceinline__ uint64_t mask(uint32_t) const { return 0ull; }
+};
+template <typename Visit, typename Known = NoKnownKept>
 __device__ __forceinline__ void wave_candidates(CandLDS& L, int lane, int x0, int y0, int x1, int y1, float mx, float my,
-                                                float4 co, float thr, Visit&& visit) {
+                                                float4 co, float thr, Visit&& visit, const Known& known = Known{}) {
     const uint32_t area = (x1 > x0 && y1 > y0) ? (uint32_t)(x1 - x0) * (uint32_t)(y1 - y0) : 0u;
     uint32_t incl = area;
 #pragma unroll
@@ -136,6 +142,8 @@ __device__ __forceinline__ void wave_candidates(CandLDS& L, int lane, int x0, in
         bool kept = false;
         int tx = 0, ty = 0;
         if (!valid) owner = 0;
+        const uint32_t step = i0 >> 6;
+        const bool have = known.have(step);  // wave-uniform
         if (valid) {
             const int r = (int)(item - L.pre[owner]);
             const int ww = L.w[owner];
@@ -147,11 +155,15 @@ __device__ __forceinline__ void wave_candidates(CandLDS& L, int lane, int x0, in
             if (rx < 0) { qy--; rx += ww; } else if (rx >= ww) { qy++; rx -= ww; }
             tx = __float_as_int(rc.z) + rx;
             ty = __float_as_int(rc.w) + qy;
-            const float4 c = L.co[owner];
-            const float p = max_contrib_power_rc<15>(f4{c.x, c.y, c.z, c.w}, g.x, g.y, (float)(tx * GS_TILE_X),
-                                                     (float)(ty * GS_TILE_Y), (float)((tx + 1) * GS_TILE_X - 1),
-                                                     (float)((ty + 1) * GS_TILE_Y - 1), rc.x, rc.y);
-            kept = p <= g.z;
+            if (have) {
+                kept = ((known.mask(step) >> lane) & 1ull) != 0ull;
+            } else {
+                const float4 c = L.co[owner];
+                const float p = max_contrib_power_rc<15>(f4{c.x, c.y, c.z, c.w}, g.x, g.y, (float)(tx * GS_TILE_X),
+                                                         (float)(ty * GS_TILE_Y), (float)((tx + 1) * GS_TILE_X - 1),
+                                                         (float)((ty + 1) * GS_TILE_Y - 1), rc.x, rc.y);
+                kept = p <= g.z;
+            }
         }
         visit(owner, tx, ty, kept, valid, item);
     }
@@ -453,13 +465,16 @@ __device__ __forceinline__ void depth_cut_block(const uint32_t* __restrict__ his
 // wave-cooperative candidate walk, into cnt[lane] (LDS, zeroed here).  keep(tx, ty) filters tiles further.
 template <typename Keep, typename OnKept>
 __device__ __forceinline__ void wave_count(CandLDS& L, uint32_t* cnt, int lane, int x0, int y0, int x1, int y1,
-                                           float mx, float my, float4 co, float thr, Keep&& keep, OnKept&& on_kept) {
+                                           float mx, float my, float4 co, float thr, Keep&& keep, OnKept&& on_kept,
+                                           uint64_t* kmask = nullptr) {
     cnt[lane] = 0u;
     wave_candidates(L, lane, x0, y0, x1, y1, mx, my, co, thr,
                     [&](int owner, int tx, int ty, bool kept, bool valid, uint32_t item) {
                         kept = kept && keep(tx, ty);
                         if (kept) on_kept(tx, ty);
                         const uint64_t km = __ballot(kept);
+                        const uint32_t step = (item - (uint32_t)lane) >> 6;
+                        if (kmask && lane == 0 && step < (uint32_t)KM_STEPS) kmask[step] = km;
                         // first item of each owner segment in this step adds the segment's kept count
                         const bool seg_start = valid && (lane == 0 || item == L.pre[owner]);
                         if (seg_start) {
@@ -601,7 +616,8 @@ __global__ void __launch_bounds__(256) k_bin_count(BinArgs a) {
     if (members) {
         wave_count(s_cand[w], s_cnt[w], lane, b.x0, b.y0, b.x1, b.y1, b.mx, b.my, b.co, b.lthr,
                    [&](int tx, int ty) { return PHASE == 1 || a.unf[ty * a.tiles_x + tx] != 0; },
-                   [&](int tx, int ty) { atomicAdd(&a.tile_cnt[ty * a.tiles_x + tx], 1u); });
+                   [&](int tx, int ty) { atomicAdd(&a.tile_cnt[ty * a.tiles_x + tx], 1u); },
+                   PHASE == 1 && KM_STEPS > 0 && a.kmask ? a.kmask + (size_t)wave * KM_STEPS : nullptr);
         c = s_cnt[w][lane];
         if (b.member) a.rcnt[g] = c;
     }
@@ -713,6 +729,13 @@ __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
         if (PHASE == 2 || !a.colors_later) binned_colour(a, g, s_key[w][lane]);
     }
     uint32_t running = 0;
+    // phase 1: the kept ballots of the first KM_STEPS steps from the count pass (the same candidates, step by step)
+    struct KnownKept {
+        const uint64_t* km;
+        __device__ __forceinline__ bool have(uint32_t step) const { return km && step < (uint32_t)KM_STEPS; }
+        __device__ __forceinline__ uint64_t mask(uint32_t step) const { return km[step]; }
+    };
+    const KnownKept known = {PHASE == 1 && KM_STEPS > 0 && a.kmask ? a.kmask + (size_t)wave * KM_STEPS : nullptr};
     wave_candidates(s_cand[w], lane, b.x0, b.y0, b.x1, b.y1, b.mx, b.my, b.co, b.lthr,
                     [&](int owner, int tx, int ty, bool kept, bool, uint32_t) {
                         kept = kept && (PHASE == 1 || a.unf[ty * a.tiles_x + tx] != 0);
@@ -727,7 +750,7 @@ __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
                             a.s_e[atomicAdd(&a.tile_cnt[t], 1u)] = e;
                         }
                         running += (uint32_t)__popcll(km);
-                    });
+                    }, known);
 }
 
 // ---- Fat binning waves (R x 64 consecutive Gaussians per wave; DG_BIN_FAT1 / DG_BIN_FAT2 = R of phase 1 / 2).
@@ -824,7 +847,8 @@ __global__ void __launch_bounds__(256) k_bin_count_fat(BinArgs a) {
         const BinLane b = member_lane(a, g, member);
         wave_count(s_cand[w], s_cnt[w], lane, b.x0, b.y0, b.x1, b.y1, b.mx, b.my, b.co, b.lthr,
                    [&](int tx, int ty) { return PHASE == 1 || a.unf[ty * a.tiles_x + tx] != 0; },
-                   [&](int tx, int ty) { atomicAdd(&a.tile_cnt[ty * a.tiles_x + tx], 1u); });
+                   [&](int tx, int ty) { atomicAdd(&a.tile_cnt[ty * a.tiles_x + tx], 1u); },
+                   PHASE == 1 && KM_STEPS > 0 && a.kmask ? a.kmask + (size_t)wave * KM_STEPS : nullptr);
         const uint32_t c = member ? s_cnt[w][lane] : 0u;
         if (member) a.rcnt[g] = c;
         uint32_t sc = c;
