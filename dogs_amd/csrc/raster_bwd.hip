@@ -310,10 +310,11 @@ __device__ __forceinline__ uint32_t replay_len(const RenderBwdArgs& a, int tile)
 __global__ void __launch_bounds__(256) BWD_WPE_ATTR k_render_bwd(RenderBwdArgs a) {
     __shared__ float4 s_b[4][64][3];
     const int lane = threadIdx.x & 63;
-    if (a.zero_base) {
-        // The replay is VALU-bound and leaves HBM mostly idle: each wave zero-fills its share of the gradient
-        // outputs (fire-and-forget 16-B stores) for the per-Gaussian pass, which then writes only the contributing
-        // Gaussians.  Shares are whole 1-KiB chunks, so every store is aligned.
+    // The replay is VALU-bound and leaves HBM mostly idle: each wave zero-fills its share of the gradient outputs
+    // (fire-and-forget 16-B stores) for the per-Gaussian pass, which then writes only the contributing Gaussians.
+    // Shares are whole 1-KiB chunks, so every store is aligned.
+    auto zero_share = [&]() {
+        if (!a.zero_base) return;
         const size_t nw = (size_t)gridDim.x * 4, gw = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
         const size_t n4 = a.zero_count / 4;
         const size_t per = ((n4 + nw - 1) / nw + 63) & ~(size_t)63;
@@ -322,9 +323,17 @@ __global__ void __launch_bounds__(256) BWD_WPE_ATTR k_render_bwd(RenderBwdArgs a
         for (size_t i = gw * per + lane; i < e4; i += 64) z4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (gw == 0)
             for (size_t i = (n4 << 2) + lane; i < a.zero_count; i += 64) a.zero_base[i] = 0.f;
-    }
+    };
     const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);
+    // The share goes out after the wave's replay: issued at the start, the first round of waves put ~140 MB of stores
+    // in front of their own gathers (render_bwd 275-277 -> 266-267 us per view with the stores at the end,
+    // profiles/r03af_bwd_fill_late_ab.txt; DG_BWD_FILL_EARLY restores the start).
+#ifdef DG_BWD_FILL_EARLY
+    zero_share();
     if (slot >= a.num_tiles) return;
+#else
+    if (slot >= a.num_tiles) { zero_share(); return; }
+#endif
     const int tile = a.order ? (int)a.order[slot] : slot;
     float4* sb = &s_b[threadIdx.x >> 6][0][0];
     const bool has_bg = a.bg[0] != 0.0f || a.bg[1] != 0.0f || a.bg[2] != 0.0f;
@@ -346,6 +355,9 @@ __global__ void __launch_bounds__(256) BWD_WPE_ATTR k_render_bwd(RenderBwdArgs a
         if (has_bg) render_bwd_tile<false, true>(a, tile, lane, sb);
         else render_bwd_tile<false, false>(a, tile, lane, sb);
     }
+#ifndef DG_BWD_FILL_EARLY
+    zero_share();
+#endif
 }
 
 // The replay order when the forward did not compute it (no phase 2: its emission launch carries the order block):
