@@ -1,0 +1,6 @@
+set -e
+OUT=gpurun_out/r3aj; mkdir -p $OUT/ab
+export TMPDIR=/tmp DOGS_TEST_LOG=$OUT/fullsize.jsonl
+DOGS_HIP_LIB=$(pwd)/ab/seg1.so timeout -k 10 600 python -u -m pytest tests/test_gpu_raster.py tests/test_gpu_boundary.py tests/test_gpu_aux.py tests/test_gpu_fullsize.py -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests_seg1.log 2>&1 || { echo "gpu tests rc=$?" >> $OUT/gpu_tests_seg1.log; exit 0; }
+bash tools/abn.sh $OUT/ab 3 ab/seg0.so ab/seg1.so
+bash tools/kprof.sh $OUT/kp ab/seg1.so
