@@ -315,7 +315,11 @@ __global__ void __launch_bounds__(256) BWD_WPE_ATTR k_render_bwd(RenderBwdArgs a
     // Shares are whole 1-KiB chunks, so every store is aligned.
     auto zero_share = [&]() {
         if (!a.zero_base) return;
-        const size_t nw = (size_t)gridDim.x * 4, gw = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+        // only the first 3/4 of the launch order (the longer replays, longest first) fill, so the kernel's tail has no
+        // store drain (render_bwd 257-260 -> 255-258 us, profiles/r03al_bwd_fill_front_ab.txt)
+        const size_t nw_all = (size_t)gridDim.x * 4, gw = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+        const size_t nw = nw_all * 3 / 4 > 0 ? nw_all * 3 / 4 : 1;
+        if (gw >= nw) return;
         const size_t n4 = a.zero_count / 4;
         const size_t per = ((n4 + nw - 1) / nw + 63) & ~(size_t)63;
         float4* z4 = reinterpret_cast<float4*>(a.zero_base);
