@@ -46,7 +46,8 @@ class DgDensifyStats(C.Structure):
 class DgTrainStepArgs(C.Structure):
     _fields_ = [("view", DgRasterArgs), ("gt", C.c_void_p), ("lambda_dssim", C.c_float), ("lambda_scale", C.c_float),
                 ("groups", DgAdamGroup * 6), ("prox", DgAdamProx * 6), ("stats", C.c_void_p), ("radii", C.c_void_p),
-                ("image", C.c_void_p), ("loss", C.c_void_p), ("sh_status", C.c_void_p)]
+                ("image", C.c_void_p), ("loss", C.c_void_p), ("sh_status", C.c_void_p), ("mask", C.c_void_p),
+                ("dmask", C.c_void_p), ("lambda_mask", C.c_float), ("depth_threshold", C.c_float)]
 
 
 class DgGaussianSet(C.Structure):

@@ -15,14 +15,21 @@ Reference order (rank 0's master, once, at the first round with iteration >= den
 Here every rank runs the entry for its own block ("one block per GPU"):
     * the blocks' tensors are all-gathered (variable row counts: one all_gather of the sizes, one of the padded
       [N_max, 59] rows), so every rank fuses the same global model -- clipping, concatenation, the box tests and the
-      prune compaction are deterministic, so the ranks agree bit for bit without further exchange;
-    * the count renders are split across ranks: rank r renders its own block's cameras only, and the per-block
-      importance sums are all-gathered and added in block order (the cameras' work is parallel, the sum order fixed);
+      prune compaction are deterministic, so the ranks agree bit for bit without further exchange.  Memory: every
+      rank holds the fused model, 236 B per Gaussian (config 5, 8 blocks x 5e6: 9.4 GB of a rank's 288 GB of HBM),
+      as the reference's master does once;
+    * the count renders are split across ranks: rank r renders its own block's cameras only, keeping each camera's
+      score vector (cameras x 4 B per fused Gaussian);
+    * the importance is then summed in the reference's exact order: prune_gaussians_after_merge concatenates the
+      blocks' camera lists and prune_list pops from the end, so the float32 sum is one left fold over block B-1's
+      cameras (last first), then block B-2's, ..., then block 0's.  The fold runs as a chain over the ranks
+      (rank B-1 folds its scores and sends the [N] partial to rank B-2, which folds its own onto it, ...; the adds are
+      cheap next to the renders, which all ranks did in parallel), and rank 0 broadcasts the total.  The result is
+      bit-identical to prune_list over the concatenated list, so the percentile threshold of v_imp_prune keeps and
+      drops the same Gaussians as the reference;
     * the expanded-box split, visibility_count and the rank's sub-model follow locally.
-The importance of a Gaussian is therefore sum_b (sum over block b's cameras, last camera first) instead of one sum
-over the concatenated camera list (prune_list pops the whole list from the end): the same terms, associated per block,
-a float rounding difference only (the counts are integers and exact).  `enter_admm_phase_sequential` restates it in one
-process with the same association (the reference's single-process order per block; the tests compare the two).
+`enter_admm_phase_sequential` runs the same entry in one process with prune_list over the concatenated camera list
+(the reference's own order; the tests compare the two bit for bit).
 
 The device work goes through `PhaseKernels` (HIP: dg_rasterize_count, dg_points_in_boxes2d, dg_prune_select +
 dg_densify_gather); the CPU tests substitute restatements of the same three operations to check the distributed
@@ -51,13 +58,18 @@ class PhaseConfig:
 class PhaseKernels:
     """The phase entry's device operations (HIP)."""
 
+    def camera_importance(self, model: GaussianSplatModel, camera, bg: torch.Tensor) -> torch.Tensor:
+        """count_render's important_score of one camera, float32 [N]."""
+        from .prune import count_render
+        cam = camera.to(model.get_xyz.device) if hasattr(camera, "to") else camera
+        return count_render(model, cam, None, bg)["important_score"]
+
     def importance(self, model: GaussianSplatModel, cameras: list, bg: torch.Tensor) -> torch.Tensor:
-        """prune_list's important_score summed over `cameras` (last camera first), float32 [N]."""
-        from .prune import prune_list
-        n = model.num_gaussians
-        if not cameras:
-            return torch.zeros(n, dtype=torch.float32, device=model.get_xyz.device)
-        return prune_list(model, cameras, None, bg)[1]
+        """prune_list's important_score summed over `cameras` (last camera first, one float32 left fold), [N]."""
+        acc = torch.zeros(model.num_gaussians, dtype=torch.float32, device=model.get_xyz.device)
+        for cam in reversed(list(cameras)):
+            acc += self.camera_importance(model, cam, bg)
+        return acc
 
     def members(self, xy: torch.Tensor, boxes: list, transform) -> list:
         """[ascending int64 indices of the points inside each closed box (in the OBB frame)]."""
@@ -127,8 +139,37 @@ def fuse_blocks(block_models: list, ori_point_bboxes, world_to_obb_transform, ke
     like = block_models[0]
     fused = GaussianSplatModel(like.max_sh_degree, like.percent_dense, like.get_xyz.device)
     fused.init_from_external_properties(*_split_rows(torch.cat(parts, 0), like), optimizable=False)
-    fused.active_sh_degree = like.active_sh_degree
+    # the master's model is created with active_sh_degree = max_sh_degree (master_gaussian_trainer.py:216-220), and
+    # the blocks' sub-models inherit it (get_sub_gaussians, gaussian_splat_model.py:290-306)
+    fused.active_sh_degree = like.max_sh_degree
     return fused
+
+
+def ordered_importance(fused: GaussianSplatModel, camera_blocks: list, kernels: PhaseKernels, bg: torch.Tensor,
+                       group=None) -> torch.Tensor:
+    """prune_list's importance over the concatenation of every block's cameras, bit for bit, with each rank rendering
+    only its own block's cameras: the per-camera scores are kept, folded down a chain of ranks in the reference's
+    order (block B-1's last camera first ... block 0's first camera last), and broadcast from rank 0."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    dev = fused.get_xyz.device
+    n = fused.num_gaussians
+    own = [kernels.camera_importance(fused, cam, bg).float() for cam in reversed(list(camera_blocks[rank]))]
+    host = _gather_device(group)
+    wire = host if host is not None else dev
+    acc = torch.zeros(n, dtype=torch.float32, device=dev)
+    if rank < world - 1:
+        buf = torch.empty(n, dtype=torch.float32, device=wire)
+        dist.recv(buf, src=dist.get_global_rank(group, rank + 1) if group is not None else rank + 1, group=group)
+        acc = buf.to(dev)
+    for sc in own:
+        acc += sc
+    del own
+    if rank > 0:
+        dist.send(acc.to(wire), dst=dist.get_global_rank(group, rank - 1) if group is not None else rank - 1,
+                  group=group)
+    out = acc.to(wire)
+    dist.broadcast(out, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    return out.to(dev)
 
 
 def v_imp_prune(model: GaussianSplatModel, imp: torch.Tensor, cfg: PhaseConfig, kernels: PhaseKernels) -> None:
@@ -205,12 +246,8 @@ def enter_admm_phase(block_model: GaussianSplatModel, camera_blocks: list, ori_p
         blocks.append(m)
     fused = fuse_blocks(blocks, ori_point_bboxes, world_to_obb_transform, kernels)
     del blocks, rows
-    # 2. importance: this rank's cameras only, then the per-block partial sums added in block order
-    part = kernels.importance(fused, camera_blocks[rank], bg).float().reshape(-1, 1)
-    parts = all_gather_rows(part, group)
-    imp = parts[0].reshape(-1).clone()
-    for p in parts[1:]:
-        imp += p.reshape(-1)
+    # 2. importance: this rank renders its cameras only, summed in the reference's order down the rank chain
+    imp = ordered_importance(fused, camera_blocks, kernels, bg, group)
     v_imp_prune(fused, imp, cfg, kernels)
     rho_gaussians = fused.num_gaussians
     # 4. the expanded-box split
@@ -229,10 +266,8 @@ def enter_admm_phase_sequential(block_models: list, camera_blocks: list, ori_poi
     dev = block_models[0].get_xyz.device
     bg = torch.zeros(3, dtype=torch.float32, device=dev) if bg is None else bg
     fused = fuse_blocks(block_models, ori_point_bboxes, world_to_obb_transform, kernels)
-    imp = None
-    for cams in camera_blocks:
-        p = kernels.importance(fused, cams, bg).float().reshape(-1)
-        imp = p.clone() if imp is None else imp + p
+    # prune_gaussians_after_merge (:103-121): prune_list over the blocks' concatenated camera lists
+    imp = kernels.importance(fused, [c for cams in camera_blocks for c in cams], bg).float().reshape(-1)
     v_imp_prune(fused, imp, cfg, kernels)
     rho_gaussians = fused.num_gaussians
     vis, gidx, subs = select_gaussians_in_each_block(exp_point_bboxes, fused, world_to_obb_transform, kernels)

@@ -66,6 +66,7 @@ class TrainConfig:
     sh_degree: int = 3
     start_iteration: int = 30000   # densify_end_iter: where the ADMM phase begins
     background: tuple = (0.0, 0.0, 0.0)
+    anti_aliasing: bool = False    # texture.anti_aliasing
 
 
 class ExponentialLR:
@@ -150,7 +151,7 @@ class BlockTrainer:
         bg = torch.tensor(c.background, dtype=torch.float32, device=self.device)
         self.rasts = [GaussianRasterizer(GaussianRasterizationSettings(
             cam.height, cam.width, cam.tanfovx, cam.tanfovy, bg, 1.0, cam.world_to_camera, cam.projective_matrix,
-            c.sh_degree, cam.camera_center, False, False, False, 0.0)) for cam in cameras]
+            c.sh_degree, cam.camera_center, False, False, bool(c.anti_aliasing), 0.0)) for cam in cameras]
         self.images = images
         self.rng = np.random.default_rng(seed)
         self.order: list[int] = []
@@ -166,7 +167,7 @@ class BlockTrainer:
             # parameters, and penalty() syncs
             self._nts = NativeTrainStep({n: self.params[n] for n in PARAM_NAMES}, self.opt, cameras, images,
                                         c.sh_degree, c.lambda_dssim, c.lambda_scale, bg, self.device,
-                                        overlap=overlap)
+                                        overlap=overlap, antialiasing=c.anti_aliasing)
 
     @property
     def last_loss(self):
@@ -205,6 +206,7 @@ class BlockTrainer:
         """One training iteration through the drop-in autograd API (the reference's route: rasterizer, clamp/L1 and
         SSIM autograd functions, torch for the loss sum and the scale regulariser, SparseGaussianAdam with the
         penalty's proximal gradient); returns the loss without the penalty (a device scalar, no sync)."""
+        self.sync()   # an overlapped native update of f_dc / f_rest may still be running
         self.iteration += 1
         for g in self.opt.param_groups:
             if g["name"] == "xyz":

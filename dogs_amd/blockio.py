@@ -102,7 +102,8 @@ class BlockCamera:
                    d["cy"], d["image_path"])
 
     def raster_camera(self, device="cpu", znear: float = 0.01, zfar: float = 100.0) -> RasterCamera:
-        return make_camera(self.width, self.height, self.fx, self.fy, self.world_to_camera, znear, zfar).to(device)
+        return make_camera(self.width, self.height, self.fx, self.fy, self.world_to_camera, znear, zfar,
+                           image_index=int(self.image_index)).to(device)
 
 
 @dataclass

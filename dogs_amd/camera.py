@@ -45,6 +45,9 @@ class RasterCamera:
     world_to_camera: torch.Tensor      # [4,4] = w2c^T (what the rasterizer calls viewmatrix)
     projective_matrix: torch.Tensor    # [4,4] = w2c^T @ P^T
     camera_center: torch.Tensor        # [3]
+    image_index: int = -1              # the dataset's image index (appearance embedding / trained exposure row)
+    znear: float = 0.01
+    zfar: float = 100.0
 
     @property
     def tanfovx(self) -> float:
@@ -57,11 +60,32 @@ class RasterCamera:
     def to(self, device) -> "RasterCamera":
         return RasterCamera(self.width, self.height, self.fov_x, self.fov_y,
                             self.world_to_camera.to(device), self.projective_matrix.to(device),
-                            self.camera_center.to(device))
+                            self.camera_center.to(device), self.image_index, self.znear, self.zfar)
+
+    @property
+    def fx(self) -> float:
+        return self.width / (2.0 * math.tan(self.fov_x * 0.5))
+
+    @property
+    def fy(self) -> float:
+        return self.height / (2.0 * math.tan(self.fov_y * 0.5))
+
+    def downsample(self, resolution: int = 1) -> "RasterCamera":
+        """Camera.downsample (conerf/geometry/camera.py:146-163): focal lengths / resolution, image size
+        ceil(size / resolution), the same pose; the matrices are rebuilt on the camera's device."""
+        if resolution == 1:
+            return self
+        dev = self.world_to_camera.device
+        w2c = self.world_to_camera.detach().cpu().transpose(0, 1)
+        cam = make_camera(math.ceil(self.width / resolution), math.ceil(self.height / resolution),
+                          self.fx / resolution, self.fy / resolution, world_to_camera=w2c, znear=self.znear,
+                          zfar=self.zfar)
+        cam.image_index = self.image_index
+        return cam.to(dev)
 
 
 def make_camera(width: int, height: int, fx: float, fy: float, world_to_camera: torch.Tensor | None = None,
-                znear: float = 0.01, zfar: float = 100.0) -> RasterCamera:
+                znear: float = 0.01, zfar: float = 100.0, image_index: int = -1) -> RasterCamera:
     if world_to_camera is None:
         world_to_camera = torch.eye(4)
     w2c = world_to_camera.to(torch.float32)
@@ -71,7 +95,8 @@ def make_camera(width: int, height: int, fx: float, fy: float, world_to_camera: 
     proj = projection_matrix(znear, zfar, fov_x, fov_y).transpose(0, 1)
     full = view @ proj
     center = view.inverse()[3, :3]
-    return RasterCamera(width, height, fov_x, fov_y, view.contiguous(), full.contiguous(), center.contiguous())
+    return RasterCamera(width, height, fov_x, fov_y, view.contiguous(), full.contiguous(), center.contiguous(),
+                        image_index, znear, zfar)
 
 
 def yaw_world_to_camera(yaw_rad: float) -> torch.Tensor:

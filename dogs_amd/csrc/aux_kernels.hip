@@ -63,13 +63,16 @@ __device__ __forceinline__ float clamp01f(float x) { return x != x ? x : fminf(f
 // FUSED (the native training step): img1 is the raw render, read through clamp(0, 1); the clamped image goes to
 // out_img, and each wave writes its partial sums of |clamped - gt| and of the map (part[wave], part[nwaves + wave])
 // instead of the map itself -- render()'s clamp, the L1 term and the SSIM mean in the same pass.
-template <bool TRAIN, bool FUSED = false>
+// MASK (with FUSED): the appearance mask multiplies the clamped render inside the L1 term (|clamped * mask - gt|), and a
+// third set of per-wave partials holds sum (mask - 1)^2 (gaussian_trainer.py:392-401)
+template <bool TRAIN, bool FUSED = false, bool MASK = false>
 __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes, float C1, float C2,
                                                         const float* __restrict__ img1, const float* __restrict__ img2,
                                                         float* __restrict__ map, float* __restrict__ dmu1,
                                                         float* __restrict__ ds1, float* __restrict__ ds12,
                                                         float* __restrict__ out_img = nullptr,
-                                                        float* __restrict__ part = nullptr) {
+                                                        float* __restrict__ part = nullptr,
+                                                        const float* __restrict__ mask = nullptr) {
     const StripPos sp = strip_of(H, W, planes);
     if (!sp.valid) return;  // wave-uniform
     const int lane = threadIdx.x & 63;
@@ -88,7 +91,7 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
     auto ldb = [&](int row) -> float {
         return (colok && row >= 0 && row < H) ? b[(size_t)row * W + sp.x] : 0.0f;
     };
-    float acc_l1 = 0.0f, acc_map = 0.0f;
+    float acc_l1 = 0.0f, acc_map = 0.0f, acc_mreg = 0.0f;
     float ring[11][5];
     // FUSED: the clamped image and the L1 term as the input rows arrive -- lanes 5..58 hold the strip's output columns
     const bool own_col = FUSED && lane >= 5 && lane < 5 + SSW_OUT && colok;
@@ -106,8 +109,15 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
                 if (FUSED) {
                     const int row = sp.y0 - 5 + rr;  // one of the strip's output rows
                     if (own_col && row >= sp.y0 && row < sp.y0 + SSW_ROWS && row < H) {
-                        out_img[plane + (size_t)row * W + sp.x] = u;
-                        acc_l1 += fabsf(u - v);
+                        const size_t gi = plane + (size_t)row * W + sp.x;
+                        out_img[gi] = u;
+                        if (MASK) {
+                            const float mk = mask[gi], dm = mk - 1.0f;
+                            acc_l1 += fabsf(u * mk - v);
+                            acc_mreg += dm * dm;
+                        } else {
+                            acc_l1 += fabsf(u - v);
+                        }
                     }
                 }
                 ring[j][0] = hconv11(u);
@@ -168,30 +178,33 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
         for (int o = 32; o > 0; o >>= 1) {
             acc_l1 += __shfl_xor(acc_l1, o);
             acc_map += __shfl_xor(acc_map, o);
+            if (MASK) acc_mreg += __shfl_xor(acc_mreg, o);
         }
         if (lane == 0) {
             const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
             const int nw = ((W + SSW_OUT - 1) / SSW_OUT) * ((H + SSW_ROWS - 1) / SSW_ROWS) * planes;
             part[wid] = acc_l1;
             part[nw + wid] = acc_map;
+            if (MASK) part[2 * nw + wid] = acc_mreg;
         }
     }
 }
 
 // The step's loss (k_loss_final's arithmetic, 256 threads): each total strided per thread, then the 4 wave sums in order.
+// loss[3]: mean (mask - 1)^2 from p_mreg, 0 without a mask.
 __device__ __forceinline__ void loss_final_block(const LossFinal& f) {
-    __shared__ float s_w[3][4];
-    const float* ps[3] = {f.p_l1, f.p_ssim, f.p_sc};
-    const uint32_t ns[3] = {f.n_l1, f.n_ssim, f.n_sc};
+    __shared__ float s_w[4][4];
+    const float* ps[4] = {f.p_l1, f.p_ssim, f.p_sc, f.p_mreg};
+    const uint32_t ns[4] = {f.n_l1, f.n_ssim, f.n_sc, f.p_mreg ? f.n_mreg : 0u};
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
+    for (int k = 0; k < 4; k++) {
         float acc = 0.0f;
         for (uint32_t i = threadIdx.x; i < ns[k]; i += 256) acc += ps[k][i];
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
         if ((threadIdx.x & 63) == 0) s_w[k][threadIdx.x >> 6] = acc;
     }
     __syncthreads();
-    if (threadIdx.x < 3) {
+    if (threadIdx.x < 4) {
         const int k = threadIdx.x;
         const float acc = (s_w[k][0] + s_w[k][1]) + (s_w[k][2] + s_w[k][3]);
         f.loss[k] = acc / (float)(k == 2 ? f.P : f.n_img);
@@ -201,13 +214,17 @@ __device__ __forceinline__ void loss_final_block(const LossFinal& f) {
 // FUSED (the native training step): img1 is the clamped image, raw the render before the clamp, and the output is
 // the gradient w.r.t. the raw render of (1 - ld) L1 + ld (1 - SSIM): (dSSIM + g_l1 sgn(img1 - img2) / n) where the
 // render lies in [0, 1], else 0 -- k_clamp_l1_bwd's expression in the same pass.
-template <bool FUSED = false>
+// MASK (with FUSED): the L1 term is of clamped * mask, so its gradient reaches the clamped image times the mask, and
+// dmask gets l1_scale sgn(clamped * mask - gt) clamped + mreg_scale (mask - 1) (mul's and pow's backward)
+template <bool FUSED = false, bool MASK = false>
 __global__ void __launch_bounds__(256) k_ssim_bwd_strip(int H, int W, int planes, const float* __restrict__ img1,
                                                         const float* __restrict__ img2, const float* __restrict__ dL,
                                                         float dl_value, const float* __restrict__ dmu1,
                                                         const float* __restrict__ ds1, const float* __restrict__ ds12,
                                                         float* __restrict__ dimg1, const float* __restrict__ raw = nullptr,
-                                                        float l1_scale = 0.0f, LossFinal lf = {}, uint32_t lblk = 0) {
+                                                        float l1_scale = 0.0f, LossFinal lf = {}, uint32_t lblk = 0,
+                                                        const float* __restrict__ mask = nullptr,
+                                                        float* __restrict__ dmask = nullptr, float mreg_scale = 0.0f) {
     // lblk = 1: block 0 computes the step's loss (dispatched first, beside the strips), the strips follow
     if (lblk && blockIdx.x == 0) { loss_final_block(lf); return; }
     const StripPos sp = strip_of(H, W, planes, lblk);
@@ -258,10 +275,14 @@ __global__ void __launch_bounds__(256) k_ssim_bwd_strip(int H, int W, int planes
                         d += (i1 * 2.0f) * v1;
                         d += i2 * v2;
                         if (FUSED) {
-                            const float x = raw[gi], e = i1 - i2;
+                            const float x = raw[gi];
+                            const float mk = MASK ? mask[gi] : 1.0f;
+                            const float e = MASK ? i1 * mk - i2 : i1 - i2;
                             const float sg = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
-                            const float gsum = d + l1_scale * sg;
+                            const float gl = l1_scale * sg;
+                            const float gsum = d + (MASK ? gl * mk : gl);
                             d = (x >= 0.f && x <= 1.f) ? gsum : 0.f;
+                            if (MASK) dmask[gi] = gl * i1 + mreg_scale * (mk - 1.0f);
                         }
                         dimg1[gi] = d;
                     }
@@ -296,19 +317,28 @@ void launch_ssim_bwd(int B, int CH, int H, int W, const float* img1, const float
                                                                         ds1, ds12, dimg1);
 }
 void launch_ssim_fwd_fused(int H, int W, float C1, float C2, const float* raw, const float* gt, float* clamped,
-                           float* dmu1, float* ds1, float* ds12, float* part, hipStream_t s) {
+                           float* dmu1, float* ds1, float* ds12, float* part, hipStream_t s, const float* mask) {
     if ((size_t)H * W == 0) return;
-    k_ssim_fwd_strip<true, true><<<ssim_strip_blocks(3, H, W), 256, 0, s>>>(H, W, 3, C1, C2, raw, gt, nullptr, dmu1, ds1,
-                                                                        ds12, clamped, part);
+    if (mask)
+        k_ssim_fwd_strip<true, true, true><<<ssim_strip_blocks(3, H, W), 256, 0, s>>>(
+            H, W, 3, C1, C2, raw, gt, nullptr, dmu1, ds1, ds12, clamped, part, mask);
+    else
+        k_ssim_fwd_strip<true, true><<<ssim_strip_blocks(3, H, W), 256, 0, s>>>(H, W, 3, C1, C2, raw, gt, nullptr, dmu1,
+                                                                            ds1, ds12, clamped, part);
 }
 void launch_ssim_bwd_fused(int H, int W, const float* clamped, const float* gt, const float* raw, float dl_value,
                            float l1_scale, const float* dmu1, const float* ds1, const float* ds12, float* d_raw,
-                           hipStream_t s, const LossFinal* lf) {
+                           hipStream_t s, const LossFinal* lf, const float* mask, float* dmask, float mreg_scale) {
     if ((size_t)H * W == 0) return;
     const uint32_t lb = lf ? 1u : 0u;
-    k_ssim_bwd_strip<true><<<ssim_strip_blocks(3, H, W) + lb, 256, 0, s>>>(H, W, 3, clamped, gt, nullptr, dl_value, dmu1,
-                                                                          ds1, ds12, d_raw, raw, l1_scale,
-                                                                          lf ? *lf : LossFinal{}, lb);
+    if (mask)
+        k_ssim_bwd_strip<true, true><<<ssim_strip_blocks(3, H, W) + lb, 256, 0, s>>>(
+            H, W, 3, clamped, gt, nullptr, dl_value, dmu1, ds1, ds12, d_raw, raw, l1_scale, lf ? *lf : LossFinal{}, lb,
+            mask, dmask, mreg_scale);
+    else
+        k_ssim_bwd_strip<true><<<ssim_strip_blocks(3, H, W) + lb, 256, 0, s>>>(H, W, 3, clamped, gt, nullptr, dl_value,
+                                                                              dmu1, ds1, ds12, d_raw, raw, l1_scale,
+                                                                              lf ? *lf : LossFinal{}, lb);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -12,6 +12,7 @@
 #include <tuple>
 #include <chrono>
 #include <mutex>
+#include <thread>
 
 #include "../../include/dogs_hip.h"
 #include "aux_kernels.h"
@@ -285,7 +286,11 @@ int wait_seq(HostCounters& h, hipStream_t s) {
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t it = 0;; it++) {
         if (__atomic_load_n(const_cast<uint32_t*>(w), __ATOMIC_ACQUIRE) == h.seq) return 0;
+#if defined(__x86_64__) || defined(__i386__)
         __builtin_ia32_pause();
+#else
+        if ((it & 63u) == 63u) std::this_thread::yield();
+#endif
         if ((it & 4095u) == 4095u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
     }
     HIP_OK(hipStreamSynchronize(s));
@@ -960,14 +965,26 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     const uint32_t nb_map = gs::block_sum_blocks((uint32_t)n_img), nb_sc = gs::block_sum_blocks((uint32_t)P);
     const uint32_t nw_ssim = gs::ssim_waves(3, H, W);  // the fused SSIM's partials: nw L1, then nw map
     const uint32_t nb_act = gs::preprocess_blocks(P);  // the fused route's regulariser partials (preprocess blocks)
-    const uint32_t n_part = (nb_l1 + nb_map > 2 * nw_ssim ? nb_l1 + nb_map : 2 * nw_ssim) + (nb_sc > nb_act ? nb_sc : nb_act);
-    // ---- the step's scratch (DG_BUF_TRAIN); the nine rasterizer gradients back to back (the replay zero-fills them)
+    // fused route: nw L1 partials, nw map partials, nw mask-regulariser partials, then the regulariser's
+    const uint32_t n_part = (nb_l1 + nb_map > 3 * nw_ssim ? nb_l1 + nb_map : 3 * nw_ssim) + (nb_sc > nb_act ? nb_sc : nb_act);
+    if (a->mask && (!a->dmask || ((reinterpret_cast<uintptr_t>(a->mask) | reinterpret_cast<uintptr_t>(a->dmask)) & 15u)))
+        return fail("train step: a mask needs a dmask output, both 16-byte aligned%s%d");
+    if (a->mask && getenv("DG_TRAIN_UNFUSED")) return fail("train step: the appearance mask needs the fused route%s%d");
+    // ---- the step's scratch (DG_BUF_TRAIN).  The nine rasterizer gradients (back to back: the replay zero-fills them)
+    // come first: the overlapped f_dc / f_rest update still reads ddc / dsh while the next step's forward writes this
+    // block, so their offsets must not depend on the image size (the arena hands the same block back to a view of
+    // another size whenever it fits)
     const size_t n9 = (3 + 3 + 1 + 3 + 6 + 3 + 3 * Mz + 3 + 4) * Pz;
     auto carve = [&](void* base, float** f) {
         Carver c(base);
+        f[11] = c.take<float>(n9);         // dmeans2D | dcolors | dopacity | dmeans3D | dcov3D | ddc | dsh | dscales | drot
         f[0] = c.take<float>(Pz);          // opacity (activated)
         f[1] = c.take<float>(3 * Pz);      // scaling
         f[2] = c.take<float>(4 * Pz);      // rotation
+        f[12] = c.take<float>(Pz);         // depth
+        f[13] = c.take<float>(Pz);         // raw opacity grad
+        f[14] = c.take<float>(3 * Pz);     // raw scaling grad
+        f[15] = c.take<float>(4 * Pz);     // raw quaternion grad
         f[3] = c.take<float>(n_img);       // raw render
         f[4] = c.take<float>(HW);          // inverse depth
         f[5] = c.take<float>(n_part);      // partial sums
@@ -976,11 +993,6 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
         f[8] = c.take<float>(n_img);       // dm/dsigma1_sq
         f[9] = c.take<float>(n_img);       // dm/dsigma12
         f[10] = c.take<float>(n_img);      // dL/dimage
-        f[11] = c.take<float>(n9);         // dmeans2D | dcolors | dopacity | dmeans3D | dcov3D | ddc | dsh | dscales | drot
-        f[12] = c.take<float>(Pz);         // depth
-        f[13] = c.take<float>(Pz);         // raw opacity grad
-        f[14] = c.take<float>(3 * Pz);     // raw scaling grad
-        f[15] = c.take<float>(4 * Pz);     // raw quaternion grad
         return c.off;
     };
     float* f[16];
@@ -1003,7 +1015,7 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     // launches).  (Running the update of those rows on a side stream, overlapping the backward, was measured and
     // dropped: DESIGN.md §8.)
     const bool unfused = getenv("DG_TRAIN_UNFUSED") != nullptr;
-    float* const p_sc_fused = part + 2 * nw_ssim;
+    float* const p_sc_fused = part + 3 * nw_ssim;
     // ---- forward: activations, rasterizer, clamp + L1, SSIM.  Default route: the activations (and the regulariser's
     // partial sums) inside the rasterizer's preprocess launch (ActFold); unfused: their own launch.
     if (unfused) gs::launch_activate_fwd((uint32_t)P, G[3].param, G[4].param, G[5].param, act_o, act_s, act_q, s);
@@ -1012,17 +1024,26 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     if (a->sh_status && !ov) return fail("train step: no side stream for the overlapped update%s%d");
     hipEvent_t prev = ov && ov->pending ? ov->done : nullptr;
     if (prev && unfused) { HIP_OK(hipStreamWaitEvent(s, prev, 0)); prev = nullptr; }
-    if (ov) ov->pending = false;
+    // `pending` stays set until the stream's wait on the previous update is enqueued: on an early error return below
+    // the wait is still enqueued (wait_prev), so dg_train_sync / a later step never lose it
+    if (ov && !prev) ov->pending = false;
     ActFold fold = {G[3].param, G[4].param, G[5].param, a->loss ? p_sc_fused : nullptr, prev, false};
+    auto wait_prev = [&]() {
+        if (prev && !fold.waited) (void)hipStreamWaitEvent(s, prev, 0);
+        if (ov) ov->pending = false;
+    };
     dg_raster_args r = a->view;
     r.means3D = G[0].param; r.dc = G[1].param; r.sh = M > 0 ? G[2].param : nullptr;
     r.opacities = act_o; r.scales = act_s; r.rotations = act_q; r.colors = nullptr; r.cov3D_precomp = nullptr;
     void *geom = nullptr, *binning = nullptr, *image = nullptr, *binning2 = nullptr;
     int64_t num_rendered = 0, num_instances = 0;
     if (forward_impl(&r, color, invd, a->radii, alloc, user, &geom, &binning, &image, &binning2, &num_rendered,
-                     &num_instances, stream, nullptr, unfused ? nullptr : &fold))
+                     &num_instances, stream, nullptr, unfused ? nullptr : &fold)) {
+        wait_prev();
         return 1;
+    }
     if (prev && !fold.waited) HIP_OK(hipStreamWaitEvent(s, prev, 0));  // nothing was binned: before the backward
+    if (ov) ov->pending = false;
     // ---- SparseGaussianAdam.step(radii > 0) over the six groups, ADMM proximal gradient, densification statistics.
     dg_adam_group groups[6];
     const float* grads[6] = {dmeans3D, ddc, dsh, unfused ? g_o : dopac, unfused ? g_s : dscales,
@@ -1062,6 +1083,7 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
         dg_densify_stats st = *a->stats;
         st.radii = a->radii; st.dmeans2D = dmeans2D; st.dmeans2D_stride = 3;
         if (fill_stats(m, &st)) return 1;
+        if (a->depth_threshold > 0.0f) { m.depth = depth; m.depth_thr = a->depth_threshold; }
     }
     if (!unfused) m.hot = carve_geom(geom, P).rcnt;
     const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;   // fused_ssim's constants
@@ -1069,11 +1091,13 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     const float g_l1 = (float)(1.0 - (double)ld);
     // loss backward of (1 - ld) L1 + ld (1 - SSIM) + ls mean(prod(scaling)): d/dmap = -ld / n (the mean's backward)
     if (!unfused) {  // render()'s clamp, L1 and the SSIM mean inside the SSIM passes (same values per pixel)
-        gs::launch_ssim_fwd_fused(H, W, C1, C2, color, a->gt, a->image, dmu1, ds1, ds12, part, s);
+        gs::launch_ssim_fwd_fused(H, W, C1, C2, color, a->gt, a->image, dmu1, ds1, ds12, part, s, a->mask);
         const gs::LossFinal lf = {part, part + nw_ssim, p_sc_fused, nw_ssim, nw_ssim, nb_act, (uint32_t)n_img,
-                                  (uint32_t)P, a->loss};
+                                  (uint32_t)P, a->loss, a->mask ? part + 2 * nw_ssim : nullptr, nw_ssim};
+        // d/dmask of lambda_mask mean((mask - 1)^2): lambda_mask (2 / n) (mask - 1)
+        const float mreg = (float)((double)a->lambda_mask * 2.0 / (double)n_img);
         gs::launch_ssim_bwd_fused(H, W, a->image, a->gt, color, (-ld) / (float)n_img, g_l1 / (float)n_img, dmu1, ds1,
-                                  ds12, dimg, s, a->loss ? &lf : nullptr);
+                                  ds12, dimg, s, a->loss ? &lf : nullptr, a->mask, a->dmask, mreg);
     } else {
         gs::launch_clamp_l1_fwd((uint32_t)n_img, color, a->gt, a->image, part, s);
         gs::launch_ssim_fwd(1, 3, H, W, C1, C2, a->image, a->gt, map, dmu1, ds1, ds12, s);

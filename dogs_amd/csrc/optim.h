@@ -46,6 +46,10 @@ struct AdamMultiArgs {
     float* max_radii2D;        // [N]
     float* grad_accum;         // [N]
     float* denom;              // [N]
+    // optional (depth_thr > 0): geometry.depth_threshold -- the screen-space gradient the statistics read is scaled by
+    // min(1, (depth[i] / depth_thr)^2) first (_RasterizeGaussians.backward's scale_tensor, gaussian_trainer.py:376)
+    const float* depth;        // [N] view-space depth (the rasterizer backward's depth output)
+    float depth_thr;
     // optional: hot[i] != 0 marks the rows that may carry a rasterizer gradient (the binned Gaussians, rcnt > 0);
     // a 4-float chunk touching no hot row takes its incoming gradient as zero without reading it (the native step,
     // where the activation fold supplies the regulariser's gradient of every row)

@@ -46,6 +46,8 @@ class GaussianSplatModel:
         self._xyz = self._features_dc = self._features_rest = e
         self._scaling = self._quaternion = self._opacity = e
         self.max_radii2D = self.xyz_gradient_accum = self.denom = e
+        self._exposure = e
+        self.image_id_to_index: dict = {}
 
     # ---- getters (gaussian_splat_model.py:156-259)
     @property
@@ -89,6 +91,21 @@ class GaussianSplatModel:
         return torch.sigmoid(self._opacity)
 
     @property
+    def get_exposure(self):
+        return self._exposure
+
+    def get_exposure_from_id(self, image_id: int):
+        """:272-273: the [3,4] affine colour transform of a training image."""
+        return self._exposure[self.image_id_to_index[image_id]]
+
+    def init_exposure(self, image_idxs) -> None:
+        """init_from_colmap_pcd's trained-exposure part (:578-582): one identity [3,4] per training image index."""
+        idxs = [int(i) for i in image_idxs]
+        self.image_id_to_index = {idx: ind for ind, idx in enumerate(idxs)}
+        exposure = torch.eye(3, 4, device=self.device)[None].repeat(len(idxs), 1, 1)
+        self._exposure = nn.Parameter(exposure.requires_grad_(True))
+
+    @property
     def num_gaussians(self) -> int:
         return int(self._xyz.shape[0])
 
@@ -108,9 +125,10 @@ class GaussianSplatModel:
         self.xyz_gradient_accum = torch.zeros((n, 1), device=self.device)
         self.denom = torch.zeros((n, 1), device=self.device)
 
-    def init_from_colmap_pcd(self, points, colors) -> None:
+    def init_from_colmap_pcd(self, points, colors, image_idxs=None) -> None:
         """:543-587: SH dc from the point colours, rest zero, scales from simple-knn's mean squared 3-NN distance
-        (distCUDA2 on the device), identity rotations, opacity 0.1."""
+        (distCUDA2 on the device), identity rotations, opacity 0.1; with image_idxs (appearance.use_trained_exposure)
+        an identity exposure per training image."""
         from .simple_knn._C import distCUDA2
         pts = torch.as_tensor(np.asarray(points)).float().to(self.device)
         col = RGB2SH(torch.as_tensor(np.asarray(colors)).float().to(self.device))
@@ -129,6 +147,8 @@ class GaussianSplatModel:
         self._quaternion = nn.Parameter(quats.requires_grad_(True))
         self._opacity = nn.Parameter(opac.contiguous().requires_grad_(True))
         self._reset_stats()
+        if image_idxs is not None:
+            self.init_exposure(image_idxs)
 
     def init_from_external_properties(self, xyz, features_dc, features_rest, scaling, quaternion, opacity,
                                       optimizable: bool = False) -> None:

@@ -29,9 +29,15 @@ class NativeTrainStep:
 
     def __init__(self, params: dict, opt, cameras: list, images: list, sh_degree: int, lambda_dssim: float,
                  lambda_scale: float, bg: torch.Tensor, device: torch.device, stats: dict | None = None,
-                 overlap: bool = False):
+                 overlap: bool = False, lambda_mask: float = 0.0, depth_threshold: float = 0.0,
+                 antialiasing: bool = False):
+        """lambda_mask: loss.lambda_mask (used by steps given a mask); depth_threshold: geometry.depth_threshold (scales
+        the screen-space gradient the densification statistics read); antialiasing: texture.anti_aliasing."""
         self.L = _lib.load()
         self.device = device
+        self.lambda_mask = float(lambda_mask)
+        self.depth_threshold = float(depth_threshold or 0.0)
+        self.antialiasing = bool(antialiasing)
         # overlap: each step returns with its f_dc / f_rest update still running on a side stream; the next step waits
         # for it before its binning emission (the first launch reading them) -- call sync() before anything else
         # touches those tensors or their Adam moments (rebind() does)
@@ -39,7 +45,8 @@ class NativeTrainStep:
         self.arena = _lib.ReuseArena(device, keep_retired=self.overlap)
         self.lambdas = (float(lambda_dssim), float(lambda_scale))
         self.sh_degree = int(sh_degree)
-        self.loss_buf = torch.zeros(3, dtype=torch.float32, device=device)
+        self.loss_buf = torch.zeros(4, dtype=torch.float32, device=device)
+        self.last_masked = False
         self.bg = bg.to(device=device, dtype=torch.float32).contiguous()
         self.cameras, self.gt_images = cameras, images
         for cam, gt in zip(cameras, images):
@@ -97,12 +104,13 @@ class NativeTrainStep:
             a = _lib.DgTrainStepArgs()
             v = a.view
             v.P, v.D, v.M, v.W, v.H = P, self.sh_degree, M, int(cam.width), int(cam.height)
-            v.prefiltered, v.antialiasing, v.debug = 0, 0, 0
+            v.prefiltered, v.antialiasing, v.debug = 0, int(self.antialiasing), 0
             v.scale_modifier, v.tanfovx, v.tanfovy = 1.0, float(cam.tanfovx), float(cam.tanfovy)
             v.bg, v.viewmatrix = self.bg.data_ptr(), cam.world_to_camera.data_ptr()
             v.projmatrix, v.campos = cam.projective_matrix.data_ptr(), cam.camera_center.data_ptr()
             a.gt = gt.data_ptr()
             a.lambda_dssim, a.lambda_scale = self.lambdas
+            a.lambda_mask, a.depth_threshold = self.lambda_mask, self.depth_threshold
             for i, n in enumerate(C_ORDER):
                 p = params[n]
                 st = opt.state[p]
@@ -131,9 +139,11 @@ class NativeTrainStep:
         return tuple(out)
 
     def step(self, k: int, xyz_lr: float | None = None, prox: dict | None = None, sh_degree: int | None = None,
-             lrs: dict | None = None) -> None:
+             lrs: dict | None = None, mask: torch.Tensor | None = None, dmask: torch.Tensor | None = None) -> None:
         """One iteration on view k; prox: {group name: (u, z, coef)} (ADMMBlockState.prox) or None; sh_degree: the
-        model's active SH degree (increase_SH_degree), default the constructor's; lrs: {group name: lr} overrides.
+        model's active SH degree (increase_SH_degree), default the constructor's; lrs: {group name: lr} overrides;
+        mask / dmask: the appearance mask [3,H,W] of this view and the buffer that receives dL/dmask (both contiguous
+        float32 on the device), or None.
         Raises when the optimizer's tensors are no longer the ones the argument blocks point at (call rebind())."""
         from .diff_gaussian_rasterization import _C
         if self._pointers() != self._bound:
@@ -155,6 +165,16 @@ class NativeTrainStep:
                 continue
             u, z, coef = prox[GROUP_NAME[n]]
             a.prox[i].u, a.prox[i].z, a.prox[i].coef = u.data_ptr(), z.data_ptr(), float(coef)
+        if mask is not None:
+            c = self.cameras[k]
+            for t in (mask, dmask):
+                if t is None or not (t.is_contiguous() and t.dtype == torch.float32 and t.device == self.device
+                                     and tuple(t.shape) == (3, int(c.height), int(c.width))):
+                    raise RuntimeError("native step: mask and dmask must be contiguous float32 [3,H,W] on the device")
+            a.mask, a.dmask = mask.data_ptr(), dmask.data_ptr()
+        else:
+            a.mask = a.dmask = None
+        self.last_masked = mask is not None
         _lib.check(self.L.dg_train_step(C.byref(a), self.arena.fn, None, self.stream))
         self.last_view = k
 
@@ -170,7 +190,11 @@ class NativeTrainStep:
         return self.images_out[(int(c.height), int(c.width))]
 
     def loss(self) -> torch.Tensor:
-        """(1 - ld) L1 + ld (1 - SSIM) + ls mean(prod(scaling)) of the last step, a device scalar."""
+        """(1 - ld) L1 + ld (1 - SSIM) [+ lm mean((mask - 1)^2)] + ls mean(prod(scaling)) of the last step (L1 of the
+        masked render when the step had a mask: gaussian_trainer.py:392-408), a device scalar."""
         ld, ls = self.lambdas
         L1, ssim, sc = self.loss_buf[0], self.loss_buf[1], self.loss_buf[2]
-        return (1.0 - ld) * L1 + ld * (1.0 - ssim) + ls * sc
+        loss = (1.0 - ld) * L1 + ld * (1.0 - ssim)
+        if self.last_masked:
+            loss = loss + self.lambda_mask * self.loss_buf[3]
+        return loss + ls * sc

@@ -188,12 +188,24 @@ typedef struct {
     const dg_densify_stats* stats;  /* optional; only max_radii2D / grad_accum / denom are read */
     int* radii;                 /* [P] out */
     float* image;               /* [3,H,W] out: the clamped render */
-    float* loss;                /* optional, device [3] out: L1, SSIM, mean prod(scaling) of this view */
+    float* loss;                /* optional, device [4] out: L1, SSIM, mean prod(scaling), mean((mask - 1)^2) (0
+                                   without a mask) of this view */
     /* optional [P] device scratch: overlap the f_dc / f_rest part of the update (81% of its bytes) with the NEXT
      * step's forward up to its binning emission, the first kernel that reads them.  The call returns with that part
      * still running on a side stream; the next dg_train_step on the same stream waits for it before its emission, and
      * any other use of the SH tensors or their moments needs dg_train_sync first. */
     uint8_t* sh_status;
+    /* optional: the decoupled appearance mask of geometry.mask (gaussian_trainer.py:392-401, AppearanceEmbedding of
+     * masks.py:8-54, evaluated by the caller): mask [3,H,W] (NULL: none).  The photometric term becomes
+     * (1 - lambda_dssim) L1(clamp(render) * mask, gt) + lambda_dssim (1 - SSIM(clamp(render), gt))
+     * + lambda_mask mean((mask - 1)^2), and dmask [3,H,W] receives dL/dmask for the caller's backward through the
+     * embedding network.  Both 16-byte aligned when given. */
+    const float* mask;
+    float* dmask;
+    float lambda_mask;
+    /* geometry.depth_threshold (gaussian_trainer.py:376 -> _RasterizeGaussians.backward): > 0 scales the screen-space
+     * gradient the densification statistics read by min(1, (depth / depth_threshold)^2); 0: unscaled. */
+    float depth_threshold;
 } dg_train_step_args;
 int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg_stream_t stream);
 /* Make `stream` wait for an overlapped f_dc / f_rest update of the last dg_train_step on it (no-op when none). */

@@ -1,4 +1,5 @@
-"""ADMM block consensus over torch.distributed (gloo, world_size 2, CPU) vs a single-process restatement of the
+"""ADMM block consensus over torch.distributed (gloo, world_size 2 and 4, CPU; at 4 some Gaussians sit in 3 or 4
+blocks) vs a single-process restatement of the
 reference master's gather/average/scatter (master_gaussian_trainer.py:459-555, gaussian_splat_model.py:316-340),
 dual update (slave_gaussian_trainer.py:100-121), residuals (master :396-456) and penalty adaptation (:337-377)."""
 import os
@@ -50,6 +51,18 @@ def _worker(rank, world, port):
         idx, params = blocks[rank]
         bc = BlockConsensus(idx, N_GLOBAL, device=torch.device("cpu"))
         assert torch.equal(bc.visibility_count.float(), cnt)
+        if world >= 4:
+            assert int((cnt >= 3).sum()) > 0 and int((cnt == 4).sum()) > 0
+        # owner = the lowest rank holding the Gaussian: every global row is owned exactly once over the ranks
+        owned = torch.zeros(N_GLOBAL, dtype=torch.int64)
+        owned[idx[bc.owned]] = 1
+        dist.all_reduce(owned)
+        assert bool((owned == 1).all())
+        lowest = torch.full((N_GLOBAL,), world, dtype=torch.int64)
+        for k in range(world):
+            i, _ = _block(k, world)
+            lowest[i] = torch.minimum(lowest[i], torch.full_like(i, k))
+        assert torch.equal(bc.owned, lowest[idx] == rank)
         z = bc.consensus(params)
         for zi, zr in zip(z, zref):
             torch.testing.assert_close(zi, zr[idx], rtol=1e-6, atol=1e-6)
@@ -83,7 +96,7 @@ def _worker(rank, world, port):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_consensus_gloo_matches_single_process(world):
     mp.spawn(_worker, args=(world, _free_port()), nprocs=world, join=True)
 

@@ -1,15 +1,17 @@
 """The ADMM phase entry (dogs_amd.admm_phase: fuse_local_gaussians without the RPC master,
-master_gaussian_trainer.py:37-172, 557-618) over torch.distributed (gloo, world size 2, CPU).
+master_gaussian_trainer.py:37-172, 557-618) over torch.distributed (gloo, world size 2 and 4, CPU).
 
 The device operations (count renders, box membership, prune compaction) are replaced by CPU restatements
 (`CPUKernels`), so this checks the distributed plumbing and the lifecycle order:
   * every rank's entry equals the single-process entry (enter_admm_phase_sequential) bit for bit -- the gathered and
-    fused model, the importance sums (per-block partials added in block order), the pruned set, the expanded-box
-    split, visibility_count and the penalty denominator;
+    fused model, the importance (folded down the rank chain in the reference's camera order), the pruned set, the
+    expanded-box split, visibility_count and the penalty denominator;
   * the single-process entry equals a plain restatement of the reference's own steps written here from its source
-    (clip to the original boxes, concatenate, prune_list, calculate_v_imp_score, prune_gaussians(0.4 p),
-    select_gaussians_in_each_block), with the importance summed with the same per-block association.
-The HIP versions of the three operations are checked on the GPU (tests/test_gpu_admm_phase.py)."""
+    (clip to the original boxes, concatenate, prune_list over the concatenated camera list popped from the end,
+    calculate_v_imp_score, prune_gaussians(0.4 p), select_gaussians_in_each_block).
+World 4 is a 2 x 2 grid whose expanded boxes overlap at the centre, so Gaussians there sit in 3 or 4 blocks (count
+3-4, owner = the lowest of up to four ranks).
+The HIP versions of the three operations are checked on the GPU (tests/test_gpu_admm_dist.py)."""
 import os
 import socket
 
@@ -20,28 +22,41 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-N_BLOCK = (300, 260)
 T = np.array([[0.8, -0.6, 0.3], [0.6, 0.8, -0.2], [0.0, 0.0, 1.0]])   # world -> OBB (a rotation + shift)
-ORI = [np.array([-5.0, -5.0, -1.0, 0.0, 5.0, 1.0]), np.array([0.0, -5.0, -1.0, 5.0, 5.0, 1.0])]
-EXP = [np.array([-6.0, -6.0, -1.0, 1.0, 6.0, 1.0]), np.array([-1.0, -6.0, -1.0, 6.0, 6.0, 1.0])]
+# world 2: two halves; world 4: a 2 x 2 grid (boxes in the OBB frame [x0, y0, z0, x1, y1, z1], expanded by 1)
+GRIDS = {
+    2: [(-5.0, -5.0, 0.0, 5.0), (0.0, -5.0, 5.0, 5.0)],
+    4: [(-5.0, -5.0, 0.0, 0.0), (0.0, -5.0, 5.0, 0.0), (-5.0, 0.0, 0.0, 5.0), (0.0, 0.0, 5.0, 5.0)],
+}
 
 
-def _cameras():
+def _boxes(world):
+    ori = [np.array([x0, y0, -1.0, x1, y1, 1.0]) for x0, y0, x1, y1 in GRIDS[world]]
+    exp = [np.array([x0 - 1.0, y0 - 1.0, -1.0, x1 + 1.0, y1 + 1.0, 1.0]) for x0, y0, x1, y1 in GRIDS[world]]
+    return ori, exp
+
+
+def _cameras(world):
     g = torch.Generator().manual_seed(3)
-    return [[torch.randn(3, generator=g) * 3.0 for _ in range(4)], [torch.randn(3, generator=g) * 3.0 for _ in range(3)]]
+    return [[torch.randn(3, generator=g) * 3.0 for _ in range(3 + (b % 2))] for b in range(world)]
 
 
-def _block_model(b):
+def _block_model(b, world):
+    """Block b's model: points around its grid cell (in the OBB frame), so blocks overlap near the cell borders."""
     from dogs_amd.gaussian_model import GaussianSplatModel
     g = torch.Generator().manual_seed(11 + b)
-    n = N_BLOCK[b]
+    n = 300 - 20 * b
     m = GaussianSplatModel(3, 0.01, "cpu")
-    xyz = torch.randn(n, 3, generator=g) * 3.0
-    xyz[:, 0] += -2.0 if b == 0 else 2.0
+    x0, y0, x1, y1 = GRIDS[world][b]
+    obb = torch.stack([x0 + (x1 - x0) * (torch.rand(n, generator=g) * 1.4 - 0.2),
+                       y0 + (y1 - y0) * (torch.rand(n, generator=g) * 1.4 - 0.2)], 1).double()
+    Ti = torch.from_numpy(np.linalg.inv(T))
+    xy = (obb @ Ti[:2, :2].T + Ti[:2, 2]).float()
+    xyz = torch.cat([xy, torch.randn(n, 1, generator=g) * 0.3], 1)
     m.init_from_external_properties(xyz, torch.randn(n, 1, 3, generator=g), torch.randn(n, 15, 3, generator=g) * 0.1,
                                     torch.randn(n, 3, generator=g) - 3.0, torch.randn(n, 4, generator=g),
                                     torch.randn(n, 1, generator=g), optimizable=True)
-    m.active_sh_degree = 3
+    m.active_sh_degree = 2
     return m
 
 
@@ -50,15 +65,12 @@ def _cpu_kernels():
     from oracle.blocksplit_oracle import points_in_bbox2D
 
     class CPUKernels(PhaseKernels):
-        def importance(self, model, cameras, bg):
+        def camera_importance(self, model, camera, bg):
             xyz = model.get_xyz.detach()
             op = torch.sigmoid(model.get_raw_opacity.detach()).reshape(-1)
-            imp = torch.zeros(xyz.shape[0])
-            for c in reversed(list(cameras)):        # prune_list pops from the end
-                d = ((xyz - c) ** 2).sum(1)
-                cnt = (d < 40.0).to(torch.int32) * (1 + (d.to(torch.int32) % 7))   # integer pixel counts
-                imp += cnt.float() * op
-            return imp
+            d = ((xyz - camera) ** 2).sum(1)
+            cnt = (d < 40.0).to(torch.int32) * (1 + (d.to(torch.int32) % 7))   # integer pixel counts
+            return cnt.float() * op
 
         def members(self, xy, boxes, transform):
             return [torch.from_numpy(points_in_bbox2D(xy.numpy(), np.asarray(b).reshape(2, 3), transform))
@@ -69,11 +81,12 @@ def _cpu_kernels():
     return CPUKernels()
 
 
-def _restated(cfg):
+def _restated(cfg, world):
     """The reference's steps, from its source text, on the same blocks and kernels."""
     from oracle.blocksplit_oracle import points_in_bbox2D
     K = _cpu_kernels()
-    models = [_block_model(b) for b in range(2)]
+    ORI, EXP = _boxes(world)
+    models = [_block_model(b, world) for b in range(world)]
     rows = []
     for b, m in enumerate(models):              # fuse_block_gaussians :55-83
         keep = torch.from_numpy(points_in_bbox2D(m.get_xyz.detach().numpy()[:, :2], ORI[b].reshape(2, 3), T))
@@ -84,8 +97,10 @@ def _restated(cfg):
     F = GaussianSplatModel(3, 0.01, "cpu")
     F.init_from_external_properties(*fused)
     F.active_sh_degree = 3
-    cams = _cameras()
-    imp = K.importance(F, cams[0], None) + K.importance(F, cams[1], None)   # per-block association
+    cameras = [c for cams in _cameras(world) for c in cams]   # prune_gaussians_after_merge: one list
+    imp = K.camera_importance(F, cameras.pop(), None)          # prune_list: pop, then += pop ...
+    while cameras:
+        imp += K.camera_importance(F, cameras.pop(), None)
     volume = torch.prod(torch.exp(F._scaling), dim=1)                       # calculate_v_imp_score
     sv, _ = torch.sort(volume, descending=True)
     v = torch.pow(volume / sv[int(len(volume) * 0.9)], cfg.v_pow) * imp
@@ -102,10 +117,11 @@ def _restated(cfg):
     return kept, gi, vis, n_rho
 
 
-def _sequential(cfg):
+def _sequential(cfg, world):
     from dogs_amd.admm_phase import enter_admm_phase_sequential
-    return enter_admm_phase_sequential([_block_model(b) for b in range(2)], _cameras(), ORI, EXP, T, cfg,
-                                       _cpu_kernels())
+    ORI, EXP = _boxes(world)
+    return enter_admm_phase_sequential([_block_model(b, world) for b in range(world)], _cameras(world), ORI, EXP, T,
+                                       cfg, _cpu_kernels())
 
 
 def _free_port():
@@ -120,8 +136,9 @@ def _worker(rank, world, port):
     try:
         from dogs_amd.admm_phase import PhaseConfig, enter_admm_phase
         cfg = PhaseConfig(prune_percent=0.5, v_pow=0.1)
-        e = enter_admm_phase(_block_model(rank), _cameras(), ORI, EXP, T, cfg, _cpu_kernels())
-        ref = _sequential(cfg)[rank]
+        ORI, EXP = _boxes(world)
+        e = enter_admm_phase(_block_model(rank, world), _cameras(world), ORI, EXP, T, cfg, _cpu_kernels())
+        ref = _sequential(cfg, world)[rank]
         assert torch.equal(e.global_indices, ref.global_indices)
         assert torch.equal(e.visibility_count, ref.visibility_count)
         assert (e.num_global, e.rho_gaussians) == (ref.num_global, ref.rho_gaussians)
@@ -129,24 +146,29 @@ def _worker(rank, world, port):
             assert torch.equal(a.detach(), b.detach())
         for a, b in zip(e.fused.get_all_properties(), ref.fused.get_all_properties()):
             assert torch.equal(a, b)
+        assert e.model.active_sh_degree == 3   # the master's degree (max), not the blocks'
     finally:
         dist.destroy_process_group()
 
 
-def test_phase_entry_gloo_matches_single_process():
-    mp.spawn(_worker, args=(2, _free_port()), nprocs=2, join=True)
+@pytest.mark.parametrize("world", [2, 4])
+def test_phase_entry_gloo_matches_single_process(world):
+    mp.spawn(_worker, args=(world, _free_port()), nprocs=world, join=True)
 
 
-def test_single_process_entry_matches_reference_steps():
+@pytest.mark.parametrize("world", [2, 4])
+def test_single_process_entry_matches_reference_steps(world):
     from dogs_amd.admm_phase import PhaseConfig
     cfg = PhaseConfig(prune_percent=0.5, v_pow=0.1)
-    entries = _sequential(cfg)
-    kept, gi, vis, n_rho = _restated(cfg)
+    entries = _sequential(cfg, world)
+    kept, gi, vis, n_rho = _restated(cfg, world)
     assert entries[0].rho_gaussians == n_rho
     assert torch.equal(entries[0].visibility_count, vis)
-    assert 0 < n_rho < sum(N_BLOCK)
+    assert 0 < n_rho < sum(300 - 20 * b for b in range(world))
     assert int((vis >= 2).sum()) > 0, "the expanded boxes must overlap"
-    for b in range(2):
+    if world == 4:
+        assert int((vis >= 3).sum()) > 0 and int((vis == 4).sum()) > 0, "the grid centre must be shared by 3-4 blocks"
+    for b in range(world):
         assert torch.equal(entries[b].global_indices, gi[b])
         for a, k in zip(entries[b].model.get_all_properties(), kept):
             assert torch.equal(a.detach(), k[gi[b]])
