@@ -55,10 +55,10 @@ def phase_bytes(phase: str, v: dict) -> float:
     writes rgb/inv-depth (16 B) per binned Gaussian, and writes Gaussian, depth key and tile slot (12 B) per instance;
     the render gathers 44 B per instance (id, xy, conic/opacity, rgb, depth) and its fused sort reads key + id and
     writes the sorted id (12 B), and writes colour, inverse depth, T and last contributor (24 B/px); the replay
-    re-gathers 44 B and writes one 40-B record per instance and reads 40 B/px; the per-Gaussian backward reads the
-    records (40 B/instance), 236 B of parameters + radius + 40-B sums per gradient-carrying Gaussian, and writes every
-    output element once (288 B per Gaussian: the dense gradient tensors, zeros included -- the zero fill itself is
-    issued by the replay's waves, in the shadow of its VALU work)."""
+    re-gathers 44 B and writes one 40-B record per instance and reads 40 B/px, and its waves issue the zero fill of the
+    dense gradient outputs (288 B per Gaussian, in the shadow of its VALU work: credited to the kernel that issues
+    it); the per-Gaussian backward reads the records (40 B/instance) and 236 B of parameters + radius + 40-B sums per
+    gradient-carrying Gaussian, and overwrites those Gaussians' output rows (counted in the fill)."""
     N, HW = v["N"], v["HW"]
     E1, E2 = v["e1"], v["e2"]
     E = E1 + E2
@@ -70,8 +70,8 @@ def phase_bytes(phase: str, v: dict) -> float:
         "tile_bin": 0.0,
         "render_fwd": 56.0 * E1 + 24.0 * HW,
         "phase2": 68.0 * E2,
-        "render_bwd": 84.0 * E + 40.0 * HW,
-        "gauss_bwd": 40.0 * E + 280.0 * Gl + 288.0 * N,
+        "render_bwd": 84.0 * E + 40.0 * HW + 288.0 * N,
+        "gauss_bwd": 40.0 * E + 280.0 * Gl,
     }.get(phase, 0.0)
 
 
@@ -328,65 +328,94 @@ def cpu_baseline(n, W, H, seed, yaws, budget_s=12.0):
                             "sample": f"{nv_one} views, 1 thread", "seconds": round(dt_one, 3)}}
 
 
+def _grid(blocks: int) -> tuple:
+    """mx x my of the Grid2D split for a block count (one block per rank)."""
+    mx = 1
+    while mx * mx < blocks:
+        mx *= 2
+    return mx, max(1, blocks // mx)
+
+
 def admm_leg(args, ws, rank, dev, n, W, H):
-    """The ADMM block trainer (dogs_amd.admm_trainer): every rank trains its block of a chain split (1e6 Gaussians,
-    20% shared with the next block, --views yaw cameras, random targets) for --admm-rounds rounds of --admm-interval
-    local iterations (activations, raster fwd/bwd, L1 + SSIM + scale regulariser, SparseGaussianAdam with the ADMM
-    penalty) each followed by the consensus round (RCCL all_reduce of the shared Gaussians, duals, residuals,
-    penalty adaptation).  Then rank 0 trains the same split sequentially on its one GPU (the single-GPU baseline of
-    the '>= 6x at 8 GPUs' target) for the same rounds; speedup = sequential / parallel wall time."""
+    """The ADMM trainer end to end (dogs_amd.admm_run, master_gaussian_trainer.py:620-728): a synthetic aerial scene of
+    ~n points per block split by the Grid2D path into one block per rank (2 x 1, 2 x 2, 4 x 2), nadir cameras at W x H
+    with seeded smooth targets; every rank runs `run()`: --admm-pre pre-phase iterations with densification (the
+    GaussianSplatTrainer loop: native steps, densify / reset on the autograd route), the phase entry (all-gather + fuse,
+    count renders of its own cameras, the order-exact importance fold, prune, expanded-box split), then --admm-rounds
+    rounds of --admm-interval local steps (activations, raster fwd/bwd, L1 + SSIM + scale regulariser, SparseGaussianAdam
+    with the ADMM penalty) + consensus (RCCL all_reduce of the shared Gaussians, duals, residuals, rho adaptation).
+    Rank 0 then runs the same split block after block on its one GPU (`run_sequential`, the single-GPU baseline of the
+    '>= 6x at 8 GPUs' target): speedup = sequential / parallel wall time, for the whole run and for the ADMM rounds.
+    At one rank the split has 2 blocks and only the sequential run is timed."""
     import gc
+    import tempfile
     from dogs_amd.admm import ADMMConfig
-    from dogs_amd.admm_trainer import barrier_time, distributed_trainer, sequential_trainer
-    cfg = ADMMConfig(consensus_interval=args.admm_interval)
-    tr, cons, run = distributed_trainer(rank, ws, n, W, H, args.views, args.shared_frac, dev, admm=cfg, overlap=True)
-    for _ in range(min(args.views, 8)):   # warm-up: allocator, adaptive capacity
-        tr.local_step()
-    tr.sync()   # the overlapped update before the parameters are read
-    ps = tuple(p.detach() for p in tr.param_tuple())
-    run.cons.residuals(ps, run.cons.consensus(ps), ps, tr.admm.rho)   # communicator / buffer setup
-    del ps
+    from dogs_amd.admm_run import ADMMRunConfig, aerial_views, run, run_sequential, split_scene
+    from dogs_amd.trainer import GSTrainConfig
+    nb = ws if ws > 1 else 2
+    mx, my = _grid(nb)
+    pre = max(0, args.admm_pre)
     rounds = max(1, args.admm_rounds)
-    t_par = barrier_time(lambda: [run.round() for _ in range(rounds)], dev, ws)
-    steps = rounds * cfg.consensus_interval
-    out = {"views_per_s": round(ws * steps / t_par, 2), "ms_per_round": round(t_par / rounds * 1e3, 2),
-           "rounds": rounds, "interval": cfg.consensus_interval, "blocks": ws, "gaussians_per_block": n,
-           "shared_gaussians": cons.num_shared,
-           "consensus_ms": round(1e3 * max(lg.seconds["consensus"] for lg in run.logs), 3),
-           "last_round": {"primal": {k: float(f"{v:.4g}") for k, v in run.logs[-1].primal.items()},
-                          "dual": {k: float(f"{v:.4g}") for k, v in run.logs[-1].dual.items()},
-                          "loss": float(tr.last_loss), "penalty": float(tr.penalty())},
-           "includes": "per local step: activations + raster fwd/bwd + clamp/L1 + fused SSIM + scale regulariser + "
-                       "SparseGaussianAdam with the ADMM proximal gradient (one launch); per round: consensus "
-                       "all_reduce of the shared set, duals, residuals, rho adaptation"}
-    del tr, cons, run
-    gc.collect()
-    torch.cuda.empty_cache()
-    nseq = args.admm_seq if args.admm_seq >= 0 else (ws if ws > 1 else 0)
-    if nseq > 0:
+    gs = GSTrainConfig(max_iterations=pre + rounds * args.admm_interval, densify_start_iter=min(50, pre // 2),
+                       densify_end_iter=pre, densification_interval=max(pre // 2, 1), opacity_reset_interval=10 ** 6,
+                       prune_iterations=(), spatial_lr_scale=-1, percent_dense=0.001, lambda_scale=0.05,
+                       position_init=0.000016, position_final=0.00000016, position_max_iterations=30000, opacity=0.05)
+    cfg = ADMMRunConfig(gs=gs, admm=ADMMConfig(consensus_interval=args.admm_interval))
+    with tempfile.TemporaryDirectory() as tmp:
+        views = aerial_views(n * nb, 2 * mx, 2 * my, W, H, extent=4.0 * mx, height=4.0, seed=77)
+        scenes = split_scene(views, mx, my, tmp, dev, image_seed=78)
+    out = {"blocks": nb, "grid": [mx, my], "pre_phase_iterations": pre, "rounds": rounds,
+           "interval": args.admm_interval, "points_per_block": [int(sc.points.shape[0]) for sc in scenes],
+           "cameras_per_block": [len(c) for c in scenes[0].camera_blocks],
+           "includes": "pre-phase (densify) + phase entry (fuse, count renders, importance prune, re-split) + ADMM "
+                       "rounds (local steps: activations + raster fwd/bwd + clamp/L1 + fused SSIM + scale regulariser "
+                       "+ SparseGaussianAdam with the proximal gradient; consensus all_reduce of the shared set, "
+                       "duals, residuals, rho adaptation)"}
+    if ws > 1:
+        from dogs_amd.admm_trainer import barrier_time
+        res = {}
+        t_par = barrier_time(lambda: res.update(r=run(cfg, scenes[rank], device=dev, seed=5)), dev, ws)
+        r = res["r"]
+        secs = {k: max_over(ws, dev, v) for k, v in r.seconds.items()}
+        steps = rounds * args.admm_interval
+        out.update({"seconds": round(t_par, 3), "phase_seconds": {k: round(v, 3) for k, v in secs.items()},
+                    "views_per_s": round(ws * steps / secs["admm"], 2),
+                    "gaussians_per_block_admm": int(r.block.params["xyz"].shape[0]),
+                    "num_global": r.entry.num_global, "shared_gaussians": r.consensus.num_shared,
+                    "consensus_ms": round(1e3 * max(lg.seconds["consensus"] for lg in r.runner.logs), 3),
+                    "last_round": {"primal": {k: float(f"{v:.4g}") for k, v in r.runner.logs[-1].primal.items()},
+                                   "dual": {k: float(f"{v:.4g}") for k, v in r.runner.logs[-1].dual.items()}}})
+        del res, r
+        gc.collect()
+        torch.cuda.empty_cache()
+        dist.barrier()
+    if rank == 0:
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        seq = run_sequential(cfg, scenes, dev, seed=5)
+        torch.cuda.synchronize(dev)
+        t_seq = time.perf_counter() - t0
+        out["sequential"] = {"blocks": nb, "seconds": round(t_seq, 3),
+                             "phase_seconds": {k: round(v, 3) for k, v in seq.seconds.items()},
+                             "views_per_s": round(nb * rounds * args.admm_interval / seq.seconds["admm"], 2),
+                             "shared_gaussians": seq.seq.cons.num_shared, "num_global": seq.entries[0].num_global}
         if ws > 1:
-            dist.barrier()
-        if rank == 0:
-            blocks, seq = sequential_trainer(nseq, n, W, H, args.views, args.shared_frac, dev, admm=cfg, overlap=True)
-            for b in blocks:
-                for _ in range(min(args.views, 8)):
-                    b.local_step()
-            for b in blocks:
-                b.sync()
-            ps = [tuple(p.detach() for p in b.param_tuple()) for b in blocks]
-            seq.cons.residuals(ps, seq.cons.consensus(ps), ps, blocks[0].admm.rho)   # warm-up of the exchange
-            del ps
-            t_seq = barrier_time(lambda: [seq.round() for _ in range(rounds)], dev, 1)
-            out["sequential"] = {"blocks": nseq, "seconds": round(t_seq, 3),
-                                 "views_per_s": round(nseq * steps / t_seq, 2)}
-            if nseq == ws:
-                out["speedup_vs_sequential"] = round(t_seq / t_par, 3)
-            del blocks, seq
-            gc.collect()
-            torch.cuda.empty_cache()
-        if ws > 1:
-            dist.barrier()
+            out["speedup_vs_sequential"] = round(t_seq / out["seconds"], 3)
+            out["speedup_admm_rounds"] = round(seq.seconds["admm"] / out["phase_seconds"]["admm"], 3)
+        del seq
+        gc.collect()
+        torch.cuda.empty_cache()
+    if ws > 1:
+        dist.barrier()
     return out
+
+
+def max_over(ws: int, dev, x: float) -> float:
+    if ws == 1:
+        return x
+    t = torch.tensor([x], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def load_pmc(n: int, W: int, H: int):
@@ -416,8 +445,8 @@ def main():
     ap.add_argument("--no-admm", action="store_true", help="skip the ADMM block-trainer leg")
     ap.add_argument("--admm-rounds", type=int, default=1, help="timed ADMM rounds (each: interval local steps)")
     ap.add_argument("--admm-interval", type=int, default=200, help="local steps per round (urban3d_admm.yaml:44)")
-    ap.add_argument("--admm-seq", type=int, default=-1,
-                    help="blocks of the sequential single-GPU baseline on rank 0 (-1: the world size when > 1)")
+    ap.add_argument("--admm-pre", type=int, default=200,
+                    help="pre-phase iterations (densify_end_iter of the ADMM leg's run; interval chunks)")
     ap.add_argument("--launch-check", action="store_true",
                     help="plumbing check, no GPU: every rank joins a gloo group, all_reduces its rank and rank 0 "
                          "prints the world it saw (tests/test_bench_launch.py)")

@@ -273,11 +273,11 @@ def split_scene(views: dict, mx: int, my: int, save_dir: str, device, bbox_scale
     for b in range(nb):
         imgs = []
         for c in ds[b].cameras:
-            if c.image_index not in imgs_all:     # one target per image, shared by the blocks that hold it
+            if c.image_path not in imgs_all:      # one target per image, shared by the blocks that hold it
                 lo = torch.rand((1, 3, 8, 8), generator=g)
-                imgs_all[c.image_index] = torch.nn.functional.interpolate(
+                imgs_all[c.image_path] = torch.nn.functional.interpolate(
                     lo, size=(c.height, c.width), mode="bilinear", align_corners=False)[0].contiguous()
-            imgs.append(imgs_all[c.image_index].to(dev))
+            imgs.append(imgs_all[c.image_path].to(dev))
         sel = points_in_bbox2D(views["points"][:, :2], ebb[b].reshape(2, 3), T)
         scenes.append(BlockScene(cams, imgs, views["points"][sel], views["colors"][sel] / 255.0,
                                  [x.reshape(-1) for x in bb], [x.reshape(-1) for x in ebb], T, b))

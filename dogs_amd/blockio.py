@@ -147,10 +147,11 @@ def export_blocks(out_dir: str, views: dict, block_image_ids: dict, image_paths=
     out = []
     for b in range(len(block_image_ids)):
         cams = []
-        for c2w, K, p in zip(bv["poses"][b], bv["intrinsics"][b], bv["image_paths"][b]):
-            i = index_of[p]
-            w, h = (int(x) for x in views["sizes"][i])
-            cams.append(BlockCamera(i, w, h, torch.linalg.inv(c2w.double()).float(), float(K[0, 0]), float(K[1, 1]),
+        for j, (c2w, K, p) in enumerate(zip(bv["poses"][b], bv["intrinsics"][b], bv["image_paths"][b])):
+            w, h = (int(x) for x in views["sizes"][index_of[p]])
+            # image_index: the camera's position in its block (compose_cameras, dataset_base.py:64-92, composes each
+            # block's list with image_index = i; the appearance embedding and the exposure are indexed by it)
+            cams.append(BlockCamera(j, w, h, torch.linalg.inv(c2w.double()).float(), float(K[0, 0]), float(K[1, 1]),
                                     float(K[0, 2]), float(K[1, 2]), p))
         ds = MiniDataset(cams, bv["poses"][b], b)
         ds.write(os.path.join(out_dir, f"block_{b}"))

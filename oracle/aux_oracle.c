@@ -162,6 +162,8 @@ int aux_knn(int P, const float* pts, float* out, uint32_t* order) {
                 if (v > bmax[3 * b + k]) bmax[3 * b + k] = v;
             }
     }
+    /* every point's search is independent and writes its own slot: threads change nothing in the result */
+#pragma omp parallel for schedule(dynamic, 256)
     for (int idx = 0; idx < P; idx++) {
         const float* pt = pts + 3 * mc[idx].idx;
         float best[3] = {FLT_MAX, FLT_MAX, FLT_MAX};

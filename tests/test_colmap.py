@@ -148,5 +148,7 @@ def test_colmap_views_and_block_export(tmp_path, exp):
                                                                           c0.image_path)
             rc = c1.raster_camera()
             assert rc.width == c1.width and torch.isfinite(rc.projective_matrix).all()
-    assert [c.image_index for c in out[1].cameras] == [2, 4, 5]
+    # image_index is the position in the block (compose_cameras); the image paths name the global images 2, 4, 5
+    assert [c.image_index for c in out[1].cameras] == [0, 1, 2]
+    assert [c.image_path for c in out[1].cameras] == [v["image_names"][i] for i in (2, 4, 5)]
     np.testing.assert_allclose(out[0].cameras[1].world_to_camera.numpy(), w2c[1].astype(np.float32), atol=1e-5)

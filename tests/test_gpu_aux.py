@@ -4,7 +4,9 @@ C-ABI library): fused-SSIM forward/backward (ssim.cu:187-444), sparse Adam (adam
 GaussianRasterizer (dc/sh split, depth_threshold scaling) end to end.
 
 Bars: integer/index work and correctly-rounded fp32 elementwise code bit-exact; SSIM within 1e-5 (the separable
-convolution sums are ordered identically, only the compiler's scheduling of independent ops differs)."""
+convolution sums are ordered identically, only the compiler's scheduling of independent ops differs).  The largest
+cases are the BASELINE sizes: SSIM at 1 x 3 x 1080 x 1920, distCUDA2 at 1e6 points (tests/test_gpu_optim.py runs
+SparseGaussianAdam at 1e6 x 59)."""
 import numpy as np
 import pytest
 import torch
@@ -16,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 # several strips across (54 output columns per wave) with even and odd widths, ragged rows (32 per strip)
 @pytest.mark.parametrize("B,C,H,W", [(1, 3, 37, 53), (1, 3, 128, 96), (2, 1, 64, 64), (1, 3, 70, 250),
-                                     (1, 1, 33, 237), (1, 2, 5, 119)])
+                                     (1, 1, 33, 237), (1, 2, 5, 119), (1, 3, 1080, 1920)])
 def test_fused_ssim_matches_oracle(oracle, hip_device, B, C, H, W):
     from fused_ssim_cuda import fusedssim, fusedssim_backward
     g = torch.Generator().manual_seed(H * W)
@@ -66,7 +68,7 @@ def test_sparse_adam_bitexact(oracle, hip_device, N, M):
     np.testing.assert_array_equal(vh.cpu().numpy(), vo)
 
 
-@pytest.mark.parametrize("P", [1, 5, 1000, 20000])
+@pytest.mark.parametrize("P", [1, 5, 1000, 20000, 1_000_000])
 def test_dist_cuda2_bitexact(oracle, hip_device, P):
     from simple_knn._C import distCUDA2
     g = torch.Generator().manual_seed(P)

@@ -127,4 +127,5 @@ def test_colmap_to_block_folders(hip_device, tmp_path):
     out = export_blocks(str(tmp_path / "blocks"), v, bids)
     for b, d in enumerate(out):
         back = MiniDataset().read(str(tmp_path / "blocks" / f"block_{b}"), block_id=b)
-        assert sorted(c.image_index for c in back.cameras) == sorted(np.concatenate(bids[b]).tolist())
+        assert [c.image_path for c in back.cameras] == [v["image_names"][i] for i in sorted(np.concatenate(bids[b]))]
+        assert [c.image_index for c in back.cameras] == list(range(len(back.cameras)))

@@ -26,7 +26,7 @@ def _params(N, seed, dev):
     return {k: v.to(dev) for k, v in p.items()}, g
 
 
-@pytest.mark.parametrize("N", [1, 777, 20000])
+@pytest.mark.parametrize("N", [1, 777, 20000, 1_000_000])   # 1e6 x 59 floats: the bench / config-2 size
 def test_adam_groups_and_stats_bitexact(oracle, hip_device, N):
     from diff_gaussian_rasterization import SparseGaussianAdam
     from oracle import densify_oracle as D
