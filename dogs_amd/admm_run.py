@@ -225,19 +225,21 @@ def run_sequential(cfg: ADMMRunConfig, scenes: list, device, seed: int = 0, kern
 # A synthetic aerial scene split by the Grid2D path (tests, the bench's ADMM leg): points on a ground slab, nadir
 # cameras on a regular grid above it, the split through cluster_image_in_grid / cluster_points_in_grid.
 
-def aerial_views(n_points: int, cams_x: int, cams_y: int, W: int, H: int, extent: float = 4.0, height: float = 6.0,
+def aerial_views(n_points: int, cams_x: int, cams_y: int, W: int, H: int, extent=4.0, height: float = 6.0,
                  seed: int = 0) -> dict:
     """{'points' [n,3] f64, 'colors' [n,3] u8, 'camtoworlds' [C,4,4] f64, 'fx', 'W', 'H'} of a ground slab
-    [-extent, extent]^2 x [-0.3, 0.3] seen by cams_x x cams_y nadir cameras at `height`."""
+    [-ex, ex] x [-ey, ey] x [-0.3, 0.3] (extent = e or (ex, ey)) seen by cams_x x cams_y nadir cameras at `height`
+    (70 degrees of horizontal field of view)."""
+    ex, ey = (float(extent), float(extent)) if np.isscalar(extent) else (float(extent[0]), float(extent[1]))
     rng = np.random.default_rng(seed)
-    pts = np.stack([rng.uniform(-extent, extent, n_points), rng.uniform(-extent, extent, n_points),
+    pts = np.stack([rng.uniform(-ex, ex, n_points), rng.uniform(-ey, ey, n_points),
                     rng.uniform(-0.3, 0.3, n_points)], 1)
     cols = rng.integers(0, 256, (n_points, 3)).astype(np.uint8)
     c2w = []
     for j in range(cams_y):
         for i in range(cams_x):
-            cx = -extent + (i + 0.5) * 2 * extent / cams_x
-            cy = -extent + (j + 0.5) * 2 * extent / cams_y
+            cx = -ex + (i + 0.5) * 2 * ex / cams_x
+            cy = -ey + (j + 0.5) * 2 * ey / cams_y
             m = np.eye(4)
             m[:3, :3] = np.diag([1.0, -1.0, -1.0])       # camera z = world -z (looking down)
             m[:3, 3] = (cx, cy, height)

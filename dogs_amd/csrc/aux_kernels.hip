@@ -33,8 +33,16 @@ constexpr float GW[11] = {0.001028380123898387f, 0.0075987582094967365f, 0.03600
 __device__ __forceinline__ float wave_shl1(float x) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x130, 0xf, 0xf, false));
 }
-// sum_k GW[k] * x(lane + k), k = 0..10, in the reference's tap order
+// sum_k GW[k] * x(lane + k), k = 0..10.
+// Default: Horner form over the lanes -- acc <- shl1(acc) + GW[k] x from k = 10 down to 0 -- where the DPP shift folds
+// into the add (v_add_f32_dpp) and the window is symmetric, so the products are the six GW[k] x of k <= 5: 16 VALU per
+// convolution instead of 21 (10 DPP moves + 11 fmas).  The sum runs k = 10 .. 0 with rounded products (a few ulp from
+// the reference's k = 0 .. 10 order, inside the 1e-5 parity bar).  DG_SSIM_TAPFMA: the tap-order fma chain.
+__device__ __forceinline__ float wave_shl1_add(float acc, float t) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(acc), 0x130, 0xf, 0xf, false)) + t;
+}
 __device__ __forceinline__ float hconv11(float x) {
+#ifdef DG_SSIM_TAPFMA
     float acc = fmaf(GW[0], x, 0.0f);
 #pragma unroll
     for (int k = 1; k < 11; k++) {
@@ -42,6 +50,15 @@ __device__ __forceinline__ float hconv11(float x) {
         acc = fmaf(GW[k], x, acc);
     }
     return acc;
+#else
+    float t[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) t[k] = GW[k] * x;
+    float acc = t[0];                               // k = 10 (GW[10] = GW[0])
+#pragma unroll
+    for (int k = 9; k >= 0; k--) acc = wave_shl1_add(acc, t[k <= 5 ? k : 10 - k]);
+    return acc;
+#endif
 }
 
 struct StripPos { int x, y0, plane; bool valid; };

@@ -382,7 +382,7 @@ BwdScratch carve_bwd(void* base, int64_t K, int P, int T) {
     Carver c(base);
     BwdScratch s;
     const size_t n = (size_t)(K > 0 ? K : 1);
-    s.rec = c.take<float>(12 * n);
+    s.rec = c.take<float>((size_t)gs::REC_STRIDE * n);
     const size_t chunks = (n + gs::SUM_CHUNK - 1) / gs::SUM_CHUNK;  // every slot < K
     s.live_list = c.take<uint32_t>(chunks * gs::SUM_CHUNK);
     s.live_cnt = c.take<uint32_t>(chunks);

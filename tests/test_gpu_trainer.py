@@ -315,3 +315,30 @@ def test_native_and_autograd_routes_agree_1080p(hip_device):
     np.testing.assert_allclose(l0[:49], l1[:49], rtol=2e-4, atol=1e-6)
     assert c0[48] == c1[48] == 40_000 and c0[49] != 40_000
     np.testing.assert_allclose(c0, c1, rtol=5e-3)
+
+
+def test_overlap_with_two_view_sizes_is_bitwise_serial(hip_device):
+    """Views of two image sizes alternate (the step's scratch block is handed back for either size): the overlapped
+    f_dc / f_rest update reads its gradients from an offset that does not depend on the image size, so overlap=True
+    ends bit-identical to overlap=False (the gradients used to follow the image-sized buffers)."""
+    from dogs_amd.camera import make_camera, yaw_world_to_camera
+    from dogs_amd.trainer import GaussianSplatTrainer
+    dev = hip_device
+    cfg = _cfg(max_iterations=24, densify_start_iter=10 ** 6, opacity_reset_interval=10 ** 6, prune_iterations=(),
+               sh_increase_interval=6)
+    out = []
+    for overlap in (False, True):
+        m, _, _ = _problem(dev, n_true=20_000, n_init=4_000, W=320, H=240, views=1)
+        cams = [make_camera(w, h, 500.0, 500.0, world_to_camera=yaw_world_to_camera(math.radians(y))).to(dev)
+                for (w, h), y in (((320, 240), 0.0), ((512, 384), 1.0), ((320, 240), -1.0), ((512, 384), 2.0))]
+        g = torch.Generator().manual_seed(3)
+        gts = [torch.rand((3, c.height, c.width), generator=g).to(dev) for c in cams]
+        tr = GaussianSplatTrainer(m, cams, gts, cfg, device=dev, seed=5, native=True, overlap=overlap)
+        tr.train()
+        assert {lg.route for lg in tr.logs} == {"native"}
+        out.append((_model_raw(m), {g_["name"]: tr.optimizer.state[g_["params"][0]]["exp_avg"].clone()
+                                    for g_ in tr.optimizer.param_groups}))
+    for k in out[0][0]:
+        assert torch.equal(out[0][0][k], out[1][0][k]), k
+    for k in out[0][1]:
+        assert torch.equal(out[0][1][k], out[1][1][k]), k

@@ -107,7 +107,7 @@ def test_masked_training_native_matches_autograd(hip_device):
         assert _rel(a, b) < 1e-3
     for k in n0:
         assert _rel(n0[k], n1[k]) < 1e-3, k
-    assert _rel(n0["appearance_embedding"], net0.state_dict()["appearance_embedding"]) > 1e-4   # it trained
+    assert _rel(n0["appearance_embedding"], net0.state_dict()["appearance_embedding"].to(dev)) > 1e-4   # it trained
 
 
 def test_depth_threshold_scales_statistics(hip_device):

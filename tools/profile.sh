@@ -1,6 +1,7 @@
 #!/bin/bash
 # Kernel-trace stats + separate PMC passes of the bench workload (run on the GPU box from the repo root).
-# usage: tools/profile.sh OUTDIR [pmc]   -- each GPU step under its own timeout; stops at the first failure
+# usage: tools/profile.sh OUTDIR [pmc [COUNTERS_FILE]]   -- each GPU step under its own timeout; stops at the first
+# failure (COUNTERS_FILE: one "pmc: ..." pass per line, default tools/pmc_counters.txt)
 set -e
 OUT=${1:-gpurun_out/prof}
 ROOT=$(pwd)
@@ -15,5 +16,5 @@ if [ "$2" = "pmc" ]; then
     i=$((i+1))
     ctrs=${line#pmc: }
     timeout -k 10 300 rocprofv3 --pmc $ctrs -d "$OUT/pmc$i" -o run -- python3 $BENCH > "$OUT/pmc$i.log" 2>&1
-  done < "$ROOT/tools/pmc_counters.txt"
+  done < "${3:-$ROOT/tools/pmc_counters.txt}"
 fi
