@@ -13,11 +13,15 @@ Reference order (rank 0's master, once, at the first round with iteration >= den
     5. new block trainers from the sub-models, penalties set, duals set up, ADMM enabled.
 
 Here every rank runs the entry for its own block ("one block per GPU"):
-    * the blocks' tensors are all-gathered (variable row counts: one all_gather of the sizes, one of the padded
-      [N_max, 59] rows), so every rank fuses the same global model -- clipping, concatenation, the box tests and the
-      prune compaction are deterministic, so the ranks agree bit for bit without further exchange.  Memory: every
-      rank holds the fused model, 236 B per Gaussian (config 5, 8 blocks x 5e6: 9.4 GB of a rank's 288 GB of HBM),
-      as the reference's master does once;
+    * each rank clips its block to its original box first (the reference clips per block too, so the rows that cross
+      the wire are only the ones the fused model keeps), then the clipped rows are all-gathered (variable row
+      counts: one all_gather of the sizes, one of the rows padded to the largest block into one flat buffer), so
+      every rank fuses the same global model -- clipping, concatenation, the box tests and the prune compaction are
+      deterministic, so the ranks agree bit for bit without further exchange.  Memory: every rank holds the fused
+      model, 236 B per Gaussian (config 5, 8 blocks x ~5e6 clipped: ~9.4 GB of a rank's 288 GB of HBM), as the
+      reference's master does once; the gather's peak is the padded buffer plus the fused copy (2x), freed before the
+      count renders.  The count renders need the whole fused model on every rank that renders (any Gaussian can
+      occlude any camera's pixels), which is why it is gathered rather than sharded;
     * the count renders are split across ranks: rank r renders its own block's cameras only, keeping each camera's
       score vector (cameras x 4 B per fused Gaussian);
     * the importance is then summed in the reference's exact order: prune_gaussians_after_merge concatenates the
@@ -107,9 +111,10 @@ def _gather_device(group) -> torch.device | None:
     return torch.device("cpu") if dist.get_backend(group) == "gloo" else None
 
 
-def all_gather_rows(rows: torch.Tensor, group=None) -> list:
-    """Every rank's [n_r, D] rows (n_r may differ), in rank order: one all_gather of the sizes, one of the padded
-    rows."""
+def all_gather_rows(rows: torch.Tensor, group=None) -> torch.Tensor:
+    """Every rank's [n_r, D] rows (n_r may differ) concatenated in rank order, [sum n_r, D]: one all_gather of the
+    sizes, one of the rows padded to max n_r into one flat buffer (the peak is that buffer plus the result; gloo on host
+    tensors, RCCL on device tensors)."""
     world = dist.get_world_size(group)
     host = _gather_device(group)
     dev = rows.device
@@ -119,30 +124,42 @@ def all_gather_rows(rows: torch.Tensor, group=None) -> list:
     dist.all_gather(ns, n, group=group)
     sizes = [int(x.item()) for x in ns]
     nmax = max(sizes) if sizes else 0
-    pad = torch.zeros((nmax, rows.shape[1]), dtype=rows.dtype, device=src.device)
-    pad[:rows.shape[0]] = src
-    outs = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(outs, pad, group=group)
-    return [o[:s].to(dev) for o, s in zip(outs, sizes)]
+    d = rows.shape[1]
+    pad = src if src.shape[0] == nmax else torch.cat(
+        [src, torch.zeros((nmax - src.shape[0], d), dtype=src.dtype, device=src.device)], 0)
+    flat = torch.empty((world * nmax, d), dtype=rows.dtype, device=src.device)
+    dist.all_gather_into_tensor(flat, pad.contiguous(), group=group)
+    del pad, src
+    if not all(s == nmax for s in sizes):
+        flat = torch.cat([flat[r * nmax:r * nmax + s] for r, s in enumerate(sizes)], 0)
+    return flat.to(dev)
+
+
+def clip_block(model: GaussianSplatModel, box, world_to_obb_transform, kernels: PhaseKernels) -> torch.Tensor:
+    """fuse_block_gaussians' per-block step (master_gaussian_trainer.py:37-100): the [n, 59] rows of `model` inside
+    its ORIGINAL point box (OBB frame); every row when `box` is None."""
+    rows = _flat(model)
+    if box is None:
+        return rows
+    keep = kernels.members(model.get_xyz.detach()[:, :2], [box], world_to_obb_transform)[0]
+    return rows[keep.to(rows.device)]
+
+
+def _fused_model(rows: torch.Tensor, like: GaussianSplatModel) -> GaussianSplatModel:
+    fused = GaussianSplatModel(like.max_sh_degree, like.percent_dense, like.get_xyz.device)
+    fused.init_from_external_properties(*_split_rows(rows, like), optimizable=False)
+    # the master's model is created with active_sh_degree = max_sh_degree (master_gaussian_trainer.py:216-220), and
+    # the blocks' sub-models inherit it (get_sub_gaussians, gaussian_splat_model.py:290-306)
+    fused.active_sh_degree = like.max_sh_degree
+    return fused
 
 
 def fuse_blocks(block_models: list, ori_point_bboxes, world_to_obb_transform, kernels: PhaseKernels):
     """fuse_block_gaussians (master_gaussian_trainer.py:37-100) without its PLY side outputs: each block clipped to
     its original box (OBB frame), concatenated in block order.  Returns the fused (non-optimisable) model."""
-    parts = []
-    for b, m in enumerate(block_models):
-        rows = _flat(m)
-        if ori_point_bboxes is not None:
-            keep = kernels.members(m.get_xyz.detach()[:, :2], [ori_point_bboxes[b]], world_to_obb_transform)[0]
-            rows = rows[keep.to(rows.device)]
-        parts.append(rows)
-    like = block_models[0]
-    fused = GaussianSplatModel(like.max_sh_degree, like.percent_dense, like.get_xyz.device)
-    fused.init_from_external_properties(*_split_rows(torch.cat(parts, 0), like), optimizable=False)
-    # the master's model is created with active_sh_degree = max_sh_degree (master_gaussian_trainer.py:216-220), and
-    # the blocks' sub-models inherit it (get_sub_gaussians, gaussian_splat_model.py:290-306)
-    fused.active_sh_degree = like.max_sh_degree
-    return fused
+    parts = [clip_block(m, None if ori_point_bboxes is None else ori_point_bboxes[b], world_to_obb_transform, kernels)
+             for b, m in enumerate(block_models)]
+    return _fused_model(torch.cat(parts, 0), block_models[0])
 
 
 def ordered_importance(fused: GaussianSplatModel, camera_blocks: list, kernels: PhaseKernels, bg: torch.Tensor,
@@ -236,16 +253,12 @@ def enter_admm_phase(block_model: GaussianSplatModel, camera_blocks: list, ori_p
         raise RuntimeError(f"{len(camera_blocks)} camera blocks for {world} ranks (one block per rank)")
     dev = block_model.get_xyz.device
     bg = torch.zeros(3, dtype=torch.float32, device=dev) if bg is None else bg
-    # 1. every block's model on every rank, fused identically
-    rows = all_gather_rows(_flat(block_model), group)
-    blocks = []
-    for r in rows:
-        m = GaussianSplatModel(block_model.max_sh_degree, block_model.percent_dense, dev)
-        m.init_from_external_properties(*_split_rows(r, block_model))
-        m.active_sh_degree = block_model.active_sh_degree
-        blocks.append(m)
-    fused = fuse_blocks(blocks, ori_point_bboxes, world_to_obb_transform, kernels)
-    del blocks, rows
+    # 1. every rank clips its own block to its original box (the reference's per-block fuse step), the clipped rows
+    #    are all-gathered in block order and every rank builds the same fused model from them
+    rows = all_gather_rows(clip_block(block_model, None if ori_point_bboxes is None else ori_point_bboxes[rank],
+                                      world_to_obb_transform, kernels), group)
+    fused = _fused_model(rows, block_model)
+    del rows
     # 2. importance: this rank renders its cameras only, summed in the reference's order down the rank chain
     imp = ordered_importance(fused, camera_blocks, kernels, bg, group)
     v_imp_prune(fused, imp, cfg, kernels)

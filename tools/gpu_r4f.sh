@@ -14,6 +14,12 @@ for r in 1 2 3; do
         > "$OUT/train_$v.$r.txt" 2>&1
   done
 done
+timeout -k 10 300 python tools/trainer_bench.py --bench-autograd --steps 200 > "$OUT/train_autograd.txt" 2>&1
+timeout -k 10 300 python tools/trainer_bench.py --bench-autograd --steps 100 --cprofile > "$OUT/train_autograd_cprof.txt" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/agtrace" -o ag -- python3 tools/trainer_bench.py \
+    --bench-autograd --steps 50 > "$OUT/agtrace.log" 2>&1
+find "$OUT/agtrace" -name "*kernel_stats.csv" -exec cp {} "$OUT/autograd_kernel_stats.csv" \; || true
+rm -rf "$OUT/agtrace"
 bash tools/profile.sh "$OUT/prof" pmc
 python3 tools/pmc_traffic.py "$OUT/prof" 1000000 1920 1080 > "$OUT/pmc_traffic.log" 2>&1
 cp profiles/pmc_traffic.json "$OUT/pmc_traffic.json"

@@ -23,16 +23,19 @@ def main():
                     help="alternate the native step's routes (DG_TRAIN_UNFUSED on/off) every 10 steps")
     ap.add_argument("--bench-native", action="store_true",
                     help="time bench.py's native train step (no ADMM penalty, densification statistics on)")
+    ap.add_argument("--bench-autograd", action="store_true",
+                    help="time bench.py's autograd-route train step (the drop-in calls as the reference trainer makes)")
     args = ap.parse_args()
     from dogs_amd.admm import ADMMConfig
     from dogs_amd.admm_trainer import make_block
     dev = torch.device("cuda", 0)
-    if args.bench_native:
+    if args.bench_native or args.bench_autograd:
         import bench
         from dogs_amd.synthetic import make_scene
         s = make_scene(args.n, args.width, args.height, seed=1234).to(dev)
         cams = bench.make_cameras(args.width, args.height, bench.view_yaws(args.views), dev)
-        step = bench.TrainStep(s, cams, dev, 1234).native()
+        ts = bench.TrainStep(s, cams, dev, 1234)
+        step = ts.native() if args.bench_native else ts.step
     elif args.raster_only:
         import bench
         from dogs_amd.synthetic import make_scene
