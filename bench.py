@@ -189,8 +189,9 @@ class TrainStep:
                                                           SparseGaussianAdam)
         from dogs_amd.activations import activate
         from dogs_amd.fused_ssim import fused_ssim
-        from dogs_amd.loss import clamp_l1
+        from dogs_amd.loss import clamp_l1, row_prod
         self.activate, self.clamp_l1, self.fused_ssim = activate, clamp_l1, fused_ssim
+        self.row_prod = row_prod  # prod(dim=1) without prod_backward's host read of the zero count
         self.cams = cams
         self.rasts = [GaussianRasterizer(GaussianRasterizationSettings(
             c.height, c.width, c.tanfovx, c.tanfovy, torch.zeros(3, device=dev), 1.0, c.world_to_camera,
@@ -226,7 +227,7 @@ class TrainStep:
         img, l1 = self.clamp_l1(img, self.gt)  # render()'s clamp + the L1 term, one launch each way
         ssim = self.fused_ssim(img.unsqueeze(0), self.gt.unsqueeze(0))
         # gaussian_trainer.py:387-408: lambda_dssim 0.2, lambda_scale 0.05 (urban3d_admm.yaml loss block)
-        loss = 0.8 * l1 + 0.2 * (1.0 - ssim) + 0.05 * scales.prod(dim=1).mean()
+        loss = 0.8 * l1 + 0.2 * (1.0 - ssim) + 0.05 * self.row_prod(scales).mean()
         loss.backward()
         vis = radii > 0
         self.opt.step(vis, radii.shape[0], stats=dict(self.stats, radii=radii, dmeans2D=m2d.grad))

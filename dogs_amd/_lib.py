@@ -84,7 +84,7 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count"
            "dg_add_densification_stats", "dg_densify_select", "dg_densify_split_stds", "dg_densify_count",
            "dg_densify_gather", "dg_splat_pack", "dg_ply_pack", "dg_ring_create", "dg_ring_submit", "dg_ring_next",
            "dg_ring_upload", "dg_ring_pending", "dg_ring_destroy", "dg_image_u8_to_chw", "dg_points_in_boxes2d", "dg_activate_forward", "dg_activate_backward", "dg_clamp_l1_blocks",
-           "dg_clamp_l1_forward", "dg_clamp_l1_backward", "dg_adaptive_capacity", "dg_debug_counters", "dg_adam_update_groups_prox", "dg_train_step", "dg_train_sync",
+           "dg_clamp_l1_forward", "dg_clamp_l1_backward", "dg_row_prod_forward", "dg_row_prod_backward", "dg_adaptive_capacity", "dg_debug_counters", "dg_adam_update_groups_prox", "dg_train_step", "dg_train_sync",
            "dg_colmap_cameras", "dg_colmap_images", "dg_colmap_points3d", "dg_prune_select", "dg_prune_gather_stats",
            "dg_last_error", "dg_version")
 
@@ -208,6 +208,10 @@ def load(path: str | None = None):
             L.dg_clamp_l1_forward.argtypes = [C.c_uint32] + [vp] * 4 + [vp]
             L.dg_clamp_l1_backward.restype = C.c_int
             L.dg_clamp_l1_backward.argtypes = [C.c_uint32] + [vp] * 6 + [vp]
+            L.dg_row_prod_forward.restype = C.c_int
+            L.dg_row_prod_forward.argtypes = [C.c_uint32, C.c_uint32, vp, vp, vp, vp]
+            L.dg_row_prod_backward.restype = C.c_int
+            L.dg_row_prod_backward.argtypes = [C.c_uint32, C.c_uint32] + [vp] * 5 + [vp]
         if hasattr(L, "dg_activate_forward"):
             L.dg_activate_forward.restype = C.c_int
             L.dg_activate_forward.argtypes = [C.c_uint32] + [vp] * 6 + [vp]

@@ -135,10 +135,11 @@ class BlockTrainer:
         from .diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer, SparseGaussianAdam
         from .activations import activate
         from .fused_ssim import fused_ssim
-        from .loss import clamp_l1
+        from .loss import clamp_l1, row_prod
         self.cfg = cfg or TrainConfig()
         self.device = device or raw["xyz"].device
         self.activate, self.clamp_l1, self.fused_ssim = activate, clamp_l1, fused_ssim
+        self.row_prod = row_prod
         self.params = {n: raw[n].detach().to(self.device).contiguous().clone().requires_grad_(True)
                        for n in PARAM_NAMES}
         c = self.cfg
@@ -221,7 +222,7 @@ class BlockTrainer:
         img, l1 = self.clamp_l1(img, gt)
         ssim = self.fused_ssim(img.unsqueeze(0), gt.unsqueeze(0))
         c = self.cfg
-        loss = (1.0 - c.lambda_dssim) * l1 + c.lambda_dssim * (1.0 - ssim) + c.lambda_scale * scales.prod(dim=1).mean()
+        loss = (1.0 - c.lambda_dssim) * l1 + c.lambda_dssim * (1.0 - ssim) + c.lambda_scale * self.row_prod(scales).mean()
         loss.backward()
         self.opt.step(radii > 0, radii.shape[0], prox=self.admm.prox(self.param_tuple()))
         self.opt.zero_grad(set_to_none=True)

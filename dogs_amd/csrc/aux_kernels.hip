@@ -15,7 +15,7 @@ namespace gs {
 // plane: the 64 lanes hold 54 + 10 halo columns, so the horizontal 11-tap pass is a chain of DPP wave_shl:1 moves
 // (lane i <- lane i+1) with no LDS at all, and the vertical pass runs over a ring of the last 11 rows' horizontal
 // moments in registers (the 11-row loop is unrolled so every ring slot is a compile-time register).  Products and
-// fma order per moment are the reference's (x taps 0..10, then y taps 0..10).  Rows are read 2 ahead of use.
+// fma order per moment are the reference's (x taps 0..10, then y taps 0..10).  Rows are read SSIM_PF ahead of use.
 // (The first version staged 42x42 halo tiles and the x-pass moments in LDS: forward 94-102 us, backward 80 us at
 // 1080p x 3; this one: 94 and 60.)
 // ------------------------------------------------------------------------------------------------
@@ -25,6 +25,10 @@ constexpr int SSW_OUT = 54;   // output columns per wave
 #endif
 constexpr int SSW_ROWS = DG_SSW_ROWS;  // output rows per wave
 constexpr int SSW_IN = SSW_ROWS + 10;
+#ifndef DG_SSIM_PF
+#define DG_SSIM_PF 2
+#endif
+constexpr int SSIM_PF = DG_SSIM_PF;   // input rows loaded ahead of use (a register queue of SSIM_PF rows)
 constexpr float GW[11] = {0.001028380123898387f, 0.0075987582094967365f, 0.036000773310661316f,
                           0.10936068743467331f, 0.21300552785396576f, 0.26601171493530273f,
                           0.21300552785396576f, 0.10936068743467331f, 0.036000773310661316f,
@@ -112,17 +116,25 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
     float ring[11][5];
     // FUSED: the clamped image and the L1 term as the input rows arrive -- lanes 5..58 hold the strip's output columns
     const bool own_col = FUSED && lane >= 5 && lane < 5 + SSW_OUT && colok;
-    float ua = lda(sp.y0 - 5), va = ldb(sp.y0 - 5);
-    float ub = lda(sp.y0 - 4), vb = ldb(sp.y0 - 4);
+    float qa[SSIM_PF], qb[SSIM_PF];
+#pragma unroll
+    for (int p = 0; p < SSIM_PF; p++) {
+        qa[p] = lda(sp.y0 - 5 + p);
+        qb[p] = ldb(sp.y0 - 5 + p);
+    }
     for (int base = 0; base < SSW_IN; base += 11) {
 #pragma unroll
         for (int j = 0; j < 11; j++) {
             const int rr = base + j;
             if (rr < SSW_IN) {
-                const float u = ua, v = va;
-                ua = ub; va = vb;
-                ub = lda(sp.y0 - 5 + rr + 2);
-                vb = ldb(sp.y0 - 5 + rr + 2);
+                const float u = qa[0], v = qb[0];
+#pragma unroll
+                for (int p = 0; p + 1 < SSIM_PF; p++) {
+                    qa[p] = qa[p + 1];
+                    qb[p] = qb[p + 1];
+                }
+                qa[SSIM_PF - 1] = lda(sp.y0 - 5 + rr + SSIM_PF);
+                qb[SSIM_PF - 1] = ldb(sp.y0 - 5 + rr + SSIM_PF);
                 if (FUSED) {
                     const int row = sp.y0 - 5 + rr;  // one of the strip's output rows
                     if (own_col && row >= sp.y0 && row < sp.y0 + SSW_ROWS && row < H) {
@@ -261,17 +273,22 @@ __global__ void __launch_bounds__(256) k_ssim_bwd_strip(int H, int W, int planes
         }
     };
     float ring[11][3];
-    float a0, a1, a2, b0, b1, b2;
-    ld3(sp.y0 - 5, a0, a1, a2);
-    ld3(sp.y0 - 4, b0, b1, b2);
+    float q0[SSIM_PF], q1[SSIM_PF], q2[SSIM_PF];
+#pragma unroll
+    for (int p = 0; p < SSIM_PF; p++) ld3(sp.y0 - 5 + p, q0[p], q1[p], q2[p]);
     for (int base = 0; base < SSW_IN; base += 11) {
 #pragma unroll
         for (int j = 0; j < 11; j++) {
             const int rr = base + j;
             if (rr < SSW_IN) {
-                const float s0 = a0, s1 = a1, s2 = a2;
-                a0 = b0; a1 = b1; a2 = b2;
-                ld3(sp.y0 - 5 + rr + 2, b0, b1, b2);
+                const float s0 = q0[0], s1 = q1[0], s2 = q2[0];
+#pragma unroll
+                for (int p = 0; p + 1 < SSIM_PF; p++) {
+                    q0[p] = q0[p + 1];
+                    q1[p] = q1[p + 1];
+                    q2[p] = q2[p + 1];
+                }
+                ld3(sp.y0 - 5 + rr + SSIM_PF, q0[SSIM_PF - 1], q1[SSIM_PF - 1], q2[SSIM_PF - 1]);
                 ring[j][0] = hconv11(s0);
                 ring[j][1] = hconv11(s1);
                 ring[j][2] = hconv11(s2);

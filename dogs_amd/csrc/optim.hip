@@ -458,6 +458,50 @@ __global__ void __launch_bounds__(256) k_clamp_l1_bwd(uint32_t n, const float* _
     d_img[i] = (x >= 0.f && x <= 1.f) ? g : 0.f;
 }
 
+// torch.prod(x, dim=1) of x [N, M], M <= 4 (the scale regulariser's prod of the scaling), and its autograd backward
+// (FunctionsManual.cpp prod_backward) without the host read: torch counts the zeros of x, reads the count back and
+// picks dprod * (prod / x) when there are none, else for EVERY row the zero-safe dprod * (exclusive left cumprod x
+// exclusive right cumprod).  Here the forward raises *any_zero (vector atomic) and the backward reads it on the device.
+// Row order: the reduction keeps one accumulator per element for M <= 4 and combines them left to right, so the
+// product is ((x0 x1) x2) x3.
+__global__ void __launch_bounds__(256) k_row_prod_fwd(uint32_t N, uint32_t M, const float* __restrict__ x,
+                                                      float* __restrict__ prod, uint32_t* __restrict__ any_zero) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    bool z = false;
+    if (i < N) {
+        const float* r = x + (size_t)i * M;
+        float p = r[0];
+        z = r[0] == 0.0f;
+        for (uint32_t k = 1; k < M; k++) {
+            p = p * r[k];
+            z |= r[k] == 0.0f;
+        }
+        prod[i] = p;
+    }
+    if (__any(z) && (threadIdx.x & 63) == 0) atomicOr(any_zero, 1u);  // every lane is live here (no early return)
+}
+__global__ void __launch_bounds__(256) k_row_prod_bwd(uint32_t N, uint32_t M, const float* __restrict__ x,
+                                                      const float* __restrict__ prod, const float* __restrict__ dprod,
+                                                      const uint32_t* __restrict__ any_zero, float* __restrict__ dx) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= N) return;
+    const float* r = x + (size_t)i * M;
+    float* d = dx + (size_t)i * M;
+    const float g = dprod[i];
+    if (*any_zero == 0u) {
+        const float p = prod[i];
+        for (uint32_t k = 0; k < M; k++) d[k] = g * (p / r[k]);
+        return;
+    }
+    // cat([1, x0 .. x(M-2)]).cumprod() and cat([1, x(M-1) .. x1]).cumprod().flip()
+    float left[4], right[4];
+    left[0] = 1.0f;
+    for (uint32_t k = 1; k < M; k++) left[k] = left[k - 1] * r[k - 1];
+    right[M - 1] = 1.0f;
+    for (int k = (int)M - 2; k >= 0; k--) right[k] = right[k + 1] * r[k + 1];
+    for (uint32_t k = 0; k < M; k++) d[k] = g * (left[k] * right[k]);
+}
+
 }  // namespace
 
 void launch_adam_multi(const AdamMultiArgs& a0, hipStream_t s) {
@@ -507,6 +551,14 @@ void launch_activate_bwd(uint32_t N, const float* o, const float* sc, const floa
                          const float* gsc, const float* gq, float* dro, float* drs, float* drq, hipStream_t s,
                          float scale_reg) {
     if (N) k_activate_bwd<<<(N + 255) / 256, 256, 0, s>>>(N, o, sc, rq, go, gsc, gq, dro, drs, drq, scale_reg);
+}
+
+void launch_row_prod_fwd(uint32_t N, uint32_t M, const float* x, float* prod, uint32_t* any_zero, hipStream_t s) {
+    if (N) k_row_prod_fwd<<<(N + 255) / 256, 256, 0, s>>>(N, M, x, prod, any_zero);
+}
+void launch_row_prod_bwd(uint32_t N, uint32_t M, const float* x, const float* prod, const float* dprod,
+                         const uint32_t* any_zero, float* dx, hipStream_t s) {
+    if (N) k_row_prod_bwd<<<(N + 255) / 256, 256, 0, s>>>(N, M, x, prod, dprod, any_zero, dx);
 }
 
 uint32_t clamp_l1_blocks(uint32_t n) { return (n + 256u * L1_PER_THREAD - 1) / (256u * L1_PER_THREAD); }

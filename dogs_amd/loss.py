@@ -49,3 +49,42 @@ class _ClampL1(torch.autograd.Function):
 def clamp_l1(image: torch.Tensor, gt: torch.Tensor):
     """(image.clamp(0, 1), mean |image.clamp(0, 1) - gt|), both differentiable w.r.t. image."""
     return _ClampL1.apply(image, gt)
+
+
+class _RowProd(torch.autograd.Function):
+    """torch.prod(x, dim=1) for x [N, M <= 4] through dg_row_prod_forward / dg_row_prod_backward: the same values and
+    gradients as torch's, without prod_backward's host read of the zero count (a stream sync in the middle of every
+    training backward; the kernels keep the zero test on the device)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        _lib.require_device(x, "x")
+        _lib.require_f32_on(x.device, x=x)
+        if x.dim() != 2 or not 1 <= x.size(1) <= 4:
+            raise RuntimeError(f"row_prod: x must be [N, M] with 1 <= M <= 4, got {tuple(x.shape)}")
+        xc = x.detach().contiguous()
+        n, m = int(xc.size(0)), int(xc.size(1))
+        prod = torch.empty(n, dtype=torch.float32, device=x.device)
+        flag = torch.empty(1, dtype=torch.int32, device=x.device)
+        with torch.cuda.device(x.device):
+            _lib.check(_lib.load().dg_row_prod_forward(n, m, xc.data_ptr(), prod.data_ptr(), flag.data_ptr(),
+                                                       _lib.stream_of(x.device)))
+        ctx.save_for_backward(xc, prod, flag)
+        return prod
+
+    @staticmethod
+    def backward(ctx, g):
+        xc, prod, flag = ctx.saved_tensors
+        n, m = int(xc.size(0)), int(xc.size(1))
+        gc = g.contiguous()
+        dx = torch.empty_like(xc)
+        with torch.cuda.device(xc.device):
+            _lib.check(_lib.load().dg_row_prod_backward(n, m, xc.data_ptr(), prod.data_ptr(), gc.data_ptr(),
+                                                        flag.data_ptr(), dx.data_ptr(), _lib.stream_of(xc.device)))
+        return dx
+
+
+def row_prod(x: torch.Tensor) -> torch.Tensor:
+    """x.prod(dim=1) for [N, M <= 4] float32 device tensors (the scale regulariser lambda_scale *
+    get_scaling.prod(dim=1).mean(), gaussian_trainer.py:405-408), bit-identical to torch's values and gradients."""
+    return _RowProd.apply(x)

@@ -365,6 +365,7 @@ class GaussianSplatTrainer:
     def _autograd_iteration(self, k: int, ev: list, resolution: int = 1) -> None:
         from .densify import densify_and_prune
         from .fused_ssim import fused_ssim
+        from .loss import row_prod
         from .prune import calculate_v_imp_score, prune_list
         from .render import render
         c, m = self.cfg, self.model
@@ -390,7 +391,7 @@ class GaussianSplatTrainer:
         else:
             l1 = F.l1_loss(colors, gt)
             loss = (1.0 - c.lambda_dssim) * l1 + c.lambda_dssim * (1.0 - loss_ssim)
-        loss = loss + c.lambda_scale * out["scaling"].prod(dim=1).mean()
+        loss = loss + c.lambda_scale * row_prod(out["scaling"]).mean()
         loss.backward()
         self.last_loss = loss.detach()
         replaced = False

@@ -271,6 +271,44 @@ def ssim_backward(img1, img2, dL_dmap, dm_dmu1, dm_dsigma1_sq, dm_dsigma12):
     return out
 
 
+# fused-ssim's window (ssim.cu:11-15): the float32 constants, held exactly in float64
+_SSIM_GW = np.array([0.001028380123898387, 0.0075987582094967365, 0.036000773310661316, 0.10936068743467331,
+                     0.21300552785396576, 0.26601171493530273, 0.21300552785396576, 0.10936068743467331,
+                     0.036000773310661316, 0.0075987582094967365, 0.001028380123898387], np.float32).astype(np.float64)
+
+
+def _conv11_f64(x: np.ndarray) -> np.ndarray:
+    """The zero-padded separable 11 x 11 Gaussian window over the last two axes, in float64."""
+    H, W = x.shape[-2:]
+    p = np.pad(x, [(0, 0)] * (x.ndim - 2) + [(5, 5), (5, 5)])
+    h = sum(g * p[..., :, k:k + W] for k, g in enumerate(_SSIM_GW))
+    return sum(g * h[..., k:k + H, :] for k, g in enumerate(_SSIM_GW))
+
+
+def ssim_forward_exact(img1, img2, C1=0.01 ** 2, C2=0.03 ** 2):
+    """ssim_forward's four maps evaluated in float64 on the same float32 inputs: the value every float32 summation
+    order approximates.  A GPU kernel that sums the window in another order than the reference's (ssim.cu:187-286)
+    is held to the reference order's own float32 error against this (tests/test_gpu_aux.py)."""
+    a, b = _f(img1).astype(np.float64), _f(img2).astype(np.float64)
+    mu1, mu2 = _conv11_f64(a), _conv11_f64(b)
+    s1 = _conv11_f64(a * a) - mu1 * mu1
+    s2 = _conv11_f64(b * b) - mu2 * mu2
+    s12 = _conv11_f64(a * b) - mu1 * mu2
+    Cc, D = 2 * mu1 * mu2 + C1, 2 * s12 + C2
+    A, B = mu1 * mu1 + mu2 * mu2 + C1, s1 + s2 + C2
+    d1 = (mu2 * 2 * D) / (A * B) - (mu2 * 2 * Cc) / (A * B) - (mu1 * 2 * Cc * D) / (A * A * B) + \
+        (mu1 * 2 * Cc * D) / (A * B * B)
+    return Cc * D / (A * B), d1, (-Cc * D) / (A * B * B), (2 * Cc) / (A * B)
+
+
+def ssim_backward_exact(img1, img2, dL_dmap, dm_dmu1, dm_dsigma1_sq, dm_dsigma12):
+    """ssim_backward in float64 on the same float32 inputs (ssim.cu:288-366)."""
+    a, b = _f(img1).astype(np.float64), _f(img2).astype(np.float64)
+    dl = _f(dL_dmap).astype(np.float64)
+    t = [_conv11_f64(_f(x).astype(np.float64) * dl) for x in (dm_dmu1, dm_dsigma1_sq, dm_dsigma12)]
+    return t[0] + 2 * a * t[1] + b * t[2]
+
+
 def knn_dist2(points):
     p = _f(points).reshape(-1, 3)
     out = np.zeros(p.shape[0], np.float32)

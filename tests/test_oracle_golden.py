@@ -59,6 +59,22 @@ def test_ssim_matches_reference_ssim_torch(oracle, tag):
     assert np.abs(g - ref).max() <= 1e-4 * np.abs(ref).max()
 
 
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_ssim_exact_restatement(oracle, tag):
+    """The float64 SSIM maps (the GPU SSIM parity bar's anchor) against the reference's golden value and the float32
+    restatement."""
+    a = _load("golden_ssim.npz")
+    img1, img2 = a[f"{tag}_img1"], a[f"{tag}_img2"]
+    ref = O.ssim_forward(img1, img2)
+    ex = O.ssim_forward_exact(img1, img2)
+    assert abs(float(ex[0].mean()) - float(a[f"{tag}_value"])) < 2e-6
+    for r, e in zip(ref, ex):
+        assert np.abs(r - e).max() <= 1e-5 * max(1.0, np.abs(e).max())
+    dmap = np.full_like(ref[0], 1.0 / ref[0].size)
+    g, ge = O.ssim_backward(img1, img2, dmap, *ref[1:]), O.ssim_backward_exact(img1, img2, dmap, *ref[1:])
+    assert np.abs(g - ge).max() <= 1e-5 * np.abs(ge).max()
+
+
 @pytest.mark.parametrize("name", ["golden_raster_64x48.npz", "golden_raster_133x97_aa.npz"])
 def test_oracle_raster_regression(oracle, name):
     a = _load(name)

@@ -8,8 +8,11 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_aux.py tests/test_gpu_admm.py tests/test_gpu_training.py \
     tests/test_gpu_admm_run.py -q -rA --timeout 500 --timeout-method thread > "$OUT/tests.log" 2>&1 || true
 for r in 1 2 3; do
-  for v in ssim_horner ssim_tapfma; do
+  for v in ssim_horner ssim_tapfma ssim_pf4 ssim_pf6 ssim_r16 ssim_r16pf4; do
+    echo "== $v" >> "$OUT/ssim_ab.txt"
     DOGS_HIP_LIB=$(pwd)/ab/$v.so timeout -k 10 120 python tools/ssim_bench.py 100 >> "$OUT/ssim_ab.txt" 2>&1
+  done
+  for v in ssim_horner ssim_tapfma; do
     DOGS_HIP_LIB=$(pwd)/ab/$v.so timeout -k 10 300 python tools/trainer_bench.py --bench-native --steps 200 \
         > "$OUT/train_$v.$r.txt" 2>&1
   done

@@ -25,7 +25,12 @@ def main():
                     help="time bench.py's native train step (no ADMM penalty, densification statistics on)")
     ap.add_argument("--bench-autograd", action="store_true",
                     help="time bench.py's autograd-route train step (the drop-in calls as the reference trainer makes)")
+    ap.add_argument("--autograd-main-thread", action="store_true",
+                    help="run the backward on the calling thread (torch.autograd.set_multithreading_enabled(False)) so "
+                         "--cprofile sees the backward functions")
     args = ap.parse_args()
+    if args.autograd_main_thread:
+        torch.autograd.set_multithreading_enabled(False)
     from dogs_amd.admm import ADMMConfig
     from dogs_amd.admm_trainer import make_block
     dev = torch.device("cuda", 0)
@@ -85,7 +90,7 @@ def main():
     if prof is not None:
         prof.disable()
         import pstats
-        pstats.Stats(prof).sort_stats("tottime").print_stats(30)
+        pstats.Stats(prof).sort_stats("tottime").print_stats(45)
     dt = (time.perf_counter() - t0) / args.steps
     host.sort()
     print(f"local step {dt * 1e3:.3f} ms ({1.0 / dt:.1f} views/s); host per step median {host[len(host) // 2] * 1e3:.3f}"
