@@ -1419,7 +1419,7 @@ int dg_clamp_l1_backward(uint32_t n, const float* img, const float* clamped, con
 }
 
 int dg_row_prod_forward(uint32_t N, uint32_t M, const float* x, float* prod, uint32_t* any_zero, dg_stream_t stream) {
-    if (M < 1 || M > 4) return fail("row_prod: 1 <= M <= 4 columns%s%d");
+    if (M < 1 || M > 3) return fail("row_prod: 1 <= M <= 3 columns%s%d");
     if (!any_zero || (N && (!x || !prod))) return fail("row_prod: NULL tensor%s%d");
     HIP_OK(hipMemsetAsync(any_zero, 0, sizeof(uint32_t), (hipStream_t)stream));
     gs::launch_row_prod_fwd(N, M, x, prod, any_zero, (hipStream_t)stream);
@@ -1429,7 +1429,7 @@ int dg_row_prod_forward(uint32_t N, uint32_t M, const float* x, float* prod, uin
 
 int dg_row_prod_backward(uint32_t N, uint32_t M, const float* x, const float* prod, const float* dprod,
                          const uint32_t* any_zero, float* dx, dg_stream_t stream) {
-    if (M < 1 || M > 4) return fail("row_prod backward: 1 <= M <= 4 columns%s%d");
+    if (M < 1 || M > 3) return fail("row_prod backward: 1 <= M <= 3 columns%s%d");
     if (N == 0) return 0;
     if (!x || !prod || !dprod || !any_zero || !dx) return fail("row_prod backward: NULL tensor%s%d");
     gs::launch_row_prod_bwd(N, M, x, prod, dprod, any_zero, dx, (hipStream_t)stream);

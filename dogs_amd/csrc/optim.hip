@@ -57,7 +57,7 @@ __device__ __forceinline__ float exp_bwd(float g, const float* __restrict__ s3, 
         if (s3[0] == 0.0f || s3[1] == 0.0f || s3[2] == 0.0f)
             d = r == 0 ? s3[2] * s3[1] : r == 1 ? s3[0] * s3[2] : s3[0] * s3[1];
         else
-            d = ((s3[0] * s3[1]) * s3[2]) / s3[r];
+            d = ((s3[0] * s3[2]) * s3[1]) / s3[r];  // torch.prod's row order on the GPU (k_row_prod_fwd)
         return (g + reg * d) * s3[r];
     }
     return g * s3[r];
@@ -458,25 +458,23 @@ __global__ void __launch_bounds__(256) k_clamp_l1_bwd(uint32_t n, const float* _
     d_img[i] = (x >= 0.f && x <= 1.f) ? g : 0.f;
 }
 
-// torch.prod(x, dim=1) of x [N, M], M <= 4 (the scale regulariser's prod of the scaling), and its autograd backward
+// torch.prod(x, dim=1) of x [N, M], M <= 3 (the scale regulariser's prod of the scaling), and its autograd backward
 // (FunctionsManual.cpp prod_backward) without the host read: torch counts the zeros of x, reads the count back and
 // picks dprod * (prod / x) when there are none, else for EVERY row the zero-safe dprod * (exclusive left cumprod x
 // exclusive right cumprod).  Here the forward raises *any_zero (vector atomic) and the backward reads it on the device.
-// Row order: the reduction keeps one accumulator per element for M <= 4 and combines them left to right, so the
-// product is ((x0 x1) x2) x3.
+// Row order: torch's reduction gives a row of M <= 4 elements to 4 lanes (identity 1 past M) and combines them with
+// shuffles at offsets 2 then 1, so the product is (x0 x2)(x1 x3): (x0 x2) x1 for M = 3 (tools/prod_order_probe.py
+// finds no other order matching on the GPU).  Every cumprod entry of the zero-safe form has at most two factors
+// for M <= 3, so its value does not depend on the scan's association.
 __global__ void __launch_bounds__(256) k_row_prod_fwd(uint32_t N, uint32_t M, const float* __restrict__ x,
                                                       float* __restrict__ prod, uint32_t* __restrict__ any_zero) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     bool z = false;
     if (i < N) {
         const float* r = x + (size_t)i * M;
-        float p = r[0];
-        z = r[0] == 0.0f;
-        for (uint32_t k = 1; k < M; k++) {
-            p = p * r[k];
-            z |= r[k] == 0.0f;
-        }
-        prod[i] = p;
+        const float a = r[0], b = M > 1 ? r[1] : 1.0f, c = M > 2 ? r[2] : 1.0f;
+        prod[i] = (a * c) * b;
+        z = a == 0.0f || b == 0.0f || c == 0.0f;
     }
     if (__any(z) && (threadIdx.x & 63) == 0) atomicOr(any_zero, 1u);  // every lane is live here (no early return)
 }
@@ -494,7 +492,7 @@ __global__ void __launch_bounds__(256) k_row_prod_bwd(uint32_t N, uint32_t M, co
         return;
     }
     // cat([1, x0 .. x(M-2)]).cumprod() and cat([1, x(M-1) .. x1]).cumprod().flip()
-    float left[4], right[4];
+    float left[3], right[3];
     left[0] = 1.0f;
     for (uint32_t k = 1; k < M; k++) left[k] = left[k - 1] * r[k - 1];
     right[M - 1] = 1.0f;
@@ -570,14 +568,14 @@ void launch_clamp_l1_bwd(uint32_t n, const float* img, const float* clamped, con
     if (n) k_clamp_l1_bwd<<<(n + 255) / 256, 256, 0, s>>>(n, img, clamped, gt, g_img, g_l1, g_l1_value, d_img);
 }
 
-// Sum of x[0..n) (mode 0) or of the row products x[3i] x[3i+1] x[3i+2] over n rows (mode 1: the scale
+// Sum of x[0..n) (mode 0) or of the row products (x[3i] x[3i+2]) x[3i+1] over n rows (mode 1: the scale
 // regulariser's prod(scaling, 1)) into one partial per 256-thread block; k_loss_final totals the partials in order.
 __global__ void __launch_bounds__(256) k_block_sum(const float* __restrict__ x, uint32_t n, int mode,
                                                    float* __restrict__ partial) {
     __shared__ float s_w[4];
     float acc = 0.0f;
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u)
-        acc += mode ? (x[3 * (size_t)i] * x[3 * (size_t)i + 1]) * x[3 * (size_t)i + 2] : x[i];
+        acc += mode ? (x[3 * (size_t)i] * x[3 * (size_t)i + 2]) * x[3 * (size_t)i + 1] : x[i];  // torch.prod's order
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = acc;
     __syncthreads();

@@ -52,7 +52,7 @@ def clamp_l1(image: torch.Tensor, gt: torch.Tensor):
 
 
 class _RowProd(torch.autograd.Function):
-    """torch.prod(x, dim=1) for x [N, M <= 4] through dg_row_prod_forward / dg_row_prod_backward: the same values and
+    """torch.prod(x, dim=1) for x [N, M <= 3] through dg_row_prod_forward / dg_row_prod_backward: the same values and
     gradients as torch's, without prod_backward's host read of the zero count (a stream sync in the middle of every
     training backward; the kernels keep the zero test on the device)."""
 
@@ -60,8 +60,8 @@ class _RowProd(torch.autograd.Function):
     def forward(ctx, x):
         _lib.require_device(x, "x")
         _lib.require_f32_on(x.device, x=x)
-        if x.dim() != 2 or not 1 <= x.size(1) <= 4:
-            raise RuntimeError(f"row_prod: x must be [N, M] with 1 <= M <= 4, got {tuple(x.shape)}")
+        if x.dim() != 2 or not 1 <= x.size(1) <= 3:
+            raise RuntimeError(f"row_prod: x must be [N, M] with 1 <= M <= 3, got {tuple(x.shape)}")
         xc = x.detach().contiguous()
         n, m = int(xc.size(0)), int(xc.size(1))
         prod = torch.empty(n, dtype=torch.float32, device=x.device)
@@ -85,6 +85,6 @@ class _RowProd(torch.autograd.Function):
 
 
 def row_prod(x: torch.Tensor) -> torch.Tensor:
-    """x.prod(dim=1) for [N, M <= 4] float32 device tensors (the scale regulariser lambda_scale *
+    """x.prod(dim=1) for [N, M <= 3] float32 device tensors (the scale regulariser lambda_scale *
     get_scaling.prod(dim=1).mean(), gaussian_trainer.py:405-408), bit-identical to torch's values and gradients."""
     return _RowProd.apply(x)

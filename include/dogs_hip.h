@@ -138,8 +138,8 @@ int dg_clamp_l1_forward(uint32_t n, const float* img, const float* gt, float* cl
 int dg_clamp_l1_backward(uint32_t n, const float* img, const float* clamped, const float* gt, const float* g_clamped,
                          const float* g_l1, float* d_img, dg_stream_t stream);
 
-/* torch.prod(x, dim=1) of x [N, M], 1 <= M <= 4 -- the scale regulariser lambda_scale * get_scaling.prod(dim=1).mean()
- * (gaussian_trainer.py:405-408) -- in torch's row order ((x0 x1) x2) x3, and *any_zero (device word, zeroed here) = 1
+/* torch.prod(x, dim=1) of x [N, M], 1 <= M <= 3 -- the scale regulariser lambda_scale * get_scaling.prod(dim=1).mean()
+ * (gaussian_trainer.py:405-408) -- in torch's row order (x0 x2) x1 on the GPU, and *any_zero (device word, zeroed here) = 1
  * when some element is 0.  The backward is torch's prod_backward (FunctionsManual.cpp) with the zero test on the device
  * instead of a host read: dx = dprod (prod / x) when *any_zero == 0, else for every row dprod (exclusive left cumprod x
  * exclusive right cumprod). */

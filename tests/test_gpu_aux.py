@@ -188,7 +188,7 @@ def test_count_mode_matches_oracle(oracle, hip_device, prefix):
     np.testing.assert_allclose(score.cpu().numpy()[same], score_o[same], rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("M", [1, 2, 3])
 def test_row_prod_matches_torch_prod(hip_device, M):
     """dogs_amd.loss.row_prod (the scale regulariser's prod(dim=1) without prod_backward's host read) is bit-identical
     to torch.prod(x, 1) and its autograd gradient, on a wide value range, and with zeros (torch then takes its zero-safe
