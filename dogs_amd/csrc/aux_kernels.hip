@@ -65,6 +65,29 @@ __device__ __forceinline__ float hconv11(float x) {
 #endif
 }
 
+// Q window sums at once with their Horner chains interleaved step by step: a DPP read of a VGPR needs two wait
+// states after the VALU write of it, and one chain alone puts an s_nop before almost every v_add_f32_dpp (503 of 508
+// in the forward); with Q >= 3 chains the other chains' adds fill them.  Same arithmetic per sum as hconv11.
+template <int Q>
+__device__ __forceinline__ void hconv11_n(const float (&x)[Q], float (&out)[Q]) {
+#if defined(DG_SSIM_TAPFMA) || defined(DG_SSIM_CHAIN1)  // A/B: one sum at a time
+#pragma unroll
+    for (int q = 0; q < Q; q++) out[q] = hconv11(x[q]);
+#else
+    float t[Q][6];
+#pragma unroll
+    for (int q = 0; q < Q; q++)
+#pragma unroll
+        for (int k = 0; k < 6; k++) t[q][k] = GW[k] * x[q];
+#pragma unroll
+    for (int q = 0; q < Q; q++) out[q] = t[q][0];
+#pragma unroll
+    for (int k = 9; k >= 0; k--)
+#pragma unroll
+        for (int q = 0; q < Q; q++) out[q] = wave_shl1_add(out[q], t[q][k <= 5 ? k : 10 - k]);
+#endif
+}
+
 struct StripPos { int x, y0, plane; bool valid; };
 __device__ __forceinline__ StripPos strip_of(int H, int W, int planes, uint32_t skip_blocks = 0) {
     const int sxn = (W + SSW_OUT - 1) / SSW_OUT, syn = (H + SSW_ROWS - 1) / SSW_ROWS;
@@ -149,11 +172,10 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
                         }
                     }
                 }
-                ring[j][0] = hconv11(u);
-                ring[j][1] = hconv11(u * u);
-                ring[j][2] = hconv11(v);
-                ring[j][3] = hconv11(v * v);
-                ring[j][4] = hconv11(u * v);
+                {
+                    const float xs[5] = {u, u * u, v, v * v, u * v};
+                    hconv11_n<5>(xs, ring[j]);
+                }
                 const int y = sp.y0 + rr - 10;
                 if (rr >= 10 && y < H) {
                     float m[5] = {0, 0, 0, 0, 0};
@@ -289,9 +311,10 @@ __global__ void __launch_bounds__(256) k_ssim_bwd_strip(int H, int W, int planes
                     q2[p] = q2[p + 1];
                 }
                 ld3(sp.y0 - 5 + rr + SSIM_PF, q0[SSIM_PF - 1], q1[SSIM_PF - 1], q2[SSIM_PF - 1]);
-                ring[j][0] = hconv11(s0);
-                ring[j][1] = hconv11(s1);
-                ring[j][2] = hconv11(s2);
+                {
+                    const float xs[3] = {s0, s1, s2};
+                    hconv11_n<3>(xs, ring[j]);
+                }
                 const int y = sp.y0 + rr - 10;
                 if (rr >= 10 && y < H) {
                     float v0 = 0, v1 = 0, v2 = 0;
