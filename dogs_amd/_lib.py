@@ -5,6 +5,7 @@ library is missing or a tensor is not on a HIP device, calls raise.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 import threading
@@ -275,7 +276,21 @@ def require_f32_on(device: torch.device, **tensors: torch.Tensor) -> None:
 
 
 def stream_of(device: torch.device):
-    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """The raw HIP stream torch's current stream on `device` wraps (torch.cuda.current_stream(device).cuda_stream
+    without building the Stream object: ~0.3 us instead of ~5 us, and a training step calls this about ten times)."""
+    idx = device.index if device.index is not None else torch._C._cuda_getDevice()
+    return C.c_void_p(torch._C._cuda_getCurrentRawStream(idx))
+
+
+_SAME_DEVICE = contextlib.nullcontext()
+
+
+def device_ctx(device: torch.device):
+    """torch.cuda.device(device), or a no-op when it is already the current device (the usual case: entering and
+    leaving the context costs a few us per call)."""
+    if device.index is None or device.index == torch._C._cuda_getDevice():
+        return _SAME_DEVICE
+    return torch.cuda.device(device)
 
 
 def _bucket(n: int) -> int:

@@ -26,7 +26,7 @@ class _Activate(torch.autograd.Function):
         if rs.shape != (n, 3) or rq.shape != (n, 4) or ro.numel() != n:
             raise RuntimeError(f"activate: shapes {tuple(ro.shape)}, {tuple(rs.shape)}, {tuple(rq.shape)}")
         o, sc, q = torch.empty_like(ro), torch.empty_like(rs), torch.empty_like(rq)
-        with torch.cuda.device(ro.device):
+        with _lib.device_ctx(ro.device):
             _lib.check(_lib.load().dg_activate_forward(n, ro.data_ptr(), rs.data_ptr(), rq.data_ptr(), o.data_ptr(),
                                                        sc.data_ptr(), q.data_ptr(), _lib.stream_of(ro.device)))
         ctx.save_for_backward(o, sc, rq)
@@ -38,7 +38,7 @@ class _Activate(torch.autograd.Function):
         n = int(o.shape[0])
         d_o, d_sc, d_q = torch.empty_like(o), torch.empty_like(sc), torch.empty_like(rq)
         p = lambda t: None if t is None else _c(t).data_ptr()  # noqa: E731
-        with torch.cuda.device(o.device):
+        with _lib.device_ctx(o.device):
             _lib.check(_lib.load().dg_activate_backward(n, o.data_ptr(), sc.data_ptr(), rq.data_ptr(), p(g_o), p(g_sc),
                                                         p(g_q), d_o.data_ptr(), d_sc.data_ptr(), d_q.data_ptr(),
                                                         _lib.stream_of(o.device)))

@@ -73,7 +73,7 @@ def points_in_boxes2d(points, boxes, transform_world_to_obb=None, labels: bool =
     tra = torch.empty((max(n, 1), 2), dtype=torch.float64, device=dev) if transformed else None
     counts = (C.c_uint32 * len(bx))()
     arena = _lib.TensorArena(dev)
-    with torch.cuda.device(dev):
+    with _lib.device_ctx(dev):
         _lib.check(_lib.load().dg_points_in_boxes2d(n, p.data_ptr() if n else None, stride, C.byref(s),
                                                     lab.data_ptr() if lab is not None else None,
                                                     tra.data_ptr() if tra is not None else None, counts,

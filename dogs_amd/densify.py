@@ -47,7 +47,7 @@ def add_densification_stats(model, screen_space_points, update_filter, radii=Non
             raise RuntimeError(f"{n} must be a contiguous float32 tensor (updated in place)")
     st = _lib.DgDensifyStats(r.data_ptr(), dm.data_ptr(), int(dm.stride(0)), mr.data_ptr(),
                              model.xyz_gradient_accum.data_ptr(), model.denom.data_ptr())
-    with torch.cuda.device(vis.device):
+    with _lib.device_ctx(vis.device):
         _lib.check(_lib.load().dg_add_densification_stats(C.byref(st), vis.data_ptr(), N, _lib.stream_of(vis.device)))
 
 
@@ -105,7 +105,7 @@ def densify_and_prune(model, max_grad, min_opacity, extent, max_screen_size, opt
     L = _lib.load()
     arena = _lib.TensorArena(dev)
     s = _lib.stream_of(dev)
-    with torch.cuda.device(dev):
+    with _lib.device_ctx(dev):
         _lib.check(L.dg_densify_select(C.byref(a), arena.fn, None, s))
         ns = int(a.ns)
         samples = None

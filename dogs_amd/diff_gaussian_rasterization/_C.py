@@ -68,7 +68,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                 torch.zeros((0,), dtype=torch.int32, device=dev), torch.empty(0, **u8), torch.empty(0, **u8),
                 torch.empty(0, **u8), torch.empty(0, **u8))
     M = _sh_m(sh)
-    with torch.cuda.device(dev):
+    with _lib.device_ctx(dev):
         out_color = torch.empty((3, H, W), **fopt)
         out_invdepth = torch.empty((1, H, W), **fopt)
         radii = torch.empty((P,), dtype=torch.int32, device=dev)
@@ -103,7 +103,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     if P == 0:
         z = lambda *s: torch.zeros(s, **fopt)  # noqa: E731
         return (z(0, 3), z(0, 3), z(0, 1), z(0, 3), z(0, 6), z(0, 1, 3), z(0, M, 3), z(0, 3), z(0, 4), z(0, 1))
-    with torch.cuda.device(dev):
+    with _lib.device_ctx(dev):
         # one buffer, outputs back to back in the C ABI's order: the library zero-fills it with a single memset
         shapes = [(P, 3), (P, 3), (P, 1), (P, 3), (P, 6), (P, 1, 3), (P, M, 3), (P, 3), (P, 4), (P, 1)]
         sizes = [math.prod(sh) for sh in shapes]
@@ -133,7 +133,7 @@ def mark_visible(means3D, viewmatrix, projmatrix):
     present = torch.zeros((P,), dtype=torch.bool, device=means3D.device)
     if P:
         m, v, p = _f32(means3D), _f32(viewmatrix), _f32(projmatrix)
-        with torch.cuda.device(means3D.device):
+        with _lib.device_ctx(means3D.device):
             _lib.check(_lib.load().dg_mark_visible(P, m.data_ptr(), v.data_ptr(), p.data_ptr(), present.data_ptr(),
                                                    _lib.stream_of(means3D.device)))
     return present
@@ -163,7 +163,7 @@ def count_gaussians(background, means3D, colors, opacity, scales, rotations, sca
         if sh is not None and sh.numel() and sh.dim() == 3 and sh.size(0) == P:
             dc, rest = sh[:, :1, :], sh[:, 1:, :]
         M = _sh_m(rest) if rest is not None else 0
-        with torch.cuda.device(dev):
+        with _lib.device_ctx(dev):
             a, keep = _args(P, degree, M, W, H, background, means3D, colors, opacity, scales, rotations,
                             scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dc, rest, campos,
                             prefiltered, antialiasing, debug)
@@ -189,7 +189,7 @@ def rasterize_gaussians_filter(means3D, scales, rotations, scale_modifier, cov3D
         a, keep = _args(P, 0, 0, image_width, image_height, None, means3D, None, None, scales, rotations,
                         scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, None, None, None,
                         prefiltered, False, debug)
-        with torch.cuda.device(dev):
+        with _lib.device_ctx(dev):
             _lib.check(_lib.load().dg_rasterize_filter(C.byref(a), radii.data_ptr(), _lib.stream_of(dev)))
         del keep
     return radii
@@ -204,7 +204,7 @@ def adamUpdate(param, param_grad, exp_avg, exp_avg_sq, visible, lr, b1, b2, eps,
     vis = visible.contiguous()
     if vis.dtype != torch.bool:
         vis = vis.bool()
-    with torch.cuda.device(param.device):
+    with _lib.device_ctx(param.device):
         _lib.check(_lib.load().dg_adam_update(param.data_ptr(), param_grad.data_ptr(), exp_avg.data_ptr(),
                                               exp_avg_sq.data_ptr(), vis.data_ptr(), float(lr), float(b1), float(b2),
                                               float(eps), int(N), int(M), _lib.stream_of(param.device)))
@@ -259,7 +259,7 @@ def adam_update_groups(groups, visible, N, b1=0.9, b2=0.999, stats=None, prox=No
                                  stats["grad_accum"].data_ptr(), stats["denom"].data_ptr())
     L = _lib.load()
     parr = (_lib.DgAdamProx * max(1, min(8, len(groups))))() if prox is not None else None
-    with torch.cuda.device(dev):
+    with _lib.device_ctx(dev):
         for c0 in range(0, max(1, len(groups)), 8):
             chunk = groups[c0:c0 + 8]
             for i, (param, grad, m, v, lr, eps) in enumerate(chunk):

@@ -52,7 +52,7 @@ def splat_bytes(model) -> np.ndarray:
     sc, op, q = _f32(model._scaling), _f32(model._opacity), _f32(model._quaternion)
     dc = _f32(model._features_dc)
     arena = _lib.TensorArena(dev)
-    with torch.cuda.device(dev):
+    with _lib.device_ctx(dev):
         _lib.check(_lib.load().dg_splat_pack(n, xyz.data_ptr(), sc.data_ptr(), op.data_ptr(), q.data_ptr(),
                                              dc.data_ptr(), out.data_ptr(), arena.fn, None, _lib.stream_of(dev)))
     return out[:32 * n].cpu().numpy()
@@ -66,7 +66,7 @@ def ply_bytes(model) -> np.ndarray:
     n = int(xyz.shape[0])
     dc = _f32(model._features_dc)
     out = torch.empty(max(27 * n, 1), dtype=torch.uint8, device=dev)
-    with torch.cuda.device(dev):
+    with _lib.device_ctx(dev):
         _lib.check(_lib.load().dg_ply_pack(n, xyz.data_ptr(), dc.data_ptr(), out.data_ptr(), _lib.stream_of(dev)))
     return out[:27 * n].cpu().numpy()
 

@@ -21,7 +21,7 @@ def fusedssim(C1, C2, img1, img2, train=True):
         d1, d2, d3 = torch.empty_like(a), torch.empty_like(a), torch.empty_like(a)
     else:
         d1 = d2 = d3 = torch.empty(0, device=dev)
-    with torch.cuda.device(dev):
+    with _lib.device_ctx(dev):
         _lib.check(_lib.load().dg_fused_ssim_forward(B, CH, H, W, float(C1), float(C2), a.data_ptr(), b.data_ptr(),
                                                      ssim_map.data_ptr(), _lib.ptr(d1), _lib.ptr(d2), _lib.ptr(d3),
                                                      _lib.stream_of(dev)))
@@ -36,7 +36,7 @@ def fusedssim_backward(C1, C2, img1, img2, dL_dmap, dm_dmu1, dm_dsigma1_sq, dm_d
     B, CH, H, W = (int(x) for x in a.shape)
     dev = a.device
     out = torch.empty_like(a)
-    with torch.cuda.device(dev):
+    with _lib.device_ctx(dev):
         _lib.check(_lib.load().dg_fused_ssim_backward(B, CH, H, W, float(C1), float(C2), a.data_ptr(), b.data_ptr(),
                                                       g.data_ptr(), _c(dm_dmu1).data_ptr(),
                                                       _c(dm_dsigma1_sq).data_ptr(), _c(dm_dsigma12).data_ptr(),

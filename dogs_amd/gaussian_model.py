@@ -270,7 +270,7 @@ def _compact(model, mask: torch.Tensor, optimizer) -> int:
     L = _lib.load()
     arena = _lib.TensorArena(dev)
     s = _lib.stream_of(dev)
-    with torch.cuda.device(dev):
+    with _lib.device_ctx(dev):
         _lib.check(L.dg_prune_select(C.byref(a), pm.data_ptr(), arena.fn, None, s))
         n_out = int(a.n_out)
         outs, out_m, out_v = [], [], []

@@ -90,7 +90,7 @@ class ImageReader:
         H, W, Cin = h.value, w.value, c.value
         composite = int(self.num_channels == 4 and Cin == 4)
         out = torch.empty((3 if composite else Cin, H, W), dtype=torch.float32, device=self.device)
-        with torch.cuda.device(self.device):
+        with _lib.device_ctx(self.device):
             rc = self._L.dg_ring_upload(self._ring, slot.value, H, W, Cin, composite, self._staging.data_ptr(),
                                         out.data_ptr(), _lib.stream_of(self.device))
         if rc:
@@ -127,7 +127,7 @@ def read_image(image_path: str, num_channels: int = 3, device=None) -> torch.Ten
     Cin = u8.shape[2] if u8.dim() == 3 else 1
     composite = int(num_channels == 4 and Cin == 4)
     out = torch.empty((3 if composite else Cin, H, W), dtype=torch.float32, device=dev)
-    with torch.cuda.device(dev):
+    with _lib.device_ctx(dev):
         _lib.check(_lib.load().dg_image_u8_to_chw(u8.data_ptr(), H, W, Cin, composite, out.data_ptr(),
                                                   _lib.stream_of(dev)))
     return out.permute(1, 2, 0)

@@ -25,7 +25,7 @@ class _ClampL1(torch.autograd.Function):
         nb = int(L.dg_clamp_l1_blocks(n))
         partial = (torch.empty(nb, dtype=torch.float32, device=x.device) if nb else
                    torch.zeros(1, dtype=torch.float32, device=x.device))   # empty image: 0 / 0 = nan, as torch's mean
-        with torch.cuda.device(x.device):
+        with _lib.device_ctx(x.device):
             _lib.check(L.dg_clamp_l1_forward(n, x.data_ptr(), g.data_ptr(), out.data_ptr(), partial.data_ptr(),
                                              _lib.stream_of(x.device)))
         l1 = partial.sum() / n
@@ -38,7 +38,7 @@ class _ClampL1(torch.autograd.Function):
         d = torch.empty_like(x)
         go = None if g_out is None else g_out.contiguous()
         gl = None if g_l1 is None else g_l1.reshape(1).to(torch.float32).contiguous()
-        with torch.cuda.device(x.device):
+        with _lib.device_ctx(x.device):
             _lib.check(_lib.load().dg_clamp_l1_backward(x.numel(), x.data_ptr(), out.data_ptr(), g.data_ptr(),
                                                         None if go is None else go.data_ptr(),
                                                         None if gl is None else gl.data_ptr(), d.data_ptr(),
@@ -66,7 +66,7 @@ class _RowProd(torch.autograd.Function):
         n, m = int(xc.size(0)), int(xc.size(1))
         prod = torch.empty(n, dtype=torch.float32, device=x.device)
         flag = torch.empty(1, dtype=torch.int32, device=x.device)
-        with torch.cuda.device(x.device):
+        with _lib.device_ctx(x.device):
             _lib.check(_lib.load().dg_row_prod_forward(n, m, xc.data_ptr(), prod.data_ptr(), flag.data_ptr(),
                                                        _lib.stream_of(x.device)))
         ctx.save_for_backward(xc, prod, flag)
@@ -78,7 +78,7 @@ class _RowProd(torch.autograd.Function):
         n, m = int(xc.size(0)), int(xc.size(1))
         gc = g.contiguous()
         dx = torch.empty_like(xc)
-        with torch.cuda.device(xc.device):
+        with _lib.device_ctx(xc.device):
             _lib.check(_lib.load().dg_row_prod_backward(n, m, xc.data_ptr(), prod.data_ptr(), gc.data_ptr(),
                                                         flag.data_ptr(), dx.data_ptr(), _lib.stream_of(xc.device)))
         return dx

@@ -14,7 +14,7 @@ def distCUDA2(points: torch.Tensor) -> torch.Tensor:  # noqa: N802
     out = torch.zeros((P,), dtype=torch.float32, device=p.device)
     if P == 0:
         return out
-    with torch.cuda.device(p.device):
+    with _lib.device_ctx(p.device):
         arena = _lib.TensorArena(p.device)
         _lib.check(_lib.load().dg_dist_cuda2(P, p.data_ptr(), out.data_ptr(), arena.fn, None,
                                              _lib.stream_of(p.device)))
