@@ -130,3 +130,18 @@ def test_ctypes_structs_match_the_header(tmp_path):
         assert int(got[s]) == C.sizeof(cls), s
         for f in fields:
             assert int(got[f"{s}.{f}"]) == getattr(cls, f).offset, f"{s}.{f}"
+
+
+def test_tensor_arena_bucket_sizes():
+    """TensorArena rounds per-view buffer requests up (caching-allocator reuse): at most 12.5% more above 1 MiB,
+    exact below, monotone, and a multiple of an eighth of the request's power of two."""
+    from dogs_amd._lib import _bucket
+    prev = 0
+    for n in [1, 17, 4096, 1 << 20, (1 << 20) + 1, 3_000_000, 50_000_123, 123_456_789, (1 << 31) + 5]:
+        b = _bucket(n)
+        assert b >= n and b >= prev
+        prev = b
+        if n <= 1 << 20:
+            assert b == n
+        else:
+            assert b <= n * 1.125 and b % (1 << (n.bit_length() - 4)) == 0
