@@ -506,7 +506,14 @@ __global__ void __launch_bounds__(256) k_tile_dsort_long(DSortArgs a) {
 // view has a handful of such lists, so this replaces a 2040-block launch that mostly exits plus a 256-block
 // grid-stride launch: the same two sort routines, so the same order.
 constexpr int DSM_TILES = 64;
-__global__ void __launch_bounds__(256) k_tile_dsort_merged(DSortArgs a) {
+#ifndef DG_DSORT_DENSE_SPLIT
+#define DG_DSORT_DENSE_SPLIT 1
+#endif
+constexpr bool DSORT_DENSE_SPLIT = DG_DSORT_DENSE_SPLIT;
+// tiles per block (4 = one per wave .. DSM_TILES): the host picks 4 when the phase-1 capacity per tile makes most lists
+// longer than the render's wave capacity (5e6 Gaussians at 1080p: ~1500 rect units per tile), where 16 sorts in a row
+// per wave over 128 blocks took ~500 us per view against ~125 with a wave per tile
+__global__ void __launch_bounds__(256) k_tile_dsort_merged(DSortArgs a, int tpb) {
     __shared__ uint32_t s_cnt[4][RS_RADIX];
     __shared__ uint32_t s_k[4][DS_WAVE_MAX2];
     __shared__ uint32_t s_v[4][DS_WAVE_MAX2];
@@ -517,8 +524,8 @@ __global__ void __launch_bounds__(256) k_tile_dsort_merged(DSortArgs a) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (threadIdx.x == 0) s_nq = 0u;
     __syncthreads();
-    const int t0 = blockIdx.x * DSM_TILES + w * (DSM_TILES / 4);
-    for (int i = 0; i < DSM_TILES / 4; i++) {
+    const int t0 = blockIdx.x * tpb + w * (tpb / 4);
+    for (int i = 0; i < tpb / 4; i++) {
         const int tile = t0 + i;
         if (tile >= a.num_tiles) break;
         const int n = wave_sort_tile<DS_ROWS2>(a, tile, lane, s_cnt[w], s_k[w], s_v[w], nullptr, DS_WAVE_MAX);
@@ -538,7 +545,17 @@ void tile_depth_sort_long_only(const DSortArgs& a, hipStream_t stream) {
     k_tile_dsort<DS_WAVE_MAX><<<(a.num_tiles + 3) / 4, 256, 0, stream>>>(a);
     k_tile_dsort_long<<<256, 256, 0, stream>>>(a);
 #else
-    k_tile_dsort_merged<<<(a.num_tiles + DSM_TILES - 1) / DSM_TILES, 256, 0, stream>>>(a);
+    // dense lists (rect units per tile past 1.5x the wave capacity; ~0.57 precise instances per rect unit): a wave per
+    // tile, and the lists past a wave's reach queued for a grid of block sorts -- many of them at 5e6 Gaussians, where
+    // a block's own queue (up to four lists in a row) left the launch waiting on its slowest blocks
+    const bool dense = (uint64_t)a.n_inst > (uint64_t)a.num_tiles * (uint64_t)(DS_WAVE_MAX * 3 / 2);
+    if (dense && DSORT_DENSE_SPLIT) {
+        k_tile_dsort<DS_WAVE_MAX><<<(a.num_tiles + 3) / 4, 256, 0, stream>>>(a);
+        k_tile_dsort_long<<<1024, 256, 0, stream>>>(a);
+        return;
+    }
+    const int tpb = dense ? 4 : DSM_TILES;
+    k_tile_dsort_merged<<<(a.num_tiles + tpb - 1) / tpb, 256, 0, stream>>>(a, tpb);
 #endif
 }
 
