@@ -35,7 +35,10 @@ void tile_offsets(uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges, hipStre
 // Both scans of a binning phase in one launch of two single-block scans: wtot[0..n) -> exclusive prefix in place
 // (*total = sum) and tile_offsets() above.  For n <= BIN_OFFSETS_MAX_N (longer wave-total arrays take
 // exclusive_scan + tile_offsets).  gate as above (*total = 0 when gated).
-constexpr uint32_t BIN_OFFSETS_MAX_N = 65536;
+#ifndef DG_BIN_OFFSETS_MAX_N
+#define DG_BIN_OFFSETS_MAX_N 65536
+#endif
+constexpr uint32_t BIN_OFFSETS_MAX_N = DG_BIN_OFFSETS_MAX_N;
 void bin_offsets(uint32_t* wtot, uint32_t n, uint32_t* total, uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges,
                  hipStream_t stream, const uint32_t* gate = nullptr, bool small_blocks = false);
 
