@@ -225,6 +225,40 @@ def fusedssim_backward(C1, C2, img1, img2, dL_dmap):
     return _cuda.fusedssim_backward(C1, C2, a, b, dL_dmap.unsqueeze(0), d1, d2, d3)[0]
 
 
+def _check_group(param, grad, m, v):
+    for t, n in ((param, "param"), (grad, "grad"), (m, "exp_avg"), (v, "exp_avg_sq")):
+        _lib.require_device(t, n)
+        if not t.is_contiguous() or t.dtype != torch.float32:
+            raise RuntimeError(f"{n} must be a contiguous float32 tensor")
+
+
+# The group table of the last few group sets (a training loop passes the same parameters, moments and -- from the
+# caching allocator -- usually the same gradient addresses every step): building and checking it was ~90 us of host
+# per step, more than the launch.  Keyed by every pointer, shape and hyper-parameter it holds; contiguity is checked
+# on every call (a view can share a pointer), dtype and device when the table is built.
+_GROUP_TABLES: dict = {}
+
+
+def _group_array(chunk, N):
+    key = (int(N),) + tuple((p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), g.numel(), m.numel(),
+                             v.numel(), float(lr), float(eps)) for p, g, m, v, lr, eps in chunk)
+    arr = _GROUP_TABLES.get(key)
+    if arr is not None:
+        for p, g, m, v, _, _ in chunk:
+            if not (p.is_contiguous() and g.is_contiguous() and m.is_contiguous() and v.is_contiguous()):
+                _check_group(p, g, m, v)  # raises with the tensor's name
+        return arr
+    arr = (_lib.DgAdamGroup * max(1, len(chunk)))()
+    for i, (param, grad, m, v, lr, eps) in enumerate(chunk):
+        _check_group(param, grad, m, v)
+        arr[i] = _lib.DgAdamGroup(param.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(), float(lr),
+                                  float(eps), int(param.numel() // N) if N else 0)
+    if len(_GROUP_TABLES) >= 16:
+        _GROUP_TABLES.clear()
+    _GROUP_TABLES[key] = arr
+    return arr
+
+
 def adam_update_groups(groups, visible, N, b1=0.9, b2=0.999, stats=None, prox=None):
     """SparseGaussianAdam over several groups in one launch (dg_adam_update_groups; each group as adamUpdate).
     groups: iterable of (param, grad, exp_avg, exp_avg_sq, lr, eps); stats (optional): dict with radii [N] int32,
@@ -262,14 +296,13 @@ def adam_update_groups(groups, visible, N, b1=0.9, b2=0.999, stats=None, prox=No
     with _lib.device_ctx(dev):
         for c0 in range(0, max(1, len(groups)), 8):
             chunk = groups[c0:c0 + 8]
-            for i, (param, grad, m, v, lr, eps) in enumerate(chunk):
-                for t, n in ((param, "param"), (grad, "grad"), (m, "exp_avg"), (v, "exp_avg_sq")):
-                    _lib.require_device(t, n)
-                    if not t.is_contiguous() or t.dtype != torch.float32:
-                        raise RuntimeError(f"{n} must be a contiguous float32 tensor")
-                arr[i] = _lib.DgAdamGroup(param.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(), float(lr),
-                                          float(eps), int(param.numel() // N) if N else 0)
-                if parr is not None:
+            if parr is None:
+                arr = _group_array(chunk, N)
+            else:
+                for i, (param, grad, m, v, lr, eps) in enumerate(chunk):
+                    _check_group(param, grad, m, v)
+                    arr[i] = _lib.DgAdamGroup(param.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(),
+                                              float(lr), float(eps), int(param.numel() // N) if N else 0)
                     pe = prox[c0 + i]
                     if pe is None:
                         parr[i] = _lib.DgAdamProx(None, None, 0.0)
