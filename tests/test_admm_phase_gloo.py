@@ -1,5 +1,6 @@
 """The ADMM phase entry (dogs_amd.admm_phase: fuse_local_gaussians without the RPC master,
-master_gaussian_trainer.py:37-172, 557-618) over torch.distributed (gloo, world size 2 and 4, CPU).
+master_gaussian_trainer.py:37-172, 557-618) over torch.distributed (gloo, world size 2, 3 and 4, CPU; at world 3
+the middle block has no cameras).
 
 The device operations (count renders, box membership, prune compaction) are replaced by CPU restatements
 (`CPUKernels`), so this checks the distributed plumbing and the lifecycle order:
@@ -27,6 +28,7 @@ T = np.array([[0.8, -0.6, 0.3], [0.6, 0.8, -0.2], [0.0, 0.0, 1.0]])   # world ->
 GRIDS = {
     2: [(-5.0, -5.0, 0.0, 5.0), (0.0, -5.0, 5.0, 5.0)],
     4: [(-5.0, -5.0, 0.0, 0.0), (0.0, -5.0, 5.0, 0.0), (-5.0, 0.0, 0.0, 5.0), (0.0, 0.0, 5.0, 5.0)],
+    3: [(-6.0, -5.0, -2.0, 5.0), (-2.0, -5.0, 2.0, 5.0), (2.0, -5.0, 6.0, 5.0)],   # block 1 has no cameras
 }
 
 
@@ -38,7 +40,9 @@ def _boxes(world):
 
 def _cameras(world):
     g = torch.Generator().manual_seed(3)
-    return [[torch.randn(3, generator=g) * 3.0 for _ in range(3 + (b % 2))] for b in range(world)]
+    # world 3: the middle block has no cameras (its rank folds nothing onto the importance chain and passes it on)
+    return [[torch.randn(3, generator=g) * 3.0 for _ in range(0 if (world == 3 and b == 1) else 3 + (b % 2))]
+            for b in range(world)]
 
 
 def _block_model(b, world):
@@ -151,12 +155,12 @@ def _worker(rank, world, port):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_phase_entry_gloo_matches_single_process(world):
     mp.spawn(_worker, args=(world, _free_port()), nprocs=world, join=True)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_single_process_entry_matches_reference_steps(world):
     from dogs_amd.admm_phase import PhaseConfig
     cfg = PhaseConfig(prune_percent=0.5, v_pow=0.1)
