@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round 4 final evidence of the committed tree: the whole -m gpu suite + smoke + default bench (tools/gpu_suite.sh),
+# Evidence of the committed tree: the whole -m gpu suite + smoke + default bench (tools/gpu_suite.sh),
 # then the kernel-trace stats of the bench workload (tools/profile.sh, no counters).
 set -e
-OUT=${1:-gpurun_out/r4final}
+OUT=${1:-gpurun_out/evidence}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 bash tools/gpu_suite.sh "$OUT"
