@@ -278,8 +278,13 @@ def require_f32_on(device: torch.device, **tensors: torch.Tensor) -> None:
 def stream_of(device: torch.device):
     """The raw HIP stream torch's current stream on `device` wraps (torch.cuda.current_stream(device).cuda_stream
     without building the Stream object: ~0.3 us instead of ~5 us, and a training step calls this about ten times)."""
+    if _RAW_STREAM is None:  # a torch without the private accessor
+        return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
     idx = device.index if device.index is not None else torch._C._cuda_getDevice()
-    return C.c_void_p(torch._C._cuda_getCurrentRawStream(idx))
+    return C.c_void_p(_RAW_STREAM(idx))
+
+
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
 _SAME_DEVICE = contextlib.nullcontext()
@@ -288,7 +293,7 @@ _SAME_DEVICE = contextlib.nullcontext()
 def device_ctx(device: torch.device):
     """torch.cuda.device(device), or a no-op when it is already the current device (the usual case: entering and
     leaving the context costs a few us per call)."""
-    if device.index is None or device.index == torch._C._cuda_getDevice():
+    if device.index is None or device.index == torch.cuda.current_device():
         return _SAME_DEVICE
     return torch.cuda.device(device)
 
