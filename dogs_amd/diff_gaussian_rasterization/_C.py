@@ -234,19 +234,22 @@ def _check_group(param, grad, m, v):
 
 # The group table of the last few group sets (a training loop passes the same parameters, moments and -- from the
 # caching allocator -- usually the same gradient addresses every step): building and checking it was ~90 us of host
-# per step, more than the launch.  Keyed by every pointer, shape and hyper-parameter it holds; contiguity is checked
-# on every call (a view can share a pointer), dtype and device when the table is built.
+# per step, more than the launch.  Keyed by every pointer and size it holds (the learning rate and eps are rewritten on
+# every call: the xyz rate follows its schedule); contiguity is checked on every call (a view can share a pointer),
+# dtype and device when the table is built.
 _GROUP_TABLES: dict = {}
 
 
 def _group_array(chunk, N):
     key = (int(N),) + tuple((p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), g.numel(), m.numel(),
-                             v.numel(), float(lr), float(eps)) for p, g, m, v, lr, eps in chunk)
+                             v.numel()) for p, g, m, v, _, _ in chunk)
     arr = _GROUP_TABLES.get(key)
     if arr is not None:
-        for p, g, m, v, _, _ in chunk:
+        for i, (p, g, m, v, lr, eps) in enumerate(chunk):
             if not (p.is_contiguous() and g.is_contiguous() and m.is_contiguous() and v.is_contiguous()):
                 _check_group(p, g, m, v)  # raises with the tensor's name
+            arr[i].lr = float(lr)         # the learning rates follow their schedules step by step
+            arr[i].eps = float(eps)
         return arr
     arr = (_lib.DgAdamGroup * max(1, len(chunk)))()
     for i, (param, grad, m, v, lr, eps) in enumerate(chunk):
