@@ -425,6 +425,58 @@ def admm_leg(args, ws, rank, dev, n, W, H):
     return out
 
 
+SWEEP = (  # (name, N, W, H, raw-opacity mean): north_star's other N, the 4K config, and a non-saturating scene
+    ("1e5@1080p", 100_000, 1920, 1080, 0.0),
+    ("5e6@1080p", 5_000_000, 1920, 1080, 0.0),
+    ("1e6@4K", 1_000_000, 3840, 2160, 0.0),
+    ("1e6@1080p-sparse", 1_000_000, 1920, 1080, -2.0),
+)
+
+
+def sweep_leg(dev, yaws, seed, steps=16, warmup=8, only=None):
+    """After the headline: the same fwd+bwd view step (same yaw batch, cold adaptive capacity, warm-up, barrier-free
+    single-rank timing) on the other workloads of SURVEY.md §8(d) / north_star -- N in {1e5, 5e6} at 1080p, 1e6 at
+    3840x2160 -- and on a non-saturating variant of the 1080p / 1e6 scene (raw opacity ~ N(-2, 1.5): far fewer tiles
+    saturate before their lists end, so most of the work is phase 2 and the depth prefix saves little).  Per entry:
+    views/s, ms/view, mean E1 / E2 / unfinished tiles / K (the reference's precise instances) and the reference-
+    equivalent view fraction (856 N + 172 K + 64 HW per view over 8 TB/s)."""
+    import gc
+    import dogs_amd._lib as L
+    from dogs_amd.synthetic import make_scene
+    out = {}
+    for name, n, W, H, om in SWEEP:
+        if only is not None and name not in only:
+            continue
+        s = make_scene(n, W, H, seed=seed, opacity_mean=om).to(dev)
+        cams = make_cameras(W, H, yaws, dev)
+        g = torch.Generator().manual_seed(seed + 99)
+        v = Views(s, cams, torch.randn((3, H, W), generator=g).to(dev), torch.zeros((1, H, W), device=dev), dev)
+        with torch.cuda.device(dev):
+            L.adaptive_capacity(W, H, reset=True)
+        for _ in range(warmup):
+            v.step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            v.step()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        st = [v.stats(k) for k in range(len(yaws))]
+        K = float(np.mean([r["K"] for r in st]))
+        ref_b = reference_view_bytes(n, int(K), W * H)
+        out[name] = {"N": n, "width": W, "height": H, "raw_opacity_mean": om,
+                     "views_per_s": round(1e3 / ms, 2), "ms_per_view": round(ms, 4),
+                     "e1_mean": round(float(np.mean([r["e1"] for r in st]))),
+                     "e2_mean": round(float(np.mean([r["e2"] for r in st]))),
+                     "unfinished_tiles_mean": round(float(np.mean([r["unfinished_tiles"] for r in st])), 1),
+                     "K_mean": round(K), "tiles": ((W + 15) // 16) * ((H + 15) // 16),
+                     "reference_equivalent_view_frac": round(ref_b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        del v, s, cams, st
+        gc.collect()
+        torch.cuda.empty_cache()
+    return out
+
+
 def max_over(ws: int, dev, x: float) -> float:
     if ws == 1:
         return x
@@ -465,6 +517,8 @@ def main():
     ap.add_argument("--launch-check", action="store_true",
                     help="plumbing check, no GPU: every rank joins a gloo group, all_reduces its rank and rank 0 "
                          "prints the world it saw (tests/test_bench_launch.py)")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the other workloads (1e5, 5e6, 4K, sparse scene)")
+    ap.add_argument("--sweep-only", default=None, help="comma-separated subset of the sweep's workload names")
     ap.add_argument("--no-reference-k", action="store_true",
                     help="skip the untimed depth-prefix-off forwards (profiling runs: keeps kernel averages clean)")
     args = ap.parse_args()
@@ -671,6 +725,10 @@ def main():
                             "routes_ms": route_ms},
                  "densify_and_prune_ms": round(dms, 3), "gaussians_after_densify": n_after}
 
+    sweep = None
+    if not args.no_sweep and ws == 1:
+        sweep = sweep_leg(dev, yaws, seed, only=args.sweep_only.split(",") if args.sweep_only else None)
+
     admm = None
     if not args.no_admm:
         del views
@@ -712,6 +770,7 @@ def main():
                            "between phases serialise the queue, so their sum exceeds ms_per_step)",
             "cpu_baseline": cpu,
             "train_step": train,
+            "sweep": sweep,
             "admm": admm,
         }
         print(json.dumps(line))

@@ -6,10 +6,16 @@ ADMM state of the slave (slave_gaussian_trainer.py:100-202) with collectives bet
 
 * Gaussians that live in exactly one block have z = x_k and a dual that never moves, so only the
   *shared* set (visibility_count >= 2) is exchanged.  Each rank packs its shared rows of the six raw
-  parameter tensors (59 floats per Gaussian) into one [N_shared, 59] buffer, ONE all_reduce(SUM)
-  over RCCL/xGMI, multiply by the precomputed 1/count, unpack z_k.
-* Primal/dual residuals are per-rank partial sums + one all_reduce of 12 scalars; every shared
-  Gaussian is owned (counted once) by the lowest rank that holds it.
+  parameter tensors (59 floats per Gaussian) into one [N_shared, 59] buffer (zeros where it holds no
+  copy).  The sum is an all-reduce built from two collectives so that its order is the reference
+  master's: all_to_all hands rank r every rank's copy of row slice r, rank r adds them in block order
+  onto zeros and divides by the count (reinitialize + plus_gaussians per block + average_gaussians,
+  gaussian_splat_model.py:316-340, master_gaussian_trainer.py:538-555), all_gather returns the
+  slices.  Same bytes on the wire as a ring all_reduce ((W-1)/W of the buffer each way, twice), and the
+  result is bit-identical to the reference's arithmetic and to the sequential baseline for every
+  count, not only where the sum has two terms.
+* Primal/dual residuals are per-rank partial sums, gathered (12 scalars per rank) and added in rank
+  order; every shared Gaussian is owned (counted once) by the lowest rank that holds it.
 * Penalty adaptation (master_gaussian_trainer.py:337-377) is deterministic given the residuals, so
   every rank applies it locally -- no broadcast.
 """
@@ -77,7 +83,8 @@ class BlockConsensus:
         loc_mask = shared[gidx]
         self.loc = torch.nonzero(loc_mask).squeeze(-1)                    # local rows of shared Gaussians
         self.sid = sid_of[gidx[self.loc]]                                # their compact shared ids
-        self.inv_count = (1.0 / vc[shared].to(torch.float32)).unsqueeze(-1) if self.num_shared else None
+        # float32 count per shared row: `x /= count` with an int64 count promotes to a float32 division
+        self.count = vc[shared].to(torch.float32).unsqueeze(-1) if self.num_shared else None
         # owner of each shared Gaussian = lowest rank holding it (counts it in the dual residual)
         owner = torch.full((max(self.num_shared, 1),), self.world, dtype=torch.int32, device=self.device)
         if self.num_shared:
@@ -104,8 +111,9 @@ class BlockConsensus:
             buf = torch.zeros((self.num_shared, D), dtype=torch.float32, device=self.device)
             buf[self.sid] = torch.cat([f[self.loc] for f in flats], dim=1)
             if self.world > 1:
-                dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
-            buf.mul_(self.inv_count)
+                buf = ordered_sum_average(buf, self.count, self.world, self.rank, self.group)
+            else:
+                buf = torch.zeros_like(buf).add_(buf).div_(self.count)
             rows = buf[self.sid]
             o = 0
             for zi, w in zip(z, widths):
@@ -130,8 +138,39 @@ class BlockConsensus:
             self._owned_f = self.owned.to(torch.float64).unsqueeze(-1)
         part = residual_parts(params, z, z_prev, self._owned_f)
         if self.world > 1:
-            dist.all_reduce(part, op=dist.ReduceOp.SUM, group=self.group)
+            parts = torch.empty((self.world * part.shape[0],), dtype=part.dtype, device=part.device)
+            dist.all_gather_into_tensor(parts, part, group=self.group)
+            parts = parts.view(self.world, -1)
+            part = torch.zeros_like(part)
+            for k in range(self.world):          # rank order, as the sequential baseline adds its blocks
+                part += parts[k]
         return residual_dicts(part.cpu(), params, z_prev is not None, self.num_global, rho)
+
+
+@torch.no_grad()
+def ordered_sum_average(buf: torch.Tensor, count: torch.Tensor, world: int, rank: int, group=None) -> torch.Tensor:
+    """(sum over ranks of buf, added in rank order onto zeros) / count, on every rank.
+
+    buf is [S, D] (this rank's copies, zeros elsewhere), count [S, 1] float32.  Row slice r of the padded
+    buffer is reduced by rank r: all_to_all delivers the W copies of the slice, they are added in rank
+    order (0 + x_0 + x_1 + ...: the reference master's reinitialize + plus_gaussians loop), divided by the
+    count, and all_gather_into_tensor reassembles the [S, D] result."""
+    S, D = buf.shape
+    chunk = -(-S // world)
+    pad = chunk * world
+    if pad != S:
+        buf = torch.cat([buf, buf.new_zeros((pad - S, D))])
+        count = torch.cat([count, count.new_ones((pad - S, 1))])
+    recv = torch.empty_like(buf)
+    dist.all_to_all_single(recv, buf, group=group)
+    recv = recv.view(world, chunk, D)
+    acc = torch.zeros((chunk, D), dtype=buf.dtype, device=buf.device)
+    for k in range(world):
+        acc += recv[k]
+    acc.div_(count[rank * chunk:(rank + 1) * chunk])
+    out = torch.empty_like(buf)
+    dist.all_gather_into_tensor(out, acc, group=group)
+    return out[:S]
 
 
 @torch.no_grad()

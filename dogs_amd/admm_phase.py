@@ -163,14 +163,21 @@ def fuse_blocks(block_models: list, ori_point_bboxes, world_to_obb_transform, ke
 
 
 def ordered_importance(fused: GaussianSplatModel, camera_blocks: list, kernels: PhaseKernels, bg: torch.Tensor,
-                       group=None) -> torch.Tensor:
+                       group=None, score_budget_bytes: int = 1 << 30) -> torch.Tensor:
     """prune_list's importance over the concatenation of every block's cameras, bit for bit, with each rank rendering
-    only its own block's cameras: the per-camera scores are kept, folded down a chain of ranks in the reference's
-    order (block B-1's last camera first ... block 0's first camera last), and broadcast from rank 0."""
+    only its own block's cameras: the per-camera scores are folded down a chain of ranks in the reference's order
+    (block B-1's last camera first ... block 0's first camera last), and broadcast from rank 0.
+
+    While a rank waits for the partial sum of the ranks after it, it renders its first cameras ahead and keeps their
+    scores -- at most `score_budget_bytes` of them (4 B per fused Gaussian per camera: 200 cameras of a 4e7-Gaussian
+    fused model would be 32 GB) -- then folds them in order and renders the rest straight into the sum.  The last
+    rank starts the chain from zeros and buffers nothing."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     dev = fused.get_xyz.device
     n = fused.num_gaussians
-    own = [kernels.camera_importance(fused, cam, bg).float() for cam in reversed(list(camera_blocks[rank]))]
+    cams = list(reversed(list(camera_blocks[rank])))
+    ahead = 0 if rank == world - 1 else min(len(cams), int(score_budget_bytes) // max(4 * n, 1))
+    own = [kernels.camera_importance(fused, cam, bg).float() for cam in cams[:ahead]]
     host = _gather_device(group)
     wire = host if host is not None else dev
     acc = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -181,6 +188,8 @@ def ordered_importance(fused: GaussianSplatModel, camera_blocks: list, kernels: 
     for sc in own:
         acc += sc
     del own
+    for cam in cams[ahead:]:
+        acc += kernels.camera_importance(fused, cam, bg).float()
     if rank > 0:
         dist.send(acc.to(wire), dst=dist.get_global_rank(group, rank - 1) if group is not None else rank - 1,
                   group=group)

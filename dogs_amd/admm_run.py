@@ -300,9 +300,11 @@ def main(argv=None) -> None:
     p.add_argument("--points", type=int, default=20000)
     p.add_argument("--width", type=int, default=320)
     p.add_argument("--height", type=int, default=240)
-    p.add_argument("--densify-end", type=int, default=200)
-    p.add_argument("--max-iterations", type=int, default=600)
-    p.add_argument("--interval", type=int, default=100)
+    # schedule overrides: applied only when given (with --config the YAML's schedule and prunes stand otherwise);
+    # without --config the defaults are a short synthetic run (densify to 200, 600 iterations, rounds of 100)
+    p.add_argument("--densify-end", type=int, default=None)
+    p.add_argument("--max-iterations", type=int, default=None)
+    p.add_argument("--interval", type=int, default=None)
     p.add_argument("--gloo", action="store_true")
     a = p.parse_args(argv)
     rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
@@ -312,12 +314,21 @@ def main(argv=None) -> None:
     dev = torch.device("cuda", 0 if a.gloo else local)
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo" if a.gloo else "nccl", rank=rank, world_size=world)
-    cfg = ADMMRunConfig.from_reference(a.config) if a.config else ADMMRunConfig()
-    cfg.gs.densify_end_iter, cfg.gs.max_iterations = a.densify_end, a.max_iterations
-    cfg.gs.densify_start_iter = min(cfg.gs.densify_start_iter, a.densify_end // 2)
-    cfg.gs.densification_interval = min(cfg.gs.densification_interval, max(a.densify_end // 4, 1))
-    cfg.gs.prune_iterations = ()
-    cfg.admm.consensus_interval = a.interval
+    cfg = ADMMRunConfig.from_reference(a.config) if a.config else None
+    if cfg is None:
+        cfg = ADMMRunConfig()
+        a.densify_end = 200 if a.densify_end is None else a.densify_end
+        a.max_iterations = 600 if a.max_iterations is None else a.max_iterations
+        a.interval = 100 if a.interval is None else a.interval
+        cfg.gs.prune_iterations = ()
+    if a.densify_end is not None:
+        cfg.gs.densify_end_iter = a.densify_end
+        cfg.gs.densify_start_iter = min(cfg.gs.densify_start_iter, a.densify_end // 2)
+        cfg.gs.densification_interval = min(cfg.gs.densification_interval, max(a.densify_end // 4, 1))
+    if a.max_iterations is not None:
+        cfg.gs.max_iterations = a.max_iterations
+    if a.interval is not None:
+        cfg.admm.consensus_interval = a.interval
     with tempfile.TemporaryDirectory() as tmp:
         views = aerial_views(a.points, 2 * a.mx, 2 * a.my, a.width, a.height)
         scenes = split_scene(views, a.mx, a.my, tmp, dev)

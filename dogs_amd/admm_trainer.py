@@ -304,7 +304,7 @@ class InProcessConsensus:
         shared = cnt >= 2
         sid_of = torch.cumsum(shared.to(torch.int64), 0) - 1
         self.num_shared = int(shared.sum().item())
-        self.inv_count = (1.0 / cnt[shared].to(torch.float32)).unsqueeze(-1) if self.num_shared else None
+        self.count = cnt[shared].to(torch.float32).unsqueeze(-1) if self.num_shared else None
         self.loc, self.sid, self.owned = [], [], []
         owner = torch.full((max(self.num_shared, 1),), len(global_indices), dtype=torch.int32, device=device)
         for b, g in enumerate(global_indices):
@@ -331,7 +331,7 @@ class InProcessConsensus:
             buf = torch.zeros((self.num_shared, sum(widths)), dtype=torch.float32, device=self.device)
             for b, fl in enumerate(flats):
                 buf.index_add_(0, self.sid[b], torch.cat([f[self.loc[b]] for f in fl], dim=1))
-            buf.mul_(self.inv_count)
+            buf.div_(self.count)           # average_gaussians (gaussian_splat_model.py:334-340)
             for b in range(len(flats)):
                 rows = buf[self.sid[b]]
                 o = 0

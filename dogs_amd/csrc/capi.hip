@@ -12,6 +12,7 @@
 #include <tuple>
 #include <chrono>
 #include <mutex>
+#include <atomic>
 #include <thread>
 
 #include "../../include/dogs_hip.h"
@@ -251,8 +252,12 @@ struct HostCountersSlot {
         hc_pool().push_back(h);
     }
 };
-HostCounters& host_counters() {
+HostCountersSlot& host_counters_slot() {
     thread_local HostCountersSlot slot;
+    return slot;
+}
+HostCounters& host_counters() {
+    HostCountersSlot& slot = host_counters_slot();
     if (!slot.h.buf) {
         {
             std::lock_guard<std::mutex> lk(hc_mu());
@@ -516,6 +521,8 @@ namespace {
 struct ActFold {
     const float *raw_o, *raw_s, *raw_q;
     float* part_sc;
+    uint64_t* zero_stamp;         // *zero_stamp = stamp when some activated scaling is 0 (the regulariser's backward)
+    uint64_t stamp;
     hipEvent_t wait_before_emit;  // optional: the previous step's overlapped SH update (the emission reads the SH)
     bool waited;                  // out: the wait was enqueued (a forward that binned nothing leaves it to the caller)
 };
@@ -549,7 +556,10 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     // its per-block parts)
     gs::PreArgs pre;
     fill_pre(pre, a);
-    if (fold) { pre.raw_o = fold->raw_o; pre.raw_s = fold->raw_s; pre.raw_q = fold->raw_q; pre.part_sc = fold->part_sc; }
+    if (fold) {
+        pre.raw_o = fold->raw_o; pre.raw_s = fold->raw_s; pre.raw_q = fold->raw_q; pre.part_sc = fold->part_sc;
+        pre.zero_stamp = fold->zero_stamp; pre.stamp = fold->stamp;
+    }
     pre.radii = radii; pre.sp = g.sp; pre.depthkey = g.dkey; pre.cnt = g.cnt; pre.rcnt = g.rcnt;
     pre.hist = g.hist;
     pre.unf_rows = UNF_ROWS ? reinterpret_cast<unsigned long long*>(im.sat) : nullptr;  // (the SAT block is larger)
@@ -993,9 +1003,10 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
         f[8] = c.take<float>(n_img);       // dm/dsigma1_sq
         f[9] = c.take<float>(n_img);       // dm/dsigma12
         f[10] = c.take<float>(n_img);      // dL/dimage
+        f[16] = reinterpret_cast<float*>(c.take<uint64_t>(1));  // the step's zero-scaling stamp
         return c.off;
     };
-    float* f[16];
+    float* f[17];
     const size_t tbytes = carve(nullptr, f);
     void* tbase = alloc(user, DG_BUF_TRAIN, tbytes);
     if (!tbase) return fail("train step scratch allocation failed%s%d");
@@ -1007,6 +1018,12 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     float *dcov3D = dmeans3D + 3 * Pz, *ddc = dcov3D + 6 * Pz, *dsh = ddc + 3 * Pz, *dscales = dsh + 3 * Mz * Pz;
     float* drot = dscales + 3 * Pz;
     float *depth = f[12], *g_o = f[13], *g_s = f[14], *g_q = f[15];
+    // torch's prod backward switches every row to its zero-safe form when any scaling is 0: the activation pass
+    // stores this step's stamp when it meets one, and the update compares (no zeroing launch; a fresh 64-bit stamp
+    // per step never matches stale memory)
+    static std::atomic<uint64_t> step_stamp{0x9e3779b97f4a7c15ull};
+    const uint64_t stamp = step_stamp.fetch_add(1, std::memory_order_relaxed) + 1;
+    uint64_t* const zstamp = reinterpret_cast<uint64_t*>(f[16]);
     const dg_adam_group* G = a->groups;  // xyz, f_dc, f_rest, opacity, scaling, quaternion
     // Default route: the activations' backward is folded into the update (gmode), and the 4-float chunks that touch
     // no binned row (rcnt == 0: rasterizer gradient exactly zero) skip reading the gradient buffers; the regulariser's
@@ -1018,7 +1035,8 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     float* const p_sc_fused = part + 3 * nw_ssim;
     // ---- forward: activations, rasterizer, clamp + L1, SSIM.  Default route: the activations (and the regulariser's
     // partial sums) inside the rasterizer's preprocess launch (ActFold); unfused: their own launch.
-    if (unfused) gs::launch_activate_fwd((uint32_t)P, G[3].param, G[4].param, G[5].param, act_o, act_s, act_q, s);
+    if (unfused)
+        gs::launch_activate_fwd((uint32_t)P, G[3].param, G[4].param, G[5].param, act_o, act_s, act_q, zstamp, stamp, s);
     // the previous step's overlapped SH update: the emission waits for it (the first launch that reads the SH rows)
     ShOverlap* ov = sh_state(s, a->sh_status != nullptr);
     if (a->sh_status && !ov) return fail("train step: no side stream for the overlapped update%s%d");
@@ -1027,7 +1045,7 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
     // `pending` stays set until the stream's wait on the previous update is enqueued: on an early error return below
     // the wait is still enqueued (wait_prev), so dg_train_sync / a later step never lose it
     if (ov && !prev) ov->pending = false;
-    ActFold fold = {G[3].param, G[4].param, G[5].param, a->loss ? p_sc_fused : nullptr, prev, false};
+    ActFold fold = {G[3].param, G[4].param, G[5].param, a->loss ? p_sc_fused : nullptr, zstamp, stamp, prev, false};
     auto wait_prev = [&]() {
         if (prev && !fold.waited) (void)hipStreamWaitEvent(s, prev, 0);
         if (ov) ov->pending = false;
@@ -1076,6 +1094,7 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
             d.gmode = k - 2;  // opacity: sigmoid, scaling: exp + regulariser, quaternion: normalize
             d.act = k == 3 ? act_o : (k == 4 ? act_s : nullptr);
             d.reg = k == 4 ? a->lambda_scale / (float)P : 0.0f;
+            if (k == 4) { d.zero_stamp = zstamp; d.stamp = stamp; }
         }
     }
     m.n = n;
@@ -1116,7 +1135,7 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
         return 1;
     if (unfused)
         gs::launch_activate_bwd((uint32_t)P, act_o, act_s, G[5].param, dopac, dscales, drot, g_o, g_s, g_q, s,
-                                a->lambda_scale / (float)P);
+                                a->lambda_scale / (float)P, zstamp, stamp);
 #ifndef DG_DIAG_NO_ADAM  // timing diagnostic only (no parameter update): what the update costs the next step's forward
     if (a->sh_status) {
         // xyz / opacity / scaling / rotation + statistics + the rows' status snapshot here (the next forward's
@@ -1444,7 +1463,8 @@ int dg_activate_forward(uint32_t N, const float* raw_opacity, const float* raw_s
         return fail("activate: NULL tensor%s%d");
     if ((reinterpret_cast<uintptr_t>(raw_rotation) | reinterpret_cast<uintptr_t>(rotation)) & 15u)
         return fail("activate: rotation rows must be 16-byte aligned%s%d");
-    gs::launch_activate_fwd(N, raw_opacity, raw_scaling, raw_rotation, opacity, scaling, rotation, (hipStream_t)stream);
+    gs::launch_activate_fwd(N, raw_opacity, raw_scaling, raw_rotation, opacity, scaling, rotation, nullptr, 0,
+                            (hipStream_t)stream);
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -1661,6 +1681,43 @@ int dg_debug_image_state(const void* image, int W, int H, float* final_T, uint32
     if (n_contrib) HIP_OK(hipMemcpyAsync(n_contrib, im.n_contrib, 4 * HW, hipMemcpyDeviceToDevice, s));
     if (max_contrib) HIP_OK(hipMemcpyAsync(max_contrib, im.max_contrib, 4 * T, hipMemcpyDeviceToDevice, s));
     if (ranges) HIP_OK(hipMemcpyAsync(ranges, im.ranges, 8 * T, hipMemcpyDeviceToDevice, s));
+    return 0;
+}
+
+int dg_shutdown(void) {
+    // side streams of the overlapped SH update: drain, then destroy (with their events)
+    {
+        std::lock_guard<std::mutex> lk(sh_mu());
+        for (auto& kv : sh_map()) {
+            ShOverlap& o = kv.second;
+            if (o.side) { (void)hipStreamSynchronize(o.side); (void)hipStreamDestroy(o.side); }
+            if (o.fork) (void)hipEventDestroy(o.fork);
+            if (o.done) (void)hipEventDestroy(o.done);
+        }
+        sh_map().clear();
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_cap_mu);
+        for (auto& kv : cap_probes())
+            if (kv.second.probe) (void)hipFree(kv.second.probe);
+        cap_probes().clear();
+    }
+    {
+        auto release = [](HostCounters& h) {
+            if (h.ev) (void)hipEventDestroy(h.ev);
+            if (h.buf) (void)hipHostFree(h.buf);
+            h = HostCounters();
+        };
+        release(host_counters_slot().h);  // this thread's; other threads return theirs to the pool on exit
+        std::lock_guard<std::mutex> lk(hc_mu());
+        for (auto& h : hc_pool()) release(h);
+        hc_pool().clear();
+    }
+    for (auto& r : g_prof_recs) { g_ev_pool.push_back(r.a); g_ev_pool.push_back(r.b); }
+    g_prof_recs.clear();
+    for (hipEvent_t e : g_ev_pool) (void)hipEventDestroy(e);
+    g_ev_pool.clear();
+    g_prof = false;
     return 0;
 }
 

@@ -29,6 +29,10 @@ struct AdamGroup {
     int gmode;
     const float* act;
     float reg;
+    // gmode 2: *zero_stamp == stamp when any scaling of the step is exactly 0 (written by the activation pass); torch's
+    // prod backward then takes its zero-safe form for EVERY row, so the regulariser's gradient does too
+    const uint64_t* zero_stamp;
+    uint64_t stamp;
 };
 
 struct AdamMultiArgs {
@@ -75,10 +79,11 @@ void launch_block_sum(const float* x, uint32_t n, int mode, float* partial, hipS
 void launch_loss_final(const float* p_l1, uint32_t n_l1, const float* p_ssim, uint32_t n_ssim, const float* p_sc,
                        uint32_t n_sc, uint32_t n_img, uint32_t P, float* loss, hipStream_t s);
 void launch_activate_fwd(uint32_t N, const float* ro, const float* rs, const float* rq, float* o, float* sc, float* q,
+                         uint64_t* zero_stamp, uint64_t stamp,
                          hipStream_t s);
 void launch_activate_bwd(uint32_t N, const float* o, const float* sc, const float* rq, const float* go,
                          const float* gsc, const float* gq, float* dro, float* drs, float* drq, hipStream_t s,
-                         float scale_reg = 0.0f);
+                         float scale_reg = 0.0f, const uint64_t* zero_stamp = nullptr, uint64_t stamp = 0);
 
 // ---- densify_and_prune
 struct DensifyArgs {

@@ -49,12 +49,14 @@ __device__ __forceinline__ float sigmoid_bwd(float g, float v) { return g * (v *
 // exp's backward of scaling column r, with the scale regulariser lambda_scale mean(prod(scaling, 1))
 // (gaussian_trainer.py:407-408): its gradient reg prod / s_r joins the rasterizer's before exp's backward.  torch's
 // prod backward is result / input when the input holds no zero and the product of the other columns otherwise
-// (prod_safe_zeros_backward); the same here per row, so an underflowed scale (exp of a raw value below ~-87) gives a
-// finite gradient instead of 0/0.
-__device__ __forceinline__ float exp_bwd(float g, const float* __restrict__ s3, int r, float reg) {
+// (prod_safe_zeros_backward), for every row of the tensor as soon as one scaling is 0 (torch tests the whole input).
+// zmode 1: some scaling of the step is 0 (the activation pass's stamp), 0: none; -1: decide per row (the C-ABI
+// activation backward, which has no stamp).  An underflowed scale (exp of a raw value below ~-87) so gives a finite
+// gradient instead of 0/0, and the rows without a zero round as torch rounds them.
+__device__ __forceinline__ float exp_bwd(float g, const float* __restrict__ s3, int r, float reg, int zmode) {
     if (reg != 0.0f) {
         float d;
-        if (s3[0] == 0.0f || s3[1] == 0.0f || s3[2] == 0.0f)
+        if (zmode > 0 || (zmode < 0 && (s3[0] == 0.0f || s3[1] == 0.0f || s3[2] == 0.0f)))
             d = r == 0 ? s3[2] * s3[1] : r == 1 ? s3[0] * s3[2] : s3[0] * s3[1];
         else
             d = ((s3[0] * s3[2]) * s3[1]) / s3[r];  // torch.prod's row order on the GPU (k_row_prod_fwd)
@@ -176,9 +178,11 @@ __device__ __forceinline__ void adam_block(const AdamMultiArgs& a, const uint32_
                 if (e0 + j < total) f4set(gr[c], j, sigmoid_bwd(f4get(gr[c], j), g.act[gi0 + j]));
         } else if (g.gmode == 2) {
             uint32_t gj = gi0, rj = r0;
+            const int zmode = g.zero_stamp ? (*g.zero_stamp == g.stamp ? 1 : 0) : -1;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                if (e0 + j < total) f4set(gr[c], j, exp_bwd(f4get(gr[c], j), g.act + 3 * (size_t)gj, (int)rj, g.reg));
+                if (e0 + j < total)
+                    f4set(gr[c], j, exp_bwd(f4get(gr[c], j), g.act + 3 * (size_t)gj, (int)rj, g.reg, zmode));
                 if (++rj == 3u) { rj = 0; gj++; }
             }
         } else if (g.gmode == 3) {
@@ -381,11 +385,18 @@ __global__ void __launch_bounds__(256) k_densify_gather(RebuildArgs a, const uin
 __global__ void __launch_bounds__(256) k_activate_fwd(uint32_t N, const float* __restrict__ ro,
                                                       const float* __restrict__ rs, const float* __restrict__ rq,
                                                       float* __restrict__ o, float* __restrict__ sc,
-                                                      float* __restrict__ q) {
+                                                      float* __restrict__ q, uint64_t* __restrict__ zero_stamp,
+                                                      uint64_t stamp) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= N) return;
     o[i] = 1.0f / (1.0f + expf(-ro[i]));
-    for (int k = 0; k < 3; k++) sc[3 * (size_t)i + k] = expf(rs[3 * (size_t)i + k]);
+    bool zero = false;
+    for (int k = 0; k < 3; k++) {
+        const float e = expf(rs[3 * (size_t)i + k]);
+        sc[3 * (size_t)i + k] = e;
+        zero |= e == 0.0f;
+    }
+    if (zero && zero_stamp) *zero_stamp = stamp;  // same value from every writer
     const float4 x = reinterpret_cast<const float4*>(rq)[i];
     const float d = fmaxf(sqrtf(((x.x * x.x + x.y * x.y) + x.z * x.z) + x.w * x.w), 1e-12f);
     reinterpret_cast<float4*>(q)[i] = make_float4(x.x / d, x.y / d, x.z / d, x.w / d);
@@ -395,14 +406,16 @@ __global__ void __launch_bounds__(256) k_activate_bwd(uint32_t N, const float* _
                                                       const float* __restrict__ go, const float* __restrict__ gs_,
                                                       const float* __restrict__ gq, float* __restrict__ dro,
                                                       float* __restrict__ drs, float* __restrict__ drq,
-                                                      float scale_reg) {
+                                                      float scale_reg, const uint64_t* __restrict__ zero_stamp,
+                                                      uint64_t stamp) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= N) return;
     dro[i] = go ? sigmoid_bwd(go[i], o[i]) : 0.0f;
     const float* sv = sc + 3 * (size_t)i;
+    const int zmode = zero_stamp ? (*zero_stamp == stamp ? 1 : 0) : -1;
     for (int k = 0; k < 3; k++)
         drs[3 * (size_t)i + k] = (gs_ || scale_reg != 0.0f) ? exp_bwd(gs_ ? gs_[3 * (size_t)i + k] : 0.0f, sv, k,
-                                                                         scale_reg)
+                                                                         scale_reg, zmode)
                                                               : 0.0f;
     float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
     if (gq) r = normalize_bwd(reinterpret_cast<const float4*>(rq)[i], reinterpret_cast<const float4*>(gq)[i]);
@@ -542,13 +555,15 @@ void launch_densify_gather(const RebuildArgs& a, const uint32_t* keep_pos, hipSt
 }
 
 void launch_activate_fwd(uint32_t N, const float* ro, const float* rs, const float* rq, float* o, float* sc, float* q,
-                         hipStream_t s) {
-    if (N) k_activate_fwd<<<(N + 255) / 256, 256, 0, s>>>(N, ro, rs, rq, o, sc, q);
+                         uint64_t* zero_stamp, uint64_t stamp, hipStream_t s) {
+    if (N) k_activate_fwd<<<(N + 255) / 256, 256, 0, s>>>(N, ro, rs, rq, o, sc, q, zero_stamp, stamp);
 }
 void launch_activate_bwd(uint32_t N, const float* o, const float* sc, const float* rq, const float* go,
                          const float* gsc, const float* gq, float* dro, float* drs, float* drq, hipStream_t s,
-                         float scale_reg) {
-    if (N) k_activate_bwd<<<(N + 255) / 256, 256, 0, s>>>(N, o, sc, rq, go, gsc, gq, dro, drs, drq, scale_reg);
+                         float scale_reg, const uint64_t* zero_stamp, uint64_t stamp) {
+    if (N)
+        k_activate_bwd<<<(N + 255) / 256, 256, 0, s>>>(N, o, sc, rq, go, gsc, gq, dro, drs, drq, scale_reg, zero_stamp,
+                                                        stamp);
 }
 
 void launch_row_prod_fwd(uint32_t N, uint32_t M, const float* x, float* prod, uint32_t* any_zero, hipStream_t s) {

@@ -38,6 +38,8 @@ struct PreArgs {
     // (which then are outputs) for every Gaussian -- and part_sc[block] = the block's sum of prod(scaling, 1)
     const float *raw_o, *raw_s, *raw_q;
     float* part_sc;
+    uint64_t* zero_stamp;  // with raw_*: *zero_stamp = stamp when some activated scaling is exactly 0
+    uint64_t stamp;
 };
 
 // Counters block at the head of the geometry state (device, uint32 slots).

@@ -302,6 +302,8 @@ __global__ void __launch_bounds__(256) k_preprocess(PreArgs a) {
         if (idx < a.P) {
             area += pre_compute(a, idx, in[k]);
             prod += in[k].prod;
+            if (a.zero_stamp && (in[k].s.x == 0.0f || in[k].s.y == 0.0f || in[k].s.z == 0.0f))
+                *a.zero_stamp = a.stamp;  // the same value from every writer
         }
     }
     unsigned long long v = area;

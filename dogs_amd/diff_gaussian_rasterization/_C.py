@@ -235,14 +235,16 @@ def _check_group(param, grad, m, v):
 # The group table of the last few group sets (a training loop passes the same parameters, moments and -- from the
 # caching allocator -- usually the same gradient addresses every step): building and checking it was ~90 us of host
 # per step, more than the launch.  Keyed by every pointer and size it holds (the learning rate and eps are rewritten on
-# every call: the xyz rate follows its schedule); contiguity is checked on every call (a view can share a pointer),
-# dtype and device when the table is built.
+# every call: the xyz rate follows its schedule) and every dtype and device, so a tensor that reuses a freed address
+# with another dtype (fp16 moments, bf16 gradients) misses the cache and fails the float32 check; contiguity is
+# checked on every call (a view can share a pointer).
 _GROUP_TABLES: dict = {}
 
 
 def _group_array(chunk, N):
     key = (int(N),) + tuple((p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), g.numel(), m.numel(),
-                             v.numel()) for p, g, m, v, _, _ in chunk)
+                             v.numel(), p.dtype, g.dtype, m.dtype, v.dtype, p.device, g.device, m.device, v.device)
+                            for p, g, m, v, _, _ in chunk)
     arr = _GROUP_TABLES.get(key)
     if arr is not None:
         for i, (p, g, m, v, lr, eps) in enumerate(chunk):

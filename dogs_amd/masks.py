@@ -47,8 +47,76 @@ class AppearanceEmbedding(nn.Module):
         code = self.appearance_embedding[index]
         x = torch.cat([image, code[:, None, None].expand(code.shape[0], h, w)], dim=0)
         x = self.upsample(self.fusion(x))
-        x = F.interpolate(x.unsqueeze(0), size=tuple(image_size), mode="bilinear")[0]
+        x = resize_bilinear(x, tuple(image_size))
         return self.out_conv(x)
+
+
+def _bilinear_taps(n_in: int, n_out: int, device) -> tuple:
+    """Per output index: (i0, i1, l0, l1) of upsample_bilinear2d with align_corners=False and a given size (torch's
+    area_pixel_compute_source_index: src = (dst + 0.5) in / out - 0.5 clamped at 0, float32 arithmetic)."""
+    scale = torch.tensor(n_in / n_out, dtype=torch.float32)
+    dst = torch.arange(n_out, dtype=torch.float32)
+    src = torch.clamp_min(scale * (dst + 0.5) - 0.5, 0.0)
+    i0 = src.to(torch.int64)
+    i1 = torch.clamp_max(i0 + 1, n_in - 1)
+    l1 = src - i0.to(torch.float32)
+    l0 = 1.0 - l1
+    return i0, i1, l0, l1
+
+
+_ADJ_CACHE: dict = {}
+
+
+def _adjoint_gather(n_in: int, n_out: int, device) -> tuple:
+    """(idx [n_in, L], wt [n_in, L]): every output index that reads input index i, with its weight, in ascending output
+    order (zero-weight padding).  The adjoint of the resize along one axis is then a gather, a product and a sum over L
+    in a fixed order -- no atomics."""
+    key = (n_in, n_out, str(device))
+    hit = _ADJ_CACHE.get(key)
+    if hit is not None:
+        return hit
+    i0, i1, l0, l1 = _bilinear_taps(n_in, n_out, "cpu")
+    taps = [[] for _ in range(n_in)]
+    for o in range(n_out):
+        a, b = int(i0[o]), int(i1[o])
+        taps[a].append((o, float(l0[o])))
+        taps[b].append((o, float(l1[o])))      # a == b at the clamped edge: two taps of the same output
+    L = max(1, max(len(t) for t in taps))
+    idx = torch.zeros((n_in, L), dtype=torch.int64)
+    wt = torch.zeros((n_in, L), dtype=torch.float32)
+    for i, t in enumerate(taps):
+        t.sort(key=lambda ow: ow[0])
+        for k, (o, w) in enumerate(t):
+            idx[i, k], wt[i, k] = o, w
+    hit = _ADJ_CACHE[key] = (idx.to(device), wt.to(device))
+    return hit
+
+
+class _ResizeBilinear(torch.autograd.Function):
+    """F.interpolate(mode="bilinear") forward (the reference module's values, bit for bit) with a deterministic
+    backward: torch's upsample_bilinear2d backward scatters with atomicAdd on the GPU, so two runs of a masked
+    training loop (or the ranks and the sequential baseline of an ADMM run) drift apart by rounding.  Here the adjoint
+    runs as two gathers along W, then H, each summing its taps in a fixed order."""
+
+    @staticmethod
+    def forward(ctx, x, size):
+        ctx.in_hw = (int(x.shape[-2]), int(x.shape[-1]))
+        return F.interpolate(x.unsqueeze(0), size=size, mode="bilinear")[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        h, w = ctx.in_hw
+        H, W = int(g.shape[-2]), int(g.shape[-1])
+        iw, ww = _adjoint_gather(w, W, g.device)
+        gw = (g[:, :, iw] * ww).sum(-1)                        # [C, H, w]
+        ih, wh = _adjoint_gather(h, H, g.device)
+        gx = (gw[:, ih, :] * wh[:, :, None]).sum(-2)           # [C, h, w]
+        return gx, None
+
+
+def resize_bilinear(x: torch.Tensor, size: tuple) -> torch.Tensor:
+    """[C, h, w] -> [C, H, W] bilinear (align_corners=False), deterministic backward (_ResizeBilinear)."""
+    return _ResizeBilinear.apply(x, size)
 
 
 def downsample_image(image: torch.Tensor, factor: int) -> torch.Tensor:

@@ -41,7 +41,9 @@ class SyntheticScene:
 
 
 def make_scene(n: int, width: int = 1920, height: int = 1080, fx: float = 1600.0, fy: float = 1600.0,
-               seed: int = 1234, sh_rest: int = 15) -> SyntheticScene:
+               seed: int = 1234, sh_rest: int = 15, opacity_mean: float = 0.0) -> SyntheticScene:
+    """opacity_mean shifts the raw opacity (N(opacity_mean, 1.5)): the default 0 is BASELINE §2's scene, where near
+    Gaussians saturate almost every tile; -2 is the bench's non-saturating variant (most tiles see their whole list)."""
     g = torch.Generator().manual_seed(seed)
     z = torch.empty(n).uniform_(2.0, 20.0, generator=g)
     ux = torch.empty(n).uniform_(-1.0, 1.0, generator=g)
@@ -52,6 +54,8 @@ def make_scene(n: int, width: int = 1920, height: int = 1080, fx: float = 1600.0
     raw_s = torch.randn(n, 3, generator=g) * 0.5 + math.log(0.02)
     raw_q = torch.randn(n, 4, generator=g)
     raw_o = torch.randn(n, 1, generator=g) * 1.5
+    if opacity_mean != 0.0:
+        raw_o = raw_o + opacity_mean
     dc = torch.randn(n, 1, 3, generator=g) * 0.3
     sh = torch.randn(n, sh_rest, 3, generator=g) * 0.05
     scales = torch.exp(raw_s)

@@ -410,6 +410,12 @@ int dg_colmap_points3d(const char* path, int min_track_length, uint64_t* n, uint
 
 const char* dg_last_error(void);
 int dg_version(void);
+/* Explicit teardown of the library's process-wide device state before interpreter / runtime exit: waits for the
+ * streams it created (the overlapped SH update's side streams), destroys them and their events, frees the adaptive-
+ * capacity probes, the pinned counter buffers and the profiling events.  Idempotent; any later call re-creates what it
+ * needs.  No reference counterpart (the reference's extension holds no such state); dogs_amd._lib registers it with
+ * Python's atexit so nothing of it is alive when the HIP runtime or a profiler tool finalises. */
+int dg_shutdown(void);
 
 #ifdef __cplusplus
 }

@@ -1,5 +1,5 @@
-"""ADMM block consensus over torch.distributed (gloo, world_size 2 and 4, CPU; at 4 some Gaussians sit in 3 or 4
-blocks) vs a single-process restatement of the
+"""ADMM block consensus over torch.distributed (gloo, world_size 2, 4 and 8, CPU; at 4 and 8 some Gaussians sit in 3 or
+more blocks) vs a single-process restatement of the
 reference master's gather/average/scatter (master_gaussian_trainer.py:459-555, gaussian_splat_model.py:316-340),
 dual update (slave_gaussian_trainer.py:100-121), residuals (master :396-456) and penalty adaptation (:337-377)."""
 import os
@@ -64,8 +64,10 @@ def _worker(rank, world, port):
             lowest[i] = torch.minimum(lowest[i], torch.full_like(i, k))
         assert torch.equal(bc.owned, lowest[idx] == rank)
         z = bc.consensus(params)
+        # bit-identical for every count: the ranks' copies are added in block order onto zeros and divided by the
+        # count, the master's reinitialize / plus_gaussians / average_gaussians arithmetic
         for zi, zr in zip(z, zref):
-            torch.testing.assert_close(zi, zr[idx], rtol=1e-6, atol=1e-6)
+            assert torch.equal(zi, zr[idx])
         # Gaussians held by one block: z == x exactly, so their dual never moves
         solo = cnt[idx] == 1
         for zi, p in zip(z, params):
@@ -96,7 +98,7 @@ def _worker(rank, world, port):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_consensus_gloo_matches_single_process(world):
     mp.spawn(_worker, args=(world, _free_port()), nprocs=world, join=True)
 
@@ -108,3 +110,29 @@ def test_consensus_single_rank_is_identity():
     z = bc.consensus(params)
     for zi, p in zip(z, params):
         assert torch.equal(zi, p)
+
+
+def test_ordered_sum_is_block_order_sum_divided_by_count():
+    """count-2 rows of a two-term sum, count-3 rows whose float association matters: both equal the block-order sum /
+    count exactly, and differ from the reversed order / the reciprocal product somewhere (so the check has teeth)."""
+    mp.spawn(_ordered_worker, args=(3, _free_port()), nprocs=3, join=True)
+
+
+def _ordered_worker(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dogs_amd.admm import ordered_sum_average
+        S, D = 1001, 7
+        g = torch.Generator().manual_seed(3)
+        xs = [torch.randn((S, D), generator=g) * (10.0 ** torch.randint(-3, 4, (S, 1), generator=g)) for _ in range(3)]
+        count = torch.full((S, 1), 3.0)
+        count[::2] = 2.0
+        xs[2][::2] = 0.0                                   # even rows: held by ranks 0 and 1 only
+        got = ordered_sum_average(xs[rank].clone(), count, world, rank)
+        ref = ((torch.zeros(S, D) + xs[0]) + xs[1]) + xs[2]
+        assert torch.equal(got, ref / count)
+        assert not torch.equal(got[1::2], (((xs[2] + xs[1]) + xs[0]) / count)[1::2])
+        assert not torch.equal(got, ref * (1.0 / count))
+    finally:
+        dist.destroy_process_group()

@@ -1,6 +1,6 @@
 """The ADMM phase entry (dogs_amd.admm_phase: fuse_local_gaussians without the RPC master,
-master_gaussian_trainer.py:37-172, 557-618) over torch.distributed (gloo, world size 2, 3 and 4, CPU; at world 3
-the middle block has no cameras).
+master_gaussian_trainer.py:37-172, 557-618) over torch.distributed (gloo, world size 2, 3, 4 and 8, CPU; at world 3
+the middle block has no cameras, world 8 is a 2 x 4 grid).
 
 The device operations (count renders, box membership, prune compaction) are replaced by CPU restatements
 (`CPUKernels`), so this checks the distributed plumbing and the lifecycle order:
@@ -29,6 +29,9 @@ GRIDS = {
     2: [(-5.0, -5.0, 0.0, 5.0), (0.0, -5.0, 5.0, 5.0)],
     4: [(-5.0, -5.0, 0.0, 0.0), (0.0, -5.0, 5.0, 0.0), (-5.0, 0.0, 0.0, 5.0), (0.0, 0.0, 5.0, 5.0)],
     3: [(-6.0, -5.0, -2.0, 5.0), (-2.0, -5.0, 2.0, 5.0), (2.0, -5.0, 6.0, 5.0)],   # block 1 has no cameras
+    # world 8: a 2 x 4 grid (the sci-art / MatrixCity block count); cells 2.5 tall, so an expanded box reaches two
+    # rows away and a Gaussian near a column border sits in up to six blocks
+    8: [(-5.0 + 5.0 * i, -5.0 + 2.5 * j, 5.0 * i, -2.5 + 2.5 * j) for j in range(4) for i in range(2)],
 }
 
 
@@ -155,12 +158,12 @@ def _worker(rank, world, port):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_phase_entry_gloo_matches_single_process(world):
     mp.spawn(_worker, args=(world, _free_port()), nprocs=world, join=True)
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_single_process_entry_matches_reference_steps(world):
     from dogs_amd.admm_phase import PhaseConfig
     cfg = PhaseConfig(prune_percent=0.5, v_pow=0.1)
@@ -172,6 +175,10 @@ def test_single_process_entry_matches_reference_steps(world):
     assert int((vis >= 2).sum()) > 0, "the expanded boxes must overlap"
     if world == 4:
         assert int((vis >= 3).sum()) > 0 and int((vis == 4).sum()) > 0, "the grid centre must be shared by 3-4 blocks"
+    if world == 8:
+        assert int((vis >= 3).sum()) > 0, "a 4-long axis of 2.5-wide cells expanded by 1: rows in >= 3 blocks"
+        sizes = {len(e.global_indices) for e in entries}
+        assert len(sizes) > 1, "the entry's padded all_gather must see unequal blocks"
     for b in range(world):
         assert torch.equal(entries[b].global_indices, gi[b])
         for a, k in zip(entries[b].model.get_all_properties(), kept):
@@ -196,5 +203,31 @@ def _gather_worker(rank, world, port):
         want = torch.cat([torch.arange(r * 5 * 4, dtype=torch.float32).reshape(r * 5, 4) + 100 * r
                           for r in range(world)], 0)
         assert got.shape == (15, 4) and torch.equal(got, want)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ordered_importance_bounded_lookahead():
+    """ordered_importance with no camera rendered ahead of the chain's partial sum, one, and all of them: the same
+    bits as prune_list's pop order over the concatenated camera list."""
+    mp.spawn(_importance_worker, args=(3, _free_port()), nprocs=3, join=True)
+
+
+def _importance_worker(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dogs_amd.admm_phase import ordered_importance
+        K = _cpu_kernels()
+        fused = _block_model(0, 4)
+        cams = _cameras(4)[:world]
+        flat = [c for cs in cams for c in cs]
+        want = K.camera_importance(fused, flat.pop(), None)
+        while flat:
+            want += K.camera_importance(fused, flat.pop(), None)
+        n = fused.num_gaussians
+        for budget in (0, 4 * n, 1 << 30):
+            got = ordered_importance(fused, cams, K, None, score_budget_bytes=budget)
+            assert torch.equal(got, want), budget
     finally:
         dist.destroy_process_group()

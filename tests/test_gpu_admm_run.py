@@ -1,15 +1,20 @@
-"""The end-to-end ADMM run (dogs_amd.admm_run: master_gaussian_trainer.py:620-728 without the RPC master) on a 2 x 2
-Grid2D split of a synthetic aerial scene, on the GPU.
+"""The end-to-end ADMM run (dogs_amd.admm_run: master_gaussian_trainer.py:620-728 without the RPC master) on Grid2D
+splits of a synthetic aerial scene, on the GPU.
 
-* Four gloo ranks sharing the test box's GPU (the driver's 8-GPU node runs the same code over RCCL) each run `run()`
-  for their block -- pre-phase training with densification and a LightGaussian prune until densify_end_iter, the phase
-  entry (fuse, order-exact importance prune, expanded-box re-split), three ADMM rounds -- and reach the single-process
-  `run_sequential` of the same split: the pre-phase models and the entry bit for bit (same kernels, same per-block
-  seeds; the entry's importance is folded in the reference's camera order), the ADMM-phase parameters, duals and
-  residual logs to float association (the all_reduce sums a shared row's copies in the collective's order).
-* The reference ADMM config's options (appearance mask with lambda_mask 0.5, depth_threshold 0.23) through the whole
-  run in one process: the pre-phase trains the embedding, the re-created block trainers have none (sub_masks is None in
-  the reference), and everything stays finite.
+* gloo ranks sharing the test box's GPU (the driver's 8-GPU node runs the same code over RCCL), one per block, each run
+  `run()` for their block -- pre-phase training with densification and a LightGaussian prune until densify_end_iter,
+  the phase entry (fuse, order-exact importance prune, expanded-box re-split), three ADMM rounds -- and reach the
+  single-process `run_sequential` of the same split BIT FOR BIT: the pre-phase models, the entry, and the ADMM phase's
+  parameters, duals and residual logs.  The consensus adds a shared row's copies in block order onto zeros and
+  divides by the count on every rank (the reference master's arithmetic, gaussian_splat_model.py:316-340), so no
+  count -- 2, 3 or more -- leaves room for a rounding difference.
+  - 2 x 2 (four ranks), the grid centre shared by 3-4 blocks;
+  - 2 x 4 and 4 x 2 (eight ranks: BASELINE configs 3 and 5, the sci-art / MatrixCity block counts), a 4-long axis
+    whose expanded boxes put Gaussians in >= 3 blocks, eight unequal blocks through the entry's padded all_gather;
+  - 2 x 2 with the reference ADMM config's options (urban3d_admm.yaml:84-111 / Mill-19 config 4): appearance mask
+    with lambda_mask 0.5, depth_threshold 0.23 and a LightGaussian prune, distributed.
+* The same options through the whole run in one process: the pre-phase trains the embedding, the re-created block
+  trainers have none (sub_masks is None in the reference), and everything stays finite.
 """
 import os
 import socket
@@ -22,7 +27,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
-MX, MY, W, H, POINTS = 2, 2, 160, 120, 6000
+W, H, POINTS = 160, 120, 6000
 
 
 def _cfg(mask=False):
@@ -36,9 +41,12 @@ def _cfg(mask=False):
     return ADMMRunConfig(gs=gs, admm=ADMMConfig(consensus_interval=20, stop_adapt_iter=100))
 
 
-def _scenes(dev, tmp):
+def _scenes(dev, tmp, mx=2, my=2):
     from dogs_amd.admm_run import aerial_views, split_scene
-    return split_scene(aerial_views(POINTS, 4, 4, W, H, seed=5), MX, MY, tmp, dev, image_seed=9)
+    # cameras: 2 per block along each axis, over a slab stretched along the longer axis
+    ext = (4.0 * mx / 2, 4.0 * my / 2)
+    return split_scene(aerial_views(POINTS * mx * my // 4, 2 * mx, 2 * my, W, H, extent=ext, seed=5), mx, my, tmp,
+                       dev, image_seed=9)
 
 
 def _free_port():
@@ -55,7 +63,7 @@ def _pack(pre_model, entry, blk, logs):
             "iters": [lg.iteration for lg in logs]}
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, mx, my, mask):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -63,30 +71,36 @@ def _worker(rank, world, port, out_dir):
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
         with tempfile.TemporaryDirectory() as tmp:
-            scenes = _scenes(dev, tmp)
-        r = run(_cfg(), scenes[rank], device=dev, seed=3)
+            scenes = _scenes(dev, tmp, mx, my)
+        r = run(_cfg(mask), scenes[rank], device=dev, seed=3)
         torch.save(_pack(r.pre.model, r.entry, r.block, r.runner.logs) | {"shared": r.consensus.num_shared},
                    os.path.join(out_dir, f"rank{rank}.pt"))
     finally:
         dist.destroy_process_group()
 
 
-def test_four_ranks_match_sequential_run(hip_device):
+@pytest.mark.parametrize("mx,my,mask", [(2, 2, False), (2, 4, False), (4, 2, False), (2, 2, True)],
+                         ids=["2x2", "2x4", "4x2", "2x2-mask-depth-prune"])
+def test_ranks_match_sequential_run(hip_device, mx, my, mask):
     from dogs_amd.admm_run import run_sequential
-    world = MX * MY
+    world = mx * my
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, mx, my, mask), nprocs=world, join=True)
         got = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(world)]
     with tempfile.TemporaryDirectory() as tmp:
-        scenes = _scenes(hip_device, tmp)
+        scenes = _scenes(hip_device, tmp, mx, my)
     assert all(len(s.camera_blocks[s.block]) > 0 for s in scenes)
-    seq = run_sequential(_cfg(), scenes, hip_device, seed=3)
+    seq = run_sequential(_cfg(mask), scenes, hip_device, seed=3)
     logs = seq.seq.logs
     assert [lg.iteration for lg in logs] == [80, 100, 120]
     vis = seq.entries[0].visibility_count
-    assert int((vis >= 2).sum()) > 0 and int((vis >= 3).sum()) > 0, "the 2 x 2 expanded boxes share a centre"
+    assert int((vis >= 2).sum()) > 0 and int((vis >= 3).sum()) > 0, "expanded boxes share rows among >= 3 blocks"
+    if world == 8:
+        assert len({len(e.global_indices) for e in seq.entries}) > 1, "unequal blocks through the padded gather"
     pre_ev = [lg.events for lg in seq.pres[0].logs if lg.events]
     assert ["densify"] in pre_ev and ["prune"] in pre_ev
+    if mask:
+        assert all(p.mask is not None for p in seq.pres)
     for r in range(world):
         g = got[r]
         for a, b in zip(g["pre"], seq.pres[r].model.get_all_properties()):
@@ -95,20 +109,10 @@ def test_four_ranks_match_sequential_run(hip_device):
         assert torch.equal(g["gidx"], e.global_indices.cpu()) and torch.equal(g["vis"], e.visibility_count.cpu())
         assert g["rho_n"] == e.rho_gaussians and g["shared"] == seq.seq.cons.num_shared
         assert g["iters"] == [80, 100, 120]
-        # a shared row's 2-4 copies are summed in the collective's order: rounding, which the later rounds' Adam steps
-        # amplify where a gradient is near zero (its normalised step flips sign).  Measured over 3 rounds: 5 of 11k
-        # and 19 of 15k elements beyond rtol 2e-4 / atol 1e-5 (worst 1.7e-4 absolute) on two boxes, tensors within
-        # 1e-5 relative L2
         for a, b in list(zip(g["params"], seq.blocks[r].param_tuple())) + list(zip(g["u"], seq.blocks[r].admm.u)):
-            b = b.detach().cpu()
-            assert float((a.double() - b.double()).norm()) <= 1e-4 * max(float(b.double().norm()), 1e-12)
-            off = ~torch.isclose(a, b, rtol=2e-4, atol=1e-5)
-            assert int(off.sum()) <= max(2, a.numel() // 200), int(off.sum())
-            assert float((a - b).abs().max()) < 1e-3
-        for k, lg in enumerate(logs):
-            for n in lg.primal:
-                assert g["primal"][k][n] == pytest.approx(lg.primal[n], rel=1e-4, abs=1e-12)
-                assert g["dual"][k][n] == pytest.approx(lg.dual[n], rel=1e-4, abs=1e-12)
+            assert torch.equal(a, b.detach().cpu()), "ADMM phase"
+        assert g["primal"] == [lg.primal for lg in logs] and g["dual"] == [lg.dual for lg in logs]
+        assert g["rho"] == [lg.rho for lg in logs]
     assert sum(logs[-1].primal.values()) > 0
 
 

@@ -6,7 +6,7 @@ GaussianRasterizer (dc/sh split, depth_threshold scaling) end to end.
 Bars: integer/index work and correctly-rounded fp32 elementwise code bit-exact; SSIM: the kernel sums the window in
 another float32 order than ssim.cu (Horner form), so each map's error against the float64 value
 (oracle.ssim_forward_exact) is held to twice the reference order's own float32 error, and every array is within 1e-5
-norm-wise relative error of the C restatement.  The largest
+norm-wise relative error, and 3e-5 of the array's scale element by element, of the C restatement.  The largest
 cases are the BASELINE sizes: SSIM at 1 x 3 x 1080 x 1920, distCUDA2 at 1e6 points (tests/test_gpu_optim.py runs
 SparseGaussianAdam at 1e6 x 59)."""
 import numpy as np
@@ -29,6 +29,10 @@ def _within_reference_order_error(x, ref32, exact, name):
     scale = max(1.0, float(np.abs(exact).max()))
     assert e_ours <= 2.0 * e_ref + 1e-6 * scale, (name, e_ours, e_ref, scale)
     assert rel_err(x, ref32) < 1e-5, name
+    # and element by element against the restatement (round 4's Horner change measured 2.4e-5 at worst), so that a
+    # regression confined to a few pixels cannot hide inside the norm
+    d = float(np.abs(x - np.asarray(ref32, np.float64)).max())
+    assert d <= 3e-5 * scale, (name, d, scale)
 
 
 # several strips across (54 output columns per wave) with even and odd widths, ragged rows (32 per strip)

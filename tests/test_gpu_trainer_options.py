@@ -110,6 +110,56 @@ def test_masked_training_native_matches_autograd(hip_device):
     assert _rel(n0["appearance_embedding"], net0.state_dict()["appearance_embedding"].to(dev)) > 1e-4   # it trained
 
 
+@pytest.mark.parametrize("case", ["mask-depth", "antialiasing", "zero-scaling"])
+def test_first_step_native_equals_autograd(hip_device, case):
+    """ONE iteration through each route from the same state, SH degree 3 (so f_rest carries gradient): the first Adam
+    moment is 0.1 x the raw-parameter gradient and the second 0.001 x its square, so they compare the two routes'
+    gradients directly, f_rest included, at 1e-5 relative (the 20-step test above bounds the drift; this one the
+    step).  Cases: the appearance mask + lambda_mask 0.5 + depth_threshold (urban3d_admm.yaml); texture.anti_aliasing
+    (the native step's antialiasing flag); one Gaussian's scaling underflowed to exactly 0, where torch's prod backward
+    switches EVERY row to its zero-safe form (the native step reads the activation pass's zero stamp)."""
+    from dogs_amd.masks import AppearanceEmbedding
+    from dogs_amd.trainer import GaussianSplatTrainer
+    dev = hip_device
+    kw = dict(densify_start_iter=10 ** 6, opacity_reset_interval=10 ** 6, prune_iterations=(), lambda_scale=0.05)
+    if case == "mask-depth":
+        kw.update(mask=True, lambda_mask=0.5, depth_threshold=6.0)
+    elif case == "antialiasing":
+        kw.update(anti_aliasing=True)
+    cfg = _cfg(**kw)
+    torch.manual_seed(1)
+    net0 = AppearanceEmbedding(2)
+    with torch.no_grad():
+        net0.appearance_embedding.normal_(0.0, 0.3)
+    out = []
+    for native in (True, False):
+        m, cams, gts = _problem(dev, n_true=30_000, n_init=6_000, W=400, H=300, views=2)
+        m.active_sh_degree = 3
+        with torch.no_grad():   # SH rest, anisotropic scales and turned rotations: every group carries gradient
+            gen = torch.Generator(device=dev).manual_seed(4)
+            m._features_rest.normal_(0.0, 0.05, generator=gen)
+            m._scaling.add_(torch.randn(m._scaling.shape, generator=gen, device=dev) * 0.3)
+            m._quaternion.add_(torch.randn(m._quaternion.shape, generator=gen, device=dev) * 0.3)
+            if case == "zero-scaling":
+                m._scaling[7, 1] = -200.0          # exp(-200) == 0 in float32
+        tr = GaussianSplatTrainer(m, cams, gts, cfg, device=dev, seed=2, native=native, normal=_normal(dev, 3),
+                                  appear_embedding=copy.deepcopy(net0) if cfg.mask else None)
+        tr.train_iteration()
+        tr.sync()
+        assert [lg.route for lg in tr.logs] == ["native" if native else "autograd"]
+        if case == "zero-scaling":
+            assert float(torch.exp(m._scaling.detach()).min()) == 0.0
+        out.append(_state(tr))
+    s0, s1 = out
+    for k in s0[1]:
+        m0, m1 = s0[1][k][0], s1[1][k][0]
+        assert float(m1.norm()) > 0, k
+        assert _rel(m0, m1) < 1e-5, (k, _rel(m0, m1))
+        assert _rel(s0[1][k][1], s1[1][k][1]) < 2e-5, k
+    for a, b in zip(s0[2], s1[2]):
+        assert _rel(a, b) < 1e-5
+
+
 def test_depth_threshold_scales_statistics(hip_device):
     """grad_accum with depth_threshold = the reference's min(1, (depth / thr)^2) scaling of each visible Gaussian's
     screen-space gradient; denom and max_radii2D unchanged; native = autograd."""
