@@ -114,6 +114,15 @@ class _ResizeBilinear(torch.autograd.Function):
         return gx, None
 
 
+def deterministic_convs():
+    """Context for the embedding's forward and backward: MIOpen restricted to its deterministic convolution
+    algorithms (tools/det_probe.py: without it the weight gradients of the upsampling and output convolutions differ run
+    to run; with it they are bitwise repeatable), every other cuDNN/MIOpen flag left as it is.  The flag is global
+    state, so it also covers the backward the autograd engine runs on its device thread while the caller waits."""
+    cd = torch.backends.cudnn
+    return cd.flags(enabled=cd.enabled, benchmark=cd.benchmark, deterministic=True, allow_tf32=cd.allow_tf32)
+
+
 def resize_bilinear(x: torch.Tensor, size: tuple) -> torch.Tensor:
     """[C, h, w] -> [C, H, W] bilinear (align_corners=False), deterministic backward (_ResizeBilinear)."""
     return _ResizeBilinear.apply(x, size)
@@ -150,7 +159,8 @@ class MaskedStep:
     def forward(self, k: int, gt: torch.Tensor, index: int) -> tuple:
         """(mask [3,H,W] contiguous, dmask buffer of the same shape) for view k."""
         H, W = int(gt.shape[1]), int(gt.shape[2])
-        self.mask = self.net(self.small_target(k, gt), index, (H, W))
+        with deterministic_convs():
+            self.mask = self.net(self.small_target(k, gt), index, (H, W))
         buf = self.dmask.get((H, W))
         if buf is None:
             buf = self.dmask[(H, W)] = torch.empty((3, H, W), dtype=torch.float32, device=gt.device)
@@ -161,7 +171,8 @@ class MaskedStep:
         return m, buf
 
     def backward_and_step(self, dmask: torch.Tensor) -> None:
-        self.mask.backward(dmask)
+        with deterministic_convs():
+            self.mask.backward(dmask)
         self.opt.step()
         self.opt.zero_grad(set_to_none=True)
         self.mask = self._m = None
