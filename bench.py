@@ -688,10 +688,14 @@ def main():
         torch.cuda.synchronize()
         tt = time.perf_counter()
         nts = max(2 * len(cams), args.steps // 2)
+        host = []
         for _ in range(nts):
+            th = time.perf_counter()
             ts.step()
+            host.append(time.perf_counter() - th)
         torch.cuda.synchronize()
         tms = (time.perf_counter() - tt) / nts * 1e3
+        host_ms = float(np.median(host)) * 1e3
         nstep = ts.native()
         route_ms = {}
         # the default route (activation backward folded into the update) and the unfused one, interleaved three
@@ -719,6 +723,9 @@ def main():
                  "includes": "activations + raster fwd/bwd + L1 + fused-SSIM fwd/bwd + scale regulariser + "
                              "densification stats + SparseGaussianAdam (one launch), cycling the view batch; "
                              "autograd route (the drop-in API)",
+                 "host_ms_per_step": round(host_ms, 3),
+                 "host_note": "median host time per autograd-route step (Python + autograd + launches, and the "
+                              "forward's one wait for the phase-1 counters); above ms_per_step the GPU waits on it",
                  "native": {"views_per_s": round(1e3 / nms, 2), "ms_per_step": round(nms, 3),
                             "route": "dg_train_step (dogs_amd.train_step): the same iteration in one C call, the "
                                      "activation backward folded into the optimizer update",

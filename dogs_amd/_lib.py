@@ -10,6 +10,7 @@ import atexit
 import ctypes as C
 import os
 import threading
+import weakref
 
 import torch
 
@@ -313,6 +314,19 @@ def _bucket(n: int) -> int:
     return (n + q - 1) // q * q
 
 
+# One ctypes callback for every arena: creating a CFUNCTYPE object per call was a measurable part of each forward /
+# backward's host time.  An arena's `fn` makes it the calling thread's current arena and returns the shared callback;
+# the library calls it synchronously, on the same thread, during the C call the pointer was passed to.
+_TLS = threading.local()
+
+
+def _arena_dispatch(user, which, nbytes):  # noqa: ARG001
+    return _TLS.arena()._alloc(int(which), max(int(nbytes), 1))
+
+
+_ARENA_FN = ALLOC_FN(_arena_dispatch)
+
+
 class TensorArena:
     """dg_alloc_fn backed by the torch caching allocator; keeps the uint8 tensors per buffer kind."""
 
@@ -320,19 +334,21 @@ class TensorArena:
         self.device = device
         self.buffers: dict[int, torch.Tensor] = {}
 
-        def _alloc(user, which, nbytes):  # noqa: ARG001
-            n = max(int(nbytes), 1)
-            try:
-                # the per-view sizes (phase-2 binning, backward scratch: num_rendered) vary view to view and drift
-                # as a scene trains; requests rounded up to an eighth of their power of two let the caching allocator
-                # hand cached blocks back instead of a hipMalloc every few views (~40 us of host each)
-                t = torch.empty(_bucket(n), dtype=torch.uint8, device=self.device)[:n]
-            except Exception:  # noqa: BLE001 - reported to C as NULL, surfaces as RuntimeError
-                return None
-            self.buffers[int(which)] = t
-            return t.data_ptr()
+    @property
+    def fn(self):
+        _TLS.arena = weakref.ref(self)   # weak: the thread does not keep the last call's buffers alive
+        return _ARENA_FN
 
-        self.fn = ALLOC_FN(_alloc)
+    def _alloc(self, which: int, n: int):
+        try:
+            # the per-view sizes (phase-2 binning, backward scratch: num_rendered) vary view to view and drift as a
+            # scene trains; requests rounded up to an eighth of their power of two let the caching allocator hand
+            # cached blocks back instead of a hipMalloc every few views (~40 us of host each)
+            t = torch.empty(_bucket(n), dtype=torch.uint8, device=self.device)[:n]
+        except Exception:  # noqa: BLE001 - reported to C as NULL, surfaces as RuntimeError
+            return None
+        self.buffers[which] = t
+        return t.data_ptr()
 
     def get(self, which: int) -> torch.Tensor:
         return self.buffers.get(which, torch.empty(0, dtype=torch.uint8, device=self.device))
@@ -350,20 +366,22 @@ class ReuseArena:
         # them: the native step's overlapped update)
         self.keep_retired, self.retired = keep_retired, []
 
-        def _alloc(user, which, nbytes):  # noqa: ARG001
-            which, nbytes = int(which), max(int(nbytes), 1)
-            t = self.buffers.get(which)
-            if t is None or t.numel() < nbytes:
-                try:
-                    nt = torch.empty(nbytes + nbytes // 4, dtype=torch.uint8, device=self.device)
-                except Exception:  # noqa: BLE001 - reported to C as NULL, surfaces as RuntimeError
-                    return None
-                if t is not None and self.keep_retired:
-                    self.retired.append(t)
-                t = self.buffers[which] = nt
-            return t.data_ptr()
+    @property
+    def fn(self):
+        _TLS.arena = weakref.ref(self)   # weak: the thread does not keep the last call's buffers alive
+        return _ARENA_FN
 
-        self.fn = ALLOC_FN(_alloc)
+    def _alloc(self, which: int, nbytes: int):
+        t = self.buffers.get(which)
+        if t is None or t.numel() < nbytes:
+            try:
+                nt = torch.empty(nbytes + nbytes // 4, dtype=torch.uint8, device=self.device)
+            except Exception:  # noqa: BLE001 - reported to C as NULL, surfaces as RuntimeError
+                return None
+            if t is not None and self.keep_retired:
+                self.retired.append(t)
+            t = self.buffers[which] = nt
+        return t.data_ptr()
 
     def release_retired(self) -> None:
         self.retired.clear()

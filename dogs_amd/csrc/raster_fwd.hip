@@ -1178,26 +1178,23 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
             const v4f p2 = splat_power4(Sa.z, Sa.w, Sb.x, Sa.x, Sa.y, pxv, pyv);
             v4f al = bc4(Sb.y) * (v4f){__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y),
                                        __builtin_amdgcn_exp2f(p2.z), __builtin_amdgcn_exp2f(p2.w)};
-            // forward.cu:451-475: skip power > 0 and alpha < 1/255, stop once T would fall below 1e-4.  test_T is taken
-            // with the unselected alpha: a pixel that does not accept the splat is alive (T >= 1e-4) or dead (it never
-            // accepts), so only accepting pixels can stop, and one select per pixel state (alpha, T, last, threshold)
-            // commits "accepted and not stopping" -- the same values as selecting alpha first (one select fewer)
+            // forward.cu:451-475: skip power > 0 and alpha < 1/255, stop once T would fall below 1e-4
             bool acc[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                al[k] = fminf(0.99f, al[k]);
-                acc[k] = !(p2[k] > 0.0f || al[k] < thr[k]);
+                const float ak = fminf(0.99f, al[k]);
+                acc[k] = !(p2[k] > 0.0f || ak < thr[k]);
+                al[k] = acc[k] ? ak : 0.0f;
             }
             const v4f test_T = T * (bc4(1.0f) - al);
             v4f Tn;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const bool term = TERM && acc[k] && test_T[k] < 0.0001f;
-                const bool eff = acc[k] && !term;               // contributed: accepted and not the stopping splat
+                const bool term = TERM && test_T[k] < 0.0001f;
                 thr[k] = term ? 2.0f : thr[k];
-                al[k] = eff ? al[k] : 0.0f;
-                Tn[k] = eff ? test_T[k] : T[k];
-                last[k] = eff ? c : last[k];
+                al[k] = term ? 0.0f : al[k];
+                Tn[k] = term ? T[k] : test_T[k];
+                last[k] = (acc[k] && !term) ? c : last[k];  // contributed: accepted and not the stopping splat
             }
             if (COUNT) {  // LightGaussian count mode: pixels the splat contributes to (old forward.cu:481-487)
                 uint32_t n = 0;

@@ -15,10 +15,18 @@ bilinearly resized to the full image size, and mapped to three channels without 
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
 from torch import nn
+
+# MIOpen's default find mode times candidate kernels on first use, so processes sharing a GPU (the ADMM ranks of one
+# box, or a run next to another job) can pick different convolution algorithms for the same problem and round
+# differently: the masked pre-phase then drifts between ranks and the sequential baseline from the first iteration
+# (tools/mask_conc_probe.py: four concurrent processes differ at iteration 1; with FAST, bit-identical).  FAST takes the
+# find-db or the immediate-mode heuristic, never a timing.  setdefault: an explicit MIOPEN_FIND_MODE wins.
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
 
 EMBEDDING_DIM = 64
 MASK_DOWNSAMPLE = 32          # camera_origin.downsample(32) (gaussian_trainer.py:394)

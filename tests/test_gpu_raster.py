@@ -21,6 +21,9 @@ CASES = [
     (1024, 133, 97, 1, (0, 0, 0), True),
     (3000, 256, 192, 2, (0.2, 0.3, 0.4), False),
     (20000, 800, 800, 3, (0, 0, 0), False),
+    # dense 16x12 tiles: with 2 per tile in phase 1 the phase-2 lists run to hundreds of splats, so the longest are
+    # composited as segments and joined (DESIGN.md §3 Forward 6), pixels stopping inside a segment included
+    (12000, 256, 192, 3, (0.2, 0.3, 0.4), False),
 ]
 
 
