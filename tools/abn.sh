@@ -7,6 +7,6 @@ mkdir -p "$OUT"
 for i in $(seq 1 "$R"); do
   for lib in "$@"; do
     v=$(basename "$lib" .so)
-    DOGS_HIP_LIB=$lib timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-train-step --no-admm --no-reference-k > "$OUT/$v.$i.log" 2>&1
+    DOGS_HIP_LIB=$lib timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-train-step --no-admm --no-reference-k --no-sweep > "$OUT/$v.$i.log" 2>&1
   done
 done
