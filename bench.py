@@ -93,6 +93,7 @@ def relaunch_command(gpus: int | None, argv: list, environ) -> list | None:
     this process is already a rank or N <= 1."""
     if gpus is None or gpus <= 1 or "WORLD_SIZE" in environ:
         return None
+    argv = ["--gaussians" if a == "--n" else ("--gaussians=" + a[4:] if a.startswith("--n=") else a) for a in argv]
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
             "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *argv]
 
@@ -400,6 +401,8 @@ def admm_leg(args, ws, rank, dev, n, W, H):
                     "consensus_ms": round(1e3 * max(lg.seconds["consensus"] for lg in r.runner.logs), 3),
                     "last_round": {"primal": {k: float(f"{v:.4g}") for k, v in r.runner.logs[-1].primal.items()},
                                    "dual": {k: float(f"{v:.4g}") for k, v in r.runner.logs[-1].dual.items()}}})
+        # rank 0's block at the end, for the bit-for-bit comparison with the sequential baseline below
+        mine = [t.detach().clone() for t in r.block.param_tuple()] if rank == 0 else None
         del res, r
         gc.collect()
         torch.cuda.empty_cache()
@@ -410,6 +413,10 @@ def admm_leg(args, ws, rank, dev, n, W, H):
         seq = run_sequential(cfg, scenes, dev, seed=5)
         torch.cuda.synchronize(dev)
         t_seq = time.perf_counter() - t0
+        if ws > 1:   # the same trajectory: every parameter of block 0 bit for bit (the consensus and capacity contexts)
+            out["rank0_equals_sequential"] = bool(all(torch.equal(a, b.detach())
+                                                      for a, b in zip(mine, seq.blocks[0].param_tuple())))
+            del mine
         out["sequential"] = {"blocks": nb, "seconds": round(t_seq, 3),
                              "phase_seconds": {k: round(v, 3) for k, v in seq.seconds.items()},
                              "views_per_s": round(nb * rounds * args.admm_interval / seq.seconds["admm"], 2),
@@ -500,7 +507,9 @@ def main():
                     help="ranks (one per GPU); > 1 without a launcher relaunches under torch.distributed.run")
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--n", type=int, default=1_000_000)
+    # --gaussians: the same, spelled so that torch.distributed.run's own argparse (which matches option prefixes
+    # anywhere on the command line) does not read `--n` as an abbreviation of its --nnodes / --nproc-per-node
+    ap.add_argument("--n", "--gaussians", dest="n", type=int, default=1_000_000)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--views", type=int, default=8)

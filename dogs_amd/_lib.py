@@ -28,7 +28,7 @@ class DgRasterArgs(C.Structure):
         ("bg", C.c_void_p), ("means3D", C.c_void_p), ("colors", C.c_void_p), ("opacities", C.c_void_p),
         ("scales", C.c_void_p), ("rotations", C.c_void_p), ("cov3D_precomp", C.c_void_p),
         ("viewmatrix", C.c_void_p), ("projmatrix", C.c_void_p), ("dc", C.c_void_p), ("sh", C.c_void_p),
-        ("campos", C.c_void_p),
+        ("campos", C.c_void_p), ("capacity_ctx", C.c_int),
     ]
 
 

@@ -191,9 +191,20 @@ class BlockTrainer:
         return int(self.order.pop())
 
     def local_step(self) -> None:
-        """One training iteration (native: one dg_train_step call; else the autograd route)."""
+        """One training iteration (native: one dg_train_step call; else the autograd route), under the trainer's own
+        adaptive-capacity context (GaussianSplatTrainer.train_iteration)."""
+        with self._capacity():
+            self._local_step()
+
+    def _capacity(self):
+        from .diff_gaussian_rasterization import _C
+        if getattr(self, "capacity_ctx", None) is None:
+            self.capacity_ctx = _C.new_capacity_context()
+        return _C.capacity_context(self.capacity_ctx)
+
+    def _local_step(self) -> None:
         if not self.native:
-            self.local_step_autograd()
+            self._local_step_autograd()
             return
         self.iteration += 1
         lr = self.xyz_lr(self.iteration)
@@ -207,6 +218,10 @@ class BlockTrainer:
         """One training iteration through the drop-in autograd API (the reference's route: rasterizer, clamp/L1 and
         SSIM autograd functions, torch for the loss sum and the scale regulariser, SparseGaussianAdam with the
         penalty's proximal gradient); returns the loss without the penalty (a device scalar, no sync)."""
+        with self._capacity():
+            return self._local_step_autograd()
+
+    def _local_step_autograd(self) -> torch.Tensor:
         self.sync()   # an overlapped native update of f_dc / f_rest may still be running
         self.iteration += 1
         for g in self.opt.param_groups:

@@ -338,10 +338,11 @@ struct CapProbe {
     uint32_t last_e1 = 0;       // phase-1 instances of the last forward at this size on this stream
 };
 std::mutex g_cap_mu;
-using CapKey = std::tuple<int, int, int>;
+// keyed also by the caller's capacity context (dg_raster_args::capacity_ctx; 0: the process-wide default)
+using CapKey = std::tuple<int, int, int, int>;
 std::map<CapKey, AdaptiveCap>& cap_states() { static auto* m = new std::map<CapKey, AdaptiveCap>; return *m; }
-std::map<std::tuple<int, int, int, hipStream_t>, CapProbe>& cap_probes() {
-    static auto* m = new std::map<std::tuple<int, int, int, hipStream_t>, CapProbe>;  // node-based: entries never move
+std::map<std::tuple<int, int, int, int, hipStream_t>, CapProbe>& cap_probes() {
+    static auto* m = new std::map<std::tuple<int, int, int, int, hipStream_t>, CapProbe>;  // node-based: never move
     return *m;
 }
 CapProbe* adaptive_cap(const dg_raster_args* a, hipStream_t s) {
@@ -349,9 +350,9 @@ CapProbe* adaptive_cap(const dg_raster_args* a, hipStream_t s) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     std::lock_guard<std::mutex> lk(g_cap_mu);
-    CapProbe& c = cap_probes()[std::make_tuple(dev, a->W, a->H, s)];
+    CapProbe& c = cap_probes()[std::make_tuple(dev, a->W, a->H, a->capacity_ctx, s)];
     if (!c.probe) {
-        c.shared = &cap_states()[std::make_tuple(dev, a->W, a->H)];
+        c.shared = &cap_states()[std::make_tuple(dev, a->W, a->H, a->capacity_ctx)];
         if (hipMalloc((void**)&c.probe, 2 * sizeof(uint32_t)) != hipSuccess) { c.probe = nullptr; return nullptr; }
         (void)hipMemset(c.probe, 0, 2 * sizeof(uint32_t));
     }
@@ -495,7 +496,7 @@ int dg_adaptive_capacity(int W, int H, int reset, int* per_tile_out) {
     int dev = 0;
     HIP_OK(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(g_cap_mu);
-    AdaptiveCap& c = cap_states()[std::make_tuple(dev, W, H)];
+    AdaptiveCap& c = cap_states()[std::make_tuple(dev, W, H, 0)];
     if (reset) {
         c.per_tile = DEFAULT_PREFIX_PER_TILE;
         for (auto& kv : cap_probes()) {

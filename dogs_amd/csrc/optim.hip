@@ -64,9 +64,11 @@ __device__ __forceinline__ float exp_bwd(float g, const float* __restrict__ s3, 
     }
     return g * s3[r];
 }
-// F.normalize(x, eps 1e-12): d(x / n) = (g - y (y . g)) / n, or g / eps on the clamped denominator
+// F.normalize(x, eps 1e-12): d(x / n) = (g - y (y . g)) / n, or g / eps on the clamped denominator.  The norm is
+// summed pairwise, (x0^2 + x1^2) + (x2^2 + x3^2), as torch's vector_norm does (tools/act_match_probe.py: the forward
+// then equals F.normalize bit for bit; sigmoid and exp already do)
 __device__ __forceinline__ float4 normalize_bwd(float4 x, float4 g) {
-    const float n = sqrtf(((x.x * x.x + x.y * x.y) + x.z * x.z) + x.w * x.w);
+    const float n = sqrtf((x.x * x.x + x.y * x.y) + (x.z * x.z + x.w * x.w));
     if (n > 1e-12f) {
         const float inv = 1.0f / n;
         const float4 y = make_float4(x.x * inv, x.y * inv, x.z * inv, x.w * inv);
@@ -398,7 +400,7 @@ __global__ void __launch_bounds__(256) k_activate_fwd(uint32_t N, const float* _
     }
     if (zero && zero_stamp) *zero_stamp = stamp;  // same value from every writer
     const float4 x = reinterpret_cast<const float4*>(rq)[i];
-    const float d = fmaxf(sqrtf(((x.x * x.x + x.y * x.y) + x.z * x.z) + x.w * x.w), 1e-12f);
+    const float d = fmaxf(sqrtf((x.x * x.x + x.y * x.y) + (x.z * x.z + x.w * x.w)), 1e-12f);
     reinterpret_cast<float4*>(q)[i] = make_float4(x.x / d, x.y / d, x.z / d, x.w / d);
 }
 __global__ void __launch_bounds__(256) k_activate_bwd(uint32_t N, const float* __restrict__ o,

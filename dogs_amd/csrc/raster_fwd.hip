@@ -193,7 +193,7 @@ __device__ __forceinline__ PreIn pre_load(const PreArgs& a, int idx) {
         in.opac = 1.0f / (1.0f + expf(-ro));
         in.s = {expf(rs0), expf(rs1), expf(rs2)};
         in.prod = (in.s.x * in.s.y) * in.s.z;
-        const float d = fmaxf(sqrtf(((x.x * x.x + x.y * x.y) + x.z * x.z) + x.w * x.w), 1e-12f);
+        const float d = fmaxf(sqrtf((x.x * x.x + x.y * x.y) + (x.z * x.z + x.w * x.w)), 1e-12f);
         in.q = {x.x / d, x.y / d, x.z / d, x.w / d};
     } else {
         if (!a.cov3D_precomp) {
@@ -1180,27 +1180,6 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
                                        __builtin_amdgcn_exp2f(p2.z), __builtin_amdgcn_exp2f(p2.w)};
             // forward.cu:451-475: skip power > 0 and alpha < 1/255, stop once T would fall below 1e-4
             bool acc[4];
-#ifdef DG_FWD_ONESEL
-            // the stop test on the unselected alpha (a pixel that does not accept the splat is alive with T >= 1e-4, or
-            // dead and never accepts): one select per pixel state commits "accepted and not stopping" -- the same
-            // values as selecting the alpha first
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                al[k] = fminf(0.99f, al[k]);
-                acc[k] = !(p2[k] > 0.0f || al[k] < thr[k]);
-            }
-            const v4f test_T = T * (bc4(1.0f) - al);
-            v4f Tn;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const bool term = TERM && acc[k] && test_T[k] < 0.0001f;
-                const bool eff = acc[k] && !term;               // contributed: accepted and not the stopping splat
-                thr[k] = term ? 2.0f : thr[k];
-                al[k] = eff ? al[k] : 0.0f;
-                Tn[k] = eff ? test_T[k] : T[k];
-                last[k] = eff ? c : last[k];
-            }
-#else
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const float ak = fminf(0.99f, al[k]);
@@ -1217,7 +1196,6 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
                 Tn[k] = term ? T[k] : test_T[k];
                 last[k] = (acc[k] && !term) ? c : last[k];  // contributed: accepted and not the stopping splat
             }
-#endif
             if (COUNT) {  // LightGaussian count mode: pixels the splat contributes to (old forward.cu:481-487)
                 uint32_t n = 0;
 #pragma unroll

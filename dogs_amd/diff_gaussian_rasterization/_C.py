@@ -3,9 +3,12 @@ C ABI of libdogs_hip.so.  Same names, argument order, return tuples and error be
 pybind11 functions in rasterize_points.cu; tensors are torch tensors on a HIP device."""
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
+import itertools
 import math
 import os
+import threading
 
 import torch
 
@@ -26,6 +29,33 @@ def set_prefix_per_tile(n: int) -> int:
     return old
 
 
+# The adaptive capacity's context (dg_raster_args.capacity_ctx): 0 is the process-wide state; a trainer renders under
+# its own (`capacity_context`), so its capacity history -- and with it the instance numbering, hence the rounding of
+# its per-Gaussian gradient sums -- depends only on its own views, not on what else the process rendered before (the
+# ADMM sequential baseline trains every block in one process; a rank trains one).  Thread-local: the autograd
+# engine's backward thread does not read it (the backward carves the capacity the forward returned).
+_CTX = threading.local()
+_NEXT_CTX = itertools.count(1)
+
+
+def new_capacity_context() -> int:
+    return next(_NEXT_CTX)
+
+
+@contextlib.contextmanager
+def capacity_context(ctx: int):
+    old = getattr(_CTX, "v", 0)
+    _CTX.v = int(ctx)
+    try:
+        yield
+    finally:
+        _CTX.v = old
+
+
+def current_capacity_context() -> int:
+    return getattr(_CTX, "v", 0)
+
+
 def _f32(t: torch.Tensor | None) -> torch.Tensor | None:
     if t is None or t.numel() == 0:
         return None
@@ -38,6 +68,7 @@ def _args(P, D, M, W, H, bg, means3D, colors, opacity, scales, rotations, scale_
     a.P, a.D, a.M, a.W, a.H = int(P), int(D), int(M), int(W), int(H)
     a.prefiltered, a.antialiasing, a.debug = int(bool(prefiltered)), int(bool(antialiasing)), int(bool(debug))
     a.prefix_per_tile = int(PREFIX_PER_TILE)
+    a.capacity_ctx = getattr(_CTX, "v", 0)
     a.scale_modifier, a.tanfovx, a.tanfovy = float(scale_modifier), float(tan_fovx), float(tan_fovy)
     keep = dict(bg=_f32(bg), means3D=_f32(means3D), colors=_f32(colors), opacities=_f32(opacity),
                 scales=_f32(scales), rotations=_f32(rotations), cov3D_precomp=_f32(cov3D_precomp),

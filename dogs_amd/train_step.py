@@ -151,6 +151,7 @@ class NativeTrainStep:
                                "reset_opacity, load_state_dict); call rebind() first")
         a = self.args[k]
         a.view.prefix_per_tile = int(_C.PREFIX_PER_TILE)
+        a.view.capacity_ctx = _C.current_capacity_context()
         if sh_degree is not None:
             a.view.D = int(sh_degree)
         if xyz_lr is not None:

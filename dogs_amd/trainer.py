@@ -337,6 +337,15 @@ class GaussianSplatTrainer:
 
     # ---- one iteration
     def train_iteration(self) -> IterationLog:
+        # the trainer's own adaptive-capacity context: its views' phase split, instance numbering and gradient-sum
+        # rounding do not depend on anything else this process rendered (dg_raster_args.capacity_ctx)
+        from .diff_gaussian_rasterization import _C
+        if getattr(self, "capacity_ctx", None) is None:
+            self.capacity_ctx = _C.new_capacity_context()
+        with _C.capacity_context(self.capacity_ctx):
+            return self._train_iteration()
+
+    def _train_iteration(self) -> IterationLog:
         c = self.cfg
         self.iteration += 1
         lr = self.update_learning_rate()

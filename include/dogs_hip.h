@@ -53,6 +53,12 @@ typedef struct {
     const float* dc;            /* [P,1,3] */
     const float* sh;            /* [P,M,3] or NULL */
     const float* campos;        /* [3] */
+    int capacity_ctx;           /* adaptive capacity context (prefix_per_tile == 0): the growth state is per (device,
+                                   image size, context); 0 is the process-wide default.  A trainer that passes its
+                                   own context sees a capacity history -- and so an instance numbering and the
+                                   rounding of its per-Gaussian gradient sums -- that does not depend on what else
+                                   the process rendered (the ADMM ranks and the sequential baseline agree bit for
+                                   bit).  No reference counterpart (the reference bins every instance). */
 } dg_raster_args;
 
 /* Replaces RasterizeGaussiansCUDA (rasterize_points.cu:55-154) / _C.rasterize_gaussians.

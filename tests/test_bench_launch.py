@@ -23,6 +23,9 @@ def test_relaunch_command():
     assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
     assert cmd[-4:] == ["--gpus", "8", "--steps", "5"]
     assert os.path.basename(cmd[-5]) == "bench.py"
+    # `--n` is a prefix of torch.distributed.run's --nnodes / --nproc-per-node: passed on as --gaussians
+    cmd = bench.relaunch_command(2, ["--gpus", "2", "--n", "5000", "--n=6000"], {})
+    assert cmd[-4:] == ["2", "--gaussians", "5000", "--gaussians=6000"]
 
 
 def test_world_mismatch_refused():

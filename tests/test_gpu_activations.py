@@ -1,6 +1,8 @@
 """Fused parameter activations (dogs_amd.activations, optim.hip k_activate_*) against the plain PyTorch fp32 ops the
-reference's GaussianSplatModel uses (sigmoid, exp, F.normalize): values and gradients within 2e-6 relative
-(fp32 rounding of expf / the reciprocal norm; the tolerance is written below), zero-norm rotations included."""
+reference's GaussianSplatModel uses (sigmoid, exp, F.normalize): values bit for bit (the quaternion norm summed
+pairwise as torch's vector_norm sums it; tools/act_match_probe.py), gradients within 2e-6 relative (the normalize
+backward is one fused expression here, a chain of torch ops there; the tolerance is written below), zero-norm rotations
+included."""
 import pytest
 import torch
 
@@ -20,7 +22,7 @@ def test_activations_match_torch(hip_device):
     o, s, q = activate(*a)
     o2, s2, q2 = torch.sigmoid(b[0]), torch.exp(b[1]), torch.nn.functional.normalize(b[2])
     for x, y in ((o, o2), (s, s2), (q, q2)):
-        torch.testing.assert_close(x, y, rtol=2e-6, atol=1e-7)
+        assert torch.equal(x, y)
     w = [torch.randn(t.shape, generator=g).to(hip_device) for t in (o, s, q)]
     sum((x * y).sum() for x, y in zip((o, s, q), w)).backward()
     sum((x * y).sum() for x, y in zip((o2, s2, q2), w)).backward()

@@ -110,12 +110,14 @@ def test_masked_training_native_matches_autograd(hip_device):
     assert _rel(n0["appearance_embedding"], net0.state_dict()["appearance_embedding"].to(dev)) > 1e-4   # it trained
 
 
-@pytest.mark.parametrize("case", ["mask-depth", "antialiasing", "zero-scaling"])
+@pytest.mark.parametrize("case", ["plain", "mask-depth", "antialiasing", "zero-scaling"])
 def test_first_step_native_equals_autograd(hip_device, case):
     """ONE iteration through each route from the same state, SH degree 3 (so f_rest carries gradient): the first Adam
     moment is 0.1 x the raw-parameter gradient and the second 0.001 x its square, so they compare the two routes'
     gradients directly, f_rest included, at 1e-5 relative (the 20-step test above bounds the drift; this one the
-    step).  Cases: the appearance mask + lambda_mask 0.5 + depth_threshold (urban3d_admm.yaml); texture.anti_aliasing
+    step; with the library's activation kernels in place of torch's in the autograd route the two agree bit for bit,
+    tools/first_step_probe.py).  Cases: plain; the appearance mask + lambda_mask 0.5 + depth_threshold
+    (urban3d_admm.yaml); texture.anti_aliasing
     (the native step's antialiasing flag); one Gaussian's scaling underflowed to exactly 0, where torch's prod backward
     switches EVERY row to its zero-safe form (the native step reads the activation pass's zero stamp)."""
     from dogs_amd.masks import AppearanceEmbedding

@@ -17,9 +17,20 @@ def main():
     from test_gpu_trainer_options import _rel, _state
     from dogs_amd.trainer import GaussianSplatTrainer
     dev = torch.device("cuda", 0)
-    for case in ("plain", "zero-scaling", "zero-scaling-noreg", "antialiasing"):
+    import dogs_amd.gaussian_model as GM
+    from dogs_amd.activations import activate
+    torch_props = {k: getattr(GM.GaussianSplatModel, k) for k in ("get_opacity", "get_scaling", "get_quaternion")}
+
+    def ours(kind):   # the model's activations through the library's kernels (the native step's expressions)
+        def get(self):
+            o, s, q = activate(self._opacity, self._scaling, self._quaternion)
+            return {"get_opacity": o, "get_scaling": s, "get_quaternion": q}[kind]
+        return property(get)
+    for case in ("plain", "plain-kernel-activations", "zero-scaling", "antialiasing"):
+        for k, v in torch_props.items():
+            setattr(GM.GaussianSplatModel, k, ours(k) if case.endswith("kernel-activations") else v)
         kw = dict(densify_start_iter=10 ** 6, opacity_reset_interval=10 ** 6, prune_iterations=(),
-                  lambda_scale=0.0 if case.endswith("noreg") else 0.05)
+                  lambda_scale=0.05)
         if case == "antialiasing":
             kw.update(anti_aliasing=True)
         cfg = _cfg(**kw)
