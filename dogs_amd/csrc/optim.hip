@@ -45,7 +45,8 @@ constexpr int ADAM_CHUNKS = DG_ADAM_CHUNKS;  // float4 chunks per lane
 
 // Backward of the parameter activations (gaussian_splat_model.py get_opacity / get_scaling / get_quaternion), shared
 // by k_activate_bwd and the activation-folded Adam so both routes evaluate the same expressions.
-__device__ __forceinline__ float sigmoid_bwd(float g, float v) { return g * (v * (1.0f - v)); }
+// (g (1 - y)) y: torch's sigmoid_backward association, so the native step's opacity gradient equals the autograd route's
+__device__ __forceinline__ float sigmoid_bwd(float g, float v) { return (g * (1.0f - v)) * v; }
 // exp's backward of scaling column r, with the scale regulariser lambda_scale mean(prod(scaling, 1))
 // (gaussian_trainer.py:407-408): its gradient reg prod / s_r joins the rasterizer's before exp's backward.  torch's
 // prod backward is result / input when the input holds no zero and the product of the other columns otherwise

@@ -230,3 +230,49 @@ def test_adaptive_prefix_capacity(oracle, hip_device):
         assert psnr(first[2].cpu().numpy(), col_o) > 80.0
     finally:
         _C.set_prefix_per_tile(old)
+
+
+def test_capacity_contexts_are_isolated(hip_device):
+    """dg_raster_args.capacity_ctx: the adaptive capacity grown under one context (a translucent scene: phase 2 on every
+    early view) leaves another context cold, and a view rendered cold under either context has the same capacity
+    token, the same images and bit-identical gradients (the per-Gaussian sums round by instance position, so the
+    rounding follows the capacity history -- which is why every trainer renders under its own context)."""
+    from dogs_amd.diff_gaussian_rasterization import _C
+    n, W, H = 20000, 104, 72  # an image size no other test uses
+    s = small_scene(n, W, H, seed=33)
+    s.opacities = (s.opacities * 0.05).contiguous()
+    bg = (0.1, 0.2, 0.3)
+    dev = hip_device
+    c = s.camera.to(dev)
+    e = torch.empty(0, device=dev)
+    d = lambda t: t.to(dev).contiguous()  # noqa: E731
+    gcol = torch.from_numpy(np.random.default_rng(5).standard_normal((3, H, W)).astype(np.float32)).to(dev)
+
+    def view():
+        o = hip_forward(s, bg, dev)
+        g = _C.rasterize_gaussians_backward(
+            torch.as_tensor(bg, dtype=torch.float32, device=dev), d(s.means3D), o[4], e, d(s.opacities), d(s.scales),
+            d(s.rotations), 1.0, e, c.world_to_camera, c.projective_matrix, c.tanfovx, c.tanfovy, gcol, d(s.dc),
+            d(s.sh), torch.zeros((1, H, W), device=dev), 3, c.camera_center, o[5], o[0], o[6], o[7], o[1], o[8],
+            False, False)
+        torch.cuda.synchronize()
+        return int(o[1]), o[2].clone(), [t.clone() for t in g]
+
+    old = _C.set_prefix_per_tile(0)
+    try:
+        a, b = _C.new_capacity_context(), _C.new_capacity_context()
+        with _C.capacity_context(a):
+            first_a = view()
+            grown = [view()[0] for _ in range(8)]
+        assert grown[-1] > first_a[0], "the translucent scene must grow context a's capacity"
+        with _C.capacity_context(b):
+            first_b = view()
+        assert first_b[0] == first_a[0], "context b starts cold"
+        assert torch.equal(first_b[1], first_a[1])
+        for x, y in zip(first_b[2], first_a[2]):
+            assert torch.equal(x, y)
+        with _C.capacity_context(a):      # context a kept its growth
+            assert view()[0] >= grown[-1]
+        assert view()[0] == first_a[0], "the default context is untouched by both"
+    finally:
+        _C.set_prefix_per_tile(old)
