@@ -72,6 +72,23 @@ ALLOC_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int, C.c_uint64)
 DG_BUF_GEOM, DG_BUF_BINNING, DG_BUF_IMAGE, DG_BUF_BACKWARD, DG_BUF_TEMP, DG_BUF_BINNING2, DG_BUF_DENSIFY, \
     DG_BUF_DENSIFY2 = range(8)
 DG_BUF_MEMBERS = 8
+
+
+class DgFixedBuffer(C.Structure):
+    """dg_fixed_buffer: the user argument of dg_fixed_alloc."""
+    _fields_ = [("ptr", C.c_void_p), ("bytes", C.c_uint64)]
+
+
+_FIXED_FN = None
+
+
+def fixed_alloc_fn():
+    """dg_fixed_alloc as a dg_alloc_fn argument: a C function pointer, so the library's allocation request does not
+    call back into Python."""
+    global _FIXED_FN
+    if _FIXED_FN is None:
+        _FIXED_FN = ALLOC_FN(C.cast(load().dg_fixed_alloc, C.c_void_p).value)
+    return _FIXED_FN
 DG_MAX_BOXES = 64
 
 
@@ -80,8 +97,10 @@ class DgBox2dSet(C.Structure):
                 ("box", (C.c_double * 4) * DG_MAX_BOXES)]
 
 EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count", "dg_mark_visible", "dg_rasterize_filter",
-           "dg_adam_update", "dg_fused_ssim_forward", "dg_fused_ssim_backward", "dg_dist_cuda2",
-           "dg_geom_bytes", "dg_image_bytes", "dg_binning_bytes", "dg_debug_sorted_instances",
+           "dg_adam_update", "dg_fused_ssim_forward", "dg_fused_ssim_backward", "dg_fused_ssim_parts",
+           "dg_fused_ssim_mean", "dg_fused_ssim_mean_backward", "dg_mean_of_parts", "dg_dist_cuda2",
+           "dg_geom_bytes", "dg_image_bytes", "dg_binning_bytes", "dg_backward_scratch_bytes", "dg_fixed_alloc",
+           "dg_debug_sorted_instances",
            "dg_debug_geometry", "dg_debug_image_state", "dg_sort_pairs_u32", "dg_exclusive_scan_u32",
            "dg_profile_enable", "dg_profile_collect", "dg_binned_instances", "dg_adam_update_groups",
            "dg_add_densification_stats", "dg_densify_select", "dg_densify_split_stds", "dg_densify_count",
@@ -128,6 +147,14 @@ def load(path: str | None = None):
         L.dg_fused_ssim_forward.argtypes = [C.c_int] * 4 + [C.c_float, C.c_float] + [vp] * 6 + [vp]
         L.dg_fused_ssim_backward.restype = C.c_int
         L.dg_fused_ssim_backward.argtypes = [C.c_int] * 4 + [C.c_float, C.c_float] + [vp] * 7 + [vp]
+        L.dg_fused_ssim_parts.restype = C.c_uint32
+        L.dg_fused_ssim_parts.argtypes = [C.c_int] * 4
+        L.dg_fused_ssim_mean.restype = C.c_int
+        L.dg_fused_ssim_mean.argtypes = [C.c_int] * 4 + [C.c_float, C.c_float] + [vp] * 7 + [vp]
+        L.dg_fused_ssim_mean_backward.restype = C.c_int
+        L.dg_fused_ssim_mean_backward.argtypes = [C.c_int] * 4 + [vp] * 7 + [vp]
+        L.dg_mean_of_parts.restype = C.c_int
+        L.dg_mean_of_parts.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp]
         L.dg_dist_cuda2.restype = C.c_int
         L.dg_dist_cuda2.argtypes = [C.c_int, vp, vp, ALLOC_FN, vp, vp]
         L.dg_geom_bytes.restype = C.c_uint64
@@ -136,6 +163,8 @@ def load(path: str | None = None):
         L.dg_image_bytes.argtypes = [C.c_int, C.c_int]
         L.dg_binning_bytes.restype = C.c_uint64
         L.dg_binning_bytes.argtypes = [C.c_int64, C.c_int, C.c_int]
+        L.dg_backward_scratch_bytes.restype = C.c_uint64
+        L.dg_backward_scratch_bytes.argtypes = [C.POINTER(DgRasterArgs), C.c_int64]
         L.dg_debug_sorted_instances.restype = C.c_int
         L.dg_debug_sorted_instances.argtypes = [C.POINTER(DgRasterArgs), vp, vp, vp, vp, C.c_int64, C.c_int64,
                                                 vp, vp, i64p, vp]
@@ -212,9 +241,9 @@ def load(path: str | None = None):
             L.dg_clamp_l1_backward.restype = C.c_int
             L.dg_clamp_l1_backward.argtypes = [C.c_uint32] + [vp] * 6 + [vp]
             L.dg_row_prod_forward.restype = C.c_int
-            L.dg_row_prod_forward.argtypes = [C.c_uint32, C.c_uint32, vp, vp, vp, vp]
+            L.dg_row_prod_forward.argtypes = [C.c_uint32, C.c_uint32, vp, vp, vp, C.c_uint32, vp]
             L.dg_row_prod_backward.restype = C.c_int
-            L.dg_row_prod_backward.argtypes = [C.c_uint32, C.c_uint32] + [vp] * 5 + [vp]
+            L.dg_row_prod_backward.argtypes = [C.c_uint32, C.c_uint32] + [vp] * 4 + [C.c_uint32, vp, vp]
         if hasattr(L, "dg_activate_forward"):
             L.dg_activate_forward.restype = C.c_int
             L.dg_activate_forward.argtypes = [C.c_uint32] + [vp] * 6 + [vp]

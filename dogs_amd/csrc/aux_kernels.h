@@ -10,6 +10,15 @@ void launch_ssim_fwd(int B, int CH, int H, int W, float C1, float C2, const floa
 void launch_ssim_bwd(int B, int CH, int H, int W, const float* img1, const float* img2, const float* dL,
                      const float* dmu1, const float* ds1, const float* ds12, float* dimg1, hipStream_t s,
                      float dl_value = 0.0f);
+// fused_ssim's mean in one pass (MEAN strips: no map; part [ssim_mean_parts()] per-wave map sums, then *mean = their
+// total / numel in a fixed order) and its backward from the mean's gradient (device scalar, dL/dmap = *dl_mean / numel)
+void launch_ssim_mean(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,
+                      float* dmu1, float* ds1, float* ds12, float* part, float* mean, hipStream_t s);
+void launch_ssim_mean_bwd(int B, int CH, int H, int W, const float* img1, const float* img2, const float* dl_mean,
+                          const float* dmu1, const float* ds1, const float* ds12, float* dimg1, hipStream_t s);
+uint32_t ssim_mean_parts(int B, int CH, int H, int W);
+// *out = sum(part[0..n)) / denom in a fixed order (one block)
+void launch_mean_parts(const float* part, uint32_t n, uint32_t denom, float* out, hipStream_t s);
 // the native training step's variants: clamp(0, 1) of the raw render, the L1 term and the SSIM mean folded into the
 // forward (part: ssim_waves() L1 partials, then as many map partials; no map written), and the clamp / L1 backward
 // folded into the backward (d_raw: dL/d raw render; l1_scale = dL/dL1 / n)

@@ -109,7 +109,9 @@ __device__ __forceinline__ float clamp01f(float x) { return x != x ? x : fminf(f
 // instead of the map itself -- render()'s clamp, the L1 term and the SSIM mean in the same pass.
 // MASK (with FUSED): the appearance mask multiplies the clamped render inside the L1 term (|clamped * mask - gt|), and a
 // third set of per-wave partials holds sum (mask - 1)^2 (gaussian_trainer.py:392-401)
-template <bool TRAIN, bool FUSED = false, bool MASK = false>
+// MEAN (the drop-in fused_ssim(...) = FusedSSIMMap(...).mean()): no clamp, no map written, each wave writes its partial
+// sum of the map to part[wave] (the FUSED map partials' arithmetic: the same per-wave values), k_mean_parts totals them.
+template <bool TRAIN, bool FUSED = false, bool MASK = false, bool MEAN = false>
 __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes, float C1, float C2,
                                                         const float* __restrict__ img1, const float* __restrict__ img2,
                                                         float* __restrict__ map, float* __restrict__ dmu1,
@@ -199,7 +201,7 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
                          // at 1080p x 3, within the 1e-5 parity bar (test_fused_ssim_matches_oracle)
                         const float rAB = __builtin_amdgcn_rcpf(A * B), rAAB = __builtin_amdgcn_rcpf(A * A * B),
                                     rABB = __builtin_amdgcn_rcpf(A * B * B);
-                        if (FUSED) {
+                        if (FUSED || MEAN) {
                             acc_map += (Cc * D) * rAB;
                         } else {
                             map[gi] = (Cc * D) * rAB;
@@ -211,7 +213,8 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
                             ds12[gi] = ((2 * Cc) * rAB);
                         }
 #else
-                        map[gi] = (Cc * D) / (A * B);
+                        if (FUSED || MEAN) acc_map += (Cc * D) / (A * B);
+                        else map[gi] = (Cc * D) / (A * B);
                         if (TRAIN) {
                             dmu1[gi] = ((mu2 * 2.0f * D) / (A * B) - (mu2 * 2.0f * Cc) / (A * B) -
                                         (mu1 * 2.0f * Cc * D) / (A * A * B) + (mu1 * 2.0f * Cc * D) / (A * B * B));
@@ -238,7 +241,24 @@ __global__ void __launch_bounds__(256) k_ssim_fwd_strip(int H, int W, int planes
             part[nw + wid] = acc_map;
             if (MASK) part[2 * nw + wid] = acc_mreg;
         }
+    } else if (MEAN) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc_map += __shfl_xor(acc_map, o);
+        if (lane == 0) part[blockIdx.x * 4 + (threadIdx.x >> 6)] = acc_map;
     }
+}
+
+// *out = (sum of part[0..n)) / denom in loss_final_block's order (strided per thread, the wave sums, then (w0 + w1) +
+// (w2 + w3)): over the MEAN partials the SSIM mean equals the native step's loss[1] bit for bit.  One 256-thread block.
+__global__ void __launch_bounds__(256) k_mean_parts(const float* __restrict__ part, uint32_t n, uint32_t denom,
+                                                    float* __restrict__ out) {
+    __shared__ float s_w[4];
+    float acc = 0.0f;
+    for (uint32_t i = threadIdx.x; i < n; i += 256) acc += part[i];
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) out[0] = ((s_w[0] + s_w[1]) + (s_w[2] + s_w[3])) / (float)denom;
 }
 
 // The step's loss (k_loss_final's arithmetic, 256 threads): each total strided per thread, then the 4 wave sums in order.
@@ -275,9 +295,13 @@ __global__ void __launch_bounds__(256) k_ssim_bwd_strip(int H, int W, int planes
                                                         float* __restrict__ dimg1, const float* __restrict__ raw = nullptr,
                                                         float l1_scale = 0.0f, LossFinal lf = {}, uint32_t lblk = 0,
                                                         const float* __restrict__ mask = nullptr,
-                                                        float* __restrict__ dmask = nullptr, float mreg_scale = 0.0f) {
+                                                        float* __restrict__ dmask = nullptr, float mreg_scale = 0.0f,
+                                                        const float* __restrict__ dl_mean = nullptr,
+                                                        uint32_t n_mean = 1u) {
     // lblk = 1: block 0 computes the step's loss (dispatched first, beside the strips), the strips follow
     if (lblk && blockIdx.x == 0) { loss_final_block(lf); return; }
+    // dl_mean: the gradient of the map's mean (device scalar) -- dL/dmap = *dl_mean / numel, torch's mean backward
+    if (dl_mean) dl_value = dl_mean[0] / (float)n_mean;
     const StripPos sp = strip_of(H, W, planes, lblk);
     if (!sp.valid) return;
     const int lane = threadIdx.x & 63;
@@ -372,6 +396,32 @@ void launch_ssim_bwd(int B, int CH, int H, int W, const float* img1, const float
     if ((size_t)B * CH * H * W == 0) return;
     k_ssim_bwd_strip<false><<<ssim_strip_blocks(B * CH, H, W), 256, 0, s>>>(H, W, B * CH, img1, img2, dL, dl_value, dmu1,
                                                                         ds1, ds12, dimg1);
+}
+void launch_ssim_mean(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,
+                      float* dmu1, float* ds1, float* ds12, float* part, float* mean, hipStream_t s) {
+    const uint32_t nw = ssim_waves(B * CH, H, W);
+    const unsigned blocks = ssim_strip_blocks(B * CH, H, W);
+    if (nw) {
+        if (dmu1)
+            k_ssim_fwd_strip<true, false, false, true><<<blocks, 256, 0, s>>>(H, W, B * CH, C1, C2, img1, img2, nullptr,
+                                                                             dmu1, ds1, ds12, nullptr, part);
+        else
+            k_ssim_fwd_strip<false, false, false, true><<<blocks, 256, 0, s>>>(H, W, B * CH, C1, C2, img1, img2, nullptr,
+                                                                              nullptr, nullptr, nullptr, nullptr, part);
+    }
+    // an empty image: 0 / 0 = nan, as torch's mean of an empty map
+    k_mean_parts<<<1, 256, 0, s>>>(part, nw, (uint32_t)((size_t)B * CH * H * W), mean);
+}
+void launch_ssim_mean_bwd(int B, int CH, int H, int W, const float* img1, const float* img2, const float* dl_mean,
+                          const float* dmu1, const float* ds1, const float* ds12, float* dimg1, hipStream_t s) {
+    if ((size_t)B * CH * H * W == 0) return;
+    k_ssim_bwd_strip<false><<<ssim_strip_blocks(B * CH, H, W), 256, 0, s>>>(
+        H, W, B * CH, img1, img2, nullptr, 0.0f, dmu1, ds1, ds12, dimg1, nullptr, 0.0f, LossFinal{}, 0u, nullptr, nullptr,
+        0.0f, dl_mean, (uint32_t)((size_t)B * CH * H * W));
+}
+uint32_t ssim_mean_parts(int B, int CH, int H, int W) { return ssim_waves(B * CH, H, W); }
+void launch_mean_parts(const float* part, uint32_t n, uint32_t denom, float* out, hipStream_t s) {
+    k_mean_parts<<<1, 256, 0, s>>>(part, n, denom, out);
 }
 void launch_ssim_fwd_fused(int H, int W, float C1, float C2, const float* raw, const float* gt, float* clamped,
                            float* dmu1, float* ds1, float* ds12, float* part, hipStream_t s, const float* mask) {

@@ -513,6 +513,22 @@ uint64_t dg_geom_bytes(int P) { return carve_geom(nullptr, P).bytes; }
 uint64_t dg_image_bytes(int W, int H) { return carve_image(nullptr, W, H).bytes; }
 uint64_t dg_binning_bytes(int64_t K, int W, int H) { (void)W; (void)H; return carve_binning(nullptr, K).bytes; }
 
+uint64_t dg_backward_scratch_bytes(const dg_raster_args* a, int64_t num_rendered) {
+    if (!a || a->P <= 0 || num_rendered < 0) return 0;
+    const int T = tiles_x_of(a->W) * tiles_y_of(a->H);
+    return carve_bwd(nullptr, inst_cap((uint64_t)num_rendered), a->P, T).bytes;
+}
+
+void* dg_fixed_alloc(void* user, int which, uint64_t nbytes) {
+    (void)which;
+    const dg_fixed_buffer* f = static_cast<const dg_fixed_buffer*>(user);
+    if (!f || !f->ptr || nbytes > f->bytes) {
+        fail("fixed buffer too small for the request (%s%d MiB held)", "", f ? (int)(f->bytes >> 20) : 0);
+        return nullptr;
+    }
+    return f->ptr;
+}
+
 }  // extern "C"
 
 namespace {
@@ -1438,21 +1454,21 @@ int dg_clamp_l1_backward(uint32_t n, const float* img, const float* clamped, con
     return 0;
 }
 
-int dg_row_prod_forward(uint32_t N, uint32_t M, const float* x, float* prod, uint32_t* any_zero, dg_stream_t stream) {
+int dg_row_prod_forward(uint32_t N, uint32_t M, const float* x, float* prod, uint32_t* zero_stamp, uint32_t stamp,
+                        dg_stream_t stream) {
     if (M < 1 || M > 3) return fail("row_prod: 1 <= M <= 3 columns%s%d");
-    if (!any_zero || (N && (!x || !prod))) return fail("row_prod: NULL tensor%s%d");
-    HIP_OK(hipMemsetAsync(any_zero, 0, sizeof(uint32_t), (hipStream_t)stream));
-    gs::launch_row_prod_fwd(N, M, x, prod, any_zero, (hipStream_t)stream);
+    if (!zero_stamp || (N && (!x || !prod))) return fail("row_prod: NULL tensor%s%d");
+    gs::launch_row_prod_fwd(N, M, x, prod, zero_stamp, stamp, (hipStream_t)stream);
     HIP_OK(hipGetLastError());
     return 0;
 }
 
 int dg_row_prod_backward(uint32_t N, uint32_t M, const float* x, const float* prod, const float* dprod,
-                         const uint32_t* any_zero, float* dx, dg_stream_t stream) {
+                         const uint32_t* zero_stamp, uint32_t stamp, float* dx, dg_stream_t stream) {
     if (M < 1 || M > 3) return fail("row_prod backward: 1 <= M <= 3 columns%s%d");
     if (N == 0) return 0;
-    if (!x || !prod || !dprod || !any_zero || !dx) return fail("row_prod backward: NULL tensor%s%d");
-    gs::launch_row_prod_bwd(N, M, x, prod, dprod, any_zero, dx, (hipStream_t)stream);
+    if (!x || !prod || !dprod || !zero_stamp || !dx) return fail("row_prod backward: NULL tensor%s%d");
+    gs::launch_row_prod_bwd(N, M, x, prod, dprod, zero_stamp, stamp, dx, (hipStream_t)stream);
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -1587,6 +1603,46 @@ int dg_fused_ssim_backward(int B, int CH, int H, int W, float C1, float C2, cons
     (void)C1; (void)C2;
     gs::launch_ssim_bwd(B, CH, H, W, img1, img2, dL_dmap, dm_dmu1, dm_dsigma1_sq, dm_dsigma12, dL_dimg1,
                         (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+uint32_t dg_fused_ssim_parts(int B, int CH, int H, int W) {
+    if (B <= 0 || CH <= 0 || H <= 0 || W <= 0) return 1u;
+    const uint32_t n = gs::ssim_mean_parts(B, CH, H, W);
+    return n ? n : 1u;
+}
+
+int dg_fused_ssim_mean(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,
+                       float* dm_dmu1, float* dm_dsigma1_sq, float* dm_dsigma12, float* part, float* mean,
+                       dg_stream_t stream) {
+    if (B < 0 || CH < 0 || H < 0 || W < 0) return fail("fused_ssim mean: negative size%s%d");
+    if ((size_t)B * CH * H * W >= 0xffffff00ull) return fail("fused_ssim mean: image too large%s%d");
+    if (!part || !mean) return fail("fused_ssim mean: NULL partials or output%s%d");
+    if (dm_dmu1 && (!dm_dsigma1_sq || !dm_dsigma12)) return fail("train=True needs all three partial maps%s%d");
+    if ((size_t)B * CH * H * W && (!img1 || !img2)) return fail("fused_ssim mean: NULL image%s%d");
+    gs::launch_ssim_mean(B, CH, H, W, C1, C2, img1, img2, dm_dmu1, dm_dsigma1_sq, dm_dsigma12, part, mean,
+                         (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_fused_ssim_mean_backward(int B, int CH, int H, int W, const float* img1, const float* img2,
+                                const float* dL_dmean, const float* dm_dmu1, const float* dm_dsigma1_sq,
+                                const float* dm_dsigma12, float* dL_dimg1, dg_stream_t stream) {
+    if ((size_t)B * CH * H * W == 0) return 0;
+    if ((size_t)B * CH * H * W >= 0xffffff00ull) return fail("fused_ssim mean backward: image too large%s%d");
+    if (!img1 || !img2 || !dL_dmean || !dm_dmu1 || !dm_dsigma1_sq || !dm_dsigma12 || !dL_dimg1)
+        return fail("fused_ssim mean backward: NULL tensor%s%d");
+    gs::launch_ssim_mean_bwd(B, CH, H, W, img1, img2, dL_dmean, dm_dmu1, dm_dsigma1_sq, dm_dsigma12, dL_dimg1,
+                             (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int dg_mean_of_parts(const float* part, uint32_t n_part, uint32_t denom, float* out, dg_stream_t stream) {
+    if (!out || (n_part && !part)) return fail("mean_of_parts: NULL tensor%s%d");
+    gs::launch_mean_parts(part, n_part, denom, out, (hipStream_t)stream);
     HIP_OK(hipGetLastError());
     return 0;
 }

@@ -69,9 +69,10 @@ struct AdamMultiArgs {
 void launch_adam_multi(const AdamMultiArgs& a, hipStream_t s);
 uint32_t clamp_l1_blocks(uint32_t n);
 void launch_clamp_l1_fwd(uint32_t n, const float* img, const float* gt, float* out, float* partial, hipStream_t s);
-void launch_row_prod_fwd(uint32_t N, uint32_t M, const float* x, float* prod, uint32_t* any_zero, hipStream_t s);
+void launch_row_prod_fwd(uint32_t N, uint32_t M, const float* x, float* prod, uint32_t* zero_stamp, uint32_t stamp,
+                         hipStream_t s);
 void launch_row_prod_bwd(uint32_t N, uint32_t M, const float* x, const float* prod, const float* dprod,
-                         const uint32_t* any_zero, float* dx, hipStream_t s);
+                         const uint32_t* zero_stamp, uint32_t stamp, float* dx, hipStream_t s);
 void launch_clamp_l1_bwd(uint32_t n, const float* img, const float* clamped, const float* gt, const float* g_img,
                          const float* g_l1, float* d_img, hipStream_t s, float g_l1_value = 0.0f);
 uint32_t block_sum_blocks(uint32_t n);

@@ -65,17 +65,17 @@ __device__ __forceinline__ float exp_bwd(float g, const float* __restrict__ s3, 
     }
     return g * s3[r];
 }
-// F.normalize(x, eps 1e-12): d(x / n) = (g - y (y . g)) / n, or g / eps on the clamped denominator.  The norm is
+// F.normalize(x, eps 1e-12): d(x / n) = g / n - y (y . g) / n, or g / eps on the clamped denominator.  The norm is
 // summed pairwise, (x0^2 + x1^2) + (x2^2 + x3^2), as torch's vector_norm does (tools/act_match_probe.py: the forward
 // then equals F.normalize bit for bit; sigmoid and exp already do)
 __device__ __forceinline__ float4 normalize_bwd(float4 x, float4 g) {
     const float n = sqrtf((x.x * x.x + x.y * x.y) + (x.z * x.z + x.w * x.w));
-    if (n > 1e-12f) {
-        const float inv = 1.0f / n;
-        const float4 y = make_float4(x.x * inv, x.y * inv, x.z * inv, x.w * inv);
-        const float yg = ((y.x * g.x + y.y * g.y) + y.z * g.z) + y.w * g.w;
-        return make_float4((g.x - y.x * yg) * inv, (g.y - y.y * yg) * inv, (g.z - y.z * yg) * inv,
-                           (g.w - y.w * yg) * inv);
+    if (n >= 1e-12f) {
+        // torch's autograd of x / n.clamp_min(eps).expand_as(x), op for op (tools/normalize_bwd_probe.py: bit-identical
+        // on 4M elements): div's other-gradient -g (y / n), its expand summed pairwise, then g / n + s y
+        const float4 y = make_float4(x.x / n, x.y / n, x.z / n, x.w / n);
+        const float s = (-g.x * (y.x / n) + -g.y * (y.y / n)) + (-g.z * (y.z / n) + -g.w * (y.w / n));
+        return make_float4(g.x / n + s * y.x, g.y / n + s * y.y, g.z / n + s * y.z, g.w / n + s * y.w);
     }
     return make_float4(g.x / 1e-12f, g.y / 1e-12f, g.z / 1e-12f, g.w / 1e-12f);
 }
@@ -477,13 +477,15 @@ __global__ void __launch_bounds__(256) k_clamp_l1_bwd(uint32_t n, const float* _
 // torch.prod(x, dim=1) of x [N, M], M <= 3 (the scale regulariser's prod of the scaling), and its autograd backward
 // (FunctionsManual.cpp prod_backward) without the host read: torch counts the zeros of x, reads the count back and
 // picks dprod * (prod / x) when there are none, else for EVERY row the zero-safe dprod * (exclusive left cumprod x
-// exclusive right cumprod).  Here the forward raises *any_zero (vector atomic) and the backward reads it on the device.
+// exclusive right cumprod).  Here the forward writes the call's stamp to *zero_stamp when some element is 0 and the
+// backward compares it with the same stamp, on the device.
 // Row order: torch's reduction gives a row of M <= 4 elements to 4 lanes (identity 1 past M) and combines them with
 // shuffles at offsets 2 then 1, so the product is (x0 x2)(x1 x3): (x0 x2) x1 for M = 3 (tools/prod_order_probe.py
 // finds no other order matching on the GPU).  Every cumprod entry of the zero-safe form has at most two factors
 // for M <= 3, so its value does not depend on the scan's association.
 __global__ void __launch_bounds__(256) k_row_prod_fwd(uint32_t N, uint32_t M, const float* __restrict__ x,
-                                                      float* __restrict__ prod, uint32_t* __restrict__ any_zero) {
+                                                      float* __restrict__ prod, uint32_t* __restrict__ zero_stamp,
+                                                      uint32_t stamp) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     bool z = false;
     if (i < N) {
@@ -492,17 +494,20 @@ __global__ void __launch_bounds__(256) k_row_prod_fwd(uint32_t N, uint32_t M, co
         prod[i] = (a * c) * b;
         z = a == 0.0f || b == 0.0f || c == 0.0f;
     }
-    if (__any(z) && (threadIdx.x & 63) == 0) atomicOr(any_zero, 1u);  // every lane is live here (no early return)
+    // the call's stamp, not a flag: the word needs no zeroing launch before the forward, and a stale value (another
+    // call's stamp) reads as "no zero" in the backward, which compares with its own call's stamp
+    if (__any(z) && (threadIdx.x & 63) == 0) *zero_stamp = stamp;  // every lane is live here (no early return)
 }
 __global__ void __launch_bounds__(256) k_row_prod_bwd(uint32_t N, uint32_t M, const float* __restrict__ x,
                                                       const float* __restrict__ prod, const float* __restrict__ dprod,
-                                                      const uint32_t* __restrict__ any_zero, float* __restrict__ dx) {
+                                                      const uint32_t* __restrict__ zero_stamp, uint32_t stamp,
+                                                      float* __restrict__ dx) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= N) return;
     const float* r = x + (size_t)i * M;
     float* d = dx + (size_t)i * M;
     const float g = dprod[i];
-    if (*any_zero == 0u) {
+    if (*zero_stamp != stamp) {
         const float p = prod[i];
         for (uint32_t k = 0; k < M; k++) d[k] = g * (p / r[k]);
         return;
@@ -569,12 +574,13 @@ void launch_activate_bwd(uint32_t N, const float* o, const float* sc, const floa
                                                         stamp);
 }
 
-void launch_row_prod_fwd(uint32_t N, uint32_t M, const float* x, float* prod, uint32_t* any_zero, hipStream_t s) {
-    if (N) k_row_prod_fwd<<<(N + 255) / 256, 256, 0, s>>>(N, M, x, prod, any_zero);
+void launch_row_prod_fwd(uint32_t N, uint32_t M, const float* x, float* prod, uint32_t* zero_stamp, uint32_t stamp,
+                         hipStream_t s) {
+    if (N) k_row_prod_fwd<<<(N + 255) / 256, 256, 0, s>>>(N, M, x, prod, zero_stamp, stamp);
 }
 void launch_row_prod_bwd(uint32_t N, uint32_t M, const float* x, const float* prod, const float* dprod,
-                         const uint32_t* any_zero, float* dx, hipStream_t s) {
-    if (N) k_row_prod_bwd<<<(N + 255) / 256, 256, 0, s>>>(N, M, x, prod, dprod, any_zero, dx);
+                         const uint32_t* zero_stamp, uint32_t stamp, float* dx, hipStream_t s) {
+    if (N) k_row_prod_bwd<<<(N + 255) / 256, 256, 0, s>>>(N, M, x, prod, dprod, zero_stamp, stamp, dx);
 }
 
 uint32_t clamp_l1_blocks(uint32_t n) { return (n + 256u * L1_PER_THREAD - 1) / (256u * L1_PER_THREAD); }

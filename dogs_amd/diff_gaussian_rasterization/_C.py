@@ -157,6 +157,56 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, ddc, dsh, dscales, drot, depth
 
 
+class BackwardPlan:
+    """What rasterize_gaussians_backward builds before its C call -- the argument struct, the ten gradient outputs (one
+    buffer) and the DG_BUF_BACKWARD scratch (through dg_fixed_alloc, no allocation callback) -- made by the autograd
+    forward right after its C call returns, while the GPU renders and the host would otherwise wait: the backward
+    (rasterize_gaussians_backward_planned) is then one C call, and the GPU does not idle while Python prepares it."""
+    __slots__ = ("a", "keep", "outs", "scratch", "fixed", "P")
+
+
+def backward_plan(background, means3D, colors, opacities, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+                  projmatrix, tan_fovx, tan_fovy, image_height, image_width, dc, sh, degree, campos, antialiasing, debug,
+                  num_rendered):
+    """A BackwardPlan for the forward just made with these arguments (num_rendered: its return), or None (P = 0)."""
+    P = int(means3D.size(0))
+    if P == 0:
+        return None
+    dev = means3D.device
+    M = _sh_m(sh)
+    fopt = dict(dtype=torch.float32, device=dev)
+    shapes = [(P, 3), (P, 3), (P, 1), (P, 3), (P, 6), (P, 1, 3), (P, M, 3), (P, 3), (P, 4), (P, 1)]
+    sizes = [math.prod(sh) for sh in shapes]
+    pl = BackwardPlan()
+    with _lib.device_ctx(dev):
+        buf = torch.empty(sum(sizes), **fopt)
+        pl.outs = tuple(t.view(sh) for t, sh in zip(torch.split(buf, sizes), shapes))
+        pl.a, pl.keep = _args(P, degree, M, int(image_width), int(image_height), background, means3D, colors, opacities,
+                              scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
+                              tan_fovy, dc, sh, campos, False, antialiasing, debug)
+        nbytes = int(_lib.load().dg_backward_scratch_bytes(C.byref(pl.a), int(num_rendered)))
+        pl.scratch = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+    pl.fixed = _lib.DgFixedBuffer(pl.scratch.data_ptr(), nbytes)
+    pl.P = P
+    return pl
+
+
+def rasterize_gaussians_backward_planned(plan, radii, dL_dout_color, dL_dout_invdepth, geomBuffer, R, binningBuffer,
+                                         imageBuffer, B, sampleBuffer):
+    """rasterize_gaussians_backward with a BackwardPlan: the same C call and outputs (dmeans2D, dcolors, dopacity,
+    dmeans3D, dcov3D, ddc, dsh, dscales, drot, depth); dL_dout_invdepth may be None (zeros)."""
+    dev = radii.device
+    gc = _f32(dL_dout_color)
+    gi = _f32(dL_dout_invdepth) if dL_dout_invdepth is not None else None
+    o = plan.outs
+    _lib.check(_lib.load().dg_rasterize_backward(
+        C.byref(plan.a), radii.data_ptr(), geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
+        _lib.ptr(sampleBuffer), int(R), int(B), gc.data_ptr(), _lib.ptr(gi), o[0].data_ptr(), o[1].data_ptr(),
+        o[2].data_ptr(), o[3].data_ptr(), o[4].data_ptr(), o[5].data_ptr(), _lib.ptr(o[6]), o[7].data_ptr(),
+        o[8].data_ptr(), o[9].data_ptr(), _lib.fixed_alloc_fn(), C.byref(plan.fixed), _lib.stream_of(dev)))
+    return o
+
+
 def mark_visible(means3D, viewmatrix, projmatrix):
     """markVisible (rasterize_points.cu:254-273)."""
     _lib.require_device(means3D, "means3D")

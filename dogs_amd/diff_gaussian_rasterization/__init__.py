@@ -9,6 +9,7 @@ The numerical work runs in libdogs_hip.so (gfx950 HIP kernels) through the `_C` 
 """
 from __future__ import annotations
 
+import threading
 from typing import NamedTuple
 
 import torch
@@ -23,8 +24,14 @@ def cpu_deep_copy_tuple(input_tuple):
     return tuple(item.cpu().clone() if isinstance(item, torch.Tensor) else item for item in input_tuple)
 
 
+# whether the caller's grad mode was on at apply time (inside Function.forward grad mode is always off, and
+# ctx.needs_input_grad reports requires_grad even under torch.no_grad): only then is the backward prepared
+_GRAD_MODE = threading.local()
+
+
 def rasterize_gaussians(means3D, means2D, dc, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                         raster_settings):
+    _GRAD_MODE.on = torch.is_grad_enabled()
     return _RasterizeGaussians.apply(means3D, means2D, dc, sh, colors_precomp, opacities, scales, rotations,
                                      cov3Ds_precomp, raster_settings)
 
@@ -48,12 +55,23 @@ class _RasterizeGaussians(torch.autograd.Function):
         else:
             out = _C.rasterize_gaussians(*args)
         num_rendered, num_buckets, color, invdepths, radii, geomBuffer, binningBuffer, imgBuffer, sampleBuffer = out
+        # the backward's arguments, outputs and scratch, prepared now: the GPU is still rendering this view, so this
+        # host work is hidden here and off the backward's launch path
+        ctx.plan = None
+        if not rs.debug and getattr(_GRAD_MODE, "on", True) and any(ctx.needs_input_grad):
+            ctx.plan = _C.backward_plan(rs.bg, means3D, colors_precomp, opacities, scales, rotations, rs.scale_modifier,
+                                        cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy,
+                                        rs.image_height, rs.image_width, dc, sh, rs.sh_degree, rs.campos,
+                                        rs.antialiasing, rs.debug, num_rendered)
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered
         ctx.num_buckets = num_buckets
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, dc, sh, opacities,
                               geomBuffer, binningBuffer, imgBuffer, sampleBuffer)
         ctx.mark_non_differentiable(radii)
+        # an unused output's gradient arrives as None instead of a zero-filled tensor (the inverse depth is usually
+        # unused: a 1 x H x W fill, and another for radii, per backward); None is passed to the library as NULL
+        ctx.set_materialize_grads(False)
         return color, radii, invdepths
 
     @staticmethod
@@ -61,20 +79,29 @@ class _RasterizeGaussians(torch.autograd.Function):
         rs = ctx.raster_settings
         (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, dc, sh, opacities, geomBuffer,
          binningBuffer, imgBuffer, sampleBuffer) = ctx.saved_tensors
-        args = (rs.bg, means3D, radii, colors_precomp, opacities, scales, rotations, rs.scale_modifier,
-                cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, dc, sh,
-                grad_out_depth, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer,
-                ctx.num_buckets, sampleBuffer, rs.antialiasing, rs.debug)
-        if rs.debug:
-            cpu_args = cpu_deep_copy_tuple(args)
-            try:
-                g = _C.rasterize_gaussians_backward(*args)
-            except Exception as ex:
-                torch.save(cpu_args, "snapshot_bw.dump")
-                print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
-                raise ex
+        if grad_out_color is None:
+            grad_out_color = torch.zeros((3, rs.image_height, rs.image_width), dtype=torch.float32,
+                                         device=means3D.device)
+        if ctx.plan is not None:
+            g = _C.rasterize_gaussians_backward_planned(ctx.plan, radii, grad_out_color, grad_out_depth, geomBuffer,
+                                                        ctx.num_rendered, binningBuffer, imgBuffer, ctx.num_buckets,
+                                                        sampleBuffer)
+            ctx.plan = None
         else:
-            g = _C.rasterize_gaussians_backward(*args)
+            args = (rs.bg, means3D, radii, colors_precomp, opacities, scales, rotations, rs.scale_modifier,
+                    cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, dc, sh,
+                    grad_out_depth, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer,
+                    ctx.num_buckets, sampleBuffer, rs.antialiasing, rs.debug)
+            if rs.debug:
+                cpu_args = cpu_deep_copy_tuple(args)
+                try:
+                    g = _C.rasterize_gaussians_backward(*args)
+                except Exception as ex:
+                    torch.save(cpu_args, "snapshot_bw.dump")
+                    print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
+                    raise ex
+            else:
+                g = _C.rasterize_gaussians_backward(*args)
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_dc, grad_sh,
          grad_scales, grad_rotations, depth) = g
 

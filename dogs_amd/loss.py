@@ -4,9 +4,13 @@ dg_clamp_l1_forward / dg_clamp_l1_backward (optim.hip k_clamp_l1_*).  The clampe
 SSIM term reads it and its gradient joins the L1 gradient and the clamp mask in the same backward pass."""
 from __future__ import annotations
 
+import itertools
+
 import torch
 
 from . import _lib
+
+_STAMPS = itertools.count(1)
 
 
 class _ClampL1(torch.autograd.Function):
@@ -28,8 +32,11 @@ class _ClampL1(torch.autograd.Function):
         with _lib.device_ctx(x.device):
             _lib.check(L.dg_clamp_l1_forward(n, x.data_ptr(), g.data_ptr(), out.data_ptr(), partial.data_ptr(),
                                              _lib.stream_of(x.device)))
-        l1 = partial.sum() / n
+            # the mean in one launch, in a fixed order (torch's partial.sum() / n took two)
+            l1 = torch.empty((), dtype=torch.float32, device=x.device)
+            _lib.check(L.dg_mean_of_parts(partial.data_ptr(), max(nb, 1), n, l1.data_ptr(), _lib.stream_of(x.device)))
         ctx.save_for_backward(x, out, g)
+        ctx.set_materialize_grads(False)   # an unused output's gradient stays None (NULL to the kernel), not a fill
         return out, l1
 
     @staticmethod
@@ -54,7 +61,8 @@ def clamp_l1(image: torch.Tensor, gt: torch.Tensor):
 class _RowProd(torch.autograd.Function):
     """torch.prod(x, dim=1) for x [N, M <= 3] through dg_row_prod_forward / dg_row_prod_backward: the same values and
     gradients as torch's, without prod_backward's host read of the zero count (a stream sync in the middle of every
-    training backward; the kernels keep the zero test on the device)."""
+    training backward; the kernels keep the zero test on the device: the forward stamps a device word with the call's
+    stamp when some element is 0, the backward compares it with the same stamp)."""
 
     @staticmethod
     def forward(ctx, x):
@@ -65,11 +73,13 @@ class _RowProd(torch.autograd.Function):
         xc = x.detach().contiguous()
         n, m = int(xc.size(0)), int(xc.size(1))
         prod = torch.empty(n, dtype=torch.float32, device=x.device)
-        flag = torch.empty(1, dtype=torch.int32, device=x.device)
+        flag = torch.empty(1, dtype=torch.int32, device=x.device)   # the zero stamp: not zeroed (no memset launch)
+        stamp = next(_STAMPS) & 0xFFFFFFFF or 1
         with _lib.device_ctx(x.device):
-            _lib.check(_lib.load().dg_row_prod_forward(n, m, xc.data_ptr(), prod.data_ptr(), flag.data_ptr(),
+            _lib.check(_lib.load().dg_row_prod_forward(n, m, xc.data_ptr(), prod.data_ptr(), flag.data_ptr(), stamp,
                                                        _lib.stream_of(x.device)))
         ctx.save_for_backward(xc, prod, flag)
+        ctx.stamp = stamp
         return prod
 
     @staticmethod
@@ -80,7 +90,8 @@ class _RowProd(torch.autograd.Function):
         dx = torch.empty_like(xc)
         with _lib.device_ctx(xc.device):
             _lib.check(_lib.load().dg_row_prod_backward(n, m, xc.data_ptr(), prod.data_ptr(), gc.data_ptr(),
-                                                        flag.data_ptr(), dx.data_ptr(), _lib.stream_of(xc.device)))
+                                                        flag.data_ptr(), ctx.stamp, dx.data_ptr(),
+                                                        _lib.stream_of(xc.device)))
         return dx
 
 

@@ -145,13 +145,15 @@ int dg_clamp_l1_backward(uint32_t n, const float* img, const float* clamped, con
                          const float* g_l1, float* d_img, dg_stream_t stream);
 
 /* torch.prod(x, dim=1) of x [N, M], 1 <= M <= 3 -- the scale regulariser lambda_scale * get_scaling.prod(dim=1).mean()
- * (gaussian_trainer.py:405-408) -- in torch's row order (x0 x2) x1 on the GPU, and *any_zero (device word, zeroed here) = 1
- * when some element is 0.  The backward is torch's prod_backward (FunctionsManual.cpp) with the zero test on the device
- * instead of a host read: dx = dprod (prod / x) when *any_zero == 0, else for every row dprod (exclusive left cumprod x
+ * (gaussian_trainer.py:405-408) -- in torch's row order (x0 x2) x1 on the GPU; when some element is 0 the forward
+ * writes `stamp` to the device word *zero_stamp (not zeroed: give every forward a stamp of its own, e.g. a counter).
+ * The backward is torch's prod_backward (FunctionsManual.cpp) with the zero test on the device instead of a host read:
+ * dx = dprod (prod / x) when *zero_stamp != stamp (the forward's), else for every row dprod (exclusive left cumprod x
  * exclusive right cumprod). */
-int dg_row_prod_forward(uint32_t N, uint32_t M, const float* x, float* prod, uint32_t* any_zero, dg_stream_t stream);
+int dg_row_prod_forward(uint32_t N, uint32_t M, const float* x, float* prod, uint32_t* zero_stamp, uint32_t stamp,
+                        dg_stream_t stream);
 int dg_row_prod_backward(uint32_t N, uint32_t M, const float* x, const float* prod, const float* dprod,
-                         const uint32_t* any_zero, float* dx, dg_stream_t stream);
+                         const uint32_t* zero_stamp, uint32_t stamp, float* dx, dg_stream_t stream);
 
 /* GaussianSplatModel activations (gaussian_splat_model.py get_opacity / get_scaling / get_quaternion): opacity =
  * sigmoid(raw_opacity) [N,1], scaling = exp(raw_scaling) [N,3], rotation = raw_rotation / max(|raw_rotation|, 1e-12)
@@ -332,6 +334,24 @@ int dg_fused_ssim_backward(int B, int CH, int H, int W, float C1, float C2, cons
                            const float* dL_dmap, const float* dm_dmu1, const float* dm_dsigma1_sq,
                            const float* dm_dsigma12, float* dL_dimg1, dg_stream_t stream);
 
+/* fused_ssim(img1, img2) with padding "same" (fused_ssim/__init__.py:35-41: FusedSSIMMap(...).mean()) in one pass:
+ * *mean (device) = the mean of the SSIM map, which is never written -- per-wave partial sums into part
+ * [dg_fused_ssim_parts(B, CH, H, W)] (scratch), totalled in a fixed order and divided by B CH H W (the native training
+ * step's SSIM term, bit for bit).  dm_* as dg_fused_ssim_forward (NULL <=> train == false). */
+uint32_t dg_fused_ssim_parts(int B, int CH, int H, int W);
+int dg_fused_ssim_mean(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,
+                       float* dm_dmu1, float* dm_dsigma1_sq, float* dm_dsigma12, float* part, float* mean,
+                       dg_stream_t stream);
+/* Its backward: dL/dimg1 for the mean's incoming gradient *dL_dmean (device scalar); dL/dmap = *dL_dmean / (B CH H W),
+ * torch's mean backward, is never materialised (the reference path expands it into a full map first). */
+int dg_fused_ssim_mean_backward(int B, int CH, int H, int W, const float* img1, const float* img2,
+                                const float* dL_dmean, const float* dm_dmu1, const float* dm_dsigma1_sq,
+                                const float* dm_dsigma12, float* dL_dimg1, dg_stream_t stream);
+
+/* *out (device) = sum(part[0..n_part)) / denom in a fixed order (strided over 256 threads, the 64-lane sums, then
+ * (w0 + w1) + (w2 + w3)): the mean from per-block partial sums, e.g. dg_clamp_l1_forward's (the L1 term). */
+int dg_mean_of_parts(const float* part, uint32_t n_part, uint32_t denom, float* out, dg_stream_t stream);
+
 /* Replaces distCUDA2 (simple-knn/spatial.cu:18-35): mean squared distance to the 3 nearest
  * neighbours (approximate, Morton boxes).  out [P].  Allocates DG_BUF_TEMP. */
 int dg_dist_cuda2(int P, const float* points, float* out, dg_alloc_fn alloc, void* user, dg_stream_t stream);
@@ -340,6 +360,18 @@ int dg_dist_cuda2(int P, const float* points, float* out, dg_alloc_fn alloc, voi
 uint64_t dg_geom_bytes(int P);
 uint64_t dg_image_bytes(int W, int H);
 uint64_t dg_binning_bytes(int64_t K, int W, int H);
+
+/* Bytes dg_rasterize_backward will request as DG_BUF_BACKWARD after a forward that returned num_rendered (the caller can
+ * allocate them while the forward's render runs). */
+uint64_t dg_backward_scratch_bytes(const dg_raster_args* a, int64_t num_rendered);
+/* A dg_alloc_fn over one caller-owned device buffer (user: dg_fixed_buffer*): every request gets ptr when it fits, NULL
+ * (an error) when it does not.  Passing this C function instead of a host-language callback takes the allocation
+ * round trip out of the call (the drop-in backward prepares its scratch during the forward). */
+typedef struct {
+    void* ptr;
+    uint64_t bytes;
+} dg_fixed_buffer;
+void* dg_fixed_alloc(void* user, int which, uint64_t nbytes);
 
 /* Introspection of the private forward state, for parity tests (device output pointers):
  * the binned (tile, Gaussian) instance lists -- phase 1 (*e1 entries) then phase 2 (dg_binned_instances - *e1),

@@ -63,6 +63,27 @@ def test_fused_ssim_matches_oracle(oracle, hip_device, B, C, H, W):
     assert rel_err(gh.cpu().numpy(), go) < 1e-5
 
 
+@pytest.mark.parametrize("B,C,H,W", [(1, 3, 37, 53), (2, 1, 64, 64), (1, 2, 5, 119), (1, 3, 1080, 1920)])
+def test_fused_ssim_mean_matches_map_route(hip_device, B, C, H, W):
+    """fused_ssim(padding="same") runs FusedSSIMMean (the map's mean summed in the kernel, the backward from the mean's
+    scalar gradient): its value equals FusedSSIMMap(...).mean() to float association (a fixed-order sum of per-wave
+    partials vs torch's mean), its gradient equals the map route's bit for bit (dL/dmap = g / numel either way), and
+    train=False gives the same value without the partial maps."""
+    from fused_ssim import FusedSSIMMap, fused_ssim
+    g = torch.Generator().manual_seed(H + W)
+    a = torch.rand((B, C, H, W), generator=g).to(hip_device)
+    b = (a.cpu() + 0.1 * torch.randn((B, C, H, W), generator=g)).clamp(0, 1).to(hip_device)
+    x1, x2 = a.clone().requires_grad_(True), a.clone().requires_grad_(True)
+    v = fused_ssim(x1, b)
+    m = FusedSSIMMap.apply(0.01 ** 2, 0.03 ** 2, x2, b, "same", True).mean()
+    assert v.dim() == 0 and v.dtype == torch.float32
+    assert abs(v.item() - m.item()) <= 2e-6 * abs(m.item()) + 1e-7, (v.item(), m.item())
+    (-0.2 * v).backward()
+    (-0.2 * m).backward()
+    assert torch.equal(x1.grad, x2.grad)
+    assert torch.equal(fused_ssim(a, b, train=False), v.detach())
+
+
 def test_fused_ssim_autograd_valid_padding(oracle, hip_device):
     from fused_ssim import fused_ssim
     g = torch.Generator().manual_seed(3)
@@ -153,6 +174,22 @@ def test_gaussian_rasterizer_autograd(oracle, hip_device):
     for k, o in pairs.items():
         assert rel_err(leaf[k].grad.cpu().numpy().reshape(go[o].shape), go[o]) < 1e-4, k
     assert rel_err(means2D.grad.cpu().numpy(), go["dmeans2D"]) < 1e-4
+    # only the inverse depth in the loss: the image's gradient arrives as None (set_materialize_grads(False)) and
+    # counts as zeros; and the image alone again, the inverse depth's gradient None -> NULL to the library
+    ginv = (0.1 * gen.standard_normal((1, H, W))).astype(np.float32)
+    for use_img, use_inv in ((False, True), (True, False)):
+        for t in leaf.values():
+            t.grad = None
+        means2D = torch.zeros_like(leaf["means3D"], requires_grad=True)
+        img, radii, invd = r(leaf["means3D"], means2D, leaf["opacities"], dc=leaf["dc"], shs=leaf["sh"],
+                             scales=leaf["scales"], rotations=leaf["rotations"])
+        loss = (invd * torch.from_numpy(ginv).to(hip_device)).sum() if use_inv else \
+            (img * torch.from_numpy(gc).to(hip_device)).sum()
+        loss.backward()
+        go = sto.backward(gc if use_img else np.zeros_like(gc), ginv[0] if use_inv else np.zeros((H, W), np.float32))
+        for k, o in pairs.items():
+            assert rel_err(leaf[k].grad.cpu().numpy().reshape(go[o].shape), go[o]) < 1e-4, (k, use_img)
+        assert rel_err(means2D.grad.cpu().numpy(), go["dmeans2D"]) < 1e-4
 
 
 @pytest.mark.parametrize("prefix", [0, 2], ids=["prefix-default", "prefix-2-per-tile"])
@@ -202,7 +239,9 @@ def test_row_prod_matches_torch_prod(hip_device, M):
     x = torch.exp(torch.randn((100_003, M), generator=g) * 4)
     x[5, 0] = 1e-30
     gout = torch.randn(x.shape[0], generator=g).to(hip_device)
-    for zeros in ((), ((77, M - 1),), ((1234, 0), (1234, M - 1), (9, 0))):
+    # zeros, then none again: the forward stamps its own call's value, so a stale stamp left in a reused word reads as
+    # "no zero"
+    for zeros in ((), ((77, M - 1),), ((1234, 0), (1234, M - 1), (9, 0)), ()):
         xx = x.clone()
         for r, c in zeros:
             xx[r, c] = 0.0
