@@ -7,7 +7,7 @@ OUT=${1:-gpurun_out/prof}
 ROOT=$(pwd)
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="$ROOT/bench.py --steps 16 --warmup 8 --no-cpu-baseline --no-train-step --no-reference-k --no-admm"
+BENCH="$ROOT/bench.py --steps 16 --warmup 8 --no-cpu-baseline --no-train-step --no-reference-k --no-admm --no-sweep"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH > "$OUT/trace.log" 2>&1
 if [ "$2" = "pmc" ]; then
   i=0
