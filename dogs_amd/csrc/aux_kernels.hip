@@ -351,12 +351,13 @@ __global__ void __launch_bounds__(256) k_ssim_bwd_strip(int H, int W, int planes
                     }
                     if (out_col) {
                         const size_t gi = plane + (size_t)y * W + ox;
-                        const float i1 = img1[gi], i2 = img2[gi];
+                        // FUSED: the clamped image is clamp01f(raw) (the forward wrote exactly that): read raw once
+                        const float x = FUSED ? raw[gi] : 0.0f;
+                        const float i1 = FUSED ? clamp01f(x) : img1[gi], i2 = img2[gi];
                         float d = v0;
                         d += (i1 * 2.0f) * v1;
                         d += i2 * v2;
                         if (FUSED) {
-                            const float x = raw[gi];
                             const float mk = MASK ? mask[gi] : 1.0f;
                             const float e = MASK ? i1 * mk - i2 : i1 - i2;
                             const float sg = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);

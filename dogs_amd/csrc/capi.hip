@@ -380,7 +380,8 @@ void adapt(CapProbe* ac, uint32_t prev_unfinished, uint32_t prev_k2, uint32_t e1
 
 struct BwdScratch {
     float* rec;
-    uint32_t *live_list, *live_cnt;  // contributing Gaussians per record-sum chunk (k_gauss_sum -> k_gauss_live)
+    uint2* live_list;                // contributing (slot, Gaussian) per record-sum chunk (k_gauss_sum -> k_gauss_live)
+    uint32_t* live_cnt;
     uint32_t* invd_flag;
     size_t bytes;
 };
@@ -390,7 +391,7 @@ BwdScratch carve_bwd(void* base, int64_t K, int P, int T) {
     const size_t n = (size_t)(K > 0 ? K : 1);
     s.rec = c.take<float>((size_t)gs::REC_STRIDE * n);
     const size_t chunks = (n + gs::SUM_CHUNK - 1) / gs::SUM_CHUNK;  // every slot < K
-    s.live_list = c.take<uint32_t>(chunks * gs::SUM_CHUNK);
+    s.live_list = c.take<uint2>(chunks * gs::SUM_CHUNK);
     s.live_cnt = c.take<uint32_t>(chunks);
     s.invd_flag = c.take<uint32_t>(4);
     (void)T;
@@ -1448,7 +1449,7 @@ int dg_clamp_l1_forward(uint32_t n, const float* img, const float* gt, float* cl
 int dg_clamp_l1_backward(uint32_t n, const float* img, const float* clamped, const float* gt, const float* g_clamped,
                          const float* g_l1, float* d_img, dg_stream_t stream) {
     if (n == 0) return 0;
-    if (!img || !clamped || !gt || !d_img) return fail("clamp_l1 backward: NULL tensor%s%d");
+    if (!img || !gt || !d_img) return fail("clamp_l1 backward: NULL tensor%s%d");  // clamped: recomputed, may be NULL
     gs::launch_clamp_l1_bwd(n, img, clamped, gt, g_clamped, g_l1, d_img, (hipStream_t)stream);
     HIP_OK(hipGetLastError());
     return 0;

@@ -155,9 +155,11 @@ struct GaussBwdArgs {
     const uint32_t* eg2;     // null: no phase-2 block
     const uint32_t* counters;  // CNT_E1, CNT_K2
     uint32_t K1;             // phase-1 capacity (the forward's num_instances token)
-    // k_gauss_sum -> k_gauss_live: per chunk, the contributing Gaussians' last instance slots
-    // (live_list[chunk * SUM_CHUNK + j], j < live_cnt[chunk]); their record sums + index overwrite that record
-    uint32_t* live_list;     // [chunks * SUM_CHUNK]
+    // k_gauss_sum -> k_gauss_live: per chunk, the contributing Gaussians as (last instance slot, Gaussian index)
+    // (live_list[chunk * SUM_CHUNK + j], j < live_cnt[chunk]); their record sums overwrite that slot's record.  The
+    // index rides along so that k_gauss_live loads the sums and every per-Gaussian input in one round trip (no owner
+    // lookup between them)
+    uint2* live_list;        // [chunks * SUM_CHUNK]
     uint32_t* live_cnt;      // [chunks]
 };
 // floats per instance record: the 10 moments of backward.cu's per-splat terms (40 B; the sum pass overwrites a

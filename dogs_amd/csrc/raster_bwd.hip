@@ -475,7 +475,7 @@ __device__ __forceinline__ bool sum_step(const GaussBwdArgs& a, uint32_t i0, uin
     if (live) {
         store_rec(a.rec, e, v);
         const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-        a.live_list[(size_t)lo + st.nlive + (uint32_t)__popcll(lm & lt)] = e;
+        a.live_list[(size_t)lo + st.nlive + (uint32_t)__popcll(lm & lt)] = make_uint2(e, own);
     }
     st.nlive += (uint32_t)__popcll(lm);
     // lane 63's segment stays open when it continues into the next step
@@ -639,10 +639,9 @@ __global__ void __launch_bounds__(LIVE_THREADS) k_gauss_live(GaussBwdArgs a) {
 #pragma unroll
             for (int st = LIVE_CHUNKS / 2; st > 0; st >>= 1)
                 if (s_pre[k + st] <= j) k += st;
-            const uint32_t e = a.live_list[(size_t)(c0 + k) * SUM_CHUNK + (j - s_pre[k])];
-            const Rec10 r = load_rec(a.rec, e);       // the Gaussian's 10 sums (k_gauss_sum wrote them here)
-            const int idx = (int)min(inst_owner(a, e, R.E1), (uint32_t)a.P - 1u);
-            if (a.radii[idx] > 0) gauss_bwd_one(a, idx, r.v);
+            const uint2 le = a.live_list[(size_t)(c0 + k) * SUM_CHUNK + (j - s_pre[k])];
+            const Rec10 r = load_rec(a.rec, le.x);    // the Gaussian's 10 sums (k_gauss_sum wrote them here)
+            gauss_bwd_one(a, (int)min(le.y, (uint32_t)a.P - 1u), r.v);
         }
         __syncthreads();
     }
@@ -780,6 +779,8 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, co
         }
         shv[44] = shp[44];
     }
+    // a Gaussian with instances was rendered (radii > 0); tested after the input loads are issued, not before them
+    if (a.radii[idx] <= 0) return;
     // ---- records -> dL/d(mean2D, conic, opacity, color, invdepth): summed by the wave (see below)
     float acc[10];
 #pragma unroll

@@ -136,8 +136,9 @@ typedef struct {
 
 /* The view's photometric L1 term (gaussian_trainer.py: rendered_image.clamp(0, 1), l1_loss(image, gt) = mean |image -
  * gt|): clamped [n] and per-block partial sums of |clamped - gt| (partial [dg_clamp_l1_blocks(n)]; the caller sums
- * them and divides by n).  Backward: d_img = (g_clamped + *g_l1 * sgn(clamped - gt) / n) where 0 <= img <= 1, else 0
- * (g_clamped, g_l1: device, NULL = zero).  img, gt, clamped 16-byte aligned. */
+ * them and divides by n, e.g. with dg_mean_of_parts).  Backward: d_img = (g_clamped + *g_l1 * sgn(clamp(img) - gt) / n)
+ * where 0 <= img <= 1, else 0 (g_clamped, g_l1: device, NULL = zero; `clamped` is not read -- the clamp is recomputed
+ * from img -- and may be NULL).  img, gt, clamped 16-byte aligned. */
 uint32_t dg_clamp_l1_blocks(uint32_t n);
 int dg_clamp_l1_forward(uint32_t n, const float* img, const float* gt, float* clamped, float* partial,
                         dg_stream_t stream);
