@@ -192,6 +192,54 @@ def test_gaussian_rasterizer_autograd(oracle, hip_device):
         assert rel_err(means2D.grad.cpu().numpy(), go["dmeans2D"]) < 1e-4
 
 
+def test_planned_backward_equals_direct_call(hip_device):
+    """_RasterizeGaussians prepares its backward during the forward (_C.backward_plan: outputs, argument struct and the
+    DG_BUF_BACKWARD scratch through dg_fixed_alloc); its gradients equal the direct _C.rasterize_gaussians_backward
+    call's bit for bit, with and without an inverse-depth gradient (each forward under a fresh capacity context, so both
+    bin with the same phase-1 capacity), and a no_grad forward renders the same image."""
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from dogs_amd.diff_gaussian_rasterization import _C
+    n, W, H = 3000, 200, 150
+    s = small_scene(n, W, H, seed=41)
+    c = s.camera.to(hip_device)
+    bg = torch.tensor([0.0, 0.0, 0.0], device=hip_device)
+    st = GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=c.tanfovx, tanfovy=c.tanfovy, bg=bg,
+                                       scale_modifier=1.0, viewmatrix=c.world_to_camera,
+                                       projmatrix=c.projective_matrix, sh_degree=3, campos=c.camera_center,
+                                       prefiltered=False, debug=False, antialiasing=False, depth_threshold=0.0)
+    r = GaussianRasterizer(st)
+    gen = torch.Generator().manual_seed(2)
+    gc = torch.randn((3, H, W), generator=gen).to(hip_device)
+    gi = (0.1 * torch.randn((1, H, W), generator=gen)).to(hip_device)
+    d = {k: getattr(s, k).to(hip_device).contiguous() for k in ("means3D", "opacities", "scales", "rotations", "dc", "sh")}
+    e = torch.empty(0, device=hip_device)
+    for use_inv in (False, True):
+        leaf = {k: v.clone().requires_grad_(True) for k, v in d.items()}
+        m2d = torch.zeros_like(leaf["means3D"], requires_grad=True)
+        with _C.capacity_context(_C.new_capacity_context()):
+            img, radii, invd = r(leaf["means3D"], m2d, leaf["opacities"], dc=leaf["dc"], shs=leaf["sh"],
+                                 scales=leaf["scales"], rotations=leaf["rotations"])
+        loss = (img * gc).sum() + ((invd * gi).sum() if use_inv else 0.0)
+        loss.backward()
+        with _C.capacity_context(_C.new_capacity_context()):
+            out = _C.rasterize_gaussians(bg, d["means3D"], e, d["opacities"], d["scales"], d["rotations"], 1.0, e,
+                                         c.world_to_camera, c.projective_matrix, c.tanfovx, c.tanfovy, H, W, d["dc"],
+                                         d["sh"], 3, c.camera_center, False, False, False)
+        g = _C.rasterize_gaussians_backward(bg, d["means3D"], out[4], e, d["opacities"], d["scales"], d["rotations"],
+                                            1.0, e, c.world_to_camera, c.projective_matrix, c.tanfovx, c.tanfovy, gc,
+                                            d["dc"], d["sh"], gi if use_inv else None, 3, c.camera_center, out[5],
+                                            out[0], out[6], out[7], out[1], out[8], False, False)
+        torch.cuda.synchronize()
+        assert torch.equal(m2d.grad, g[0])
+        for k, gk in (("opacities", g[2]), ("means3D", g[3]), ("dc", g[5]), ("sh", g[6]), ("scales", g[7]),
+                      ("rotations", g[8])):
+            assert torch.equal(leaf[k].grad, gk.reshape(leaf[k].shape)), (k, use_inv)
+    with torch.no_grad(), _C.capacity_context(_C.new_capacity_context()):
+        img2, _, _ = r(d["means3D"], torch.zeros_like(d["means3D"]), d["opacities"], dc=d["dc"], shs=d["sh"],
+                       scales=d["scales"], rotations=d["rotations"])
+    assert torch.equal(img2, img.detach())
+
+
 @pytest.mark.parametrize("prefix", [0, 2], ids=["prefix-default", "prefix-2-per-tile"])
 def test_count_mode_matches_oracle(oracle, hip_device, prefix):
     """LightGaussian count mode (GaussianRasterizationSettings(f_count=True), as count_render,
