@@ -104,3 +104,20 @@ def test_clamp_l1_matches_torch(hip_device):
     flat = img.reshape(-1)[1:]                                   # misaligned start
     torch.testing.assert_close(clamp_l1(flat, gt.reshape(-1)[1:])[1], (flat.clamp(0, 1) - gt.reshape(-1)[1:]).abs().mean(),
                                rtol=1e-6, atol=0)
+    # an empty image: the mean is 0 / 0 = nan, as torch's mean of an empty tensor (dg_mean_of_parts over no partials)
+    e = torch.empty((3, 0, 7), device=hip_device)
+    c, l1 = clamp_l1(e, e)
+    assert c.shape == e.shape and bool(torch.isnan(l1)) and l1.dim() == 0
+
+
+def test_fused_ssim_mean_without_train_has_no_backward(hip_device):
+    """fused_ssim(..., train=False) computes the value only (no partial maps, as the reference's forward with
+    train=False); a backward through it raises instead of reading absent maps."""
+    from fused_ssim import fused_ssim
+    g = torch.Generator().manual_seed(9)
+    a = torch.rand((1, 3, 40, 60), generator=g).to(hip_device).requires_grad_(True)
+    b = torch.rand((1, 3, 40, 60), generator=g).to(hip_device)
+    v = fused_ssim(a, b, train=False)
+    assert torch.isfinite(v)
+    with pytest.raises(RuntimeError):
+        v.backward()
