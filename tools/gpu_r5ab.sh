@@ -12,5 +12,5 @@ export TMPDIR=/tmp
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 DOGS_DIST_BACKEND=gloo DOGS_BENCH_SHARE_DEVICE=1 timeout -k 10 ${TO:-850} python -m torch.distributed.run --nnodes 1 \
-    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 tools/admm_rehearsal.py --points "$PTS" \
+    --nproc-per-node ${NPROC:-2} --master-addr 127.0.0.1 --master-port 29533 tools/admm_rehearsal.py --points "$PTS" \
     --width 3840 --height 2160 --admm-pre 100 --admm-interval 100 > "$OUT/rehearsal.json" 2> "$OUT/rehearsal.err"
