@@ -397,6 +397,8 @@ def admm_leg(args, ws, rank, dev, n, W, H):
         out.update({"seconds": round(t_par, 3), "phase_seconds": {k: round(v, 3) for k, v in secs.items()},
                     "views_per_s": round(ws * steps / secs["admm"], 2),
                     "gaussians_per_block_admm": int(r.block.params["xyz"].shape[0]),
+                    **({"entry_stages_s": {k: round(max_over(ws, dev, v), 4) for k, v in r.entry.timings.items()}}
+                       if r.entry.timings else {}),
                     "num_global": r.entry.num_global, "shared_gaussians": r.consensus.num_shared,
                     "consensus_ms": round(1e3 * max(lg.seconds["consensus"] for lg in r.runner.logs), 3),
                     "last_round": {"primal": {k: float(f"{v:.4g}") for k, v in r.runner.logs[-1].primal.items()},

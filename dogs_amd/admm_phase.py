@@ -41,6 +41,8 @@ plumbing with gloo.
 """
 from __future__ import annotations
 
+import os
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -241,6 +243,7 @@ class PhaseEntry:
     num_global: int
     rho_gaussians: int
     fused: GaussianSplatModel
+    timings: dict | None = None  # per stage seconds, with DOGS_ENTRY_TIMING=1 (device-synchronised stage by stage)
 
     def raw(self) -> dict:
         """The sub-model as BlockTrainer's raw dict (dogs_amd.admm.PARAM_NAMES)."""
@@ -262,20 +265,36 @@ def enter_admm_phase(block_model: GaussianSplatModel, camera_blocks: list, ori_p
         raise RuntimeError(f"{len(camera_blocks)} camera blocks for {world} ranks (one block per rank)")
     dev = block_model.get_xyz.device
     bg = torch.zeros(3, dtype=torch.float32, device=dev) if bg is None else bg
+    timings = {} if os.environ.get("DOGS_ENTRY_TIMING") == "1" else None
+    t = [time.perf_counter()]
+
+    def stage(name):
+        if timings is not None:
+            torch.cuda.synchronize(dev)
+            t.append(time.perf_counter())
+            timings[name] = t[-1] - t[-2]
     # 1. every rank clips its own block to its original box (the reference's per-block fuse step), the clipped rows
     #    are all-gathered in block order and every rank builds the same fused model from them
-    rows = all_gather_rows(clip_block(block_model, None if ori_point_bboxes is None else ori_point_bboxes[rank],
-                                      world_to_obb_transform, kernels), group)
+    clipped = clip_block(block_model, None if ori_point_bboxes is None else ori_point_bboxes[rank],
+                         world_to_obb_transform, kernels)
+    stage("clip")
+    rows = all_gather_rows(clipped, group)
+    del clipped
+    stage("gather")
     fused = _fused_model(rows, block_model)
     del rows
+    stage("fuse")
     # 2. importance: this rank renders its cameras only, summed in the reference's order down the rank chain
     imp = ordered_importance(fused, camera_blocks, kernels, bg, group)
+    stage("importance")
     v_imp_prune(fused, imp, cfg, kernels)
     rho_gaussians = fused.num_gaussians
+    stage("prune")
     # 4. the expanded-box split
     vis, gidx, subs = select_gaussians_in_each_block(exp_point_bboxes, fused, world_to_obb_transform, kernels,
                                                      blocks=[rank])
-    return PhaseEntry(subs[rank], gidx[rank], vis, int(vis.shape[0]), rho_gaussians, fused)
+    stage("split")
+    return PhaseEntry(subs[rank], gidx[rank], vis, int(vis.shape[0]), rho_gaussians, fused, timings)
 
 
 def enter_admm_phase_sequential(block_models: list, camera_blocks: list, ori_point_bboxes: list,

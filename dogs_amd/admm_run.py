@@ -149,6 +149,10 @@ def run(cfg: ADMMRunConfig, scene: BlockScene, group=None, device=None, seed: in
     while pre.iteration < n_pre:            # train_every_x_interval chunks (the master's RPC rounds)
         pre.train(cfg.admm.consensus_interval)
     pre.sync()
+    # the entry starts with a collective: without this barrier its time would include the wait for the slowest rank's
+    # pre-phase (the per-phase times are maxima over ranks; the wall clock is the same either way)
+    if dist.get_world_size(group) > 1:
+        dist.barrier(group=group)
     secs["pre_phase"] = time.perf_counter() - t0
     t1 = time.perf_counter()
     pc = PhaseConfig(prune_percent=cfg.gs.prune_percent, v_pow=cfg.gs.prune_v_pow)
