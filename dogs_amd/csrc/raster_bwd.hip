@@ -19,6 +19,10 @@
 
 namespace gs {
 
+#ifdef DG_BWD_STATS  // measurement build only: replay utilisation counters, printed per backward by k_bwd_stats_dump
+__device__ unsigned long long g_bs[256 * 4];
+#endif
+
 __device__ __forceinline__ float bcastf(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
@@ -129,6 +133,18 @@ __device__ __forceinline__ void replay_splat(const RenderBwdArgs& a, const float
     } else {
         p[9] = 0.0f;
     }
+#ifdef DG_BWD_STATS
+    {
+        const uint32_t nok = (uint32_t)__popcll(__ballot(ok[0])) + (uint32_t)__popcll(__ballot(ok[1])) +
+                             (uint32_t)__popcll(__ballot(ok[2])) + (uint32_t)__popcll(__ballot(ok[3]));
+        if (lane == 0) {
+            const uint32_t b = (uint32_t)(blockIdx.x & 255u) * 4u;
+            atomicAdd(&g_bs[b + 0], 1ull);
+            atomicAdd(&g_bs[b + 1], nok ? 1ull : 0ull);
+            atomicAdd(&g_bs[b + 2], (unsigned long long)nok);
+        }
+    }
+#endif
     if (__any(ok[0] || ok[1] || ok[2] || ok[3])) {
         int slot;
         const float tot = wave_reduce10(p, lane, slot);
@@ -933,11 +949,23 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, co
     }
 }
 
+#ifdef DG_BWD_STATS
+__global__ void k_bwd_stats_dump() {
+    unsigned long long t[3] = {0, 0, 0};
+    for (int b = 0; b < 256; b++)
+        for (int i = 0; i < 3; i++) { t[i] += g_bs[b * 4 + i]; g_bs[b * 4 + i] = 0ull; }
+    printf("BWDSTATS iterations %llu any_ok %llu ok_pixels %llu util_of_iter %.4f util_of_anyok %.4f\n", t[0], t[1], t[2],
+           t[0] ? (double)t[2] / (256.0 * (double)t[0]) : 0.0, t[1] ? (double)t[2] / (256.0 * (double)t[1]) : 0.0);
+}
+#endif
 void launch_render_bwd(const RenderBwdArgs& a, uint32_t* counters, hipStream_t s, bool order_ready) {
     (void)counters;
     if (a.num_tiles <= 0) return;
     if (a.order && !order_ready) k_bwd_order<<<1, 1024, 0, s>>>(a);
     k_render_bwd<<<(a.num_tiles + 3) / 4, 256, 0, s>>>(a);
+#ifdef DG_BWD_STATS
+    k_bwd_stats_dump<<<1, 1, 0, s>>>();
+#endif
 }
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
