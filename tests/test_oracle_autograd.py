@@ -37,7 +37,7 @@ def sh_rgb(deg, dc, sh, dirs):
     return r + 0.5
 
 
-def dense_forward(s, lists, W, H, deg, bg=None, extra=None):
+def dense_forward(s, lists, W, H, deg, bg=None, extra=None, antialiasing=False):
     """Returns (loss closure inputs): leaves dict and outputs (color, invdepth, ndc2, rgb, cov6).  bg: the colour
     behind the splats (final colour + T_final bg, forward.cu:575-580); extra (a dict) receives the per-pixel final
     transmittance `T_final` [H,W], `qlog` = sum over the pixel's accepted splats of -log(1 - alpha) [H,W] and the
@@ -94,6 +94,20 @@ def dense_forward(s, lists, W, H, deg, bg=None, extra=None):
     rgb_c.retain_grad()
     invz = 1.0 / pv[:, 2]
     op = leaves["opacities"][:, 0]
+    if antialiasing:
+        # the opacity compensation of the 0.3 px dilation (forward.cu:218-233): sqrt(max(2.5e-5, det / det+)).  Its
+        # gradient is the reference's, not the exact one: backward.cu:212-246 evaluates d(det / det+)/d(xx, xy, yy) --
+        # derived for the undilated entries -- at the DILATED ones (it adds h_var first).  So the value is the true
+        # scaling and the gradient flows through r(xx + 0.3, xy, yy + 0.3), the same function at the shifted point
+        # (the reference's second quirk; exact autograd of the true forward puts dcov3D 64% off it), and none when
+        # the clamp holds.
+        def ratio(a_, b_, c_):
+            return (a_ * c_ - b_ * b_) / ((a_ + 0.3) * (c_ + 0.3) - b_ * b_)
+        r0 = ratio(c2[:, 0, 0], c2[:, 0, 1], c2[:, 1, 1])
+        hs = torch.sqrt(torch.clamp_min(r0, 0.000025)).detach()
+        rs = ratio(c2[:, 0, 0] + 0.3, c2[:, 0, 1], c2[:, 1, 1] + 0.3)
+        live = (r0.detach() > 0.000025).to(rs.dtype)
+        op = op * (hs + live * (rs - rs.detach()) / (2.0 * hs))
     color = torch.zeros((3, H, W), dtype=f64)
     invd = torch.zeros((H, W), dtype=f64)
     tfin = torch.ones((H, W), dtype=f64)
@@ -199,10 +213,12 @@ def rect_tile_lists(s, radii, means2D, W, H):
     return lists
 
 
-@pytest.mark.parametrize("n,W,H,deg,seed,bg", [(60, 64, 48, 3, 5, (0.3, 0.6, 0.9)), (120, 80, 64, 3, 6, (1.0, 0.5, 0.0)),
-                                              (40, 64, 48, 2, 7, (0.0, 0.0, 0.0)),
-                                              (1200, 64, 48, 3, 8, (0.2, 0.4, 0.6))])  # dense: pixels saturate
-def test_oracle_backward_matches_autograd_uncull_bg(oracle, n, W, H, deg, seed, bg):
+@pytest.mark.parametrize("n,W,H,deg,seed,bg,aa", [(60, 64, 48, 3, 5, (0.3, 0.6, 0.9), False),
+                                                 (120, 80, 64, 3, 6, (1.0, 0.5, 0.0), False),
+                                                 (40, 64, 48, 2, 7, (0.0, 0.0, 0.0), False),
+                                                 (150, 64, 48, 3, 9, (0.5, 0.5, 0.5), True),   # anti-aliasing
+                                                 (1200, 64, 48, 3, 8, (0.2, 0.4, 0.6), False)])  # pixels saturate
+def test_oracle_backward_matches_autograd_uncull_bg(oracle, n, W, H, deg, seed, bg, aa):
     """The stronger anchor (bg = 0 only, the oracle's own lists): the dense float64 forward over the
     uncull rect lists above, with a background, differentiated by autograd, against the oracle's restatement of the
     reference backward.  The reference counts the background twice in dL/dalpha (its accumulated colour starts from
@@ -215,10 +231,10 @@ def test_oracle_backward_matches_autograd_uncull_bg(oracle, n, W, H, deg, seed, 
     if n >= 1200:  # dense, large and nearly opaque: ~570 of the 3072 pixels reach the T < 1e-4 stop
         s.opacities = torch.full_like(s.opacities, 0.95)
         s.scales = (s.scales * 7.0).contiguous()
-    col_o, radii_o, inv_o, st = oracle_forward(oracle, s, bg, deg=deg)
+    col_o, radii_o, inv_o, st = oracle_forward(oracle, s, bg, deg=deg, antialiasing=aa)
     lists = rect_tile_lists(s, radii_o, st.geom()["means2D"], W, H)
     extra = {}
-    leaves, color, invd, ndc2, rgb_c, cov6 = dense_forward(s, lists, W, H, deg, bg=bg, extra=extra)
+    leaves, color, invd, ndc2, rgb_c, cov6 = dense_forward(s, lists, W, H, deg, bg=bg, extra=extra, antialiasing=aa)
     np.testing.assert_allclose(color.detach().numpy(), col_o, atol=2e-5)
     np.testing.assert_allclose(invd.detach().numpy(), inv_o[0], atol=2e-5)
     if n >= 1200:  # the dense case reaches the T < 1e-4 stop (forward.cu:560-566) in many pixels
