@@ -188,13 +188,73 @@ def test_oracle_backward_matches_autograd(oracle, n, W, H, deg, seed):
     assert err < 2e-4, f"dmeans2D: rel err {err}"
 
 
+def reference_radii(s, W, H):
+    """forward.cu:196-266 restated in float64: in_frustum (view z > 0.2, auxiliary.h:151-172), the dilated EWA
+    covariance, det != 0, my_radius = ceil(3 sqrt(max(lambda1, lambda2))) with the eigenvalue floor of 0.1, the
+    projected centre ndc2Pix, and radius 0 when getRect's rectangle is empty (auxiliary.h:45-55; its int() truncation
+    equals floor after the clamp at 0).  Returns (radii int64 [P], means2D float64 [P, 2])."""
+    f64 = torch.float64
+    c = s.camera
+    V = c.world_to_camera.to(f64)
+    Pm = c.projective_matrix.to(f64)
+    m = s.means3D.to(f64)
+    ph = torch.cat([m, torch.ones((m.shape[0], 1), dtype=f64)], 1)
+    pv = (ph @ V)[:, :3]
+    pp = ph @ Pm
+    ndc = pp[:, :3] / (pp[:, 3:4] + 1e-7)
+    px = ((ndc[:, 0] + 1.0) * W - 1.0) * 0.5
+    py = ((ndc[:, 1] + 1.0) * H - 1.0) * 0.5
+    q = s.rotations.to(f64)
+    r_, x_, y_, z_ = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    R = torch.stack([1 - 2 * (y_ * y_ + z_ * z_), 2 * (x_ * y_ - r_ * z_), 2 * (x_ * z_ + r_ * y_),
+                     2 * (x_ * y_ + r_ * z_), 1 - 2 * (x_ * x_ + z_ * z_), 2 * (y_ * z_ - r_ * x_),
+                     2 * (x_ * z_ - r_ * y_), 2 * (y_ * z_ + r_ * x_), 1 - 2 * (x_ * x_ + y_ * y_)], 1).reshape(-1, 3, 3)
+    L = R * s.scales.to(f64)[:, None, :]
+    Sg = L @ L.transpose(1, 2)
+    fx, fy = W / (2.0 * c.tanfovx), H / (2.0 * c.tanfovy)
+    limx, limy = 1.3 * c.tanfovx, 1.3 * c.tanfovy
+    tz = pv[:, 2]
+    tx = torch.clamp(pv[:, 0] / tz, -limx, limx) * tz
+    ty = torch.clamp(pv[:, 1] / tz, -limy, limy) * tz
+    zero = torch.zeros_like(tz)
+    J = torch.stack([fx / tz, zero, -fx * tx / (tz * tz), zero, fy / tz, -fy * ty / (tz * tz)], 1).reshape(-1, 2, 3)
+    Rwc = V[:3, :3].T
+    c2 = J @ (Rwc @ Sg @ Rwc.T) @ J.transpose(1, 2)
+    a, b, cc = c2[:, 0, 0] + 0.3, c2[:, 0, 1], c2[:, 1, 1] + 0.3
+    det = a * cc - b * b
+    mid = 0.5 * (a + cc)
+    l1 = mid + torch.sqrt(torch.clamp_min(mid * mid - det, 0.1))
+    l2 = mid - torch.sqrt(torch.clamp_min(mid * mid - det, 0.1))
+    rad = torch.ceil(3.0 * torch.sqrt(torch.maximum(l1, l2)))
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    x0 = torch.clamp((px - rad) / 16, min=0).floor().clamp(max=gx)
+    x1 = torch.clamp((px + rad + 15) / 16, min=0).floor().clamp(max=gx)
+    y0 = torch.clamp((py - rad) / 16, min=0).floor().clamp(max=gy)
+    y1 = torch.clamp((py + rad + 15) / 16, min=0).floor().clamp(max=gy)
+    ok = (pv[:, 2] > 0.2) & (det != 0) & ((x1 - x0) * (y1 - y0) > 0)
+    radii = torch.where(ok, rad, torch.zeros_like(rad)).numpy().astype(np.int64)
+    return radii, torch.stack([px, py], 1).numpy()
+
+
+@pytest.mark.parametrize("n,W,H,seed,k", [(60, 64, 48, 5, 1.0), (1200, 64, 48, 8, 7.0), (3000, 256, 192, 3, 1.0),
+                                         (20000, 800, 600, 4, 1.0)])
+def test_reference_radii_equal_oracle(oracle, n, W, H, seed, k):
+    """The float64 restatement of the reference's culling and radius rules gives the oracle's radii exactly (0 of
+    24,570 Gaussians differed when this was written)."""
+    s = small_scene(n, W, H, seed=seed)
+    s.scales = (s.scales * k).contiguous()
+    _, radii_o, _, _ = oracle_forward(oracle, s, (0, 0, 0), deg=3)
+    r64, _ = reference_radii(s, W, H)
+    np.testing.assert_array_equal(r64, radii_o.astype(np.int64))
+
+
 def rect_tile_lists(s, radii, means2D, W, H):
     """The reference's tile lists without its precise per-tile cull and without its key sort: every rendered Gaussian
     (radii > 0) in every tile of its getRect rectangle (auxiliary.h getRect: the 3-sigma radius around the projected
     centre, in 16 x 16 tiles), ordered by view depth computed here in float64 (ties: Gaussian index).  The cull only
     drops tiles no pixel of which accepts the splat (alpha < 1/255 everywhere), so compositing over these lists must
     give the reference's image and gradients: an anchor that shares no keying, culling or sorting code with the
-    oracle (the oracle's radii and projected centres only set the rectangles)."""
+    oracle: the radii and centres come from reference_radii (float64), checked equal to the oracle's first."""
     tx, ty = (W + 15) // 16, (H + 15) // 16
     c = s.camera
     ph = torch.cat([s.means3D.double(), torch.ones((s.means3D.shape[0], 1), dtype=torch.float64)], 1)
@@ -232,7 +292,9 @@ def test_oracle_backward_matches_autograd_uncull_bg(oracle, n, W, H, deg, seed, 
         s.opacities = torch.full_like(s.opacities, 0.95)
         s.scales = (s.scales * 7.0).contiguous()
     col_o, radii_o, inv_o, st = oracle_forward(oracle, s, bg, deg=deg, antialiasing=aa)
-    lists = rect_tile_lists(s, radii_o, st.geom()["means2D"], W, H)
+    r64, m64 = reference_radii(s, W, H)
+    np.testing.assert_array_equal(r64, radii_o.astype(np.int64))
+    lists = rect_tile_lists(s, r64, m64, W, H)
     extra = {}
     leaves, color, invd, ndc2, rgb_c, cov6 = dense_forward(s, lists, W, H, deg, bg=bg, extra=extra, antialiasing=aa)
     np.testing.assert_allclose(color.detach().numpy(), col_o, atol=2e-5)
