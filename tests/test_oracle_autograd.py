@@ -113,6 +113,7 @@ def dense_forward(s, lists, W, H, deg, bg=None, extra=None, antialiasing=False):
     tfin = torch.ones((H, W), dtype=f64)
     qlog = torch.zeros((H, W), dtype=f64)
     nstop = 0
+    counts = torch.zeros(m.shape[0], dtype=torch.int64)
     bgv = None if bg is None else torch.as_tensor(bg, dtype=f64)
     tiles_x = (W + 15) // 16
     yy, xx = torch.meshgrid(torch.arange(16, dtype=f64), torch.arange(16, dtype=f64), indexing="ij")
@@ -125,6 +126,7 @@ def dense_forward(s, lists, W, H, deg, bg=None, extra=None, antialiasing=False):
         D = torch.zeros(256, dtype=f64)
         Q = torch.zeros(256, dtype=f64)
         stop = torch.zeros(256, dtype=torch.bool)
+        in_img = (pxs < W) & (pys < H)
         for g in gl:
             dx, dy = px[g] - pxs, py[g] - pys
             power = -0.5 * (ca[g] * dx * dx + cc[g] * dy * dy) - cb[g] * dx * dy
@@ -135,6 +137,7 @@ def dense_forward(s, lists, W, H, deg, bg=None, extra=None, antialiasing=False):
             stop = stop | term
             live = live & ~term
             ok = ok & ~term
+            counts[g] += int((ok & in_img).sum())
             a = torch.where(ok, alpha, torch.zeros_like(alpha))
             C = C + rgb_c[g][:, None] * (a * T)[None, :]
             D = D + invz[g] * a * T
@@ -151,6 +154,7 @@ def dense_forward(s, lists, W, H, deg, bg=None, extra=None, antialiasing=False):
         qlog = qlog.index_put((iy, ix), Q[inside])
     if extra is not None:
         extra["T_final"], extra["qlog"], extra["stopped_pixels"] = tfin, qlog, nstop
+        extra["counts"] = counts.numpy()  # accepted pixels per Gaussian: LightGaussian's count (old forward.cu:485)
     return leaves, color, invd, ndc2, rgb_c, cov6
 
 
@@ -301,6 +305,10 @@ def test_oracle_backward_matches_autograd_uncull_bg(oracle, n, W, H, deg, seed, 
     np.testing.assert_allclose(invd.detach().numpy(), inv_o[0], atol=2e-5)
     if n >= 1200:  # the dense case reaches the T < 1e-4 stop (forward.cu:560-566) in many pixels
         assert extra["stopped_pixels"] > 100
+    # the count mode's per-Gaussian accepted-pixel counts (old forward.cu:455-490) over the same independent lists
+    cnt_o, _ = st.counts()
+    cnt64 = extra["counts"]
+    assert np.abs(cnt_o.astype(np.int64) - cnt64).max() <= 1 and (cnt_o == cnt64).mean() > 0.98
     rng = np.random.default_rng(seed)
     gcol = rng.standard_normal((3, H, W))
     ginv = 0.1 * rng.standard_normal((H, W))
