@@ -305,6 +305,26 @@ def test_oracle_backward_matches_autograd_uncull_bg(oracle, n, W, H, deg, seed, 
     np.testing.assert_allclose(invd.detach().numpy(), inv_o[0], atol=2e-5)
     if n >= 1200:  # the dense case reaches the T < 1e-4 stop (forward.cu:560-566) in many pixels
         assert extra["stopped_pixels"] > 100
+    # the precise per-tile cull is conservative, checked directly: every (tile, Gaussian) pair of the rect lists that
+    # the oracle's keying dropped has no pixel of that tile where the splat reaches alpha >= 1/255 with power <= 0
+    t_o, i_o, _ = st.sorted_list()
+    kept = set(zip(t_o.tolist(), i_o.tolist()))
+    g64 = st.geom()
+    co, xy = g64["conic_opacity"].astype(np.float64), g64["means2D"].astype(np.float64)
+    gx = (W + 15) // 16
+    yy, xx = np.meshgrid(np.arange(16.0), np.arange(16.0), indexing="ij")
+    dropped = 0
+    for t, gl in lists.items():
+        x0, y0 = (t % gx) * 16, (t // gx) * 16
+        for g in gl:
+            if (t, g) in kept:
+                continue
+            dropped += 1
+            dx, dy = xy[g, 0] - (xx + x0), xy[g, 1] - (yy + y0)
+            power = -0.5 * (co[g, 0] * dx * dx + co[g, 2] * dy * dy) - co[g, 1] * dx * dy
+            alpha = np.minimum(0.99, co[g, 3] * np.exp(power))
+            assert not np.any((power <= 0) & (alpha >= (1.0 / 255.0) * (1 + 1e-5))), (t, g)
+    assert dropped > 0 or n < 100
     # the count mode's per-Gaussian accepted-pixel counts (old forward.cu:455-490) over the same independent lists
     cnt_o, _ = st.counts()
     cnt64 = extra["counts"]
