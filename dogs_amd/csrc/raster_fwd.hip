@@ -387,6 +387,10 @@ __device__ __forceinline__ void depth_cut_block(const uint32_t* __restrict__ his
     __shared__ uint32_t s_err;
     constexpr int PER = DH_BINS / 1024;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    // the histogram's loads go out first: the rect-area reduction and the zero fill below run under them
+    uint32_t v[PER], loc = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) v[k] = hist[t * PER + k];
     if (t == 0) s_err = 0u;
     __syncthreads();
     {  // num_rendered = sum of the preprocess's per-block rect areas
@@ -406,18 +410,9 @@ __device__ __forceinline__ void depth_cut_block(const uint32_t* __restrict__ his
     // tile_cnt2 is followed by the replay-order histogram of the phase-2 launches (order_hist_piece: counts, cursors)
     for (uint32_t i = t; i < 2u * ORDER_NB; i += 1024) tile_cnt2[num_tiles + i] = 0u;
     if (t == 0) s_best = -1;
-    uint32_t v[PER], loc = 0;
 #pragma unroll
-    for (int k = 0; k < PER; k++) {
-        v[k] = hist[t * PER + k];
-        loc += v[k];
-    }
-    uint32_t x = loc;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
+    for (int k = 0; k < PER; k++) loc += v[k];
+    const uint32_t x = wave_incl_scan(loc);
     if (lane == 63) s_w[w] = x;
     __syncthreads();
     uint32_t off = 0, K = 0;

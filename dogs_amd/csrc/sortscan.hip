@@ -398,6 +398,91 @@ void tile_offsets(uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges, hipStre
     if (num_tiles) k_tile_offsets<<<1, 1024, 0, stream>>>(tile_cnt, num_tiles, ranges, gate);
 }
 
+#ifndef DG_BO_OLD
+// Block 0: exclusive scan of the wave totals in place (+ total); block 1: the per-tile ranges (tile_offsets).
+// 16 contiguous items per thread (four 16-B loads), so one round covers 16 * NT items -- a 1e6-Gaussian view's 15625
+// wave totals in one round at NT = 1024: one HBM round trip, one barrier.  The wave scan is DPP (row_shr 1/2/4/8,
+// row_bcast 15/31; no LDS), the wave sums meet in LDS.
+constexpr int BO_ITEMS = 16;
+template <int NT>
+__global__ void __launch_bounds__(NT) k_bin_offsets(uint32_t* __restrict__ wtot, uint32_t n,
+                                                      uint32_t* __restrict__ total, uint32_t* __restrict__ tile_cnt,
+                                                      uint32_t num_tiles, uint2* __restrict__ ranges,
+                                                      const uint32_t* __restrict__ gate) {
+    constexpr int NW = NT / 64;
+    constexpr uint32_t PER = (uint32_t)BO_ITEMS * NT;
+    __shared__ uint32_t s_w[2][NW];
+    const bool tiles = blockIdx.x == 1;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    // the gate is tested after the first round's loads are issued (in bounds either way: the arrays are sized for n),
+    // so the block waits on one round trip, not two
+    const uint32_t gv = gate ? *gate : 1u;
+    const uint32_t N = tiles ? num_tiles : n;
+    uint32_t* src = tiles ? tile_cnt : wtot;
+    // the 16-B paths need 16-B aligned arrays (the carver's are 256-B aligned); otherwise element by element
+    const bool vec = ((reinterpret_cast<uintptr_t>(src) | (tiles ? reinterpret_cast<uintptr_t>(ranges) : 0u)) & 15u) == 0u;
+    uint32_t carry = 0u;
+    int par = 0;
+    for (uint32_t b = 0; b < N; b += PER, par ^= 1) {
+        const uint32_t i0 = b + (uint32_t)BO_ITEMS * (uint32_t)t;
+        uint32_t v[BO_ITEMS];
+        if (vec && i0 + BO_ITEMS <= N) {
+            const uint4* s4 = reinterpret_cast<const uint4*>(src + i0);
+#pragma unroll
+            for (int q = 0; q < BO_ITEMS / 4; q++) {
+                const uint4 u = s4[q];
+                v[4 * q] = u.x; v[4 * q + 1] = u.y; v[4 * q + 2] = u.z; v[4 * q + 3] = u.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < BO_ITEMS; k++) v[k] = i0 + k < N ? src[i0 + k] : 0u;
+        }
+        if (gv == 0u) break;  // block-uniform: nothing to scan (total = carry = 0)
+        uint32_t loc = 0u;
+#pragma unroll
+        for (int k = 0; k < BO_ITEMS; k++) loc += v[k];
+        const uint32_t x = wave_incl_scan(loc);
+        if (lane == 63) s_w[par][w] = x;
+        __syncthreads();  // s_w[par] complete; the other parity's readers finished before the previous round's barrier
+        uint32_t off = carry, tot = 0u;
+#pragma unroll
+        for (int k = 0; k < NW; k++) {
+            const uint32_t s = s_w[par][k];
+            off += k < w ? s : 0u;
+            tot += s;
+        }
+        carry += tot;
+        uint32_t ex = off + x - loc;
+        if (vec && i0 + BO_ITEMS <= N) {
+            if (tiles) {
+#pragma unroll
+                for (int k = 0; k < BO_ITEMS; k += 2) {
+                    const uint32_t e1 = ex + v[k], e2 = e1 + v[k + 1];
+                    reinterpret_cast<uint4*>(ranges + i0)[k / 2] = make_uint4(ex, e1, e1, e2);
+                    ex = e2;
+                }
+                ex = off + x - loc;
+            }
+            uint32_t o[BO_ITEMS];
+#pragma unroll
+            for (int k = 0; k < BO_ITEMS; k++) { o[k] = ex; ex += v[k]; }
+            uint4* d4 = reinterpret_cast<uint4*>(src + i0);
+#pragma unroll
+            for (int q = 0; q < BO_ITEMS / 4; q++) d4[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < BO_ITEMS; k++) {
+                if (i0 + k < N) {
+                    if (tiles) ranges[i0 + k] = make_uint2(ex, ex + v[k]);
+                    src[i0 + k] = ex;
+                }
+                ex += v[k];
+            }
+        }
+    }
+    if (!tiles && t == 0) *total = carry;
+}
+#else
 // Block 0: exclusive scan of the wave totals in place (+ total); block 1: the per-tile ranges (tile_offsets).
 // 4 items per thread per 4096-item round, wave shuffle scan + 16 wave sums in LDS, running carry.  The loads of
 // BO_ROUNDS rounds are issued before the first scan (one HBM round trip per 16384 items instead of one per round:
@@ -463,6 +548,7 @@ __global__ void __launch_bounds__(NT) k_bin_offsets(uint32_t* __restrict__ wtot,
     }
     if (!tiles && t == 0) *total = s_carry;
 }
+#endif
 
 void bin_offsets(uint32_t* wtot, uint32_t n, uint32_t* total, uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges,
                  hipStream_t stream, const uint32_t* gate, bool small_blocks) {
