@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include "gs_common.h"
 #include "raster.h"
+#include "wave_sort.h"
 
 namespace gs {
 
@@ -215,15 +216,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
     // per quadrant (qx = k >> 1, qy = k & 1 -> quadrant 2 qy + qx): max last contributor over the wave
     int qlast[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        int m = last[k];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const int y = __shfl_xor(m, o);
-            m = y > m ? y : m;
-        }
-        qlast[2 * (k & 1) + (k >> 1)] = __builtin_amdgcn_readfirstlane(m);
-    }
+    for (int k = 0; k < 4; k++) qlast[2 * (k & 1) + (k >> 1)] = (int)wave_max_u32((uint32_t)last[k]);
 #ifndef DG_BWD_NO_PREFETCH
     // The batch gather is a dependent chain (list slot -> emission index -> Gaussian -> splat record).  The first two
     // links of batch b + 1 (and the first of b + 2) are loaded while batch b replays, so a batch start waits on one
@@ -639,12 +632,8 @@ __global__ void __launch_bounds__(LIVE_THREADS) k_gauss_live(GaussBwdArgs a) {
     for (uint32_t c0 = blockIdx.x * LIVE_CHUNKS; c0 < nchunks; c0 += gridDim.x * LIVE_CHUNKS) {
         if (threadIdx.x < 64) {
             const uint32_t t = threadIdx.x;
-            uint32_t incl = (t < (uint32_t)LIVE_CHUNKS && c0 + t < nchunks) ? a.live_cnt[c0 + t] : 0u;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o);
-                if ((int)t >= o) incl += y;
-            }
+            const uint32_t incl =
+                wave_incl_scan((t < (uint32_t)LIVE_CHUNKS && c0 + t < nchunks) ? a.live_cnt[c0 + t] : 0u);
             if (t < (uint32_t)LIVE_CHUNKS) s_pre[t + 1] = incl;
             if (t == 0) s_pre[0] = 0u;
         }

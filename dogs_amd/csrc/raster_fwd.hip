@@ -106,12 +106,7 @@ template <typename Visit, typename Known = NoKnownKept>
 __device__ __forceinline__ void wave_candidates(CandLDS& L, int lane, int x0, int y0, int x1, int y1, float mx, float my,
                                                 float4 co, float thr, Visit&& visit, const Known& known = Known{}) {
     const uint32_t area = (x1 > x0 && y1 > y0) ? (uint32_t)(x1 - x0) * (uint32_t)(y1 - y0) : 0u;
-    uint32_t incl = area;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
+    const uint32_t incl = wave_incl_scan(area);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     L.pre[lane] = incl - area;
     L.w[lane] = x1 - x0; L.area[lane] = (int)area;
@@ -625,9 +620,7 @@ __global__ void __launch_bounds__(256) k_bin_count(BinArgs a) {
         c = s_cnt[w][lane];
         if (b.member) a.rcnt[g] = c;
     }
-    uint32_t tot = c;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+    const uint32_t tot = wave_sum_u32(c);
     if (lane == 0) a.wtot[wave] = tot;
 }
 
@@ -732,12 +725,7 @@ __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
     const BinLane b = bin_lane<PHASE>(a, g, lane, a.counters[CNT_THR], s_key[w], (int)((members >> lane) & 1ull));
     const uint32_t base = a.wtot[wave];
     const uint32_t c = b.member ? a.rcnt[g] : 0u;
-    uint32_t incl = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
+    const uint32_t incl = wave_incl_scan(c);
     const uint32_t wt = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (wt == 0u || base + wt > a.cap) return;  // nothing kept; (capacity: never with consistent inputs)
     if (b.member && c) {
@@ -901,12 +889,7 @@ __global__ void __launch_bounds__(256) k_bin_emit_fat(BinArgs a) {
         s_g[w][lane] = (uint32_t)g;
         const BinLane b = member_lane(a, g, member);
         const uint32_t c = member ? a.rcnt[g] : 0u;
-        uint32_t incl = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
+        const uint32_t incl = wave_incl_scan(c);
         const uint32_t wt = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         if (base + running + wt > a.cap) return;  // (capacity: never with consistent inputs)
         if (member && c) {
@@ -1255,11 +1238,7 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
         a.img_invd[pid] = D[k];
         mx = last[k] > mx ? last[k] : mx;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t y = __shfl_xor(mx, o);
-        mx = y > mx ? y : mx;
-    }
+    mx = wave_max_u32(mx);
     if (lane == 0) a.max_contrib[tile] = mx;
     if (PHASE == 1) {
         // A tile with a live pixel after a truncated (prefix) list needs phase 2: keep its raw state.
@@ -1467,11 +1446,7 @@ __device__ __forceinline__ void render_fwd2_tile(const RenderArgs& a, int tile, 
         a.img_invd[pid] = D;
         mx = last;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t y = __shfl_xor(mx, o);
-        mx = y > mx ? y : mx;
-    }
+    mx = wave_max_u32(mx);
     if (lane == 0) s_mx[w] = mx;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1623,11 +1598,7 @@ __global__ void __launch_bounds__(1024) k_render_fwd2x(RenderArgs a) {
         a.img_invd[pid] = D;
         mx = last;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t y = __shfl_xor(mx, o);
-        mx = y > mx ? y : mx;
-    }
+    mx = wave_max_u32(mx);
     if (pix && lane == 0) s_mx[w] = mx;
     __syncthreads();
     if (threadIdx.x == 0) {

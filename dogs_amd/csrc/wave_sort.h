@@ -50,15 +50,23 @@ __device__ __forceinline__ uint32_t ds_gid(const DSortArgs& a, uint32_t v) {
     return a.eg[v < a.n_inst ? v : a.n_inst - 1];
 }
 
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { const uint32_t y = __shfl_xor(x, o); x = y < x ? y : x; }
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+// wave min / max by the DPP scan's pattern (identity from rows and lanes without a source); lane 63 holds the result
+template <bool MAX>
+__device__ __forceinline__ uint32_t wave_minmax_u32(uint32_t x) {
+    constexpr int ID = MAX ? 0 : -1;
+    auto f = [](uint32_t a, uint32_t b) { return MAX ? (a > b ? a : b) : (a < b ? a : b); };
+    x = f(x, (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x111, 0xf, 0xf, false));
+    x = f(x, (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x112, 0xf, 0xf, false));
+    x = f(x, (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x114, 0xf, 0xf, false));
+    x = f(x, (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x118, 0xf, 0xf, false));
+    x = f(x, (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x142, 0xa, 0xf, false));
+    x = f(x, (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x143, 0xc, 0xf, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { const uint32_t y = __shfl_xor(x, o); x = y > x ? y : x; }
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) { return wave_minmax_u32<false>(x); }
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) { return wave_minmax_u32<true>(x); }
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(x), 63);
 }
 __device__ __forceinline__ int passes_for(uint32_t range) { return range ? (32 - __clz((int)range) + 7) >> 3 : 0; }
 
@@ -89,12 +97,7 @@ __device__ __forceinline__ void wave_radix(uint32_t (&k)[ROWS], uint32_t (&v)[RO
         {  // exclusive scan of the 256 digit counts, 4 per lane
             const uint32_t c0 = cnt[4 * lane], c1 = cnt[4 * lane + 1], c2 = cnt[4 * lane + 2], c3 = cnt[4 * lane + 3];
             const uint32_t loc = c0 + c1 + c2 + c3;
-            uint32_t x = loc;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(x, o);
-                if (lane >= o) x += y;
-            }
+            const uint32_t x = wave_incl_scan(loc);
             const uint32_t ex = x - loc;
             __builtin_amdgcn_wave_barrier();
             cnt[4 * lane] = ex; cnt[4 * lane + 1] = ex + c0; cnt[4 * lane + 2] = ex + c0 + c1;
@@ -174,7 +177,7 @@ __device__ __forceinline__ int wave_sort_tile(const DSortArgs& a, int tile, int 
 #pragma unroll
     for (int r = 0; r < ROWS; r++) {
         if (r < R) {
-            uint32_t prev = __shfl_up(k[r], 1);
+            uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k[r], 0x138, 0xf, 0xf, false);  // wave_shr:1
             if (lane == 0) prev = r > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)k[r > 0 ? r - 1 : 0], 63) : ~k[r];
             const int i = r * 64 + lane;
             tie |= (i < n) && prev == k[r];
@@ -281,12 +284,7 @@ __device__ __forceinline__ void block_radix_global(uint32_t*& va, uint32_t*& vb,
         __syncthreads();
         {  // exclusive scan of the digit counts (thread t = digit t)
             const uint32_t c = on ? s_base[t] : 0u;
-            uint32_t x = c;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(x, o);
-                if (lane >= o) x += y;
-            }
+            const uint32_t x = wave_incl_scan(c);
             if (on && lane == 63) s_red[0][w] = x;
             __syncthreads();
             uint32_t off = 0;
