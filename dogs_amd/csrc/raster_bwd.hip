@@ -464,12 +464,16 @@ __device__ __forceinline__ bool sum_step(const GaussBwdArgs& a, uint32_t i0, uin
     // segmented inclusive scan with DPP (no LDS): row_shr 1, 2, 4, 8 within each 16-lane row, then row_bcast:15
     // and row_bcast:31 across rows; a lane adds its partner's partial only when both have the same owner (segments
     // are contiguous, so everything between them does too)
-    seg_level<0x111, 0xf>(own, v);
-    seg_level<0x112, 0xf>(own, v);
-    seg_level<0x114, 0xf>(own, v);
-    seg_level<0x118, 0xf>(own, v);
-    seg_level<0x142, 0xa>(own, v);
-    seg_level<0x143, 0xc>(own, v);
+    // a step with no flagged record (more than half the binned Gaussians have no accepted pixel: their instances lie
+    // past their tiles' last contributors) scans zeros: +0 everywhere, so the scan is skipped with the same bits
+    if (__any(use)) {
+        seg_level<0x111, 0xf>(own, v);
+        seg_level<0x112, 0xf>(own, v);
+        seg_level<0x114, 0xf>(own, v);
+        seg_level<0x118, 0xf>(own, v);
+        seg_level<0x142, 0xa>(own, v);
+        seg_level<0x143, 0xc>(own, v);
+    }
     if (own == st.carry_owner) {  // the step's first segment continues the open one
 #pragma unroll
         for (int k = 0; k < 10; k++) v[k] += st.carry[k];
