@@ -276,3 +276,35 @@ def test_capacity_contexts_are_isolated(hip_device):
         assert view()[0] == first_a[0], "the default context is untouched by both"
     finally:
         _C.set_prefix_per_tile(old)
+
+
+@pytest.mark.parametrize("per_tile", [0, -1], ids=["prefix-default", "prefix-off"])
+def test_forward_many_binning_waves(oracle, hip_device, per_tile):
+    """More than 16384 binning waves (P > 2^20): the ranges scan runs several rounds of 16 items per thread, with a
+    ragged last round (P = 1,100,003).  With the depth prefix off every list is binned whole, so the sorted
+    instances and the per-tile ranges must equal the oracle's element for element."""
+    from dogs_amd.diff_gaussian_rasterization import _C
+    n, W, H = 1_100_003, 256, 192
+    s = small_scene(n, W, H, seed=41, sh_rest=3)
+    s.scales = (s.scales * 0.5).contiguous()
+    old = _C.set_prefix_per_tile(per_tile)
+    try:
+        col_o, radii_o, inv_o, st = oracle_forward(oracle, s, (0, 0, 0), deg=1)
+        out = hip_forward(s, (0, 0, 0), hip_device, deg=1)
+        assert out[0] == st.num_rendered
+        np.testing.assert_array_equal(out[4].cpu().numpy(), radii_o)
+        t_o, i_o, _ = st.sorted_list()
+        t_h, i_h, e1 = hip_sorted_instances(out, W, H, hip_device, n)
+        fT, nc, mc, rg = hip_image_state(out, W, H, hip_device)
+        if per_tile:
+            assert e1 == st.num_valid
+            np.testing.assert_array_equal(t_h, t_o)
+            np.testing.assert_array_equal(i_h, i_o)
+            np.testing.assert_array_equal(rg, st.ranges())
+        else:
+            full = per_tile_lists(t_o, i_o, len(t_o))
+            for t, lst in per_tile_lists(t_h, i_h, e1).items():
+                assert lst == full[t][:len(lst)], f"tile {t}: not a prefix of the reference list"
+        assert psnr(out[2].cpu().numpy(), col_o) > 80.0
+    finally:
+        _C.set_prefix_per_tile(old)
