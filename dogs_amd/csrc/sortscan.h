@@ -36,7 +36,7 @@ void tile_offsets(uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges, hipStre
 // (*total = sum) and tile_offsets() above.  For n <= BIN_OFFSETS_MAX_N (longer wave-total arrays take
 // exclusive_scan + tile_offsets).  gate as above (*total = 0 when gated).
 #ifndef DG_BIN_OFFSETS_MAX_N
-#define DG_BIN_OFFSETS_MAX_N 65536
+#define DG_BIN_OFFSETS_MAX_N 262144
 #endif
 constexpr uint32_t BIN_OFFSETS_MAX_N = DG_BIN_OFFSETS_MAX_N;
 void bin_offsets(uint32_t* wtot, uint32_t n, uint32_t* total, uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges,

@@ -403,7 +403,10 @@ void tile_offsets(uint32_t* tile_cnt, uint32_t num_tiles, uint2* ranges, hipStre
 // 16 contiguous items per thread (four 16-B loads), so one round covers 16 * NT items -- a 1e6-Gaussian view's 15625
 // wave totals in one round at NT = 1024: one HBM round trip, one barrier.  The wave scan is DPP (row_shr 1/2/4/8,
 // row_bcast 15/31; no LDS), the wave sums meet in LDS.
-constexpr int BO_ITEMS = 16;
+#ifndef DG_BO_ITEMS
+#define DG_BO_ITEMS 16
+#endif
+constexpr int BO_ITEMS = DG_BO_ITEMS;
 template <int NT>
 __global__ void __launch_bounds__(NT) k_bin_offsets(uint32_t* __restrict__ wtot, uint32_t n,
                                                       uint32_t* __restrict__ total, uint32_t* __restrict__ tile_cnt,
@@ -421,11 +424,8 @@ __global__ void __launch_bounds__(NT) k_bin_offsets(uint32_t* __restrict__ wtot,
     uint32_t* src = tiles ? tile_cnt : wtot;
     // the 16-B paths need 16-B aligned arrays (the carver's are 256-B aligned); otherwise element by element
     const bool vec = ((reinterpret_cast<uintptr_t>(src) | (tiles ? reinterpret_cast<uintptr_t>(ranges) : 0u)) & 15u) == 0u;
-    uint32_t carry = 0u;
-    int par = 0;
-    for (uint32_t b = 0; b < N; b += PER, par ^= 1) {
+    auto load = [&](uint32_t b, uint32_t (&v)[BO_ITEMS]) {
         const uint32_t i0 = b + (uint32_t)BO_ITEMS * (uint32_t)t;
-        uint32_t v[BO_ITEMS];
         if (vec && i0 + BO_ITEMS <= N) {
             const uint4* s4 = reinterpret_cast<const uint4*>(src + i0);
 #pragma unroll
@@ -437,6 +437,19 @@ __global__ void __launch_bounds__(NT) k_bin_offsets(uint32_t* __restrict__ wtot,
 #pragma unroll
             for (int k = 0; k < BO_ITEMS; k++) v[k] = i0 + k < N ? src[i0 + k] : 0u;
         }
+    };
+    uint32_t carry = 0u;
+    int par = 0;
+    // the next round's loads are issued before this round's scan (its in-place stores cover other items), so a
+    // multi-round scan (5e6 Gaussians: 78k wave totals, 5 rounds) waits on memory once, not once per round
+    uint32_t nv[BO_ITEMS];
+    if (N) load(0u, nv);
+    for (uint32_t b = 0; b < N; b += PER, par ^= 1) {
+        const uint32_t i0 = b + (uint32_t)BO_ITEMS * (uint32_t)t;
+        uint32_t v[BO_ITEMS];
+#pragma unroll
+        for (int k = 0; k < BO_ITEMS; k++) v[k] = nv[k];
+        if (b + PER < N) load(b + PER, nv);  // block-uniform
         if (gv == 0u) break;  // block-uniform: nothing to scan (total = carry = 0)
         uint32_t loc = 0u;
 #pragma unroll
