@@ -619,19 +619,32 @@ __global__ void __launch_bounds__(256) k_tile_dsort_merged(DSortArgs a, int tpb)
     __shared__ uint32_t s_q[DSM_TILES];
     __shared__ uint32_t s_nq;
     __shared__ int s_tie;
-    if (a.gate && *a.gate == 0u) return;
+    // the gate is read with the tile lengths below (in bounds either way), one memory round trip instead of two
+    const uint32_t gv = a.gate ? *a.gate : 1u;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (threadIdx.x == 0) s_nq = 0u;
     __syncthreads();
     const int t0 = blockIdx.x * tpb + w * (tpb / 4);
-    for (int i = 0; i < tpb / 4; i++) {
-        const int tile = t0 + i;
-        if (tile >= a.num_tiles) break;
-        const int n = wave_sort_tile<DS_ROWS2>(a, tile, lane, s_cnt[w], s_k[w], s_v[w], nullptr, DS_WAVE_MAX);
-        if (n > DS_WAVE_MAX2 && lane == 0) s_q[atomicAdd(&s_nq, 1u)] = (uint32_t)tile;
+    // the wave's tile lengths in one load round (lane i: tile t0 + i), then only the lists past the render's own sort
+    // capacity are visited -- at 1e6 Gaussians almost none, and the 16 dependent range loads of a tile-by-tile walk
+    // were the whole launch (~6 us)
+    for (int i0 = 0; i0 < tpb / 4; i0 += 64) {
+        const int tile = t0 + i0 + lane;
+        bool longer = false;
+        if (i0 + lane < tpb / 4 && tile < a.num_tiles) {
+            const uint2 rg = a.ranges[tile];
+            longer = rg.y - rg.x > (uint32_t)DS_WAVE_MAX;
+        }
+        uint64_t m = gv ? __ballot(longer) : 0ull;
+        while (m) {
+            const int i = i0 + (int)__builtin_ctzll(m);
+            m &= m - 1;
+            const int n = wave_sort_tile<DS_ROWS2>(a, t0 + i, lane, s_cnt[w], s_k[w], s_v[w], nullptr, DS_WAVE_MAX);
+            if (n > DS_WAVE_MAX2 && lane == 0) s_q[atomicAdd(&s_nq, 1u)] = (uint32_t)(t0 + i);
+        }
     }
     __syncthreads();
-    const uint32_t nq = s_nq;
+    const uint32_t nq = s_nq;  // 0 when gated
     uint32_t* scr = &s_k[0][0];  // the wave sorts are done: their scratch serves the block sort
     for (uint32_t q = 0; q < nq; q++)
         block_sort_long(a, (int)s_q[q], scr, reinterpret_cast<uint32_t(*)[BS_RADIX]>(scr + BS_RADIX),
