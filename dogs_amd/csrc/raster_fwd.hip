@@ -662,6 +662,8 @@ __device__ __forceinline__ uint32_t fwd2_replay_len(const uint8_t* unf, const ui
     return (r1.y - r1.x) + (r2.y - r2.x);
 }
 
+__device__ __forceinline__ BinLane member_lane(const BinArgs& a, int g, bool member);
+
 // Pass 2: wave base = exclusive scan of the wave totals (wtot, scanned in place); first_e of every binned
 // Gaussian, and a second walk writes its instances (Gaussian, depth key) at consecutive indices in (lane, ty, tx)
 // order, so every Gaussian's instances are contiguous: [first_e, first_e + rcnt); each instance index is also
@@ -728,9 +730,15 @@ __global__ void __launch_bounds__(256) k_bin_emit(BinArgs a) {
     const uint64_t members = a.wmask[wave];
     if (!members) return;  // no member in this wave (no key, record or SAT loads)
     const int g = g0 + lane;
-    const BinLane b = bin_lane<PHASE>(a, g, lane, a.counters[CNT_THR], s_key[w], (int)((members >> lane) & 1ull));
+    // the count pass's members (each with g < P): key, record, count and the wave's base in one load round (bin_lane's
+    // membership tests would put the key load in front of the others)
+    const bool mine = lane < EMIT_RANKS && ((members >> lane) & 1ull) != 0ull;
+    const uint32_t key = mine ? a.dkey[g] : 0u;
     const uint32_t base = a.wtot[wave];
-    const uint32_t c = b.member ? a.rcnt[g] : 0u;
+    const uint32_t cm = mine ? a.rcnt[g] : 0u;
+    const BinLane b = member_lane(a, g, mine);
+    s_key[w][lane] = key;
+    const uint32_t c = b.member ? cm : 0u;
     const uint32_t incl = wave_incl_scan(c);
     const uint32_t wt = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (wt == 0u || base + wt > a.cap) return;  // nothing kept; (capacity: never with consistent inputs)
