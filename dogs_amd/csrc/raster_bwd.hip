@@ -331,9 +331,10 @@ __global__ void __launch_bounds__(256) BWD_WPE_ATTR k_render_bwd(RenderBwdArgs a
         if (gw >= nw) return;
         const size_t n4 = a.zero_count / 4;
         const size_t per = ((n4 + nw - 1) / nw + 63) & ~(size_t)63;
-        float4* z4 = reinterpret_cast<float4*>(a.zero_base);
+        // non-temporal (streaming) stores: ~284 MB of zeros per 1e6-Gaussian view that nothing reads back soon
+        v4f* z4 = reinterpret_cast<v4f*>(a.zero_base);
         const size_t e4 = (gw + 1) * per < n4 ? (gw + 1) * per : n4;
-        for (size_t i = gw * per + lane; i < e4; i += 64) z4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (size_t i = gw * per + lane; i < e4; i += 64) __builtin_nontemporal_store(bc4(0.0f), &z4[i]);
         if (gw == 0)
             for (size_t i = (n4 << 2) + lane; i < a.zero_count; i += 64) a.zero_base[i] = 0.f;
     };
