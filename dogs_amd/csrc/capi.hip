@@ -822,6 +822,9 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
             total += counts[i];
         }
         if (adjacent) zero_count = total;
+#ifdef DG_NO_ZERO_FILL  // timing experiment only (tools/gpu_r5be.sh): no zero fill anywhere, wrong non-contributing rows
+        zero_count = 0;
+#endif
     }
     {
         gs::RenderBwdArgs r;
@@ -854,7 +857,11 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
     q.dmeans2D = dmeans2D; q.dcolors = dcolors; q.dopacity = dopacity; q.dmeans3D = dmeans3D; q.dcov3D = dcov3D;
     q.ddc = ddc; q.dsh = dsh; q.dscales = dscales; q.drot = drot; q.depth = depth;
     q.live_list = sc.live_list; q.live_cnt = sc.live_cnt;
+#ifdef DG_NO_ZERO_FILL
+    q.outputs_zeroed = true;
+#else
     q.outputs_zeroed = zero_count != 0;
+#endif
     { PROF("gauss_bwd"); gs::launch_gauss_bwd(q, s); }
     DBG_SYNC(a->debug, s);
     HIP_OK(hipGetLastError());

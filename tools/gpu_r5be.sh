@@ -1,5 +1,6 @@
 #!/bin/bash
-# timing only: the backward without any zero fill of the gradient outputs (DG_NO_ZERO_FILL) against HEAD
+# timing only: the backward without any zero fill of the gradient outputs against HEAD; build the variant first:
+#   tools/build_variant.sh ablibs/nozero.so -DDG_NO_ZERO_FILL; cp dogs_amd/_lib/libdogs_hip.so ablibs/base.so
 OUT=${1:-gpurun_out/r5be}
 mkdir -p "$OUT"
 bash tools/gpu_r5al.sh "$OUT/a" ablibs/base.so ablibs/nozero.so || exit $?
