@@ -327,7 +327,10 @@ __global__ void __launch_bounds__(256) BWD_WPE_ATTR k_render_bwd(RenderBwdArgs a
         // only the first 3/4 of the launch order (the longer replays, longest first) fill, so the kernel's tail has no
         // store drain (render_bwd 257-260 -> 255-258 us, profiles/r03al_bwd_fill_front_ab.txt)
         const size_t nw_all = (size_t)gridDim.x * 4, gw = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-        const size_t nw = nw_all * 3 / 4 > 0 ? nw_all * 3 / 4 : 1;
+#ifndef DG_BWD_FILL_FRAC4
+#define DG_BWD_FILL_FRAC4 3
+#endif
+        const size_t nw = nw_all * DG_BWD_FILL_FRAC4 / 4 > 0 ? nw_all * DG_BWD_FILL_FRAC4 / 4 : 1;
         if (gw >= nw) return;
         const size_t n4 = a.zero_count / 4;
         const size_t per = ((n4 + nw - 1) / nw + 63) & ~(size_t)63;
