@@ -876,6 +876,13 @@ int dg_mark_visible(int P, const float* means3D, const float* viewmatrix, const 
     return 0;
 }
 
+int dg_cull_log_threshold(int64_t n, const float* opacity, float* thr, dg_stream_t stream) {
+    if (n < 0 || (n > 0 && (!opacity || !thr))) return fail("bad args%s%d");
+    gs::launch_cull_log_threshold(n, opacity, thr, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
 int dg_rasterize_filter(const dg_raster_args* a, int* radii, dg_stream_t stream) {
     if (!a || a->P < 0) return fail("bad args%s%d");
     if (a->P == 0) return 0;

@@ -82,23 +82,45 @@ __device__ __forceinline__ float ndc2pix(float v, int S) { return (float)((((dou
 // v_cvt_i32_f32 saturates and maps NaN to 0 -- the semantics the oracle restates
 __device__ __forceinline__ int f2i(float f) { return (int)f; }
 
-// Deterministic log shared with the oracle (gs_logf in oracle/gs_oracle.c): same operations, same order.
-__device__ __forceinline__ float gs_logf(float a) {
+// logf of the precise tile cull (rasterizer_impl.cu:151: logf(co.w / (1/255))): correctly rounded, the closest
+// stand-in for CUDA's logf (<= 1 ulp).  The same IEEE double operation sequence as gs_crlogf in oracle/gs_oracle.c
+// (log a = e ln2 + 2 atanh s, s = (m - 1)/(m + 1), the atanh series to s^19, one rounding to float), so the kernels
+// and the oracle agree bit for bit; correctly rounded on every float in [2^-20, 256) with the two listed exceptions
+// (exact log within 3e-16 of a float midpoint).  Round 5's float polynomial was 1-3 ulp off on 7.7% of the
+// opacities (profiles/r06_logf_census.json).  Evaluated once per binned Gaussian.
+__device__ __forceinline__ float gs_crlogf(float a) {
     if (!(a > 0.0f)) return (a == 0.0f) ? -__builtin_inff() : __builtin_nanf("");
     if (a == __builtin_inff()) return __builtin_inff();
+    if (a == 0x1.827a74p-7f) return -0x1.1c2b1ep+2f;
+    if (a == 0x1.2f1fd6p+3f) return 0x1.1fcbcep+1f;
     uint32_t u = __float_as_uint(a);
     int e = 0;
     if (u < 0x00800000u) { u = __float_as_uint(a * 8388608.0f); e = -23; }
     e += (int)((u >> 23) & 0xff) - 127;
-    float m = __uint_as_float((u & 0x007fffffu) | 0x3f800000u);
-    if (m > 1.41421356f) { m = m * 0.5f; e += 1; }
-    const float s = (m - 1.0f) / (m + 1.0f);
-    const float s2 = s * s;
-    float p = fmaf(s2, 0.22222222f, 0.28571429f);
-    p = fmaf(s2, p, 0.4f);
-    p = fmaf(s2, p, 0.66666669f);
-    p = fmaf(s2, p, 2.0f);
-    return fmaf((float)e, 0.693147182f, s * p);
+    uint32_t mu = (u & 0x007fffffu) | 0x3f800000u;
+    if (mu > 0x3fb504f3u) { mu -= 0x00800000u; e += 1; }   // m in [sqrt(1/2), sqrt(2))
+    const double m = (double)__uint_as_float(mu);
+    const double s = (m - 1.0) / (m + 1.0);
+    const double s2 = s * s;
+    double p = __builtin_fma(s2, 0.10526315789473684, 0.11764705882352941);
+    p = __builtin_fma(s2, p, 0.13333333333333333);
+    p = __builtin_fma(s2, p, 0.15384615384615385);
+    p = __builtin_fma(s2, p, 0.18181818181818182);
+    p = __builtin_fma(s2, p, 0.22222222222222222);
+    p = __builtin_fma(s2, p, 0.2857142857142857);
+    p = __builtin_fma(s2, p, 0.4);
+    p = __builtin_fma(s2, p, 0.6666666666666666);
+    const double lm = __builtin_fma(s * s2, p, 2.0 * s);
+    const double ed = (double)e;
+    return (float)__builtin_fma(ed, 0x1.62e42fefa3800p-1, __builtin_fma(ed, 0x1.ef35793c76730p-45, lm));
+}
+
+// The same threshold for the render kernels' 8x8-quadrant masks (quad_mask), which only skip work: a quadrant is
+// dropped when even its nearest point is past the threshold by QUAD_MARGIN (0.01), and a pixel there fails the
+// per-pixel alpha >= 1/255 test anyway.  So any value within the margin gives the same outputs; the hardware log2
+// (v_log_f32, ~1 ulp) of o * 255 is within ~1e-6 of the exact one, and costs 3 VALU per splat lane instead of ~30.
+__device__ __forceinline__ float quad_log_thr(float opacity) {
+    return __builtin_amdgcn_logf(opacity * 255.0f) * 0.693147182f;
 }
 
 // getRect (auxiliary.h:45-55) with the int radius overload

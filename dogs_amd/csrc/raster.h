@@ -261,6 +261,7 @@ bool bin_emit_orders();
 // count mode: score[i] = gcount[i] x the (AA-scaled) opacity of splat record i (0 when culled)
 void launch_count_score(int P, const int* radii, const float4* sp, const uint32_t* gcount, float* score,
                         hipStream_t s);
+void launch_cull_log_threshold(int64_t n, const float* opacity, float* thr, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);
 void launch_filter(const PreArgs& a, hipStream_t s);
 // the replay; order_ready: the forward's phase-2 emission already wrote the replay order, else one block sorts it

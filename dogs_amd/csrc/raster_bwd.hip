@@ -261,7 +261,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, int tile
             const float2 m = make_float2(s0.x, s0.y);
             const float4 c4 = make_float4(s0.z, s0.w, s1.x, s1.y);
             const float4 q = a.rgbi[g];
-            const float thr = gs_logf(c4.w / (1.0f / 255.0f));
+            const float thr = quad_log_thr(c4.w);
             qm = quad_mask({c4.x, c4.y, c4.z, c4.w}, m.x, m.y, thr, tx0, ty0);
 #pragma unroll
             for (int k = 0; k < 4; k++) qm &= (j < qlast[k]) ? 0xfu : ~(1u << k);

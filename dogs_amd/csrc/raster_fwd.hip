@@ -590,7 +590,7 @@ __device__ __forceinline__ BinLane bin_lane(const BinArgs& a, int g, int lane, u
             if (m) {
                 b.co = make_float4(s0.z, s0.w, s1.x, s1.y);
                 b.mx = s0.x; b.my = s0.y;
-                b.lthr = gs_logf(b.co.w / (1.0f / 255.0f));
+                b.lthr = gs_crlogf(b.co.w / (1.0f / 255.0f));
                 tight_rect(b);
             }
         }
@@ -795,7 +795,7 @@ __device__ __forceinline__ BinLane member_lane(const BinArgs& a, int g, bool mem
         sp_rect(s1, b.x0, b.y0, b.x1, b.y1);
         b.co = make_float4(s0.z, s0.w, s1.x, s1.y);
         b.mx = s0.x; b.my = s0.y;
-        b.lthr = gs_logf(b.co.w / (1.0f / 255.0f));
+        b.lthr = gs_crlogf(b.co.w / (1.0f / 255.0f));
         tight_rect(b);
         b.member = true;
     }
@@ -1073,7 +1073,7 @@ __global__ void __launch_bounds__(256) FWD_WPE_ATTR k_render_fwd(RenderArgs a) {
             const uint32_t g = min(a.eg[e], a.P - 1);
             const float4 s0 = a.sp[2 * g], s1 = a.sp[2 * g + 1];
             const float4 q = a.rgbi[g];
-            const float lthr = gs_logf(s1.y / (1.0f / 255.0f));
+            const float lthr = quad_log_thr(s1.y);
             touch = quad_mask({s0.z, s0.w, s1.x, s1.y}, s0.x, s0.y, lthr, tx0, ty0) != 0u;
             const SplatExp k = splat_exp_coeffs(s0.z, s0.w, s1.x);
             sb[lane * 3 + 0] = make_float4(s0.x, s0.y, k.A, k.B);
@@ -1621,6 +1621,13 @@ __global__ void __launch_bounds__(1024) k_render_fwd2x(RenderArgs a) {
     }
 }
 
+// the precise cull's threshold per opacity, exactly as the binning evaluates it (parity probe of gs_crlogf)
+__global__ void __launch_bounds__(256) k_cull_log_threshold(int64_t n, const float* __restrict__ opacity,
+                                                            float* __restrict__ thr) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) thr[i] = gs_crlogf(opacity[i] / (1.0f / 255.0f));
+}
+
 // checkFrustum (rasterizer_impl.cu:104-116)
 __global__ void __launch_bounds__(256) k_mark_visible(int P, const float* __restrict__ means3D,
                                                       const float* __restrict__ view, bool* __restrict__ present) {
@@ -1770,6 +1777,9 @@ __global__ void __launch_bounds__(256) k_count_score(int P, const int* __restric
 void launch_count_score(int P, const int* radii, const float4* sp, const uint32_t* gcount, float* score,
                         hipStream_t s) {
     if (P > 0) k_count_score<<<(P + 255) / 256, 256, 0, s>>>(P, radii, sp, gcount, score);
+}
+void launch_cull_log_threshold(int64_t n, const float* opacity, float* thr, hipStream_t s) {
+    if (n > 0) k_cull_log_threshold<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(n, opacity, thr);
 }
 void launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s) {
     if (P > 0) k_mark_visible<<<(P + 255) / 256, 256, 0, s>>>(P, means3D, view, present);

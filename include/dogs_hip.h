@@ -101,6 +101,11 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
 int dg_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                     uint8_t* present, dg_stream_t stream);
 
+/* The precise tile cull's threshold logf(opacity / (1/255)) of each of n opacities, with the arithmetic the binning
+ * uses (duplicateWithKeys, rasterizer_impl.cu:149-151: the correctly rounded logf).  A parity probe:
+ * the reference has no such entry; the tests compare it with the oracle on every opacity in (2^-24, 1]. */
+int dg_cull_log_threshold(int64_t n, const float* opacity, float* thr, dg_stream_t stream);
+
 /* Replaces RasterizeGaussiansFilterCUDA (rasterize_points.cu:276-334) / _C.rasterize_gaussians_filter:
  * radii [P] only (no low-pass filter), uses P, W, H, tanfov*, scale_modifier, means3D, scales,
  * rotations, cov3D_precomp, viewmatrix, projmatrix, prefiltered of `a`. */

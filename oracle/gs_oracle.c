@@ -15,8 +15,14 @@
  *   - glm matrices are column-major: m[col][row];
  *   - division and sqrt are IEEE correctly rounded (hipcc's default
  *     -fhip-fp32-correctly-rounded-divide-sqrt matches);
- *   - logf() in the precise tile cull uses the deterministic gs_logf() below,
- *     the same polynomial the HIP kernel evaluates;
+ *   - logf() in the precise tile cull (rasterizer_impl.cu:151) is gs_crlogf()
+ *     below: the correctly rounded logf, the closest stand-in for CUDA's logf
+ *     (<= 1 ulp), evaluated in double by the same operation sequence as the HIP
+ *     kernels' (gs_common.h), so oracle and kernels agree bit for bit and both
+ *     are correctly rounded on the cull's whole domain (all opacities, checked
+ *     exhaustively: gso_crlogf_check, tests/test_oracle_logf.py).  Until round 5
+ *     both used a float polynomial (gs_logf_r5 below, kept for the census
+ *     gso_logf_census) that is up to 3 ulp off on 7.7% of the opacities;
  *   - float->int conversions saturate (GPU v_cvt_i32_f32 semantics);
  *   - ndc2Pix is evaluated in double, as the reference's double literals imply
  *     (auxiliary.h:40-43).
@@ -56,11 +62,12 @@ typedef struct { float x, y, z, w; } v4;
 typedef struct { float m[3][3]; } mat3; /* glm column-major: m[col][row] */
 
 /* ------------------------------------------------------------------ */
-/* deterministic logf (shared algorithm with dogs_amd/csrc/gs_common.h)  */
+/* logf of the precise tile cull                                        */
 /* ------------------------------------------------------------------ */
-float gs_logf(float a) {
-    /* log(a) = e*ln2 + log(m), m in [sqrt(.5), sqrt(2)); log(m) = 2 atanh(s),
-       s = (m-1)/(m+1); odd series in s to s^9. |err| < 2 ulp on normals. */
+/* Round 5's deterministic float logf (the HIP kernels evaluated the same polynomial).  It is not the reference's:
+   on 7.7% of the opacities o in (2^-24, 1] its value of logf(o / (1/255)) is 1-3 ulp away from the correctly
+   rounded one.  Kept only for the flip census (gso_logf_census). */
+static float gs_logf_r5(float a) {
     if (!(a > 0.0f)) return (a == 0.0f) ? -INFINITY : NAN;
     if (a == INFINITY) return INFINITY;
     uint32_t u; memcpy(&u, &a, 4);
@@ -80,6 +87,68 @@ float gs_logf(float a) {
     p = fmaf(s2, p, 2.0f);
     float lm = s * p;
     return fmaf((float)e, 0.693147182f, lm);
+}
+
+/* Correctly rounded logf on the cull's domain (rasterizer_impl.cu:151: logf(co.w / (1/255)), co.w an opacity).
+   log(a) = e ln2 + 2 atanh(s), s = (m - 1)/(m + 1), m in [sqrt(1/2), sqrt(2)), in double: the atanh series to
+   s^19 (|s| <= 0.1716, truncation < 2^-60 relative), ln2 split hi/lo so e*ln2_hi is exact, then one rounding to
+   float.  Every operation is an IEEE double op (+, *, /, fma), so the GPU (gs_common.h, the same sequence) returns
+   the same bits.  The double result is within a few double ulps of log(a); on every float a in [2^-20, 256)
+   (2.35e8 inputs, a superset of the cull's o * 255) that rounds correctly except for the two inputs below, whose
+   exact logarithm lies within 3e-16 of a float midpoint (arbitrated at 80 digits, tests/test_oracle_logf.py). */
+float gs_crlogf(float a) {
+    if (!(a > 0.0f)) return (a == 0.0f) ? -INFINITY : NAN;
+    if (a == INFINITY) return INFINITY;
+    if (a == 0x1.827a74p-7f) return -0x1.1c2b1ep+2f;
+    if (a == 0x1.2f1fd6p+3f) return 0x1.1fcbcep+1f;
+    uint32_t u; memcpy(&u, &a, 4);
+    int e = 0;
+    if (u < 0x00800000u) { float b = a * 8388608.0f; memcpy(&u, &b, 4); e = -23; }
+    e += (int)((u >> 23) & 0xff) - 127;
+    uint32_t mu = (u & 0x007fffffu) | 0x3f800000u;
+    if (mu > 0x3fb504f3u) { mu -= 0x00800000u; e += 1; }   /* m in [sqrt(1/2), sqrt(2)) */
+    float mf; memcpy(&mf, &mu, 4);
+    const double m = (double)mf;
+    const double s = (m - 1.0) / (m + 1.0);
+    const double s2 = s * s;
+    double p = fma(s2, 0.10526315789473684, 0.11764705882352941);   /* 2/19, 2/17 */
+    p = fma(s2, p, 0.13333333333333333);                            /* 2/15 */
+    p = fma(s2, p, 0.15384615384615385);                            /* 2/13 */
+    p = fma(s2, p, 0.18181818181818182);                            /* 2/11 */
+    p = fma(s2, p, 0.22222222222222222);                            /* 2/9 */
+    p = fma(s2, p, 0.2857142857142857);                             /* 2/7 */
+    p = fma(s2, p, 0.4);                                            /* 2/5 */
+    p = fma(s2, p, 0.6666666666666666);                             /* 2/3 */
+    const double lm = fma(s * s2, p, 2.0 * s);
+    const double ed = (double)e;
+    return (float)fma(ed, 0x1.62e42fefa3800p-1, fma(ed, 0x1.ef35793c76730p-45, lm));
+}
+
+/* the cull threshold of n opacities (rasterizer_impl.cu:149-151), the oracle side of dg_cull_log_threshold */
+void gso_cull_log_threshold(int64_t n, const float* opacity, float* thr) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) thr[i] = gs_crlogf(opacity[i] / (1.0f / 255.0f));
+}
+
+/* Exhaustive check of gs_crlogf against logl (x87 80-bit, rounded once to float) over the float bit patterns
+   [lo, hi): returns the number of disagreements and writes up to max_bad of the disagreeing inputs (the caller
+   arbitrates them at high precision: logl's own error can misround within ~2^-40 of a midpoint). */
+int64_t gso_crlogf_check(uint32_t lo, uint32_t hi, float* bad, int64_t max_bad) {
+    int64_t nbad = 0;
+#pragma omp parallel for schedule(static, 65536) reduction(+ : nbad)
+    for (int64_t i = lo; i < (int64_t)hi; i++) {
+        const uint32_t u = (uint32_t)i;
+        float x; memcpy(&x, &u, 4);
+        if (gs_crlogf(x) != (float)logl((long double)x)) nbad++;
+    }
+    if (nbad > 0 && max_bad > 0) {   /* second, sequential pass for the (few) inputs themselves, in order */
+        int64_t k = 0;
+        for (uint32_t u = lo; u < hi && k < max_bad; u++) {
+            float x; memcpy(&x, &u, 4);
+            if (gs_crlogf(x) != (float)logl((long double)x)) bad[k++] = x;
+        }
+    }
+    return nbad;
 }
 
 /* threads of the parallel loops (OpenMP); <= 0 -> all cores.  Results do not depend on it. */
@@ -404,6 +473,54 @@ void gso_free(gso_ctx* c) {
     free(c);
 }
 
+/* The logf census: preprocess the view as gso_forward does, then walk every rendered
+   Gaussian's getRect tiles with the precise cull test (rasterizer_impl.cu:151, 171) under both thresholds: round 5's
+   gs_logf_r5 and the correctly rounded gs_crlogf.  out[0] (tile, Gaussian) pairs tested, out[1] kept under gs_crlogf,
+   out[2] kept only under gs_logf_r5, out[3] kept only under gs_crlogf, out[4] rendered Gaussians, out[5] of them with a
+   different threshold.  Returns 0, or 2 on OOM. */
+int gso_logf_census(const gso_params* prm, int64_t* out) {
+    gso_ctx* c = (gso_ctx*)calloc(1, sizeof(gso_ctx));
+    if (!c) return 2;
+    c->p = *prm;
+    const int P = prm->P;
+    c->focal_y = prm->H / (2.0f * prm->tanfovy);
+    c->focal_x = prm->W / (2.0f * prm->tanfovx);
+    c->tiles_x = (prm->W + BLOCK_X - 1) / BLOCK_X;
+    c->tiles_y = (prm->H + BLOCK_Y - 1) / BLOCK_Y;
+    c->num_tiles = c->tiles_x * c->tiles_y;
+    size_t Pn = P > 0 ? (size_t)P : 1;
+    c->depths = calloc(Pn, 4); c->radii = calloc(Pn, 4); c->means2D = calloc(Pn * 2, 4); c->cov3D = calloc(Pn * 6, 4);
+    c->conic_opacity = calloc(Pn * 4, 4); c->rgb = calloc(Pn * 3, 4); c->clamped = calloc(Pn * 3, 1);
+    c->tiles_touched = calloc(Pn, 4);
+    if (!c->depths || !c->radii || !c->means2D || !c->cov3D || !c->conic_opacity || !c->rgb || !c->clamped ||
+        !c->tiles_touched) { gso_free(c); return 2; }
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < P; i++) preprocess_one(c, i);
+    int64_t tested = 0, kept = 0, only_r5 = 0, only_cr = 0, rendered = 0, thr_diff = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : tested, kept, only_r5, only_cr, rendered, thr_diff)
+    for (int idx = 0; idx < P; idx++) {
+        if (!(c->radii[idx] > 0)) continue;
+        rendered++;
+        uint32_t rmin[2], rmax[2];
+        const float mx = c->means2D[2 * idx], my = c->means2D[2 * idx + 1];
+        get_rect(mx, my, c->radii[idx], rmin, rmax, c->tiles_x, c->tiles_y);
+        v4 co = {c->conic_opacity[4 * idx], c->conic_opacity[4 * idx + 1], c->conic_opacity[4 * idx + 2],
+                 c->conic_opacity[4 * idx + 3]};
+        const float t_cr = gs_crlogf(co.w / (1.0f / 255.0f)), t_r5 = gs_logf_r5(co.w / (1.0f / 255.0f));
+        thr_diff += t_cr != t_r5;
+        for (uint32_t y = rmin[1]; y < rmax[1]; y++)
+            for (uint32_t x = rmin[0]; x < rmax[0]; x++) {
+                const float p = max_contrib_power_rect(co, mx, my, (float)(x * BLOCK_X), (float)(y * BLOCK_Y),
+                                                       (float)((x + 1) * BLOCK_X - 1), (float)((y + 1) * BLOCK_Y - 1));
+                const int a = p <= t_cr, b = p <= t_r5;
+                tested++; kept += a; only_r5 += b && !a; only_cr += a && !b;
+            }
+    }
+    out[0] = tested; out[1] = kept; out[2] = only_r5; out[3] = only_cr; out[4] = rendered; out[5] = thr_diff;
+    gso_free(c);
+    return 0;
+}
+
 /* Rasterizer::forward, rasterizer_impl.cu:334-498.  out_color [3,H,W], out_invdepth [H,W], radii [P].
    Returns NULL on error (*err set: 1 = prefiltered violation, 2 = OOM). */
 gso_ctx* gso_forward(const gso_params* prm, float* out_color, float* out_invdepth, int* radii_out, int* err) {
@@ -459,7 +576,7 @@ gso_ctx* gso_forward(const gso_params* prm, float* out_color, float* out_invdept
             get_rect(mx, my, c->radii[idx], rmin, rmax, c->tiles_x, c->tiles_y);
             v4 co = {c->conic_opacity[4 * idx], c->conic_opacity[4 * idx + 1], c->conic_opacity[4 * idx + 2],
                      c->conic_opacity[4 * idx + 3]};
-            const float thr = gs_logf(co.w / (1.0f / 255.0f));
+            const float thr = gs_crlogf(co.w / (1.0f / 255.0f));
             uint32_t dbits; memcpy(&dbits, &c->depths[idx], 4);
             int64_t o = pass ? voff[idx] : 0;
             uint32_t cnt = 0;

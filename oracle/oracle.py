@@ -70,8 +70,13 @@ def lib():
                                C.c_uint32, C.c_uint32]
         L.gso_set_threads.argtypes = [C.c_int]
         L.gso_get_threads.restype = C.c_int
-        L.gs_logf.restype = C.c_float
-        L.gs_logf.argtypes = [C.c_float]
+        L.gs_crlogf.restype = C.c_float
+        L.gs_crlogf.argtypes = [C.c_float]
+        L.gso_crlogf_check.restype = C.c_int64
+        L.gso_crlogf_check.argtypes = [C.c_uint32, C.c_uint32, f32p, C.c_int64]
+        L.gso_cull_log_threshold.argtypes = [C.c_int64, f32p, f32p]
+        L.gso_logf_census.restype = C.c_int
+        L.gso_logf_census.argtypes = [C.POINTER(GsoParams), C.POINTER(C.c_int64)]
         L.aux_ssim_fwd.argtypes = [C.c_int] * 4 + [C.c_float, C.c_float] + [f32p] * 6
         L.aux_ssim_bwd.argtypes = [C.c_int] * 4 + [f32p] * 7
         L.aux_knn.restype = C.c_int
@@ -318,5 +323,40 @@ def knn_dist2(points):
     return out
 
 
-def gs_logf(x: float) -> float:
-    return float(lib().gs_logf(float(x)))
+def gs_crlogf(x: float) -> float:
+    """The cull's logf (gs_oracle.c gs_crlogf): correctly rounded on the cull's domain."""
+    return float(lib().gs_crlogf(float(x)))
+
+
+def cull_log_threshold(opacity) -> np.ndarray:
+    """logf(opacity / (1/255)) as the precise cull evaluates it (gs_crlogf), per element."""
+    o = _f(opacity).reshape(-1)
+    out = np.empty_like(o)
+    lib().gso_cull_log_threshold(o.size, _p(o), _p(out))
+    return out
+
+
+def crlogf_check(lo_bits: int, hi_bits: int, max_bad: int = 64):
+    """gs_crlogf against logl rounded to float over the float bit patterns [lo_bits, hi_bits): (count, inputs)."""
+    bad = np.zeros(max(max_bad, 1), np.float32)
+    n = int(lib().gso_crlogf_check(lo_bits, hi_bits, _p(bad), max_bad))
+    return n, bad[:min(n, max_bad)].copy()
+
+
+def logf_census(means3D, opacities, viewmatrix, projmatrix, campos, tanfovx, tanfovy, H, W, scales, rotations,
+                antialiasing=False):
+    """gso_logf_census: the precise cull's keep decisions under round 5's gs_logf and under gs_crlogf."""
+    means3D = _f(means3D).reshape(-1, 3)
+    keep = dict(o=_f(opacities).reshape(-1), v=_f(viewmatrix).reshape(16), p=_f(projmatrix).reshape(16),
+                c=_f(campos).reshape(3), s=_f(scales), r=_f(rotations), bg=np.zeros(3, np.float32),
+                col=np.zeros((means3D.shape[0], 3), np.float32))
+    prm = GsoParams(P=means3D.shape[0], D=0, M=0, W=int(W), H=int(H), prefiltered=0, antialiasing=int(antialiasing),
+                    scale_modifier=1.0, tanfovx=float(tanfovx), tanfovy=float(tanfovy), bg=_p(keep["bg"]),
+                    means3D=_p(means3D), colors=_p(keep["col"]),
+                    opacities=_p(keep["o"]), scales=_p(keep["s"]), rotations=_p(keep["r"]), cov3D_precomp=None,
+                    viewmatrix=_p(keep["v"]), projmatrix=_p(keep["p"]), dc=None, sh=None, campos=_p(keep["c"]))
+    out = (C.c_int64 * 6)()
+    if lib().gso_logf_census(C.byref(prm), out) != 0:
+        raise MemoryError("oracle census: allocation failed")
+    keys = ("tested", "kept", "kept_only_r5", "kept_only_cr", "rendered", "threshold_differs")
+    return dict(zip(keys, (int(v) for v in out)))

@@ -308,3 +308,28 @@ def test_forward_many_binning_waves(oracle, hip_device, per_tile):
         assert psnr(out[2].cpu().numpy(), col_o) > 80.0
     finally:
         _C.set_prefix_per_tile(old)
+
+
+def test_cull_log_threshold_every_opacity(oracle, hip_device):
+    """The binning's cull threshold logf(o / (1/255)) (rasterizer_impl.cu:151; gs_crlogf) equals the
+    oracle's bit for bit on EVERY float opacity in (2^-24, 1] (2.0e8 values, in chunks of 2^25), so the (tile,
+    Gaussian) keep decisions cannot differ at the threshold for any opacity."""
+    from dogs_amd import _lib
+    L = _lib.load()
+    lo, hi = 0x33800001, 0x3F800001                 # (2^-24, 1]
+    chunk = 1 << 25
+    oracle.set_threads(0)
+    checked = 0
+    for start in range(lo, hi, chunk):
+        bits = np.arange(start, min(start + chunk, hi), dtype=np.uint32)
+        o = bits.view(np.float32)
+        want = oracle.cull_log_threshold(o)
+        od = torch.from_numpy(o).to(hip_device)
+        got = torch.empty_like(od)
+        _lib.check(L.dg_cull_log_threshold(od.numel(), od.data_ptr(), got.data_ptr(),
+                                           _lib.stream_of(hip_device)))
+        g = got.cpu().numpy()
+        bad = np.flatnonzero(g.view(np.uint32) != want.view(np.uint32))
+        assert bad.size == 0, [(float(o[i]).hex(), float(g[i]).hex(), float(want[i]).hex()) for i in bad[:8]]
+        checked += o.size
+    assert checked == hi - lo
