@@ -157,12 +157,55 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, ddc, dsh, dscales, drot, depth
 
 
+_PLAN_LOCK = threading.Lock()
+_EAGER_PLANS: dict = {}      # device -> number of plans holding their buffers ahead of the backward
+
+
 class BackwardPlan:
     """What rasterize_gaussians_backward builds before its C call -- the argument struct, the ten gradient outputs (one
     buffer) and the DG_BUF_BACKWARD scratch (through dg_fixed_alloc, no allocation callback) -- made by the autograd
     forward right after its C call returns, while the GPU renders and the host would otherwise wait: the backward
-    (rasterize_gaussians_backward_planned) is then one C call, and the GPU does not idle while Python prepares it."""
-    __slots__ = ("a", "keep", "outs", "scratch", "fixed", "P")
+    (rasterize_gaussians_backward_planned) is then one C call, and the GPU does not idle while Python prepares it.
+
+    Only the argument struct and the sizes are always made in the forward.  The buffers (about 0.9 GB for a 1e6-Gaussian
+    1080p view) are allocated there only while no other plan on the device holds its buffers ("eager"): the training
+    loop's forward -> backward alternation keeps the hidden host work, while a caller that renders several grad-mode
+    views before one backward, or keeps a grad-mode render for metrics, holds at most one view's buffers ahead of
+    time -- the other plans allocate in their backward, as the reference does.  An eager plan hands its slot back when
+    its backward ran or when it is dropped with its autograd graph."""
+    __slots__ = ("a", "keep", "outs", "scratch", "fixed", "P", "M", "nbytes", "dev", "eager", "__weakref__")
+
+    def allocate(self) -> None:
+        if self.outs is not None:
+            return
+        P, M = self.P, self.M
+        shapes = [(P, 3), (P, 3), (P, 1), (P, 3), (P, 6), (P, 1, 3), (P, M, 3), (P, 3), (P, 4), (P, 1)]
+        sizes = [math.prod(sh) for sh in shapes]
+        with _lib.device_ctx(self.dev):
+            buf = torch.empty(sum(sizes), dtype=torch.float32, device=self.dev)
+            self.outs = tuple(t.view(sh) for t, sh in zip(torch.split(buf, sizes), shapes))
+            self.scratch = torch.empty(max(self.nbytes, 1), dtype=torch.uint8, device=self.dev)
+        self.fixed = _lib.DgFixedBuffer(self.scratch.data_ptr(), self.nbytes)
+
+    def release(self) -> None:
+        """Drop the scratch (the outputs belong to the caller once returned) and the eager slot."""
+        self.scratch = self.fixed = None
+        if self.eager:
+            self.eager = False
+            with _PLAN_LOCK:
+                _EAGER_PLANS[self.dev] -= 1
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:   # interpreter shutdown
+            pass
+
+
+def eager_plans(device) -> int:
+    """Plans on `device` whose buffers are allocated ahead of their backward (0 or 1)."""
+    with _PLAN_LOCK:
+        return _EAGER_PLANS.get(torch.device(device), 0)
 
 
 def backward_plan(background, means3D, colors, opacities, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
@@ -173,21 +216,20 @@ def backward_plan(background, means3D, colors, opacities, scales, rotations, sca
     if P == 0:
         return None
     dev = means3D.device
-    M = _sh_m(sh)
-    fopt = dict(dtype=torch.float32, device=dev)
-    shapes = [(P, 3), (P, 3), (P, 1), (P, 3), (P, 6), (P, 1, 3), (P, M, 3), (P, 3), (P, 4), (P, 1)]
-    sizes = [math.prod(sh) for sh in shapes]
     pl = BackwardPlan()
+    pl.P, pl.M, pl.dev, pl.eager = P, _sh_m(sh), dev, False
+    pl.outs = pl.scratch = pl.fixed = None
     with _lib.device_ctx(dev):
-        buf = torch.empty(sum(sizes), **fopt)
-        pl.outs = tuple(t.view(sh) for t, sh in zip(torch.split(buf, sizes), shapes))
-        pl.a, pl.keep = _args(P, degree, M, int(image_width), int(image_height), background, means3D, colors, opacities,
-                              scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
-                              tan_fovy, dc, sh, campos, False, antialiasing, debug)
-        nbytes = int(_lib.load().dg_backward_scratch_bytes(C.byref(pl.a), int(num_rendered)))
-        pl.scratch = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
-    pl.fixed = _lib.DgFixedBuffer(pl.scratch.data_ptr(), nbytes)
-    pl.P = P
+        pl.a, pl.keep = _args(P, degree, pl.M, int(image_width), int(image_height), background, means3D, colors,
+                              opacities, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
+                              tan_fovx, tan_fovy, dc, sh, campos, False, antialiasing, debug)
+        pl.nbytes = int(_lib.load().dg_backward_scratch_bytes(C.byref(pl.a), int(num_rendered)))
+    with _PLAN_LOCK:
+        if _EAGER_PLANS.get(dev, 0) == 0:
+            _EAGER_PLANS[dev] = 1
+            pl.eager = True
+    if pl.eager:
+        pl.allocate()
     return pl
 
 
@@ -198,12 +240,14 @@ def rasterize_gaussians_backward_planned(plan, radii, dL_dout_color, dL_dout_inv
     dev = radii.device
     gc = _f32(dL_dout_color)
     gi = _f32(dL_dout_invdepth) if dL_dout_invdepth is not None else None
+    plan.allocate()
     o = plan.outs
     _lib.check(_lib.load().dg_rasterize_backward(
         C.byref(plan.a), radii.data_ptr(), geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
         _lib.ptr(sampleBuffer), int(R), int(B), gc.data_ptr(), _lib.ptr(gi), o[0].data_ptr(), o[1].data_ptr(),
         o[2].data_ptr(), o[3].data_ptr(), o[4].data_ptr(), o[5].data_ptr(), _lib.ptr(o[6]), o[7].data_ptr(),
         o[8].data_ptr(), o[9].data_ptr(), _lib.fixed_alloc_fn(), C.byref(plan.fixed), _lib.stream_of(dev)))
+    plan.release()
     return o
 
 

@@ -55,8 +55,8 @@ class _RasterizeGaussians(torch.autograd.Function):
         else:
             out = _C.rasterize_gaussians(*args)
         num_rendered, num_buckets, color, invdepths, radii, geomBuffer, binningBuffer, imgBuffer, sampleBuffer = out
-        # the backward's arguments, outputs and scratch, prepared now: the GPU is still rendering this view, so this
-        # host work is hidden here and off the backward's launch path
+        # the backward's arguments (and, when no other plan holds its buffers, its outputs and scratch), prepared now:
+        # the GPU is still rendering this view, so this host work is hidden here and off the backward's launch path
         ctx.plan = None
         if not rs.debug and getattr(_GRAD_MODE, "on", True) and any(ctx.needs_input_grad):
             ctx.plan = _C.backward_plan(rs.bg, means3D, colors_precomp, opacities, scales, rotations, rs.scale_modifier,

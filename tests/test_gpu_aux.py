@@ -144,6 +144,79 @@ def test_mark_visible_and_filter_bitexact(oracle, hip_device):
     np.testing.assert_array_equal(r.cpu().numpy(), r_o)
 
 
+def test_several_grad_forwards_hold_one_plan(hip_device):
+    """the autograd forward prepares its backward's buffers ahead (BackwardPlan) only while no other plan on
+    the device holds them.  Two grad-mode renders before one backward: the second allocates nothing ahead (its
+    forward grows the allocated memory by less than the first one's plan), both backwards give the gradients of
+    separate single-view backwards bit for bit, and every slot is handed back -- after the backwards, and when a
+    grad-mode render is dropped without a backward."""
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from dogs_amd.diff_gaussian_rasterization import _C
+    n, W, H = 200_000, 1280, 720
+    s = small_scene(n, W, H, seed=33)
+    c = s.camera.to(hip_device)
+    st = GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=c.tanfovx, tanfovy=c.tanfovy,
+                                       bg=torch.zeros(3, device=hip_device), scale_modifier=1.0,
+                                       viewmatrix=c.world_to_camera, projmatrix=c.projective_matrix, sh_degree=3,
+                                       campos=c.camera_center, prefiltered=False, debug=False)
+    r = GaussianRasterizer(st)
+    leaf = {k: getattr(s, k).to(hip_device).clone().requires_grad_(True)
+            for k in ("means3D", "opacities", "scales", "rotations", "dc", "sh")}
+    g1 = torch.randn((3, H, W), generator=torch.Generator().manual_seed(1)).to(hip_device)
+    g2 = torch.randn((3, H, W), generator=torch.Generator().manual_seed(2)).to(hip_device)
+
+    def render():
+        m2 = torch.zeros_like(leaf["means3D"], requires_grad=True)
+        return r(leaf["means3D"], m2, leaf["opacities"], dc=leaf["dc"], shs=leaf["sh"], scales=leaf["scales"],
+                 rotations=leaf["rotations"])[0]
+
+    def grads():
+        out = {k: t.grad.clone() for k, t in leaf.items()}
+        for t in leaf.values():
+            t.grad = None
+        return out
+
+    old = _C.set_prefix_per_tile(448)     # a fixed phase-1 capacity: the same instance numbering in every render
+    try:
+        _two_forwards_one_backward(render, grads, leaf, g1, g2, n, hip_device)
+    finally:
+        _C.set_prefix_per_tile(old)
+
+
+def _two_forwards_one_backward(render, grads, leaf, g1, g2, n, hip_device):
+    from dogs_amd.diff_gaussian_rasterization import _C
+    torch.cuda.synchronize()
+    assert _C.eager_plans(hip_device) == 0
+    (render() * g1).sum().backward()
+    want1 = grads()
+    (render() * g2).sum().backward()
+    want2 = grads()
+    assert _C.eager_plans(hip_device) == 0
+    torch.cuda.synchronize()
+    m0 = torch.cuda.memory_allocated(hip_device)
+    a = render()
+    torch.cuda.synchronize()
+    m1 = torch.cuda.memory_allocated(hip_device)
+    b = render()
+    torch.cuda.synchronize()
+    m2 = torch.cuda.memory_allocated(hip_device)
+    assert _C.eager_plans(hip_device) == 1
+    plan_bytes = n * (3 + 3 + 1 + 3 + 6 + 3 + 45 + 3 + 4 + 1) * 4
+    assert (m2 - m1) < (m1 - m0) - plan_bytes // 2, (m0, m1, m2, plan_bytes)
+    (a * g1).sum().backward()
+    got1 = grads()
+    (b * g2).sum().backward()
+    got2 = grads()
+    assert _C.eager_plans(hip_device) == 0
+    for k in leaf:
+        assert torch.equal(got1[k], want1[k]), k
+        assert torch.equal(got2[k], want2[k]), k
+    d = render()            # a grad-mode render kept for a metric, then dropped without a backward
+    assert _C.eager_plans(hip_device) == 1
+    del d
+    assert _C.eager_plans(hip_device) == 0
+
+
 def test_gaussian_rasterizer_autograd(oracle, hip_device):
     """GaussianRasterizer (the import surface callers use) end to end: forward image and the autograd gradients
     of means3D / dc / sh / opacities / scales / rotations against the oracle, depth_threshold = 0."""
