@@ -97,7 +97,7 @@ class DgBox2dSet(C.Structure):
                 ("box", (C.c_double * 4) * DG_MAX_BOXES)]
 
 EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count", "dg_mark_visible", "dg_rasterize_filter",
-           "dg_cull_log_threshold",
+           "dg_cull_log_threshold", "dg_conv3x3_wgrad", "dg_conv3x3_wgrad_scratch_bytes",
            "dg_adam_update", "dg_fused_ssim_forward", "dg_fused_ssim_backward", "dg_fused_ssim_parts",
            "dg_fused_ssim_mean", "dg_fused_ssim_mean_backward", "dg_mean_of_parts", "dg_dist_cuda2",
            "dg_geom_bytes", "dg_image_bytes", "dg_binning_bytes", "dg_backward_scratch_bytes", "dg_fixed_alloc",
@@ -141,6 +141,10 @@ def load(path: str | None = None):
         L.dg_mark_visible.argtypes = [C.c_int, vp, vp, vp, vp, vp]
         L.dg_rasterize_filter.restype = C.c_int
         L.dg_cull_log_threshold.restype = C.c_int
+        L.dg_conv3x3_wgrad_scratch_bytes.restype = C.c_size_t
+        L.dg_conv3x3_wgrad_scratch_bytes.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int]
+        L.dg_conv3x3_wgrad.restype = C.c_int
+        L.dg_conv3x3_wgrad.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, C.c_size_t, vp]
         L.dg_cull_log_threshold.argtypes = [C.c_int64, vp, vp, vp]
         L.dg_rasterize_filter.argtypes = [C.POINTER(DgRasterArgs), vp, vp]
         L.dg_adam_update.restype = C.c_int

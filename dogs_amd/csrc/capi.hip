@@ -19,6 +19,7 @@
 #include "aux_kernels.h"
 #include "blocksplit.h"
 #include "optim.h"
+#include "mask_conv.h"
 #include "export.h"
 #include "raster.h"
 #include "sortscan.h"
@@ -872,6 +873,22 @@ int dg_mark_visible(int P, const float* means3D, const float* viewmatrix, const 
                     dg_stream_t stream) {
     (void)projmatrix;
     gs::launch_mark_visible(P, means3D, viewmatrix, (bool*)present, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+size_t dg_conv3x3_wgrad_scratch_bytes(int Cin, int Cout, int H, int W) {
+    if (Cin < 1 || Cout < 1 || H < 1 || W < 1) return 0;
+    return gs::conv3x3_wgrad_scratch_bytes(Cin, Cout, H, W);
+}
+
+int dg_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const float* dy, float* dw, float* db,
+                     void* scratch, size_t scratch_bytes, dg_stream_t stream) {
+    if (H < 1 || W < 1 || !x || !dy || !dw || !db || !scratch) return fail("conv3x3_wgrad: bad args%s%d");
+    if (!gs::conv3x3_wgrad_supported(Cin, Cout)) return fail("conv3x3_wgrad: unsupported channel counts%s%d", "", Cin * Cout);
+    if (scratch_bytes < gs::conv3x3_wgrad_scratch_bytes(Cin, Cout, H, W))
+        return fail("conv3x3_wgrad: scratch too small%s%d");
+    gs::launch_conv3x3_wgrad(Cin, Cout, H, W, x, dy, dw, db, (float*)scratch, (hipStream_t)stream);
     HIP_OK(hipGetLastError());
     return 0;
 }

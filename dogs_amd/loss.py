@@ -11,6 +11,16 @@ import torch
 from . import _lib
 
 _STAMPS = itertools.count(1)
+_RING = 4096
+_RINGS: dict = {}
+
+
+def _stamp_ring(device) -> torch.Tensor:
+    """The zero-stamp words of _RowProd on `device` (zeroed once; stamps start at 1)."""
+    r = _RINGS.get(device)
+    if r is None:
+        r = _RINGS[device] = torch.zeros(_RING, dtype=torch.int32, device=device)
+    return r
 
 
 class _ClampL1(torch.autograd.Function):
@@ -62,7 +72,10 @@ class _RowProd(torch.autograd.Function):
     """torch.prod(x, dim=1) for x [N, M <= 3] through dg_row_prod_forward / dg_row_prod_backward: the same values and
     gradients as torch's, without prod_backward's host read of the zero count (a stream sync in the middle of every
     training backward; the kernels keep the zero test on the device: the forward stamps a device word with the call's
-    stamp when some element is 0, the backward compares it with the same stamp)."""
+    stamp when some element is 0, the backward compares it with the same stamp).  The words are a persistent,
+    zero-initialised ring per device (call i uses word i mod 4096 with stamp i): a word only ever holds the stamp of an
+    earlier call of its slot, so stale memory cannot match, and up to 4096 forwards may await their
+    backward."""
 
     @staticmethod
     def forward(ctx, x):
@@ -73,8 +86,9 @@ class _RowProd(torch.autograd.Function):
         xc = x.detach().contiguous()
         n, m = int(xc.size(0)), int(xc.size(1))
         prod = torch.empty(n, dtype=torch.float32, device=x.device)
-        flag = torch.empty(1, dtype=torch.int32, device=x.device)   # the zero stamp: not zeroed (no memset launch)
-        stamp = next(_STAMPS) & 0xFFFFFFFF or 1
+        i = next(_STAMPS)
+        stamp = i & 0xFFFFFFFF or 1
+        flag = _stamp_ring(x.device)[i % _RING:i % _RING + 1]
         with _lib.device_ctx(x.device):
             _lib.check(_lib.load().dg_row_prod_forward(n, m, xc.data_ptr(), prod.data_ptr(), flag.data_ptr(), stamp,
                                                        _lib.stream_of(x.device)))

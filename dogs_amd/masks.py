@@ -21,12 +21,19 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-# MIOpen's default find mode times candidate kernels on first use, so processes sharing a GPU (the ADMM ranks of one
-# box, or a run next to another job) can pick different convolution algorithms for the same problem and round
-# differently: the masked pre-phase then drifts between ranks and the sequential baseline from the first iteration
-# (tools/mask_conc_probe.py: four concurrent processes differ at iteration 1; with FAST, bit-identical).  FAST takes the
-# find-db or the immediate-mode heuristic, never a timing.  setdefault: an explicit MIOPEN_FIND_MODE wins.
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+
+
+def ensure_fast_find_mode() -> None:
+    """MIOpen's default find mode times candidate kernels on first use, so processes sharing a GPU (the ADMM ranks of
+    one box, or a run next to another job) can pick different convolution algorithms for the same problem and round
+    differently: the masked pre-phase then drifts between ranks and the sequential baseline from the first iteration
+    (tools/mask_conc_probe.py: four concurrent processes differ at iteration 1; with FAST, bit-identical).  FAST takes
+    the find-db or the immediate-mode heuristic, never a timing.  Called when an AppearanceEmbedding is built (before
+    its first convolution; not at import: ADVICE r5) and by the entry points (admm_run.main, bench.py) before anything
+    touches the GPU; an explicit MIOPEN_FIND_MODE wins.  MIOpen reads it when its handle is created, so a process
+    that ran a convolution before building the embedding keeps its earlier mode."""
+    os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+
 
 EMBEDDING_DIM = 64
 MASK_DOWNSAMPLE = 32          # camera_origin.downsample(32) (gaussian_trainer.py:394)
@@ -34,12 +41,73 @@ _STAGE_CHANNELS = (256, 128, 64, 32)
 
 
 def _conv3(cin: int, cout: int) -> nn.Conv2d:
-    return nn.Conv2d(cin, cout, kernel_size=3, padding=1)
+    return Conv3x3(cin, cout)
+
+
+class Conv3x3(nn.Conv2d):
+    """nn.Conv2d(cin, cout, 3, padding=1) -- the same parameters and forward -- whose backward takes the weight and
+    bias gradients from dg_conv3x3_wgrad (a fixed-order reduction, no atomics) when the library supports the channel
+    counts.  MIOpen's deterministic weight-gradient algorithm for the embedding's full-resolution convolutions (a
+    Winograd WrW kernel) takes 83 ms per 1080p call, 200 ms per masked iteration; its fast ones use atomics.  The input
+    gradient stays MIOpen's (im2col GEMM + col2im: deterministic)."""
+
+    def __init__(self, cin: int, cout: int) -> None:
+        super().__init__(cin, cout, kernel_size=3, padding=1)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda and _native_wgrad(self.in_channels, self.out_channels):
+            return _Conv3x3Fn.apply(x, self.weight, self.bias)
+        return super().forward(x)
+
+
+def _native_wgrad(cin: int, cout: int) -> bool:
+    return cin * cout <= 4096
+
+
+class _Conv3x3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return F.conv2d(x, weight, bias, padding=1)
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import _lib
+        x, w = ctx.saved_tensors
+        x4 = x if x.dim() == 4 else x.unsqueeze(0)
+        g4 = (g if g.dim() == 4 else g.unsqueeze(0)).contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(g4, x4, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
+            dx = dx if x.dim() == 4 else dx[0]
+        dw = db = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            cout, cin = int(w.shape[0]), int(w.shape[1])
+            dw = torch.empty_like(w)
+            db = torch.empty(cout, dtype=torch.float32, device=w.device)
+            xc = x4.contiguous()
+            L = _lib.load()
+            for b in range(int(x4.shape[0])):    # one image per call, summed in batch order
+                H, W = int(x4.shape[2]), int(x4.shape[3])
+                nbytes = int(L.dg_conv3x3_wgrad_scratch_bytes(cin, cout, H, W))
+                scratch = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=w.device)
+                dwb, dbb = (dw, db) if b == 0 else (torch.empty_like(dw), torch.empty_like(db))
+                with _lib.device_ctx(w.device):
+                    _lib.check(L.dg_conv3x3_wgrad(cin, cout, H, W, xc[b].data_ptr(), g4[b].data_ptr(), dwb.data_ptr(),
+                                                  dbb.data_ptr(), scratch.data_ptr(), nbytes,
+                                                  _lib.stream_of(w.device)))
+                if b:
+                    dw += dwb
+                    db += dbb
+        return dx, dw, (db if ctx.has_bias else None)
 
 
 class AppearanceEmbedding(nn.Module):
     def __init__(self, num_views: int, embedding_dim: int = EMBEDDING_DIM) -> None:
         super().__init__()
+        ensure_fast_find_mode()
         self.appearance_embedding = nn.Parameter(torch.zeros(num_views, embedding_dim))
         self.fusion = _conv3(embedding_dim + 3, _STAGE_CHANNELS[0])
         stages = []

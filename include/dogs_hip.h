@@ -101,6 +101,15 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
 int dg_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                     uint8_t* present, dg_stream_t stream);
 
+/* The weight gradient of the appearance embedding's 3x3 convolutions (conerf/model/gaussian_fields/masks.py:8-54,
+ * geometry.mask; replaces the MIOpen/cuDNN backward-weights call torch makes for nn.Conv2d(k=3, padding=1)):
+ * dw [Cout][Cin][3][3] = sum over pixels of dy[co] x [ci] shifted, db [Cout] = sum of dy[co], for x [Cin][H][W] and
+ * dy [Cout][H][W] (one image).  Deterministic (fixed-order partial sums, no atomics).  Cin * Cout <= 4096 (an error
+ * otherwise); scratch of dg_conv3x3_wgrad_scratch_bytes() bytes. */
+size_t dg_conv3x3_wgrad_scratch_bytes(int Cin, int Cout, int H, int W);
+int dg_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const float* dy, float* dw, float* db,
+                     void* scratch, size_t scratch_bytes, dg_stream_t stream);
+
 /* The precise tile cull's threshold logf(opacity / (1/255)) of each of n opacities, with the arithmetic the binning
  * uses (duplicateWithKeys, rasterizer_impl.cu:149-151: the correctly rounded logf).  A parity probe:
  * the reference has no such entry; the tests compare it with the oracle on every opacity in (2^-24, 1]. */

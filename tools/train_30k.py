@@ -129,6 +129,7 @@ def run_full(args, dev):
     cfg = reference_cfg(**over)
     m, cams, gts = problem(dev, args.n_true, args.n_init, args.width, args.height, args.fx, args.views)
     tr_idx, te_idx = split(cams, gts)
+    torch.manual_seed(0)
     tr = GaussianSplatTrainer(m, [cams[i] for i in tr_idx], [gts[i] for i in tr_idx], cfg, device=dev, seed=42,
                               native=True)
     rec = {"workload": "mipnerf360.yaml schedule (config 2), synthetic 1e6-Gaussian 1080p scene",
@@ -198,6 +199,7 @@ def run_compare(args, dev):
         m, cams, gts = problem(dev, args.n_true, args.n_init, args.width, args.height, args.fx, args.views)
         tr_idx, te_idx = split(cams, gts)
         g = torch.Generator(device=dev).manual_seed(7)
+        torch.manual_seed(0)    # the appearance embedding's initial weights: the same for both routes
         tr = GaussianSplatTrainer(m, [cams[i] for i in tr_idx], [gts[i] for i in tr_idx], cfg, device=dev, seed=42,
                                   native=native, normal=lambda mean, std: torch.normal(mean, std, generator=g))
         losses, counts = [], []
