@@ -442,6 +442,47 @@ SWEEP = (  # (name, N, W, H, raw-opacity mean): north_star's other N, the 4K con
 )
 
 
+def phase_profile(views, yaws, vstats, pmc: dict) -> dict:
+    """One profiled pass over the views (per-phase hipEvent durations on the stream the kernels run on): per phase
+    its ms per view, the algorithmic bytes of the work it did (phase_bytes) and their fraction of the HBM peak, the
+    dominant phase (the most time among phases with bytes), and the render kernels' VALU issue fraction when the PMC
+    passes of this workload are committed (profiles/pmc_traffic.json)."""
+    import dogs_amd._lib as L
+    torch.cuda.synchronize()
+    views.i = 0
+    L.profile_enable(True)
+    for _ in range(len(yaws)):
+        views.step()
+    torch.cuda.synchronize()
+    prof = L.profile_collect()
+    L.profile_enable(False)
+    nv = float(len(yaws))
+    phase_ms = {k: v[0] / nv for k, v in prof.items()}
+    phase_b = {k: float(np.mean([phase_bytes(k, r) for r in vstats])) for k in phase_ms}
+    dom = max(phase_ms, key=lambda k: phase_ms[k] if phase_b.get(k, 0) > 0 else -1.0)
+
+    def valu(phase):
+        e = pmc.get(phase)
+        if not isinstance(e, dict) or "valu_insts" not in e:
+            return None
+        t = phase_ms[phase] * 1e-3
+        out = {"insts": e["valu_insts"], "achieved_ginst_s": round(e["valu_insts"] / t / 1e9, 1),
+               "peak_ginst_s": VALU_PEAK_GINST, "frac": round(e["valu_insts"] / t / 1e9 / VALU_PEAK_GINST, 4)}
+        if "valu_busy" in e:
+            out["busy"] = e["valu_busy"]
+        if "hbm_bytes" in e:
+            out["traffic"] = e["hbm_bytes"]
+        return out
+
+    return {"phase_ms_raw": phase_ms, "phase_b_raw": phase_b, "dominant": dom,
+            "phases_ms": {k: round(v, 4) for k, v in sorted(phase_ms.items(), key=lambda kv: -kv[1])},
+            "phase_bytes": {k: round(v) for k, v in phase_b.items() if v > 0},
+            "phase_hbm_frac": {k: round(phase_b[k] / (phase_ms[k] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                               for k in phase_ms if phase_b.get(k, 0) > 0 and phase_ms[k] > 0},
+            "view_bytes": float(sum(phase_b.values())),
+            "valu": {k: valu(k) for k in ("render_bwd", "render_fwd") if k in phase_ms}}
+
+
 def sweep_leg(dev, yaws, seed, steps=16, warmup=8, only=None):
     """After the headline: the same fwd+bwd view step (same yaw batch, cold adaptive capacity, warm-up, barrier-free
     single-rank timing) on the other workloads of SURVEY.md §8(d) / north_star -- N in {1e5, 5e6} at 1080p, 1e6 at
@@ -471,15 +512,23 @@ def sweep_leg(dev, yaws, seed, steps=16, warmup=8, only=None):
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / steps * 1e3
         st = [v.stats(k) for k in range(len(yaws))]
+        for r in st:
+            r.update(N=n, HW=W * H)
         K = float(np.mean([r["K"] for r in st]))
         ref_b = reference_view_bytes(n, int(K), W * H)
+        pmc_key = f"{n}x{W}x{H}" + ("-sparse" if om != 0.0 else "")
+        prof = phase_profile(v, yaws, st, load_pmc_key(pmc_key))
         out[name] = {"N": n, "width": W, "height": H, "raw_opacity_mean": om,
                      "views_per_s": round(1e3 / ms, 2), "ms_per_view": round(ms, 4),
                      "e1_mean": round(float(np.mean([r["e1"] for r in st]))),
                      "e2_mean": round(float(np.mean([r["e2"] for r in st]))),
                      "unfinished_tiles_mean": round(float(np.mean([r["unfinished_tiles"] for r in st])), 1),
                      "K_mean": round(K), "tiles": ((W + 15) // 16) * ((H + 15) // 16),
-                     "reference_equivalent_view_frac": round(ref_b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                     "reference_equivalent_view_frac": round(ref_b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "view_frac": round(prof["view_bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "dominant": prof["dominant"], "phases_ms": prof["phases_ms"],
+                     "phase_bytes": prof["phase_bytes"], "phase_hbm_frac": prof["phase_hbm_frac"],
+                     "valu": prof["valu"], "pmc_key": pmc_key}
         del v, s, cams, st
         gc.collect()
         torch.cuda.empty_cache()
@@ -494,13 +543,18 @@ def max_over(ws: int, dev, x: float) -> float:
     return float(t.item())
 
 
-def load_pmc(n: int, W: int, H: int):
-    """Per-phase HBM bytes and VALU figures per launch from the committed PMC passes (tools/pmc_traffic.py)."""
+def load_pmc_key(key: str) -> dict:
+    """Per-phase HBM bytes and VALU figures per launch from the committed PMC passes (tools/pmc_traffic.py), keyed by
+    workload ("{N}x{W}x{H}", "-sparse" for the non-saturating scene)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        return json.load(open(path)).get(f"{n}x{W}x{H}", {})
+        return json.load(open(path)).get(key, {})
     except Exception:  # noqa: BLE001
         return {}
+
+
+def load_pmc(n: int, W: int, H: int):
+    return load_pmc_key(f"{n}x{W}x{H}")
 
 
 def main():
@@ -648,35 +702,14 @@ def main():
         r = views.stats(k, reference_k=not args.no_reference_k)
         r.update(view=k, yaw=round(y, 3), N=n, HW=HW)
         vstats.append(r)
-    torch.cuda.synchronize()
-    views.i = 0
-    L.profile_enable(True)
-    for _ in range(len(yaws)):
-        views.step()
-    torch.cuda.synchronize()
-    prof = L.profile_collect()
-    L.profile_enable(False)
-    nv = float(len(yaws))
-    phase_ms = {k: v[0] / nv for k, v in prof.items()}
-    phase_b = {k: float(np.mean([phase_bytes(k, r) for r in vstats])) for k in phase_ms}
-    dom = max(phase_ms, key=lambda k: phase_ms[k] if phase_b.get(k, 0) > 0 else -1.0)
+    pmc = load_pmc(n, W, H)
+    pp = phase_profile(views, yaws, vstats, pmc)
+    phase_ms, phase_b, dom = pp["phase_ms_raw"], pp["phase_b_raw"], pp["dominant"]
     dom_ms, dom_bytes = phase_ms[dom], phase_b[dom]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    view_bytes = float(sum(phase_b.values()))
+    view_bytes = pp["view_bytes"]
     K_mean = float(np.mean([r["K"] for r in vstats])) if not args.no_reference_k else float("nan")
     ref_bytes = reference_view_bytes(n, int(K_mean), HW) if K_mean == K_mean else float("nan")
-    pmc = load_pmc(n, W, H)
-
-    def valu(phase):
-        e = pmc.get(phase)
-        if not isinstance(e, dict) or "valu_insts" not in e:
-            return None
-        t = phase_ms[phase] * 1e-3
-        out = {"insts": e["valu_insts"], "achieved_ginst_s": round(e["valu_insts"] / t / 1e9, 1),
-               "peak_ginst_s": VALU_PEAK_GINST, "frac": round(e["valu_insts"] / t / 1e9 / VALU_PEAK_GINST, 4)}
-        if "valu_busy" in e:
-            out["busy"] = e["valu_busy"]
-        return out
 
     traffic = pmc.get(dom, {}).get("hbm_bytes") if isinstance(pmc.get(dom), dict) else None
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -685,7 +718,7 @@ def main():
             "view_bytes": round(view_bytes), "view_achieved_GBs": round(view_bytes / (view_ms * 1e-3) / 1e9, 1),
             "view_frac": round(view_bytes / (view_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "phase_bytes": {k: round(v) for k, v in phase_b.items() if v > 0},
-            "valu": {k: valu(k) for k in ("render_bwd", "render_fwd") if k in phase_ms},
+            "valu": pp["valu"], "phase_hbm_frac": pp["phase_hbm_frac"],
             "reference_equivalent": {
                 "formula": "856 N + 172 K + 64 HW (SURVEY.md 8(d), the reference's full per-tile lists)",
                 "view_bytes": round(ref_bytes) if ref_bytes == ref_bytes else None,
