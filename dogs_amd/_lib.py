@@ -98,6 +98,7 @@ class DgBox2dSet(C.Structure):
 
 EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count", "dg_mark_visible", "dg_rasterize_filter",
            "dg_cull_log_threshold", "dg_conv3x3_wgrad", "dg_conv3x3_wgrad_scratch_bytes",
+           "dg_mask_head_forward", "dg_mask_head_backward", "dg_mask_head_scratch_bytes", "dg_mask_head_nparams",
            "dg_adam_update", "dg_fused_ssim_forward", "dg_fused_ssim_backward", "dg_fused_ssim_parts",
            "dg_fused_ssim_mean", "dg_fused_ssim_mean_backward", "dg_mean_of_parts", "dg_dist_cuda2",
            "dg_geom_bytes", "dg_image_bytes", "dg_binning_bytes", "dg_backward_scratch_bytes", "dg_fixed_alloc",
@@ -144,6 +145,13 @@ def load(path: str | None = None):
         L.dg_conv3x3_wgrad_scratch_bytes.restype = C.c_size_t
         L.dg_conv3x3_wgrad_scratch_bytes.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int]
         L.dg_conv3x3_wgrad.restype = C.c_int
+        L.dg_mask_head_forward.restype = C.c_int
+        L.dg_mask_head_forward.argtypes = [C.c_int] * 4 + [vp] * 6 + [vp]
+        L.dg_mask_head_backward.restype = C.c_int
+        L.dg_mask_head_backward.argtypes = [C.c_int] * 4 + [vp] * 9 + [C.c_size_t, vp]
+        L.dg_mask_head_scratch_bytes.restype = C.c_size_t
+        L.dg_mask_head_scratch_bytes.argtypes = [C.c_int, C.c_int]
+        L.dg_mask_head_nparams.restype = C.c_int
         L.dg_conv3x3_wgrad.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, C.c_size_t, vp]
         L.dg_cull_log_threshold.argtypes = [C.c_int64, vp, vp, vp]
         L.dg_rasterize_filter.argtypes = [C.POINTER(DgRasterArgs), vp, vp]

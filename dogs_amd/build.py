@@ -13,7 +13,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(OUT_DIR, "libdogs_hip.so")
 SOURCES = ["sortscan.hip", "raster_fwd.hip", "raster_bwd.hip", "aux_kernels.hip", "optim.hip", "export.hip", "loader.hip", "blocksplit.hip",
-           "colmap.hip", "mask_conv.hip", "capi.hip"]
+           "colmap.hip", "mask_conv.hip", "mask_head.hip", "capi.hip"]
 ARCH = os.environ.get("DOGS_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off + explicit fmaf and correctly rounded div/sqrt: the bit-exact key contract with the
 # CPU oracle (DESIGN.md "Bit-exact keys").

@@ -893,6 +893,54 @@ int dg_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const floa
     return 0;
 }
 
+static bool head_shape_ok(int H, int W, int h2, int w2) {
+    // the adjoint gather lists at most 12 samples per source index and axis: upsampling by at most 4
+    return H > 0 && W > 0 && h2 > 0 && w2 > 0 && H <= 4 * h2 && W <= 4 * w2;
+}
+
+static gs::HeadArgs head_args(int H, int W, int h2, int w2, const float* u, const float* w1, const float* b1,
+                              const float* w2p, const float* b2) {
+    gs::HeadArgs a = {};
+    a.H = H; a.W = W; a.h2 = h2; a.w2 = w2;
+    a.sh = (float)h2 / (float)H; a.sw = (float)w2 / (float)W;
+    a.U = u; a.k1 = w1; a.b1 = b1; a.k2 = w2p; a.b2 = b2;
+    return a;
+}
+
+int dg_mask_head_forward(int H, int W, int h2, int w2, const float* u, const float* w1, const float* b1,
+                         const float* w2p, const float* b2, float* mask, dg_stream_t stream) {
+    if (!head_shape_ok(H, W, h2, w2) || !u || !w1 || !b1 || !w2p || !b2 || !mask)
+        return fail("mask_head_forward: bad args%s%d");
+    gs::HeadArgs a = head_args(H, W, h2, w2, u, w1, b1, w2p, b2);
+    a.mask = mask;
+    gs::launch_mask_head_fwd(a, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+size_t dg_mask_head_scratch_bytes(int H, int W) {
+    if (H < 1 || W < 1) return 0;
+    const size_t HW = (size_t)H * W;
+    return (24 * HW + (size_t)gs::mask_head_tiles(H, W) * gs::mask_head_nparams()) * sizeof(float);
+}
+
+int dg_mask_head_nparams(void) { return gs::mask_head_nparams(); }
+
+int dg_mask_head_backward(int H, int W, int h2, int w2, const float* u, const float* w1, const float* b1,
+                          const float* w2p, const float* b2, const float* dmask, float* du, float* dparams,
+                          void* scratch, size_t scratch_bytes, dg_stream_t stream) {
+    if (!head_shape_ok(H, W, h2, w2) || !u || !w1 || !b1 || !w2p || !b2 || !dmask || !du || !dparams || !scratch)
+        return fail("mask_head_backward: bad args%s%d");
+    if (scratch_bytes < dg_mask_head_scratch_bytes(H, W)) return fail("mask_head_backward: scratch too small%s%d");
+    gs::HeadArgs a = head_args(H, W, h2, w2, u, w1, b1, w2p, b2);
+    const size_t HW = (size_t)H * W;
+    float* f = (float*)scratch;
+    a.dmask = dmask; a.dh = f; a.dx = f + 8 * HW; a.part = f + 24 * HW; a.du = du;
+    gs::launch_mask_head_bwd(a, dparams, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
 int dg_cull_log_threshold(int64_t n, const float* opacity, float* thr, dg_stream_t stream) {
     if (n < 0 || (n > 0 && (!opacity || !thr))) return fail("bad args%s%d");
     gs::launch_cull_log_threshold(n, opacity, thr, (hipStream_t)stream);

@@ -10,4 +10,21 @@ size_t conv3x3_wgrad_scratch_bytes(int Cin, int Cout, int H, int W);
 bool conv3x3_wgrad_supported(int Cin, int Cout);
 void launch_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const float* dy, float* dw, float* db,
                           float* scratch, hipStream_t st);
+
+// The embedding's full-resolution head (mask_head.hip): mask [3][H][W] = conv2(relu(conv1(resize(u)))), u [16][h2][w2],
+// w1 [8][16][3][3], b1 [8], w2 [3][8][3][3], b2 [3]; the backward takes dmask and writes du [16][h2][w2] and the
+// parameter gradients in one [mask_head_nparams()] row: dW1 | db1 | dW2 | db2.
+struct HeadArgs {
+    int H, W, h2, w2;
+    float sh, sw;          // (float) h2 / H, (float) w2 / W (torch's scale for a size-given resize)
+    const float *U, *k1, *b1, *k2, *b2;   // conv1 / conv2 weights and biases
+    float* mask;           // forward output
+    const float* dmask;    // backward input
+    float *dh, *dx, *du, *part;   // backward scratch (dh [8][H][W], dx [16][H][W], part [tiles][nparams]) and du
+    int tiles_x, tiles_y;
+};
+int mask_head_tiles(int H, int W);
+int mask_head_nparams();
+void launch_mask_head_fwd(HeadArgs a, hipStream_t st);
+void launch_mask_head_bwd(HeadArgs a, float* grads, hipStream_t st);
 }  // namespace gs

@@ -1,0 +1,388 @@
+// mask_head.hip -- the full-resolution head of the appearance embedding (geometry.mask; the reference module
+// conerf/model/gaussian_fields/masks.py:8-54: x = upsample(fusion(...)); x = F.interpolate(x, image_size, "bilinear");
+// mask = out_conv(x), out_conv = Conv2d(16, 8, 3, pad 1) -> ReLU -> Conv2d(8, 3, 3, pad 1)), forward and backward.
+//
+// Through torch this head is the embedding's cost at 1080p: a 16-channel 1920 x 1080 tensor (133 MB) written by the
+// resize, im2col GEMMs and col2im for the two convolutions, their weight gradients, and the resize's adjoint as
+// gathers -- about 3 ms of the 4.5 ms a masked 1080p iteration spends in the embedding (gpurun_out/r6a/mtrace).
+// Here the 16-channel image never exists:
+//   k_head_fwd    per 8 x 64 output tile: the bilinear samples of the stage-4 output on the tile + 2 halo into LDS,
+//                 conv1 + ReLU on the tile + 1 halo into LDS, conv2 -> the [3, H, W] mask;
+//   k_head_bwd_h  per tile: recompute the samples (tile + 1 halo) and h on the tile; dL/dh = [h > 0] conv2^T(dmask)
+//                 (dmask on the tile + 1 halo) -> dh [8, H, W]; the tile's partial dW2, db2 (fixed-order sums);
+//   k_head_bwd_x  per tile: the samples (tile + 1 halo) and dh (tile + 1 halo) -> the tile's partial dW1, db1 and
+//                 dL/dsample = conv1^T(dh) on the tile -> dx [16, H, W];
+//   k_head_bwd_u  per stage-4 pixel: the resize's adjoint as a gather over the samples that read it, in a fixed order;
+//   k_head_reduce one wave per weight: the tiles' partials summed lane-strided, then across the wave.
+// No atomics: bitwise repeatable for a given shape (the ADMM ranks and the sequential baseline rely on it).
+// Weights are wave-uniform: the compiler keeps them in SGPRs (scalar loads), the per-position data in LDS.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mask_conv.h"
+
+namespace gs {
+namespace {
+
+constexpr int HC = 16, HM = 8, HO = 3;        // sample channels, hidden channels, mask channels
+constexpr int TH = 8, TW = 64;                 // output tile
+constexpr int HT = 256;                        // threads per block
+constexpr int NW1 = HM * HC * 9, NW2 = HO * HM * 9;
+constexpr int P_W1 = 0, P_B1 = NW1, P_W2 = NW1 + HM, P_B2 = NW1 + HM + NW2;
+constexpr int NPART = NW1 + HM + NW2 + HO;     // 1379 partial sums per tile
+
+// bilinear taps of destination index d (torch's upsample_bilinear2d, align_corners = False, no scale factor):
+// src = max(0, scale (d + 0.5) - 0.5), i0 = (int) src, i1 = i0 + (i0 < n - 1), l1 = src - i0, l0 = 1 - l1
+__device__ __forceinline__ void taps(int d, int n, float scale, int& i0, int& i1, float& l0, float& l1) {
+    float src = fmaf(scale, (float)d + 0.5f, -0.5f);
+    src = src < 0.0f ? 0.0f : src;
+    i0 = (int)src;
+    i1 = i0 + (i0 < n - 1 ? 1 : 0);
+    l1 = src - (float)i0;
+    l0 = 1.0f - l1;
+}
+
+// samples of rows [ry0, ry0 + RR) x cols [rx0, rx0 + RC) of the resized image into xs[HC][RR][RC] (0 outside it)
+template <int RR, int RC>
+__device__ __forceinline__ void stage_samples(const HeadArgs& a, int ry0, int rx0, float* xs) {
+    const size_t hw2 = (size_t)a.h2 * a.w2;
+    for (int i = threadIdx.x; i < RR * RC; i += HT) {
+        const int r = i / RC, c = i % RC, y = ry0 + r, x = rx0 + c;
+        if (y < 0 || y >= a.H || x < 0 || x >= a.W) {
+#pragma unroll
+            for (int ch = 0; ch < HC; ch++) xs[(ch * RR + r) * RC + c] = 0.0f;
+            continue;
+        }
+        int iy0, iy1, ix0, ix1;
+        float ly0, ly1, lx0, lx1;
+        taps(y, a.h2, a.sh, iy0, iy1, ly0, ly1);
+        taps(x, a.w2, a.sw, ix0, ix1, lx0, lx1);
+        const size_t o00 = (size_t)iy0 * a.w2 + ix0, o01 = (size_t)iy0 * a.w2 + ix1;
+        const size_t o10 = (size_t)iy1 * a.w2 + ix0, o11 = (size_t)iy1 * a.w2 + ix1;
+#pragma unroll 4
+        for (int ch = 0; ch < HC; ch++) {
+            const float* u = a.U + ch * hw2;
+            xs[(ch * RR + r) * RC + c] = ly0 * (lx0 * u[o00] + lx1 * u[o01]) + ly1 * (lx0 * u[o10] + lx1 * u[o11]);
+        }
+    }
+}
+
+// conv1 + ReLU at position (r, c) of a region whose samples xs[HC][XR][XC] start one row and column earlier
+template <int XR, int XC>
+__device__ __forceinline__ void conv1_at(const HeadArgs& a, const float* xs, int r, int c, float (&h)[HM]) {
+#pragma unroll
+    for (int co = 0; co < HM; co++) h[co] = a.b1[co];
+    for (int ci = 0; ci < HC; ci++) {
+#pragma unroll
+        for (int ky = 0; ky < 3; ky++) {
+            const float* row = xs + (ci * XR + r + ky) * XC + c;
+            const float x0 = row[0], x1 = row[1], x2 = row[2];
+#pragma unroll
+            for (int co = 0; co < HM; co++) {
+                const float* w = a.k1 + ((co * HC + ci) * 3 + ky) * 3;
+                h[co] = fmaf(w[0], x0, h[co]);
+                h[co] = fmaf(w[1], x1, h[co]);
+                h[co] = fmaf(w[2], x2, h[co]);
+            }
+        }
+    }
+#pragma unroll
+    for (int co = 0; co < HM; co++) h[co] = h[co] > 0.0f ? h[co] : 0.0f;
+}
+
+// sliding-window weight-gradient sums over TH rows x TW columns: acc[ky][kx] = sum_(r, c) g[r][c] in[r + ky][c + kx]
+// (rows r of the group: grp, grp + G, ...), bacc = sum g
+__device__ __forceinline__ void window_sums(const float* in, int in_stride, const float* g, int g_stride, int grp,
+                                            int G, float (&acc)[9], float& bacc) {
+#pragma unroll
+    for (int k = 0; k < 9; k++) acc[k] = 0.0f;
+    bacc = 0.0f;
+    for (int r = grp; r < TH; r += G) {
+        const float* x0r = in + r * in_stride;
+        float w00 = x0r[0], w01 = x0r[1];
+        float w10 = x0r[in_stride], w11 = x0r[in_stride + 1];
+        float w20 = x0r[2 * in_stride], w21 = x0r[2 * in_stride + 1];
+        const float* gr = g + r * g_stride;
+#pragma unroll 4
+        for (int c = 0; c < TW; c++) {
+            const float w02 = x0r[c + 2], w12 = x0r[in_stride + c + 2], w22 = x0r[2 * in_stride + c + 2];
+            const float gv = gr[c];
+            acc[0] = fmaf(gv, w00, acc[0]); acc[1] = fmaf(gv, w01, acc[1]); acc[2] = fmaf(gv, w02, acc[2]);
+            acc[3] = fmaf(gv, w10, acc[3]); acc[4] = fmaf(gv, w11, acc[4]); acc[5] = fmaf(gv, w12, acc[5]);
+            acc[6] = fmaf(gv, w20, acc[6]); acc[7] = fmaf(gv, w21, acc[7]); acc[8] = fmaf(gv, w22, acc[8]);
+            bacc += gv;
+            w00 = w01; w01 = w02; w10 = w11; w11 = w12; w20 = w21; w21 = w22;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(HT) k_head_fwd(HeadArgs a) {
+    constexpr int XR = TH + 4, XC = TW + 4, QR = TH + 2, QC = TW + 2;
+    __shared__ float xs[HC * XR * XC];   // samples, tile + 2 halo
+    __shared__ float hs[HM * QR * QC];   // hidden, tile + 1 halo (0 outside the image: conv2's padding)
+    const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
+    const int y0 = ty * TH, x0 = tx * TW;
+    stage_samples<XR, XC>(a, y0 - 2, x0 - 2, xs);
+    __syncthreads();
+    for (int i = threadIdx.x; i < QR * QC; i += HT) {
+        const int r = i / QC, c = i % QC, y = y0 - 1 + r, x = x0 - 1 + c;
+        float h[HM];
+        if (y >= 0 && y < a.H && x >= 0 && x < a.W) {
+            conv1_at<XR, XC>(a, xs, r, c, h);
+        } else {
+#pragma unroll
+            for (int co = 0; co < HM; co++) h[co] = 0.0f;
+        }
+#pragma unroll
+        for (int co = 0; co < HM; co++) hs[(co * QR + r) * QC + c] = h[co];
+    }
+    __syncthreads();
+    const size_t HW = (size_t)a.H * a.W;
+    for (int i = threadIdx.x; i < TH * TW; i += HT) {
+        const int r = i / TW, c = i % TW, y = y0 + r, x = x0 + c;
+        if (y >= a.H || x >= a.W) continue;
+        float m[HO];
+#pragma unroll
+        for (int o = 0; o < HO; o++) m[o] = a.b2[o];
+        for (int co = 0; co < HM; co++) {
+#pragma unroll
+            for (int ky = 0; ky < 3; ky++) {
+                const float* row = hs + (co * QR + r + ky) * QC + c;
+                const float v0 = row[0], v1 = row[1], v2 = row[2];
+#pragma unroll
+                for (int o = 0; o < HO; o++) {
+                    const float* w = a.k2 + ((o * HM + co) * 3 + ky) * 3;
+                    m[o] = fmaf(w[0], v0, m[o]);
+                    m[o] = fmaf(w[1], v1, m[o]);
+                    m[o] = fmaf(w[2], v2, m[o]);
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < HO; o++) a.mask[o * HW + (size_t)y * a.W + x] = m[o];
+    }
+}
+
+__global__ void __launch_bounds__(HT) k_head_bwd_h(HeadArgs a) {
+    constexpr int XR = TH + 2, XC = TW + 2;
+    __shared__ float xs[HC * XR * XC];   // samples, tile + 1 halo
+    __shared__ float ms[HO * XR * XC];   // dmask, tile + 1 halo (0 outside the image)
+    __shared__ float hs[HM * TH * TW];   // hidden on the tile (0 outside the image)
+    __shared__ float red[10 * 24 * 10];  // row-group sums of the dW2 pairs
+    const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
+    const int y0 = ty * TH, x0 = tx * TW;
+    const size_t HW = (size_t)a.H * a.W;
+    stage_samples<XR, XC>(a, y0 - 1, x0 - 1, xs);
+    for (int i = threadIdx.x; i < XR * XC; i += HT) {
+        const int r = i / XC, c = i % XC, y = y0 - 1 + r, x = x0 - 1 + c;
+        const bool in = y >= 0 && y < a.H && x >= 0 && x < a.W;
+#pragma unroll
+        for (int o = 0; o < HO; o++) ms[(o * XR + r) * XC + c] = in ? a.dmask[o * HW + (size_t)y * a.W + x] : 0.0f;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < TH * TW; i += HT) {
+        const int r = i / TW, c = i % TW, y = y0 + r, x = x0 + c;
+        float h[HM];
+        const bool in = y < a.H && x < a.W;
+        if (in) {
+            conv1_at<XR, XC>(a, xs, r, c, h);
+        } else {
+#pragma unroll
+            for (int co = 0; co < HM; co++) h[co] = 0.0f;
+        }
+#pragma unroll
+        for (int co = 0; co < HM; co++) hs[(co * TH + r) * TW + c] = h[co];
+        if (!in) continue;
+        // dL/dh = [h > 0] conv2^T(dmask): dh[co][q] = sum_(o, ky, kx) w2[o][co][ky][kx] dmask[o][q - (ky, kx) + 1]
+        float d[HM];
+#pragma unroll
+        for (int co = 0; co < HM; co++) d[co] = 0.0f;
+        for (int o = 0; o < HO; o++) {
+#pragma unroll
+            for (int ky = 0; ky < 3; ky++) {
+                const float* row = ms + (o * XR + r + 2 - ky) * XC + c + 2;
+                const float m0 = row[0], m1 = row[-1], m2 = row[-2];   // kx = 0, 1, 2
+#pragma unroll
+                for (int co = 0; co < HM; co++) {
+                    const float* w = a.k2 + ((o * HM + co) * 3 + ky) * 3;
+                    d[co] = fmaf(w[0], m0, d[co]);
+                    d[co] = fmaf(w[1], m1, d[co]);
+                    d[co] = fmaf(w[2], m2, d[co]);
+                }
+            }
+        }
+#pragma unroll
+        for (int co = 0; co < HM; co++) a.dh[co * HW + (size_t)y * a.W + x] = h[co] > 0.0f ? d[co] : 0.0f;
+    }
+    __syncthreads();
+    // dW2[o][co][ky][kx] = sum_q h[co][q] dmask[o][q - (ky, kx) + 1]: the window sums of dmask (tile + 1 halo) against
+    // h, with the kernel flipped (window offset k' = 2 - k); db2[o] = sum over the tile's pixels of dmask[o]
+    constexpr int NP = HO * HM, G = HT / NP;    // 24 pairs x 10 row groups
+    const int t = threadIdx.x, pr = t % NP, grp = t / NP;
+    float* prow = a.part + (size_t)blockIdx.x * NPART;
+    if (grp < G) {
+        const int o = pr / HM, co = pr % HM;
+        float acc[9], bacc;
+        window_sums(ms + o * XR * XC, XC, hs + co * TH * TW, TW, grp, G, acc, bacc);
+#pragma unroll
+        for (int k = 0; k < 9; k++) red[(grp * NP + pr) * 10 + k] = acc[k];
+    }
+    __syncthreads();
+    for (int i = t; i < NP * 9; i += HT) {
+        const int p = i / 9, k = i % 9, o = p / HM, co = p % HM;
+        float v = red[p * 10 + k];
+        for (int gg = 1; gg < G; gg++) v += red[(gg * NP + p) * 10 + k];
+        prow[P_W2 + (o * HM + co) * 9 + (8 - k)] = v;     // flipped kernel
+    }
+    if (t < HO) {   // db2: the tile's pixels, rows then columns
+        float v = 0.0f;
+        for (int r = 0; r < TH; r++)
+            for (int c = 0; c < TW; c++) v += ms[(t * XR + r + 1) * XC + c + 1];
+        prow[P_B2 + t] = v;
+    }
+}
+
+__global__ void __launch_bounds__(HT) k_head_bwd_x(HeadArgs a) {
+    constexpr int XR = TH + 2, XC = TW + 2;
+    __shared__ float xs[HC * XR * XC];   // samples, tile + 1 halo
+    __shared__ float ds[HM * XR * XC];   // dh, tile + 1 halo (0 outside the image)
+    const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
+    const int y0 = ty * TH, x0 = tx * TW;
+    const size_t HW = (size_t)a.H * a.W;
+    stage_samples<XR, XC>(a, y0 - 1, x0 - 1, xs);
+    for (int i = threadIdx.x; i < XR * XC; i += HT) {
+        const int r = i / XC, c = i % XC, y = y0 - 1 + r, x = x0 - 1 + c;
+        const bool in = y >= 0 && y < a.H && x >= 0 && x < a.W;
+#pragma unroll
+        for (int co = 0; co < HM; co++) ds[(co * XR + r) * XC + c] = in ? a.dh[co * HW + (size_t)y * a.W + x] : 0.0f;
+    }
+    __syncthreads();
+    // dL/dsample = conv1^T(dh): dx[ci][p] = sum_(co, ky, kx) w1[co][ci][ky][kx] dh[co][p - (ky, kx) + 1]
+    for (int i = threadIdx.x; i < TH * TW; i += HT) {
+        const int r = i / TW, c = i % TW, y = y0 + r, x = x0 + c;
+        if (y >= a.H || x >= a.W) continue;
+        float d[HC];
+#pragma unroll
+        for (int ci = 0; ci < HC; ci++) d[ci] = 0.0f;
+        for (int co = 0; co < HM; co++) {
+#pragma unroll
+            for (int ky = 0; ky < 3; ky++) {
+                const float* row = ds + (co * XR + r + 2 - ky) * XC + c + 2;
+                const float g0 = row[0], g1 = row[-1], g2 = row[-2];   // kx = 0, 1, 2
+#pragma unroll
+                for (int ci = 0; ci < HC; ci++) {
+                    const float* w = a.k1 + ((co * HC + ci) * 3 + ky) * 3;
+                    d[ci] = fmaf(w[0], g0, d[ci]);
+                    d[ci] = fmaf(w[1], g1, d[ci]);
+                    d[ci] = fmaf(w[2], g2, d[ci]);
+                }
+            }
+        }
+#pragma unroll
+        for (int ci = 0; ci < HC; ci++) a.dx[ci * HW + (size_t)y * a.W + x] = d[ci];
+    }
+    // dW1[co][ci][ky][kx] = sum over the tile of dh[co][q] sample[ci][q + (ky, kx) - 1]; db1[co] = sum dh[co]
+    // (128 pairs x 2 row groups; the groups' sums in order through LDS, reusing xs once every thread is past it)
+    constexpr int NP = HM * HC, G = HT / NP;
+    const int t = threadIdx.x, pr = t % NP, grp = t / NP;
+    const int co = pr / HC, ci = pr % HC;
+    float acc[9], bacc;
+    window_sums(xs + ci * XR * XC, XC, ds + co * XR * XC + XC + 1, XC, grp, G, acc, bacc);
+    __syncthreads();
+    float* red = xs;
+#pragma unroll
+    for (int k = 0; k < 9; k++) red[(grp * NP + pr) * 10 + k] = acc[k];
+    red[(grp * NP + pr) * 10 + 9] = bacc;
+    __syncthreads();
+    float* prow = a.part + (size_t)blockIdx.x * NPART;
+    for (int i = t; i < NP * 10; i += HT) {
+        const int p = i / 10, k = i % 10;
+        float v = red[p * 10 + k];
+        for (int gg = 1; gg < G; gg++) v += red[(gg * NP + p) * 10 + k];
+        const int pco = p / HC, pci = p % HC;
+        if (k < 9) prow[P_W1 + (pco * HC + pci) * 9 + k] = v;
+        else if (pci == 0) prow[P_B1 + pco] = v;
+    }
+}
+
+// the samples (along one axis) that read source index u: candidates around u / scale, each tested with taps(); returns
+// the count, writing (destination, weight) pairs in ascending destination order (both taps of a clamped edge sample)
+__device__ __forceinline__ int rev_taps(int u, int n_src, int n_dst, float scale, int (&dst)[12], float (&wt)[12]) {
+    const float inv = (float)n_dst / (float)n_src;
+    int lo = (int)floorf(((float)u - 1.0f) * inv) - 2, hi = (int)ceilf(((float)u + 2.0f) * inv) + 2;
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > n_dst - 1 ? n_dst - 1 : hi;
+    int k = 0;
+    for (int d = lo; d <= hi && k < 12; d++) {
+        int i0, i1;
+        float l0, l1;
+        taps(d, n_src, scale, i0, i1, l0, l1);
+        if (i0 == u && i1 == u) { dst[k] = d; wt[k] = l0 + l1; k++; }
+        else if (i0 == u) { dst[k] = d; wt[k] = l0; k++; }
+        else if (i1 == u) { dst[k] = d; wt[k] = l1; k++; }
+    }
+    return k;
+}
+
+// the resize's adjoint: du[ci][uy][ux] = sum over samples (y, x) reading (uy, ux) of wy wx dx[ci][y][x]
+__global__ void __launch_bounds__(256) k_head_bwd_u(HeadArgs a) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (int64_t)a.h2 * a.w2) return;
+    const int uy = (int)(idx / a.w2), ux = (int)(idx % a.w2);
+    int dy[12], dx[12];
+    float wy[12], wx[12];
+    const int ny = rev_taps(uy, a.h2, a.H, a.sh, dy, wy);
+    const int nx = rev_taps(ux, a.w2, a.W, a.sw, dx, wx);
+    const size_t HW = (size_t)a.H * a.W, hw2 = (size_t)a.h2 * a.w2;
+    float acc[HC];
+#pragma unroll
+    for (int ci = 0; ci < HC; ci++) acc[ci] = 0.0f;
+    for (int i = 0; i < ny; i++) {
+        float rs[HC];
+#pragma unroll
+        for (int ci = 0; ci < HC; ci++) rs[ci] = 0.0f;
+        for (int j = 0; j < nx; j++) {
+            const size_t o = (size_t)dy[i] * a.W + dx[j];
+#pragma unroll
+            for (int ci = 0; ci < HC; ci++) rs[ci] = fmaf(wx[j], a.dx[ci * HW + o], rs[ci]);
+        }
+#pragma unroll
+        for (int ci = 0; ci < HC; ci++) acc[ci] = fmaf(wy[i], rs[ci], acc[ci]);
+    }
+#pragma unroll
+    for (int ci = 0; ci < HC; ci++) a.du[ci * hw2 + idx] = acc[ci];
+}
+
+__global__ void __launch_bounds__(256) k_head_reduce(int nblk, const float* __restrict__ part, float* __restrict__ out) {
+    const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (wv >= NPART) return;
+    float v = 0.0f;
+    for (int b = lane; b < nblk; b += 64) v += part[(size_t)b * NPART + wv];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) out[wv] = v;
+}
+
+}  // namespace
+
+int mask_head_tiles(int H, int W) { return ((W + TW - 1) / TW) * ((H + TH - 1) / TH); }
+int mask_head_nparams() { return NPART; }
+
+void launch_mask_head_fwd(HeadArgs a, hipStream_t st) {
+    a.tiles_x = (a.W + TW - 1) / TW;
+    a.tiles_y = (a.H + TH - 1) / TH;
+    k_head_fwd<<<a.tiles_x * a.tiles_y, HT, 0, st>>>(a);
+}
+
+void launch_mask_head_bwd(HeadArgs a, float* grads, hipStream_t st) {
+    a.tiles_x = (a.W + TW - 1) / TW;
+    a.tiles_y = (a.H + TH - 1) / TH;
+    const int nb = a.tiles_x * a.tiles_y;
+    k_head_bwd_h<<<nb, HT, 0, st>>>(a);
+    k_head_bwd_x<<<nb, HT, 0, st>>>(a);
+    const int64_t nu = (int64_t)a.h2 * a.w2;
+    k_head_bwd_u<<<(unsigned)((nu + 255) / 256), 256, 0, st>>>(a);
+    k_head_reduce<<<(NPART + 3) / 4, 256, 0, st>>>(nb, a.part, grads);
+}
+
+}  // namespace gs

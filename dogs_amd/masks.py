@@ -123,8 +123,57 @@ class AppearanceEmbedding(nn.Module):
         code = self.appearance_embedding[index]
         x = torch.cat([image, code[:, None, None].expand(code.shape[0], h, w)], dim=0)
         x = self.upsample(self.fusion(x))
-        x = resize_bilinear(x, tuple(image_size))
+        H, W = int(image_size[0]), int(image_size[1])
+        if x.is_cuda and x.dim() == 3 and H <= 4 * x.shape[1] and W <= 4 * x.shape[2]:
+            c1, c2 = self.out_conv[0], self.out_conv[2]
+            return _MaskHead.apply(x, c1.weight, c1.bias, c2.weight, c2.bias, (H, W))
+        x = resize_bilinear(x, (H, W))
         return self.out_conv(x)
+
+
+class _MaskHead(torch.autograd.Function):
+    """The full-resolution head resize -> out_conv (Conv2d 16 -> 8, ReLU, Conv2d 8 -> 3) as dg_mask_head_forward /
+    dg_mask_head_backward (mask_head.hip): the 16-channel full-size image is never materialised, and the backward's
+    sums run in a fixed order (deterministic, no atomics).  The same function as the torch modules (fp32 rounding
+    differs: tests/test_gpu_mask_conv.py)."""
+
+    @staticmethod
+    def forward(ctx, u, w1, b1, w2, b2, size):
+        from . import _lib
+        H, W = size
+        uc = u.detach().contiguous()
+        ps = [t.detach().contiguous() for t in (w1, b1, w2, b2)]
+        mask = torch.empty((3, H, W), dtype=torch.float32, device=u.device)
+        with _lib.device_ctx(u.device):
+            _lib.check(_lib.load().dg_mask_head_forward(H, W, int(uc.shape[1]), int(uc.shape[2]), uc.data_ptr(),
+                                                        *[p.data_ptr() for p in ps], mask.data_ptr(),
+                                                        _lib.stream_of(u.device)))
+        ctx.save_for_backward(uc, *ps)
+        ctx.size = (H, W)
+        return mask
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import _lib
+        uc, w1, b1, w2, b2 = ctx.saved_tensors
+        H, W = ctx.size
+        L = _lib.load()
+        gc = g.contiguous()
+        du = torch.empty_like(uc)
+        npar = int(L.dg_mask_head_nparams())
+        dp = torch.empty(npar, dtype=torch.float32, device=uc.device)
+        nbytes = int(L.dg_mask_head_scratch_bytes(H, W))
+        scratch = torch.empty(nbytes, dtype=torch.uint8, device=uc.device)
+        with _lib.device_ctx(uc.device):
+            _lib.check(L.dg_mask_head_backward(H, W, int(uc.shape[1]), int(uc.shape[2]), uc.data_ptr(),
+                                               w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
+                                               gc.data_ptr(), du.data_ptr(), dp.data_ptr(), scratch.data_ptr(),
+                                               nbytes, _lib.stream_of(uc.device)))
+        n1, n2 = w1.numel(), w2.numel()
+        dw1, db1 = dp[:n1].view_as(w1), dp[n1:n1 + b1.numel()]
+        o = n1 + b1.numel()
+        dw2, db2 = dp[o:o + n2].view_as(w2), dp[o + n2:o + n2 + b2.numel()]
+        return du, dw1, db1, dw2, db2, None
 
 
 def _bilinear_taps(n_in: int, n_out: int, device) -> tuple:

@@ -114,8 +114,7 @@ def test_masked_training_native_matches_autograd(hip_device):
 def test_first_step_native_equals_autograd(hip_device, case):
     """ONE iteration through each route from the same state, SH degree 3 (so f_rest carries gradient): the first Adam
     moment is 0.1 x the raw-parameter gradient and the second 0.001 x its square, so they compare the two routes'
-    gradients directly, f_rest included: bit for bit in every row for the plain, anti-aliasing and zero-scaling cases
-    (tools/first_step_probe.py), at 1e-5 relative with the appearance mask (see below).  Cases: plain; the appearance mask + lambda_mask 0.5 + depth_threshold
+    gradients directly, f_rest included: bit for bit in every row, in every case (tools/first_step_probe.py).  Cases: plain; the appearance mask + lambda_mask 0.5 + depth_threshold
     (urban3d_admm.yaml); texture.anti_aliasing
     (the native step's antialiasing flag); one Gaussian's scaling underflowed to exactly 0, where torch's prod backward
     switches EVERY row to its zero-safe form (the native step reads the activation pass's zero stamp)."""
@@ -152,30 +151,16 @@ def test_first_step_native_equals_autograd(hip_device, case):
             assert float(torch.exp(m._scaling.detach()).min()) == 0.0
         out.append(_state(tr))
     s0, s1 = out
-    if case != "mask-depth":
-        # the same kernels and activations with torch's association on both routes: every group's two
-        # Adam moments and the statistics are bit-identical, every row -- the degenerate Gaussian 7 included
-        for k in s0[1]:
-            assert float(s1[1][k][0].norm()) > 0, k
-            for j in (0, 1):
-                d = (s0[1][k][j] - s1[1][k][j]).abs().max()
-                assert torch.equal(s0[1][k][j], s1[1][k][j]), (k, j, float(d))
-        for a, b in zip(s0[2], s1[2]):
-            assert torch.equal(a, b)
-    else:
-        # the mask's route differs: the autograd route forms dL/dmask through torch's expression (F.l1_loss of
-        # colors * mask, the mask regulariser's mean) where the native step's fused SSIM backward writes it, and the
-        # embedding's MIOpen backward then sees those values -- the raster gradients agree to rounding only
-        diffs = {}
-        for k in s0[1]:
-            m0, m1 = s0[1][k][0], s1[1][k][0]
-            assert float(m1.norm()) > 0, k
-            diffs[k] = _rel(m0, m1)
-            assert diffs[k] < 1e-5, (k, diffs[k])
-            assert _rel(s0[1][k][1], s1[1][k][1]) < 2e-5, k
-        for a, b in zip(s0[2], s1[2]):
-            assert _rel(a, b) < 1e-5
-        print("mask-depth first-step relative differences", diffs)
+    # the same kernels and activations with torch's association on both routes, and the masked L1's
+    # dL/dmask and dL/dcolour formed as torch's autograd forms them: every group's two Adam moments and the statistics
+    # are bit-identical, every row -- the degenerate Gaussian 7 included
+    for k in s0[1]:
+        assert float(s1[1][k][0].norm()) > 0, k
+        for j in (0, 1):
+            d = (s0[1][k][j] - s1[1][k][j]).abs().max()
+            assert torch.equal(s0[1][k][j], s1[1][k][j]), (k, j, float(d))
+    for a, b in zip(s0[2], s1[2]):
+        assert torch.equal(a, b)
     if case == "zero-scaling":   # finite, and the zero axis gets exactly no scaling gradient on either route
         for st in (s0, s1):
             assert all(bool(torch.isfinite(v[0][7]).all()) for v in st[1].values())
