@@ -1190,7 +1190,7 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
         if (!unfused && k >= 3) {
             d.gmode = k - 2;  // opacity: sigmoid, scaling: exp + regulariser, quaternion: normalize
             d.act = k == 3 ? act_o : (k == 4 ? act_s : nullptr);
-            d.reg = k == 4 ? a->lambda_scale / (float)P : 0.0f;
+            d.reg = k == 4 ? a->lambda_scale * (1.0f / (float)P) : 0.0f;   // torch's mean backward: x (1 / N)
             if (k == 4) { d.zero_stamp = zstamp; d.stamp = stamp; }
         }
     }
@@ -1210,8 +1210,9 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
         gs::launch_ssim_fwd_fused(H, W, C1, C2, color, a->gt, a->image, dmu1, ds1, ds12, part, s, a->mask);
         const gs::LossFinal lf = {part, part + nw_ssim, p_sc_fused, nw_ssim, nw_ssim, nb_act, (uint32_t)n_img,
                                   (uint32_t)P, a->loss, a->mask ? part + 2 * nw_ssim : nullptr, nw_ssim};
-        // d/dmask of lambda_mask mean((mask - 1)^2): lambda_mask (2 / n) (mask - 1)
-        const float mreg = (float)((double)a->lambda_mask * 2.0 / (double)n_img);
+        // d/dmask of lambda_mask mean((mask - 1)^2): (lambda_mask (1 / n)) (2 (mask - 1)), as torch's mean backward
+        // (a multiply by the float reciprocal) and pow's backward form it; the factor 2 is exact
+        const float mreg = 2.0f * (a->lambda_mask * (1.0f / (float)n_img));
         gs::launch_ssim_bwd_fused(H, W, a->image, a->gt, color, (-ld) / (float)n_img, g_l1 / (float)n_img, dmu1, ds1,
                                   ds12, dimg, s, a->loss ? &lf : nullptr, a->mask, a->dmask, mreg);
     } else {
@@ -1232,7 +1233,7 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
         return 1;
     if (unfused)
         gs::launch_activate_bwd((uint32_t)P, act_o, act_s, G[5].param, dopac, dscales, drot, g_o, g_s, g_q, s,
-                                a->lambda_scale / (float)P, zstamp, stamp);
+                                a->lambda_scale * (1.0f / (float)P), zstamp, stamp);
 #ifndef DG_DIAG_NO_ADAM  // timing diagnostic only (no parameter update): what the update costs the next step's forward
     if (a->sh_status) {
         // xyz / opacity / scaling / rotation + statistics + the rows' status snapshot here (the next forward's

@@ -67,27 +67,54 @@ __device__ __forceinline__ void stage_samples(const HeadArgs& a, int ry0, int rx
     }
 }
 
-// conv1 + ReLU at position (r, c) of a region whose samples xs[HC][XR][XC] start one row and column earlier
+// The weights, staged once per block in LDS as float4 rows {w[..][0], w[..][1], w[..][2], 0} of one (kernel row,
+// input, output) triple, in the order each product reads them (every lane reads the same row: a broadcast
+// ds_read_b128).  Read from global memory per use, they were scalar loads whose latency the block's two waves per
+// SIMD could not hide.
+//   w1f[(ci 3 + ky) 8 + co]   conv1,        w1t[(co 3 + ky) 16 + ci]  conv1^T (the input gradient)
+//   w2t[(o 3 + ky) 8 + co]    conv2^T (the forward's conv2 reads its 216 weights as scalar loads)
+constexpr int NF1 = HC * 3 * HM, NF2 = HM * 3 * HO;   // float4 rows per weight tensor
+
+__device__ __forceinline__ float4 wrow(const float* w) { return make_float4(w[0], w[1], w[2], 0.0f); }
+
+template <bool CONV1, bool CONV1T, bool CONV2T>
+__device__ __forceinline__ void stage_weights(const HeadArgs& a, float4* w1f, float4* w1t, float4* w2t) {
+    for (int i = threadIdx.x; i < NF1; i += HT) {
+        if (CONV1) { const int co = i % HM, ky = (i / HM) % 3, ci = i / (3 * HM); w1f[i] = wrow(a.k1 + ((co * HC + ci) * 3 + ky) * 3); }
+        if (CONV1T) { const int ci = i % HC, ky = (i / HC) % 3, co = i / (3 * HC); w1t[i] = wrow(a.k1 + ((co * HC + ci) * 3 + ky) * 3); }
+    }
+    for (int i = threadIdx.x; i < NF2; i += HT) {
+        if (CONV2T) { const int co = i % HM, ky = (i / HM) % 3, o = i / (3 * HM); w2t[i] = wrow(a.k2 + ((o * HM + co) * 3 + ky) * 3); }
+    }
+}
+
+// conv1 + ReLU at the two positions (r, c), (r, c + 1) of a region whose samples xs[HC][XR][XC] start one row and
+// column earlier.  Each output sums its 144 products in the same order whichever pair it is computed in, so the
+// forward and the backward's recomputation give the same bits.
 template <int XR, int XC>
-__device__ __forceinline__ void conv1_at(const HeadArgs& a, const float* xs, int r, int c, float (&h)[HM]) {
+__device__ __forceinline__ void conv1_pair(const float* b1, const float4* w1f, const float* xs, int r, int c,
+                                           float (&h0)[HM], float (&h1)[HM]) {
 #pragma unroll
-    for (int co = 0; co < HM; co++) h[co] = a.b1[co];
+    for (int co = 0; co < HM; co++) h0[co] = h1[co] = b1[co];
+#pragma unroll 1
     for (int ci = 0; ci < HC; ci++) {
 #pragma unroll
         for (int ky = 0; ky < 3; ky++) {
             const float* row = xs + (ci * XR + r + ky) * XC + c;
-            const float x0 = row[0], x1 = row[1], x2 = row[2];
+            const float x0 = row[0], x1 = row[1], x2 = row[2], x3 = row[3];
 #pragma unroll
             for (int co = 0; co < HM; co++) {
-                const float* w = a.k1 + ((co * HC + ci) * 3 + ky) * 3;
-                h[co] = fmaf(w[0], x0, h[co]);
-                h[co] = fmaf(w[1], x1, h[co]);
-                h[co] = fmaf(w[2], x2, h[co]);
+                const float4 w = w1f[(ci * 3 + ky) * HM + co];
+                h0[co] = fmaf(w.x, x0, h0[co]); h0[co] = fmaf(w.y, x1, h0[co]); h0[co] = fmaf(w.z, x2, h0[co]);
+                h1[co] = fmaf(w.x, x1, h1[co]); h1[co] = fmaf(w.y, x2, h1[co]); h1[co] = fmaf(w.z, x3, h1[co]);
             }
         }
     }
 #pragma unroll
-    for (int co = 0; co < HM; co++) h[co] = h[co] > 0.0f ? h[co] : 0.0f;
+    for (int co = 0; co < HM; co++) {
+        h0[co] = h0[co] > 0.0f ? h0[co] : 0.0f;
+        h1[co] = h1[co] > 0.0f ? h1[co] : 0.0f;
+    }
 }
 
 // sliding-window weight-gradient sums over TH rows x TW columns: acc[ky][kx] = sum_(r, c) g[r][c] in[r + ky][c + kx]
@@ -116,62 +143,75 @@ __device__ __forceinline__ void window_sums(const float* in, int in_stride, cons
     }
 }
 
-__global__ void __launch_bounds__(HT) k_head_fwd(HeadArgs a) {
+__global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_fwd(HeadArgs a) {
     constexpr int XR = TH + 4, XC = TW + 4, QR = TH + 2, QC = TW + 2;
     __shared__ float xs[HC * XR * XC];   // samples, tile + 2 halo
     __shared__ float hs[HM * QR * QC];   // hidden, tile + 1 halo (0 outside the image: conv2's padding)
+    __shared__ float4 w1f[NF1];          // (conv2's 216 weights stay scalar loads: two blocks per CU fit 160 KB)
+    __shared__ float sb1[HM], sb2[HO];
     const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
     const int y0 = ty * TH, x0 = tx * TW;
+    stage_weights<true, false, false>(a, w1f, nullptr, nullptr);
+    if (threadIdx.x < HM) sb1[threadIdx.x] = a.b1[threadIdx.x];
+    if (threadIdx.x < HO) sb2[threadIdx.x] = a.b2[threadIdx.x];
     stage_samples<XR, XC>(a, y0 - 2, x0 - 2, xs);
     __syncthreads();
-    for (int i = threadIdx.x; i < QR * QC; i += HT) {
-        const int r = i / QC, c = i % QC, y = y0 - 1 + r, x = x0 - 1 + c;
-        float h[HM];
-        if (y >= 0 && y < a.H && x >= 0 && x < a.W) {
-            conv1_at<XR, XC>(a, xs, r, c, h);
-        } else {
+    for (int i = threadIdx.x; i < QR * (QC / 2); i += HT) {     // position pairs (r, c), (r, c + 1)
+        const int r = i / (QC / 2), c = 2 * (i % (QC / 2)), y = y0 - 1 + r, x = x0 - 1 + c;
+        float h0[HM], h1[HM];
+        conv1_pair<XR, XC>(sb1, w1f, xs, r, c, h0, h1);
+        const bool in0 = y >= 0 && y < a.H && x >= 0 && x < a.W, in1 = y >= 0 && y < a.H && x + 1 >= 0 && x + 1 < a.W;
 #pragma unroll
-            for (int co = 0; co < HM; co++) h[co] = 0.0f;
+        for (int co = 0; co < HM; co++) {
+            hs[(co * QR + r) * QC + c] = in0 ? h0[co] : 0.0f;
+            hs[(co * QR + r) * QC + c + 1] = in1 ? h1[co] : 0.0f;
         }
-#pragma unroll
-        for (int co = 0; co < HM; co++) hs[(co * QR + r) * QC + c] = h[co];
     }
     __syncthreads();
     const size_t HW = (size_t)a.H * a.W;
-    for (int i = threadIdx.x; i < TH * TW; i += HT) {
-        const int r = i / TW, c = i % TW, y = y0 + r, x = x0 + c;
+    for (int i = threadIdx.x; i < TH * (TW / 2); i += HT) {
+        const int r = i / (TW / 2), c = 2 * (i % (TW / 2)), y = y0 + r, x = x0 + c;
         if (y >= a.H || x >= a.W) continue;
-        float m[HO];
+        float m0[HO], m1[HO];
 #pragma unroll
-        for (int o = 0; o < HO; o++) m[o] = a.b2[o];
+        for (int o = 0; o < HO; o++) m0[o] = m1[o] = sb2[o];
+#pragma unroll 1
         for (int co = 0; co < HM; co++) {
 #pragma unroll
             for (int ky = 0; ky < 3; ky++) {
                 const float* row = hs + (co * QR + r + ky) * QC + c;
-                const float v0 = row[0], v1 = row[1], v2 = row[2];
+                const float v0 = row[0], v1 = row[1], v2 = row[2], v3 = row[3];
 #pragma unroll
                 for (int o = 0; o < HO; o++) {
-                    const float* w = a.k2 + ((o * HM + co) * 3 + ky) * 3;
-                    m[o] = fmaf(w[0], v0, m[o]);
-                    m[o] = fmaf(w[1], v1, m[o]);
-                    m[o] = fmaf(w[2], v2, m[o]);
+                    const float* wp = a.k2 + ((o * HM + co) * 3 + ky) * 3;
+                    const float4 w = make_float4(wp[0], wp[1], wp[2], 0.0f);
+                    m0[o] = fmaf(w.x, v0, m0[o]); m0[o] = fmaf(w.y, v1, m0[o]); m0[o] = fmaf(w.z, v2, m0[o]);
+                    m1[o] = fmaf(w.x, v1, m1[o]); m1[o] = fmaf(w.y, v2, m1[o]); m1[o] = fmaf(w.z, v3, m1[o]);
                 }
             }
         }
+        const size_t p = (size_t)y * a.W + x;
 #pragma unroll
-        for (int o = 0; o < HO; o++) a.mask[o * HW + (size_t)y * a.W + x] = m[o];
+        for (int o = 0; o < HO; o++) {
+            a.mask[o * HW + p] = m0[o];
+            if (x + 1 < a.W) a.mask[o * HW + p + 1] = m1[o];
+        }
     }
 }
 
-__global__ void __launch_bounds__(HT) k_head_bwd_h(HeadArgs a) {
+__global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_bwd_h(HeadArgs a) {
     constexpr int XR = TH + 2, XC = TW + 2;
-    __shared__ float xs[HC * XR * XC];   // samples, tile + 1 halo
+    constexpr int NP = HO * HM, G = HT / NP;    // dW2: 24 pairs x 10 row groups
+    __shared__ float xs[HC * XR * XC];   // samples, tile + 1 halo; then the dW2 row-group sums
     __shared__ float ms[HO * XR * XC];   // dmask, tile + 1 halo (0 outside the image)
     __shared__ float hs[HM * TH * TW];   // hidden on the tile (0 outside the image)
-    __shared__ float red[10 * 24 * 10];  // row-group sums of the dW2 pairs
+    __shared__ float4 w1f[NF1], w2t[NF2];
+    __shared__ float sb1[HM], colsum[HO * TW];
     const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
     const int y0 = ty * TH, x0 = tx * TW;
     const size_t HW = (size_t)a.H * a.W;
+    stage_weights<true, false, true>(a, w1f, nullptr, w2t);
+    if (threadIdx.x < HM) sb1[threadIdx.x] = a.b1[threadIdx.x];
     stage_samples<XR, XC>(a, y0 - 1, x0 - 1, xs);
     for (int i = threadIdx.x; i < XR * XC; i += HT) {
         const int r = i / XC, c = i % XC, y = y0 - 1 + r, x = x0 - 1 + c;
@@ -180,75 +220,89 @@ __global__ void __launch_bounds__(HT) k_head_bwd_h(HeadArgs a) {
         for (int o = 0; o < HO; o++) ms[(o * XR + r) * XC + c] = in ? a.dmask[o * HW + (size_t)y * a.W + x] : 0.0f;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < TH * TW; i += HT) {
-        const int r = i / TW, c = i % TW, y = y0 + r, x = x0 + c;
-        float h[HM];
-        const bool in = y < a.H && x < a.W;
-        if (in) {
-            conv1_at<XR, XC>(a, xs, r, c, h);
-        } else {
+    for (int i = threadIdx.x; i < TH * (TW / 2); i += HT) {     // owned position pairs
+        const int r = i / (TW / 2), c = 2 * (i % (TW / 2)), y = y0 + r, x = x0 + c;
+        float h0[HM], h1[HM];
+        conv1_pair<XR, XC>(sb1, w1f, xs, r, c, h0, h1);
+        const bool in0 = y < a.H && x < a.W, in1 = y < a.H && x + 1 < a.W;
 #pragma unroll
-            for (int co = 0; co < HM; co++) h[co] = 0.0f;
+        for (int co = 0; co < HM; co++) {
+            if (!in0) h0[co] = 0.0f;
+            if (!in1) h1[co] = 0.0f;
+            hs[(co * TH + r) * TW + c] = h0[co];
+            hs[(co * TH + r) * TW + c + 1] = h1[co];
         }
-#pragma unroll
-        for (int co = 0; co < HM; co++) hs[(co * TH + r) * TW + c] = h[co];
-        if (!in) continue;
+        if (!in0) continue;
         // dL/dh = [h > 0] conv2^T(dmask): dh[co][q] = sum_(o, ky, kx) w2[o][co][ky][kx] dmask[o][q - (ky, kx) + 1]
-        float d[HM];
+        float d0[HM], d1[HM];
 #pragma unroll
-        for (int co = 0; co < HM; co++) d[co] = 0.0f;
+        for (int co = 0; co < HM; co++) d0[co] = d1[co] = 0.0f;
+#pragma unroll 1
         for (int o = 0; o < HO; o++) {
 #pragma unroll
             for (int ky = 0; ky < 3; ky++) {
-                const float* row = ms + (o * XR + r + 2 - ky) * XC + c + 2;
-                const float m0 = row[0], m1 = row[-1], m2 = row[-2];   // kx = 0, 1, 2
+                const float* row = ms + (o * XR + r + 2 - ky) * XC + c;
+                const float m0 = row[0], m1 = row[1], m2 = row[2], m3 = row[3];
 #pragma unroll
                 for (int co = 0; co < HM; co++) {
-                    const float* w = a.k2 + ((o * HM + co) * 3 + ky) * 3;
-                    d[co] = fmaf(w[0], m0, d[co]);
-                    d[co] = fmaf(w[1], m1, d[co]);
-                    d[co] = fmaf(w[2], m2, d[co]);
+                    const float4 w = w2t[(o * 3 + ky) * HM + co];   // kx = 0, 1, 2 read columns c + 2, c + 1, c
+                    d0[co] = fmaf(w.x, m2, d0[co]); d0[co] = fmaf(w.y, m1, d0[co]); d0[co] = fmaf(w.z, m0, d0[co]);
+                    d1[co] = fmaf(w.x, m3, d1[co]); d1[co] = fmaf(w.y, m2, d1[co]); d1[co] = fmaf(w.z, m1, d1[co]);
                 }
             }
         }
+        const size_t p = (size_t)y * a.W + x;
 #pragma unroll
-        for (int co = 0; co < HM; co++) a.dh[co * HW + (size_t)y * a.W + x] = h[co] > 0.0f ? d[co] : 0.0f;
+        for (int co = 0; co < HM; co++) {
+            a.dh[co * HW + p] = h0[co] > 0.0f ? d0[co] : 0.0f;
+            if (in1) a.dh[co * HW + p + 1] = h1[co] > 0.0f ? d1[co] : 0.0f;
+        }
     }
     __syncthreads();
     // dW2[o][co][ky][kx] = sum_q h[co][q] dmask[o][q - (ky, kx) + 1]: the window sums of dmask (tile + 1 halo) against
-    // h, with the kernel flipped (window offset k' = 2 - k); db2[o] = sum over the tile's pixels of dmask[o]
-    constexpr int NP = HO * HM, G = HT / NP;    // 24 pairs x 10 row groups
+    // h, with the kernel flipped (window offset k' = 2 - k); db2[o] = sum over the tile's pixels of dmask[o], per
+    // column over the rows, then over the columns
     const int t = threadIdx.x, pr = t % NP, grp = t / NP;
-    float* prow = a.part + (size_t)blockIdx.x * NPART;
+    float acc[9], bacc;
     if (grp < G) {
         const int o = pr / HM, co = pr % HM;
-        float acc[9], bacc;
         window_sums(ms + o * XR * XC, XC, hs + co * TH * TW, TW, grp, G, acc, bacc);
+    }
+    if (t < HO * TW) {
+        const int o = t / TW, c = t % TW;
+        float v = 0.0f;
+        for (int r = 0; r < TH; r++) v += ms[(o * XR + r + 1) * XC + c + 1];
+        colsum[t] = v;
+    }
+    float* red = xs;   // every thread is past the samples
+    if (grp < G) {
 #pragma unroll
         for (int k = 0; k < 9; k++) red[(grp * NP + pr) * 10 + k] = acc[k];
     }
     __syncthreads();
+    float* prow = a.part + (size_t)blockIdx.x * NPART;
     for (int i = t; i < NP * 9; i += HT) {
         const int p = i / 9, k = i % 9, o = p / HM, co = p % HM;
         float v = red[p * 10 + k];
         for (int gg = 1; gg < G; gg++) v += red[(gg * NP + p) * 10 + k];
         prow[P_W2 + (o * HM + co) * 9 + (8 - k)] = v;     // flipped kernel
     }
-    if (t < HO) {   // db2: the tile's pixels, rows then columns
+    if (t < HO) {
         float v = 0.0f;
-        for (int r = 0; r < TH; r++)
-            for (int c = 0; c < TW; c++) v += ms[(t * XR + r + 1) * XC + c + 1];
+        for (int c = 0; c < TW; c++) v += colsum[t * TW + c];
         prow[P_B2 + t] = v;
     }
 }
 
-__global__ void __launch_bounds__(HT) k_head_bwd_x(HeadArgs a) {
+__global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_bwd_x(HeadArgs a) {
     constexpr int XR = TH + 2, XC = TW + 2;
     __shared__ float xs[HC * XR * XC];   // samples, tile + 1 halo
     __shared__ float ds[HM * XR * XC];   // dh, tile + 1 halo (0 outside the image)
+    __shared__ float4 w1t[NF1];
     const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
     const int y0 = ty * TH, x0 = tx * TW;
     const size_t HW = (size_t)a.H * a.W;
+    stage_weights<false, true, false>(a, nullptr, w1t, nullptr);
     stage_samples<XR, XC>(a, y0 - 1, x0 - 1, xs);
     for (int i = threadIdx.x; i < XR * XC; i += HT) {
         const int r = i / XC, c = i % XC, y = y0 - 1 + r, x = x0 - 1 + c;
@@ -258,28 +312,32 @@ __global__ void __launch_bounds__(HT) k_head_bwd_x(HeadArgs a) {
     }
     __syncthreads();
     // dL/dsample = conv1^T(dh): dx[ci][p] = sum_(co, ky, kx) w1[co][ci][ky][kx] dh[co][p - (ky, kx) + 1]
-    for (int i = threadIdx.x; i < TH * TW; i += HT) {
-        const int r = i / TW, c = i % TW, y = y0 + r, x = x0 + c;
+    for (int i = threadIdx.x; i < TH * (TW / 2); i += HT) {
+        const int r = i / (TW / 2), c = 2 * (i % (TW / 2)), y = y0 + r, x = x0 + c;
         if (y >= a.H || x >= a.W) continue;
-        float d[HC];
+        float d0[HC], d1[HC];
 #pragma unroll
-        for (int ci = 0; ci < HC; ci++) d[ci] = 0.0f;
+        for (int ci = 0; ci < HC; ci++) d0[ci] = d1[ci] = 0.0f;
+#pragma unroll 1
         for (int co = 0; co < HM; co++) {
 #pragma unroll
             for (int ky = 0; ky < 3; ky++) {
-                const float* row = ds + (co * XR + r + 2 - ky) * XC + c + 2;
-                const float g0 = row[0], g1 = row[-1], g2 = row[-2];   // kx = 0, 1, 2
+                const float* row = ds + (co * XR + r + 2 - ky) * XC + c;
+                const float g0 = row[0], g1 = row[1], g2 = row[2], g3 = row[3];
 #pragma unroll
                 for (int ci = 0; ci < HC; ci++) {
-                    const float* w = a.k1 + ((co * HC + ci) * 3 + ky) * 3;
-                    d[ci] = fmaf(w[0], g0, d[ci]);
-                    d[ci] = fmaf(w[1], g1, d[ci]);
-                    d[ci] = fmaf(w[2], g2, d[ci]);
+                    const float4 w = w1t[(co * 3 + ky) * HC + ci];   // kx = 0, 1, 2 read columns c + 2, c + 1, c
+                    d0[ci] = fmaf(w.x, g2, d0[ci]); d0[ci] = fmaf(w.y, g1, d0[ci]); d0[ci] = fmaf(w.z, g0, d0[ci]);
+                    d1[ci] = fmaf(w.x, g3, d1[ci]); d1[ci] = fmaf(w.y, g2, d1[ci]); d1[ci] = fmaf(w.z, g1, d1[ci]);
                 }
             }
         }
+        const size_t p = (size_t)y * a.W + x;
 #pragma unroll
-        for (int ci = 0; ci < HC; ci++) a.dx[ci * HW + (size_t)y * a.W + x] = d[ci];
+        for (int ci = 0; ci < HC; ci++) {
+            a.dx[ci * HW + p] = d0[ci];
+            if (x + 1 < a.W) a.dx[ci * HW + p + 1] = d1[ci];
+        }
     }
     // dW1[co][ci][ky][kx] = sum over the tile of dh[co][q] sample[ci][q + (ky, kx) - 1]; db1[co] = sum dh[co]
     // (128 pairs x 2 row groups; the groups' sums in order through LDS, reusing xs once every thread is past it)

@@ -103,7 +103,8 @@ __device__ __forceinline__ void adam_block(const AdamMultiArgs& a, const uint32_
             gx = a.dmeans2D[(size_t)i * a.dm_stride];
             gy = a.dmeans2D[(size_t)i * a.dm_stride + 1];
             if (a.depth_thr > 0.0f) {  // torch.minimum(ones, (depth / thr) ** 2), then grad * factor
-                const float q = a.depth[i] / a.depth_thr;
+                // torch divides by a Python scalar as a multiply by its float reciprocal (div_true_kernel_cuda)
+                const float q = a.depth[i] * (1.0f / a.depth_thr);
                 const float sq = q * q;
                 const float f = (sq < 1.0f || sq != sq) ? sq : 1.0f;  // torch.minimum propagates NaN
                 gx = gx * f;

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--W", type=int, default=400)
     ap.add_argument("--H", type=int, default=300)
+    ap.add_argument("--ref", action="store_true", help="tools/train_30k.py's problem and mipnerf360.yaml schedule")
     args = ap.parse_args()
     from test_gpu_trainer import _cfg, _normal, _problem
     from dogs_amd.masks import AppearanceEmbedding
@@ -35,9 +36,19 @@ def main():
     net0 = AppearanceEmbedding(4)
     trs = []
     for native in (True, False):
-        m, cams, gts = _problem(dev, n_true=30_000, n_init=6_000, W=args.W, H=args.H, views=4)
-        tr = GaussianSplatTrainer(m, cams, gts, cfg, device=dev, seed=2, native=native, normal=_normal(dev, 3),
-                                  appear_embedding=copy.deepcopy(net0) if args.mask else None)
+        if args.ref:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import train_30k as T
+            cfg = T.reference_cfg()
+            m, cams, gts = T.problem(dev, 1_000_000, 100_000, 1920, 1080, 1000.0, 24)
+            tr_idx, _ = T.split(cams, gts)
+            torch.manual_seed(0)
+            tr = GaussianSplatTrainer(m, [cams[i] for i in tr_idx], [gts[i] for i in tr_idx], cfg, device=dev,
+                                      seed=42, native=native, normal=_normal(dev, 7))
+        else:
+            m, cams, gts = _problem(dev, n_true=30_000, n_init=6_000, W=args.W, H=args.H, views=4)
+            tr = GaussianSplatTrainer(m, cams, gts, cfg, device=dev, seed=2, native=native, normal=_normal(dev, 3),
+                                      appear_embedding=copy.deepcopy(net0) if args.mask else None)
         trs.append(tr)
     first = {}
     for it in range(1, args.iters + 1):

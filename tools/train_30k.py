@@ -195,6 +195,7 @@ def run_compare(args, dev):
     cfg = reference_cfg()
     out = {"iterations": args.compare, "workload": "mipnerf360.yaml schedule, first iterations, both routes",
            "routes": {}}
+    states = []
     for native in (True, False):
         m, cams, gts = problem(dev, args.n_true, args.n_init, args.width, args.height, args.fx, args.views)
         tr_idx, te_idx = split(cams, gts)
@@ -212,6 +213,12 @@ def run_compare(args, dev):
                 log(f"{'native' if native else 'autograd'} {i + 1} loss {losses[-1]:.5f} gaussians {counts[-1]}")
         tr.sync()
         wall = time.perf_counter() - t0
+        st = {f"param.{k}": v.detach().clone() for k, v in m.params().items()}
+        for g_ in tr.optimizer.param_groups:
+            o_ = tr.optimizer.state[g_["params"][0]]
+            st[f"m.{g_['name']}"], st[f"v.{g_['name']}"] = o_["exp_avg"].clone(), o_["exp_avg_sq"].clone()
+        st["net"] = torch.cat([p_.detach().reshape(-1) for p_ in tr.mask.parameters()]) if tr.mask is not None else None
+        states.append(st)
         out["routes"]["native" if native else "autograd"] = {
             "losses": losses, "counts": counts, "wall_s": wall, "finite": finite(m),
             "test_psnr": evaluate(m, cams, gts, te_idx, dev), "train_psnr": evaluate(m, cams, gts, tr_idx, dev)}
@@ -226,6 +233,9 @@ def run_compare(args, dev):
     out["count_rel_diff_at_densify"] = {str(i + 1): float(abs(ca[i] - cb[i]) / cb[i]) for i in dens}
     out["mean_rel_loss_diff_last_500"] = float(np.mean(np.abs(la[-500:] - lb[-500:]) / lb[-500:]))
     out["test_psnr_diff"] = a["test_psnr"] - b["test_psnr"]
+    out["counts_equal_every_iteration"] = bool(np.array_equal(ca, cb))
+    out["final_state_bitwise_equal"] = {k: bool(torch.equal(states[0][k], states[1][k])) if states[0][k] is not None
+                                        else None for k in states[0]}
     for r in out["routes"].values():    # keep the record small: losses every 10 iterations
         r["losses"] = r["losses"][::10]
         r["counts"] = r["counts"][::10]
