@@ -571,6 +571,8 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--views", type=int, default=8)
+    ap.add_argument("--opacity-mean", type=float, default=0.0,
+                    help="raw opacity ~ N(mean, 1.5): -2 is the sweep's non-saturating scene (profiling runs)")
     ap.add_argument("--consensus-interval", type=int, default=200)
     ap.add_argument("--shared-frac", type=float, default=0.2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -627,7 +629,7 @@ def main():
     n, W, H = args.n, args.width, args.height
     seed = 1234 + rank
     from dogs_amd.synthetic import make_scene
-    s = make_scene(n, W, H, seed=seed).to(dev)
+    s = make_scene(n, W, H, seed=seed, opacity_mean=args.opacity_mean).to(dev)
     yaws = view_yaws(args.views)
     cams = make_cameras(W, H, yaws, dev)
     g = torch.Generator().manual_seed(seed + 99)
@@ -702,7 +704,7 @@ def main():
         r = views.stats(k, reference_k=not args.no_reference_k)
         r.update(view=k, yaw=round(y, 3), N=n, HW=HW)
         vstats.append(r)
-    pmc = load_pmc(n, W, H)
+    pmc = load_pmc_key(f"{n}x{W}x{H}" + ("-sparse" if args.opacity_mean != 0.0 else ""))
     pp = phase_profile(views, yaws, vstats, pmc)
     phase_ms, phase_b, dom = pp["phase_ms_raw"], pp["phase_b_raw"], pp["dominant"]
     dom_ms, dom_bytes = phase_ms[dom], phase_b[dom]

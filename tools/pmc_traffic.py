@@ -9,7 +9,7 @@ Per phase (the sum over its kernels, each averaged per dispatch):
   us          kernel-trace duration
 Kernels are matched by name prefix (pmc_summary._short names); phase-2 kernels launched under the same names by the
 gated phase-2 path are the '<2' template instances and are not matched.
-usage: python tools/pmc_traffic.py PROFILE_DIR N W H
+usage: python tools/pmc_traffic.py PROFILE_DIR N W H [SUFFIX]   (key "{N}x{W}x{H}{SUFFIX}", e.g. SUFFIX -sparse)
 """
 import json
 import os
@@ -27,13 +27,13 @@ PHASE_KERNELS = {
 }
 
 
-def main(root, n, W, H):
+def main(root, n, W, H, suffix=""):
     acc = load_counters(root)
     dur = load_durations(root)
     out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                             "pmc_traffic.json")
     d = json.load(open(out_path)) if os.path.exists(out_path) else {}
-    key = f"{n}x{W}x{H}"
+    key = f"{n}x{W}x{H}{suffix}"
     ent = {}
     for phase, prefixes in PHASE_KERNELS.items():
         ks = sorted({k for k in set(acc) | set(dur) for p in prefixes if k.startswith(p)})
@@ -55,4 +55,4 @@ def main(root, n, W, H):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))
+    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5] if len(sys.argv) > 5 else "")
