@@ -97,7 +97,7 @@ class DgBox2dSet(C.Structure):
                 ("box", (C.c_double * 4) * DG_MAX_BOXES)]
 
 EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count", "dg_mark_visible", "dg_rasterize_filter",
-           "dg_cull_log_threshold", "dg_conv3x3_wgrad", "dg_conv3x3_wgrad_scratch_bytes",
+           "dg_cull_log_threshold", "dg_adaptive_capacity_ctx", "dg_release_capacity_context", "dg_capacity_contexts", "dg_conv3x3_wgrad", "dg_conv3x3_wgrad_scratch_bytes",
            "dg_mask_head_forward", "dg_mask_head_backward", "dg_mask_head_scratch_bytes", "dg_mask_head_nparams",
            "dg_adam_update", "dg_fused_ssim_forward", "dg_fused_ssim_backward", "dg_fused_ssim_parts",
            "dg_fused_ssim_mean", "dg_fused_ssim_mean_backward", "dg_mean_of_parts", "dg_dist_cuda2",
@@ -206,6 +206,12 @@ def load(path: str | None = None):
         if hasattr(L, "dg_adaptive_capacity"):
             L.dg_adaptive_capacity.restype = C.c_int
             L.dg_adaptive_capacity.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
+            L.dg_adaptive_capacity_ctx.restype = C.c_int
+            L.dg_adaptive_capacity_ctx.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
+            L.dg_release_capacity_context.restype = C.c_int
+            L.dg_release_capacity_context.argtypes = [C.c_int]
+            L.dg_capacity_contexts.restype = C.c_int
+            L.dg_capacity_contexts.argtypes = [C.POINTER(C.c_int)]
         L.dg_debug_geometry.restype = C.c_int
         L.dg_debug_geometry.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp]
         L.dg_debug_image_state.restype = C.c_int
@@ -436,6 +442,29 @@ def adaptive_capacity(W: int, H: int, reset: bool = False) -> int:
     first returns it to its cold default."""
     v = C.c_int(0)
     check(load().dg_adaptive_capacity(int(W), int(H), 1 if reset else 0, C.byref(v)))
+    return int(v.value)
+
+
+def adaptive_capacity_ctx(ctx: int, W: int, H: int, reset: bool = False) -> int:
+    """The same for one capacity context only (dg_adaptive_capacity_ctx)."""
+    v = C.c_int(0)
+    check(load().dg_adaptive_capacity_ctx(int(ctx), int(W), int(H), 1 if reset else 0, C.byref(v)))
+    return int(v.value)
+
+
+def release_capacity_context(ctx: int) -> None:
+    """Drop a capacity context's state and device probes (dg_release_capacity_context); quiet at interpreter exit."""
+    try:
+        L = load()
+    except Exception:  # noqa: BLE001
+        return
+    L.dg_release_capacity_context(int(ctx))
+
+
+def capacity_contexts() -> int:
+    """Capacity contexts that hold a device probe."""
+    v = C.c_int(0)
+    check(load().dg_capacity_contexts(C.byref(v)))
     return int(v.value)
 
 

@@ -199,7 +199,7 @@ class BlockTrainer:
     def _capacity(self):
         from .diff_gaussian_rasterization import _C
         if getattr(self, "capacity_ctx", None) is None:
-            self.capacity_ctx = _C.new_capacity_context()
+            self.capacity_ctx = _C.new_capacity_context(owner=self)
         return _C.capacity_context(self.capacity_ctx)
 
     def _local_step(self) -> None:

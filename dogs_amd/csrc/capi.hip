@@ -14,6 +14,10 @@
 #include <mutex>
 #include <atomic>
 #include <thread>
+#include <algorithm>
+#include <atomic>
+#include <thread>
+#include <algorithm>
 
 #include "../../include/dogs_hip.h"
 #include "aux_kernels.h"
@@ -346,6 +350,45 @@ std::map<std::tuple<int, int, int, int, hipStream_t>, CapProbe>& cap_probes() {
     static auto* m = new std::map<std::tuple<int, int, int, int, hipStream_t>, CapProbe>;  // node-based: never move
     return *m;
 }
+// Released contexts (dg_release_capacity_context): their map nodes are extracted -- so no new render finds them --
+// but kept alive until no library call is in flight, since a forward may still hold a CapProbe* of the context.
+std::vector<std::map<std::tuple<int, int, int, int, hipStream_t>, CapProbe>::node_type>& cap_probe_graveyard() {
+    static auto* v = new std::vector<std::map<std::tuple<int, int, int, int, hipStream_t>, CapProbe>::node_type>;
+    return *v;
+}
+std::vector<std::map<CapKey, AdaptiveCap>::node_type>& cap_state_graveyard() {
+    static auto* v = new std::vector<std::map<CapKey, AdaptiveCap>::node_type>;
+    return *v;
+}
+
+// Library calls in flight, and the shutdown flag (dg_shutdown): a call registers itself before it checks the flag,
+// and dg_shutdown sets the flag before it waits for the count to drain, so no call that passed the check can meet
+// freed state (the autograd device thread or a ring thread may still be inside the library at exit).
+std::atomic<bool> g_shutting_down{false};
+std::atomic<int> g_calls_in_flight{0};
+struct ApiGuard {
+    bool ok;
+    ApiGuard() {
+        g_calls_in_flight.fetch_add(1, std::memory_order_acq_rel);
+        ok = !g_shutting_down.load(std::memory_order_acquire);
+    }
+    ~ApiGuard() { g_calls_in_flight.fetch_sub(1, std::memory_order_acq_rel); }
+    ApiGuard(const ApiGuard&) = delete;
+    ApiGuard& operator=(const ApiGuard&) = delete;
+};
+#define API_GUARD()                                              \
+    ApiGuard api_guard_;                                         \
+    if (!api_guard_.ok) return fail("the library is shutting down%s%d")
+
+// free the released contexts' probes once this call is the only one in flight (g_cap_mu held)
+void drain_cap_graveyard_locked() {
+    if (g_calls_in_flight.load(std::memory_order_acquire) > 1) return;
+    for (auto& nh : cap_probe_graveyard())
+        if (!nh.empty() && nh.mapped().probe) (void)hipFree(nh.mapped().probe);
+    cap_probe_graveyard().clear();
+    cap_state_graveyard().clear();
+}
+
 CapProbe* adaptive_cap(const dg_raster_args* a, hipStream_t s) {
     if (a->prefix_per_tile != 0) return nullptr;
     int dev = 0;
@@ -494,20 +537,66 @@ int dg_exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_
 }
 int dg_version(void) { return 1; }
 
-int dg_adaptive_capacity(int W, int H, int reset, int* per_tile_out) {
+// reset / query the adaptive capacity at (device, W, H): ctx < 0 resets every context (state and probes alike) and
+// reports context 0; ctx >= 0 only that context
+static int adaptive_capacity_impl(int ctx, int W, int H, int reset, int* per_tile_out) {
     int dev = 0;
     HIP_OK(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(g_cap_mu);
-    AdaptiveCap& c = cap_states()[std::make_tuple(dev, W, H, 0)];
     if (reset) {
-        c.per_tile = DEFAULT_PREFIX_PER_TILE;
+        for (auto& kv : cap_states())
+            if (std::get<0>(kv.first) == dev && std::get<1>(kv.first) == W && std::get<2>(kv.first) == H &&
+                (ctx < 0 || std::get<3>(kv.first) == ctx))
+                kv.second.per_tile = DEFAULT_PREFIX_PER_TILE;
         for (auto& kv : cap_probes()) {
             if (std::get<0>(kv.first) != dev || std::get<1>(kv.first) != W || std::get<2>(kv.first) != H) continue;
+            if (ctx >= 0 && std::get<3>(kv.first) != ctx) continue;
             kv.second.last_e1 = 0;
             if (kv.second.probe) HIP_OK(hipMemset(kv.second.probe, 0, 2 * sizeof(uint32_t)));
         }
     }
-    if (per_tile_out) *per_tile_out = c.per_tile;
+    if (per_tile_out) *per_tile_out = cap_states()[std::make_tuple(dev, W, H, ctx < 0 ? 0 : ctx)].per_tile;
+    return 0;
+}
+
+int dg_adaptive_capacity(int W, int H, int reset, int* per_tile_out) {
+    API_GUARD();
+    return adaptive_capacity_impl(-1, W, H, reset, per_tile_out);
+}
+
+int dg_adaptive_capacity_ctx(int ctx, int W, int H, int reset, int* per_tile_out) {
+    API_GUARD();
+    if (ctx < 0) return fail("adaptive_capacity_ctx: negative context%s%d");
+    return adaptive_capacity_impl(ctx, W, H, reset, per_tile_out);
+}
+
+int dg_release_capacity_context(int ctx) {
+    API_GUARD();
+    if (ctx <= 0) return 0;   // 0 is the process-wide default, never released
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    for (auto it = cap_probes().begin(); it != cap_probes().end();) {
+        auto nx = std::next(it);
+        if (std::get<3>(it->first) == ctx) cap_probe_graveyard().push_back(cap_probes().extract(it));
+        it = nx;
+    }
+    for (auto it = cap_states().begin(); it != cap_states().end();) {
+        auto nx = std::next(it);
+        if (std::get<3>(it->first) == ctx) cap_state_graveyard().push_back(cap_states().extract(it));
+        it = nx;
+    }
+    drain_cap_graveyard_locked();
+    return 0;
+}
+
+int dg_capacity_contexts(int* n_out) {
+    API_GUARD();
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    std::vector<int> seen;
+    for (auto& kv : cap_probes()) {
+        const int c = std::get<3>(kv.first);
+        if (std::find(seen.begin(), seen.end(), c) == seen.end()) seen.push_back(c);
+    }
+    if (n_out) *n_out = (int)seen.size();
     return 0;
 }
 
@@ -749,6 +838,7 @@ extern "C" {
 int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_invdepth, int* radii,
                          dg_alloc_fn alloc, void* user, void** geom_out, void** binning_out, void** image_out,
                          void** binning2_out, int64_t* num_rendered, int64_t* num_instances, dg_stream_t stream) {
+    API_GUARD();
     return forward_impl(a, out_color, out_invdepth, radii, alloc, user, geom_out, binning_out, image_out,
                         binning2_out, num_rendered, num_instances, stream, nullptr);
 }
@@ -756,6 +846,7 @@ int dg_rasterize_forward(const dg_raster_args* a, float* out_color, float* out_i
 int dg_rasterize_count(const dg_raster_args* a, float* out_color, int* radii, int32_t* gaussians_count,
                        float* important_score, dg_alloc_fn alloc, void* user, int64_t* num_rendered,
                        dg_stream_t stream) {
+    API_GUARD();
     if (check_args(a)) return 1;
     if (a->P > 0 && (!gaussians_count || !important_score)) return fail("count outputs required%s%d");
     hipStream_t s = (hipStream_t)stream;
@@ -780,6 +871,7 @@ int dg_rasterize_backward(const dg_raster_args* a, const int* radii, const void*
                           const float* dL_dout_color, const float* dL_dout_invdepth, float* dmeans2D, float* dcolors,
                           float* dopacity, float* dmeans3D, float* dcov3D, float* ddc, float* dsh, float* dscales,
                           float* drot, float* depth, dg_alloc_fn alloc, void* user, dg_stream_t stream_) {
+    API_GUARD();
     if (check_args(a)) return 1;
     hipStream_t s = (hipStream_t)stream_;
     const int P = a->P, W = a->W, H = a->H;
@@ -1059,6 +1151,7 @@ int dg_adam_update_groups_prox(const dg_adam_group* groups, const dg_adam_prox* 
 }
 
 int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg_stream_t stream) {
+    API_GUARD();
     if (!a || !a->gt || !a->radii || !a->image) return fail("train step: args, gt, radii and image are required%s%d");
     hipStream_t s = (hipStream_t)stream;
     const int P = a->view.P, W = a->view.W, H = a->view.H, M = a->view.M;
@@ -1264,6 +1357,7 @@ int dg_train_step(const dg_train_step_args* a, dg_alloc_fn alloc, void* user, dg
 }
 
 int dg_train_sync(dg_stream_t stream) {
+    API_GUARD();
     ShOverlap* ov = sh_state((hipStream_t)stream, false);
     if (ov && ov->pending) {
         HIP_OK(hipStreamWaitEvent((hipStream_t)stream, ov->done, 0));
@@ -1823,6 +1917,11 @@ int dg_debug_image_state(const void* image, int W, int H, float* final_T, uint32
 }
 
 int dg_shutdown(void) {
+    // new calls fail from here on; wait (bounded) for the calls already inside the library to leave
+    g_shutting_down.store(true, std::memory_order_release);
+    for (int i = 0; i < 5000 && g_calls_in_flight.load(std::memory_order_acquire) > 0; i++)
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    if (g_calls_in_flight.load(std::memory_order_acquire) > 0) return fail("shutdown: calls still in flight%s%d");
     // side streams of the overlapped SH update: drain, then destroy (with their events)
     {
         std::lock_guard<std::mutex> lk(sh_mu());
@@ -1839,6 +1938,7 @@ int dg_shutdown(void) {
         for (auto& kv : cap_probes())
             if (kv.second.probe) (void)hipFree(kv.second.probe);
         cap_probes().clear();
+        drain_cap_graveyard_locked();
     }
     {
         auto release = [](HostCounters& h) {

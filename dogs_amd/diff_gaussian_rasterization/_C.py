@@ -38,8 +38,14 @@ _CTX = threading.local()
 _NEXT_CTX = itertools.count(1)
 
 
-def new_capacity_context() -> int:
-    return next(_NEXT_CTX)
+def new_capacity_context(owner=None) -> int:
+    """A fresh capacity context; with `owner`, its library state is released when the owner is garbage collected
+    (dg_release_capacity_context: the per-context device probes do not outlive the trainer)."""
+    ctx = next(_NEXT_CTX)
+    if owner is not None:
+        import weakref
+        weakref.finalize(owner, _lib.release_capacity_context, ctx)
+    return ctx
 
 
 @contextlib.contextmanager

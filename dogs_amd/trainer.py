@@ -341,7 +341,7 @@ class GaussianSplatTrainer:
         # rounding do not depend on anything else this process rendered (dg_raster_args.capacity_ctx)
         from .diff_gaussian_rasterization import _C
         if getattr(self, "capacity_ctx", None) is None:
-            self.capacity_ctx = _C.new_capacity_context()
+            self.capacity_ctx = _C.new_capacity_context(owner=self)
         with _C.capacity_context(self.capacity_ctx):
             return self._train_iteration()
 

@@ -419,6 +419,14 @@ int dg_debug_counters(const void* geom, int P, uint32_t* counters16, dg_stream_t
  * units per tile (*per_tile_out, may be NULL); reset != 0 sets it back to its cold default first.  Tests and the
  * bench use it to start a scene cold and to report what the views settled on. */
 int dg_adaptive_capacity(int W, int H, int reset, int* per_tile_out);
+/* The same for one capacity context (dg_raster_args.capacity_ctx) only; dg_adaptive_capacity resets every context at
+ * (device, W, H) and reports context 0. */
+int dg_adaptive_capacity_ctx(int ctx, int W, int H, int reset, int* per_tile_out);
+/* Drop a capacity context's state and device probes (a trainer that is gone); context 0 is never released.  The
+ * probes are freed once no library call is in flight. */
+int dg_release_capacity_context(int ctx);
+/* Number of capacity contexts that hold a device probe (diagnostics and tests). */
+int dg_capacity_contexts(int* n_out);
 int dg_debug_geometry(const void* geom, int P, float* means2D, float* conic_opacity, float* rgb_invdepth,
                       uint32_t* tile_count, dg_stream_t stream);
 int dg_debug_image_state(const void* image, int W, int H, float* final_T, uint32_t* n_contrib,

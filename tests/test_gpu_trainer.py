@@ -356,3 +356,29 @@ def test_overlap_with_two_view_sizes_is_bitwise_serial(hip_device):
         assert torch.equal(out[0][0][k], out[1][0][k]), k
     for k in out[0][1]:
         assert torch.equal(out[0][1][k], out[1][1][k]), k
+
+
+def test_capacity_context_released_with_trainer(hip_device):
+    """a trainer's own adaptive-capacity context (its device probe and state in the library) is released
+    when the trainer is garbage collected; dg_adaptive_capacity(reset) resets every context of the image size and
+    dg_adaptive_capacity_ctx queries one."""
+    import gc
+    from dogs_amd import _lib
+    from dogs_amd.trainer import GaussianSplatTrainer
+    gc.collect()
+    torch.cuda.synchronize()
+    n0 = _lib.capacity_contexts()
+    m, cams, gts = _problem(hip_device, n_true=20_000, n_init=4_000, W=320, H=240, views=2)
+    tr = GaussianSplatTrainer(m, cams, gts, _cfg(densify_start_iter=10 ** 6), device=hip_device, seed=0, native=True)
+    for _ in range(3):
+        tr.train_iteration()
+    tr.sync()
+    torch.cuda.synchronize()
+    ctx = tr.capacity_ctx
+    assert _lib.capacity_contexts() == n0 + 1
+    _lib.adaptive_capacity(320, 240, reset=True)
+    assert _lib.adaptive_capacity_ctx(ctx, 320, 240) == _lib.adaptive_capacity(320, 240)
+    del tr
+    gc.collect()
+    torch.cuda.synchronize()
+    assert _lib.capacity_contexts() == n0
