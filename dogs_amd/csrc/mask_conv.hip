@@ -141,27 +141,47 @@ __global__ void __launch_bounds__(WG_THREADS) k_conv3x3_wgrad_part(WgradShape s,
     }
 }
 
-// one wave per weight: lane l sums blocks l, l + 64, ... in order, then the wave sums its lanes in a fixed tree
-__global__ void __launch_bounds__(256) k_conv3x3_wgrad_reduce(int npart, int nblk, const float* __restrict__ part,
-                                                               float* __restrict__ dw, float* __restrict__ db,
-                                                               int nw) {
-    const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (wv >= npart) return;
+}  // namespace
+
+// Column sums of a [nrows][ncols] array of per-block partials in a fixed order: pass 1 sums each column over
+// RS_SEG contiguous row segments (a block covers 64 columns x 4 segments: each wave reads whole 256-B row pieces),
+// pass 2 adds the segments in order.  (One wave per column striding over the rows read 64 cache lines per load and
+// took 25-37 us; this takes a few.)
+constexpr int RS_SEG = 32;
+
+__global__ void __launch_bounds__(256) k_rowsum_seg(const float* __restrict__ part, int nrows, int ncols,
+                                                     float* __restrict__ seg) {
+    const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int sg = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (col >= ncols) return;
+    const int r0 = (int)((int64_t)nrows * sg / RS_SEG), r1 = (int)((int64_t)nrows * (sg + 1) / RS_SEG);
     float v = 0.0f;
-    for (int b = lane; b < nblk; b += 64) v += part[(size_t)b * npart + wv];
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-    if (lane == 0) {
-        if (wv < nw) dw[wv] = v;
-        else db[wv - nw] = v;
-    }
+    for (int r = r0; r < r1; r++) v += part[(size_t)r * ncols + col];
+    seg[(size_t)sg * ncols + col] = v;
 }
 
-}  // namespace
+__global__ void __launch_bounds__(256) k_rowsum_final(const float* __restrict__ seg, int ncols, int nsplit,
+                                                       float* __restrict__ out_a, float* __restrict__ out_b) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    if (col >= ncols) return;
+    float v = 0.0f;
+#pragma unroll 8
+    for (int sg = 0; sg < RS_SEG; sg++) v += seg[(size_t)sg * ncols + col];
+    if (col < nsplit) out_a[col] = v;
+    else out_b[col - nsplit] = v;
+}
+
+void launch_rowsum(const float* part, int nrows, int ncols, float* seg, float* out_a, int nsplit, float* out_b,
+                   hipStream_t st) {
+    k_rowsum_seg<<<dim3((ncols + 63) / 64, RS_SEG / 4), 256, 0, st>>>(part, nrows, ncols, seg);
+    k_rowsum_final<<<(ncols + 255) / 256, 256, 0, st>>>(seg, ncols, nsplit, out_a, out_b);
+}
+
+size_t rowsum_scratch_floats(int ncols) { return (size_t)RS_SEG * ncols; }
 
 size_t conv3x3_wgrad_scratch_bytes(int Cin, int Cout, int H, int W) {
     const WgradShape s = wgrad_shape(Cin, Cout, H, W);
-    return (size_t)s.tiles_x * s.tiles_y * s.npart * sizeof(float);
+    return ((size_t)s.tiles_x * s.tiles_y * s.npart + rowsum_scratch_floats(s.npart)) * sizeof(float);
 }
 
 bool conv3x3_wgrad_supported(int Cin, int Cout) {
@@ -178,7 +198,7 @@ void launch_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const
     const int stage = Cin * s.xs_stride + Cout * s.dy_stride;
     const size_t lds = (size_t)(stage > WG_THREADS * 10 ? stage : WG_THREADS * 10) * sizeof(float);
     k_conv3x3_wgrad_part<<<nblk, WG_THREADS, lds, st>>>(s, x, dy, scratch);
-    k_conv3x3_wgrad_reduce<<<(s.npart + 3) / 4, 256, 0, st>>>(s.npart, nblk, scratch, dw, db, Cout * Cin * 9);
+    launch_rowsum(scratch, nblk, s.npart, scratch + (size_t)nblk * s.npart, dw, Cout * Cin * 9, db, st);
 }
 
 }  // namespace gs

@@ -13,7 +13,7 @@
 //   k_head_bwd_x  per tile: the samples (tile + 1 halo) and dh (tile + 1 halo) -> the tile's partial dW1, db1 and
 //                 dL/dsample = conv1^T(dh) on the tile -> dx [16, H, W];
 //   k_head_bwd_u  per stage-4 pixel: the resize's adjoint as a gather over the samples that read it, in a fixed order;
-//   k_head_reduce one wave per weight: the tiles' partials summed lane-strided, then across the wave.
+//   launch_rowsum the tiles' partials summed per parameter in a fixed order (mask_conv.hip).
 // No atomics: bitwise repeatable for a given shape (the ADMM ranks and the sequential baseline rely on it).
 // Weights are wave-uniform: the compiler keeps them in SGPRs (scalar loads), the per-position data in LDS.
 #include <hip/hip_runtime.h>
@@ -411,16 +411,6 @@ __global__ void __launch_bounds__(256) k_head_bwd_u(HeadArgs a) {
     for (int ci = 0; ci < HC; ci++) a.du[ci * hw2 + idx] = acc[ci];
 }
 
-__global__ void __launch_bounds__(256) k_head_reduce(int nblk, const float* __restrict__ part, float* __restrict__ out) {
-    const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (wv >= NPART) return;
-    float v = 0.0f;
-    for (int b = lane; b < nblk; b += 64) v += part[(size_t)b * NPART + wv];
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-    if (lane == 0) out[wv] = v;
-}
-
 }  // namespace
 
 int mask_head_tiles(int H, int W) { return ((W + TW - 1) / TW) * ((H + TH - 1) / TH); }
@@ -440,7 +430,7 @@ void launch_mask_head_bwd(HeadArgs a, float* grads, hipStream_t st) {
     k_head_bwd_x<<<nb, HT, 0, st>>>(a);
     const int64_t nu = (int64_t)a.h2 * a.w2;
     k_head_bwd_u<<<(unsigned)((nu + 255) / 256), 256, 0, st>>>(a);
-    k_head_reduce<<<(NPART + 3) / 4, 256, 0, st>>>(nb, a.part, grads);
+    launch_rowsum(a.part, nb, NPART, a.part + (size_t)nb * NPART, grads, NPART, nullptr, st);
 }
 
 }  // namespace gs
