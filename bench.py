@@ -598,8 +598,6 @@ def load_pmc(n: int, W: int, H: int):
 
 
 def main():
-    from dogs_amd.masks import ensure_fast_find_mode
-    ensure_fast_find_mode()      # before any convolution (the ADMM leg's ranks pick the same MIOpen algorithms)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks (one per GPU); > 1 without a launcher relaunches under torch.distributed.run")

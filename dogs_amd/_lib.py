@@ -98,6 +98,7 @@ class DgBox2dSet(C.Structure):
 
 EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count", "dg_mark_visible", "dg_rasterize_filter",
            "dg_cull_log_threshold", "dg_adaptive_capacity_ctx", "dg_release_capacity_context", "dg_capacity_contexts", "dg_conv3x3_wgrad", "dg_conv3x3_wgrad_scratch_bytes",
+           "dg_conv3x3",
            "dg_mask_head_forward", "dg_mask_head_backward", "dg_mask_head_scratch_bytes", "dg_mask_head_nparams",
            "dg_adam_update", "dg_fused_ssim_forward", "dg_fused_ssim_backward", "dg_fused_ssim_parts",
            "dg_fused_ssim_mean", "dg_fused_ssim_mean_backward", "dg_mean_of_parts", "dg_dist_cuda2",
@@ -153,6 +154,8 @@ def load(path: str | None = None):
         L.dg_mask_head_scratch_bytes.argtypes = [C.c_int, C.c_int]
         L.dg_mask_head_nparams.restype = C.c_int
         L.dg_conv3x3_wgrad.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, C.c_size_t, vp]
+        L.dg_conv3x3.restype = C.c_int
+        L.dg_conv3x3.argtypes = [C.c_int] * 4 + [vp] * 4 + [C.c_int, vp]
         L.dg_cull_log_threshold.argtypes = [C.c_int64, vp, vp, vp]
         L.dg_rasterize_filter.argtypes = [C.POINTER(DgRasterArgs), vp, vp]
         L.dg_adam_update.restype = C.c_int

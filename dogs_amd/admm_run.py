@@ -297,8 +297,6 @@ def main(argv=None) -> None:
     import json
     import os
     import tempfile
-    from .masks import ensure_fast_find_mode
-    ensure_fast_find_mode()      # before any convolution: the ranks' embeddings pick the same MIOpen algorithms
     p = argparse.ArgumentParser()
     p.add_argument("--config", default=None, help="a reference YAML (urban3d_admm.yaml); default: the built-in keys")
     p.add_argument("--mx", type=int, default=2)

@@ -985,6 +985,17 @@ int dg_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const floa
     return 0;
 }
 
+int dg_conv3x3(int Cin, int Cout, int H, int W, const float* x, const float* w, const float* b, float* y, int adjoint,
+               dg_stream_t stream) {
+    if (!x || !w || !y) return fail("conv3x3: bad args%s%d");
+    if (!gs::conv3x3_supported(Cin, Cout, H, W)) return fail("conv3x3: unsupported shape%s%d", "", Cin * Cout);
+    // the adjoint launches Cout -> Cin over the forward's weights
+    if (adjoint) gs::launch_conv3x3(Cout, Cin, H, W, x, w, nullptr, y, true, (hipStream_t)stream);
+    else gs::launch_conv3x3(Cin, Cout, H, W, x, w, b, y, false, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
 static bool head_shape_ok(int H, int W, int h2, int w2) {
     // the adjoint gather lists at most 12 samples per source index and axis: upsampling by at most 4
     return H > 0 && W > 0 && h2 > 0 && w2 > 0 && H <= 4 * h2 && W <= 4 * w2;

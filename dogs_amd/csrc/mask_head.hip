@@ -6,7 +6,7 @@
 // resize, im2col GEMMs and col2im for the two convolutions, their weight gradients, and the resize's adjoint as
 // gathers -- about 3 ms of the 4.5 ms a masked 1080p iteration spends in the embedding (gpurun_out/r6a/mtrace).
 // Here the 16-channel image never exists:
-//   k_head_fwd    per 8 x 64 output tile: the bilinear samples of the stage-4 output on the tile + 2 halo into LDS,
+//   k_head_fwd    per 6 x 62 output tile: the bilinear samples of the stage-4 output on the tile + 2 halo into LDS,
 //                 conv1 + ReLU on the tile + 1 halo into LDS, conv2 -> the [3, H, W] mask;
 //   k_head_bwd_h  per tile: recompute the samples (tile + 1 halo) and h on the tile; dL/dh = [h > 0] conv2^T(dmask)
 //                 (dmask on the tile + 1 halo) -> dh [8, H, W]; the tile's partial dW2, db2 (fixed-order sums);
@@ -25,7 +25,10 @@ namespace gs {
 namespace {
 
 constexpr int HC = 16, HM = 8, HO = 3;        // sample channels, hidden channels, mask channels
-constexpr int TH = 8, TW = 64;                 // output tile
+constexpr int TH = 8, TW = 64;                 // output tile of the backward kernels
+// The forward's tile: its conv1 covers the tile + 1 halo, (6 + 2) x (62 + 2) = 256 position pairs, one per thread
+// (an 8 x 64 tile's 10 x 66 = 330 pairs took two passes at 64% use).
+constexpr int FTH = 6, FTW = 62;
 constexpr int HT = 256;                        // threads per block
 constexpr int NW1 = HM * HC * 9, NW2 = HO * HM * 9;
 constexpr int P_W1 = 0, P_B1 = NW1, P_W2 = NW1 + HM, P_B2 = NW1 + HM + NW2;
@@ -77,6 +80,12 @@ constexpr int NF1 = HC * 3 * HM, NF2 = HM * 3 * HO;   // float4 rows per weight 
 
 __device__ __forceinline__ float4 wrow(const float* w) { return make_float4(w[0], w[1], w[2], 0.0f); }
 
+// Two positions of a row at once: v_pk_fma_f32 with the weight broadcast to both halves (each half is the same fmaf
+// as the scalar form, so the bits do not change).  Left to itself the compiler paired output channels instead, and
+// spent a v_mov per weight building the pairs.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 fma2(float w, f2 x, f2 acc) { return __builtin_elementwise_fma((f2)(w), x, acc); }
+
 template <bool CONV1, bool CONV1T, bool CONV2T>
 __device__ __forceinline__ void stage_weights(const HeadArgs& a, float4* w1f, float4* w1t, float4* w2t) {
     for (int i = threadIdx.x; i < NF1; i += HT) {
@@ -94,26 +103,26 @@ __device__ __forceinline__ void stage_weights(const HeadArgs& a, float4* w1f, fl
 template <int XR, int XC>
 __device__ __forceinline__ void conv1_pair(const float* b1, const float4* w1f, const float* xs, int r, int c,
                                            float (&h0)[HM], float (&h1)[HM]) {
+    f2 h[HM];
 #pragma unroll
-    for (int co = 0; co < HM; co++) h0[co] = h1[co] = b1[co];
+    for (int co = 0; co < HM; co++) h[co] = (f2)(b1[co]);
 #pragma unroll 1
     for (int ci = 0; ci < HC; ci++) {
 #pragma unroll
         for (int ky = 0; ky < 3; ky++) {
             const float* row = xs + (ci * XR + r + ky) * XC + c;
-            const float x0 = row[0], x1 = row[1], x2 = row[2], x3 = row[3];
+            const f2 xa = {row[0], row[1]}, xb = {row[1], row[2]}, xc = {row[2], row[3]};
 #pragma unroll
             for (int co = 0; co < HM; co++) {
                 const float4 w = w1f[(ci * 3 + ky) * HM + co];
-                h0[co] = fmaf(w.x, x0, h0[co]); h0[co] = fmaf(w.y, x1, h0[co]); h0[co] = fmaf(w.z, x2, h0[co]);
-                h1[co] = fmaf(w.x, x1, h1[co]); h1[co] = fmaf(w.y, x2, h1[co]); h1[co] = fmaf(w.z, x3, h1[co]);
+                h[co] = fma2(w.x, xa, h[co]); h[co] = fma2(w.y, xb, h[co]); h[co] = fma2(w.z, xc, h[co]);
             }
         }
     }
 #pragma unroll
     for (int co = 0; co < HM; co++) {
-        h0[co] = h0[co] > 0.0f ? h0[co] : 0.0f;
-        h1[co] = h1[co] > 0.0f ? h1[co] : 0.0f;
+        h0[co] = h[co].x > 0.0f ? h[co].x : 0.0f;
+        h1[co] = h[co].y > 0.0f ? h[co].y : 0.0f;
     }
 }
 
@@ -144,13 +153,16 @@ __device__ __forceinline__ void window_sums(const float* in, int in_stride, cons
 }
 
 __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_fwd(HeadArgs a) {
-    constexpr int XR = TH + 4, XC = TW + 4, QR = TH + 2, QC = TW + 2;
-    __shared__ float xs[HC * XR * XC];   // samples, tile + 2 halo
-    __shared__ float hs[HM * QR * QC];   // hidden, tile + 1 halo (0 outside the image: conv2's padding)
-    __shared__ float4 w1f[NF1];          // (conv2's 216 weights stay scalar loads: two blocks per CU fit 160 KB)
-    __shared__ float sb1[HM], sb2[HO];
+    constexpr int XR = FTH + 4, XC = FTW + 4, QR = FTH + 2, QC = FTW + 2;
+    // one LDS array, the weights first: their reads take immediate offsets from one base (< 64 KB)
+    __shared__ float4 smem[NF1 + (HC * XR * XC + HM * QR * QC + 12) / 4];
+    float4* w1f = smem;                  // (conv2's 216 weights stay scalar loads: two blocks per CU fit 160 KB)
+    float* sb1 = (float*)(smem + NF1);
+    float* sb2 = sb1 + HM;
+    float* xs = sb1 + 12;                // samples, tile + 2 halo
+    float* hs = xs + HC * XR * XC;       // hidden, tile + 1 halo (0 outside the image: conv2's padding)
     const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
-    const int y0 = ty * TH, x0 = tx * TW;
+    const int y0 = ty * FTH, x0 = tx * FTW;
     stage_weights<true, false, false>(a, w1f, nullptr, nullptr);
     if (threadIdx.x < HM) sb1[threadIdx.x] = a.b1[threadIdx.x];
     if (threadIdx.x < HO) sb2[threadIdx.x] = a.b2[threadIdx.x];
@@ -169,32 +181,30 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
     __syncthreads();
     const size_t HW = (size_t)a.H * a.W;
-    for (int i = threadIdx.x; i < TH * (TW / 2); i += HT) {
-        const int r = i / (TW / 2), c = 2 * (i % (TW / 2)), y = y0 + r, x = x0 + c;
+    for (int i = threadIdx.x; i < FTH * (FTW / 2); i += HT) {
+        const int r = i / (FTW / 2), c = 2 * (i % (FTW / 2)), y = y0 + r, x = x0 + c;
         if (y >= a.H || x >= a.W) continue;
-        float m0[HO], m1[HO];
+        f2 m[HO];
 #pragma unroll
-        for (int o = 0; o < HO; o++) m0[o] = m1[o] = sb2[o];
+        for (int o = 0; o < HO; o++) m[o] = (f2)(sb2[o]);
 #pragma unroll 1
         for (int co = 0; co < HM; co++) {
 #pragma unroll
             for (int ky = 0; ky < 3; ky++) {
                 const float* row = hs + (co * QR + r + ky) * QC + c;
-                const float v0 = row[0], v1 = row[1], v2 = row[2], v3 = row[3];
+                const f2 va = {row[0], row[1]}, vb = {row[1], row[2]}, vc = {row[2], row[3]};
 #pragma unroll
                 for (int o = 0; o < HO; o++) {
                     const float* wp = a.k2 + ((o * HM + co) * 3 + ky) * 3;
-                    const float4 w = make_float4(wp[0], wp[1], wp[2], 0.0f);
-                    m0[o] = fmaf(w.x, v0, m0[o]); m0[o] = fmaf(w.y, v1, m0[o]); m0[o] = fmaf(w.z, v2, m0[o]);
-                    m1[o] = fmaf(w.x, v1, m1[o]); m1[o] = fmaf(w.y, v2, m1[o]); m1[o] = fmaf(w.z, v3, m1[o]);
+                    m[o] = fma2(wp[0], va, m[o]); m[o] = fma2(wp[1], vb, m[o]); m[o] = fma2(wp[2], vc, m[o]);
                 }
             }
         }
         const size_t p = (size_t)y * a.W + x;
 #pragma unroll
         for (int o = 0; o < HO; o++) {
-            a.mask[o * HW + p] = m0[o];
-            if (x + 1 < a.W) a.mask[o * HW + p + 1] = m1[o];
+            a.mask[o * HW + p] = m[o].x;
+            if (x + 1 < a.W) a.mask[o * HW + p + 1] = m[o].y;
         }
     }
 }
@@ -202,11 +212,14 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
 __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_bwd_h(HeadArgs a) {
     constexpr int XR = TH + 2, XC = TW + 2;
     constexpr int NP = HO * HM, G = HT / NP;    // dW2: 24 pairs x 10 row groups
-    __shared__ float xs[HC * XR * XC];   // samples, tile + 1 halo; then the dW2 row-group sums
-    __shared__ float ms[HO * XR * XC];   // dmask, tile + 1 halo (0 outside the image)
-    __shared__ float hs[HM * TH * TW];   // hidden on the tile (0 outside the image)
-    __shared__ float4 w1f[NF1], w2t[NF2];
-    __shared__ float sb1[HM], colsum[HO * TW];
+    __shared__ float4 smem[NF1 + NF2 + (HM + HO * TW + HC * XR * XC + HO * XR * XC + HM * TH * TW) / 4];
+    float4* w1f = smem;                  // weights first (immediate offsets)
+    float4* w2t = w1f + NF1;
+    float* sb1 = (float*)(w2t + NF2);
+    float* colsum = sb1 + HM;
+    float* xs = colsum + HO * TW;        // samples, tile + 1 halo; then the dW2 row-group sums
+    float* ms = xs + HC * XR * XC;       // dmask, tile + 1 halo (0 outside the image)
+    float* hs = ms + HO * XR * XC;       // hidden on the tile (0 outside the image)
     const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
     const int y0 = ty * TH, x0 = tx * TW;
     const size_t HW = (size_t)a.H * a.W;
@@ -234,28 +247,27 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
         }
         if (!in0) continue;
         // dL/dh = [h > 0] conv2^T(dmask): dh[co][q] = sum_(o, ky, kx) w2[o][co][ky][kx] dmask[o][q - (ky, kx) + 1]
-        float d0[HM], d1[HM];
+        f2 d[HM];
 #pragma unroll
-        for (int co = 0; co < HM; co++) d0[co] = d1[co] = 0.0f;
+        for (int co = 0; co < HM; co++) d[co] = (f2)(0.0f);
 #pragma unroll 1
         for (int o = 0; o < HO; o++) {
 #pragma unroll
             for (int ky = 0; ky < 3; ky++) {
                 const float* row = ms + (o * XR + r + 2 - ky) * XC + c;
-                const float m0 = row[0], m1 = row[1], m2 = row[2], m3 = row[3];
+                const f2 m21 = {row[2], row[3]}, m10 = {row[1], row[2]}, m0_ = {row[0], row[1]};
 #pragma unroll
                 for (int co = 0; co < HM; co++) {
                     const float4 w = w2t[(o * 3 + ky) * HM + co];   // kx = 0, 1, 2 read columns c + 2, c + 1, c
-                    d0[co] = fmaf(w.x, m2, d0[co]); d0[co] = fmaf(w.y, m1, d0[co]); d0[co] = fmaf(w.z, m0, d0[co]);
-                    d1[co] = fmaf(w.x, m3, d1[co]); d1[co] = fmaf(w.y, m2, d1[co]); d1[co] = fmaf(w.z, m1, d1[co]);
+                    d[co] = fma2(w.x, m21, d[co]); d[co] = fma2(w.y, m10, d[co]); d[co] = fma2(w.z, m0_, d[co]);
                 }
             }
         }
         const size_t p = (size_t)y * a.W + x;
 #pragma unroll
         for (int co = 0; co < HM; co++) {
-            a.dh[co * HW + p] = h0[co] > 0.0f ? d0[co] : 0.0f;
-            if (in1) a.dh[co * HW + p + 1] = h1[co] > 0.0f ? d1[co] : 0.0f;
+            a.dh[co * HW + p] = h0[co] > 0.0f ? d[co].x : 0.0f;
+            if (in1) a.dh[co * HW + p + 1] = h1[co] > 0.0f ? d[co].y : 0.0f;
         }
     }
     __syncthreads();
@@ -296,9 +308,10 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
 
 __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_bwd_x(HeadArgs a) {
     constexpr int XR = TH + 2, XC = TW + 2;
-    __shared__ float xs[HC * XR * XC];   // samples, tile + 1 halo
-    __shared__ float ds[HM * XR * XC];   // dh, tile + 1 halo (0 outside the image)
-    __shared__ float4 w1t[NF1];
+    __shared__ float4 smem[NF1 + (HC * XR * XC + HM * XR * XC) / 4];
+    float4* w1t = smem;                  // weights first (immediate offsets)
+    float* xs = (float*)(smem + NF1);    // samples, tile + 1 halo
+    float* ds = xs + HC * XR * XC;       // dh, tile + 1 halo (0 outside the image)
     const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
     const int y0 = ty * TH, x0 = tx * TW;
     const size_t HW = (size_t)a.H * a.W;
@@ -315,49 +328,87 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (int i = threadIdx.x; i < TH * (TW / 2); i += HT) {
         const int r = i / (TW / 2), c = 2 * (i % (TW / 2)), y = y0 + r, x = x0 + c;
         if (y >= a.H || x >= a.W) continue;
-        float d0[HC], d1[HC];
+        f2 d[HC];
 #pragma unroll
-        for (int ci = 0; ci < HC; ci++) d0[ci] = d1[ci] = 0.0f;
+        for (int ci = 0; ci < HC; ci++) d[ci] = (f2)(0.0f);
 #pragma unroll 1
         for (int co = 0; co < HM; co++) {
 #pragma unroll
             for (int ky = 0; ky < 3; ky++) {
                 const float* row = ds + (co * XR + r + 2 - ky) * XC + c;
-                const float g0 = row[0], g1 = row[1], g2 = row[2], g3 = row[3];
+                const f2 g21 = {row[2], row[3]}, g10 = {row[1], row[2]}, g0_ = {row[0], row[1]};
 #pragma unroll
                 for (int ci = 0; ci < HC; ci++) {
                     const float4 w = w1t[(co * 3 + ky) * HC + ci];   // kx = 0, 1, 2 read columns c + 2, c + 1, c
-                    d0[ci] = fmaf(w.x, g2, d0[ci]); d0[ci] = fmaf(w.y, g1, d0[ci]); d0[ci] = fmaf(w.z, g0, d0[ci]);
-                    d1[ci] = fmaf(w.x, g3, d1[ci]); d1[ci] = fmaf(w.y, g2, d1[ci]); d1[ci] = fmaf(w.z, g1, d1[ci]);
+                    d[ci] = fma2(w.x, g21, d[ci]); d[ci] = fma2(w.y, g10, d[ci]); d[ci] = fma2(w.z, g0_, d[ci]);
                 }
             }
         }
         const size_t p = (size_t)y * a.W + x;
 #pragma unroll
         for (int ci = 0; ci < HC; ci++) {
-            a.dx[ci * HW + p] = d0[ci];
-            if (x + 1 < a.W) a.dx[ci * HW + p + 1] = d1[ci];
+            a.dx[ci * HW + p] = d[ci].x;
+            if (x + 1 < a.W) a.dx[ci * HW + p + 1] = d[ci].y;
         }
     }
-    // dW1[co][ci][ky][kx] = sum over the tile of dh[co][q] sample[ci][q + (ky, kx) - 1]; db1[co] = sum dh[co]
-    // (128 pairs x 2 row groups; the groups' sums in order through LDS, reusing xs once every thread is past it)
-    constexpr int NP = HM * HC, G = HT / NP;
-    const int t = threadIdx.x, pr = t % NP, grp = t / NP;
-    const int co = pr / HC, ci = pr % HC;
-    float acc[9], bacc;
-    window_sums(xs + ci * XR * XC, XC, ds + co * XR * XC + XC + 1, XC, grp, G, acc, bacc);
+    // dW1[co][ci][ky][kx] = sum over the tile of dh[co][q] sample[ci][q + (ky, kx) - 1]; db1[co] = sum dh[co].
+    // A thread owns one input x four hidden channels (3 sample + 4 dh LDS reads per 36 FMAs; one pair per thread read
+    // 1 + 3 per 9) over its group's 16-column row segments: 32 slots x 8 groups, 4 segments each; the groups' sums in
+    // order through LDS, reusing xs once every thread is past it.
+    constexpr int Q = 4, NQ = HM / Q, SLOTS = HC * NQ, G = HT / SLOTS, SEG = 16, ITEMS = TH * (TW / SEG), NV = Q * 10;
+    static_assert(G * SLOTS == HT && G * SLOTS * NV <= HC * XR * XC, "dW1 group sums fit the sample area");
+    const int t = threadIdx.x, slot = t % SLOTS, grp = t / SLOTS;
+    const int q = slot % NQ, ci = slot / NQ;
+    float acc[Q][9], bacc[Q];
+#pragma unroll
+    for (int j = 0; j < Q; j++) {
+        bacc[j] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 9; k++) acc[j][k] = 0.0f;
+    }
+    {
+        const float* xc = xs + ci * XR * XC;
+        const float* dc = ds + (q * Q) * XR * XC + XC + 1;    // the tile's dh (inside the halo)
+#pragma unroll 1
+        for (int it = grp; it < ITEMS; it += G) {
+            const int r = it / (TW / SEG), c0 = (it % (TW / SEG)) * SEG;
+            const float* x0r = xc + r * XC + c0;
+            float w00 = x0r[0], w01 = x0r[1];
+            float w10 = x0r[XC], w11 = x0r[XC + 1];
+            float w20 = x0r[2 * XC], w21 = x0r[2 * XC + 1];
+            const float* dr = dc + r * XC + c0;
+#pragma unroll 4
+            for (int c = 0; c < SEG; c++) {
+                const float w02 = x0r[c + 2], w12 = x0r[XC + c + 2], w22 = x0r[2 * XC + c + 2];
+#pragma unroll
+                for (int j = 0; j < Q; j++) {
+                    const float g = dr[j * XR * XC + c];
+                    acc[j][0] = fmaf(g, w00, acc[j][0]); acc[j][1] = fmaf(g, w01, acc[j][1]);
+                    acc[j][2] = fmaf(g, w02, acc[j][2]); acc[j][3] = fmaf(g, w10, acc[j][3]);
+                    acc[j][4] = fmaf(g, w11, acc[j][4]); acc[j][5] = fmaf(g, w12, acc[j][5]);
+                    acc[j][6] = fmaf(g, w20, acc[j][6]); acc[j][7] = fmaf(g, w21, acc[j][7]);
+                    acc[j][8] = fmaf(g, w22, acc[j][8]);
+                    bacc[j] += g;
+                }
+                w00 = w01; w01 = w02; w10 = w11; w11 = w12; w20 = w21; w21 = w22;
+            }
+        }
+    }
     __syncthreads();
     float* red = xs;
 #pragma unroll
-    for (int k = 0; k < 9; k++) red[(grp * NP + pr) * 10 + k] = acc[k];
-    red[(grp * NP + pr) * 10 + 9] = bacc;
+    for (int j = 0; j < Q; j++) {
+#pragma unroll
+        for (int k = 0; k < 9; k++) red[(grp * SLOTS + slot) * NV + j * 10 + k] = acc[j][k];
+        red[(grp * SLOTS + slot) * NV + j * 10 + 9] = bacc[j];
+    }
     __syncthreads();
     float* prow = a.part + (size_t)blockIdx.x * NPART;
-    for (int i = t; i < NP * 10; i += HT) {
-        const int p = i / 10, k = i % 10;
-        float v = red[p * 10 + k];
-        for (int gg = 1; gg < G; gg++) v += red[(gg * NP + p) * 10 + k];
-        const int pco = p / HC, pci = p % HC;
+    for (int i = t; i < SLOTS * NV; i += HT) {
+        const int sl = i / NV, e = i % NV, j = e / 10, k = e % 10;
+        const int pci = sl / NQ, pco = (sl % NQ) * Q + j;
+        float v = red[i];
+        for (int gg = 1; gg < G; gg++) v += red[gg * SLOTS * NV + i];
         if (k < 9) prow[P_W1 + (pco * HC + pci) * 9 + k] = v;
         else if (pci == 0) prow[P_B1 + pco] = v;
     }
@@ -417,8 +468,8 @@ int mask_head_tiles(int H, int W) { return ((W + TW - 1) / TW) * ((H + TH - 1) /
 int mask_head_nparams() { return NPART; }
 
 void launch_mask_head_fwd(HeadArgs a, hipStream_t st) {
-    a.tiles_x = (a.W + TW - 1) / TW;
-    a.tiles_y = (a.H + TH - 1) / TH;
+    a.tiles_x = (a.W + FTW - 1) / FTW;
+    a.tiles_y = (a.H + FTH - 1) / FTH;
     k_head_fwd<<<a.tiles_x * a.tiles_y, HT, 0, st>>>(a);
 }
 

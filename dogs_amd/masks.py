@@ -2,8 +2,10 @@
 (conerf/model/gaussian_fields/masks.py:8-54; gaussian_trainer.py:171-183 build, :232-235 its Adam, :392-401 the masked
 loss, :482-484 the step).
 
-The network is small and convolutional -- torch (MIOpen) runs it; what the hot path needs from it is the [3, H, W] mask
-the photometric term multiplies the render with.  The native training step (dg_train_step) takes that mask and returns
+The network is small and convolutional; on the GPU its 3x3 convolutions run on the library's kernels (Conv3x3:
+dg_conv3x3 / dg_conv3x3_wgrad) and its full-resolution head on dg_mask_head_* (fixed-order sums, so the same bits in
+every process), the rest is torch.  What the hot path needs from it is the [3, H, W] mask the photometric term
+multiplies the render with.  The native training step (dg_train_step) takes that mask and returns
 dL/dmask, and the trainer back-propagates it through this module (`MaskedStep`).
 
 Parameter names and shapes follow the reference module, so its state dicts load unchanged: `appearance_embedding`
@@ -15,24 +17,11 @@ bilinearly resized to the full image size, and mapped to three channels without 
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 import torch.nn.functional as F
 from torch import nn
 
-
-
-def ensure_fast_find_mode() -> None:
-    """MIOpen's default find mode times candidate kernels on first use, so processes sharing a GPU (the ADMM ranks of
-    one box, or a run next to another job) can pick different convolution algorithms for the same problem and round
-    differently: the masked pre-phase then drifts between ranks and the sequential baseline from the first iteration
-    (tools/mask_conc_probe.py: four concurrent processes differ at iteration 1; with FAST, bit-identical).  FAST takes
-    the find-db or the immediate-mode heuristic, never a timing.  Called when an AppearanceEmbedding is built (before
-    its first convolution; not at import: ADVICE r5) and by the entry points (admm_run.main, bench.py) before anything
-    touches the GPU; an explicit MIOPEN_FIND_MODE wins.  MIOpen reads it when its handle is created, so a process
-    that ran a convolution before building the embedding keeps its earlier mode."""
-    os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
 
 
 EMBEDDING_DIM = 64
@@ -45,57 +34,73 @@ def _conv3(cin: int, cout: int) -> nn.Conv2d:
 
 
 class Conv3x3(nn.Conv2d):
-    """nn.Conv2d(cin, cout, 3, padding=1) -- the same parameters and forward -- whose backward takes the weight and
-    bias gradients from dg_conv3x3_wgrad (a fixed-order reduction, no atomics) when the library supports the channel
-    counts.  MIOpen's deterministic weight-gradient algorithm for the embedding's full-resolution convolutions (a
-    Winograd WrW kernel) takes 83 ms per 1080p call, 200 ms per masked iteration; its fast ones use atomics.  The input
-    gradient stays MIOpen's (im2col GEMM + col2im: deterministic)."""
+    """nn.Conv2d(cin, cout, 3, padding=1) -- the same parameters -- whose forward and backward on the GPU are the
+    library's: dg_conv3x3 (the forward, and the input gradient as its adjoint) and dg_conv3x3_wgrad (weight and bias
+    gradients), each a fixed-order sum with no atomics.  So the embedding is bitwise the same in every process: MIOpen
+    picks its algorithm per process from its find database and what ran before (the masked ADMM ranks differed from the
+    sequential baseline after other convolutions had run in the baseline's process, gpurun_out/det1), and its
+    deterministic weight-gradient algorithm for the full-resolution convolutions took 83 ms per 1080p call."""
 
     def __init__(self, cin: int, cout: int) -> None:
         super().__init__(cin, cout, kernel_size=3, padding=1)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if x.is_cuda and _native_wgrad(self.in_channels, self.out_channels):
+        if x.is_cuda:
             return _Conv3x3Fn.apply(x, self.weight, self.bias)
         return super().forward(x)
 
 
-def _native_wgrad(cin: int, cout: int) -> bool:
-    return cin * cout <= 4096
+def _conv3x3(L, x4: torch.Tensor, w: torch.Tensor, b, cout: int, adjoint: bool) -> torch.Tensor:
+    """dg_conv3x3 over each image of x4 [N, C, H, W] (float32, contiguous)."""
+    from . import _lib
+    n, _, H, W = (int(v) for v in x4.shape)
+    cin_w, cout_w = int(w.shape[1]), int(w.shape[0])
+    y = torch.empty((n, cout, H, W), dtype=torch.float32, device=x4.device)
+    with _lib.device_ctx(x4.device):
+        st = _lib.stream_of(x4.device)
+        for i in range(n):
+            _lib.check(L.dg_conv3x3(cin_w, cout_w, H, W, x4[i].data_ptr(), w.data_ptr(),
+                                    b.data_ptr() if b is not None else None, y[i].data_ptr(), int(adjoint), st))
+    return y
 
 
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
-        ctx.save_for_backward(x, weight)
+        from . import _lib
+        if x.dtype != torch.float32 or weight.dtype != torch.float32:
+            raise TypeError("Conv3x3 on the GPU takes float32")
+        x4 = (x if x.dim() == 4 else x.unsqueeze(0)).contiguous()
+        w = weight.contiguous()
+        b = bias.contiguous() if bias is not None else None
+        ctx.save_for_backward(x4, w)
         ctx.has_bias = bias is not None
-        return F.conv2d(x, weight, bias, padding=1)
+        ctx.batched = x.dim() == 4
+        y = _conv3x3(_lib.load(), x4, w, b, int(w.shape[0]), False)
+        return y if ctx.batched else y[0]
 
     @staticmethod
     def backward(ctx, g):
         from . import _lib
-        x, w = ctx.saved_tensors
-        x4 = x if x.dim() == 4 else x.unsqueeze(0)
+        x4, w = ctx.saved_tensors
+        L = _lib.load()
         g4 = (g if g.dim() == 4 else g.unsqueeze(0)).contiguous()
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = torch.ops.aten.convolution_backward(g4, x4, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
-                                                     [True, False, False])[0]
-            dx = dx if x.dim() == 4 else dx[0]
+            dx = _conv3x3(L, g4, w, None, int(w.shape[1]), True)
+            dx = dx if ctx.batched else dx[0]
         dw = db = None
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             cout, cin = int(w.shape[0]), int(w.shape[1])
             dw = torch.empty_like(w)
             db = torch.empty(cout, dtype=torch.float32, device=w.device)
-            xc = x4.contiguous()
-            L = _lib.load()
             for b in range(int(x4.shape[0])):    # one image per call, summed in batch order
                 H, W = int(x4.shape[2]), int(x4.shape[3])
                 nbytes = int(L.dg_conv3x3_wgrad_scratch_bytes(cin, cout, H, W))
                 scratch = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=w.device)
                 dwb, dbb = (dw, db) if b == 0 else (torch.empty_like(dw), torch.empty_like(db))
                 with _lib.device_ctx(w.device):
-                    _lib.check(L.dg_conv3x3_wgrad(cin, cout, H, W, xc[b].data_ptr(), g4[b].data_ptr(), dwb.data_ptr(),
+                    _lib.check(L.dg_conv3x3_wgrad(cin, cout, H, W, x4[b].data_ptr(), g4[b].data_ptr(), dwb.data_ptr(),
                                                   dbb.data_ptr(), scratch.data_ptr(), nbytes,
                                                   _lib.stream_of(w.device)))
                 if b:
@@ -107,7 +112,6 @@ class _Conv3x3Fn(torch.autograd.Function):
 class AppearanceEmbedding(nn.Module):
     def __init__(self, num_views: int, embedding_dim: int = EMBEDDING_DIM) -> None:
         super().__init__()
-        ensure_fast_find_mode()
         self.appearance_embedding = nn.Parameter(torch.zeros(num_views, embedding_dim))
         self.fusion = _conv3(embedding_dim + 3, _STAGE_CHANNELS[0])
         stages = []
@@ -239,15 +243,6 @@ class _ResizeBilinear(torch.autograd.Function):
         return gx, None
 
 
-def deterministic_convs():
-    """Context for the embedding's forward and backward: MIOpen restricted to its deterministic convolution
-    algorithms (tools/det_probe.py: without it the weight gradients of the upsampling and output convolutions differ run
-    to run; with it they are bitwise repeatable), every other cuDNN/MIOpen flag left as it is.  The flag is global
-    state, so it also covers the backward the autograd engine runs on its device thread while the caller waits."""
-    cd = torch.backends.cudnn
-    return cd.flags(enabled=cd.enabled, benchmark=cd.benchmark, deterministic=True, allow_tf32=cd.allow_tf32)
-
-
 def resize_bilinear(x: torch.Tensor, size: tuple) -> torch.Tensor:
     """[C, h, w] -> [C, H, W] bilinear (align_corners=False), deterministic backward (_ResizeBilinear)."""
     return _ResizeBilinear.apply(x, size)
@@ -284,8 +279,7 @@ class MaskedStep:
     def forward(self, k: int, gt: torch.Tensor, index: int) -> tuple:
         """(mask [3,H,W] contiguous, dmask buffer of the same shape) for view k."""
         H, W = int(gt.shape[1]), int(gt.shape[2])
-        with deterministic_convs():
-            self.mask = self.net(self.small_target(k, gt), index, (H, W))
+        self.mask = self.net(self.small_target(k, gt), index, (H, W))
         buf = self.dmask.get((H, W))
         if buf is None:
             buf = self.dmask[(H, W)] = torch.empty((3, H, W), dtype=torch.float32, device=gt.device)
@@ -296,8 +290,7 @@ class MaskedStep:
         return m, buf
 
     def backward_and_step(self, dmask: torch.Tensor) -> None:
-        with deterministic_convs():
-            self.mask.backward(dmask)
+        self.mask.backward(dmask)
         self.opt.step()
         self.opt.zero_grad(set_to_none=True)
         self.mask = self._m = None

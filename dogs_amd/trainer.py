@@ -366,12 +366,7 @@ class GaussianSplatTrainer:
             log = IterationLog(self.iteration, "native", self.model.num_gaussians)
         else:
             self.sync()
-            if self.mask is not None:   # the embedding's convolutions on MIOpen's deterministic algorithms
-                from .masks import deterministic_convs
-                with deterministic_convs():
-                    self._autograd_iteration(k, ev, res)
-            else:
-                self._autograd_iteration(k, ev, res)
+            self._autograd_iteration(k, ev, res)
             log = IterationLog(self.iteration, "autograd", self.model.num_gaussians, ev)
         self.logs.append(log)
         return log

@@ -1,16 +1,18 @@
 """The appearance embedding's kernels (masks.py:8-54, the geometry.mask of mipnerf360.yaml / urban3d_admm.yaml;
-DESIGN.md §3): dg_conv3x3_wgrad, the weight / bias gradient of its 3x3 convolutions (MIOpen's backward-weights call
-replaced), and dg_mask_head_*, its full-resolution head (resize -> conv 16 -> 8 -> ReLU -> conv 8 -> 3) fused.
+DESIGN.md §3): dg_conv3x3 (its 3x3 convolutions' forward and input gradient) and dg_conv3x3_wgrad (weight / bias
+gradient) -- MIOpen's calls replaced -- and dg_mask_head_*, its full-resolution head (resize -> conv 16 -> 8 -> ReLU ->
+conv 8 -> 3) fused.
 
 * against a float64 reference (nine shifted float64 GEMMs on the device) at the embedding's real shapes -- the
   full-resolution 16 -> 8 and 8 -> 3 convolutions at 1920 x 1080, the upsampling stages 8 -> 16 at 544 x 960, 16 -> 32 at
   272 x 480, 32 -> 64 at 136 x 240 -- and at ragged ones (1 x 1 images, widths and heights off the 64 x TR tiles):
   norm-wise relative error < 1e-5 (the fp32 sums of 2M products), and within 1e-4 of MIOpen's fp32 result;
 * deterministic: two calls are bit-identical;
+* dg_conv3x3's forward and adjoint against float64 at the same shapes, 1e-5;
 * the head against torch's float64 resize + convolutions with autograd, up- and downsampling and ragged sizes, 1e-5;
   its backward bitwise repeatable;
 * the module: AppearanceEmbedding's mask and gradients (fused head, Conv3x3) against the same network through torch's
-  own ops within 1e-5 / 1e-4; unsupported channel counts (fusion 67 -> 256) keep MIOpen's path.
+  own ops within 1e-5 / 1e-4, and bitwise repeatable.
 """
 import numpy as np
 import pytest
@@ -20,6 +22,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 SHAPES = [(16, 8, 1080, 1920), (8, 3, 1080, 1920), (8, 16, 544, 960), (16, 32, 272, 480), (32, 64, 136, 240),
+          (67, 256, 34, 60), (64, 128, 68, 120), (19, 33, 20, 70),
           (3, 5, 17, 70), (1, 1, 1, 1), (7, 9, 33, 65), (2, 3, 5, 129)]
 
 
@@ -74,10 +77,81 @@ def test_wgrad_matches_float64(hip_device, cin, cout, H, W):
 def test_unsupported_channels_are_an_error(hip_device):
     from dogs_amd import _lib
     L = _lib.load()
-    assert L.dg_conv3x3_wgrad(67, 256, 8, 8, 1, 1, 1, 1, 1, 1 << 30, None) != 0
+    assert L.dg_conv3x3_wgrad(5000, 2, 8, 8, 1, 1, 1, 1, 1, 1 << 30, None) != 0
+    assert L.dg_conv3x3(0, 2, 8, 8, 1, 1, None, 1, 0, None) != 0
 
 
-def _torch_embedding(net, img, index, size):
+def _conv(x, w, b, adjoint):
+    from dogs_amd import _lib
+    L = _lib.load()
+    cout, cin = w.shape[:2]
+    _, H, W = x.shape
+    y = torch.full(((cin if adjoint else cout), H, W), float("nan"), device=x.device)
+    _lib.check(L.dg_conv3x3(cin, cout, H, W, x.data_ptr(), w.data_ptr(), b.data_ptr() if b is not None else None,
+                            y.data_ptr(), int(adjoint), _lib.stream_of(x.device)))
+    return y
+
+
+def _conv64(x, w, b, adjoint):
+    """float64 shifted GEMMs: the forward y = b + sum_k W_k X_k, or the input gradient of dy = x."""
+    cout, cin = w.shape[:2]
+    _, H, W = x.shape
+    wd, xd = w.double(), x.double()
+    if not adjoint:
+        xp = F.pad(xd, (1, 1, 1, 1))
+        y = torch.zeros((cout, H * W), dtype=torch.float64, device=x.device)
+        for ky in range(3):
+            for kx in range(3):
+                y += wd[:, :, ky, kx] @ xp[:, ky:ky + H, kx:kx + W].reshape(cin, -1)
+        if b is not None:
+            y += b.double()[:, None]
+        return y.reshape(cout, H, W)
+    dxp = torch.zeros((cin, H + 2, W + 2), dtype=torch.float64, device=x.device)
+    g = xd.reshape(cout, -1)
+    for ky in range(3):
+        for kx in range(3):
+            dxp[:, ky:ky + H, kx:kx + W] += (wd[:, :, ky, kx].T @ g).reshape(cin, H, W)
+    return dxp[:, 1:H + 1, 1:W + 1]
+
+
+@pytest.mark.parametrize("cin,cout,H,W", SHAPES + [(256, 67, 34, 60), (3, 67, 9, 64), (8, 24, 40, 130)])
+def test_conv_and_its_adjoint_match_float64(hip_device, cin, cout, H, W):
+    """dg_conv3x3's forward (with and without bias) and adjoint against float64: the embedding's shapes (fusion
+    67 -> 256 at 34 x 60 and its adjoint, every upsampling stage, the full-resolution convolutions when the fused head
+    does not apply) and ragged ones -- 1 x 1, channel counts off the 8-channel groups (67, 33, 5, 3), rows and columns
+    off the tiles.  Norm-wise 1e-5 (fp32 sums of up to 2304 products); bit-identical on a second call; every output
+    written (NaN-filled before)."""
+    gen = torch.Generator(device=hip_device).manual_seed(cin * 17 + cout * 5 + W)
+    x = torch.randn((cin, H, W), generator=gen, device=hip_device)
+    w = torch.randn((cout, cin, 3, 3), generator=gen, device=hip_device) / (3 * cin ** 0.5)
+    b = torch.randn(cout, generator=gen, device=hip_device)
+    g = torch.randn((cout, H, W), generator=gen, device=hip_device)
+    for bias in (b, None):
+        y = _conv(x, w, bias, False)
+        assert torch.isfinite(y).all()
+        assert _rel(y, _conv64(x, w, bias, False)) < 1e-5
+        assert torch.equal(y, _conv(x, w, bias, False))
+    dx = _conv(g, w, None, True)
+    assert torch.isfinite(dx).all()
+    assert _rel(dx, _conv64(g, w, None, True)) < 1e-5
+    assert torch.equal(dx, _conv(g, w, None, True))
+
+
+def _resize64(x, size):
+    """Bilinear resize (align_corners=False) of x [C, h, w] in float64 arithmetic with the float32 source indices and
+    weights of torch's float32 kernel (its weight matrices, read off by resizing one-hot images in float32): the
+    reference the float32 routes are measured against.  (torch's float64 kernel computes the indices in float64, and
+    the 1e-7 index difference, scaled by the gradients, swamped the summation error being measured.)"""
+    _, h, w = x.shape
+    H, W = size
+    eh = torch.eye(h, device=x.device).reshape(1, h, h, 1)
+    ew = torch.eye(w, device=x.device).reshape(1, w, 1, w)
+    ry = F.interpolate(eh, size=(H, 1), mode="bilinear")[0, :, :, 0].T.double()    # [H, h]
+    rx = F.interpolate(ew, size=(1, W), mode="bilinear")[0, :, 0, :].T.double()    # [W, w]
+    return torch.einsum("yi,cij,xj->cyx", ry, x, rx)
+
+
+def _torch_embedding(net, img, index, size, resize=None):
     """AppearanceEmbedding.forward through torch's own ops (nn.Conv2d / F.interpolate / F.conv2d), same parameters."""
     _, h, w = img.shape
     code = net.appearance_embedding[index]
@@ -85,32 +159,48 @@ def _torch_embedding(net, img, index, size):
     x = F.conv2d(x, net.fusion.weight, net.fusion.bias, padding=1)
     for st in net.upsample:
         x = F.relu(F.conv2d(F.pixel_shuffle(x[None], 2)[0], st[1].weight, st[1].bias, padding=1))
-    x = F.interpolate(x[None], size=size, mode="bilinear")[0]
+    x = resize(x, size) if resize else F.interpolate(x[None], size=size, mode="bilinear")[0]
     x = F.relu(F.conv2d(x, net.out_conv[0].weight, net.out_conv[0].bias, padding=1))
     return F.conv2d(x, net.out_conv[2].weight, net.out_conv[2].bias, padding=1)
 
 
-@pytest.mark.parametrize("size", [(1080, 1920), (540, 960)])
-def test_embedding_gradients_match_torch(hip_device, size):
-    """The module (fused head + Conv3x3 weight gradients) against the same network through torch's ops: the mask
-    within 1e-5, every parameter gradient within 1e-4 (norm-wise)."""
+@pytest.mark.parametrize("img_hw,size", [((34, 60), (1080, 1920)), ((34, 60), (540, 960)), ((2, 2), (150, 140))])
+def test_embedding_gradients_match_torch(hip_device, img_hw, size):
+    """The module (fused head, Conv3x3 on dg_conv3x3 / dg_conv3x3_wgrad) against the same network in float64 (with
+    float32 resize weights, _resize64) through torch's ops: the mask and every parameter gradient within twice the
+    error of torch's own float32 route (MIOpen) or 1e-5 norm-wise, whichever is larger.  The last case upsamples more
+    than 4x, so the head runs unfused (resize + Conv3x3)."""
+    import copy
     from dogs_amd.masks import AppearanceEmbedding
     torch.manual_seed(3)
     net = AppearanceEmbedding(4).to(hip_device)
     with torch.no_grad():
         net.appearance_embedding.normal_(0.0, 0.3)
-    img = torch.rand((3, 34, 60), device=hip_device)
+    net64 = copy.deepcopy(net).double()
+    img = torch.rand((3,) + img_hw, device=hip_device)
     g = torch.randn((3,) + size, generator=torch.Generator(device=hip_device).manual_seed(9), device=hip_device)
     outs = []
-    for route in ("module", "torch"):
-        net.zero_grad(set_to_none=True)
-        y = net(img, 2, size) if route == "module" else _torch_embedding(net, img, 2, size)
-        (y * g).sum().backward()
-        outs.append((y.detach(), {k: p.grad.clone() for k, p in net.named_parameters()}))
-    (y0, g0), (y1, g1) = outs
-    assert _rel(y0, y1) < 1e-5, _rel(y0, y1)
+    for route in ("module", "torch", "float64"):
+        m = net64 if route == "float64" else net
+        m.zero_grad(set_to_none=True)
+        if route == "module":
+            y = net(img, 2, size)
+        else:
+            y = _torch_embedding(m, img.double() if route == "float64" else img, 2, size,
+                                 _resize64 if route == "float64" else None)
+        (y * (g.double() if route == "float64" else g)).sum().backward()
+        outs.append((y.detach(), {k: p.grad.clone() for k, p in m.named_parameters()}))
+    (y0, g0), (y1, g1), (y64, g64) = outs
+    assert _rel(y0, y64) <= max(2 * _rel(y1, y64), 1e-5), (_rel(y0, y64), _rel(y1, y64))
     for k in g0:
-        assert _rel(g0[k], g1[k]) < 1e-4, (k, _rel(g0[k], g1[k]))
+        e0, e1 = _rel(g0[k], g64[k]), _rel(g1[k], g64[k])
+        print(f"{k}: module {e0:.3g}, torch fp32 {e1:.3g} from float64")
+        assert e0 <= max(2 * e1, 1e-5), (k, e0, e1)
+    # bitwise repeatable (the ADMM ranks and the sequential baseline rely on it): every parameter's gradient again
+    net.zero_grad(set_to_none=True)
+    (net(img, 2, size) * g).sum().backward()
+    for k, p in net.named_parameters():
+        assert torch.equal(p.grad, g0[k]), k
 
 
 def _head(u, w1, b1, w2, b2, size):
@@ -119,7 +209,7 @@ def _head(u, w1, b1, w2, b2, size):
 
 
 def _head64(u, w1, b1, w2, b2, size):
-    x = F.interpolate(u[None].double(), size=size, mode="bilinear")[0]
+    x = _resize64(u.double(), size)
     h = F.relu(F.conv2d(x, w1.double(), b1.double(), padding=1))
     return F.conv2d(h, w2.double(), b2.double(), padding=1)
 
@@ -127,10 +217,10 @@ def _head64(u, w1, b1, w2, b2, size):
 @pytest.mark.parametrize("uh,uw,H,W", [(544, 960, 1080, 1920), (48, 80, 77, 131), (544, 960, 540, 960),
                                        (544, 960, 270, 480), (3, 5, 9, 17)])
 def test_mask_head_matches_float64(hip_device, uh, uw, H, W):
-    """dg_mask_head_forward / _backward (resize -> conv 16 -> 8 -> ReLU -> conv 8 -> 3) against torch's float64
-    resize and convolutions with autograd: the mask within 5e-5 (the resize's source indices are float32 arithmetic
-    in both torch's fp32 kernel and this one, scale (d + 0.5) - 0.5: ~1e-7 relative, amplified by |dU|), du and dW1
-    within 5e-5 for the same reason, db1, dW2, db2 within 1e-5 (norm-wise); the backward bitwise repeatable.  The hidden biases put every pre-activation of
+    """dg_mask_head_forward / _backward (resize -> conv 16 -> 8 -> ReLU -> conv 8 -> 3) against float64 resize (with
+    torch's float32 source indices and weights, which this kernel computes the same way: _resize64) and convolutions
+    with autograd: the mask and every gradient within 1e-5 norm-wise; the backward bitwise repeatable.  The hidden
+    biases put every pre-activation of
     channels 0-5 far above 0 and of 6-7 far below it, so fp32 and fp64 take the same ReLU branch everywhere (a
     pre-activation within rounding of 0 flips between any two summation orders) and both branches are checked."""
     gen = torch.Generator(device=hip_device).manual_seed(uh + W)
@@ -147,15 +237,14 @@ def test_mask_head_matches_float64(hip_device, uh, uw, H, W):
     ref = [t.clone().double().requires_grad_(True) for t in (u, w1, b1, w2, b2)]
     m64 = _head64(*ref, (H, W))
     m64.backward(dm.double())
-    assert _rel(m, m64) < 5e-5, _rel(m, m64)
+    assert _rel(m, m64) < 1e-5, _rel(m, m64)
     for name, a, b in zip(("du", "dw1", "db1", "dw2", "db2"), got, ref):
         if name == "db1":     # channels 6-7 are dead: their bias gradient is exactly 0 on both
             assert torch.equal(a[6:], torch.zeros_like(a[6:])) and float(b.grad[6:].abs().max()) == 0.0
             a, b = a[:6], b.grad[:6]
         else:
             b = b.grad
-        # du and dW1 carry the resize weights' float32 rounding, as the mask does
-        assert _rel(a, b) < (5e-5 if name in ("du", "dw1") else 1e-5), (name, _rel(a, b))
+        assert _rel(a, b) < 1e-5, (name, _rel(a, b))
     for t in leaves:
         t.grad = None
     _head(*leaves, (H, W)).backward(dm)

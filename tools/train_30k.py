@@ -255,16 +255,11 @@ def main():
     ap.add_argument("--fx", type=float, default=1000.0)
     ap.add_argument("--views", type=int, default=24)
     ap.add_argument("--mask", choices=("yaml", "off"), default="yaml", help="off: geometry.mask false (probe only)")
-    ap.add_argument("--mask-det", type=int, default=1, help="0: MIOpen's default algorithms for the mask CNN (probe)")
     args = ap.parse_args()
     assert torch.cuda.is_available(), "needs a HIP device"
     dev = torch.device("cuda:0")
     import dogs_amd._lib as L
     L.load()
-    if not args.mask_det:
-        import contextlib
-        import dogs_amd.masks as MK
-        MK.deterministic_convs = contextlib.nullcontext
     rec = run_compare(args, dev) if args.compare else run_full(args, dev)
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     with open(args.out, "w") as f:
