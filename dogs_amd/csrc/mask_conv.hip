@@ -22,6 +22,75 @@
 namespace gs {
 namespace {
 
+// q / d for the small q and d of the staging loops (q, d < 2^16): one multiply-high with m = ceil(2^32 / d).  The
+// staging loops issue their loads back to back (unrolled, no loop-carried index), which a runtime division or a
+// stepped index kept them from: staged one dependent load at a time, the staging took 2-3x the arithmetic.
+__host__ inline uint32_t div_magic(uint32_t d) { return (uint32_t)((((uint64_t)1 << 32) + d - 1) / d); }
+__device__ __forceinline__ int div_m(int q, uint32_t m) { return (int)__umulhi((uint32_t)q, m); }
+
+// Stage nrows image rows into LDS, one row per wave and step: row q is channel ch = q / rpc (of the nvalid channels
+// from ch0; zeros past them), tile row r = q % rpc at image row gy0 + r, columns gx0 .. gx0 + ncols - 1 (ncols <= 128,
+// zeros outside the image) -> dst[ch * ch_stride + r * row_stride + c].  Two phases per batch of B rows: every load
+// from a clamped (valid) address with the out-of-image lanes zeroed by a select, then the stores -- no branch
+// between a load and the next, so the B rows' loads are in flight together.
+template <int B>
+__device__ __forceinline__ void stage_rows(const float* __restrict__ src, size_t HW, int H, int W, int ch0, int nvalid,
+                                           int gy0, int gx0, int nrows, int rpc, uint32_t m_rpc, int ncols,
+                                           float* dst, int ch_stride, int row_stride, int wave, int lane) {
+    const int gxa = gx0 + lane, gxb = gx0 + 64 + lane;
+    const bool cola = gxa >= 0 && gxa < W, colb = gxb < W;
+    const int gxac = gxa < 0 ? 0 : (gxa >= W ? W - 1 : gxa), gxbc = gxb >= W ? W - 1 : gxb;
+    for (int base = wave; base < nrows; base += 4 * B) {
+        float v0[B], v1[B];
+        uint32_t rok = 0;
+#pragma unroll
+        for (int b = 0; b < B; b++) {   // loads only: the selects wait for phase 2
+            const int q = base + 4 * b, ch = div_m(q, m_rpc), r = q - ch * rpc;
+            const int gy = gy0 + r;
+            rok |= (q < nrows && ch < nvalid && gy >= 0 && gy < H) ? (1u << b) : 0u;
+            const int chc = ch < nvalid ? ch : nvalid - 1, gyc = gy < 0 ? 0 : (gy >= H ? H - 1 : gy);
+            const float* row = src + (size_t)(ch0 + chc) * HW + (size_t)gyc * W;
+            v0[b] = row[gxac];
+            v1[b] = row[gxbc];
+        }
+#pragma unroll
+        for (int b = 0; b < B; b++) {
+            const int q = base + 4 * b;
+            if (q < nrows) {
+                const int ch = div_m(q, m_rpc), r = q - ch * rpc;
+                float* d = dst + ch * ch_stride + r * row_stride;
+                const bool ok = (rok >> b) & 1u;
+                if (lane < ncols) d[lane] = ok && cola ? v0[b] : 0.0f;
+                if (64 + lane < ncols) d[64 + lane] = ok && colb ? v1[b] : 0.0f;
+            }
+        }
+    }
+}
+
+// Stage the weights of input channels c0 .. c0 + nc - 1 for output channels cob .. cob + 2^lg_nco - 1 as
+// wl[(ci 9 + k) 2^lg_nco + co] (the adjoint reads w transposed and flipped); output channels past Cout repeat the last
+// one (their results are never stored).  Batched as stage_rows.
+template <int B, bool ADJ>
+__device__ __forceinline__ void stage_weights_kco(const float* __restrict__ w, int Cin, int Cout, int c0, int nc,
+                                                  int cob, int lg_nco, float* wl) {
+    const int nco = 1 << lg_nco, n = nc * 9 * nco;
+    for (int base = threadIdx.x; base < n; base += 256 * B) {
+        float v[B];
+#pragma unroll
+        for (int b = 0; b < B; b++) {
+            const int e = base + 256 * b, q = e >> lg_nco, co = e & (nco - 1);
+            const int ci = q / 9 < nc ? q / 9 : nc - 1, k = q - (q / 9) * 9;
+            const int o = cob + co < Cout ? cob + co : Cout - 1, i = c0 + ci;
+            v[b] = ADJ ? w[((size_t)i * Cout + o) * 9 + 8 - k] : w[((size_t)o * Cin + i) * 9 + k];
+        }
+#pragma unroll
+        for (int b = 0; b < B; b++) {
+            const int e = base + 256 * b;
+            if (e < n) wl[e] = v[b];
+        }
+    }
+}
+
 constexpr int WG_TC = 64;        // tile columns
 constexpr int WG_THREADS = 256;
 constexpr int WG_LDS_FLOATS = 16384;   // 64 KB
@@ -40,6 +109,7 @@ struct WgradShape {
     int CI, CO, nci, nco;       // chunk sizes (CO a multiple of 4) and counts
     int slots, G;               // threads per group (CI x CO / 4), groups
     int xs_stride, dy_stride;   // LDS channel strides (odd: the per-channel reads of a wave spread over the banks)
+    uint32_t m_tr2, m_tr;       // div_magic(TR + 2), div_magic(TR)
 };
 
 __host__ __device__ inline int odd_up(int v) { return v | 1; }
@@ -65,6 +135,8 @@ WgradShape wgrad_shape(int Cin, int Cout, int H, int W) {
     s.tiles_x = (W + WG_TC - 1) / WG_TC;
     s.tiles_y = (H + tr - 1) / tr;
     s.npart = Cout * Cin * 9 + Cout;
+    s.m_tr2 = div_magic(tr + 2);
+    s.m_tr = div_magic(tr);
     return s;
 }
 
@@ -83,21 +155,12 @@ __global__ void __launch_bounds__(WG_THREADS) k_conv3x3_wgrad_part(WgradShape s,
     const size_t HW = (size_t)H * W;
     const int xrow = WG_TC + 2;
     const int nx = Cin * (TR + 2) * xrow;
-    for (int i = threadIdx.x; i < nx; i += WG_THREADS) {
-        const int c = i % xrow, r = (i / xrow) % (TR + 2), ci = i / (xrow * (TR + 2));
-        const int gy = y0 + r - 1, gx = x0 + c - 1;
-        float v = 0.0f;
-        if (gy >= 0 && gy < H && gx >= 0 && gx < W) v = x[(size_t)(ci0 + ci) * HW + (size_t)gy * W + gx];
-        xs[ci * s.xs_stride + r * xrow + c] = v;
-    }
-    const int nd = s.CO * TR * WG_TC;
-    for (int i = threadIdx.x; i < nd; i += WG_THREADS) {
-        const int c = i % WG_TC, r = (i / WG_TC) % TR, co = i / (WG_TC * TR);
-        const int gy = y0 + r, gx = x0 + c;
-        float v = 0.0f;
-        if (co < Cout && gy < H && gx < W) v = dy[(size_t)(co0 + co) * HW + (size_t)gy * W + gx];
-        ds[co * s.dy_stride + r * WG_TC + c] = v;
-    }
+    // one staged row per wave and pass, (channel, row) stepped without a division (a runtime integer division per
+    // element made the staging, not the sums, the kernel's cost)
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    stage_rows<8>(x, HW, H, W, ci0, Cin, y0 - 1, x0 - 1, Cin * (TR + 2), TR + 2, s.m_tr2, xrow, xs, s.xs_stride, xrow,
+                  wv, ln);
+    stage_rows<8>(dy, HW, H, W, co0, Cout, y0, x0, s.CO * TR, TR, s.m_tr, WG_TC, ds, s.dy_stride, WG_TC, wv, ln);
     __syncthreads();
     const int nq = s.CO / WG_CQ, slots = s.slots, G = s.G;
     const int t = threadIdx.x, grp = t / slots, slot = t % slots;
@@ -164,92 +227,103 @@ __global__ void __launch_bounds__(WG_THREADS) k_conv3x3_wgrad_part(WgradShape s,
 
 // ---- the direct 3x3 convolution: forward, and the data gradient as its adjoint ----
 //
-// y[o][p] = b[o] + sum_i sum_k w(o, i, k) x[i][p + off(k)] with zero padding, summed in (i, k) order per chunk of 8
-// input channels, the chunks' sums then added in order: deterministic,
-// whatever the process (MIOpen's choice of algorithm for the same problem depends on its find database and on what
-// ran before in the process).  The adjoint reads the forward's weights transposed and flipped,
-// w'(o, i, k) = w[i][o][8 - k], so dx = conv(dy, w') with no repacked copy.
-// Mapping: a lane owns one column of R rows for 8 output channels (8R accumulators); a block's 4 waves cover WC
-// channel groups x WR row groups of one 64-column tile.  Input channels are staged 8 at a time in LDS with the halo; a
-// lane reads its 3 x (R + 2) window (conflict-free, lanes are consecutive columns) and the 72 weights of the channel,
-// which are wave-uniform (scalar loads), for 72R FMAs.
+// y[o][p] = b[o] + sum_i sum_k w(o, i, k) x[i][p + off(k)] with zero padding.  Deterministic, whatever the process
+// (MIOpen's choice of algorithm for the same problem depends on its find database and on what ran before in the
+// process).  The adjoint reads the forward's weights transposed and flipped, w'(o, i, k) = w[i][o][8 - k], so
+// dx = conv(dy, w') with no repacked copy.
+// Mapping: a lane owns one column of R rows for 8 output channels (8R accumulators).  A block's 4 waves split as
+// WC channel groups x WR row groups x KS input-channel splits over one 64-column tile.  Per round the block stages
+// 8 KS input channels with the halo and their weights for the block's 8 WC output channels in LDS; wave (wc, wr, ks)
+// sums the round's channels 8 ks .. 8 ks + 7 (3 (R + 2) input reads and 18 broadcast float4 weight reads per 72R
+// FMAs) into a round partial that is then added to its total (two-level summation: the fusion's adjoint sums 2304
+// products).  With KS > 1 the waves' totals are added in ks order through LDS.  KS splits the long input-channel
+// sums of the small low-resolution convolutions (the fusion and its adjoint at 34 x 60 have ~100-300 blocks
+// otherwise: one wave per SIMD walking 256 channels, 232 us per adjoint call).
 constexpr int CV_TC = 64, CV_CO = 8, CV_CIB = 8, CV_SROW = CV_TC + 2;
+constexpr int CV_WFLOATS = CV_CIB * 4 * 9 * CV_CO;   // weights per round: 8 KS x 9 x 8 WC with KS WC <= 4
 
 struct ConvShape {
     int Cin, Cout, H, W;    // as launched: input -> output channels
-    int WC, WR, rows;       // channel groups x row groups of waves; tile rows = WR * R
+    int WC, WR, KS, rows;   // waves: channel groups x row groups x input splits; tile rows = WR * R
     int tiles_x, tiles_y, cblocks;
+    int lg_nco;             // log2(8 WC)
+    uint32_t m_srows;       // div_magic(rows + 2)
 };
 
 template <int R, bool ADJ>
 __global__ void __launch_bounds__(256) k_conv3x3(ConvShape s, const float* __restrict__ x, const float* __restrict__ w,
                                                   const float* __restrict__ b, float* __restrict__ y) {
-    extern __shared__ float lds[];   // [CV_CIB][rows + 2][66]
+    extern __shared__ float4 lds4[];
+    float4* wl = lds4;                                  // [8 KS][9][8 WC / 4] float4
+    float* xl = reinterpret_cast<float*>(lds4 + CV_WFLOATS / 4);   // [8 KS][rows + 2][66]
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int wr = wave % s.WR, wc = wave / s.WR;
+    const int ks = wave % s.KS, wr = (wave / s.KS) % s.WR, wc = wave / (s.KS * s.WR);
     const int tx = blockIdx.x % s.tiles_x, ty = blockIdx.x / s.tiles_x;
     const int x0 = tx * CV_TC, y0 = ty * s.rows;
-    const int co0 = (blockIdx.y * s.WC + wc) * CV_CO;
+    const int cob = blockIdx.y * s.WC * CV_CO;          // the block's first output channel
     const int H = s.H, W = s.W, Cin = s.Cin, Cout = s.Cout;
     const size_t HW = (size_t)H * W;
-    const int srows = s.rows + 2, sch = srows * CV_SROW;
+    const int srows = s.rows + 2, sch = srows * CV_SROW, nco = s.WC * CV_CO, nco4 = nco / 4;
     float acc[R][CV_CO];
 #pragma unroll
     for (int r = 0; r < R; r++)
 #pragma unroll
         for (int j = 0; j < CV_CO; j++) acc[r][j] = 0.0f;
-    const bool live = co0 < Cout;
-    for (int c0 = 0; c0 < Cin; c0 += CV_CIB) {
-        const int nc = Cin - c0 < CV_CIB ? Cin - c0 : CV_CIB;
+    const bool live = cob + wc * CV_CO < Cout;
+    const int per_round = CV_CIB * s.KS;
+    for (int c0 = 0; c0 < Cin; c0 += per_round) {
+        const int nc = Cin - c0 < per_round ? Cin - c0 : per_round;
         if (c0) __syncthreads();
-        for (int row = wave; row < nc * srows; row += 4) {   // one staged row of 66 per wave and pass
-            const int ci = row / srows, r = row - ci * srows;
-            const int gy = y0 + r - 1;
-            float* dst = lds + ci * sch + r * CV_SROW;
-            float v0 = 0.0f, v1 = 0.0f;
-            if (gy >= 0 && gy < H) {
-                const float* src = x + (size_t)(c0 + ci) * HW + (size_t)gy * W;
-                const int gx = x0 + lane - 1, gx1 = x0 + CV_TC - 1 + lane;
-                if (gx >= 0 && gx < W) v0 = src[gx];
-                if (lane < 2 && gx1 < W) v1 = src[gx1];
-            }
-            dst[lane] = v0;
-            if (lane < 2) dst[CV_TC + lane] = v1;
-        }
+        stage_rows<8>(x, HW, H, W, c0, nc, y0 - 1, x0 - 1, nc * srows, srows, s.m_srows, CV_SROW, xl, sch, CV_SROW,
+                      wave, lane);
+        stage_weights_kco<4, ADJ>(w, Cin, Cout, c0, nc, cob, s.lg_nco, reinterpret_cast<float*>(wl));
         __syncthreads();
         if (!live) continue;
-        float part[R][CV_CO];   // the chunk's sum, then added to the total: two-level summation (the fusion's
-                                // adjoint sums 2304 products; one running sum lost ~2x against MIOpen's GEMM)
+        const int cb = ks * CV_CIB, ce = nc < cb + CV_CIB ? nc : cb + CV_CIB;
+        float part[R][CV_CO];
 #pragma unroll
         for (int r = 0; r < R; r++)
 #pragma unroll
             for (int j = 0; j < CV_CO; j++) part[r][j] = 0.0f;
 #pragma unroll 1
-        for (int ci = 0; ci < nc; ci++) {
-            const float* l = lds + ci * sch + wr * R * CV_SROW + lane;
+        for (int ci = cb; ci < ce; ci++) {
+            const float* l = xl + ci * sch + wr * R * CV_SROW + lane;
             float v[R + 2][3];
 #pragma unroll
             for (int rr = 0; rr < R + 2; rr++)
 #pragma unroll
                 for (int kx = 0; kx < 3; kx++) v[rr][kx] = l[rr * CV_SROW + kx];
-            const int i = c0 + ci;
+            const float4* wk = wl + ci * 9 * nco4 + wc * 2;
 #pragma unroll
-            for (int j = 0; j < CV_CO; j++) {
-                const int o = co0 + j < Cout ? co0 + j : Cout - 1;
-                float wk[9];
-#pragma unroll
-                for (int k = 0; k < 9; k++)
-                    wk[k] = ADJ ? w[((size_t)i * Cout + o) * 9 + 8 - k] : w[((size_t)o * Cin + i) * 9 + k];
+            for (int k = 0; k < 9; k++) {
+                const float4 wa = wk[k * nco4], wb = wk[k * nco4 + 1];
+                const float wj[CV_CO] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
 #pragma unroll
                 for (int r = 0; r < R; r++)
 #pragma unroll
-                    for (int k = 0; k < 9; k++) part[r][j] = fmaf(v[r + k / 3][k % 3], wk[k], part[r][j]);
+                    for (int j = 0; j < CV_CO; j++) part[r][j] = fmaf(v[r + k / 3][k % 3], wj[j], part[r][j]);
             }
         }
 #pragma unroll
         for (int r = 0; r < R; r++)
 #pragma unroll
             for (int j = 0; j < CV_CO; j++) acc[r][j] += part[r][j];
+    }
+    if (s.KS > 1) {   // the splits' totals in ks order
+        __syncthreads();
+        float* red = xl;
+        if (live && ks > 0)
+#pragma unroll
+            for (int r = 0; r < R; r++)
+#pragma unroll
+                for (int j = 0; j < CV_CO; j++) red[wave * (R * CV_CO * 64) + (r * CV_CO + j) * 64 + lane] = acc[r][j];
+        __syncthreads();
+        if (ks > 0 || !live) return;
+        for (int q = 1; q < s.KS; q++)
+#pragma unroll
+            for (int r = 0; r < R; r++)
+#pragma unroll
+                for (int j = 0; j < CV_CO; j++) acc[r][j] += red[(wave + q) * (R * CV_CO * 64) + (r * CV_CO + j) * 64 + lane];
     }
     if (!live) return;
     const int gx = x0 + lane;
@@ -260,7 +334,7 @@ __global__ void __launch_bounds__(256) k_conv3x3(ConvShape s, const float* __res
         if (gy >= H) break;
 #pragma unroll
         for (int j = 0; j < CV_CO; j++) {
-            const int o = co0 + j;
+            const int o = cob + wc * CV_CO + j;
             if (o < Cout) y[(size_t)o * HW + (size_t)gy * W + gx] = acc[r][j] + (b ? b[o] : 0.0f);
         }
     }
@@ -273,33 +347,52 @@ bool conv3x3_supported(int Cin, int Cout, int H, int W) {
            (int64_t)H * W <= ((int64_t)1 << 31);
 }
 
+static size_t conv_lds_bytes(const ConvShape& s, int R) {
+    const size_t stage = (size_t)CV_CIB * s.KS * (s.rows + 2) * CV_SROW;
+    const size_t red = s.KS > 1 ? (size_t)4 * R * CV_CO * 64 : 0;   // one slot per wave (a group's waves are consecutive)
+    return (CV_WFLOATS + (stage > red ? stage : red)) * sizeof(float);
+}
+
 void launch_conv3x3(int Cin, int Cout, int H, int W, const float* x, const float* w, const float* b, float* y,
                     bool adjoint, hipStream_t st) {
-    ConvShape s;
-    s.Cin = Cin; s.Cout = Cout; s.H = H; s.W = W;
-    const int groups = (Cout + CV_CO - 1) / CV_CO;
-    s.WC = groups >= 4 ? 4 : groups == 3 ? 4 : groups;
-    s.WR = 4 / s.WC;
-    s.tiles_x = (W + CV_TC - 1) / CV_TC;
-    s.cblocks = (groups + s.WC - 1) / s.WC;
-    int R = 4;   // the most rows per lane that still gives >= 2 blocks per CU
-    for (; R > 1; R /= 2) {
-        const int64_t blocks = (int64_t)s.tiles_x * ((H + s.WR * R - 1) / (s.WR * R)) * s.cblocks;
-        if (blocks >= 512) break;
+    const int groups = (Cout + CV_CO - 1) / CV_CO, kmax = (Cin + CV_CIB - 1) / CV_CIB;
+    // (R, KS) candidates, most work per wave first: the first with >= 256 blocks (one per CU), else the most blocks.
+    // (>= 960 blocks, i.e. more splitting for the small low-resolution layers, measured 3% slower over the network's
+    // ten calls, >= 64 9% slower: gpurun_out/mf6.)
+    const int cand[9][2] = {{4, 1}, {4, 2}, {4, 4}, {2, 1}, {2, 2}, {2, 4}, {1, 1}, {1, 2}, {1, 4}};
+    ConvShape best{};
+    int bestR = 1;
+    int64_t best_blocks = -1;
+    for (const auto& c : cand) {
+        const int R = c[0], KS = c[1];
+        if (KS > 1 && KS > kmax) continue;
+        ConvShape s;
+        s.Cin = Cin; s.Cout = Cout; s.H = H; s.W = W; s.KS = KS;
+        const int wcmax = 4 / KS;
+        s.WC = groups >= wcmax ? wcmax : (groups == 3 ? 4 / KS : groups);
+        if (s.WC * KS > 4) s.WC = 4 / KS;
+        s.WR = 4 / (KS * s.WC);
+        s.rows = s.WR * R;
+        s.tiles_x = (W + CV_TC - 1) / CV_TC;
+        s.tiles_y = (H + s.rows - 1) / s.rows;
+        s.cblocks = (groups + s.WC - 1) / s.WC;
+        s.lg_nco = s.WC == 4 ? 5 : s.WC == 2 ? 4 : 3;
+        s.m_srows = div_magic((uint32_t)(s.rows + 2));
+        const int64_t blocks = (int64_t)s.tiles_x * s.tiles_y * s.cblocks;
+        if (blocks > best_blocks) { best = s; bestR = R; best_blocks = blocks; }
+        if (blocks >= 256) { best = s; bestR = R; break; }
     }
-    s.rows = s.WR * R;
-    s.tiles_y = (H + s.rows - 1) / s.rows;
-    const dim3 grid(s.tiles_x * s.tiles_y, s.cblocks);
-    const size_t lds = (size_t)CV_CIB * (s.rows + 2) * CV_SROW * sizeof(float);
+    const dim3 grid(best.tiles_x * best.tiles_y, best.cblocks);
+    const size_t lds = conv_lds_bytes(best, bestR);
     const float* bb = adjoint ? nullptr : b;
     if (adjoint) {
-        if (R == 4) k_conv3x3<4, true><<<grid, 256, lds, st>>>(s, x, w, bb, y);
-        else if (R == 2) k_conv3x3<2, true><<<grid, 256, lds, st>>>(s, x, w, bb, y);
-        else k_conv3x3<1, true><<<grid, 256, lds, st>>>(s, x, w, bb, y);
+        if (bestR == 4) k_conv3x3<4, true><<<grid, 256, lds, st>>>(best, x, w, bb, y);
+        else if (bestR == 2) k_conv3x3<2, true><<<grid, 256, lds, st>>>(best, x, w, bb, y);
+        else k_conv3x3<1, true><<<grid, 256, lds, st>>>(best, x, w, bb, y);
     } else {
-        if (R == 4) k_conv3x3<4, false><<<grid, 256, lds, st>>>(s, x, w, bb, y);
-        else if (R == 2) k_conv3x3<2, false><<<grid, 256, lds, st>>>(s, x, w, bb, y);
-        else k_conv3x3<1, false><<<grid, 256, lds, st>>>(s, x, w, bb, y);
+        if (bestR == 4) k_conv3x3<4, false><<<grid, 256, lds, st>>>(best, x, w, bb, y);
+        else if (bestR == 2) k_conv3x3<2, false><<<grid, 256, lds, st>>>(best, x, w, bb, y);
+        else k_conv3x3<1, false><<<grid, 256, lds, st>>>(best, x, w, bb, y);
     }
 }
 

@@ -164,18 +164,26 @@ def _torch_embedding(net, img, index, size, resize=None):
     return F.conv2d(x, net.out_conv[2].weight, net.out_conv[2].bias, padding=1)
 
 
-@pytest.mark.parametrize("img_hw,size", [((34, 60), (1080, 1920)), ((34, 60), (540, 960)), ((2, 2), (150, 140))])
-def test_embedding_gradients_match_torch(hip_device, img_hw, size):
+@pytest.mark.parametrize("img_hw,size,branches", [((34, 60), (1080, 1920), "fixed"), ((34, 60), (540, 960), "fixed"),
+                                                  ((2, 2), (150, 140), "fixed"), ((34, 60), (540, 960), "random")])
+def test_embedding_gradients_match_torch(hip_device, img_hw, size, branches):
     """The module (fused head, Conv3x3 on dg_conv3x3 / dg_conv3x3_wgrad) against the same network in float64 (with
-    float32 resize weights, _resize64) through torch's ops: the mask and every parameter gradient within twice the
-    error of torch's own float32 route (MIOpen) or 1e-5 norm-wise, whichever is larger.  The last case upsamples more
-    than 4x, so the head runs unfused (resize + Conv3x3)."""
+    float32 resize weights, _resize64) through torch's ops.  "fixed": every ReLU's biases are +-10 (channels
+    alternately live and dead) and its weights scaled by 0.1, so no pre-activation lies within rounding of 0 and float32 and float64 take the same
+    branches: the mask and every parameter gradient within 1e-5 norm-wise (~1e-6 measured, torch's float32 route
+    alike).  "random": the reference's initialisation, where a few pre-activations sit within rounding of 0 and flip
+    between any two summation orders -- both float32 routes then sit ~1e-4 from float64 (gpurun_out/cv4): within 1e-3.
+    The third case upsamples more than 4x, so the head runs unfused (resize + Conv3x3)."""
     import copy
     from dogs_amd.masks import AppearanceEmbedding
     torch.manual_seed(3)
     net = AppearanceEmbedding(4).to(hip_device)
     with torch.no_grad():
         net.appearance_embedding.normal_(0.0, 0.3)
+        if branches == "fixed":
+            for conv in [st[1] for st in net.upsample] + [net.out_conv[0]]:
+                conv.weight.mul_(0.1)   # pre-activations 10 +- 1.5 (min |pre| 8.97 in float64 at these inputs)
+                conv.bias.copy_(torch.tensor([10.0, -10.0], device=hip_device).repeat(conv.out_channels // 2))
     net64 = copy.deepcopy(net).double()
     img = torch.rand((3,) + img_hw, device=hip_device)
     g = torch.randn((3,) + size, generator=torch.Generator(device=hip_device).manual_seed(9), device=hip_device)
@@ -191,11 +199,12 @@ def test_embedding_gradients_match_torch(hip_device, img_hw, size):
         (y * (g.double() if route == "float64" else g)).sum().backward()
         outs.append((y.detach(), {k: p.grad.clone() for k, p in m.named_parameters()}))
     (y0, g0), (y1, g1), (y64, g64) = outs
-    assert _rel(y0, y64) <= max(2 * _rel(y1, y64), 1e-5), (_rel(y0, y64), _rel(y1, y64))
+    bar = 1e-5 if branches == "fixed" else 1e-3
+    assert _rel(y0, y64) < bar, (_rel(y0, y64), _rel(y1, y64))
     for k in g0:
         e0, e1 = _rel(g0[k], g64[k]), _rel(g1[k], g64[k])
         print(f"{k}: module {e0:.3g}, torch fp32 {e1:.3g} from float64")
-        assert e0 <= max(2 * e1, 1e-5), (k, e0, e1)
+        assert e0 < bar, (k, e0, e1)
     # bitwise repeatable (the ADMM ranks and the sequential baseline rely on it): every parameter's gradient again
     net.zero_grad(set_to_none=True)
     (net(img, 2, size) * g).sum().backward()
