@@ -298,9 +298,9 @@ def masked_iteration_leg(s, cams, dev, seed, iters=40, warmup=10) -> dict:
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / iters * 1e3
     out = {"ms_per_iteration": round(ms, 3), "iterations_per_s": round(1e3 / ms, 1), "iterations": iters,
-           "includes": "appearance-embedding forward (MIOpen + dg_mask_head_forward) + dg_train_step (raster fwd/bwd, "
-                       "masked L1, fused SSIM, scale regulariser, statistics, SparseGaussianAdam) + the embedding's "
-                       "backward (dg_mask_head_backward, dg_conv3x3_wgrad, MIOpen) and Adam",
+           "includes": "appearance-embedding forward (dg_conv3x3 + dg_mask_head_forward) + dg_train_step (raster "
+                       "fwd/bwd, masked L1, fused SSIM, scale regulariser, statistics, SparseGaussianAdam) + the "
+                       "embedding's backward (dg_mask_head_backward, dg_conv3x3 adjoint, dg_conv3x3_wgrad) and Adam",
            "config": "mipnerf360.yaml (geometry.mask true, lambda_mask 0, lambda_dssim 0.2, lambda_scale 0.01), "
                      "1e6 Gaussians at 1920x1080, native route"}
     del tr, m, gts

@@ -342,9 +342,9 @@ __global__ void __launch_bounds__(256) k_conv3x3(ConvShape s, const float* __res
 
 }  // namespace
 
-bool conv3x3_supported(int Cin, int Cout, int H, int W) {
-    return Cin >= 1 && Cout >= 1 && H >= 1 && W >= 1 && (int64_t)Cin * Cout <= (1 << 24) &&
-           (int64_t)H * W <= ((int64_t)1 << 31);
+bool conv3x3_supported(int Cin, int Cout, int H, int W) {   // output-channel blocks index grid.y (<= 65535)
+    return Cin >= 1 && Cout >= 1 && H >= 1 && W >= 1 && Cin <= 65536 && Cout <= 65536 &&
+           (int64_t)Cin * Cout <= (1 << 24) && (int64_t)H * W <= ((int64_t)1 << 31);
 }
 
 static size_t conv_lds_bytes(const ConvShape& s, int R) {
@@ -437,8 +437,8 @@ size_t conv3x3_wgrad_scratch_bytes(int Cin, int Cout, int H, int W) {
     return ((size_t)s.tiles_x * s.tiles_y * s.npart + rowsum_scratch_floats(s.npart)) * sizeof(float);
 }
 
-bool conv3x3_wgrad_supported(int Cin, int Cout) {
-    return Cin >= 1 && Cout >= 1 && Cin <= 4096 && Cout <= 4096;
+bool conv3x3_wgrad_supported(int Cin, int Cout) {   // the 16 x 16 channel chunks index grid.y (<= 65535)
+    return Cin >= 1 && Cout >= 1 && Cin <= 4000 && Cout <= 4000;
 }
 
 void launch_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const float* dy, float* dw, float* db,

@@ -15,7 +15,7 @@
 //   k_head_bwd_u  per stage-4 pixel: the resize's adjoint as a gather over the samples that read it, in a fixed order;
 //   launch_rowsum the tiles' partials summed per parameter in a fixed order (mask_conv.hip).
 // No atomics: bitwise repeatable for a given shape (the ADMM ranks and the sequential baseline rely on it).
-// Weights are wave-uniform: the compiler keeps them in SGPRs (scalar loads), the per-position data in LDS.
+// Weights are wave-uniform scalar loads (SGPR operands), the per-position data in LDS.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -70,38 +70,20 @@ __device__ __forceinline__ void stage_samples(const HeadArgs& a, int ry0, int rx
     }
 }
 
-// The weights, staged once per block in LDS as float4 rows {w[..][0], w[..][1], w[..][2], 0} of one (kernel row,
-// input, output) triple, in the order each product reads them (every lane reads the same row: a broadcast
-// ds_read_b128).  Read from global memory per use, they were scalar loads whose latency the block's two waves per
-// SIMD could not hide.
-//   w1f[(ci 3 + ky) 8 + co]   conv1,        w1t[(co 3 + ky) 16 + ci]  conv1^T (the input gradient)
-//   w2t[(o 3 + ky) 8 + co]    conv2^T (the forward's conv2 reads its 216 weights as scalar loads)
-constexpr int NF1 = HC * 3 * HM, NF2 = HM * 3 * HO;   // float4 rows per weight tensor
-
-__device__ __forceinline__ float4 wrow(const float* w) { return make_float4(w[0], w[1], w[2], 0.0f); }
-
+// The weights are wave-uniform: every product reads them as scalar loads (SGPR operands of v_pk_fma_f32).  Staged in
+// LDS as broadcast float4 rows they cost one LDS read per 6 FMAs and made the convolution loops LDS-issue-bound: head
+// forward 214 -> 169 us, backward 215 + 255 -> 182 + 225 us with the scalar form (gpurun_out/hw1, same box).
 // Two positions of a row at once: v_pk_fma_f32 with the weight broadcast to both halves (each half is the same fmaf
 // as the scalar form, so the bits do not change).  Left to itself the compiler paired output channels instead, and
 // spent a v_mov per weight building the pairs.
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 fma2(float w, f2 x, f2 acc) { return __builtin_elementwise_fma((f2)(w), x, acc); }
 
-template <bool CONV1, bool CONV1T, bool CONV2T>
-__device__ __forceinline__ void stage_weights(const HeadArgs& a, float4* w1f, float4* w1t, float4* w2t) {
-    for (int i = threadIdx.x; i < NF1; i += HT) {
-        if (CONV1) { const int co = i % HM, ky = (i / HM) % 3, ci = i / (3 * HM); w1f[i] = wrow(a.k1 + ((co * HC + ci) * 3 + ky) * 3); }
-        if (CONV1T) { const int ci = i % HC, ky = (i / HC) % 3, co = i / (3 * HC); w1t[i] = wrow(a.k1 + ((co * HC + ci) * 3 + ky) * 3); }
-    }
-    for (int i = threadIdx.x; i < NF2; i += HT) {
-        if (CONV2T) { const int co = i % HM, ky = (i / HM) % 3, o = i / (3 * HM); w2t[i] = wrow(a.k2 + ((o * HM + co) * 3 + ky) * 3); }
-    }
-}
-
 // conv1 + ReLU at the two positions (r, c), (r, c + 1) of a region whose samples xs[HC][XR][XC] start one row and
 // column earlier.  Each output sums its 144 products in the same order whichever pair it is computed in, so the
 // forward and the backward's recomputation give the same bits.
 template <int XR, int XC>
-__device__ __forceinline__ void conv1_pair(const float* b1, const float4* w1f, const float* xs, int r, int c,
+__device__ __forceinline__ void conv1_pair(const float* b1, const float* __restrict__ k1, const float* xs, int r, int c,
                                            float (&h0)[HM], float (&h1)[HM]) {
     f2 h[HM];
 #pragma unroll
@@ -114,8 +96,8 @@ __device__ __forceinline__ void conv1_pair(const float* b1, const float4* w1f, c
             const f2 xa = {row[0], row[1]}, xb = {row[1], row[2]}, xc = {row[2], row[3]};
 #pragma unroll
             for (int co = 0; co < HM; co++) {
-                const float4 w = w1f[(ci * 3 + ky) * HM + co];
-                h[co] = fma2(w.x, xa, h[co]); h[co] = fma2(w.y, xb, h[co]); h[co] = fma2(w.z, xc, h[co]);
+                const float* wp = k1 + ((co * HC + ci) * 3 + ky) * 3;
+                h[co] = fma2(wp[0], xa, h[co]); h[co] = fma2(wp[1], xb, h[co]); h[co] = fma2(wp[2], xc, h[co]);
             }
         }
     }
@@ -155,15 +137,13 @@ __device__ __forceinline__ void window_sums(const float* in, int in_stride, cons
 __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_fwd(HeadArgs a) {
     constexpr int XR = FTH + 4, XC = FTW + 4, QR = FTH + 2, QC = FTW + 2;
     // one LDS array, the weights first: their reads take immediate offsets from one base (< 64 KB)
-    __shared__ float4 smem[NF1 + (HC * XR * XC + HM * QR * QC + 12) / 4];
-    float4* w1f = smem;                  // (conv2's 216 weights stay scalar loads: two blocks per CU fit 160 KB)
-    float* sb1 = (float*)(smem + NF1);
+    __shared__ float smem[12 + HC * XR * XC + HM * QR * QC];
+    float* sb1 = smem;
     float* sb2 = sb1 + HM;
     float* xs = sb1 + 12;                // samples, tile + 2 halo
     float* hs = xs + HC * XR * XC;       // hidden, tile + 1 halo (0 outside the image: conv2's padding)
     const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
     const int y0 = ty * FTH, x0 = tx * FTW;
-    stage_weights<true, false, false>(a, w1f, nullptr, nullptr);
     if (threadIdx.x < HM) sb1[threadIdx.x] = a.b1[threadIdx.x];
     if (threadIdx.x < HO) sb2[threadIdx.x] = a.b2[threadIdx.x];
     stage_samples<XR, XC>(a, y0 - 2, x0 - 2, xs);
@@ -171,7 +151,7 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (int i = threadIdx.x; i < QR * (QC / 2); i += HT) {     // position pairs (r, c), (r, c + 1)
         const int r = i / (QC / 2), c = 2 * (i % (QC / 2)), y = y0 - 1 + r, x = x0 - 1 + c;
         float h0[HM], h1[HM];
-        conv1_pair<XR, XC>(sb1, w1f, xs, r, c, h0, h1);
+        conv1_pair<XR, XC>(sb1, a.k1, xs, r, c, h0, h1);
         const bool in0 = y >= 0 && y < a.H && x >= 0 && x < a.W, in1 = y >= 0 && y < a.H && x + 1 >= 0 && x + 1 < a.W;
 #pragma unroll
         for (int co = 0; co < HM; co++) {
@@ -212,10 +192,8 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
 __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_bwd_h(HeadArgs a) {
     constexpr int XR = TH + 2, XC = TW + 2;
     constexpr int NP = HO * HM, G = HT / NP;    // dW2: 24 pairs x 10 row groups
-    __shared__ float4 smem[NF1 + NF2 + (HM + HO * TW + HC * XR * XC + HO * XR * XC + HM * TH * TW) / 4];
-    float4* w1f = smem;                  // weights first (immediate offsets)
-    float4* w2t = w1f + NF1;
-    float* sb1 = (float*)(w2t + NF2);
+    __shared__ float smem[HM + HO * TW + HC * XR * XC + HO * XR * XC + HM * TH * TW];
+    float* sb1 = smem;
     float* colsum = sb1 + HM;
     float* xs = colsum + HO * TW;        // samples, tile + 1 halo; then the dW2 row-group sums
     float* ms = xs + HC * XR * XC;       // dmask, tile + 1 halo (0 outside the image)
@@ -223,7 +201,6 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
     const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
     const int y0 = ty * TH, x0 = tx * TW;
     const size_t HW = (size_t)a.H * a.W;
-    stage_weights<true, false, true>(a, w1f, nullptr, w2t);
     if (threadIdx.x < HM) sb1[threadIdx.x] = a.b1[threadIdx.x];
     stage_samples<XR, XC>(a, y0 - 1, x0 - 1, xs);
     for (int i = threadIdx.x; i < XR * XC; i += HT) {
@@ -236,7 +213,7 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (int i = threadIdx.x; i < TH * (TW / 2); i += HT) {     // owned position pairs
         const int r = i / (TW / 2), c = 2 * (i % (TW / 2)), y = y0 + r, x = x0 + c;
         float h0[HM], h1[HM];
-        conv1_pair<XR, XC>(sb1, w1f, xs, r, c, h0, h1);
+        conv1_pair<XR, XC>(sb1, a.k1, xs, r, c, h0, h1);
         const bool in0 = y < a.H && x < a.W, in1 = y < a.H && x + 1 < a.W;
 #pragma unroll
         for (int co = 0; co < HM; co++) {
@@ -258,7 +235,8 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
                 const f2 m21 = {row[2], row[3]}, m10 = {row[1], row[2]}, m0_ = {row[0], row[1]};
 #pragma unroll
                 for (int co = 0; co < HM; co++) {
-                    const float4 w = w2t[(o * 3 + ky) * HM + co];   // kx = 0, 1, 2 read columns c + 2, c + 1, c
+                    const float* wq = a.k2 + ((o * HM + co) * 3 + ky) * 3;   // kx = 0, 1, 2 read c + 2, c + 1, c
+                    const float4 w = make_float4(wq[0], wq[1], wq[2], 0.0f);
                     d[co] = fma2(w.x, m21, d[co]); d[co] = fma2(w.y, m10, d[co]); d[co] = fma2(w.z, m0_, d[co]);
                 }
             }
@@ -308,14 +286,12 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
 
 __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_bwd_x(HeadArgs a) {
     constexpr int XR = TH + 2, XC = TW + 2;
-    __shared__ float4 smem[NF1 + (HC * XR * XC + HM * XR * XC) / 4];
-    float4* w1t = smem;                  // weights first (immediate offsets)
-    float* xs = (float*)(smem + NF1);    // samples, tile + 1 halo
+    __shared__ float smem[HC * XR * XC + HM * XR * XC];
+    float* xs = smem;                    // samples, tile + 1 halo
     float* ds = xs + HC * XR * XC;       // dh, tile + 1 halo (0 outside the image)
     const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
     const int y0 = ty * TH, x0 = tx * TW;
     const size_t HW = (size_t)a.H * a.W;
-    stage_weights<false, true, false>(a, nullptr, w1t, nullptr);
     stage_samples<XR, XC>(a, y0 - 1, x0 - 1, xs);
     for (int i = threadIdx.x; i < XR * XC; i += HT) {
         const int r = i / XC, c = i % XC, y = y0 - 1 + r, x = x0 - 1 + c;
@@ -339,7 +315,8 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
                 const f2 g21 = {row[2], row[3]}, g10 = {row[1], row[2]}, g0_ = {row[0], row[1]};
 #pragma unroll
                 for (int ci = 0; ci < HC; ci++) {
-                    const float4 w = w1t[(co * 3 + ky) * HC + ci];   // kx = 0, 1, 2 read columns c + 2, c + 1, c
+                    const float* wq = a.k1 + ((co * HC + ci) * 3 + ky) * 3;   // kx = 0, 1, 2 read c + 2, c + 1, c
+                    const float4 w = make_float4(wq[0], wq[1], wq[2], 0.0f);
                     d[ci] = fma2(w.x, g21, d[ci]); d[ci] = fma2(w.y, g10, d[ci]); d[ci] = fma2(w.z, g0_, d[ci]);
                 }
             }
