@@ -259,3 +259,34 @@ def test_mask_head_matches_float64(hip_device, uh, uw, H, W):
     _head(*leaves, (H, W)).backward(dm)
     for a, t in zip(got, leaves):
         assert torch.equal(a, t.grad)
+
+
+def test_embedding_bitwise_across_processes(hip_device, tmp_path):
+    """The embedding's mask and every parameter gradient are the same bits in other processes (two fresh children
+    running concurrently on the same GPU) as in this one, after this process has run MIOpen convolutions of its own.
+    With MIOpen inside the embedding this failed: the algorithm MIOpen picks depends on its find database and on what
+    ran before in the process, and the masked ADMM ranks stopped matching the sequential baseline (gpurun_out/det1)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    probe = os.path.join(root, "tools", "embed_det_probe.py")
+    sys.path.insert(0, os.path.join(root, "tools"))
+    try:
+        import embed_det_probe
+    finally:
+        sys.path.pop(0)
+    x = torch.randn((1, 67, 34, 60), device=hip_device, requires_grad=True)
+    w = torch.randn((256, 67, 3, 3), device=hip_device, requires_grad=True)
+    F.conv2d(x, w, padding=1).square().sum().backward()     # MIOpen state in this process
+    torch.cuda.synchronize()
+    paths = [str(tmp_path / f"child{i}.pt") for i in range(2)]
+    procs = [subprocess.Popen([sys.executable, probe, "--child", p, "--W", "960", "--H", "540"]) for p in paths]
+    mine = embed_det_probe.once(960, 540)
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    for p in paths:
+        other = torch.load(p, weights_only=True)
+        assert sorted(other) == sorted(mine)
+        for k in mine:
+            assert torch.equal(mine[k], other[k]), k
