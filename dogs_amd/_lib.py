@@ -147,9 +147,9 @@ def load(path: str | None = None):
         L.dg_conv3x3_wgrad_scratch_bytes.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int]
         L.dg_conv3x3_wgrad.restype = C.c_int
         L.dg_mask_head_forward.restype = C.c_int
-        L.dg_mask_head_forward.argtypes = [C.c_int] * 4 + [vp] * 6 + [vp]
+        L.dg_mask_head_forward.argtypes = [C.c_int] * 4 + [vp] * 7 + [vp]
         L.dg_mask_head_backward.restype = C.c_int
-        L.dg_mask_head_backward.argtypes = [C.c_int] * 4 + [vp] * 9 + [C.c_size_t, vp]
+        L.dg_mask_head_backward.argtypes = [C.c_int] * 4 + [vp] * 10 + [C.c_size_t, vp]
         L.dg_mask_head_scratch_bytes.restype = C.c_size_t
         L.dg_mask_head_scratch_bytes.argtypes = [C.c_int, C.c_int]
         L.dg_mask_head_nparams.restype = C.c_int

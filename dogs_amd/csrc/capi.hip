@@ -1011,11 +1011,12 @@ static gs::HeadArgs head_args(int H, int W, int h2, int w2, const float* u, cons
 }
 
 int dg_mask_head_forward(int H, int W, int h2, int w2, const float* u, const float* w1, const float* b1,
-                         const float* w2p, const float* b2, float* mask, dg_stream_t stream) {
+                         const float* w2p, const float* b2, float* mask, float* hidden, dg_stream_t stream) {
     if (!head_shape_ok(H, W, h2, w2) || !u || !w1 || !b1 || !w2p || !b2 || !mask)
         return fail("mask_head_forward: bad args%s%d");
     gs::HeadArgs a = head_args(H, W, h2, w2, u, w1, b1, w2p, b2);
     a.mask = mask;
+    a.hid = hidden;
     gs::launch_mask_head_fwd(a, (hipStream_t)stream);
     HIP_OK(hipGetLastError());
     return 0;
@@ -1031,8 +1032,8 @@ size_t dg_mask_head_scratch_bytes(int H, int W) {
 int dg_mask_head_nparams(void) { return gs::mask_head_nparams(); }
 
 int dg_mask_head_backward(int H, int W, int h2, int w2, const float* u, const float* w1, const float* b1,
-                          const float* w2p, const float* b2, const float* dmask, float* du, float* dparams,
-                          void* scratch, size_t scratch_bytes, dg_stream_t stream) {
+                          const float* w2p, const float* b2, const float* dmask, const float* hidden, float* du,
+                          float* dparams, void* scratch, size_t scratch_bytes, dg_stream_t stream) {
     if (!head_shape_ok(H, W, h2, w2) || !u || !w1 || !b1 || !w2p || !b2 || !dmask || !du || !dparams || !scratch)
         return fail("mask_head_backward: bad args%s%d");
     if (scratch_bytes < dg_mask_head_scratch_bytes(H, W)) return fail("mask_head_backward: scratch too small%s%d");
@@ -1040,6 +1041,7 @@ int dg_mask_head_backward(int H, int W, int h2, int w2, const float* u, const fl
     const size_t HW = (size_t)H * W;
     float* f = (float*)scratch;
     a.dmask = dmask; a.dh = f; a.dx = f + 8 * HW; a.part = f + 24 * HW; a.du = du;
+    a.hid = const_cast<float*>(hidden);
     gs::launch_mask_head_bwd(a, dparams, (hipStream_t)stream);
     HIP_OK(hipGetLastError());
     return 0;

@@ -31,6 +31,8 @@ struct HeadArgs {
     float* mask;           // forward output
     const float* dmask;    // backward input
     float *dh, *dx, *du, *part;   // backward scratch (dh [8][H][W], dx [16][H][W], part [tiles][nparams]) and du
+    float* hid;            // the hidden layer relu(conv1(...)) [8][H][W]: written by the forward, read by the backward
+                           // (nullptr: the forward stores nothing, the backward recomputes it)
     int tiles_x, tiles_y;
 };
 int mask_head_tiles(int H, int W);

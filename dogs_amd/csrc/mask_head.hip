@@ -8,7 +8,7 @@
 // Here the 16-channel image never exists:
 //   k_head_fwd    per 6 x 62 output tile: the bilinear samples of the stage-4 output on the tile + 2 halo into LDS,
 //                 conv1 + ReLU on the tile + 1 halo into LDS, conv2 -> the [3, H, W] mask;
-//   k_head_bwd_h  per tile: recompute the samples (tile + 1 halo) and h on the tile; dL/dh = [h > 0] conv2^T(dmask)
+//   k_head_bwd_h  per tile: h on the tile (stored by the forward, or recomputed from the samples); dL/dh = [h > 0] conv2^T(dmask)
 //                 (dmask on the tile + 1 halo) -> dh [8, H, W]; the tile's partial dW2, db2 (fixed-order sums);
 //   k_head_bwd_x  per tile: the samples (tile + 1 halo) and dh (tile + 1 halo) -> the tile's partial dW1, db1 and
 //                 dL/dsample = conv1^T(dh) on the tile -> dx [16, H, W];
@@ -161,6 +161,12 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
     __syncthreads();
     const size_t HW = (size_t)a.H * a.W;
+    if (a.hid) {   // the tile's hidden layer for the backward (which then neither stages the samples nor runs conv1)
+        for (int i = threadIdx.x; i < HM * FTH * FTW; i += HT) {
+            const int c = i % FTW, r = (i / FTW) % FTH, co = i / (FTW * FTH), y = y0 + r, x = x0 + c;
+            if (y < a.H && x < a.W) a.hid[co * HW + (size_t)y * a.W + x] = hs[(co * QR + r + 1) * QC + c + 1];
+        }
+    }
     for (int i = threadIdx.x; i < FTH * (FTW / 2); i += HT) {
         const int r = i / (FTW / 2), c = 2 * (i % (FTW / 2)), y = y0 + r, x = x0 + c;
         if (y >= a.H || x >= a.W) continue;
@@ -189,6 +195,7 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
 }
 
+template <bool HID>   // HID: h from the forward's store (a.hid), else recomputed from the samples
 __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_bwd_h(HeadArgs a) {
     constexpr int XR = TH + 2, XC = TW + 2;
     constexpr int NP = HO * HM, G = HT / NP;    // dW2: 24 pairs x 10 row groups
@@ -202,7 +209,7 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
     const int y0 = ty * TH, x0 = tx * TW;
     const size_t HW = (size_t)a.H * a.W;
     if (threadIdx.x < HM) sb1[threadIdx.x] = a.b1[threadIdx.x];
-    stage_samples<XR, XC>(a, y0 - 1, x0 - 1, xs);
+    if (!HID) stage_samples<XR, XC>(a, y0 - 1, x0 - 1, xs);
     for (int i = threadIdx.x; i < XR * XC; i += HT) {
         const int r = i / XC, c = i % XC, y = y0 - 1 + r, x = x0 - 1 + c;
         const bool in = y >= 0 && y < a.H && x >= 0 && x < a.W;
@@ -213,8 +220,17 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (int i = threadIdx.x; i < TH * (TW / 2); i += HT) {     // owned position pairs
         const int r = i / (TW / 2), c = 2 * (i % (TW / 2)), y = y0 + r, x = x0 + c;
         float h0[HM], h1[HM];
-        conv1_pair<XR, XC>(sb1, a.k1, xs, r, c, h0, h1);
         const bool in0 = y < a.H && x < a.W, in1 = y < a.H && x + 1 < a.W;
+        if (HID) {
+            const size_t q = in0 ? (size_t)y * a.W + x : 0;
+#pragma unroll
+            for (int co = 0; co < HM; co++) {
+                h0[co] = in0 ? a.hid[co * HW + q] : 0.0f;
+                h1[co] = in1 ? a.hid[co * HW + q + 1] : 0.0f;
+            }
+        } else {
+            conv1_pair<XR, XC>(sb1, a.k1, xs, r, c, h0, h1);
+        }
 #pragma unroll
         for (int co = 0; co < HM; co++) {
             if (!in0) h0[co] = 0.0f;
@@ -454,7 +470,8 @@ void launch_mask_head_bwd(HeadArgs a, float* grads, hipStream_t st) {
     a.tiles_x = (a.W + TW - 1) / TW;
     a.tiles_y = (a.H + TH - 1) / TH;
     const int nb = a.tiles_x * a.tiles_y;
-    k_head_bwd_h<<<nb, HT, 0, st>>>(a);
+    if (a.hid) k_head_bwd_h<true><<<nb, HT, 0, st>>>(a);
+    else k_head_bwd_h<false><<<nb, HT, 0, st>>>(a);
     k_head_bwd_x<<<nb, HT, 0, st>>>(a);
     const int64_t nu = (int64_t)a.h2 * a.w2;
     k_head_bwd_u<<<(unsigned)((nu + 255) / 256), 256, 0, st>>>(a);

@@ -148,10 +148,14 @@ class _MaskHead(torch.autograd.Function):
         uc = u.detach().contiguous()
         ps = [t.detach().contiguous() for t in (w1, b1, w2, b2)]
         mask = torch.empty((3, H, W), dtype=torch.float32, device=u.device)
+        # the hidden layer, kept for the backward when one will run (it then skips the samples and conv1)
+        hid = torch.empty((8, H, W), dtype=torch.float32, device=u.device) if any(ctx.needs_input_grad) else None
         with _lib.device_ctx(u.device):
             _lib.check(_lib.load().dg_mask_head_forward(H, W, int(uc.shape[1]), int(uc.shape[2]), uc.data_ptr(),
                                                         *[p.data_ptr() for p in ps], mask.data_ptr(),
+                                                        hid.data_ptr() if hid is not None else None,
                                                         _lib.stream_of(u.device)))
+        ctx.hid = hid
         ctx.save_for_backward(uc, *ps)
         ctx.size = (H, W)
         return mask
@@ -169,10 +173,13 @@ class _MaskHead(torch.autograd.Function):
         nbytes = int(L.dg_mask_head_scratch_bytes(H, W))
         scratch = torch.empty(nbytes, dtype=torch.uint8, device=uc.device)
         with _lib.device_ctx(uc.device):
+            hid = ctx.hid
             _lib.check(L.dg_mask_head_backward(H, W, int(uc.shape[1]), int(uc.shape[2]), uc.data_ptr(),
                                                w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
-                                               gc.data_ptr(), du.data_ptr(), dp.data_ptr(), scratch.data_ptr(),
-                                               nbytes, _lib.stream_of(uc.device)))
+                                               gc.data_ptr(), hid.data_ptr() if hid is not None else None,
+                                               du.data_ptr(), dp.data_ptr(), scratch.data_ptr(), nbytes,
+                                               _lib.stream_of(uc.device)))
+        ctx.hid = None
         n1, n2 = w1.numel(), w2.numel()
         dw1, db1 = dp[:n1].view_as(w1), dp[n1:n1 + b1.numel()]
         o = n1 + b1.numel()

@@ -121,16 +121,18 @@ int dg_conv3x3(int Cin, int Cout, int H, int W, const float* x, const float* w, 
 /* The appearance embedding's full-resolution head (masks.py:8-54: F.interpolate(x, (H, W), "bilinear") then
  * out_conv = Conv2d(16, 8, 3, pad 1) -> ReLU -> Conv2d(8, 3, 3, pad 1); replaces the resize, the two nn.Conv2d calls
  * and their autograd backward): u [16][h2][w2] (the last upsampling stage's output), w1 [8][16][3][3], b1 [8],
- * w2p [3][8][3][3], b2 [3] -> mask [3][H][W].  The backward takes dmask [3][H][W] and writes du [16][h2][w2] and
+ * w2p [3][8][3][3], b2 [3] -> mask [3][H][W]; `hidden` [8][H][W] (may be NULL) receives relu(conv1(resize(u))).
+ * The backward takes dmask [3][H][W] and `hidden` (the forward's; NULL: recomputed) and writes du [16][h2][w2] and
  * dparams [dg_mask_head_nparams()] = dW1 | db1 | dW2 | db2, with scratch of dg_mask_head_scratch_bytes(H, W) bytes.
- * Deterministic (fixed-order sums, no atomics).  H <= 4 h2 and W <= 4 w2 (an error otherwise). */
+ * Deterministic (fixed-order sums, no atomics; the same bits with and without `hidden`).  H <= 4 h2 and W <= 4 w2
+ * (an error otherwise). */
 int dg_mask_head_forward(int H, int W, int h2, int w2, const float* u, const float* w1, const float* b1,
-                         const float* w2p, const float* b2, float* mask, dg_stream_t stream);
+                         const float* w2p, const float* b2, float* mask, float* hidden, dg_stream_t stream);
 size_t dg_mask_head_scratch_bytes(int H, int W);
 int dg_mask_head_nparams(void);
 int dg_mask_head_backward(int H, int W, int h2, int w2, const float* u, const float* w1, const float* b1,
-                          const float* w2p, const float* b2, const float* dmask, float* du, float* dparams,
-                          void* scratch, size_t scratch_bytes, dg_stream_t stream);
+                          const float* w2p, const float* b2, const float* dmask, const float* hidden, float* du,
+                          float* dparams, void* scratch, size_t scratch_bytes, dg_stream_t stream);
 
 /* The precise tile cull's threshold logf(opacity / (1/255)) of each of n opacities, with the arithmetic the binning
  * uses (duplicateWithKeys, rasterizer_impl.cu:149-151: the correctly rounded logf).  A parity probe:

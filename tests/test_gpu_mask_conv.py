@@ -290,3 +290,37 @@ def test_embedding_bitwise_across_processes(hip_device, tmp_path):
         assert sorted(other) == sorted(mine)
         for k in mine:
             assert torch.equal(mine[k], other[k]), k
+
+
+def test_mask_head_backward_same_bits_with_stored_hidden(hip_device):
+    """The backward with the forward's stored hidden layer (the default: k_head_bwd_h skips the samples and conv1) and
+    with it recomputed (hidden = NULL) give the same bits: the forward stores exactly the values the recomputation
+    produces (one conv1 function, the same summation order)."""
+    from dogs_amd import _lib
+    L = _lib.load()
+    gen = torch.Generator(device=hip_device).manual_seed(21)
+    H, W, h2, w2 = 77, 131, 48, 80
+    u = torch.relu(torch.randn((16, h2, w2), generator=gen, device=hip_device))
+    w1 = torch.randn((8, 16, 3, 3), generator=gen, device=hip_device) * 0.1
+    b1 = torch.randn(8, generator=gen, device=hip_device) * 0.1
+    w2_ = torch.randn((3, 8, 3, 3), generator=gen, device=hip_device) * 0.1
+    b2 = torch.randn(3, generator=gen, device=hip_device) * 0.1
+    dm = torch.randn((3, H, W), generator=gen, device=hip_device)
+    P = [t.data_ptr() for t in (u, w1, b1, w2_, b2)]
+    st = _lib.stream_of(hip_device)
+    mask = torch.empty((3, H, W), device=hip_device)
+    hid = torch.full((8, H, W), float("nan"), device=hip_device)
+    _lib.check(L.dg_mask_head_forward(H, W, h2, w2, *P, mask.data_ptr(), hid.data_ptr(), st))
+    mask2 = torch.empty_like(mask)
+    _lib.check(L.dg_mask_head_forward(H, W, h2, w2, *P, mask2.data_ptr(), None, st))
+    assert torch.equal(mask, mask2) and torch.isfinite(hid).all() and (hid >= 0).all()
+    nb = int(L.dg_mask_head_scratch_bytes(H, W))
+    outs = []
+    for h in (hid.data_ptr(), None):
+        du = torch.empty_like(u)
+        dp = torch.empty(int(L.dg_mask_head_nparams()), device=hip_device)
+        scr = torch.empty(nb, dtype=torch.uint8, device=hip_device)
+        _lib.check(L.dg_mask_head_backward(H, W, h2, w2, *P, dm.data_ptr(), h, du.data_ptr(), dp.data_ptr(),
+                                           scr.data_ptr(), nb, st))
+        outs.append((du, dp))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

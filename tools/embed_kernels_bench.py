@@ -50,11 +50,15 @@ def main():
     nb = int(L.dg_mask_head_scratch_bytes(H, W))
     scr = torch.empty(nb, dtype=torch.uint8, device=dev)
     P = [t.data_ptr() for t in (u, w1, b1, w2_, b2)]
-    res = {"head_fwd": timed(lambda: _lib.check(L.dg_mask_head_forward(H, W, h2, w2, *P, mask.data_ptr(), st)),
-                             args.iters),
-           "head_bwd": timed(lambda: _lib.check(L.dg_mask_head_backward(H, W, h2, w2, *P, dm.data_ptr(), du.data_ptr(),
-                                                                        dp.data_ptr(), scr.data_ptr(), nb, st)),
-                             args.iters)}
+    hid = torch.empty((8, H, W), device=dev)
+    res = {"head_fwd": timed(lambda: _lib.check(L.dg_mask_head_forward(H, W, h2, w2, *P, mask.data_ptr(),
+                                                                       hid.data_ptr(), st)), args.iters),
+           "head_bwd": timed(lambda: _lib.check(L.dg_mask_head_backward(H, W, h2, w2, *P, dm.data_ptr(), hid.data_ptr(),
+                                                                        du.data_ptr(), dp.data_ptr(), scr.data_ptr(),
+                                                                        nb, st)), args.iters),
+           "head_bwd_recompute": timed(lambda: _lib.check(L.dg_mask_head_backward(
+               H, W, h2, w2, *P, dm.data_ptr(), None, du.data_ptr(), dp.data_ptr(), scr.data_ptr(), nb, st)),
+               args.iters)}
     has_conv = hasattr(L, "dg_conv3x3") and not args.miopen
     for cin, cout, h, w in CONVS:
         x = torch.randn((cin, h, w), generator=g, device=dev)
