@@ -775,6 +775,7 @@ def main():
         tt = time.perf_counter()
         nts = max(2 * len(cams), args.steps // 2)
         host = []
+        w0 = int(L.load().dg_host_wait_ns())
         for _ in range(nts):
             th = time.perf_counter()
             ts.step()
@@ -782,6 +783,7 @@ def main():
         torch.cuda.synchronize()
         tms = (time.perf_counter() - tt) / nts * 1e3
         host_ms = float(np.median(host)) * 1e3
+        wait_ms = (int(L.load().dg_host_wait_ns()) - w0) / nts / 1e6
         nstep = ts.native()
         route_ms = {}
         # the default route (activation backward folded into the update) and the unfused one, interleaved three
@@ -811,8 +813,11 @@ def main():
                              "densification stats + SparseGaussianAdam (one launch), cycling the view batch; "
                              "autograd route (the drop-in API)",
                  "host_ms_per_step": round(host_ms, 3),
+                 "host_wait_ms_per_step": round(wait_ms, 3),
                  "host_note": "median host time per autograd-route step (Python + autograd + launches, and the "
-                              "forward's one wait for the phase-1 counters); above ms_per_step the GPU waits on it",
+                              "forward's one wait for the phase-1 counters); above ms_per_step the GPU waits on it. "
+                              "host_wait_ms_per_step: the mean of that wait (dg_host_wait_ns), i.e. host time that "
+                              "is the GPU's, not Python's",
                  "native": {"views_per_s": round(1e3 / nms, 2), "ms_per_step": round(nms, 3),
                             "route": "dg_train_step (dogs_amd.train_step): the same iteration in one C call, the "
                                      "activation backward folded into the optimizer update",

@@ -111,7 +111,7 @@ EXPORTS = ("dg_rasterize_forward", "dg_rasterize_backward", "dg_rasterize_count"
            "dg_ring_upload", "dg_ring_pending", "dg_ring_destroy", "dg_image_u8_to_chw", "dg_points_in_boxes2d", "dg_activate_forward", "dg_activate_backward", "dg_clamp_l1_blocks",
            "dg_clamp_l1_forward", "dg_clamp_l1_backward", "dg_row_prod_forward", "dg_row_prod_backward", "dg_adaptive_capacity", "dg_debug_counters", "dg_adam_update_groups_prox", "dg_train_step", "dg_train_sync",
            "dg_colmap_cameras", "dg_colmap_images", "dg_colmap_points3d", "dg_prune_select", "dg_prune_gather_stats",
-           "dg_last_error", "dg_version", "dg_shutdown")
+           "dg_last_error", "dg_version", "dg_host_wait_ns", "dg_shutdown")
 
 _lib = None
 _lock = threading.Lock()
@@ -296,6 +296,8 @@ def load(path: str | None = None):
         L.dg_last_error.restype = C.c_char_p
         L.dg_last_error.argtypes = []
         L.dg_version.restype = C.c_int
+        L.dg_host_wait_ns.restype = C.c_uint64
+        L.dg_host_wait_ns.argtypes = []
         if hasattr(L, "dg_shutdown"):  # absent in older builds used for A/B runs
             L.dg_shutdown.restype = C.c_int
             L.dg_shutdown.argtypes = []

@@ -291,6 +291,9 @@ HostCounters& host_counters() {
 // Spin on the sequence word the long-list sort launch writes after the counters (no event: an event record is a
 // barrier packet, ~6 us of idle GPU per view).  A fault or a stall ends the spin after 2 s: the stream's error, if any,
 // is reported, else the word is re-read once the stream has drained.
+// host time spent waiting for the forward's counter read-back, process-wide (dg_host_wait_ns)
+std::atomic<uint64_t> g_host_wait_ns{0};
+
 int wait_seq(HostCounters& h, hipStream_t s) {
     volatile uint32_t* w = h.buf + 16;
     const auto t0 = std::chrono::steady_clock::now();
@@ -537,6 +540,8 @@ int dg_exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_
 }
 int dg_version(void) { return 1; }
 
+uint64_t dg_host_wait_ns(void) { return g_host_wait_ns.load(std::memory_order_relaxed); }
+
 // reset / query the adaptive capacity at (device, W, H): ctx < 0 resets every context (state and probes alike) and
 // reports context 0; ctx >= 0 only that context
 static int adaptive_capacity_impl(int ctx, int W, int H, int reset, int* per_tile_out) {
@@ -764,10 +769,15 @@ int forward_impl(const dg_raster_args* a, float* out_color, float* out_invdepth,
     { PROF("render_fwd"); gs::launch_render_fwd(r, s); }
     DBG_SYNC(a->debug, s);
 
-    if (kcopy) {
-        if (wait_seq(hcs, s)) return 1;
-    } else {
-        HIP_OK(hipEventSynchronize(hcs.ev));
+    {
+        const auto w0 = std::chrono::steady_clock::now();
+        if (kcopy) {
+            if (wait_seq(hcs, s)) return 1;
+        } else {
+            HIP_OK(hipEventSynchronize(hcs.ev));
+        }
+        g_host_wait_ns.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                     std::chrono::steady_clock::now() - w0).count(), std::memory_order_relaxed);
     }
     const uint32_t* hc = hcs.buf;
     adapt(ac, hc[gs::CNT_PREV_UNF], hc[gs::CNT_PREV_K2], hc[gs::CNT_E1]);

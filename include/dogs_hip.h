@@ -495,6 +495,10 @@ int dg_colmap_points3d(const char* path, int min_track_length, uint64_t* n, uint
 
 const char* dg_last_error(void);
 int dg_version(void);
+/* Cumulative host time (ns, process-wide) the forward has spent waiting for its one counter read-back (phase 1's
+ * num_rendered / cut / error flag, dg_rasterize_forward): the part of a caller's host time per step that is waiting
+ * for the GPU rather than work.  Introspection for the bench; no reference counterpart. */
+uint64_t dg_host_wait_ns(void);
 /* Explicit teardown of the library's process-wide device state before interpreter / runtime exit: waits for the
  * streams it created (the overlapped SH update's side streams), destroys them and their events, frees the adaptive-
  * capacity probes, the pinned counter buffers and the profiling events.  Idempotent; any later call re-creates what it
