@@ -324,3 +324,27 @@ def test_mask_head_backward_same_bits_with_stored_hidden(hip_device):
                                            scr.data_ptr(), nb, st))
         outs.append((du, dp))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_conv3x3_module_batched_and_unbatched(hip_device):
+    """Conv3x3 (the embedding's nn.Conv2d on dg_conv3x3 / dg_conv3x3_wgrad) on a batch of 2 and on one unbatched
+    image: output and the input / weight / bias gradients against float64 autograd of F.conv2d, 1e-5 norm-wise (the
+    weight gradient summed over the batch in batch order)."""
+    from dogs_amd.masks import Conv3x3
+    torch.manual_seed(4)
+    conv = Conv3x3(5, 7).to(hip_device)
+    for shape in ((2, 5, 9, 13), (5, 17, 70)):
+        x = torch.randn(shape, device=hip_device, requires_grad=True)
+        g = torch.randn(((shape[0],) if len(shape) == 4 else ()) + (7,) + shape[-2:], device=hip_device)
+        conv.zero_grad(set_to_none=True)
+        y = conv(x)
+        (y * g).sum().backward()
+        x64 = x.detach().double().requires_grad_(True)
+        w64 = conv.weight.detach().double().requires_grad_(True)
+        b64 = conv.bias.detach().double().requires_grad_(True)
+        y64 = F.conv2d(x64, w64, b64, padding=1)
+        (y64 * g.double()).sum().backward()
+        assert y.shape == y64.shape
+        assert _rel(y, y64) < 1e-5
+        assert _rel(x.grad, x64.grad) < 1e-5
+        assert _rel(conv.weight.grad, w64.grad) < 1e-5 and _rel(conv.bias.grad, b64.grad) < 1e-5
