@@ -318,7 +318,8 @@ def test_count_mode_matches_oracle(oracle, hip_device, prefix):
     """LightGaussian count mode (GaussianRasterizationSettings(f_count=True), as count_render,
     conerf/render/gaussian_render.py:161-278, calls it with the full SH features): per-Gaussian contributing-pixel
     counts and importance scores against the oracle's restatement of renderCUDA_count (old forward.cu:392-500).
-    Counts are exact integers here; a decision at the alpha/T thresholds may flip between v_exp_f32 and expf."""
+    Counts are exact integers and equal the oracle's on this scene (a decision within an ulp of the alpha / T thresholds
+    could flip between v_exp_f32 and expf; none does here)."""
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
     from dogs_amd.diff_gaussian_rasterization import _C
     n, W, H = 2000, 160, 120
@@ -344,10 +345,11 @@ def test_count_mode_matches_oracle(oracle, hip_device, prefix):
     assert np.abs(img.cpu().numpy() - col_o).max() < 5e-3
     cnt = count.cpu().numpy()
     assert count.dtype == torch.int32 and cnt.sum() > 0
-    assert (cnt == cnt_o).mean() > 0.99
-    assert np.abs(cnt.astype(np.int64) - cnt_o).sum() <= 1e-3 * cnt_o.sum()
-    same = cnt == cnt_o
-    np.testing.assert_allclose(score.cpu().numpy()[same], score_o[same], rtol=1e-4, atol=1e-6)
+    # every count equal: no (pixel, Gaussian) decision of this scene sits within an ulp of the 1/255 or T thresholds
+    # where v_exp_f32 and expf could disagree (measured: 0 of 28,274 counted pixels differ; the inputs are fixed, so
+    # the result is too)
+    np.testing.assert_array_equal(cnt, cnt_o)
+    np.testing.assert_allclose(score.cpu().numpy(), score_o, rtol=1e-4, atol=1e-6)
 
 
 @pytest.mark.parametrize("M", [1, 2, 3])
