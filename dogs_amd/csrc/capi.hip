@@ -1036,7 +1036,7 @@ size_t dg_mask_head_scratch_bytes(int H, int W) {
     if (H < 1 || W < 1) return 0;
     const size_t HW = (size_t)H * W;
     return (24 * HW + (size_t)gs::mask_head_tiles(H, W) * gs::mask_head_nparams() +
-            gs::rowsum_scratch_floats(gs::mask_head_nparams())) * sizeof(float);
+            gs::rowsum_scratch_floats(gs::mask_head_tiles(H, W), gs::mask_head_nparams())) * sizeof(float);
 }
 
 int dg_mask_head_nparams(void) { return gs::mask_head_nparams(); }

@@ -8,9 +8,9 @@ namespace gs {
 // dy [Cout][H][W]; scratch: conv3x3_wgrad_scratch_bytes(...) bytes of per-block partials.  Deterministic.
 size_t conv3x3_wgrad_scratch_bytes(int Cin, int Cout, int H, int W);
 bool conv3x3_wgrad_supported(int Cin, int Cout);
-// column sums of per-block partials [nrows][ncols] in a fixed order; seg: rowsum_scratch_floats(ncols) floats;
+// column sums of per-block partials [nrows][ncols] in a fixed order; seg: rowsum_scratch_floats(nrows, ncols) floats;
 // columns < nsplit go to out_a, the rest to out_b
-size_t rowsum_scratch_floats(int ncols);
+size_t rowsum_scratch_floats(int nrows, int ncols);
 void launch_rowsum(const float* part, int nrows, int ncols, float* seg, float* out_a, int nsplit, float* out_b,
                    hipStream_t st);
 void launch_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const float* dy, float* dw, float* db,

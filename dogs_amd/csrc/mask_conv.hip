@@ -396,45 +396,69 @@ void launch_conv3x3(int Cin, int Cout, int H, int W, const float* x, const float
     }
 }
 
-// Column sums of a [nrows][ncols] array of per-block partials in a fixed order: pass 1 sums each column over
-// RS_SEG contiguous row segments (a block covers 64 columns x 4 segments: each wave reads whole 256-B row pieces),
-// pass 2 adds the segments in order.  (One wave per column striding over the rows read 64 cache lines per load and
-// took 25-37 us; this takes a few.)
-constexpr int RS_SEG = 32;
+// Column sums of a [nrows][ncols] array of per-block partials in a fixed order: pass 1 sums each column over nseg
+// contiguous row segments (a block covers 64 columns x 4 segments: each wave reads whole 256-B row pieces), pass 2
+// adds the segments in order.  nseg follows the shape (~16 rows per segment, rowsum_segments), and a few rows are
+// summed in one pass: with 32 segments always, the weight gradient's few-row partials of the wide low-resolution
+// layers (6 x 154k for the fusion) wrote and re-read 32 segment rows, and the head's tall, narrow 4050 x 1379 partials
+// ran 176 blocks walking 126 rows each (50 us).
+// (One wave per column striding over the rows read 64 cache lines per load and took 25-37 us.)
+constexpr int RS_SEG_MAX = 256;
 
-__global__ void __launch_bounds__(256) k_rowsum_seg(const float* __restrict__ part, int nrows, int ncols,
+// segments: ~16 rows each, at most RS_SEG_MAX and at most 4M floats of segment sums (the wide arrays have few rows)
+__host__ __device__ inline int rowsum_segments(int nrows, int ncols) {
+    if (nrows < 64) return 1;
+    int s = (nrows / 16) & ~3;
+    const int cap = (int)((((int64_t)1 << 22) / (ncols > 0 ? ncols : 1)) & ~3);
+    if (s > RS_SEG_MAX) s = RS_SEG_MAX;
+    if (s > cap) s = cap;
+    return s < 4 ? 1 : s;
+}
+
+__global__ void __launch_bounds__(256) k_rowsum_seg(const float* __restrict__ part, int nrows, int ncols, int nseg,
                                                      float* __restrict__ seg) {
     const int col = blockIdx.x * 64 + (threadIdx.x & 63);
     const int sg = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (col >= ncols) return;
-    const int r0 = (int)((int64_t)nrows * sg / RS_SEG), r1 = (int)((int64_t)nrows * (sg + 1) / RS_SEG);
+    const int r0 = (int)((int64_t)nrows * sg / nseg), r1 = (int)((int64_t)nrows * (sg + 1) / nseg);
     float v = 0.0f;
+#pragma unroll 8
     for (int r = r0; r < r1; r++) v += part[(size_t)r * ncols + col];
     seg[(size_t)sg * ncols + col] = v;
 }
 
-__global__ void __launch_bounds__(256) k_rowsum_final(const float* __restrict__ seg, int ncols, int nsplit,
+// the segments' sums in order (or, with one segment, the rows themselves)
+__global__ void __launch_bounds__(256) k_rowsum_final(const float* __restrict__ seg, int nseg, int ncols, int nsplit,
                                                        float* __restrict__ out_a, float* __restrict__ out_b) {
     const int col = blockIdx.x * 256 + threadIdx.x;
     if (col >= ncols) return;
     float v = 0.0f;
 #pragma unroll 8
-    for (int sg = 0; sg < RS_SEG; sg++) v += seg[(size_t)sg * ncols + col];
+    for (int sg = 0; sg < nseg; sg++) v += seg[(size_t)sg * ncols + col];
     if (col < nsplit) out_a[col] = v;
     else out_b[col - nsplit] = v;
 }
 
 void launch_rowsum(const float* part, int nrows, int ncols, float* seg, float* out_a, int nsplit, float* out_b,
                    hipStream_t st) {
-    k_rowsum_seg<<<dim3((ncols + 63) / 64, RS_SEG / 4), 256, 0, st>>>(part, nrows, ncols, seg);
-    k_rowsum_final<<<(ncols + 255) / 256, 256, 0, st>>>(seg, ncols, nsplit, out_a, out_b);
+    const int nseg = rowsum_segments(nrows, ncols);
+    if (nseg == 1) {   // few rows: one pass over the partials themselves
+        k_rowsum_final<<<(ncols + 255) / 256, 256, 0, st>>>(part, nrows, ncols, nsplit, out_a, out_b);
+        return;
+    }
+    k_rowsum_seg<<<dim3((ncols + 63) / 64, nseg / 4), 256, 0, st>>>(part, nrows, ncols, nseg, seg);
+    k_rowsum_final<<<(ncols + 255) / 256, 256, 0, st>>>(seg, nseg, ncols, nsplit, out_a, out_b);
 }
 
-size_t rowsum_scratch_floats(int ncols) { return (size_t)RS_SEG * ncols; }
+size_t rowsum_scratch_floats(int nrows, int ncols) {
+    const int nseg = rowsum_segments(nrows, ncols);
+    return nseg > 1 ? (size_t)nseg * ncols : 0;
+}
 
 size_t conv3x3_wgrad_scratch_bytes(int Cin, int Cout, int H, int W) {
     const WgradShape s = wgrad_shape(Cin, Cout, H, W);
-    return ((size_t)s.tiles_x * s.tiles_y * s.npart + rowsum_scratch_floats(s.npart)) * sizeof(float);
+    return ((size_t)s.tiles_x * s.tiles_y * s.npart + rowsum_scratch_floats(s.tiles_x * s.tiles_y, s.npart)) *
+           sizeof(float);
 }
 
 bool conv3x3_wgrad_supported(int Cin, int Cout) {   // the 16 x 16 channel chunks index grid.y (<= 65535)
