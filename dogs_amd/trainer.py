@@ -229,7 +229,10 @@ class GaussianSplatTrainer:
         if self.mask is not None:
             from .masks import MaskedStep
             self.mask = self.mask.to(self.device)
-            self.mask_optimizer = torch.optim.Adam(self.mask.parameters(), lr=c.mask_lr)
+            # torch's fused Adam on the GPU: one launch per step instead of ~8 foreach kernels (~100 us per masked
+            # iteration); the same optimizer in both routes and in every ADMM rank
+            self.mask_optimizer = torch.optim.Adam(self.mask.parameters(), lr=c.mask_lr,
+                                                   fused=self.device.type == "cuda")
             self._masked = MaskedStep(self.mask, self.mask_optimizer)
         # the trained exposure and its Adam + schedule (:246-257); the model holds one [3,4] per training image
         self.exposure_optimizer = self.exposure_scheduler = None
