@@ -33,15 +33,18 @@ __device__ __forceinline__ int div_m(int q, uint32_t m) { return (int)__umulhi((
 // zeros outside the image) -> dst[ch * ch_stride + r * row_stride + c].  Two phases per batch of B rows: every load
 // from a clamped (valid) address with the out-of-image lanes zeroed by a select, then the stores -- no branch
 // between a load and the next, so the B rows' loads are in flight together.
-template <int B>
+// gate (may be nullptr, same layout as src): a value is kept only where gate > 0 -- a ReLU's backward folded into the
+// staging of its output gradient (gate = the ReLU's output).
+template <int B, bool GATED = false>
 __device__ __forceinline__ void stage_rows(const float* __restrict__ src, size_t HW, int H, int W, int ch0, int nvalid,
                                            int gy0, int gx0, int nrows, int rpc, uint32_t m_rpc, int ncols,
-                                           float* dst, int ch_stride, int row_stride, int wave, int lane) {
+                                           float* dst, int ch_stride, int row_stride, int wave, int lane,
+                                           const float* __restrict__ gate = nullptr) {
     const int gxa = gx0 + lane, gxb = gx0 + 64 + lane;
     const bool cola = gxa >= 0 && gxa < W, colb = gxb < W;
     const int gxac = gxa < 0 ? 0 : (gxa >= W ? W - 1 : gxa), gxbc = gxb >= W ? W - 1 : gxb;
     for (int base = wave; base < nrows; base += 4 * B) {
-        float v0[B], v1[B];
+        float v0[B], v1[B], g0[B], g1[B];
         uint32_t rok = 0;
 #pragma unroll
         for (int b = 0; b < B; b++) {   // loads only: the selects wait for phase 2
@@ -49,9 +52,11 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, size_t
             const int gy = gy0 + r;
             rok |= (q < nrows && ch < nvalid && gy >= 0 && gy < H) ? (1u << b) : 0u;
             const int chc = ch < nvalid ? ch : nvalid - 1, gyc = gy < 0 ? 0 : (gy >= H ? H - 1 : gy);
-            const float* row = src + (size_t)(ch0 + chc) * HW + (size_t)gyc * W;
-            v0[b] = row[gxac];
-            v1[b] = row[gxbc];
+            const size_t ro = (size_t)(ch0 + chc) * HW + (size_t)gyc * W;
+            v0[b] = src[ro + gxac];
+            v1[b] = src[ro + gxbc];
+            g0[b] = GATED ? gate[ro + gxac] : 1.0f;   // compile-time: no branch between the loads
+            g1[b] = GATED ? gate[ro + gxbc] : 1.0f;
         }
 #pragma unroll
         for (int b = 0; b < B; b++) {
@@ -60,8 +65,8 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, size_t
                 const int ch = div_m(q, m_rpc), r = q - ch * rpc;
                 float* d = dst + ch * ch_stride + r * row_stride;
                 const bool ok = (rok >> b) & 1u;
-                if (lane < ncols) d[lane] = ok && cola ? v0[b] : 0.0f;
-                if (64 + lane < ncols) d[64 + lane] = ok && colb ? v1[b] : 0.0f;
+                if (lane < ncols) d[lane] = ok && cola && g0[b] > 0.0f ? v0[b] : 0.0f;
+                if (64 + lane < ncols) d[64 + lane] = ok && colb && g1[b] > 0.0f ? v1[b] : 0.0f;
             }
         }
     }
@@ -140,8 +145,10 @@ WgradShape wgrad_shape(int Cin, int Cout, int H, int W) {
     return s;
 }
 
+template <bool GATED>
 __global__ void __launch_bounds__(WG_THREADS) k_conv3x3_wgrad_part(WgradShape s, const float* __restrict__ x,
                                                                     const float* __restrict__ dy,
+                                                                    const float* __restrict__ gate,
                                                                     float* __restrict__ part) {
     extern __shared__ float lds[];
     const int H = s.H, W = s.W, TR = s.TR;
@@ -160,7 +167,8 @@ __global__ void __launch_bounds__(WG_THREADS) k_conv3x3_wgrad_part(WgradShape s,
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     stage_rows<8>(x, HW, H, W, ci0, Cin, y0 - 1, x0 - 1, Cin * (TR + 2), TR + 2, s.m_tr2, xrow, xs, s.xs_stride, xrow,
                   wv, ln);
-    stage_rows<8>(dy, HW, H, W, co0, Cout, y0, x0, s.CO * TR, TR, s.m_tr, WG_TC, ds, s.dy_stride, WG_TC, wv, ln);
+    stage_rows<8, GATED>(dy, HW, H, W, co0, Cout, y0, x0, s.CO * TR, TR, s.m_tr, WG_TC, ds, s.dy_stride, WG_TC, wv,
+                         ln, gate);
     __syncthreads();
     const int nq = s.CO / WG_CQ, slots = s.slots, G = s.G;
     const int t = threadIdx.x, grp = t / slots, slot = t % slots;
@@ -248,11 +256,13 @@ struct ConvShape {
     int tiles_x, tiles_y, cblocks;
     int lg_nco;             // log2(8 WC)
     uint32_t m_srows;       // div_magic(rows + 2)
+    int relu;               // forward: y = max(y, 0) (the stage's ReLU folded into the store)
 };
 
-template <int R, bool ADJ>
+template <int R, bool ADJ, bool GATED = false>
 __global__ void __launch_bounds__(256) k_conv3x3(ConvShape s, const float* __restrict__ x, const float* __restrict__ w,
-                                                  const float* __restrict__ b, float* __restrict__ y) {
+                                                  const float* __restrict__ b, float* __restrict__ y,
+                                                  const float* __restrict__ gate) {
     extern __shared__ float4 lds4[];
     float4* wl = lds4;                                  // [8 KS][9][8 WC / 4] float4
     float* xl = reinterpret_cast<float*>(lds4 + CV_WFLOATS / 4);   // [8 KS][rows + 2][66]
@@ -274,8 +284,8 @@ __global__ void __launch_bounds__(256) k_conv3x3(ConvShape s, const float* __res
     for (int c0 = 0; c0 < Cin; c0 += per_round) {
         const int nc = Cin - c0 < per_round ? Cin - c0 : per_round;
         if (c0) __syncthreads();
-        stage_rows<8>(x, HW, H, W, c0, nc, y0 - 1, x0 - 1, nc * srows, srows, s.m_srows, CV_SROW, xl, sch, CV_SROW,
-                      wave, lane);
+        stage_rows<8, GATED>(x, HW, H, W, c0, nc, y0 - 1, x0 - 1, nc * srows, srows, s.m_srows, CV_SROW, xl, sch,
+                             CV_SROW, wave, lane, gate);
         stage_weights_kco<4, ADJ>(w, Cin, Cout, c0, nc, cob, s.lg_nco, reinterpret_cast<float*>(wl));
         __syncthreads();
         if (!live) continue;
@@ -335,7 +345,10 @@ __global__ void __launch_bounds__(256) k_conv3x3(ConvShape s, const float* __res
 #pragma unroll
         for (int j = 0; j < CV_CO; j++) {
             const int o = cob + wc * CV_CO + j;
-            if (o < Cout) y[(size_t)o * HW + (size_t)gy * W + gx] = acc[r][j] + (b ? b[o] : 0.0f);
+            if (o < Cout) {
+                const float v = acc[r][j] + (b ? b[o] : 0.0f);
+                y[(size_t)o * HW + (size_t)gy * W + gx] = s.relu && !(v > 0.0f) ? 0.0f : v;
+            }
         }
     }
 }
@@ -354,7 +367,7 @@ static size_t conv_lds_bytes(const ConvShape& s, int R) {
 }
 
 void launch_conv3x3(int Cin, int Cout, int H, int W, const float* x, const float* w, const float* b, float* y,
-                    bool adjoint, hipStream_t st) {
+                    bool adjoint, bool relu, const float* gate, hipStream_t st) {
     const int groups = (Cout + CV_CO - 1) / CV_CO, kmax = (Cin + CV_CIB - 1) / CV_CIB;
     // (R, KS) candidates, most work per wave first: the first with >= 256 blocks (one per CU), else the most blocks.
     // (>= 960 blocks, i.e. more splitting for the small low-resolution layers, measured 3% slower over the network's
@@ -382,17 +395,24 @@ void launch_conv3x3(int Cin, int Cout, int H, int W, const float* x, const float
         if (blocks > best_blocks) { best = s; bestR = R; best_blocks = blocks; }
         if (blocks >= 256) { best = s; bestR = R; break; }
     }
+    best.relu = relu && !adjoint;
     const dim3 grid(best.tiles_x * best.tiles_y, best.cblocks);
     const size_t lds = conv_lds_bytes(best, bestR);
     const float* bb = adjoint ? nullptr : b;
     if (adjoint) {
-        if (bestR == 4) k_conv3x3<4, true><<<grid, 256, lds, st>>>(best, x, w, bb, y);
-        else if (bestR == 2) k_conv3x3<2, true><<<grid, 256, lds, st>>>(best, x, w, bb, y);
-        else k_conv3x3<1, true><<<grid, 256, lds, st>>>(best, x, w, bb, y);
+        if (gate) {
+            if (bestR == 4) k_conv3x3<4, true, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, gate);
+            else if (bestR == 2) k_conv3x3<2, true, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, gate);
+            else k_conv3x3<1, true, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, gate);
+        } else {
+            if (bestR == 4) k_conv3x3<4, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
+            else if (bestR == 2) k_conv3x3<2, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
+            else k_conv3x3<1, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
+        }
     } else {
-        if (bestR == 4) k_conv3x3<4, false><<<grid, 256, lds, st>>>(best, x, w, bb, y);
-        else if (bestR == 2) k_conv3x3<2, false><<<grid, 256, lds, st>>>(best, x, w, bb, y);
-        else k_conv3x3<1, false><<<grid, 256, lds, st>>>(best, x, w, bb, y);
+        if (bestR == 4) k_conv3x3<4, false><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
+        else if (bestR == 2) k_conv3x3<2, false><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
+        else k_conv3x3<1, false><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
     }
 }
 
@@ -465,14 +485,15 @@ bool conv3x3_wgrad_supported(int Cin, int Cout) {   // the 16 x 16 channel chunk
     return Cin >= 1 && Cout >= 1 && Cin <= 4000 && Cout <= 4000;
 }
 
-void launch_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const float* dy, float* dw, float* db,
-                          float* scratch, hipStream_t st) {
+void launch_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const float* dy, const float* gate,
+                          float* dw, float* db, float* scratch, hipStream_t st) {
     const WgradShape s = wgrad_shape(Cin, Cout, H, W);
     const int nblk = s.tiles_x * s.tiles_y;
     // the staged tiles, or the groups' sums (at most 256 x 40 floats) when they are larger
     const int stage = s.CI * s.xs_stride + s.CO * s.dy_stride, sums = WG_THREADS * WG_CQ * 10;
     const size_t lds = (size_t)(stage > sums ? stage : sums) * sizeof(float);
-    k_conv3x3_wgrad_part<<<dim3(nblk, s.nci * s.nco), WG_THREADS, lds, st>>>(s, x, dy, scratch);
+    if (gate) k_conv3x3_wgrad_part<true><<<dim3(nblk, s.nci * s.nco), WG_THREADS, lds, st>>>(s, x, dy, gate, scratch);
+    else k_conv3x3_wgrad_part<false><<<dim3(nblk, s.nci * s.nco), WG_THREADS, lds, st>>>(s, x, dy, nullptr, scratch);
     launch_rowsum(scratch, nblk, s.npart, scratch + (size_t)nblk * s.npart, dw, Cout * Cin * 9, db, st);
 }
 

@@ -44,14 +44,19 @@ class Conv3x3(nn.Conv2d):
     def __init__(self, cin: int, cout: int) -> None:
         super().__init__(cin, cout, kernel_size=3, padding=1)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, relu: bool = False) -> torch.Tensor:
+        """relu: max(conv(x), 0), the following nn.ReLU folded into the kernels (its backward too)."""
         if x.is_cuda:
-            return _Conv3x3Fn.apply(x, self.weight, self.bias)
-        return super().forward(x)
+            return _Conv3x3Fn.apply(x, self.weight, self.bias, relu)
+        y = super().forward(x)
+        return F.relu(y) if relu else y
 
 
-def _conv3x3(L, x4: torch.Tensor, w: torch.Tensor, b, cout: int, adjoint: bool) -> torch.Tensor:
-    """dg_conv3x3 over each image of x4 [N, C, H, W] (float32, contiguous)."""
+DG_CONV_ADJOINT, DG_CONV_RELU = 1, 2   # dg_conv3x3 flags (include/dogs_hip.h)
+
+
+def _conv3x3(L, x4: torch.Tensor, w: torch.Tensor, b, cout: int, flags: int, gate=None) -> torch.Tensor:
+    """dg_conv3x3 over each image of x4 [N, C, H, W] (float32, contiguous); gate: [N, ...] like x4 or None."""
     from . import _lib
     n, _, H, W = (int(v) for v in x4.shape)
     cin_w, cout_w = int(w.shape[1]), int(w.shape[0])
@@ -60,34 +65,37 @@ def _conv3x3(L, x4: torch.Tensor, w: torch.Tensor, b, cout: int, adjoint: bool) 
         st = _lib.stream_of(x4.device)
         for i in range(n):
             _lib.check(L.dg_conv3x3(cin_w, cout_w, H, W, x4[i].data_ptr(), w.data_ptr(),
-                                    b.data_ptr() if b is not None else None, y[i].data_ptr(), int(adjoint), st))
+                                    b.data_ptr() if b is not None else None, y[i].data_ptr(), flags,
+                                    gate[i].data_ptr() if gate is not None else None, st))
     return y
 
 
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, relu=False):
         from . import _lib
         if x.dtype != torch.float32 or weight.dtype != torch.float32:
             raise TypeError("Conv3x3 on the GPU takes float32")
         x4 = (x if x.dim() == 4 else x.unsqueeze(0)).contiguous()
         w = weight.contiguous()
         b = bias.contiguous() if bias is not None else None
-        ctx.save_for_backward(x4, w)
         ctx.has_bias = bias is not None
         ctx.batched = x.dim() == 4
-        y = _conv3x3(_lib.load(), x4, w, b, int(w.shape[0]), False)
+        ctx.relu = bool(relu)
+        y = _conv3x3(_lib.load(), x4, w, b, int(w.shape[0]), DG_CONV_RELU if relu else 0)
+        # with the ReLU folded in, its output gates the output gradient in both backward kernels
+        ctx.save_for_backward(x4, w, y if relu else None)
         return y if ctx.batched else y[0]
 
     @staticmethod
     def backward(ctx, g):
         from . import _lib
-        x4, w = ctx.saved_tensors
+        x4, w, gate = ctx.saved_tensors
         L = _lib.load()
         g4 = (g if g.dim() == 4 else g.unsqueeze(0)).contiguous()
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = _conv3x3(L, g4, w, None, int(w.shape[1]), True)
+            dx = _conv3x3(L, g4, w, None, int(w.shape[1]), DG_CONV_ADJOINT, gate)
             dx = dx if ctx.batched else dx[0]
         dw = db = None
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
@@ -100,13 +108,14 @@ class _Conv3x3Fn(torch.autograd.Function):
                 scratch = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=w.device)
                 dwb, dbb = (dw, db) if b == 0 else (torch.empty_like(dw), torch.empty_like(db))
                 with _lib.device_ctx(w.device):
-                    _lib.check(L.dg_conv3x3_wgrad(cin, cout, H, W, x4[b].data_ptr(), g4[b].data_ptr(), dwb.data_ptr(),
+                    _lib.check(L.dg_conv3x3_wgrad(cin, cout, H, W, x4[b].data_ptr(), g4[b].data_ptr(),
+                                                  gate[b].data_ptr() if gate is not None else None, dwb.data_ptr(),
                                                   dbb.data_ptr(), scratch.data_ptr(), nbytes,
                                                   _lib.stream_of(w.device)))
                 if b:
                     dw += dwb
                     db += dbb
-        return dx, dw, (db if ctx.has_bias else None)
+        return dx, dw, (db if ctx.has_bias else None), None
 
 
 class AppearanceEmbedding(nn.Module):
@@ -126,7 +135,9 @@ class AppearanceEmbedding(nn.Module):
         _, h, w = image.shape
         code = self.appearance_embedding[index]
         x = torch.cat([image, code[:, None, None].expand(code.shape[0], h, w)], dim=0)
-        x = self.upsample(self.fusion(x))
+        x = self.fusion(x)
+        for st in self.upsample:   # (PixelShuffle, Conv3x3, ReLU): the ReLU folded into the convolution's kernels
+            x = st[1](st[0](x), relu=True)
         H, W = int(image_size[0]), int(image_size[1])
         if x.is_cuda and x.dim() == 3 and H <= 4 * x.shape[1] and W <= 4 * x.shape[2]:
             c1, c2 = self.out_conv[0], self.out_conv[2]

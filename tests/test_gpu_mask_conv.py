@@ -26,7 +26,7 @@ SHAPES = [(16, 8, 1080, 1920), (8, 3, 1080, 1920), (8, 16, 544, 960), (16, 32, 2
           (3, 5, 17, 70), (1, 1, 1, 1), (7, 9, 33, 65), (2, 3, 5, 129)]
 
 
-def _wgrad(x, g):
+def _wgrad(x, g, gate=None):
     from dogs_amd import _lib
     L = _lib.load()
     cin, H, W = x.shape
@@ -35,7 +35,8 @@ def _wgrad(x, g):
     db = torch.empty(cout, dtype=torch.float32, device=x.device)
     n = int(L.dg_conv3x3_wgrad_scratch_bytes(cin, cout, H, W))
     s = torch.empty(max(n, 1), dtype=torch.uint8, device=x.device)
-    _lib.check(L.dg_conv3x3_wgrad(cin, cout, H, W, x.data_ptr(), g.data_ptr(), dw.data_ptr(), db.data_ptr(),
+    _lib.check(L.dg_conv3x3_wgrad(cin, cout, H, W, x.data_ptr(), g.data_ptr(),
+                                  gate.data_ptr() if gate is not None else None, dw.data_ptr(), db.data_ptr(),
                                   s.data_ptr(), n, _lib.stream_of(x.device)))
     return dw, db
 
@@ -77,18 +78,21 @@ def test_wgrad_matches_float64(hip_device, cin, cout, H, W):
 def test_unsupported_channels_are_an_error(hip_device):
     from dogs_amd import _lib
     L = _lib.load()
-    assert L.dg_conv3x3_wgrad(5000, 2, 8, 8, 1, 1, 1, 1, 1, 1 << 30, None) != 0
-    assert L.dg_conv3x3(0, 2, 8, 8, 1, 1, None, 1, 0, None) != 0
+    assert L.dg_conv3x3_wgrad(5000, 2, 8, 8, 1, 1, None, 1, 1, 1, 1 << 30, None) != 0
+    assert L.dg_conv3x3(0, 2, 8, 8, 1, 1, None, 1, 0, None, None) != 0
+    assert L.dg_conv3x3(2, 2, 8, 8, 1, 1, None, 1, 4, None, None) != 0   # unknown flag
 
 
-def _conv(x, w, b, adjoint):
+def _conv(x, w, b, adjoint, relu=False, gate=None):
     from dogs_amd import _lib
     L = _lib.load()
     cout, cin = w.shape[:2]
     _, H, W = x.shape
     y = torch.full(((cin if adjoint else cout), H, W), float("nan"), device=x.device)
+    flags = (1 if adjoint else 0) | (2 if relu else 0)
     _lib.check(L.dg_conv3x3(cin, cout, H, W, x.data_ptr(), w.data_ptr(), b.data_ptr() if b is not None else None,
-                            y.data_ptr(), int(adjoint), _lib.stream_of(x.device)))
+                            y.data_ptr(), flags, gate.data_ptr() if gate is not None else None,
+                            _lib.stream_of(x.device)))
     return y
 
 
@@ -348,3 +352,26 @@ def test_conv3x3_module_batched_and_unbatched(hip_device):
         assert _rel(y, y64) < 1e-5
         assert _rel(x.grad, x64.grad) < 1e-5
         assert _rel(conv.weight.grad, w64.grad) < 1e-5 and _rel(conv.bias.grad, b64.grad) < 1e-5
+
+
+@pytest.mark.parametrize("cin,cout,H,W", [(8, 16, 544, 960), (64, 128, 68, 120), (7, 9, 33, 65)])
+def test_relu_folded_into_conv_and_its_backward(hip_device, cin, cout, H, W):
+    """The stages' ReLU folded into the kernels: the forward with DG_CONV_RELU = max(conv, 0) of the plain forward (bit
+    for bit: the same sums, then the clamp); the adjoint and the weight gradient with gate = that output equal the
+    plain kernels applied to dy * [y > 0] (bit for bit), and float64 within 1e-5."""
+    gen = torch.Generator(device=hip_device).manual_seed(cin + cout + W)
+    x = torch.randn((cin, H, W), generator=gen, device=hip_device)
+    w = torch.randn((cout, cin, 3, 3), generator=gen, device=hip_device) / (3 * cin ** 0.5)
+    b = torch.randn(cout, generator=gen, device=hip_device) * 0.3
+    g = torch.randn((cout, H, W), generator=gen, device=hip_device)
+    y = _conv(x, w, b, False, relu=True)
+    plain = _conv(x, w, b, False)
+    assert torch.equal(y, torch.clamp_min(plain, 0.0)) and 0.1 < float((y > 0).float().mean()) < 0.9
+    gm = torch.where(y > 0, g, torch.zeros_like(g))
+    assert torch.equal(_conv(g, w, None, True, gate=y), _conv(gm, w, None, True))
+    dw, db = _wgrad(x, g, gate=y)
+    dw2, db2 = _wgrad(x, gm)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+    rw, rb = _ref64(x, gm)
+    assert _rel(dw, rw) < 1e-5 and _rel(db, rb) < 1e-5
+    assert _rel(_conv(g, w, None, True, gate=y), _conv64(gm, w, None, True)) < 1e-5

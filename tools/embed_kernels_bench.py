@@ -73,17 +73,17 @@ def main():
         key = f"{cin}x{cout}@{h}x{w}"
         if has_conv:
             res["fwd " + key] = timed(lambda: _lib.check(L.dg_conv3x3(cin, cout, h, w, x.data_ptr(), wt.data_ptr(),
-                                                                      bias.data_ptr(), y.data_ptr(), 0, st)), args.iters)
+                                                                      bias.data_ptr(), y.data_ptr(), 0, None, st)), args.iters)
             res["adj " + key] = timed(lambda: _lib.check(L.dg_conv3x3(cin, cout, h, w, dy.data_ptr(), wt.data_ptr(),
-                                                                      None, dx.data_ptr(), 1, st)), args.iters)
+                                                                      None, dx.data_ptr(), 1, None, st)), args.iters)
         else:   # MIOpen's forward and backward-data for comparison
             x4, dy4 = x[None], dy[None]
             res["fwd " + key] = timed(lambda: torch.nn.functional.conv2d(x4, wt, bias, padding=1), args.iters)
             res["adj " + key] = timed(lambda: torch.ops.aten.convolution_backward(
                 dy4, x4, wt, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False]), args.iters)
         res["wgrad " + key] = timed(lambda: _lib.check(L.dg_conv3x3_wgrad(cin, cout, h, w, x.data_ptr(), dy.data_ptr(),
-                                                                          dw.data_ptr(), db.data_ptr(), s2.data_ptr(),
-                                                                          n, st)), args.iters)
+                                                                          None, dw.data_ptr(), db.data_ptr(),
+                                                                          s2.data_ptr(), n, st)), args.iters)
     tot = 0.0
     for k, v in res.items():
         tot += v
