@@ -153,7 +153,8 @@ def load(path: str | None = None):
         L.dg_mask_head_scratch_bytes.restype = C.c_size_t
         L.dg_mask_head_scratch_bytes.argtypes = [C.c_int, C.c_int]
         L.dg_mask_head_nparams.restype = C.c_int
-        L.dg_conv3x3_wgrad.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, C.c_size_t, vp]
+        L.dg_conv3x3_wgrad.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp,
+                                       C.c_size_t, vp]
         L.dg_conv3x3.restype = C.c_int
         L.dg_conv3x3.argtypes = [C.c_int] * 4 + [vp] * 4 + [C.c_int, vp, vp]
         L.dg_cull_log_threshold.argtypes = [C.c_int64, vp, vp, vp]

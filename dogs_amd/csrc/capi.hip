@@ -984,24 +984,32 @@ size_t dg_conv3x3_wgrad_scratch_bytes(int Cin, int Cout, int H, int W) {
     return gs::conv3x3_wgrad_scratch_bytes(Cin, Cout, H, W);
 }
 
-int dg_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const float* dy, const float* gate, float* dw,
-                     float* db, void* scratch, size_t scratch_bytes, dg_stream_t stream) {
+int dg_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const float* dy, const float* gate, int flags,
+                     float* dw, float* db, void* scratch, size_t scratch_bytes, dg_stream_t stream) {
+    if ((flags & ~DG_CONV_SHUFFLE) || ((flags & DG_CONV_SHUFFLE) && ((H | W) & 1)))
+        return fail("conv3x3_wgrad: bad flags%s%d");
     if (H < 1 || W < 1 || !x || !dy || !dw || !db || !scratch) return fail("conv3x3_wgrad: bad args%s%d");
     if (!gs::conv3x3_wgrad_supported(Cin, Cout)) return fail("conv3x3_wgrad: unsupported channel counts%s%d", "", Cin * Cout);
     if (scratch_bytes < gs::conv3x3_wgrad_scratch_bytes(Cin, Cout, H, W))
         return fail("conv3x3_wgrad: scratch too small%s%d");
-    gs::launch_conv3x3_wgrad(Cin, Cout, H, W, x, dy, gate, dw, db, (float*)scratch, (hipStream_t)stream);
+    gs::launch_conv3x3_wgrad(Cin, Cout, H, W, x, dy, gate, (flags & DG_CONV_SHUFFLE) != 0, dw, db, (float*)scratch,
+                             (hipStream_t)stream);
     HIP_OK(hipGetLastError());
     return 0;
 }
 
 int dg_conv3x3(int Cin, int Cout, int H, int W, const float* x, const float* w, const float* b, float* y, int flags,
                const float* gate, dg_stream_t stream) {
-    if (!x || !w || !y || (flags & ~3)) return fail("conv3x3: bad args%s%d");
+    if (!x || !w || !y || (flags & ~7)) return fail("conv3x3: bad args%s%d");
+    if ((flags & DG_CONV_SHUFFLE) && ((H | W) & 1)) return fail("conv3x3: odd size with DG_CONV_SHUFFLE%s%d");
     if (!gs::conv3x3_supported(Cin, Cout, H, W)) return fail("conv3x3: unsupported shape%s%d", "", Cin * Cout);
+    const bool sh = (flags & DG_CONV_SHUFFLE) != 0;
     // the adjoint launches Cout -> Cin over the forward's weights
-    if (flags & DG_CONV_ADJOINT) gs::launch_conv3x3(Cout, Cin, H, W, x, w, nullptr, y, true, false, gate, (hipStream_t)stream);
-    else gs::launch_conv3x3(Cin, Cout, H, W, x, w, b, y, false, (flags & DG_CONV_RELU) != 0, nullptr, (hipStream_t)stream);
+    if (flags & DG_CONV_ADJOINT)
+        gs::launch_conv3x3(Cout, Cin, H, W, x, w, nullptr, y, true, false, gate, sh, (hipStream_t)stream);
+    else
+        gs::launch_conv3x3(Cin, Cout, H, W, x, w, b, y, false, (flags & DG_CONV_RELU) != 0, nullptr, sh,
+                           (hipStream_t)stream);
     HIP_OK(hipGetLastError());
     return 0;
 }

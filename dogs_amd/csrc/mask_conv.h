@@ -14,14 +14,16 @@ size_t rowsum_scratch_floats(int nrows, int ncols);
 void launch_rowsum(const float* part, int nrows, int ncols, float* seg, float* out_a, int nsplit, float* out_b,
                    hipStream_t st);
 // gate (may be nullptr): dy counts only where gate > 0 (the backward of a ReLU whose output gate is, folded in)
+// shuffle: x is [4 Cin][H / 2][W / 2], read as its pixel shuffle (PixelShuffle(2))
 void launch_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const float* dy, const float* gate,
-                          float* dw, float* db, float* scratch, hipStream_t st);
+                          bool shuffle, float* dw, float* db, float* scratch, hipStream_t st);
 // y [Cout][H][W] = conv3x3(x [Cin][H][W], w [Cout][Cin][3][3]) + b (b may be null), relu: max(y, 0); adjoint: y [Cin]
 // = the data gradient for dy = x [Cout] (w read transposed and flipped, b unused), gate (may be null): dy counts only
 // where gate > 0.  Fixed summation order.
 bool conv3x3_supported(int Cin, int Cout, int H, int W);
+// shuffle: the forward's x is [4 Cin][H / 2][W / 2] read as its pixel shuffle; the adjoint's y is written unshuffled
 void launch_conv3x3(int Cin, int Cout, int H, int W, const float* x, const float* w, const float* b, float* y,
-                    bool adjoint, bool relu, const float* gate, hipStream_t st);
+                    bool adjoint, bool relu, const float* gate, bool shuffle, hipStream_t st);
 
 // The embedding's full-resolution head (mask_head.hip): mask [3][H][W] = conv2(relu(conv1(resize(u)))), u [16][h2][w2],
 // w1 [8][16][3][3], b1 [8], w2 [3][8][3][3], b2 [3]; the backward takes dmask and writes du [16][h2][w2] and the

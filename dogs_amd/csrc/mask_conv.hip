@@ -35,14 +35,21 @@ __device__ __forceinline__ int div_m(int q, uint32_t m) { return (int)__umulhi((
 // between a load and the next, so the B rows' loads are in flight together.
 // gate (may be nullptr, same layout as src): a value is kept only where gate > 0 -- a ReLU's backward folded into the
 // staging of its output gradient (gate = the ReLU's output).
-template <int B, bool GATED = false>
+// SHUF: src is [4 C][H / 2][W / 2] read as its pixel shuffle (torch.nn.PixelShuffle(2): channel 4 c + 2 (y & 1) +
+// (x & 1) at (y / 2, x / 2) is pixel (y, x) of channel c), the upsampling stages' PixelShuffle folded into the staging.
+template <int B, bool GATED = false, bool SHUF = false>
 __device__ __forceinline__ void stage_rows(const float* __restrict__ src, size_t HW, int H, int W, int ch0, int nvalid,
                                            int gy0, int gx0, int nrows, int rpc, uint32_t m_rpc, int ncols,
                                            float* dst, int ch_stride, int row_stride, int wave, int lane,
                                            const float* __restrict__ gate = nullptr) {
+    static_assert(!(GATED && SHUF), "the gate reads src's own layout");
     const int gxa = gx0 + lane, gxb = gx0 + 64 + lane;
     const bool cola = gxa >= 0 && gxa < W, colb = gxb < W;
     const int gxac = gxa < 0 ? 0 : (gxa >= W ? W - 1 : gxa), gxbc = gxb >= W ? W - 1 : gxb;
+    const size_t HWq = HW / 4;
+    const int Wq = W / 2;
+    const size_t offa = SHUF ? (size_t)(gxac & 1) * HWq + (size_t)(gxac >> 1) : (size_t)gxac;
+    const size_t offb = SHUF ? (size_t)(gxbc & 1) * HWq + (size_t)(gxbc >> 1) : (size_t)gxbc;
     for (int base = wave; base < nrows; base += 4 * B) {
         float v0[B], v1[B], g0[B], g1[B];
         uint32_t rok = 0;
@@ -52,11 +59,12 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, size_t
             const int gy = gy0 + r;
             rok |= (q < nrows && ch < nvalid && gy >= 0 && gy < H) ? (1u << b) : 0u;
             const int chc = ch < nvalid ? ch : nvalid - 1, gyc = gy < 0 ? 0 : (gy >= H ? H - 1 : gy);
-            const size_t ro = (size_t)(ch0 + chc) * HW + (size_t)gyc * W;
-            v0[b] = src[ro + gxac];
-            v1[b] = src[ro + gxbc];
-            g0[b] = GATED ? gate[ro + gxac] : 1.0f;   // compile-time: no branch between the loads
-            g1[b] = GATED ? gate[ro + gxbc] : 1.0f;
+            const size_t ro = SHUF ? (size_t)(4 * (ch0 + chc) + 2 * (gyc & 1)) * HWq + (size_t)(gyc >> 1) * Wq
+                                   : (size_t)(ch0 + chc) * HW + (size_t)gyc * W;
+            v0[b] = src[ro + offa];
+            v1[b] = src[ro + offb];
+            g0[b] = GATED ? gate[ro + offa] : 1.0f;   // compile-time: no branch between the loads
+            g1[b] = GATED ? gate[ro + offb] : 1.0f;
         }
 #pragma unroll
         for (int b = 0; b < B; b++) {
@@ -145,7 +153,7 @@ WgradShape wgrad_shape(int Cin, int Cout, int H, int W) {
     return s;
 }
 
-template <bool GATED>
+template <bool GATED, bool SHUF>
 __global__ void __launch_bounds__(WG_THREADS) k_conv3x3_wgrad_part(WgradShape s, const float* __restrict__ x,
                                                                     const float* __restrict__ dy,
                                                                     const float* __restrict__ gate,
@@ -165,7 +173,8 @@ __global__ void __launch_bounds__(WG_THREADS) k_conv3x3_wgrad_part(WgradShape s,
     // one staged row per wave and pass, (channel, row) stepped without a division (a runtime integer division per
     // element made the staging, not the sums, the kernel's cost)
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-    stage_rows<8>(x, HW, H, W, ci0, Cin, y0 - 1, x0 - 1, Cin * (TR + 2), TR + 2, s.m_tr2, xrow, xs, s.xs_stride, xrow,
+    stage_rows<8, false, SHUF>(x, HW, H, W, ci0, Cin, y0 - 1, x0 - 1, Cin * (TR + 2), TR + 2, s.m_tr2, xrow, xs,
+                               s.xs_stride, xrow,
                   wv, ln);
     stage_rows<8, GATED>(dy, HW, H, W, co0, Cout, y0, x0, s.CO * TR, TR, s.m_tr, WG_TC, ds, s.dy_stride, WG_TC, wv,
                          ln, gate);
@@ -259,7 +268,9 @@ struct ConvShape {
     int relu;               // forward: y = max(y, 0) (the stage's ReLU folded into the store)
 };
 
-template <int R, bool ADJ, bool GATED = false>
+// SH: the forward reads x as its pixel shuffle (stage_rows SHUF); the adjoint writes y as the pixel unshuffle
+// ([4 Cin][H / 2][W / 2]), the input gradient of the shuffle folded into the store.
+template <int R, bool ADJ, bool GATED = false, bool SH = false>
 __global__ void __launch_bounds__(256) k_conv3x3(ConvShape s, const float* __restrict__ x, const float* __restrict__ w,
                                                   const float* __restrict__ b, float* __restrict__ y,
                                                   const float* __restrict__ gate) {
@@ -284,8 +295,8 @@ __global__ void __launch_bounds__(256) k_conv3x3(ConvShape s, const float* __res
     for (int c0 = 0; c0 < Cin; c0 += per_round) {
         const int nc = Cin - c0 < per_round ? Cin - c0 : per_round;
         if (c0) __syncthreads();
-        stage_rows<8, GATED>(x, HW, H, W, c0, nc, y0 - 1, x0 - 1, nc * srows, srows, s.m_srows, CV_SROW, xl, sch,
-                             CV_SROW, wave, lane, gate);
+        stage_rows<8, GATED, SH && !ADJ>(x, HW, H, W, c0, nc, y0 - 1, x0 - 1, nc * srows, srows, s.m_srows, CV_SROW,
+                                         xl, sch, CV_SROW, wave, lane, gate);
         stage_weights_kco<4, ADJ>(w, Cin, Cout, c0, nc, cob, s.lg_nco, reinterpret_cast<float*>(wl));
         __syncthreads();
         if (!live) continue;
@@ -347,7 +358,10 @@ __global__ void __launch_bounds__(256) k_conv3x3(ConvShape s, const float* __res
             const int o = cob + wc * CV_CO + j;
             if (o < Cout) {
                 const float v = acc[r][j] + (b ? b[o] : 0.0f);
-                y[(size_t)o * HW + (size_t)gy * W + gx] = s.relu && !(v > 0.0f) ? 0.0f : v;
+                const size_t at = SH && ADJ ? (size_t)(4 * o + 2 * (gy & 1) + (gx & 1)) * (HW / 4) +
+                                                  (size_t)(gy >> 1) * (W / 2) + (size_t)(gx >> 1)
+                                            : (size_t)o * HW + (size_t)gy * W + gx;
+                y[at] = s.relu && !(v > 0.0f) ? 0.0f : v;
             }
         }
     }
@@ -367,7 +381,7 @@ static size_t conv_lds_bytes(const ConvShape& s, int R) {
 }
 
 void launch_conv3x3(int Cin, int Cout, int H, int W, const float* x, const float* w, const float* b, float* y,
-                    bool adjoint, bool relu, const float* gate, hipStream_t st) {
+                    bool adjoint, bool relu, const float* gate, bool shuffle, hipStream_t st) {
     const int groups = (Cout + CV_CO - 1) / CV_CO, kmax = (Cin + CV_CIB - 1) / CV_CIB;
     // (R, KS) candidates, most work per wave first: the first with >= 256 blocks (one per CU), else the most blocks.
     // (>= 960 blocks, i.e. more splitting for the small low-resolution layers, measured 3% slower over the network's
@@ -400,19 +414,33 @@ void launch_conv3x3(int Cin, int Cout, int H, int W, const float* x, const float
     const size_t lds = conv_lds_bytes(best, bestR);
     const float* bb = adjoint ? nullptr : b;
     if (adjoint) {
-        if (gate) {
+        if (gate && shuffle) {
+            if (bestR == 4) k_conv3x3<4, true, true, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, gate);
+            else if (bestR == 2) k_conv3x3<2, true, true, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, gate);
+            else k_conv3x3<1, true, true, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, gate);
+        } else if (gate) {
             if (bestR == 4) k_conv3x3<4, true, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, gate);
             else if (bestR == 2) k_conv3x3<2, true, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, gate);
             else k_conv3x3<1, true, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, gate);
+        } else if (shuffle) {
+            if (bestR == 4) k_conv3x3<4, true, false, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
+            else if (bestR == 2) k_conv3x3<2, true, false, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
+            else k_conv3x3<1, true, false, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
         } else {
             if (bestR == 4) k_conv3x3<4, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
             else if (bestR == 2) k_conv3x3<2, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
             else k_conv3x3<1, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
         }
     } else {
-        if (bestR == 4) k_conv3x3<4, false><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
-        else if (bestR == 2) k_conv3x3<2, false><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
-        else k_conv3x3<1, false><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
+        if (shuffle) {
+            if (bestR == 4) k_conv3x3<4, false, false, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
+            else if (bestR == 2) k_conv3x3<2, false, false, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
+            else k_conv3x3<1, false, false, true><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
+        } else {
+            if (bestR == 4) k_conv3x3<4, false><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
+            else if (bestR == 2) k_conv3x3<2, false><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
+            else k_conv3x3<1, false><<<grid, 256, lds, st>>>(best, x, w, bb, y, nullptr);
+        }
     }
 }
 
@@ -486,14 +514,17 @@ bool conv3x3_wgrad_supported(int Cin, int Cout) {   // the 16 x 16 channel chunk
 }
 
 void launch_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const float* dy, const float* gate,
-                          float* dw, float* db, float* scratch, hipStream_t st) {
+                          bool shuffle, float* dw, float* db, float* scratch, hipStream_t st) {
     const WgradShape s = wgrad_shape(Cin, Cout, H, W);
     const int nblk = s.tiles_x * s.tiles_y;
     // the staged tiles, or the groups' sums (at most 256 x 40 floats) when they are larger
     const int stage = s.CI * s.xs_stride + s.CO * s.dy_stride, sums = WG_THREADS * WG_CQ * 10;
     const size_t lds = (size_t)(stage > sums ? stage : sums) * sizeof(float);
-    if (gate) k_conv3x3_wgrad_part<true><<<dim3(nblk, s.nci * s.nco), WG_THREADS, lds, st>>>(s, x, dy, gate, scratch);
-    else k_conv3x3_wgrad_part<false><<<dim3(nblk, s.nci * s.nco), WG_THREADS, lds, st>>>(s, x, dy, nullptr, scratch);
+    const dim3 grid(nblk, s.nci * s.nco);
+    if (gate && shuffle) k_conv3x3_wgrad_part<true, true><<<grid, WG_THREADS, lds, st>>>(s, x, dy, gate, scratch);
+    else if (gate) k_conv3x3_wgrad_part<true, false><<<grid, WG_THREADS, lds, st>>>(s, x, dy, gate, scratch);
+    else if (shuffle) k_conv3x3_wgrad_part<false, true><<<grid, WG_THREADS, lds, st>>>(s, x, dy, nullptr, scratch);
+    else k_conv3x3_wgrad_part<false, false><<<grid, WG_THREADS, lds, st>>>(s, x, dy, nullptr, scratch);
     launch_rowsum(scratch, nblk, s.npart, scratch + (size_t)nblk * s.npart, dw, Cout * Cin * 9, db, st);
 }
 

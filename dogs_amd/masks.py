@@ -44,23 +44,27 @@ class Conv3x3(nn.Conv2d):
     def __init__(self, cin: int, cout: int) -> None:
         super().__init__(cin, cout, kernel_size=3, padding=1)
 
-    def forward(self, x: torch.Tensor, relu: bool = False) -> torch.Tensor:
-        """relu: max(conv(x), 0), the following nn.ReLU folded into the kernels (its backward too)."""
+    def forward(self, x: torch.Tensor, relu: bool = False, shuffle: bool = False) -> torch.Tensor:
+        """relu: max(conv(x), 0), the following nn.ReLU folded into the kernels (its backward too); shuffle: the
+        convolution of pixel_shuffle(x, 2), the preceding nn.PixelShuffle(2) folded into the kernels' addressing."""
         if x.is_cuda:
-            return _Conv3x3Fn.apply(x, self.weight, self.bias, relu)
-        y = super().forward(x)
+            return _Conv3x3Fn.apply(x, self.weight, self.bias, relu, shuffle)
+        y = super().forward(F.pixel_shuffle(x, 2) if shuffle else x)
         return F.relu(y) if relu else y
 
 
-DG_CONV_ADJOINT, DG_CONV_RELU = 1, 2   # dg_conv3x3 flags (include/dogs_hip.h)
+DG_CONV_ADJOINT, DG_CONV_RELU, DG_CONV_SHUFFLE = 1, 2, 4   # dg_conv3x3 flags (include/dogs_hip.h)
 
 
-def _conv3x3(L, x4: torch.Tensor, w: torch.Tensor, b, cout: int, flags: int, gate=None) -> torch.Tensor:
-    """dg_conv3x3 over each image of x4 [N, C, H, W] (float32, contiguous); gate: [N, ...] like x4 or None."""
+def _conv3x3(L, x4: torch.Tensor, w: torch.Tensor, b, out_chw: tuple, flags: int, gate=None) -> torch.Tensor:
+    """dg_conv3x3 over each image of x4 [N, C, h, w] (float32, contiguous) into [N, *out_chw]; gate: [N, ...] like the
+    output gradient or None.  H, W passed to the kernel are the convolution's (the larger side with the shuffle)."""
     from . import _lib
-    n, _, H, W = (int(v) for v in x4.shape)
+    n = int(x4.shape[0])
+    H, W = (int(x4.shape[2]), int(x4.shape[3])) if not flags & DG_CONV_SHUFFLE or flags & DG_CONV_ADJOINT \
+        else (2 * int(x4.shape[2]), 2 * int(x4.shape[3]))
     cin_w, cout_w = int(w.shape[1]), int(w.shape[0])
-    y = torch.empty((n, cout, H, W), dtype=torch.float32, device=x4.device)
+    y = torch.empty((n, *out_chw), dtype=torch.float32, device=x4.device)
     with _lib.device_ctx(x4.device):
         st = _lib.stream_of(x4.device)
         for i in range(n):
@@ -72,7 +76,7 @@ def _conv3x3(L, x4: torch.Tensor, w: torch.Tensor, b, cout: int, flags: int, gat
 
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, relu=False):
+    def forward(ctx, x, weight, bias, relu=False, shuffle=False):
         from . import _lib
         if x.dtype != torch.float32 or weight.dtype != torch.float32:
             raise TypeError("Conv3x3 on the GPU takes float32")
@@ -81,8 +85,12 @@ class _Conv3x3Fn(torch.autograd.Function):
         b = bias.contiguous() if bias is not None else None
         ctx.has_bias = bias is not None
         ctx.batched = x.dim() == 4
-        ctx.relu = bool(relu)
-        y = _conv3x3(_lib.load(), x4, w, b, int(w.shape[0]), DG_CONV_RELU if relu else 0)
+        ctx.shuffle = bool(shuffle)
+        H, W = int(x4.shape[2]) * (2 if shuffle else 1), int(x4.shape[3]) * (2 if shuffle else 1)
+        if shuffle and int(x4.shape[1]) != 4 * int(w.shape[1]):
+            raise ValueError("Conv3x3 with shuffle takes 4 * in_channels input channels")
+        flags = (DG_CONV_RELU if relu else 0) | (DG_CONV_SHUFFLE if shuffle else 0)
+        y = _conv3x3(_lib.load(), x4, w, b, (int(w.shape[0]), H, W), flags)
         # with the ReLU folded in, its output gates the output gradient in both backward kernels
         ctx.save_for_backward(x4, w, y if relu else None)
         return y if ctx.batched else y[0]
@@ -95,7 +103,8 @@ class _Conv3x3Fn(torch.autograd.Function):
         g4 = (g if g.dim() == 4 else g.unsqueeze(0)).contiguous()
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = _conv3x3(L, g4, w, None, int(w.shape[1]), DG_CONV_ADJOINT, gate)
+            sh = DG_CONV_SHUFFLE if ctx.shuffle else 0
+            dx = _conv3x3(L, g4, w, None, tuple(int(v) for v in x4.shape[1:]), DG_CONV_ADJOINT | sh, gate)
             dx = dx if ctx.batched else dx[0]
         dw = db = None
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
@@ -103,19 +112,20 @@ class _Conv3x3Fn(torch.autograd.Function):
             dw = torch.empty_like(w)
             db = torch.empty(cout, dtype=torch.float32, device=w.device)
             for b in range(int(x4.shape[0])):    # one image per call, summed in batch order
-                H, W = int(x4.shape[2]), int(x4.shape[3])
+                H, W = int(g4.shape[2]), int(g4.shape[3])
                 nbytes = int(L.dg_conv3x3_wgrad_scratch_bytes(cin, cout, H, W))
                 scratch = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=w.device)
                 dwb, dbb = (dw, db) if b == 0 else (torch.empty_like(dw), torch.empty_like(db))
                 with _lib.device_ctx(w.device):
                     _lib.check(L.dg_conv3x3_wgrad(cin, cout, H, W, x4[b].data_ptr(), g4[b].data_ptr(),
-                                                  gate[b].data_ptr() if gate is not None else None, dwb.data_ptr(),
+                                                  gate[b].data_ptr() if gate is not None else None,
+                                                  DG_CONV_SHUFFLE if ctx.shuffle else 0, dwb.data_ptr(),
                                                   dbb.data_ptr(), scratch.data_ptr(), nbytes,
                                                   _lib.stream_of(w.device)))
                 if b:
                     dw += dwb
                     db += dbb
-        return dx, dw, (db if ctx.has_bias else None), None
+        return dx, dw, (db if ctx.has_bias else None), None, None
 
 
 class AppearanceEmbedding(nn.Module):
@@ -136,8 +146,8 @@ class AppearanceEmbedding(nn.Module):
         code = self.appearance_embedding[index]
         x = torch.cat([image, code[:, None, None].expand(code.shape[0], h, w)], dim=0)
         x = self.fusion(x)
-        for st in self.upsample:   # (PixelShuffle, Conv3x3, ReLU): the ReLU folded into the convolution's kernels
-            x = st[1](st[0](x), relu=True)
+        for st in self.upsample:   # (PixelShuffle, Conv3x3, ReLU): shuffle and ReLU folded into the convolution's kernels
+            x = st[1](x, relu=True, shuffle=True)
         H, W = int(image_size[0]), int(image_size[1])
         if x.is_cuda and x.dim() == 3 and H <= 4 * x.shape[1] and W <= 4 * x.shape[2]:
             c1, c2 = self.out_conv[0], self.out_conv[2]

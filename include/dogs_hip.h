@@ -105,20 +105,22 @@ int dg_mark_visible(int P, const float* means3D, const float* viewmatrix, const 
  * geometry.mask; replaces the MIOpen/cuDNN backward-weights call torch makes for nn.Conv2d(k=3, padding=1)):
  * dw [Cout][Cin][3][3] = sum over pixels of dy[co] x [ci] shifted, db [Cout] = sum of dy[co], for x [Cin][H][W] and
  * dy [Cout][H][W] (one image).  gate (may be NULL, [Cout][H][W]): dy counts only where gate > 0 -- the backward of a
- * ReLU applied to the convolution's output (gate = that output) folded in.  Deterministic (fixed-order partial sums,
- * no atomics).  Cin, Cout <= 4000 (an error otherwise); scratch of dg_conv3x3_wgrad_scratch_bytes() bytes. */
+ * ReLU applied to the convolution's output (gate = that output) folded in.  flags DG_CONV_SHUFFLE: x is [4 Cin][H/2]
+ * [W/2], read as its PixelShuffle(2) (H, W even).  Deterministic (fixed-order partial sums, no atomics).  Cin, Cout <= 4000 (an error otherwise); scratch of dg_conv3x3_wgrad_scratch_bytes() bytes. */
 size_t dg_conv3x3_wgrad_scratch_bytes(int Cin, int Cout, int H, int W);
-int dg_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const float* dy, const float* gate, float* dw,
-                     float* db, void* scratch, size_t scratch_bytes, dg_stream_t stream);
+int dg_conv3x3_wgrad(int Cin, int Cout, int H, int W, const float* x, const float* dy, const float* gate, int flags,
+                     float* dw, float* db, void* scratch, size_t scratch_bytes, dg_stream_t stream);
 
 /* The same convolutions' forward and data gradient (masks.py:8-54: nn.Conv2d(k=3, padding=1) on one image; replaces
  * the MIOpen forward and backward-data calls, whose algorithm choice depends on MIOpen's find database and on what the
  * process ran before).  flags 0: y [Cout][H][W] = conv(x [Cin][H][W], w [Cout][Cin][3][3]) + b (b may be NULL);
  * | DG_CONV_RELU: max(y, 0) (nn.Sequential's following ReLU folded into the store);  DG_CONV_ADJOINT: y [Cin][H][W] =
  * the input gradient for the output gradient x [Cout][H][W] (b unused), counting x only where gate > 0 when gate is
- * given (the ReLU's backward, gate = the forward's output; NULL: no ReLU).  Each output sums over (input channel, tap)
- * in a fixed order.  Cin, Cout <= 65536 and Cin * Cout <= 2^24 (an error otherwise). */
-enum { DG_CONV_ADJOINT = 1, DG_CONV_RELU = 2 };
+ * given (the ReLU's backward, gate = the forward's output; NULL: no ReLU).  DG_CONV_SHUFFLE (H, W even): the
+ * forward's x is [4 Cin][H/2][W/2] read as its PixelShuffle(2), and the adjoint writes y as [4 Cin][H/2][W/2] (the
+ * shuffle's input gradient) -- the upsampling stages' nn.PixelShuffle folded in.  Each output sums over (input
+ * channel, tap) in a fixed order.  Cin, Cout <= 65536 and Cin * Cout <= 2^24 (an error otherwise). */
+enum { DG_CONV_ADJOINT = 1, DG_CONV_RELU = 2, DG_CONV_SHUFFLE = 4 };
 int dg_conv3x3(int Cin, int Cout, int H, int W, const float* x, const float* w, const float* b, float* y, int flags,
                const float* gate, dg_stream_t stream);
 

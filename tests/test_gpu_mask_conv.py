@@ -26,17 +26,20 @@ SHAPES = [(16, 8, 1080, 1920), (8, 3, 1080, 1920), (8, 16, 544, 960), (16, 32, 2
           (3, 5, 17, 70), (1, 1, 1, 1), (7, 9, 33, 65), (2, 3, 5, 129)]
 
 
-def _wgrad(x, g, gate=None):
+def _wgrad(x, g, gate=None, shuffle=False):
     from dogs_amd import _lib
     L = _lib.load()
     cin, H, W = x.shape
+    if shuffle:
+        cin, H, W = cin // 4, 2 * H, 2 * W
     cout = g.shape[0]
     dw = torch.empty((cout, cin, 3, 3), dtype=torch.float32, device=x.device)
     db = torch.empty(cout, dtype=torch.float32, device=x.device)
     n = int(L.dg_conv3x3_wgrad_scratch_bytes(cin, cout, H, W))
     s = torch.empty(max(n, 1), dtype=torch.uint8, device=x.device)
     _lib.check(L.dg_conv3x3_wgrad(cin, cout, H, W, x.data_ptr(), g.data_ptr(),
-                                  gate.data_ptr() if gate is not None else None, dw.data_ptr(), db.data_ptr(),
+                                  gate.data_ptr() if gate is not None else None, 4 if shuffle else 0,
+                                  dw.data_ptr(), db.data_ptr(),
                                   s.data_ptr(), n, _lib.stream_of(x.device)))
     return dw, db
 
@@ -78,9 +81,12 @@ def test_wgrad_matches_float64(hip_device, cin, cout, H, W):
 def test_unsupported_channels_are_an_error(hip_device):
     from dogs_amd import _lib
     L = _lib.load()
-    assert L.dg_conv3x3_wgrad(5000, 2, 8, 8, 1, 1, None, 1, 1, 1, 1 << 30, None) != 0
+    assert L.dg_conv3x3_wgrad(5000, 2, 8, 8, 1, 1, None, 0, 1, 1, 1, 1 << 30, None) != 0
+    assert L.dg_conv3x3_wgrad(2, 2, 8, 8, 1, 1, None, 1, 1, 1, 1, 1 << 30, None) != 0   # unknown flag
+    assert L.dg_conv3x3_wgrad(2, 2, 8, 9, 1, 1, None, 4, 1, 1, 1, 1 << 30, None) != 0   # odd size with the shuffle
     assert L.dg_conv3x3(0, 2, 8, 8, 1, 1, None, 1, 0, None, None) != 0
-    assert L.dg_conv3x3(2, 2, 8, 8, 1, 1, None, 1, 4, None, None) != 0   # unknown flag
+    assert L.dg_conv3x3(2, 2, 8, 8, 1, 1, None, 1, 8, None, None) != 0   # unknown flag
+    assert L.dg_conv3x3(2, 2, 7, 8, 1, 1, None, 1, 4, None, None) != 0   # odd size with the shuffle
 
 
 def _conv(x, w, b, adjoint, relu=False, gate=None):
@@ -375,3 +381,47 @@ def test_relu_folded_into_conv_and_its_backward(hip_device, cin, cout, H, W):
     rw, rb = _ref64(x, gm)
     assert _rel(dw, rw) < 1e-5 and _rel(db, rb) < 1e-5
     assert _rel(_conv(g, w, None, True, gate=y), _conv64(gm, w, None, True)) < 1e-5
+
+
+@pytest.mark.parametrize("cin,cout,H,W", [(16, 32, 272, 480), (64, 128, 68, 120), (3, 5, 34, 130)])
+def test_pixel_shuffle_folded_into_conv_and_its_backward(hip_device, cin, cout, H, W):
+    """The stages' PixelShuffle(2) folded into the kernels' addressing (DG_CONV_SHUFFLE): the forward of xq [4 cin][H/2]
+    [W/2] equals the plain forward of pixel_shuffle(xq) bit for bit (the same sums over the same values), the adjoint
+    equals pixel_unshuffle of the plain adjoint and the weight gradient the plain one of the shuffled input, both bit
+    for bit, with and without the ReLU gate; the Conv3x3 module with shuffle=True equals float64 within 1e-5."""
+    gen = torch.Generator(device=hip_device).manual_seed(cin * 3 + cout + W)
+    xq = torch.randn((4 * cin, H // 2, W // 2), generator=gen, device=hip_device)
+    x = F.pixel_shuffle(xq[None], 2)[0].contiguous()
+    w = torch.randn((cout, cin, 3, 3), generator=gen, device=hip_device) / (3 * cin ** 0.5)
+    b = torch.randn(cout, generator=gen, device=hip_device) * 0.3
+    g = torch.randn((cout, H, W), generator=gen, device=hip_device)
+    from dogs_amd import _lib
+    L = _lib.load()
+    st = _lib.stream_of(x.device)
+    for relu in (False, True):
+        ys = torch.full((cout, H, W), float("nan"), device=hip_device)
+        _lib.check(L.dg_conv3x3(cin, cout, H, W, xq.data_ptr(), w.data_ptr(), b.data_ptr(), ys.data_ptr(),
+                                4 | (2 if relu else 0), None, st))
+        y = _conv(x, w, b, False, relu=relu)
+        assert torch.equal(ys, y)
+        gate = y if relu else None
+        dq = torch.full((4 * cin, H // 2, W // 2), float("nan"), device=hip_device)
+        _lib.check(L.dg_conv3x3(cin, cout, H, W, g.data_ptr(), w.data_ptr(), None, dq.data_ptr(), 5,
+                                gate.data_ptr() if relu else None, st))
+        assert torch.equal(dq, F.pixel_unshuffle(_conv(g, w, None, True, gate=gate)[None], 2)[0])
+        dws, dbs = _wgrad(xq, g, gate=gate, shuffle=True)
+        dw, db = _wgrad(x, g, gate=gate)
+        assert torch.equal(dws, dw) and torch.equal(dbs, db)
+    from dogs_amd.masks import Conv3x3
+    conv = Conv3x3(cin, cout).to(hip_device)
+    xr = xq[None].clone().requires_grad_(True)
+    y = conv(xr, relu=True, shuffle=True)
+    (y * g).sum().backward()
+    x64 = xq[None].double().requires_grad_(True)
+    w64 = conv.weight.detach().double().requires_grad_(True)
+    b64 = conv.bias.detach().double().requires_grad_(True)
+    y64 = F.conv2d(F.pixel_shuffle(x64, 2), w64, b64, padding=1)
+    # the ReLU's mask taken from the float32 output: a float64 one flips where y rounds across 0
+    (y64 * torch.where(y[0] > 0, g, torch.zeros_like(g)).double()).sum().backward()
+    assert _rel(y, F.relu(y64)) < 1e-5 and _rel(xr.grad, x64.grad) < 1e-5
+    assert _rel(conv.weight.grad, w64.grad) < 1e-5 and _rel(conv.bias.grad, b64.grad) < 1e-5

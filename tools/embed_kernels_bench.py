@@ -82,7 +82,7 @@ def main():
             res["adj " + key] = timed(lambda: torch.ops.aten.convolution_backward(
                 dy4, x4, wt, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False]), args.iters)
         res["wgrad " + key] = timed(lambda: _lib.check(L.dg_conv3x3_wgrad(cin, cout, h, w, x.data_ptr(), dy.data_ptr(),
-                                                                          None, dw.data_ptr(), db.data_ptr(),
+                                                                          None, 0, dw.data_ptr(), db.data_ptr(),
                                                                           s2.data_ptr(), n, st)), args.iters)
     tot = 0.0
     for k, v in res.items():

@@ -1,7 +1,7 @@
 """BASELINE config 2's masked iteration (bench.masked_iteration_leg's trainer) split into host and GPU time: the host
 time of each train_iteration() call without a sync (median) against the synchronised wall time per iteration; run it
 under rocprofv3 --kernel-trace and tools/step_gaps.py shows where the GPU idles.
-python tools/masked_step_probe.py [--iters 60]"""
+python tools/masked_step_probe.py [--iters 60] [--unfold-shuffle]"""
 import argparse
 import os
 import sys
@@ -17,7 +17,17 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=60)
+    ap.add_argument("--unfold-shuffle", action="store_true",
+                    help="run the stages' PixelShuffle as its own torch op (the A/B of the folded one)")
     args = ap.parse_args()
+    if args.unfold_shuffle:
+        import torch.nn.functional as F
+        from dogs_amd.masks import Conv3x3
+        fold = Conv3x3.forward
+
+        def unfolded(self, x, relu=False, shuffle=False):
+            return fold(self, F.pixel_shuffle(x, 2) if shuffle else x, relu)
+        Conv3x3.forward = unfolded
     import bench
     from dogs_amd.synthetic import make_scene
     dev = torch.device("cuda", 0)
