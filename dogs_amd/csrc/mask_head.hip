@@ -136,23 +136,28 @@ __device__ __forceinline__ void window_sums(const float* in, int in_stride, cons
 
 __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_fwd(HeadArgs a) {
     constexpr int XR = FTH + 4, XC = FTW + 4, QR = FTH + 2, QC = FTW + 2;
-    // one LDS array, the weights first: their reads take immediate offsets from one base (< 64 KB)
-    __shared__ float smem[12 + HC * XR * XC + HM * QR * QC];
+    // one LDS array, the weights first: their reads take immediate offsets from one base (< 64 KB).  The hidden layer
+    // overwrites the samples once every thread has its conv1 outputs in registers (one position pair per thread): 59 ->
+    // 43 KB, 3 blocks per CU instead of 2
+    static_assert(QR * (QC / 2) == HT && HM * QR * QC <= HC * XR * XC, "one pair per thread; h fits the samples' area");
+    __shared__ float smem[12 + HC * XR * XC];
     float* sb1 = smem;
     float* sb2 = sb1 + HM;
     float* xs = sb1 + 12;                // samples, tile + 2 halo
-    float* hs = xs + HC * XR * XC;       // hidden, tile + 1 halo (0 outside the image: conv2's padding)
+    float* hs = xs;                      // then the hidden layer, tile + 1 halo (0 outside the image: conv2's padding)
     const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
     const int y0 = ty * FTH, x0 = tx * FTW;
     if (threadIdx.x < HM) sb1[threadIdx.x] = a.b1[threadIdx.x];
     if (threadIdx.x < HO) sb2[threadIdx.x] = a.b2[threadIdx.x];
     stage_samples<XR, XC>(a, y0 - 2, x0 - 2, xs);
     __syncthreads();
-    for (int i = threadIdx.x; i < QR * (QC / 2); i += HT) {     // position pairs (r, c), (r, c + 1)
+    {   // position pair (r, c), (r, c + 1)
+        const int i = threadIdx.x;
         const int r = i / (QC / 2), c = 2 * (i % (QC / 2)), y = y0 - 1 + r, x = x0 - 1 + c;
         float h0[HM], h1[HM];
         conv1_pair<XR, XC>(sb1, a.k1, xs, r, c, h0, h1);
         const bool in0 = y >= 0 && y < a.H && x >= 0 && x < a.W, in1 = y >= 0 && y < a.H && x + 1 >= 0 && x + 1 < a.W;
+        __syncthreads();   // every thread is past the samples
 #pragma unroll
         for (int co = 0; co < HM; co++) {
             hs[(co * QR + r) * QC + c] = in0 ? h0[co] : 0.0f;
@@ -199,11 +204,15 @@ template <bool HID>   // HID: h from the forward's store (a.hid), else recompute
 __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_bwd_h(HeadArgs a) {
     constexpr int XR = TH + 2, XC = TW + 2;
     constexpr int NP = HO * HM, G = HT / NP;    // dW2: 24 pairs x 10 row groups
-    __shared__ float smem[HM + HO * TW + HC * XR * XC + HO * XR * XC + HM * TH * TW];
+    // with HID the samples are not staged: their region only holds the dW2 row-group sums, and the block's LDS halves
+    // (67 -> 35 KB: 4 blocks per CU instead of 2)
+    constexpr int XS = HID ? G * NP * 10 : HC * XR * XC;
+    static_assert(G * NP * 10 <= HC * XR * XC, "the row-group sums reuse the samples' region");
+    __shared__ float smem[HM + HO * TW + XS + HO * XR * XC + HM * TH * TW];
     float* sb1 = smem;
     float* colsum = sb1 + HM;
     float* xs = colsum + HO * TW;        // samples, tile + 1 halo; then the dW2 row-group sums
-    float* ms = xs + HC * XR * XC;       // dmask, tile + 1 halo (0 outside the image)
+    float* ms = xs + XS;                 // dmask, tile + 1 halo (0 outside the image)
     float* hs = ms + HO * XR * XC;       // hidden on the tile (0 outside the image)
     const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
     const int y0 = ty * TH, x0 = tx * TW;
