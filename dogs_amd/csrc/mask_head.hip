@@ -26,9 +26,10 @@ namespace {
 
 constexpr int HC = 16, HM = 8, HO = 3;        // sample channels, hidden channels, mask channels
 constexpr int TH = 8, TW = 64;                 // output tile of the backward kernels
-// The forward's tile: its conv1 covers the tile + 1 halo, (6 + 2) x (62 + 2) = 256 position pairs, one per thread
-// (an 8 x 64 tile's 10 x 66 = 330 pairs took two passes at 64% use).
-constexpr int FTH = 6, FTW = 62;
+// The forward's tile: its conv1 covers the tile + 1 halo, (6 + 2) x (60 + 2) = 248 position pairs, one per thread
+// (an 8 x 64 tile's 10 x 66 = 330 pairs took two passes at 64% use); its samples, 16 x 10 x 64 floats, are 40 KB:
+// 4 blocks per CU (62 columns: 42 KB, 3 blocks)
+constexpr int FTH = 6, FTW = 60;
 constexpr int HT = 256;                        // threads per block
 constexpr int NW1 = HM * HC * 9, NW2 = HO * HM * 9;
 constexpr int P_W1 = 0, P_B1 = NW1, P_W2 = NW1 + HM, P_B2 = NW1 + HM + NW2;
@@ -136,32 +137,30 @@ __device__ __forceinline__ void window_sums(const float* in, int in_stride, cons
 
 __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_fwd(HeadArgs a) {
     constexpr int XR = FTH + 4, XC = FTW + 4, QR = FTH + 2, QC = FTW + 2;
-    // one LDS array, the weights first: their reads take immediate offsets from one base (< 64 KB).  The hidden layer
-    // overwrites the samples once every thread has its conv1 outputs in registers (one position pair per thread): 59 ->
-    // 43 KB, 3 blocks per CU instead of 2
-    static_assert(QR * (QC / 2) == HT && HM * QR * QC <= HC * XR * XC, "one pair per thread; h fits the samples' area");
-    __shared__ float smem[12 + HC * XR * XC];
-    float* sb1 = smem;
-    float* sb2 = sb1 + HM;
-    float* xs = sb1 + 12;                // samples, tile + 2 halo
+    // The hidden layer overwrites the samples once every thread has its conv1 outputs in registers (at most one position
+    // pair per thread); the biases are scalar loads like the weights.  59 -> 40 KB of LDS, 4 blocks per CU instead of 2
+    static_assert(QR * (QC / 2) <= HT && HM * QR * QC <= HC * XR * XC, "one pair per thread; h fits the samples' area");
+    __shared__ float smem[HC * XR * XC];
+    float* xs = smem;                    // samples, tile + 2 halo
     float* hs = xs;                      // then the hidden layer, tile + 1 halo (0 outside the image: conv2's padding)
     const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
     const int y0 = ty * FTH, x0 = tx * FTW;
-    if (threadIdx.x < HM) sb1[threadIdx.x] = a.b1[threadIdx.x];
-    if (threadIdx.x < HO) sb2[threadIdx.x] = a.b2[threadIdx.x];
     stage_samples<XR, XC>(a, y0 - 2, x0 - 2, xs);
     __syncthreads();
     {   // position pair (r, c), (r, c + 1)
         const int i = threadIdx.x;
+        const bool act = i < QR * (QC / 2);
         const int r = i / (QC / 2), c = 2 * (i % (QC / 2)), y = y0 - 1 + r, x = x0 - 1 + c;
         float h0[HM], h1[HM];
-        conv1_pair<XR, XC>(sb1, a.k1, xs, r, c, h0, h1);
+        if (act) conv1_pair<XR, XC>(a.b1, a.k1, xs, r, c, h0, h1);
         const bool in0 = y >= 0 && y < a.H && x >= 0 && x < a.W, in1 = y >= 0 && y < a.H && x + 1 >= 0 && x + 1 < a.W;
         __syncthreads();   // every thread is past the samples
+        if (act) {
 #pragma unroll
-        for (int co = 0; co < HM; co++) {
-            hs[(co * QR + r) * QC + c] = in0 ? h0[co] : 0.0f;
-            hs[(co * QR + r) * QC + c + 1] = in1 ? h1[co] : 0.0f;
+            for (int co = 0; co < HM; co++) {
+                hs[(co * QR + r) * QC + c] = in0 ? h0[co] : 0.0f;
+                hs[(co * QR + r) * QC + c + 1] = in1 ? h1[co] : 0.0f;
+            }
         }
     }
     __syncthreads();
@@ -177,7 +176,7 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
         if (y >= a.H || x >= a.W) continue;
         f2 m[HO];
 #pragma unroll
-        for (int o = 0; o < HO; o++) m[o] = (f2)(sb2[o]);
+        for (int o = 0; o < HO; o++) m[o] = (f2)(a.b2[o]);
 #pragma unroll 1
         for (int co = 0; co < HM; co++) {
 #pragma unroll
@@ -204,10 +203,11 @@ template <bool HID>   // HID: h from the forward's store (a.hid), else recompute
 __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_bwd_h(HeadArgs a) {
     constexpr int XR = TH + 2, XC = TW + 2;
     constexpr int NP = HO * HM, G = HT / NP;    // dW2: 24 pairs x 10 row groups
-    // with HID the samples are not staged: their region only holds the dW2 row-group sums, and the block's LDS halves
-    // (67 -> 35 KB: 4 blocks per CU instead of 2)
-    constexpr int XS = HID ? G * NP * 10 : HC * XR * XC;
-    static_assert(G * NP * 10 <= HC * XR * XC, "the row-group sums reuse the samples' region");
+    // with HID the samples are not staged and the dW2 row-group sums reuse dmask's and h's area once every thread is
+    // past them: 67 -> 25 KB of LDS, 6 blocks per CU instead of 2
+    constexpr int XS = HID ? 0 : HC * XR * XC;
+    static_assert(G * NP * 10 <= HC * XR * XC && G * NP * 10 <= HO * XR * XC + HM * TH * TW,
+                  "the row-group sums reuse the samples' region, or dmask's and h's");
     __shared__ float smem[HM + HO * TW + XS + HO * XR * XC + HM * TH * TW];
     float* sb1 = smem;
     float* colsum = sb1 + HM;
@@ -289,7 +289,8 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
         for (int r = 0; r < TH; r++) v += ms[(o * XR + r + 1) * XC + c + 1];
         colsum[t] = v;
     }
-    float* red = xs;   // every thread is past the samples
+    float* red = HID ? ms : xs;   // every thread is past the samples
+    if (HID) __syncthreads();     // ... and past dmask and h
     if (grp < G) {
 #pragma unroll
         for (int k = 0; k < 9; k++) red[(grp * NP + pr) * 10 + k] = acc[k];
