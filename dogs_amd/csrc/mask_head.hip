@@ -46,15 +46,16 @@ __device__ __forceinline__ void taps(int d, int n, float scale, int& i0, int& i1
     l0 = 1.0f - l1;
 }
 
-// samples of rows [ry0, ry0 + RR) x cols [rx0, rx0 + RC) of the resized image into xs[HC][RR][RC] (0 outside it)
-template <int RR, int RC>
-__device__ __forceinline__ void stage_samples(const HeadArgs& a, int ry0, int rx0, float* xs) {
+// samples of rows [ry0, ry0 + RR) x cols [rx0, rx0 + RC) of the resized image's channels [ch0, ch0 + NCH) into
+// xs[NCH][RR][RC] (0 outside it)
+template <int RR, int RC, int NCH = HC>
+__device__ __forceinline__ void stage_samples(const HeadArgs& a, int ry0, int rx0, float* xs, int ch0 = 0) {
     const size_t hw2 = (size_t)a.h2 * a.w2;
     for (int i = threadIdx.x; i < RR * RC; i += HT) {
         const int r = i / RC, c = i % RC, y = ry0 + r, x = rx0 + c;
         if (y < 0 || y >= a.H || x < 0 || x >= a.W) {
 #pragma unroll
-            for (int ch = 0; ch < HC; ch++) xs[(ch * RR + r) * RC + c] = 0.0f;
+            for (int ch = 0; ch < NCH; ch++) xs[(ch * RR + r) * RC + c] = 0.0f;
             continue;
         }
         int iy0, iy1, ix0, ix1;
@@ -64,8 +65,8 @@ __device__ __forceinline__ void stage_samples(const HeadArgs& a, int ry0, int rx
         const size_t o00 = (size_t)iy0 * a.w2 + ix0, o01 = (size_t)iy0 * a.w2 + ix1;
         const size_t o10 = (size_t)iy1 * a.w2 + ix0, o11 = (size_t)iy1 * a.w2 + ix1;
 #pragma unroll 4
-        for (int ch = 0; ch < HC; ch++) {
-            const float* u = a.U + ch * hw2;
+        for (int ch = 0; ch < NCH; ch++) {
+            const float* u = a.U + (ch0 + ch) * hw2;
             xs[(ch * RR + r) * RC + c] = ly0 * (lx0 * u[o00] + lx1 * u[o01]) + ly1 * (lx0 * u[o10] + lx1 * u[o11]);
         }
     }
@@ -310,15 +311,93 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
 }
 
-__global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_head_bwd_x(HeadArgs a) {
+// dW1 over one half of the sample channels (xh: channels [half * 8, half * 8 + 8), tile + 1 halo; ds: dh, tile + 1
+// halo): dW1[co][ci][ky][kx] = sum over the tile of dh[co][q] sample[ci][q + (ky, kx) - 1], db1[co] = sum dh[co] (with
+// the first half).  A thread owns one input x four hidden channels (3 sample + 4 dh LDS reads per 36 FMAs) over two
+// 16-column row segments: 16 slots x 16 groups; the four groups of a wave summed by lane exchange ((g0 + g1) +
+// (g2 + g3), the same bits in every lane), the waves in order through LDS.
+constexpr int W1_Q = 4, W1_NQ = HM / W1_Q, W1_CH = HC / 2, W1_SLOTS = W1_CH * W1_NQ, W1_G = HT / W1_SLOTS;
+constexpr int W1_SEG = 16, W1_ITEMS = TH * (TW / W1_SEG), W1_NV = W1_Q * 10, W1_WAVES = HT / 64;
+static_assert(W1_G * W1_SLOTS == HT && W1_SLOTS == 16 && W1_ITEMS % W1_G == 0, "four groups of 16 slots per wave");
+
+__device__ __forceinline__ void head_dw1_half(const float* xh, const float* ds, float* red, int half) {
     constexpr int XR = TH + 2, XC = TW + 2;
-    __shared__ float smem[HC * XR * XC + HM * XR * XC];
-    float* xs = smem;                    // samples, tile + 1 halo
-    float* ds = xs + HC * XR * XC;       // dh, tile + 1 halo (0 outside the image)
+    const int t = threadIdx.x, slot = t % W1_SLOTS, grp = t / W1_SLOTS;
+    const int q = slot % W1_NQ, cl = slot / W1_NQ;
+    float acc[W1_Q][9], bacc[W1_Q];
+#pragma unroll
+    for (int j = 0; j < W1_Q; j++) {
+        bacc[j] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 9; k++) acc[j][k] = 0.0f;
+    }
+    const float* xc = xh + cl * XR * XC;
+    const float* dc = ds + (q * W1_Q) * XR * XC + XC + 1;    // the tile's dh (inside the halo)
+#pragma unroll 1
+    for (int it = grp; it < W1_ITEMS; it += W1_G) {
+        const int r = it / (TW / W1_SEG), c0 = (it % (TW / W1_SEG)) * W1_SEG;
+        const float* x0r = xc + r * XC + c0;
+        float w00 = x0r[0], w01 = x0r[1];
+        float w10 = x0r[XC], w11 = x0r[XC + 1];
+        float w20 = x0r[2 * XC], w21 = x0r[2 * XC + 1];
+        const float* dr = dc + r * XC + c0;
+#pragma unroll 4
+        for (int c = 0; c < W1_SEG; c++) {
+            const float w02 = x0r[c + 2], w12 = x0r[XC + c + 2], w22 = x0r[2 * XC + c + 2];
+#pragma unroll
+            for (int j = 0; j < W1_Q; j++) {
+                const float g = dr[j * XR * XC + c];
+                acc[j][0] = fmaf(g, w00, acc[j][0]); acc[j][1] = fmaf(g, w01, acc[j][1]);
+                acc[j][2] = fmaf(g, w02, acc[j][2]); acc[j][3] = fmaf(g, w10, acc[j][3]);
+                acc[j][4] = fmaf(g, w11, acc[j][4]); acc[j][5] = fmaf(g, w12, acc[j][5]);
+                acc[j][6] = fmaf(g, w20, acc[j][6]); acc[j][7] = fmaf(g, w21, acc[j][7]);
+                acc[j][8] = fmaf(g, w22, acc[j][8]);
+                bacc[j] += g;
+            }
+            w00 = w01; w01 = w02; w10 = w11; w11 = w12; w20 = w21; w21 = w22;
+        }
+    }
+    // the wave's groups are its lanes l, l + 16, l + 32, l + 48: (g0 + g1) + (g2 + g3), commutative adds, so every lane
+    // of a slot holds the same bits
+    const int lane = t & 63, wave = t >> 6;
+    float* wr = red + (wave * W1_SLOTS + slot) * W1_NV;
+#pragma unroll
+    for (int j = 0; j < W1_Q; j++) {
+#pragma unroll
+        for (int k = 0; k < 10; k++) {
+            float v = k < 9 ? acc[j][k] : bacc[j];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            if (lane < W1_SLOTS) wr[j * 10 + k] = v;
+        }
+    }
+}
+
+// the waves' sums of one half in order -> the tile's partial row
+__device__ __forceinline__ void head_dw1_store(const float* red, float* prow, int half) {
+    for (int i = threadIdx.x; i < W1_SLOTS * W1_NV; i += HT) {
+        const int sl = i / W1_NV, e = i % W1_NV, j = e / 10, k = e % 10;
+        const int pci = half * W1_CH + sl / W1_NQ, pco = (sl % W1_NQ) * W1_Q + j;
+        float v = red[i];
+#pragma unroll
+        for (int w = 1; w < W1_WAVES; w++) v += red[w * W1_SLOTS * W1_NV + i];
+        if (k < 9) prow[P_W1 + (pco * HC + pci) * 9 + k] = v;
+        else if (pci == 0) prow[P_B1 + pco] = v;
+    }
+}
+
+// dL/dsample = conv1^T(dh) and dW1, db1 per tile.  LDS: dh (8 channels, tile + 1 halo), half of the samples at a time
+// and the waves' dW1 sums, 52 KB: 3 blocks per CU (all 16 sample channels at once were 63 KB, 2 blocks)
+__global__ void __launch_bounds__(HT) k_head_bwd_x(HeadArgs a) {
+    constexpr int XR = TH + 2, XC = TW + 2;
+    __shared__ float smem[HM * XR * XC + W1_CH * XR * XC + W1_WAVES * W1_SLOTS * W1_NV];
+    float* ds = smem;                    // dh, tile + 1 halo (0 outside the image)
+    float* xh = ds + HM * XR * XC;       // samples of one channel half, tile + 1 halo
+    float* red = xh + W1_CH * XR * XC;   // the waves' dW1 sums
     const int tx = blockIdx.x % a.tiles_x, ty = blockIdx.x / a.tiles_x;
     const int y0 = ty * TH, x0 = tx * TW;
     const size_t HW = (size_t)a.H * a.W;
-    stage_samples<XR, XC>(a, y0 - 1, x0 - 1, xs);
+    stage_samples<XR, XC, W1_CH>(a, y0 - 1, x0 - 1, xh, 0);
     for (int i = threadIdx.x; i < XR * XC; i += HT) {
         const int r = i / XC, c = i % XC, y = y0 - 1 + r, x = x0 - 1 + c;
         const bool in = y >= 0 && y < a.H && x >= 0 && x < a.W;
@@ -354,67 +433,15 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) k_
             if (x + 1 < a.W) a.dx[ci * HW + p + 1] = d[ci].y;
         }
     }
-    // dW1[co][ci][ky][kx] = sum over the tile of dh[co][q] sample[ci][q + (ky, kx) - 1]; db1[co] = sum dh[co].
-    // A thread owns one input x four hidden channels (3 sample + 4 dh LDS reads per 36 FMAs; one pair per thread read
-    // 1 + 3 per 9) over its group's 16-column row segments: 32 slots x 8 groups, 4 segments each; the groups' sums in
-    // order through LDS, reusing xs once every thread is past it.
-    constexpr int Q = 4, NQ = HM / Q, SLOTS = HC * NQ, G = HT / SLOTS, SEG = 16, ITEMS = TH * (TW / SEG), NV = Q * 10;
-    static_assert(G * SLOTS == HT && G * SLOTS * NV <= HC * XR * XC, "dW1 group sums fit the sample area");
-    const int t = threadIdx.x, slot = t % SLOTS, grp = t / SLOTS;
-    const int q = slot % NQ, ci = slot / NQ;
-    float acc[Q][9], bacc[Q];
-#pragma unroll
-    for (int j = 0; j < Q; j++) {
-        bacc[j] = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 9; k++) acc[j][k] = 0.0f;
-    }
-    {
-        const float* xc = xs + ci * XR * XC;
-        const float* dc = ds + (q * Q) * XR * XC + XC + 1;    // the tile's dh (inside the halo)
-#pragma unroll 1
-        for (int it = grp; it < ITEMS; it += G) {
-            const int r = it / (TW / SEG), c0 = (it % (TW / SEG)) * SEG;
-            const float* x0r = xc + r * XC + c0;
-            float w00 = x0r[0], w01 = x0r[1];
-            float w10 = x0r[XC], w11 = x0r[XC + 1];
-            float w20 = x0r[2 * XC], w21 = x0r[2 * XC + 1];
-            const float* dr = dc + r * XC + c0;
-#pragma unroll 4
-            for (int c = 0; c < SEG; c++) {
-                const float w02 = x0r[c + 2], w12 = x0r[XC + c + 2], w22 = x0r[2 * XC + c + 2];
-#pragma unroll
-                for (int j = 0; j < Q; j++) {
-                    const float g = dr[j * XR * XC + c];
-                    acc[j][0] = fmaf(g, w00, acc[j][0]); acc[j][1] = fmaf(g, w01, acc[j][1]);
-                    acc[j][2] = fmaf(g, w02, acc[j][2]); acc[j][3] = fmaf(g, w10, acc[j][3]);
-                    acc[j][4] = fmaf(g, w11, acc[j][4]); acc[j][5] = fmaf(g, w12, acc[j][5]);
-                    acc[j][6] = fmaf(g, w20, acc[j][6]); acc[j][7] = fmaf(g, w21, acc[j][7]);
-                    acc[j][8] = fmaf(g, w22, acc[j][8]);
-                    bacc[j] += g;
-                }
-                w00 = w01; w01 = w02; w10 = w11; w11 = w12; w20 = w21; w21 = w22;
-            }
-        }
-    }
-    __syncthreads();
-    float* red = xs;
-#pragma unroll
-    for (int j = 0; j < Q; j++) {
-#pragma unroll
-        for (int k = 0; k < 9; k++) red[(grp * SLOTS + slot) * NV + j * 10 + k] = acc[j][k];
-        red[(grp * SLOTS + slot) * NV + j * 10 + 9] = bacc[j];
-    }
-    __syncthreads();
     float* prow = a.part + (size_t)blockIdx.x * NPART;
-    for (int i = t; i < SLOTS * NV; i += HT) {
-        const int sl = i / NV, e = i % NV, j = e / 10, k = e % 10;
-        const int pci = sl / NQ, pco = (sl % NQ) * Q + j;
-        float v = red[i];
-        for (int gg = 1; gg < G; gg++) v += red[gg * SLOTS * NV + i];
-        if (k < 9) prow[P_W1 + (pco * HC + pci) * 9 + k] = v;
-        else if (pci == 0) prow[P_B1 + pco] = v;
-    }
+    head_dw1_half(xh, ds, red, 0);
+    __syncthreads();                     // every thread is past the first half's samples and has stored its sums
+    head_dw1_store(red, prow, 0);
+    stage_samples<XR, XC, W1_CH>(a, y0 - 1, x0 - 1, xh, W1_CH);
+    __syncthreads();                     // the second half staged, the first half's sums read
+    head_dw1_half(xh, ds, red, 1);
+    __syncthreads();
+    head_dw1_store(red, prow, 1);
 }
 
 // the samples (along one axis) that read source index u: candidates around u / scale, each tested with taps(); returns
